@@ -1,0 +1,236 @@
+"""bench.py -- BASELINE.json metric: GB/s of device-resident fp32 gradient buckets
+quantised + reduced (+ dequantised), 256 MiB per bucket, 1/2/4/8 GPUs.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Workload (one "step"): every rank holds R = 2 resident 256 MiB fp32 buckets
+(the reference's FAN_IN = 2 children per switch, non_termination_switch.c:23)
+and produces their allreduce over all ranks into a third buffer:
+  N = 1   one fused HIP kernel: dequant(sum_r quant(x_r))          (config 2)
+  N > 1   quant + local sum (HIP) -> RCCL reduce-scatter int32 -> dequant own
+          shard (HIP) -> RCCL all-gather fp32                       (config 4)
+value = bucket bytes reduced per second over the whole job = N * R * 256 MiB / t.
+
+Extra JSON fields: ``roofline`` for the dominant kernel (the fused / quant+sum
+kernel, algorithmic bytes (R+1)*4*n per launch, timed with HIP events on its
+own stream) and ``cpu_baseline`` (the C oracle on a bounded sample, rank 0 at
+N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--bucket-mib", type=int, default=256)
+    p.add_argument("--local-buckets", type=int, default=2)
+    p.add_argument("--scale-exp", type=int, default=25)
+    p.add_argument("--chunks", type=int, default=int(os.environ.get("INCCL_BENCH_CHUNKS", "4")))
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--grid-cap", type=int, default=0)
+    p.add_argument("--json-out", default="")
+    return p.parse_args()
+
+
+def cpu_baseline(n_elems: int, R: int, k: int, seconds: float) -> dict:
+    """The C restatement (oracle/inccl_oracle.c, scalar, 1 core) on a bounded
+    sample of the same workload: R buckets of 16 Mi elements (64 MiB each)."""
+    import numpy as np
+
+    from oracle import oracle as O
+    O.build()
+    m = min(n_elems, 1 << 24)
+    rng = np.random.default_rng(1000)
+    xs = [rng.standard_normal(m).astype(np.float32) for _ in range(R)]
+    out = None
+    t0 = time.perf_counter()
+    iters = 0
+    while True:
+        out = O.reduce_f32(xs, k)
+        iters += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    del out
+    return {"value": round(iters * R * m * 4 / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{iters} x fused quantise+sum+dequantise of R={R} x {m * 4 >> 20} MiB fp32 buckets "
+                      f"(oracle/inccl_oracle.c orc_reduce_f32, 1 thread, {dt:.1f} s)"}
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    PMC summary (profiles/pmc_traffic.json), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        return d.get(workload, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import container_inc_amd
+    from container_inc_amd import inccl
+    from container_inc_amd.plan import chunk_plan
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"warning: WORLD_SIZE={world} but --gpus={a.gpus}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    container_inc_amd.load()
+    if a.grid_cap:
+        inccl.set_tuning(a.grid_cap, True)
+
+    R, k = a.local_buckets, a.scale_exp
+    n = a.bucket_mib * (1 << 20) // 4
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 + rank)
+    srcs = [torch.randn(n, generator=gen, device=dev, dtype=torch.float32) for _ in range(R)]
+    out = torch.empty(n, device=dev, dtype=torch.float32)
+
+    master = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ.get("MASTER_PORT", "29500")) + 17
+    grp = inccl.inccl_group_create(world, rank, master, port=port, device=local_rank)
+    if grp is None:
+        raise SystemExit("inccl_group_create failed: " + container_inc_amd.load().inccl_last_error().decode())
+    comm = inccl.inccl_communicator_create(grp, 0)
+    stream = torch.cuda.Stream(device=dev)
+    chunks = a.chunks if world > 1 else 1
+
+    def step():
+        comm.allreduce_f32(srcs, out=out, scale_exp=k, chunks=chunks, stream=stream.cuda_stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(a.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+    dev_ms = ev0.elapsed_time(ev1)
+    t = torch.tensor([wall], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    ms_per_step = wall * 1e3 / a.steps
+
+    # dominant kernel alone: fused (N=1) or quant + local sum (N>1), HIP events on its stream
+    kstream = torch.cuda.Stream(device=dev)
+    qbuf = torch.empty(n, device=dev, dtype=torch.int32) if world > 1 else None
+
+    def kernel():
+        if world == 1:
+            inccl.reduce_f32(srcs, k, out=out, stream=kstream.cuda_stream)
+        else:
+            inccl.quant_sum(srcs, k, out=qbuf, stream=kstream.cuda_stream)
+
+    for _ in range(3):
+        kernel()
+    kev0, kev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    kiters = max(a.steps, 20)
+    kev0.record(kstream)
+    for _ in range(kiters):
+        kernel()
+    kev1.record(kstream)
+    torch.cuda.synchronize()
+    k_ms = kev0.elapsed_time(kev1) / kiters
+    alg_bytes = (R + 1) * 4 * n
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    workload = (f"fused quantise+sum+dequantise of R={R} resident {a.bucket_mib} MiB fp32 buckets, 1 GPU"
+                if world == 1 else
+                f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: quant+local sum -> RCCL reduce-scatter "
+                f"int32 -> dequant shard -> RCCL all-gather fp32, {chunks} pipelined chunks")
+    kname = "k_stream_vec<F32,F32,R>" if world == 1 else "k_stream_vec<F32,Q32,R>"
+    traffic = load_traffic(kname + f" R={R} n={n}")
+
+    value = world * R * n * 4 / (ms_per_step * 1e-3) / 1e9
+    res = {
+        "metric": "GB/s device-resident fp32 bucket quantise+reduce, 256 MiB, 1/2/4/8 GPUs",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "device_ms_per_step_rank0": round(dev_ms / a.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32->int32 (fixed point, 2^-%d)" % k,
+        "data": "synthetic N(0,1) fp32 buckets, torch.Generator seed 1000+rank",
+        "config": {
+            "workload": workload,
+            "bucket_mib": a.bucket_mib,
+            "local_buckets": R,
+            "scale_exp": k,
+            "global_batch": world * R,
+            "parallelism": f"dp{world}",
+            "chunks": chunks,
+            "shard_elems": chunk_plan(n, world, chunks)[0][2] if world > 1 else n,
+        },
+        "roofline": {
+            "kernel": kname,
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "alg_bytes_per_launch": alg_bytes,
+            "kernel_ms": round(k_ms, 5),
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(n, R, k, a.cpu_seconds)
+    if rank == 0:
+        line = json.dumps(res)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    comm.destroy()
+    grp.destroy()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,96 @@
+"""Loader for the in-tree ``libinccl_amd.so`` (C ABI of include/api.h + include/inccl_amd.h).
+
+The product has no CPU fallback: if the library is missing this module raises
+immediately, and every compute call fails loudly without a GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libinccl_amd.so")
+
+# Public symbols, one per declaration in include/api.h and include/inccl_amd.h.
+# (name, restype, argtypes)
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_SZ = ctypes.c_size_t
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_F = ctypes.c_float
+_S = ctypes.c_char_p
+
+SIGNATURES = {
+    # include/api.h (reference repository/include/api.h:93-101)
+    "inccl_group_create": (_P, [_I, _I, _S]),
+    "inccl_group_destroy": (_I, [_P]),
+    "inccl_communicator_create": (_P, [_P, _U32]),
+    "inccl_communicator_destroy": (_I, [_P]),
+    "inccl_allreduce_sendrecv": (None, [_P, _P, _U32, _P]),
+    "inccl_allreduce_write": (None, [_P, _P, _U32, _P]),
+    # include/inccl_amd.h
+    "inccl_last_error": (_S, []),
+    "inccl_version": (_S, []),
+    "inccl_quantise_f32": (_I, [_P, _P, _SZ, _I, _I, _P]),
+    "inccl_dequantise_q32": (_I, [_P, _P, _SZ, _I, _I, _P]),
+    "inccl_reduce_f32": (_I, [_P, _I, _P, _SZ, _I, _P]),
+    "inccl_reduce_f32_auto": (_I, [_P, _I, _P, _SZ, _P, _P]),
+    "inccl_quant_sum_f32": (_I, [_P, _I, _P, _SZ, _I, _I, _P]),
+    "inccl_sum_q32": (_I, [_P, _I, _P, _SZ, _I, _I, _P]),
+    "inccl_sum_dequant_q32": (_I, [_P, _I, _P, _SZ, _I, _I, _P]),
+    "inccl_stream_op": (_I, [_I, _I, _P, _I, _P, _SZ, _I, _P, _I, _P]),
+    "inccl_absmax_f32": (_I, [_P, _I, _SZ, _P, _I, _P]),
+    "inccl_checksum_q32": (_I, [_P, _SZ, _U64, _P, _I, _P]),
+    "inccl_choose_scale": (_I, [_F, _I]),
+    "inccl_set_tuning": (None, [_I, _I]),
+    "inccl_group_create_ex": (_P, [_I, _I, _S, _I, _I]),
+    "inccl_group_create_local": (_P, [_I, _I, _S, _I]),
+    "inccl_group_rank": (_I, [_P]),
+    "inccl_group_size": (_I, [_P]),
+    "inccl_group_device": (_I, [_P]),
+    "inccl_group_transport": (_S, [_P]),
+    "inccl_comm_stream": (_P, [_P]),
+    "inccl_comm_barrier": (_I, [_P]),
+    "inccl_allreduce_f32": (_I, [_P, _P, _I, _P, _SZ, _I, _P]),
+    "inccl_allreduce_f32_pipelined": (_I, [_P, _P, _I, _P, _SZ, _I, _I, _P]),
+    "inccl_allreduce_q32": (_I, [_P, _P, _P, _SZ, _P]),
+    "inccl_allreduce_f32_host": (_I, [_P, _P, _P, _SZ, _I, _SZ]),
+}
+
+_lib = None
+
+
+class IncclError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load the library (RTLD_GLOBAL so the HIP runtime is shared with torch)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise IncclError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(make -C container_inc_amd/csrc).  There is no CPU fallback.")
+    # torch bundles its own HIP/HSA/RCCL runtimes under the same sonames.  Load
+    # it first so this library binds to those copies: loading /opt/rocm's
+    # libamdhip64 first and torch's later puts two HSA runtimes in one process.
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - pure C consumers need no torch
+        pass
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().inccl_last_error().decode(errors="replace")
+        raise IncclError(f"{what} failed (rc={rc}): {msg}")

@@ -1,0 +1,612 @@
+/* api.c -- libinccl_amd host API (C11).
+ *
+ * Drop-in implementation of repository/include/api.h:93-101 plus the additive
+ * MI355X entry points of include/inccl_amd.h.  Host code only: every byte of
+ * arithmetic runs in the HIP kernels behind inccl_kernels.h or in RCCL.
+ * There is no CPU fallback: without a usable GPU the calls fail. */
+#define _GNU_SOURCE
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "inccl_internal.h"
+#include "inccl_kernels.h"
+
+/* ------------------------------------------------------------------ */
+/* errors                                                               */
+/* ------------------------------------------------------------------ */
+static __thread char g_err[512];
+
+int inccl_set_error(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    if (getenv("INCCL_DEBUG")) fprintf(stderr, "[inccl] %s\n", g_err);
+    return code;
+}
+
+int inccl_hip_check(hipError_t e, const char *what)
+{
+    return inccl_set_error(INCCL_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+const char *inccl_last_error(void) { return g_err; }
+
+const char *inccl_version(void) { return "inccl-amd 0.1.0 gfx950"; }
+
+int inccl_ensure_dev(void **p, size_t *cur, size_t need)
+{
+    if (*p && *cur >= need) return 0;
+    if (*p) {
+        INCCL_HIP(hipDeviceSynchronize());
+        INCCL_HIP(hipFree(*p));
+        *p = NULL;
+        *cur = 0;
+    }
+    if (need == 0) return 0;
+    INCCL_HIP(hipMalloc(p, need));
+    *cur = need;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* stateless device API                                                 */
+/* ------------------------------------------------------------------ */
+static int kerr(int rc)
+{
+    if (rc == 0) return 0;
+    if (rc == INCCL_ERR_ARG) return inccl_set_error(rc, "invalid argument");
+    return inccl_set_error(INCCL_ERR_HIP, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
+}
+
+int inccl_stream_op(int in_kind, int out_kind, const void *const *srcs_dev, int R, void *dst_dev, size_t n,
+                    int scale_exp, const uint32_t *amax_bits_dev, int scale_R, void *stream)
+{
+    if (!srcs_dev) return inccl_set_error(INCCL_ERR_ARG, "srcs is NULL");
+    return kerr(inccl_k_stream(in_kind, out_kind, srcs_dev, R, dst_dev, n, scale_exp, amax_bits_dev, scale_R, stream));
+}
+
+int inccl_quantise_f32(const float *x_dev, int32_t *q_dev, size_t n, int scale_exp, int wire_be, void *stream)
+{
+    const void *s[1] = {x_dev};
+    return inccl_stream_op(INCCL_KIND_F32, wire_be ? INCCL_KIND_Q32BE : INCCL_KIND_Q32, s, 1, q_dev, n, scale_exp,
+                           NULL, 1, stream);
+}
+
+int inccl_dequantise_q32(const int32_t *q_dev, float *y_dev, size_t n, int scale_exp, int wire_be, void *stream)
+{
+    const void *s[1] = {q_dev};
+    return inccl_stream_op(wire_be ? INCCL_KIND_Q32BE : INCCL_KIND_Q32, INCCL_KIND_F32, s, 1, y_dev, n, scale_exp,
+                           NULL, 1, stream);
+}
+
+int inccl_reduce_f32(const float *const *srcs_dev, int R, float *dst_dev, size_t n, int scale_exp, void *stream)
+{
+    return inccl_stream_op(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, scale_exp,
+                           NULL, R, stream);
+}
+
+int inccl_absmax_f32(const float *const *srcs_dev, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
+                     void *stream)
+{
+    if (!srcs_dev) return inccl_set_error(INCCL_ERR_ARG, "srcs is NULL");
+    return kerr(inccl_k_absmax(srcs_dev, R, n, amax_bits_dev, zero_first, stream));
+}
+
+int inccl_reduce_f32_auto(const float *const *srcs_dev, int R, float *dst_dev, size_t n, uint32_t *amax_word_dev,
+                          void *stream)
+{
+    int rc = inccl_absmax_f32(srcs_dev, R, n, amax_word_dev, 1, stream);
+    if (rc) return rc;
+    return inccl_stream_op(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, 0,
+                           amax_word_dev, R, stream);
+}
+
+int inccl_quant_sum_f32(const float *const *srcs_dev, int R, int32_t *dst_dev, size_t n, int scale_exp, int wire_be,
+                        void *stream)
+{
+    return inccl_stream_op(INCCL_KIND_F32, wire_be ? INCCL_KIND_Q32BE : INCCL_KIND_Q32,
+                           (const void *const *)srcs_dev, R, dst_dev, n, scale_exp, NULL, R, stream);
+}
+
+int inccl_sum_q32(const int32_t *const *srcs_dev, int R, int32_t *dst_dev, size_t n, int in_be, int out_be,
+                  void *stream)
+{
+    return inccl_stream_op(in_be ? INCCL_KIND_Q32BE : INCCL_KIND_Q32, out_be ? INCCL_KIND_Q32BE : INCCL_KIND_Q32,
+                           (const void *const *)srcs_dev, R, dst_dev, n, 0, NULL, R, stream);
+}
+
+int inccl_sum_dequant_q32(const int32_t *const *srcs_dev, int R, float *dst_dev, size_t n, int scale_exp, int in_be,
+                          void *stream)
+{
+    return inccl_stream_op(in_be ? INCCL_KIND_Q32BE : INCCL_KIND_Q32, INCCL_KIND_F32, (const void *const *)srcs_dev,
+                           R, dst_dev, n, scale_exp, NULL, R, stream);
+}
+
+int inccl_checksum_q32(const int32_t *q_dev, size_t n, uint64_t index_base, uint32_t *out_dev, int zero_first,
+                       void *stream)
+{
+    return kerr(inccl_k_checksum(q_dev, n, index_base, out_dev, zero_first, stream));
+}
+
+int inccl_choose_scale(float absmax, int R_total)
+{
+    /* host twin of choose_scale() in inccl_kernels.hip */
+    if (!(absmax > 0.0f)) return INCCL_SCALE_MAX;
+    if (isinf(absmax)) return INCCL_SCALE_MIN;
+    double t = (double)absmax * (double)(R_total > 0 ? R_total : 1);
+    int e = 0;
+    double m = frexp(t, &e);
+    int k = (m == 0.5) ? (31 - e) : (30 - e);
+    if (k < INCCL_SCALE_MIN) k = INCCL_SCALE_MIN;
+    if (k > INCCL_SCALE_MAX) k = INCCL_SCALE_MAX;
+    return k;
+}
+
+void inccl_set_tuning(int grid_cap, int nt_loads) { inccl_k_set_tuning(grid_cap, nt_loads); }
+
+/* ------------------------------------------------------------------ */
+/* groups                                                               */
+/* ------------------------------------------------------------------ */
+static int pick_device(int rank, int device)
+{
+    if (device >= 0) return device;
+    const char *e = getenv("INCCL_DEVICE");
+    if (e && *e) return atoi(e);
+    e = getenv("LOCAL_RANK");
+    if (e && *e) return atoi(e);
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -1;
+    return rank % n;
+}
+
+static struct inccl_group *group_alloc(int world_size, int rank, int device)
+{
+    if (world_size < 1 || rank < 0 || rank >= world_size) {
+        inccl_set_error(INCCL_ERR_ARG, "bad world_size %d / rank %d", world_size, rank);
+        return NULL;
+    }
+    /* INCCL_BOOTSTRAP_ONLY=1: a GPU-less group for rendezvous/barrier tests of
+     * the host logic; every communicator call on it fails. */
+    const char *bo = getenv("INCCL_BOOTSTRAP_ONLY");
+    const int bootstrap_only = bo && atoi(bo) != 0;
+    int dev = bootstrap_only ? -1 : pick_device(rank, device);
+    if (dev < 0 && !bootstrap_only) {
+        inccl_set_error(INCCL_ERR_HIP, "no HIP device available");
+        return NULL;
+    }
+    if (dev >= 0) {
+        hipError_t e = hipSetDevice(dev);
+        if (e != hipSuccess) {
+            inccl_hip_check(e, "hipSetDevice");
+            return NULL;
+        }
+    }
+    struct inccl_group *g = (struct inccl_group *)calloc(1, sizeof(*g));
+    if (!g) return NULL;
+    g->rank = rank;
+    g->world_size = world_size;
+    g->device = dev;
+    g->master_fd = -1;
+    return g;
+}
+
+struct inccl_group *inccl_group_create_local(int world_size, int rank, const char *hub_name, int device)
+{
+    struct inccl_group *g = group_alloc(world_size, rank, device);
+    if (!g) return NULL;
+    g->transport = INCCL_TRANSPORT_LOCAL;
+    snprintf(g->master_ip, sizeof(g->master_ip), "local");
+    g->hub = inccl_hub_attach(hub_name ? hub_name : "default", world_size);
+    if (!g->hub) {
+        free(g);
+        return NULL;
+    }
+    return g;
+}
+
+struct inccl_group *inccl_group_create_ex(int world_size, int rank, const char *master_ip, int port, int device)
+{
+    if (master_ip && strcmp(master_ip, "local") == 0) return inccl_group_create_local(world_size, rank, "default", device);
+    struct inccl_group *g = group_alloc(world_size, rank, device);
+    if (!g) return NULL;
+    g->transport = INCCL_TRANSPORT_RCCL;
+    snprintf(g->master_ip, sizeof(g->master_ip), "%s", master_ip ? master_ip : "127.0.0.1");
+    if (port <= 0) {
+        const char *e = getenv("INCCL_MASTER_PORT");
+        port = (e && *e) ? atoi(e) : MASTER_PORT;
+    }
+    g->port = port;
+    int rc = (world_size == 1) ? 0 : (rank == 0 ? inccl_boot_master(g) : inccl_boot_worker(g));
+    if (rc == 0 && rank == 0 && g->peer_fds == NULL) {
+        g->peer_fds = (int *)calloc((size_t)world_size, sizeof(int));
+        for (int i = 0; g->peer_fds && i < world_size; ++i) g->peer_fds[i] = -1;
+    }
+    if (rc != 0) {
+        fprintf(stderr, "inccl_group_create: %s\n", inccl_last_error());
+        inccl_boot_close(g);
+        free(g);
+        return NULL;
+    }
+    return g;
+}
+
+struct inccl_group *inccl_group_create(int world_size, int rank, const char *master_ip)
+{
+    return inccl_group_create_ex(world_size, rank, master_ip, 0, -1);
+}
+
+int inccl_group_destroy(struct inccl_group *group)
+{
+    if (group) {
+        inccl_boot_close(group);
+        inccl_hub_detach(group->hub);
+        free(group);
+    }
+    return 1;   /* api.c:151-154 returns 1 */
+}
+
+int inccl_group_rank(const struct inccl_group *g) { return g ? g->rank : -1; }
+int inccl_group_size(const struct inccl_group *g) { return g ? g->world_size : -1; }
+int inccl_group_device(const struct inccl_group *g) { return g ? g->device : -1; }
+const char *inccl_group_transport(const struct inccl_group *g)
+{
+    return (g && g->transport == INCCL_TRANSPORT_LOCAL) ? "local" : "rccl";
+}
+
+/* ------------------------------------------------------------------ */
+/* communicators                                                        */
+/* ------------------------------------------------------------------ */
+static int comm_init(struct inccl_communicator *c, uint32_t size)
+{
+    struct inccl_group *g = c->group;
+    if (g->device < 0) return inccl_set_error(INCCL_ERR_STATE, "group has no device (bootstrap-only)");
+    INCCL_HIP(hipSetDevice(g->device));
+    c->payload_buf_size = size * 2u;             /* api.c:164 */
+    c->window_size = WINDOW_SIZE;                /* api.c:226 */
+    if (c->payload_buf_size) {
+        INCCL_HIP(hipHostMalloc((void **)&c->send_payload, c->payload_buf_size, hipHostMallocDefault));
+        INCCL_HIP(hipHostMalloc((void **)&c->receive_payload, c->payload_buf_size, hipHostMallocDefault));
+        memset(c->send_payload, 0, c->payload_buf_size);      /* api.c:171-172 */
+        memset(c->receive_payload, 0, c->payload_buf_size);
+    }
+    INCCL_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    INCCL_HIP(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
+    INCCL_HIP(hipStreamCreateWithFlags(&c->copy_streams[0], hipStreamNonBlocking));
+    INCCL_HIP(hipStreamCreateWithFlags(&c->copy_streams[1], hipStreamNonBlocking));
+    for (int i = 0; i < 8; ++i) INCCL_HIP(hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming));
+    INCCL_HIP(hipMalloc((void **)&c->d_words, 256));
+    INCCL_HIP(hipMemset(c->d_words, 0, 256));
+    c->comm_id = g->comm_seq++;
+    if (g->transport == INCCL_TRANSPORT_RCCL) {
+        const char *force = getenv("INCCL_FORCE_RCCL");
+        if (g->world_size > 1 || (force && atoi(force) != 0)) {
+            int rc = inccl_rccl_comm_init(c);
+            if (rc) return rc;
+        }
+    }
+    /* int32 workspace of one bucket of `size` bytes up front */
+    if (size) {
+        int rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, (size_t)size);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+int inccl_communicator_destroy(struct inccl_communicator *comm)
+{
+    if (!comm) return 0;
+    if (comm->group->device >= 0) hipSetDevice(comm->group->device);
+    if (comm->stream) hipStreamSynchronize(comm->stream);
+    inccl_rccl_comm_destroy(comm);
+    if (comm->d_q32) hipFree(comm->d_q32);
+    if (comm->d_f32) hipFree(comm->d_f32);
+    if (comm->d_stage) hipFree(comm->d_stage);
+    if (comm->d_words) hipFree(comm->d_words);
+    if (comm->send_payload) hipHostFree(comm->send_payload);
+    if (comm->receive_payload) hipHostFree(comm->receive_payload);
+    for (int i = 0; i < 8; ++i)
+        if (comm->ev[i]) hipEventDestroy(comm->ev[i]);
+    if (comm->copy_streams[0]) hipStreamDestroy(comm->copy_streams[0]);
+    if (comm->copy_streams[1]) hipStreamDestroy(comm->copy_streams[1]);
+    if (comm->side_stream) hipStreamDestroy(comm->side_stream);
+    if (comm->stream) hipStreamDestroy(comm->stream);
+    free(comm);
+    return 0;
+}
+
+struct inccl_communicator *inccl_communicator_create(struct inccl_group *group, uint32_t size)
+{
+    if (!group) {
+        inccl_set_error(INCCL_ERR_ARG, "group is NULL");
+        return NULL;
+    }
+    struct inccl_communicator *c = (struct inccl_communicator *)calloc(1, sizeof(*c));
+    if (!c) return NULL;
+    c->group = group;
+    int rc = comm_init(c, size);
+    if (rc) {
+        fprintf(stderr, "inccl_communicator_create: %s\n", inccl_last_error());
+        inccl_communicator_destroy(c);
+        return NULL;
+    }
+    return c;
+}
+
+void *inccl_comm_stream(struct inccl_communicator *comm) { return comm ? (void *)comm->stream : NULL; }
+
+int inccl_comm_barrier(struct inccl_communicator *comm)
+{
+    if (!comm) return inccl_set_error(INCCL_ERR_ARG, "comm is NULL");
+    return inccl_tp_barrier(comm);
+}
+
+/* ------------------------------------------------------------------ */
+/* device-resident collectives                                          */
+/* ------------------------------------------------------------------ */
+int inccl_allreduce_q32(struct inccl_communicator *c, const int32_t *src_dev, int32_t *dst_dev, size_t n,
+                        void *stream)
+{
+    if (!c || (!src_dev && n) || (!dst_dev && n)) return inccl_set_error(INCCL_ERR_ARG, "bad allreduce_q32 args");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (n == 0) return 0;
+    return inccl_tp_allreduce_q32(c, src_dev, dst_dev, n, st);
+}
+
+/* One bucket piece: quant + local sum -> reduce-scatter -> dequant shard ->
+ * all-gather.  `ws` holds W*shard + shard int32; `fws` (if the gather cannot
+ * land in dst in place) W*shard fp32. */
+static int allreduce_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n,
+                           int k, const uint32_t *amax, int scale_R, int32_t *ws, float *fws, hipStream_t st)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
+    int32_t *qsend = ws, *qrecv = ws + total;
+    int rc = kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_Q32, (const void *const *)srcs, R, qsend, n, k, amax,
+                                 scale_R, st));
+    if (rc) return rc;
+    if (total > n) INCCL_HIP(hipMemsetAsync(qsend + n, 0, (total - n) * sizeof(int32_t), st));
+    rc = inccl_tp_reduce_scatter_q32(c, qsend, qrecv, shard, st);
+    if (rc) return rc;
+    const size_t lo = (size_t)me * shard;
+    const int in_place = (total == n);
+    float *gather = in_place ? dst : fws;
+    const void *s1[1] = {qrecv};
+    rc = kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, gather + lo, shard, k, amax, scale_R, st));
+    if (rc) return rc;
+    rc = inccl_tp_all_gather_f32(c, gather + lo, gather, shard, st);
+    if (rc) return rc;
+    if (!in_place) INCCL_HIP(hipMemcpyAsync(dst, fws, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    return 0;
+}
+
+static int resolve_scale(struct inccl_communicator *c, const float *const *srcs, int R, size_t n, int scale_exp,
+                         hipStream_t st, const uint32_t **amax_out)
+{
+    *amax_out = NULL;
+    if (scale_exp != INCCL_SCALE_AUTO) {
+        if (scale_exp < INCCL_SCALE_MIN || scale_exp > INCCL_SCALE_MAX)
+            return inccl_set_error(INCCL_ERR_ARG, "scale_exp %d out of range", scale_exp);
+        return 0;
+    }
+    int rc = inccl_absmax_f32(srcs, R, n, c->d_words, 1, st);
+    if (rc) return rc;
+    if (c->group->world_size > 1) {
+        rc = inccl_tp_allreduce_max_u32(c, c->d_words, 1, st);
+        if (rc) return rc;
+    }
+    *amax_out = c->d_words;
+    return 0;
+}
+
+int inccl_allreduce_f32(struct inccl_communicator *c, const float *const *srcs_dev, int R, float *dst_dev, size_t n,
+                        int scale_exp, void *stream)
+{
+    return inccl_allreduce_f32_pipelined(c, srcs_dev, R, dst_dev, n, scale_exp, 1, stream);
+}
+
+int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *const *srcs_dev, int R, float *dst_dev,
+                                  size_t n, int scale_exp, int chunks, void *stream)
+{
+    if (!c || !srcs_dev || R < 1 || R > INCCL_MAX_LOCAL_INPUTS || (!dst_dev && n))
+        return inccl_set_error(INCCL_ERR_ARG, "bad allreduce_f32 args");
+    for (int r = 0; r < R; ++r)
+        if (!srcs_dev[r] && n) return inccl_set_error(INCCL_ERR_ARG, "srcs[%d] is NULL", r);
+    if (n == 0) return 0;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const int W = c->group->world_size;
+    const uint32_t *amax = NULL;
+    int rc = resolve_scale(c, srcs_dev, R, n, scale_exp, st, &amax);
+    if (rc) return rc;
+    const int k = amax ? 0 : scale_exp;
+    const int scale_R = R * W;
+
+    const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: RS/AG path even at world 1 */
+    if (W == 1 && !(fs && atoi(fs) != 0))   /* one fused HBM pass: quant + sum + dequant */
+        return kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, k,
+                                   amax, scale_R, st));
+
+    /* chunk boundaries: multiples of W*64 elements so every chunk's shards are
+     * 256-B aligned inside dst; each chunk has its own workspace region */
+    if (chunks < 1) chunks = 1;
+    const size_t unit = (size_t)W * 64;
+    size_t per = ((n + (size_t)chunks - 1) / (size_t)chunks + unit - 1) / unit * unit;
+    if (per == 0) per = unit;
+    size_t ws_elems = 0, fws_elems = 0;
+    for (size_t off = 0; off < n; off += per) {
+        const size_t cnt = (n - off) < per ? (n - off) : per;
+        const size_t shard = inccl_shard_elems(cnt, W);
+        ws_elems += shard * (size_t)W + shard;
+        if (shard * (size_t)W != cnt) fws_elems = shard * (size_t)W;
+    }
+    rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, ws_elems * sizeof(int32_t));
+    if (rc) return rc;
+    if (fws_elems) {
+        rc = inccl_ensure_dev(&c->d_f32, &c->d_f32_bytes, fws_elems * sizeof(float));
+        if (rc) return rc;
+    }
+    int32_t *ws = (int32_t *)c->d_q32;
+    const float *sub[INCCL_MAX_LOCAL_INPUTS];
+    if (per >= n) return allreduce_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, ws, (float *)c->d_f32, st);
+
+    /* pipelined: quantise chunk i+1 on the side stream while chunk i's
+     * collectives run on `st` (RCCL kernels and the HBM-bound quantiser share
+     * the chip).  ev[0]: side stream caught up with st's prior work. */
+    INCCL_HIP(hipEventRecord(c->ev[0], st));
+    INCCL_HIP(hipStreamWaitEvent(c->side_stream, c->ev[0], 0));
+    for (size_t off = 0; off < n; off += per) {
+        const size_t cnt = (n - off) < per ? (n - off) : per;
+        const size_t shard = inccl_shard_elems(cnt, W), total = shard * (size_t)W;
+        for (int r = 0; r < R; ++r) sub[r] = srcs_dev[r] + off;
+        int32_t *qsend = ws, *qrecv = ws + total;
+        rc = kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_Q32, (const void *const *)sub, R, qsend, cnt, k, amax,
+                                 scale_R, c->side_stream));
+        if (rc) return rc;
+        if (total > cnt) INCCL_HIP(hipMemsetAsync(qsend + cnt, 0, (total - cnt) * sizeof(int32_t), c->side_stream));
+        INCCL_HIP(hipEventRecord(c->ev[1], c->side_stream));
+        INCCL_HIP(hipStreamWaitEvent(st, c->ev[1], 0));
+        rc = inccl_tp_reduce_scatter_q32(c, qsend, qrecv, shard, st);
+        if (rc) return rc;
+        const int in_place = (total == cnt);
+        float *gather = in_place ? dst_dev + off : (float *)c->d_f32;
+        const size_t lo = (size_t)c->group->rank * shard;
+        const void *s1[1] = {qrecv};
+        rc = kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, gather + lo, shard, k, amax, scale_R, st));
+        if (rc) return rc;
+        rc = inccl_tp_all_gather_f32(c, gather + lo, gather, shard, st);
+        if (rc) return rc;
+        if (!in_place)
+            INCCL_HIP(hipMemcpyAsync(dst_dev + off, c->d_f32, cnt * sizeof(float), hipMemcpyDeviceToDevice, st));
+        ws += total + shard;
+    }
+    /* `st` already waited on every side-stream chunk */
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* host-memory collectives                                              */
+/* ------------------------------------------------------------------ */
+/* Replaces api.c:403-452 / :330-401.  The reference encodes 1024-element
+ * messages into the registered buffer (api.c:300-302), lets the switch add
+ * them and decodes completions into dst (api.c:428-430).  Here the messages
+ * become large chunks staged through the pinned send/receive buffers, the
+ * sum runs on the GPU (RCCL or the local hub's sum kernel), and the same
+ * "whole messages only" rule applies. */
+static int allreduce_host_q32(struct inccl_communicator *c, const int32_t *src, uint32_t len, int32_t *dst)
+{
+    const size_t message_num = len / PAYLOAD_COUNT;          /* api.c:406 */
+    const size_t n = message_num * PAYLOAD_COUNT;
+    if (n == 0) return 0;
+    if (!src || !dst) return inccl_set_error(INCCL_ERR_ARG, "NULL src/dst");
+    INCCL_HIP(hipSetDevice(c->group->device));
+    hipStream_t st = c->stream;
+    int rc = inccl_ensure_dev(&c->d_stage, &c->d_stage_bytes, n * sizeof(int32_t));
+    if (rc) return rc;
+    int32_t *d = (int32_t *)c->d_stage;
+    /* two halves of each pinned buffer alternate (ping-pong) */
+    size_t chunk = c->payload_buf_size / 2 / sizeof(int32_t);
+    chunk = chunk / PAYLOAD_COUNT * PAYLOAD_COUNT;
+    if (chunk == 0) {
+        INCCL_HIP(hipMemcpyAsync(d, src, n * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    } else {
+        for (size_t off = 0, i = 0; off < n; off += chunk, ++i) {
+            const size_t cnt = (n - off) < chunk ? (n - off) : chunk;
+            char *half = c->send_payload + (i & 1) * chunk * sizeof(int32_t);
+            INCCL_HIP(hipEventSynchronize(c->ev[2 + (i & 1)]));   /* the DMA that last read this half */
+            memcpy(half, src + off, cnt * sizeof(int32_t));
+            INCCL_HIP(hipMemcpyAsync(d + off, half, cnt * sizeof(int32_t), hipMemcpyHostToDevice, st));
+            INCCL_HIP(hipEventRecord(c->ev[2 + (i & 1)], st));
+        }
+    }
+    rc = inccl_tp_allreduce_q32(c, d, d, n, st);
+    if (rc) return rc;
+    if (chunk == 0) {
+        INCCL_HIP(hipMemcpyAsync(dst, d, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        INCCL_HIP(hipStreamSynchronize(st));
+        return 0;
+    }
+    size_t prev_off = 0, prev_cnt = 0;
+    for (size_t off = 0, i = 0; off < n; off += chunk, ++i) {
+        const size_t cnt = (n - off) < chunk ? (n - off) : chunk;
+        char *half = c->receive_payload + (i & 1) * chunk * sizeof(int32_t);
+        INCCL_HIP(hipMemcpyAsync(half, d + off, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        INCCL_HIP(hipEventRecord(c->ev[4 + (i & 1)], st));
+        if (i > 0) {   /* decode the previous completion while this one is in flight (api.c:428-430) */
+            INCCL_HIP(hipEventSynchronize(c->ev[4 + ((i - 1) & 1)]));
+            memcpy(dst + prev_off, c->receive_payload + ((i - 1) & 1) * chunk * sizeof(int32_t),
+                   prev_cnt * sizeof(int32_t));
+        }
+        prev_off = off;
+        prev_cnt = cnt;
+    }
+    const size_t last = (n + chunk - 1) / chunk - 1;
+    INCCL_HIP(hipEventSynchronize(c->ev[4 + (last & 1)]));
+    memcpy(dst + prev_off, c->receive_payload + (last & 1) * chunk * sizeof(int32_t), prev_cnt * sizeof(int32_t));
+    return 0;
+}
+
+void inccl_allreduce_write(struct inccl_communicator *comm, int32_t *src_data, uint32_t len, int32_t *dst_data)
+{
+    if (!comm) {
+        fprintf(stderr, "inccl_allreduce_write: NULL communicator\n");
+        return;
+    }
+    if (allreduce_host_q32(comm, src_data, len, dst_data) != 0)
+        fprintf(stderr, "inccl_allreduce_write: %s\n", inccl_last_error());
+}
+
+void inccl_allreduce_sendrecv(struct inccl_communicator *comm, int32_t *src_data, uint32_t len, int32_t *dst_data)
+{
+    if (!comm) {
+        fprintf(stderr, "inccl_allreduce_sendrecv: NULL communicator\n");
+        return;
+    }
+    if (allreduce_host_q32(comm, src_data, len, dst_data) != 0)
+        fprintf(stderr, "inccl_allreduce_sendrecv: %s\n", inccl_last_error());
+}
+
+/* BASELINE config 3: fp32 gradient in host memory, buckets pipelined over
+ * three streams -- H2D (copy_streams[0]), reduce (stream), D2H (copy_streams[1]). */
+int inccl_allreduce_f32_host(struct inccl_communicator *c, const float *src_host, float *dst_host, size_t n,
+                             int scale_exp, size_t bucket_bytes)
+{
+    if (!c || (!src_host && n) || (!dst_host && n)) return inccl_set_error(INCCL_ERR_ARG, "bad allreduce_f32_host args");
+    if (n == 0) return 0;
+    INCCL_HIP(hipSetDevice(c->group->device));
+    size_t B = bucket_bytes / sizeof(float);
+    B = B / 64 * 64;
+    if (B == 0 || B > n) B = n;
+    int rc = inccl_ensure_dev(&c->d_stage, &c->d_stage_bytes, 4 * B * sizeof(float));
+    if (rc) return rc;
+    float *in[2] = {(float *)c->d_stage, (float *)c->d_stage + B};
+    float *out[2] = {(float *)c->d_stage + 2 * B, (float *)c->d_stage + 3 * B};
+    hipStream_t h2d = c->copy_streams[0], d2h = c->copy_streams[1], ks = c->stream;
+    hipEvent_t ev_h2d[2] = {c->ev[0], c->ev[1]}, ev_k[2] = {c->ev[2], c->ev[3]}, ev_d2h[2] = {c->ev[4], c->ev[5]};
+    /* start clean: streams idle w.r.t. earlier work on the compute stream */
+    INCCL_HIP(hipStreamSynchronize(ks));
+    size_t i = 0;
+    for (size_t off = 0; off < n; off += B, ++i) {
+        const size_t cnt = (n - off) < B ? (n - off) : B;
+        const int s = (int)(i & 1);
+        if (i >= 2) INCCL_HIP(hipStreamWaitEvent(h2d, ev_k[s], 0));      /* in[s] consumed */
+        INCCL_HIP(hipMemcpyAsync(in[s], src_host + off, cnt * sizeof(float), hipMemcpyHostToDevice, h2d));
+        INCCL_HIP(hipEventRecord(ev_h2d[s], h2d));
+        INCCL_HIP(hipStreamWaitEvent(ks, ev_h2d[s], 0));
+        if (i >= 2) INCCL_HIP(hipStreamWaitEvent(ks, ev_d2h[s], 0));     /* out[s] drained */
+        const float *srcs[1] = {in[s]};
+        rc = inccl_allreduce_f32(c, srcs, 1, out[s], cnt, scale_exp, ks);
+        if (rc) return rc;
+        INCCL_HIP(hipEventRecord(ev_k[s], ks));
+        INCCL_HIP(hipStreamWaitEvent(d2h, ev_k[s], 0));
+        INCCL_HIP(hipMemcpyAsync(dst_host + off, out[s], cnt * sizeof(float), hipMemcpyDeviceToHost, d2h));
+        INCCL_HIP(hipEventRecord(ev_d2h[s], d2h));
+    }
+    INCCL_HIP(hipStreamSynchronize(d2h));
+    INCCL_HIP(hipStreamSynchronize(ks));
+    INCCL_HIP(hipStreamSynchronize(h2d));
+    return 0;
+}

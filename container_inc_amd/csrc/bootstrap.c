@@ -1,0 +1,207 @@
+/* bootstrap.c -- TCP rendezvous of a group (replaces repository/src/api.c:34-144).
+ *
+ * Reference: rank 0 accepts world_size-1 connections on MASTER_PORT, each
+ * rank sends {rank, ip} (api.c:43-76, :112-144), and rank 0 relays controller
+ * data to the group.  Here rank 0 accepts the same connections and later
+ * broadcasts the RCCL unique id of every communicator over them; there is no
+ * controller, topology YAML or switch to configure. */
+#define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <errno.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "inccl_internal.h"
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static double boot_timeout_s(void)
+{
+    const char *e = getenv("INCCL_BOOT_TIMEOUT");
+    double t = e ? atof(e) : 0.0;
+    return t > 0.0 ? t : 300.0;
+}
+
+static int send_all(int fd, const void *buf, size_t n)
+{
+    const char *p = (const char *)buf;
+    while (n > 0) {
+        ssize_t k = send(fd, p, n, MSG_NOSIGNAL);
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            return -1;
+        }
+        p += k;
+        n -= (size_t)k;
+    }
+    return 0;
+}
+
+static int recv_all(int fd, void *buf, size_t n)
+{
+    char *p = (char *)buf;
+    const double deadline = now_s() + boot_timeout_s();
+    while (n > 0) {
+        struct pollfd pf = {fd, POLLIN, 0};
+        int ms = (int)((deadline - now_s()) * 1000.0);
+        if (ms <= 0) return -1;
+        int pr = poll(&pf, 1, ms);
+        if (pr < 0 && errno == EINTR) continue;
+        if (pr <= 0) return -1;
+        ssize_t k = recv(fd, p, n, 0);
+        if (k < 0 && errno == EINTR) continue;
+        if (k <= 0) return -1;
+        p += k;
+        n -= (size_t)k;
+    }
+    return 0;
+}
+
+static void tune_fd(int fd)
+{
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+}
+
+int inccl_boot_master(struct inccl_group *g)
+{
+    const int peers = g->world_size - 1;
+    g->peer_fds = (int *)calloc((size_t)g->world_size, sizeof(int));
+    if (!g->peer_fds) return inccl_set_error(INCCL_ERR_NOMEM, "bootstrap: out of memory");
+    for (int i = 0; i < g->world_size; ++i) g->peer_fds[i] = -1;
+    if (peers == 0) return 0;
+
+    int ls = socket(AF_INET, SOCK_STREAM, 0);
+    if (ls < 0) return inccl_set_error(INCCL_ERR_SYS, "bootstrap: socket: %s", strerror(errno));
+    int one = 1;
+    setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    struct sockaddr_in addr;
+    memset(&addr, 0, sizeof(addr));
+    addr.sin_family = AF_INET;
+    addr.sin_addr.s_addr = htonl(INADDR_ANY);
+    addr.sin_port = htons((uint16_t)g->port);
+    if (bind(ls, (struct sockaddr *)&addr, sizeof(addr)) < 0 || listen(ls, peers + 4) < 0) {
+        int rc = inccl_set_error(INCCL_ERR_SYS, "bootstrap: bind/listen port %d: %s", g->port, strerror(errno));
+        close(ls);
+        return rc;
+    }
+    const double deadline = now_s() + boot_timeout_s();
+    int joined = 0;
+    while (joined < peers) {
+        struct pollfd pf = {ls, POLLIN, 0};
+        int ms = (int)((deadline - now_s()) * 1000.0);
+        if (ms <= 0) break;
+        int pr = poll(&pf, 1, ms);
+        if (pr < 0 && errno == EINTR) continue;
+        if (pr <= 0) break;
+        int fd = accept(ls, NULL, NULL);
+        if (fd < 0) continue;
+        tune_fd(fd);
+        int32_t hello[2];
+        /* {rank, world_size}: the reference sends {rank, ip} (api.c:130-134) */
+        if (recv_all(fd, hello, sizeof(hello)) != 0 || hello[0] <= 0 || hello[0] >= g->world_size ||
+            hello[1] != g->world_size || g->peer_fds[hello[0]] != -1) {
+            close(fd);
+            continue;
+        }
+        g->peer_fds[hello[0]] = fd;
+        joined++;
+    }
+    close(ls);
+    if (joined < peers) return inccl_set_error(INCCL_ERR_SYS, "bootstrap: only %d of %d ranks joined", joined, peers);
+    /* release the workers only once everyone is in */
+    const char go = 'G';
+    for (int r = 1; r < g->world_size; ++r)
+        if (send_all(g->peer_fds[r], &go, 1) != 0)
+            return inccl_set_error(INCCL_ERR_SYS, "bootstrap: send to rank %d failed", r);
+    return 0;
+}
+
+int inccl_boot_worker(struct inccl_group *g)
+{
+    struct addrinfo hints, *res = NULL;
+    memset(&hints, 0, sizeof(hints));
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    char port[16];
+    snprintf(port, sizeof(port), "%d", g->port);
+    if (getaddrinfo(g->master_ip, port, &hints, &res) != 0 || !res)
+        return inccl_set_error(INCCL_ERR_SYS, "bootstrap: cannot resolve %s", g->master_ip);
+    const double deadline = now_s() + boot_timeout_s();
+    int fd = -1;
+    while (now_s() < deadline) {
+        fd = socket(AF_INET, SOCK_STREAM, 0);
+        if (fd < 0) break;
+        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0) break;
+        close(fd);
+        fd = -1;
+        usleep(20000);   /* rank 0 may not be listening yet */
+    }
+    freeaddrinfo(res);
+    if (fd < 0) return inccl_set_error(INCCL_ERR_SYS, "bootstrap: connect %s:%d failed", g->master_ip, g->port);
+    tune_fd(fd);
+    int32_t hello[2] = {g->rank, g->world_size};
+    char go = 0;
+    if (send_all(fd, hello, sizeof(hello)) != 0 || recv_all(fd, &go, 1) != 0 || go != 'G') {
+        close(fd);
+        return inccl_set_error(INCCL_ERR_SYS, "bootstrap: handshake with rank 0 failed");
+    }
+    g->master_fd = fd;
+    return 0;
+}
+
+int inccl_boot_bcast(struct inccl_group *g, void *buf, size_t bytes)
+{
+    if (g->world_size == 1) return 0;
+    if (g->rank == 0) {
+        for (int r = 1; r < g->world_size; ++r)
+            if (send_all(g->peer_fds[r], buf, bytes) != 0)
+                return inccl_set_error(INCCL_ERR_SYS, "bootstrap: bcast to rank %d failed", r);
+        return 0;
+    }
+    if (recv_all(g->master_fd, buf, bytes) != 0) return inccl_set_error(INCCL_ERR_SYS, "bootstrap: bcast recv failed");
+    return 0;
+}
+
+int inccl_boot_barrier(struct inccl_group *g)
+{
+    if (g->world_size == 1) return 0;
+    char b = 'B';
+    if (g->rank == 0) {
+        for (int r = 1; r < g->world_size; ++r)
+            if (recv_all(g->peer_fds[r], &b, 1) != 0) return inccl_set_error(INCCL_ERR_SYS, "barrier: recv failed");
+        for (int r = 1; r < g->world_size; ++r)
+            if (send_all(g->peer_fds[r], &b, 1) != 0) return inccl_set_error(INCCL_ERR_SYS, "barrier: send failed");
+        return 0;
+    }
+    if (send_all(g->master_fd, &b, 1) != 0 || recv_all(g->master_fd, &b, 1) != 0)
+        return inccl_set_error(INCCL_ERR_SYS, "barrier: exchange with rank 0 failed");
+    return 0;
+}
+
+void inccl_boot_close(struct inccl_group *g)
+{
+    if (g->peer_fds) {
+        for (int r = 0; r < g->world_size; ++r)
+            if (g->peer_fds[r] >= 0) close(g->peer_fds[r]);
+        free(g->peer_fds);
+        g->peer_fds = NULL;
+    }
+    if (g->master_fd >= 0) {
+        close(g->master_fd);
+        g->master_fd = -1;
+    }
+}

@@ -1,0 +1,120 @@
+/* inccl_internal.h -- private definitions of libinccl_amd.so (C11 host code).
+ *
+ * The reference's structs (repository/include/api.h:42-91) hold libibverbs
+ * handles; here the same roles are played by a transport (RCCL over xGMI, or
+ * the in-process "local" hub where the GPU acts as the aggregation switch),
+ * pinned host staging buffers (the registered MRs) and device workspaces. */
+#ifndef INCCL_INTERNAL_H
+#define INCCL_INTERNAL_H
+
+#include <pthread.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "inccl_amd.h"
+
+#define INCCL_TRANSPORT_RCCL 0
+#define INCCL_TRANSPORT_LOCAL 1
+
+struct inccl_local_hub;
+
+struct inccl_group {
+    int rank;
+    int world_size;
+    int device;
+    int transport;
+    char master_ip[64];
+    int port;
+    /* rccl transport: control sockets.  rank 0 holds one fd per peer (the
+     * reference's group_fd_list, api.h:58); other ranks hold master_fd. */
+    int master_fd;
+    int *peer_fds;
+    /* local transport */
+    struct inccl_local_hub *hub;
+    int comm_seq;   /* communicators created so far (names the hub slot) */
+};
+
+struct inccl_communicator {
+    struct inccl_group *group;
+    uint32_t payload_buf_size;   /* 2*size bytes, api.c:164 */
+    uint32_t window_size;        /* WINDOW_SIZE, api.c:226 */
+    char *send_payload;          /* pinned host staging (api.c:168) */
+    char *receive_payload;       /* pinned host staging (api.c:169) */
+    hipStream_t stream;          /* the communicator's compute/comm stream */
+    hipStream_t side_stream;     /* second stream for pipelined variants */
+    hipStream_t copy_streams[2]; /* H2D / D2H for the host-memory pipeline */
+    void *nccl;                  /* ncclComm_t (rccl transport) */
+    int comm_id;                 /* index within the group */
+    /* device workspaces, grown on demand (never inside a capture) */
+    void *d_q32;                 /* int32 partials, padded to world * shard */
+    size_t d_q32_bytes;
+    void *d_f32;                 /* fp32 gather target when dst cannot be used in place */
+    size_t d_f32_bytes;
+    void *d_stage;               /* host-path device staging (2 x in + 2 x out buckets) */
+    size_t d_stage_bytes;
+    uint32_t *d_words;           /* small scratch words: [0] absmax, [1] checksum */
+    hipEvent_t ev[8];
+};
+
+/* transport operations; all stream-ordered on `st` */
+int inccl_tp_reduce_scatter_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t shard,
+                                hipStream_t st);
+int inccl_tp_all_gather_f32(struct inccl_communicator *c, const float *send, float *recv, size_t shard,
+                            hipStream_t st);
+int inccl_tp_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
+                           hipStream_t st);
+int inccl_tp_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st);
+int inccl_tp_barrier(struct inccl_communicator *c);
+
+/* rccl transport */
+int inccl_rccl_comm_init(struct inccl_communicator *c);
+void inccl_rccl_comm_destroy(struct inccl_communicator *c);
+int inccl_rccl_reduce_scatter_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t shard,
+                                  hipStream_t st);
+int inccl_rccl_all_gather_f32(struct inccl_communicator *c, const float *send, float *recv, size_t shard,
+                              hipStream_t st);
+int inccl_rccl_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
+                             hipStream_t st);
+int inccl_rccl_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st);
+
+/* local transport */
+struct inccl_local_hub *inccl_hub_attach(const char *name, int world_size);
+void inccl_hub_detach(struct inccl_local_hub *hub);
+int inccl_local_reduce_scatter_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t shard,
+                                   hipStream_t st);
+int inccl_local_all_gather_f32(struct inccl_communicator *c, const float *send, float *recv, size_t shard,
+                               hipStream_t st);
+int inccl_local_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
+                              hipStream_t st);
+int inccl_local_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st);
+int inccl_local_barrier(struct inccl_communicator *c);
+
+/* TCP bootstrap (bootstrap.c) */
+int inccl_boot_master(struct inccl_group *g);
+int inccl_boot_worker(struct inccl_group *g);
+int inccl_boot_bcast(struct inccl_group *g, void *buf, size_t bytes);   /* from rank 0 */
+int inccl_boot_barrier(struct inccl_group *g);
+void inccl_boot_close(struct inccl_group *g);
+
+/* errors */
+int inccl_set_error(int code, const char *fmt, ...);
+int inccl_hip_check(hipError_t e, const char *what);
+#define INCCL_HIP(call)                                         \
+    do {                                                        \
+        hipError_t e_ = (call);                                 \
+        if (e_ != hipSuccess) return inccl_hip_check(e_, #call); \
+    } while (0)
+
+/* shard size for world ranks: multiple of 64 elements (256 B) so every shard
+ * starts 16-B aligned for the dwordx4 kernels */
+static inline size_t inccl_shard_elems(size_t n, int world)
+{
+    size_t per = (n + (size_t)world - 1) / (size_t)world;
+    return (per + 63) & ~(size_t)63;
+}
+
+int inccl_ensure_dev(void **p, size_t *cur, size_t need);
+
+#endif

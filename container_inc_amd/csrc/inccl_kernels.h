@@ -1,0 +1,26 @@
+/* inccl_kernels.h -- the thin C-ABI shim between the C host code and the HIP
+ * kernels in inccl_kernels.hip.  Internal to libinccl_amd.so. */
+#ifndef INCCL_KERNELS_H
+#define INCCL_KERNELS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "inccl_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* out[i] = OUT(sum_r IN(srcs[r][i])), kinds INCCL_KIND_*.  Returns 0 or a hipError_t / INCCL_ERR_ARG. */
+int inccl_k_stream(int in_kind, int out_kind, const void *const *srcs, int R, void *dst, size_t n, int scale_exp,
+                   const uint32_t *amax_bits_dev, int scale_R, void *stream);
+int inccl_k_absmax(const float *const *srcs, int R, size_t n, uint32_t *amax_bits_dev, int zero_first, void *stream);
+int inccl_k_checksum(const int32_t *q, size_t n, uint64_t index_base, uint32_t *out_dev, int zero_first,
+                     void *stream);
+void inccl_k_set_tuning(int grid_cap, int nt_loads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,432 @@
+// inccl_kernels.hip -- CDNA4 (gfx950) kernels of the INCCL aggregation hot path.
+//
+// Every kernel here is element-wise and HBM-bound (a few VALU ops per 4-byte
+// element): no MFMA, no LDS staging of the stream.  One generic streaming
+// kernel covers the whole per-element family of the reference path:
+//
+//   input  kind  F32      fp32 gradient, quantised on load  (new front stage)
+//                Q32      int32 host order                   (nts.c:361 aggregator lanes)
+//                Q32BE    int32 big-endian wire word         (api.c:301 / nts.c:362 ntohl)
+//   output kind  F32      dequantised fp32                   (new back stage)
+//                Q32      int32 host order                   (api.c:429 decode)
+//                Q32BE    int32 big-endian wire word         (util.c:404 egress htonl)
+//
+//   out[i] = OUT( sum_{r<R} IN(src_r[i]) )     sum in uint32 = exact mod-2^32 wrap.
+//
+// So quantise = <F32,Q32,1>, dequantise = <Q32,F32,1>, the fused single-GPU
+// bucket reduce = <F32,F32,R>, the switch aggregate = <Q32BE,Q32BE,R>, the
+// multi-GPU first stage = <F32,Q32,R>, and the byte swap codec = <Q32BE,Q32,1>.
+//
+// Layout: each lane moves 16 B per access (global_load_dwordx4 = one 1 KiB
+// wave-instruction = exactly one reference packet payload of 256 lanes,
+// nts.c:55).  A workgroup of 256 lanes owns a tile of 256*U float4 per input and
+// issues all R*U loads before touching them (R*U*16 B in flight per lane), then
+// writes U nontemporal float4 stores.  Grid-stride over tiles.
+//
+// The horizontal reductions (absmax for automatic scaling, the position
+// weighted checksum) use wave64 __shfl_xor trees, an LDS stage across the
+// block's waves and one global atomic per block.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "inccl_kernels.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxR = INCCL_MAX_LOCAL_INPUTS;
+
+enum Kind { F32 = 0, Q32 = 1, Q32BE = 2 };
+
+struct SrcPtrs {
+    const void* p[kMaxR];
+};
+
+// Quantiser scale source: a static exponent, or the absmax word written by
+// k_absmax (auto scaling, spec = orc_choose_scale).
+struct Scale {
+    int k;
+    const uint32_t* amax_bits;  // nullptr -> use k
+    int scale_R;                // contributors for auto scale
+};
+
+__device__ __forceinline__ float pow2f(int k) { return __uint_as_float((uint32_t)(k + 127) << 23); }
+
+// Same arithmetic as orc_choose_scale (oracle/inccl_oracle.c).
+__device__ __forceinline__ int choose_scale(float amax, int R)
+{
+    if (!(amax > 0.0f)) return INCCL_SCALE_MAX;
+    if (__builtin_isinf(amax)) return INCCL_SCALE_MIN;
+    double t = (double)amax * (double)R;
+    int e;
+    double m = frexp(t, &e);
+    int k = (m == 0.5) ? (31 - e) : (30 - e);
+    k = k < INCCL_SCALE_MIN ? INCCL_SCALE_MIN : k;
+    k = k > INCCL_SCALE_MAX ? INCCL_SCALE_MAX : k;
+    return k;
+}
+
+__device__ __forceinline__ int resolve_k(const Scale& s)
+{
+    if (s.amax_bits == nullptr) return s.k;
+    const uint32_t bits = __builtin_nontemporal_load(s.amax_bits);
+    return choose_scale(__uint_as_float(bits), s.scale_R);
+}
+
+// q = sat_i32(rne(x * 2^k)), NaN -> 0  (orc_quantise_one)
+__device__ __forceinline__ uint32_t quant1(float x, float scale)
+{
+    float y = x * scale;
+    y = (y != y) ? 0.0f : y;
+    y = __builtin_rintf(y);
+    int32_t q = (y >= 2147483648.0f) ? INT32_MAX : ((y <= -2147483648.0f) ? INT32_MIN : (int32_t)y);
+    return (uint32_t)q;
+}
+
+template <int IN>
+__device__ __forceinline__ uint32_t load_xform(uint32_t raw, float scale)
+{
+    if constexpr (IN == F32) return quant1(__uint_as_float(raw), scale);
+    else if constexpr (IN == Q32BE) return __builtin_bswap32(raw);
+    else return raw;
+}
+
+template <int OUT>
+__device__ __forceinline__ uint32_t store_xform(uint32_t acc, float inv)
+{
+    if constexpr (OUT == F32) return __float_as_uint((float)(int32_t)acc * inv);
+    else if constexpr (OUT == Q32BE) return __builtin_bswap32(acc);
+    else return acc;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Loads per lane per input in one tile; keeps R*U*16 B in flight per lane.
+template <int R>
+struct Unroll {
+    static constexpr int U = (R >= 8) ? 1 : ((R >= 4) ? 2 : ((R >= 2) ? 4 : 8));
+};
+
+template <int IN, int OUT, int R, bool NT>
+__global__ __launch_bounds__(kBlock) void k_stream_vec(SrcPtrs src, void* __restrict__ dst, int64_t n4,
+                                                       Scale sc)
+{
+    constexpr int U = Unroll<R>::U;
+    const int k = resolve_k(sc);
+    const float scale = pow2f(k);
+    const float inv = pow2f(-k);
+    const int64_t tile_elems = (int64_t)kBlock * U;
+    const int64_t stride = (int64_t)gridDim.x * tile_elems;
+    u32x4* __restrict__ out = reinterpret_cast<u32x4*>(dst);
+
+    for (int64_t base = (int64_t)blockIdx.x * tile_elems; base < n4; base += stride) {
+        const int64_t i0 = base + threadIdx.x;
+        if (base + tile_elems <= n4) {
+            u32x4 v[R][U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const u32x4* p = reinterpret_cast<const u32x4*>(src.p[r]) + i0 + (int64_t)u * kBlock;
+                    v[r][u] = NT ? __builtin_nontemporal_load(p) : *p;
+                }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    acc.x += load_xform<IN>(v[r][u].x, scale);
+                    acc.y += load_xform<IN>(v[r][u].y, scale);
+                    acc.z += load_xform<IN>(v[r][u].z, scale);
+                    acc.w += load_xform<IN>(v[r][u].w, scale);
+                }
+                u32x4 o;
+                o.x = store_xform<OUT>(acc.x, inv);
+                o.y = store_xform<OUT>(acc.y, inv);
+                o.z = store_xform<OUT>(acc.z, inv);
+                o.w = store_xform<OUT>(acc.w, inv);
+                __builtin_nontemporal_store(o, out + i0 + (int64_t)u * kBlock);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = i0 + (int64_t)u * kBlock;
+                if (i < n4) {
+                    u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const u32x4 x = reinterpret_cast<const u32x4*>(src.p[r])[i];
+                        acc.x += load_xform<IN>(x.x, scale);
+                        acc.y += load_xform<IN>(x.y, scale);
+                        acc.z += load_xform<IN>(x.z, scale);
+                        acc.w += load_xform<IN>(x.w, scale);
+                    }
+                    u32x4 o;
+                    o.x = store_xform<OUT>(acc.x, inv);
+                    o.y = store_xform<OUT>(acc.y, inv);
+                    o.z = store_xform<OUT>(acc.z, inv);
+                    o.w = store_xform<OUT>(acc.w, inv);
+                    out[i] = o;
+                }
+            }
+        }
+    }
+}
+
+// Element-granular variant: the scalar tail after the float4 body, and the whole
+// range when any pointer is not 16-B aligned.
+template <int IN, int OUT, int R>
+__global__ __launch_bounds__(kBlock) void k_stream_scalar(SrcPtrs src, void* __restrict__ dst, int64_t begin,
+                                                          int64_t n, Scale sc)
+{
+    const int k = resolve_k(sc);
+    const float scale = pow2f(k);
+    const float inv = pow2f(-k);
+    uint32_t* __restrict__ out = reinterpret_cast<uint32_t*>(dst);
+    for (int64_t i = begin + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc += load_xform<IN>(reinterpret_cast<const uint32_t*>(src.p[r])[i], scale);
+        out[i] = store_xform<OUT>(acc, inv);
+    }
+}
+
+// ---- horizontal reductions: wave64 shuffle -> LDS -> one atomic per block ----
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)v, off, 64);
+        v = v > o ? v : o;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off, 64);
+    return v;
+}
+
+// |x| bits of a float; NaN -> 0 (ignored, as orc_absmax_f32).  Non-negative
+// IEEE floats order like their bit patterns, so max over bits == max over values.
+__device__ __forceinline__ uint32_t abs_bits(uint32_t b)
+{
+    const uint32_t a = b & 0x7fffffffu;
+    return a > 0x7f800000u ? 0u : a;
+}
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_absmax(SrcPtrs src, int64_t n, uint32_t* __restrict__ out)
+{
+    __shared__ uint32_t part[kBlock / 64];
+    uint32_t m = 0;
+    const int64_t n4 = n >> 2;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const u32x4* p = reinterpret_cast<const u32x4*>(src.p[r]);
+        for (int64_t i = t0; i < n4; i += stride) {
+            const u32x4 x = __builtin_nontemporal_load(p + i);
+            const uint32_t a = max(max(abs_bits(x.x), abs_bits(x.y)), max(abs_bits(x.z), abs_bits(x.w)));
+            m = m > a ? m : a;
+        }
+        const uint32_t* s = reinterpret_cast<const uint32_t*>(src.p[r]);
+        for (int64_t i = (n4 << 2) + t0; i < n; i += stride) {
+            const uint32_t a = abs_bits(s[i]);
+            m = m > a ? m : a;
+        }
+    }
+    m = wave_max_u32(m);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) part[wave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t b = part[0];
+#pragma unroll
+        for (int w = 1; w < kBlock / 64; ++w) b = b > part[w] ? b : part[w];
+        atomicMax(out, b);
+    }
+}
+
+// cs = sum_i (2*(base+i)+1) * q[i]  mod 2^32  (orc_checksum_q32); linear in q.
+__global__ __launch_bounds__(kBlock) void k_checksum(const uint32_t* __restrict__ q, int64_t n, uint64_t base,
+                                                     uint32_t* __restrict__ out)
+{
+    __shared__ uint32_t part[kBlock / 64];
+    uint32_t s = 0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const int64_t n4 = n >> 2;
+    const u32x4* q4 = reinterpret_cast<const u32x4*>(q);
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride) {
+        const u32x4 x = q4[i];
+        const uint32_t w = 2u * (uint32_t)(base + (uint64_t)(i << 2)) + 1u;
+        s += w * x.x + (w + 2u) * x.y + (w + 4u) * x.z + (w + 6u) * x.w;
+    }
+    for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        s += (2u * (uint32_t)(base + (uint64_t)i) + 1u) * q[i];
+    s = wave_sum_u32(s);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) part[wave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t b = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) b += part[w];
+        atomicAdd(out, b);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-side dispatch
+// ---------------------------------------------------------------------------
+int g_num_cus = 0;
+int g_grid_cap = 0;   // 0 -> default; settable for tuning sweeps
+bool g_nt_loads = true;
+
+int num_cus()
+{
+    if (g_num_cus == 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            g_num_cus = v;
+        else
+            g_num_cus = 256;
+    }
+    return g_num_cus;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template <int IN, int OUT, int R>
+int launch_stream_R(const SrcPtrs& s, void* dst, int64_t n, const Scale& sc, hipStream_t st)
+{
+    bool vec = aligned16(dst);
+    for (int r = 0; r < R; ++r) vec = vec && aligned16(s.p[r]);
+    int64_t done = 0;
+    if (vec) {
+        const int64_t n4 = n >> 2;
+        if (n4 > 0) {
+            constexpr int U = Unroll<R>::U;
+            const int64_t tiles = (n4 + (int64_t)kBlock * U - 1) / ((int64_t)kBlock * U);
+            const int64_t cap = g_grid_cap > 0 ? g_grid_cap : (int64_t)num_cus() * 16;
+            const int grid = (int)(tiles < cap ? tiles : cap);
+            if (g_nt_loads)
+                hipLaunchKernelGGL((k_stream_vec<IN, OUT, R, true>), dim3(grid), dim3(kBlock), 0, st, s, dst, n4, sc);
+            else
+                hipLaunchKernelGGL((k_stream_vec<IN, OUT, R, false>), dim3(grid), dim3(kBlock), 0, st, s, dst, n4, sc);
+        }
+        done = n4 << 2;
+    }
+    if (done < n) {
+        const int64_t rem = n - done;
+        int64_t blocks = (rem + kBlock - 1) / kBlock;
+        const int64_t cap = (int64_t)num_cus() * 8;
+        const int grid = (int)(blocks < cap ? blocks : cap);
+        hipLaunchKernelGGL((k_stream_scalar<IN, OUT, R>), dim3(grid), dim3(kBlock), 0, st, s, dst, done, n, sc);
+    }
+    return (int)hipGetLastError();
+}
+
+template <int IN, int OUT>
+int launch_stream(const void* const* srcs, int R, void* dst, int64_t n, const Scale& sc, hipStream_t st)
+{
+    if (R < 1 || R > kMaxR) return INCCL_ERR_ARG;
+    if (n <= 0) return 0;
+    SrcPtrs s = {};
+    for (int r = 0; r < R; ++r) {
+        if (srcs[r] == nullptr) return INCCL_ERR_ARG;
+        s.p[r] = srcs[r];
+    }
+    switch (R) {
+    case 1: return launch_stream_R<IN, OUT, 1>(s, dst, n, sc, st);
+    case 2: return launch_stream_R<IN, OUT, 2>(s, dst, n, sc, st);
+    case 3: return launch_stream_R<IN, OUT, 3>(s, dst, n, sc, st);
+    case 4: return launch_stream_R<IN, OUT, 4>(s, dst, n, sc, st);
+    case 5: return launch_stream_R<IN, OUT, 5>(s, dst, n, sc, st);
+    case 6: return launch_stream_R<IN, OUT, 6>(s, dst, n, sc, st);
+    case 7: return launch_stream_R<IN, OUT, 7>(s, dst, n, sc, st);
+    default: return launch_stream_R<IN, OUT, 8>(s, dst, n, sc, st);
+    }
+}
+
+int dispatch(int in_kind, int out_kind, const void* const* srcs, int R, void* dst, int64_t n, const Scale& sc,
+             hipStream_t st)
+{
+#define INCCL_CASE(I, O) \
+    if (in_kind == I && out_kind == O) return launch_stream<I, O>(srcs, R, dst, n, sc, st);
+    INCCL_CASE(F32, F32) INCCL_CASE(F32, Q32) INCCL_CASE(F32, Q32BE)
+    INCCL_CASE(Q32, F32) INCCL_CASE(Q32, Q32) INCCL_CASE(Q32, Q32BE)
+    INCCL_CASE(Q32BE, F32) INCCL_CASE(Q32BE, Q32) INCCL_CASE(Q32BE, Q32BE)
+#undef INCCL_CASE
+    return INCCL_ERR_ARG;
+}
+
+bool scale_ok(int k) { return k >= INCCL_SCALE_MIN && k <= INCCL_SCALE_MAX; }
+
+}  // namespace
+
+extern "C" {
+
+int inccl_k_stream(int in_kind, int out_kind, const void* const* srcs, int R, void* dst, size_t n, int scale_exp,
+                   const uint32_t* amax_bits_dev, int scale_R, void* stream)
+{
+    if (amax_bits_dev == nullptr && !scale_ok(scale_exp)) return INCCL_ERR_ARG;
+    if (dst == nullptr && n > 0) return INCCL_ERR_ARG;
+    Scale sc{scale_exp, amax_bits_dev, scale_R > 0 ? scale_R : R};
+    return dispatch(in_kind, out_kind, srcs, R, dst, (int64_t)n, sc, (hipStream_t)stream);
+}
+
+int inccl_k_absmax(const float* const* srcs, int R, size_t n, uint32_t* amax_bits_dev, int zero_first, void* stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    if (R < 1 || R > kMaxR || amax_bits_dev == nullptr) return INCCL_ERR_ARG;
+    SrcPtrs s = {};
+    for (int r = 0; r < R; ++r) {
+        if (srcs[r] == nullptr || !aligned16(srcs[r])) return INCCL_ERR_ARG;
+        s.p[r] = srcs[r];
+    }
+    if (zero_first) {
+        hipError_t e = hipMemsetAsync(amax_bits_dev, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return (int)e;
+    }
+    if (n == 0) return 0;
+    const int64_t blocks = ((int64_t)(n >> 2) + kBlock - 1) / kBlock;
+    const int64_t cap = (int64_t)num_cus() * 8;
+    const int grid = (int)(blocks < 1 ? 1 : (blocks < cap ? blocks : cap));
+    switch (R) {
+#define INCCL_AM(RR) \
+    case RR: hipLaunchKernelGGL((k_absmax<RR>), dim3(grid), dim3(kBlock), 0, st, s, (int64_t)n, amax_bits_dev); break;
+        INCCL_AM(1) INCCL_AM(2) INCCL_AM(3) INCCL_AM(4) INCCL_AM(5) INCCL_AM(6) INCCL_AM(7) INCCL_AM(8)
+#undef INCCL_AM
+    }
+    return (int)hipGetLastError();
+}
+
+int inccl_k_checksum(const int32_t* q, size_t n, uint64_t index_base, uint32_t* out_dev, int zero_first, void* stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    if (out_dev == nullptr || (q == nullptr && n > 0) || !aligned16(q)) return INCCL_ERR_ARG;
+    if (zero_first) {
+        hipError_t e = hipMemsetAsync(out_dev, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return (int)e;
+    }
+    if (n == 0) return 0;
+    const int64_t blocks = ((int64_t)(n >> 2) + kBlock - 1) / kBlock;
+    const int64_t cap = (int64_t)num_cus() * 8;
+    const int grid = (int)(blocks < 1 ? 1 : (blocks < cap ? blocks : cap));
+    hipLaunchKernelGGL(k_checksum, dim3(grid), dim3(kBlock), 0, st, reinterpret_cast<const uint32_t*>(q),
+                       (int64_t)n, index_base, out_dev);
+    return (int)hipGetLastError();
+}
+
+void inccl_k_set_tuning(int grid_cap, int nt_loads)
+{
+    g_grid_cap = grid_cap;
+    g_nt_loads = nt_loads != 0;
+}
+
+}  // extern "C"

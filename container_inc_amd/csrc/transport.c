@@ -1,0 +1,284 @@
+/* transport.c -- the exchange step of the allreduce, over one of two transports.
+ *
+ *  rccl   one process per GPU; RCCL (rccl.h, "nccl" on ROCm) over xGMI.  The
+ *         reference's equivalent is the RoCE RC path to the software switch
+ *         (repository/src/api.c:293-327, non_termination_switch.c:303-501).
+ *  local  the ranks are threads of one process sharing one GPU; the GPU is the
+ *         aggregation switch: the reduce-scatter runs this library's own sum
+ *         kernel over every rank's buffer (the nts.c:361-363 aggregate), the
+ *         all-gather is device-to-device copies.  Used for the single-process
+ *         loopback harness and for multi-rank tests on a one-GPU box.
+ */
+#define _GNU_SOURCE
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <rccl/rccl.h>
+
+#include "inccl_internal.h"
+#include "inccl_kernels.h"
+
+/* ------------------------------------------------------------------ */
+/* rccl                                                                 */
+/* ------------------------------------------------------------------ */
+static int nccl_check(ncclResult_t r, const char *what)
+{
+    if (r == ncclSuccess) return 0;
+    return inccl_set_error(INCCL_ERR_NCCL, "%s: %s", what, ncclGetErrorString(r));
+}
+
+int inccl_rccl_comm_init(struct inccl_communicator *c)
+{
+    struct inccl_group *g = c->group;
+    ncclUniqueId id;
+    memset(&id, 0, sizeof(id));
+    if (g->rank == 0) {
+        int rc = nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+        if (rc) return rc;
+    }
+    int rc = inccl_boot_bcast(g, &id, sizeof(id));
+    if (rc) return rc;
+    ncclComm_t comm = NULL;
+    rc = nccl_check(ncclCommInitRank(&comm, g->world_size, id, g->rank), "ncclCommInitRank");
+    if (rc) return rc;
+    c->nccl = comm;
+    return 0;
+}
+
+void inccl_rccl_comm_destroy(struct inccl_communicator *c)
+{
+    if (c->nccl) {
+        ncclCommDestroy((ncclComm_t)c->nccl);
+        c->nccl = NULL;
+    }
+}
+
+int inccl_rccl_reduce_scatter_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t shard,
+                                  hipStream_t st)
+{
+    return nccl_check(ncclReduceScatter(send, recv, shard, ncclInt32, ncclSum, (ncclComm_t)c->nccl, st),
+                      "ncclReduceScatter");
+}
+
+int inccl_rccl_all_gather_f32(struct inccl_communicator *c, const float *send, float *recv, size_t shard,
+                              hipStream_t st)
+{
+    return nccl_check(ncclAllGather(send, recv, shard, ncclFloat32, (ncclComm_t)c->nccl, st), "ncclAllGather");
+}
+
+int inccl_rccl_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
+                             hipStream_t st)
+{
+    return nccl_check(ncclAllReduce(send, recv, n, ncclInt32, ncclSum, (ncclComm_t)c->nccl, st), "ncclAllReduce");
+}
+
+int inccl_rccl_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st)
+{
+    return nccl_check(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, (ncclComm_t)c->nccl, st),
+                      "ncclAllReduce(max)");
+}
+
+/* ------------------------------------------------------------------ */
+/* local hub                                                            */
+/* ------------------------------------------------------------------ */
+struct inccl_local_hub {
+    char name[64];
+    int world_size;
+    int refs;
+    pthread_barrier_t bar;
+    const void *send[INCCL_MAX_LOCAL_INPUTS];
+    uint32_t words[INCCL_MAX_LOCAL_INPUTS];
+    struct inccl_local_hub *next;
+};
+
+static pthread_mutex_t g_hub_mu = PTHREAD_MUTEX_INITIALIZER;
+static struct inccl_local_hub *g_hubs;
+
+struct inccl_local_hub *inccl_hub_attach(const char *name, int world_size)
+{
+    if (world_size < 1 || world_size > INCCL_MAX_LOCAL_INPUTS) {
+        inccl_set_error(INCCL_ERR_ARG, "local transport supports 1..%d ranks", INCCL_MAX_LOCAL_INPUTS);
+        return NULL;
+    }
+    pthread_mutex_lock(&g_hub_mu);
+    struct inccl_local_hub *h = g_hubs;
+    while (h && strncmp(h->name, name, sizeof(h->name)) != 0) h = h->next;
+    if (h && h->world_size != world_size) {
+        pthread_mutex_unlock(&g_hub_mu);
+        inccl_set_error(INCCL_ERR_ARG, "hub '%s' exists with world_size %d", name, h->world_size);
+        return NULL;
+    }
+    if (!h) {
+        h = (struct inccl_local_hub *)calloc(1, sizeof(*h));
+        if (!h) {
+            pthread_mutex_unlock(&g_hub_mu);
+            return NULL;
+        }
+        snprintf(h->name, sizeof(h->name), "%s", name);
+        h->world_size = world_size;
+        pthread_barrier_init(&h->bar, NULL, (unsigned)world_size);
+        h->next = g_hubs;
+        g_hubs = h;
+    }
+    h->refs++;
+    pthread_mutex_unlock(&g_hub_mu);
+    return h;
+}
+
+void inccl_hub_detach(struct inccl_local_hub *hub)
+{
+    if (!hub) return;
+    pthread_mutex_lock(&g_hub_mu);
+    if (--hub->refs == 0) {
+        struct inccl_local_hub **pp = &g_hubs;
+        while (*pp && *pp != hub) pp = &(*pp)->next;
+        if (*pp) *pp = hub->next;
+        pthread_barrier_destroy(&hub->bar);
+        free(hub);
+    }
+    pthread_mutex_unlock(&g_hub_mu);
+}
+
+int inccl_local_barrier(struct inccl_communicator *c)
+{
+    pthread_barrier_wait(&c->group->hub->bar);
+    return 0;
+}
+
+/* publish this rank's buffer once its producers on `st` have finished */
+static int hub_publish(struct inccl_communicator *c, const void *p, hipStream_t st)
+{
+    INCCL_HIP(hipStreamSynchronize(st));
+    c->group->hub->send[c->group->rank] = p;
+    pthread_barrier_wait(&c->group->hub->bar);
+    return 0;
+}
+
+static int hub_release(struct inccl_communicator *c, hipStream_t st)
+{
+    hipError_t e = hipStreamSynchronize(st);
+    pthread_barrier_wait(&c->group->hub->bar);   /* nobody reads a peer buffer after this */
+    return e == hipSuccess ? 0 : inccl_hip_check(e, "hipStreamSynchronize");
+}
+
+int inccl_local_reduce_scatter_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t shard,
+                                   hipStream_t st)
+{
+    struct inccl_local_hub *h = c->group->hub;
+    const int W = h->world_size, me = c->group->rank;
+    int rc = hub_publish(c, send, st);
+    if (rc) return rc;
+    const void *srcs[INCCL_MAX_LOCAL_INPUTS];
+    for (int j = 0; j < W; ++j) srcs[j] = (const int32_t *)h->send[j] + (size_t)me * shard;
+    rc = inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_Q32, srcs, W, recv, shard, 0, NULL, W, st);
+    int rc2 = hub_release(c, st);
+    return rc ? inccl_set_error(INCCL_ERR_HIP, "local reduce-scatter kernel failed (%d)", rc) : rc2;
+}
+
+int inccl_local_all_gather_f32(struct inccl_communicator *c, const float *send, float *recv, size_t shard,
+                               hipStream_t st)
+{
+    struct inccl_local_hub *h = c->group->hub;
+    const int W = h->world_size;
+    int rc = hub_publish(c, send, st);
+    if (rc) return rc;
+    for (int j = 0; j < W && rc == 0; ++j) {
+        float *d = recv + (size_t)j * shard;
+        if ((const void *)d == h->send[j]) continue;   /* in-place own shard */
+        hipError_t e = hipMemcpyAsync(d, h->send[j], shard * sizeof(float), hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) rc = inccl_hip_check(e, "hipMemcpyAsync(all-gather)");
+    }
+    int rc2 = hub_release(c, st);
+    return rc ? rc : rc2;
+}
+
+int inccl_local_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
+                              hipStream_t st)
+{
+    struct inccl_local_hub *h = c->group->hub;
+    const int W = h->world_size;
+    /* sum into private scratch first: recv may alias a buffer a peer is still reading */
+    int rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
+    if (rc) return rc;
+    rc = hub_publish(c, send, st);
+    if (rc) return rc;
+    const void *srcs[INCCL_MAX_LOCAL_INPUTS];
+    for (int j = 0; j < W; ++j) srcs[j] = h->send[j];
+    rc = inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_Q32, srcs, W, c->d_q32, n, 0, NULL, W, st);
+    int rc2 = hub_release(c, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "local allreduce kernel failed (%d)", rc);
+    if (rc2) return rc2;
+    INCCL_HIP(hipMemcpyAsync(recv, c->d_q32, n * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    return 0;
+}
+
+int inccl_local_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st)
+{
+    struct inccl_local_hub *h = c->group->hub;
+    const int W = h->world_size, me = c->group->rank;
+    if (n != 1) return inccl_set_error(INCCL_ERR_ARG, "local max-allreduce handles one word");
+    uint32_t v = 0;
+    INCCL_HIP(hipMemcpyAsync(&v, buf, sizeof(v), hipMemcpyDeviceToHost, st));
+    INCCL_HIP(hipStreamSynchronize(st));
+    h->words[me] = v;
+    pthread_barrier_wait(&h->bar);
+    uint32_t m = 0;
+    for (int j = 0; j < W; ++j) m = h->words[j] > m ? h->words[j] : m;
+    pthread_barrier_wait(&h->bar);
+    INCCL_HIP(hipMemcpyAsync(buf, &m, sizeof(m), hipMemcpyHostToDevice, st));
+    INCCL_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* dispatch                                                             */
+/* ------------------------------------------------------------------ */
+static int is_local(const struct inccl_communicator *c) { return c->group->transport == INCCL_TRANSPORT_LOCAL; }
+
+int inccl_tp_reduce_scatter_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t shard,
+                                hipStream_t st)
+{
+    if (is_local(c)) return inccl_local_reduce_scatter_q32(c, send, recv, shard, st);
+    if (!c->nccl) {   /* world 1 without RCCL: the reduce-scatter is a copy */
+        if (send != recv) INCCL_HIP(hipMemcpyAsync(recv, send, shard * 4, hipMemcpyDeviceToDevice, st));
+        return 0;
+    }
+    return inccl_rccl_reduce_scatter_q32(c, send, recv, shard, st);
+}
+
+int inccl_tp_all_gather_f32(struct inccl_communicator *c, const float *send, float *recv, size_t shard,
+                            hipStream_t st)
+{
+    if (is_local(c)) return inccl_local_all_gather_f32(c, send, recv, shard, st);
+    if (!c->nccl) {
+        if (send != recv) INCCL_HIP(hipMemcpyAsync(recv, send, shard * 4, hipMemcpyDeviceToDevice, st));
+        return 0;
+    }
+    return inccl_rccl_all_gather_f32(c, send, recv, shard, st);
+}
+
+int inccl_tp_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
+                           hipStream_t st)
+{
+    if (is_local(c)) return inccl_local_allreduce_q32(c, send, recv, n, st);
+    if (!c->nccl) {
+        if (send != recv) INCCL_HIP(hipMemcpyAsync(recv, send, n * 4, hipMemcpyDeviceToDevice, st));
+        return 0;
+    }
+    return inccl_rccl_allreduce_q32(c, send, recv, n, st);
+}
+
+int inccl_tp_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st)
+{
+    if (is_local(c)) return inccl_local_allreduce_max_u32(c, buf, n, st);
+    if (!c->nccl) return 0;
+    return inccl_rccl_allreduce_max_u32(c, buf, n, st);
+}
+
+int inccl_tp_barrier(struct inccl_communicator *c)
+{
+    if (is_local(c)) return inccl_local_barrier(c);
+    return inccl_boot_barrier(c->group);
+}

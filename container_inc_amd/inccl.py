@@ -1,0 +1,337 @@
+"""Python host mirror of the INCCL interface over ``libinccl_amd.so``.
+
+Reference interface: ``repository/include/api.h:93-101`` (group / communicator /
+``inccl_allreduce_write`` / ``inccl_allreduce_sendrecv``), kept with the same
+names, argument meaning (``len`` in int32 elements, communicator ``size`` in
+bytes, whole-message rule of ``api.c:406``) and error behaviour (``None`` from a
+failed group create, ``api.c:82-98``).  The additive fp32 / device API of
+``include/inccl_amd.h`` is exposed on torch tensors (PyTorch is plumbing here:
+device memory and streams).
+
+Every compute call goes through the HIP library; nothing here computes on the
+CPU.  Shapes and dtypes are validated on the host before any launch.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import numpy as np
+
+from ._lib import IncclError, check, load
+
+KIND_F32, KIND_Q32, KIND_Q32BE = 0, 1, 2
+SCALE_MIN, SCALE_MAX, SCALE_AUTO = -64, 64, 0x7FFFFFFF
+MAX_LOCAL_INPUTS = 8
+PAYLOAD_LEN = 1024           # util.h:85
+MESSAGE_SIZE = 4 * PAYLOAD_LEN   # api.h:39
+PAYLOAD_COUNT = MESSAGE_SIZE // 4  # api.h:40
+WINDOW_SIZE = 8192           # api.h:38
+MASTER_PORT = 52223          # parameter.h:1
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _dev_ptr(t, dtype, name: str, numel: int | None = None) -> int:
+    torch = _torch()
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor, got {type(t)!r}")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name}: tensor must live on the GPU (got {t.device})")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+    if numel is not None and t.numel() < numel:
+        raise ValueError(f"{name}: needs {numel} elements, has {t.numel()}")
+    return t.data_ptr()
+
+
+def _stream_handle(stream) -> int | None:
+    torch = _torch()
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def _ptr_array(ptrs: Sequence[int]):
+    return (ctypes.c_void_p * len(ptrs))(*ptrs)
+
+
+def _check_scale(k: int) -> int:
+    k = int(k)
+    if k != SCALE_AUTO and not (SCALE_MIN <= k <= SCALE_MAX):
+        raise ValueError(f"scale exponent {k} outside [{SCALE_MIN}, {SCALE_MAX}]")
+    return k
+
+
+_TORCH_KIND = {KIND_F32: "float32", KIND_Q32: "int32", KIND_Q32BE: "int32"}
+
+
+def stream_op(in_kind: int, out_kind: int, srcs, out=None, scale_exp: int = 0, n: int | None = None,
+              amax_word=None, scale_R: int = 0, stream=None):
+    """Generic ``out = OUT(sum_r IN(srcs[r]))`` (see inccl_kernels.hip)."""
+    torch = _torch()
+    if len(srcs) < 1 or len(srcs) > MAX_LOCAL_INPUTS:
+        raise ValueError(f"1..{MAX_LOCAL_INPUTS} inputs per launch, got {len(srcs)}")
+    in_dt = getattr(torch, _TORCH_KIND[in_kind])
+    out_dt = getattr(torch, _TORCH_KIND[out_kind])
+    if n is None:
+        n = srcs[0].numel()
+    ptrs = [_dev_ptr(s, in_dt, f"srcs[{i}]", n) for i, s in enumerate(srcs)]
+    if out is None:
+        out = torch.empty(n, dtype=out_dt, device=srcs[0].device)
+    optr = _dev_ptr(out, out_dt, "out", n)
+    aptr = None
+    if amax_word is not None:
+        aptr = _dev_ptr(amax_word, torch.int32, "amax_word", 1)
+    else:
+        scale_exp = _check_scale(scale_exp)
+    rc = load().inccl_stream_op(in_kind, out_kind, _ptr_array(ptrs), len(ptrs), optr, n, int(scale_exp), aptr,
+                                int(scale_R), _stream_handle(stream))
+    check(rc, "inccl_stream_op")
+    return out
+
+
+def quantise(x, scale_exp: int, wire_be: bool = False, out=None, stream=None):
+    """fp32 -> int32 fixed point (+ optional htonl, api.c:300-302)."""
+    return stream_op(KIND_F32, KIND_Q32BE if wire_be else KIND_Q32, [x], out, scale_exp, stream=stream)
+
+
+def dequantise(q, scale_exp: int, wire_be: bool = False, out=None, stream=None):
+    """int32 (optionally big-endian, api.c:428-430) -> fp32."""
+    return stream_op(KIND_Q32BE if wire_be else KIND_Q32, KIND_F32, [q], out, scale_exp, stream=stream)
+
+
+def reduce_f32(srcs, scale_exp: int, out=None, stream=None):
+    """Fused single-GPU bucket reduce dequant(sum_r quant(srcs[r]))."""
+    return stream_op(KIND_F32, KIND_F32, list(srcs), out, scale_exp, scale_R=len(srcs), stream=stream)
+
+
+def quant_sum(srcs, scale_exp: int, wire_be: bool = False, out=None, stream=None):
+    return stream_op(KIND_F32, KIND_Q32BE if wire_be else KIND_Q32, list(srcs), out, scale_exp, stream=stream)
+
+
+def sum_q32(srcs, in_be: bool = False, out_be: bool = False, out=None, stream=None):
+    """The switch aggregate (non_termination_switch.c:361-363) on the GPU."""
+    return stream_op(KIND_Q32BE if in_be else KIND_Q32, KIND_Q32BE if out_be else KIND_Q32, list(srcs), out, 0,
+                     stream=stream)
+
+
+def sum_dequant(srcs, scale_exp: int, in_be: bool = False, out=None, stream=None):
+    return stream_op(KIND_Q32BE if in_be else KIND_Q32, KIND_F32, list(srcs), out, scale_exp, stream=stream)
+
+
+def absmax_word(srcs, word=None, stream=None):
+    """Device absmax over R buckets; returns the int32 word tensor holding float bits."""
+    torch = _torch()
+    n = srcs[0].numel()
+    ptrs = [_dev_ptr(s, torch.float32, f"srcs[{i}]", n) for i, s in enumerate(srcs)]
+    if word is None:
+        word = torch.zeros(4, dtype=torch.int32, device=srcs[0].device)
+    rc = load().inccl_absmax_f32(_ptr_array(ptrs), len(ptrs), n, _dev_ptr(word, torch.int32, "word", 1), 1,
+                                 _stream_handle(stream))
+    check(rc, "inccl_absmax_f32")
+    return word
+
+
+def absmax(srcs, stream=None) -> float:
+    w = absmax_word(srcs, stream=stream)
+    bits = int(w[0].item()) & 0xFFFFFFFF
+    return float(np.array([bits], np.uint32).view(np.float32)[0])
+
+
+def reduce_f32_auto(srcs, out=None, word=None, stream=None):
+    torch = _torch()
+    n = srcs[0].numel()
+    ptrs = [_dev_ptr(s, torch.float32, f"srcs[{i}]", n) for i, s in enumerate(srcs)]
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=srcs[0].device)
+    if word is None:
+        word = torch.zeros(4, dtype=torch.int32, device=srcs[0].device)
+    rc = load().inccl_reduce_f32_auto(_ptr_array(ptrs), len(ptrs), _dev_ptr(out, torch.float32, "out", n), n,
+                                      _dev_ptr(word, torch.int32, "word", 1), _stream_handle(stream))
+    check(rc, "inccl_reduce_f32_auto")
+    return out
+
+
+def checksum_q32(q, index_base: int = 0, stream=None) -> int:
+    torch = _torch()
+    word = torch.zeros(4, dtype=torch.int32, device=q.device)
+    rc = load().inccl_checksum_q32(_dev_ptr(q, torch.int32, "q"), q.numel(), int(index_base),
+                                   _dev_ptr(word, torch.int32, "word", 1), 1, _stream_handle(stream))
+    check(rc, "inccl_checksum_q32")
+    return int(word[0].item()) & 0xFFFFFFFF
+
+
+def choose_scale(amax: float, R_total: int) -> int:
+    return int(load().inccl_choose_scale(ctypes.c_float(amax), int(R_total)))
+
+
+def set_tuning(grid_cap: int = 0, nt_loads: bool = True) -> None:
+    load().inccl_set_tuning(int(grid_cap), 1 if nt_loads else 0)
+
+
+def version() -> str:
+    return load().inccl_version().decode()
+
+
+# ---------------------------------------------------------------------------
+# groups / communicators (reference api.h:42-101)
+# ---------------------------------------------------------------------------
+class Group:
+    def __init__(self, handle: int):
+        if not handle:
+            raise IncclError(load().inccl_last_error().decode(errors="replace") or "group create failed")
+        self.handle = handle
+
+    @property
+    def rank(self) -> int:
+        return load().inccl_group_rank(self.handle)
+
+    @property
+    def world_size(self) -> int:
+        return load().inccl_group_size(self.handle)
+
+    @property
+    def device(self) -> int:
+        return load().inccl_group_device(self.handle)
+
+    @property
+    def transport(self) -> str:
+        return load().inccl_group_transport(self.handle).decode()
+
+    def destroy(self) -> int:
+        rc = 1
+        if self.handle:
+            rc = load().inccl_group_destroy(self.handle)
+            self.handle = None
+        return rc
+
+
+class Communicator:
+    def __init__(self, group: Group, handle: int):
+        if not handle:
+            raise IncclError(load().inccl_last_error().decode(errors="replace") or "communicator create failed")
+        self.group = group
+        self.handle = handle
+
+    @property
+    def stream(self) -> int:
+        return load().inccl_comm_stream(self.handle)
+
+    def barrier(self) -> None:
+        check(load().inccl_comm_barrier(self.handle), "inccl_comm_barrier")
+
+    # -- reference collectives on host int32 arrays (api.c:330-452) --
+    def allreduce_write(self, src: np.ndarray, length: int, dst: np.ndarray) -> None:
+        _host_int32_call(load().inccl_allreduce_write, self.handle, src, length, dst)
+
+    def allreduce_sendrecv(self, src: np.ndarray, length: int, dst: np.ndarray) -> None:
+        _host_int32_call(load().inccl_allreduce_sendrecv, self.handle, src, length, dst)
+
+    # -- additive device API --
+    def allreduce_f32(self, srcs, out=None, scale_exp: int = 25, chunks: int = 1, stream=None):
+        torch = _torch()
+        srcs = list(srcs)
+        if not 1 <= len(srcs) <= MAX_LOCAL_INPUTS:
+            raise ValueError(f"1..{MAX_LOCAL_INPUTS} local buckets, got {len(srcs)}")
+        n = srcs[0].numel()
+        ptrs = [_dev_ptr(s, torch.float32, f"srcs[{i}]", n) for i, s in enumerate(srcs)]
+        if out is None:
+            out = torch.empty(n, dtype=torch.float32, device=srcs[0].device)
+        optr = _dev_ptr(out, torch.float32, "out", n)
+        rc = load().inccl_allreduce_f32_pipelined(self.handle, _ptr_array(ptrs), len(ptrs), optr, n,
+                                                  _check_scale(scale_exp), int(chunks), _stream_handle(stream))
+        check(rc, "inccl_allreduce_f32")
+        return out
+
+    def allreduce_q32(self, src, out=None, stream=None):
+        torch = _torch()
+        n = src.numel()
+        if out is None:
+            out = torch.empty_like(src)
+        rc = load().inccl_allreduce_q32(self.handle, _dev_ptr(src, torch.int32, "src"),
+                                        _dev_ptr(out, torch.int32, "out", n), n, _stream_handle(stream))
+        check(rc, "inccl_allreduce_q32")
+        return out
+
+    def allreduce_f32_host(self, src, dst, scale_exp: int = 25, bucket_bytes: int = 64 << 20) -> None:
+        """Host-memory buckets (numpy arrays or pinned CPU tensors)."""
+        sp, sn = _host_ptr(src, np.float32, "src")
+        dp, dn = _host_ptr(dst, np.float32, "dst")
+        if dn < sn:
+            raise ValueError("dst smaller than src")
+        rc = load().inccl_allreduce_f32_host(self.handle, sp, dp, sn, _check_scale(scale_exp), int(bucket_bytes))
+        check(rc, "inccl_allreduce_f32_host")
+
+    def destroy(self) -> int:
+        rc = 0
+        if self.handle:
+            rc = load().inccl_communicator_destroy(self.handle)
+            self.handle = None
+        return rc
+
+
+def _host_ptr(a, np_dtype, name):
+    torch = None
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover
+        pass
+    if torch is not None and isinstance(a, torch.Tensor):
+        if a.device.type != "cpu" or not a.is_contiguous() or a.dtype != getattr(torch, np.dtype(np_dtype).name):
+            raise ValueError(f"{name}: expected a contiguous CPU {np.dtype(np_dtype).name} tensor")
+        return a.data_ptr(), a.numel()
+    if not isinstance(a, np.ndarray) or a.dtype != np_dtype or not a.flags["C_CONTIGUOUS"]:
+        raise ValueError(f"{name}: expected a contiguous numpy {np.dtype(np_dtype).name} array")
+    return a.ctypes.data, a.size
+
+
+def _host_int32_call(fn, handle, src, length, dst):
+    sp, sn = _host_ptr(src, np.int32, "src")
+    dp, dn = _host_ptr(dst, np.int32, "dst")
+    length = int(length)
+    n = (length // PAYLOAD_COUNT) * PAYLOAD_COUNT   # api.c:406 whole messages
+    if length < 0 or sn < n or dn < n:
+        raise ValueError(f"len={length} exceeds src ({sn}) or dst ({dn})")
+    fn(handle, sp, ctypes.c_uint32(length), dp)
+
+
+# -- reference-named entry points (api.h:93-101) --
+def inccl_group_create(world_size: int, rank: int, master_ip: str = "127.0.0.1", port: int = 0,
+                       device: int = -1) -> Group | None:
+    """NULL (None) on failure, like api.c:82-98."""
+    h = load().inccl_group_create_ex(int(world_size), int(rank), master_ip.encode(), int(port), int(device))
+    return Group(h) if h else None
+
+
+def inccl_group_create_local(world_size: int, rank: int, hub: str = "default", device: int = -1) -> Group | None:
+    h = load().inccl_group_create_local(int(world_size), int(rank), hub.encode(), int(device))
+    return Group(h) if h else None
+
+
+def inccl_group_destroy(group: Group) -> int:
+    return group.destroy()
+
+
+def inccl_communicator_create(group: Group, size: int) -> Communicator | None:
+    h = load().inccl_communicator_create(group.handle, ctypes.c_uint32(int(size)))
+    return Communicator(group, h) if h else None
+
+
+def inccl_communicator_destroy(comm: Communicator) -> int:
+    return comm.destroy()
+
+
+def inccl_allreduce_write(comm: Communicator, src_data: np.ndarray, length: int, dst_data: np.ndarray) -> None:
+    comm.allreduce_write(src_data, length, dst_data)
+
+
+def inccl_allreduce_sendrecv(comm: Communicator, src_data: np.ndarray, length: int, dst_data: np.ndarray) -> None:
+    comm.allreduce_sendrecv(src_data, length, dst_data)

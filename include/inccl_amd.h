@@ -1,0 +1,143 @@
+/*
+ * inccl_amd.h -- additive MI355X API of libinccl_amd.so (fp32 gradient buckets,
+ * device pointers, explicit streams).  None of this exists in the reference;
+ * each entry point names the reference code whose arithmetic it carries.
+ *
+ * Conventions
+ *   - Pointers named *_dev are device (HBM) pointers; `srcs` arguments are HOST
+ *     arrays holding R device pointers.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ *     Calls are stream-ordered and do not synchronise unless stated.
+ *   - Return 0 on success; a negative INCCL_ERR_* code, or a positive
+ *     hipError_t / ncclResult_t value, on failure.  inccl_last_error() has text.
+ *   - 16-byte-aligned buffers take the dwordx4 streaming path; anything else
+ *     falls back to an element-granular kernel (still on the GPU).
+ *
+ * Numerics (the spec the CPU oracle restates, oracle/inccl_oracle.c)
+ *   quantise    q = sat_int32(round_half_even(x * 2^k)); NaN -> 0; +-Inf saturate
+ *   reduce      s = sum_r q_r  mod 2^32                  (non_termination_switch.c:361-363)
+ *   dequantise  y = (float)s * 2^-k                       ((float) rounds to nearest even)
+ *   k in [INCCL_SCALE_MIN, INCCL_SCALE_MAX]; INCCL_SCALE_AUTO picks the largest k
+ *   with R_total * max|x| * 2^k <= 2^30 from a device-side absmax reduction.
+ */
+#ifndef INCCL_AMD_H
+#define INCCL_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "api.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define INCCL_MAX_LOCAL_INPUTS 8        /* R per kernel launch */
+#define INCCL_SCALE_MIN (-64)
+#define INCCL_SCALE_MAX 64
+#define INCCL_SCALE_AUTO 0x7fffffff
+
+#define INCCL_OK 0
+#define INCCL_ERR_ARG (-1)
+#define INCCL_ERR_HIP (-2)
+#define INCCL_ERR_NCCL (-3)
+#define INCCL_ERR_SYS (-4)
+#define INCCL_ERR_STATE (-5)
+#define INCCL_ERR_NOMEM (-6)
+
+/* element kinds of the generic streaming kernel */
+#define INCCL_KIND_F32 0     /* fp32 gradient                                  */
+#define INCCL_KIND_Q32 1     /* int32, host byte order                         */
+#define INCCL_KIND_Q32BE 2   /* int32, big-endian wire word (api.c:301, util.c:404) */
+
+const char *inccl_last_error(void);
+const char *inccl_version(void);
+
+/* ---------- stateless device kernels (one GPU, stream-ordered) ---------- */
+
+/* fp32 -> int32 fixed point (new front stage).  wire_be != 0 also applies the
+ * reference's htonl encode (api.c:300-302) in the same pass. */
+int inccl_quantise_f32(const float *x_dev, int32_t *q_dev, size_t n, int scale_exp, int wire_be, void *stream);
+/* int32 -> fp32 (new back stage).  wire_be != 0 first applies ntohl (api.c:428-430). */
+int inccl_dequantise_q32(const int32_t *q_dev, float *y_dev, size_t n, int scale_exp, int wire_be, void *stream);
+/* Fused single-GPU bucket reduce: dst = dequant(sum_r quant(srcs[r])), R <= 8.
+ * One HBM pass: (R + 1) * 4 * n bytes.  dst may alias srcs[0]. */
+int inccl_reduce_f32(const float *const *srcs_dev, int R, float *dst_dev, size_t n, int scale_exp, void *stream);
+/* As above with INCCL_SCALE_AUTO semantics; amax_word_dev is a 4-byte device
+ * scratch word (zeroed and written by the call). */
+int inccl_reduce_f32_auto(const float *const *srcs_dev, int R, float *dst_dev, size_t n, uint32_t *amax_word_dev,
+                          void *stream);
+/* Local quantise + sum to int32 (first stage of the multi-GPU path). */
+int inccl_quant_sum_f32(const float *const *srcs_dev, int R, int32_t *dst_dev, size_t n, int scale_exp, int wire_be,
+                        void *stream);
+/* Switch aggregate (non_termination_switch.c:361-363, util.c:403-405):
+ * dst = sum_r srcs[r] mod 2^32, optional big-endian decode of the inputs
+ * (in_be) and encode of the output (out_be). */
+int inccl_sum_q32(const int32_t *const *srcs_dev, int R, int32_t *dst_dev, size_t n, int in_be, int out_be,
+                  void *stream);
+/* Sum + dequantise: dst = dequant(sum_r srcs[r]) (reduce-scatter variant B epilogue). */
+int inccl_sum_dequant_q32(const int32_t *const *srcs_dev, int R, float *dst_dev, size_t n, int scale_exp, int in_be,
+                          void *stream);
+/* Generic form of all of the above (kinds INCCL_KIND_*).  amax_bits_dev != NULL
+ * derives k from that device word and scale_R contributors instead of scale_exp. */
+int inccl_stream_op(int in_kind, int out_kind, const void *const *srcs_dev, int R, void *dst_dev, size_t n,
+                    int scale_exp, const uint32_t *amax_bits_dev, int scale_R, void *stream);
+/* max |x| over R buckets into *amax_bits_dev (float bits; NaN ignored).  The word
+ * is zeroed first when zero_first != 0, else max-accumulated. */
+int inccl_absmax_f32(const float *const *srcs_dev, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
+                     void *stream);
+/* Position-weighted linear checksum sum_i (2(base+i)+1)*q[i] mod 2^32 into *out_dev. */
+int inccl_checksum_q32(const int32_t *q_dev, size_t n, uint64_t index_base, uint32_t *out_dev, int zero_first,
+                       void *stream);
+/* Host helper: the scale rule of INCCL_SCALE_AUTO. */
+int inccl_choose_scale(float absmax, int R_total);
+/* Tuning knobs of the streaming kernel (grid cap in workgroups, 0 = default;
+ * nontemporal loads on/off).  For benchmarks and sweeps only. */
+void inccl_set_tuning(int grid_cap, int nt_loads);
+
+/* ---------- groups and communicators ---------- */
+
+/* Like inccl_group_create with an explicit rendezvous port (0 = MASTER_PORT or
+ * $INCCL_MASTER_PORT) and HIP device (-1 = $INCCL_DEVICE, $LOCAL_RANK, or rank
+ * modulo the device count). */
+struct inccl_group *inccl_group_create_ex(int world_size, int rank, const char *master_ip, int port, int device);
+/* In-process transport: `world_size` ranks are threads of this process sharing
+ * one GPU.  Every rank thread calls this with the same `hub_name`; the GPU plays
+ * the aggregation switch (its sum kernel reduces the ranks' buffers). */
+struct inccl_group *inccl_group_create_local(int world_size, int rank, const char *hub_name, int device);
+int inccl_group_rank(const struct inccl_group *group);
+int inccl_group_size(const struct inccl_group *group);
+int inccl_group_device(const struct inccl_group *group);
+/* "rccl" or "local" */
+const char *inccl_group_transport(const struct inccl_group *group);
+/* The communicator's own HIP stream (void* hipStream_t). */
+void *inccl_comm_stream(struct inccl_communicator *comm);
+int inccl_comm_barrier(struct inccl_communicator *comm);
+
+/* Device-resident fp32 allreduce of R local buckets per rank:
+ *   dst = dequant( sum over ranks, sum over r<R  quant(srcs[r]) )
+ * world == 1: one fused kernel.  world > 1: quant+local sum -> reduce-scatter
+ * (int32, sum) -> dequantise own shard -> all-gather (fp32).  `scale_exp` may be
+ * INCCL_SCALE_AUTO (adds an absmax pass and a 4-byte max-allreduce).
+ * stream NULL = the communicator's stream.  dst may alias srcs[0]. */
+int inccl_allreduce_f32(struct inccl_communicator *comm, const float *const *srcs_dev, int R, float *dst_dev,
+                        size_t n, int scale_exp, void *stream);
+/* Same with the bucket split into `chunks` pieces pipelined over two streams
+ * (compute of chunk c+1 overlaps the collectives of chunk c).  chunks <= 1 is
+ * inccl_allreduce_f32. */
+int inccl_allreduce_f32_pipelined(struct inccl_communicator *comm, const float *const *srcs_dev, int R,
+                                  float *dst_dev, size_t n, int scale_exp, int chunks, void *stream);
+/* Device int32 allreduce (sum, wrap): the arithmetic of inccl_allreduce_write
+ * without the host copies. */
+int inccl_allreduce_q32(struct inccl_communicator *comm, const int32_t *src_dev, int32_t *dst_dev, size_t n,
+                        void *stream);
+/* Host-memory fp32 allreduce (BASELINE config 3): src/dst in host memory,
+ * pipelined H2D / reduce / D2H over `bucket_bytes` buckets on three streams.
+ * Synchronous. */
+int inccl_allreduce_f32_host(struct inccl_communicator *comm, const float *src_host, float *dst_host, size_t n,
+                             int scale_exp, size_t bucket_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* INCCL_AMD_H */

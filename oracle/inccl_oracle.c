@@ -1,0 +1,415 @@
+/*
+ * inccl_oracle.c -- TEST INFRASTRUCTURE ONLY (see inccl_oracle.h).
+ *
+ * Plain-C restatement of the INCCL hot path.  Scalar on purpose: it mirrors the
+ * reference's per-element loops so it can also serve as the single-core CPU
+ * baseline ("port") in bench.py.  Compiled with the reference's flags
+ * (-O3 -march=native -funroll-loops, repository/CMakeLists.txt:30).
+ */
+#include "inccl_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ */
+/* byte order                                                           */
+/* ------------------------------------------------------------------ */
+static inline uint32_t bswap32(uint32_t v)
+{
+    return (v >> 24) | ((v >> 8) & 0x0000FF00u) | ((v << 8) & 0x00FF0000u) | (v << 24);
+}
+
+/* htonl on a little-endian host (x86-64 and the MI355X hosts are LE). */
+static inline uint32_t to_be(uint32_t v) { return bswap32(v); }
+
+void orc_encode_be32(const int32_t *src, uint32_t *wire, size_t n)
+{
+    /* api.c:300-302 */
+    for (size_t i = 0; i < n; ++i) wire[i] = to_be((uint32_t)src[i]);
+}
+
+void orc_decode_be32(const uint32_t *wire, int32_t *dst, size_t n)
+{
+    /* api.c:428-430 */
+    for (size_t i = 0; i < n; ++i) dst[i] = (int32_t)to_be(wire[i]);
+}
+
+/* ------------------------------------------------------------------ */
+/* quantise / dequantise (engine spec; no reference counterpart)       */
+/* ------------------------------------------------------------------ */
+static inline float pow2f(int k)
+{
+    /* exact 2^k for k in [-126, 127] built from the exponent field */
+    union { uint32_t u; float f; } c;
+    c.u = (uint32_t)(k + 127) << 23;
+    return c.f;
+}
+
+int32_t orc_quantise_one(float x, int k)
+{
+    if (x != x) return 0;                       /* NaN -> 0 */
+    /* For |k| <= 64 the product is exact whenever it is a normal number; a
+     * subnormal product has magnitude < 2^-126 and rounds to 0 below. */
+    float y = x * pow2f(k);
+    if (y >= 2147483648.0f) return INT32_MAX;   /* saturate (also +Inf) */
+    if (y <= -2147483648.0f) return INT32_MIN;  /* saturate (also -Inf) */
+    return (int32_t)nearbyintf(y);              /* round half to even */
+}
+
+void orc_quantise_f32(const float *x, int32_t *q, size_t n, int k)
+{
+    for (size_t i = 0; i < n; ++i) q[i] = orc_quantise_one(x[i], k);
+}
+
+float orc_dequantise_one(int32_t q, int k)
+{
+    return (float)q * pow2f(-k);
+}
+
+void orc_dequantise_q32(const int32_t *q, float *f, size_t n, int k)
+{
+    const float s = pow2f(-k);
+    for (size_t i = 0; i < n; ++i) f[i] = (float)q[i] * s;
+}
+
+/* ------------------------------------------------------------------ */
+/* reduction                                                            */
+/* ------------------------------------------------------------------ */
+void orc_sum_q32(const int32_t *const *srcs, int R, int32_t *dst, size_t n)
+{
+    /* nts.c:361-363, accumulated in uint32 (exact mod 2^32 wrap) */
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t acc = 0;
+        for (int r = 0; r < R; ++r) acc += (uint32_t)srcs[r][i];
+        dst[i] = (int32_t)acc;
+    }
+}
+
+void orc_quant_sum(const float *const *srcs, int R, int32_t *dst, size_t n, int k)
+{
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t acc = 0;
+        for (int r = 0; r < R; ++r) acc += (uint32_t)orc_quantise_one(srcs[r][i], k);
+        dst[i] = (int32_t)acc;
+    }
+}
+
+void orc_reduce_f32(const float *const *srcs, int R, float *dst, size_t n, int k)
+{
+    const float s = pow2f(-k);
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t acc = 0;
+        for (int r = 0; r < R; ++r) acc += (uint32_t)orc_quantise_one(srcs[r][i], k);
+        dst[i] = (float)(int32_t)acc * s;
+    }
+}
+
+float orc_absmax_f32(const float *const *srcs, int R, size_t n)
+{
+    float m = 0.0f;
+    for (int r = 0; r < R; ++r)
+        for (size_t i = 0; i < n; ++i) {
+            float a = fabsf(srcs[r][i]);
+            if (a > m) m = a;   /* NaN compares false: ignored */
+        }
+    return m;
+}
+
+int orc_choose_scale(float absmax, int R)
+{
+    if (!(absmax > 0.0f)) return ORC_SCALE_MAX;
+    if (isinf(absmax)) return ORC_SCALE_MIN;
+    double t = (double)absmax * (double)R;   /* exact: 24-bit mantissa x small int */
+    int e;
+    double m = frexp(t, &e);                 /* t = m * 2^e, m in [0.5, 1) */
+    int k = (m == 0.5) ? (31 - e) : (30 - e);
+    if (k < ORC_SCALE_MIN) k = ORC_SCALE_MIN;
+    if (k > ORC_SCALE_MAX) k = ORC_SCALE_MAX;
+    return k;
+}
+
+uint32_t orc_checksum_q32(const int32_t *q, size_t n, uint64_t index_base)
+{
+    uint32_t cs = 0;
+    for (size_t i = 0; i < n; ++i)
+        cs += (uint32_t)(2u * (uint32_t)(index_base + i) + 1u) * (uint32_t)q[i];
+    return cs;
+}
+
+/* ------------------------------------------------------------------ */
+/* root-switch aggregation (nts.c:231-250, :303-501)                    */
+/* ------------------------------------------------------------------ */
+#define SLOT(psn) ((psn) % ORC_SW_SLOTS)          /* nts.c:25 Idx() */
+
+void orc_switch_init(orc_switch *sw, int fan_in)
+{
+    memset(sw, 0, sizeof(*sw));
+    sw->fan_in = fan_in;
+}
+
+static void sw_clear(orc_switch *sw, uint32_t psn)
+{
+    /* nts.c:235-242 clear_state_data */
+    const int s = SLOT(psn);
+    sw->arrival_state[s] = 0;
+    sw->degree[s] = 0;
+    memset(sw->aggregator[s], 0, sizeof(sw->aggregator[s]));
+}
+
+static inline int sw_all_fan_in(const orc_switch *sw, int s)
+{
+    const uint32_t mask = 0xffffffffu >> (32 - sw->fan_in);   /* nts.c:29 */
+    return (sw->arrival_state[s] & mask) == mask;              /* nts.c:244-246 */
+}
+
+int orc_switch_ingress(orc_switch *sw, int port, uint32_t psn,
+                       const uint32_t *payload_be, uint32_t *egress_be)
+{
+    const int s = SLOT(psn);
+    const uint32_t port_bit = 1u << port;
+    const uint32_t result_bit = 1u << sw->fan_in;              /* bit FAN_IN (nts.c:366) */
+    sw->degree[s] += 1;                                        /* nts.c:351 */
+
+    if (sw->arrival_state[s] & port_bit) {                     /* nts.c:353 retransmit */
+        if (sw->arrival_state[s] & result_bit) {               /* nts.c:354-356 replay */
+            for (int i = 0; i < ORC_LANES; ++i) egress_be[i] = to_be((uint32_t)sw->aggregator[s][i]);
+            sw->replays++;
+            return ORC_SW_REPLAY;
+        }
+        return ORC_SW_DROPPED;
+    }
+    /* first transmission: nts.c:359-363 */
+    sw->arrival_state[s] |= port_bit;
+    {
+        uint32_t *acc = (uint32_t *)sw->aggregator[s];
+        for (int i = 0; i < ORC_LANES; ++i) acc[i] += to_be(payload_be[i]);
+    }
+    sw->adds++;
+    if (sw_all_fan_in(sw, s)) {                                /* nts.c:365-372 */
+        sw->arrival_state[s] |= result_bit;
+        sw_clear(sw, psn + ORC_SW_WINDOW);                     /* nts.c:367 */
+        /* egress re-encode (util.c:403-405) */
+        for (int i = 0; i < ORC_LANES; ++i) egress_be[i] = to_be((uint32_t)sw->aggregator[s][i]);
+        return ORC_SW_BROADCAST;
+    }
+    return ORC_SW_ABSORBED;
+}
+
+/* ------------------------------------------------------------------ */
+/* CRC32 / ICRC / framing (util.c:106-195, :250-286, :331-442)          */
+/* ------------------------------------------------------------------ */
+static uint32_t crc_tab[8][256];
+static int crc_ready;
+
+static void crc_init(void)
+{
+    /* util.c:141-159: reflected table for poly 0xEDB88320, then the seven
+     * derived slice-by-8 tables */
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int j = 0; j < 8; ++j) c = (c >> 1) ^ ((c & 1u) ? 0xEDB88320u : 0u);
+        crc_tab[0][i] = c;
+    }
+    for (int t = 1; t < 8; ++t)
+        for (int i = 0; i < 256; ++i)
+            crc_tab[t][i] = (crc_tab[t - 1][i] >> 8) ^ crc_tab[0][crc_tab[t - 1][i] & 0xFFu];
+    crc_ready = 1;
+}
+
+uint32_t orc_crc32(const void *data, size_t len)
+{
+    if (!crc_ready) crc_init();
+    const uint8_t *p = (const uint8_t *)data;
+    uint32_t c = 0xFFFFFFFFu;
+    /* slice-by-8 main loop (util.c:165-187) */
+    while (len >= 8) {
+        uint32_t lo = ((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24)) ^ c;
+        c = crc_tab[7][lo & 0xFF] ^ crc_tab[6][(lo >> 8) & 0xFF] ^ crc_tab[5][(lo >> 16) & 0xFF] ^
+            crc_tab[4][lo >> 24] ^ crc_tab[3][p[4]] ^ crc_tab[2][p[5]] ^ crc_tab[1][p[6]] ^
+            crc_tab[0][p[7]];
+        p += 8;
+        len -= 8;
+    }
+    while (len--) c = (c >> 8) ^ crc_tab[0][(c ^ *p++) & 0xFFu];   /* util.c:190-192 */
+    return c ^ 0xFFFFFFFFu;
+}
+
+uint32_t orc_icrc(const uint8_t *frame)
+{
+    /* util.c:250-286 */
+    const uint8_t *ip = frame + ORC_ETH_HDR;
+    const int len = (int)(((uint32_t)ip[2] << 8) | ip[3]) - ORC_ICRC_LEN;  /* IP total length - ICRC */
+    uint8_t buf[8 + 4096];
+    if (len < 0 || len > 4096) return 0;
+    memset(buf, 0xFF, 8);
+    memcpy(buf + 8, ip, (size_t)len);
+    uint8_t *mip = buf + 8;
+    mip[1] = 0xFF;                                   /* tos        (util.c:266) */
+    mip[8] = 0xFF;                                   /* ttl        (util.c:267) */
+    mip[10] = 0xFF; mip[11] = 0xFF;                  /* ip csum    (util.c:268) */
+    uint8_t *udp = mip + ORC_IP_HDR;
+    udp[6] = 0xFF; udp[7] = 0xFF;                    /* udp csum   (util.c:269) */
+    uint8_t *bth = udp + ORC_UDP_HDR;
+    bth[4] = 0xFF;                                   /* BTH resv8a (util.c:270) */
+    return orc_crc32(buf, (size_t)len + 8);
+}
+
+uint16_t orc_ipv4_checksum(const uint8_t *ip_hdr)
+{
+    /* util.c:106-127, checksum field treated as 0; result in network order bytes */
+    const int ihl = (ip_hdr[0] & 0x0F) * 4;
+    uint32_t sum = 0;
+    for (int i = 0; i < ihl; i += 2) {
+        if (i == 10) continue;
+        sum += ((uint32_t)ip_hdr[i] << 8) | ip_hdr[i + 1];
+    }
+    while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
+    return (uint16_t)~sum;   /* host-order value; caller stores it big-endian */
+}
+
+static inline void put16(uint8_t *p, uint16_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+static inline void put32(uint8_t *p, uint32_t v)
+{
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+
+size_t orc_build_data_frame(uint8_t *frame, const orc_frame_hdr *h, const int32_t *payload_host,
+                            int n_words, int with_reth, const uint8_t *reth16)
+{
+    const int data_len = n_words * 4;
+    size_t total = ORC_ETH_HDR + ORC_IP_HDR + ORC_UDP_HDR + ORC_BTH_HDR + (size_t)data_len + ORC_ICRC_LEN;
+    if (with_reth) total += ORC_RETH_HDR;                               /* util.c:341-345 */
+    uint8_t *eth = frame;
+    memcpy(eth, h->dst_mac, 6);                                         /* util.c:349-351 */
+    memcpy(eth + 6, h->src_mac, 6);
+    put16(eth + 12, 0x0800);
+    uint8_t *ip = frame + ORC_ETH_HDR;                                  /* util.c:354-364 */
+    ip[0] = 0x45; ip[1] = 0x00;
+    put16(ip + 2, (uint16_t)(total - ORC_ETH_HDR));
+    ip[4] = 0x11; ip[5] = 0x11;
+    put16(ip + 6, 0x4000);
+    ip[8] = 0x40; ip[9] = 0x11;
+    memcpy(ip + 12, &h->src_ip, 4);
+    memcpy(ip + 16, &h->dst_ip, 4);
+    ip[10] = 0; ip[11] = 0;
+    put16(ip + 10, orc_ipv4_checksum(ip));
+    uint8_t *udp = ip + ORC_IP_HDR;                                     /* util.c:367-372 */
+    put16(udp + 0, h->src_port);
+    put16(udp + 2, h->dst_port);
+    put16(udp + 4, (uint16_t)(total - ORC_ETH_HDR - ORC_IP_HDR));
+    udp[6] = 0; udp[7] = 0;
+    uint8_t *bth = udp + ORC_UDP_HDR;                                   /* util.c:376-388 */
+    bth[0] = h->opcode; bth[1] = 0x00; bth[2] = 0xFF; bth[3] = 0xFF;
+    put32(bth + 4, h->qp & 0x00FFFFFFu);
+    put32(bth + 8, h->psn | 0x80000000u);
+    uint8_t *d = bth + ORC_BTH_HDR;
+    if (with_reth) {                                                    /* util.c:409-417 */
+        if (reth16) memcpy(d, reth16, ORC_RETH_HDR); else memset(d, 0, ORC_RETH_HDR);
+        d += ORC_RETH_HDR;
+    }
+    for (int i = 0; i < n_words; ++i) put32(d + 4 * i, (uint32_t)payload_host[i]);   /* util.c:403-405 */
+    const uint32_t icrc = orc_icrc(frame);                              /* util.c:425-426 */
+    memcpy(frame + total - ORC_ICRC_LEN, &icrc, 4);                     /* stored host order */
+    return total;
+}
+
+/* ------------------------------------------------------------------ */
+/* loopback: api.c:293-327 + :403-452 against nts.c pipeline()          */
+/* ------------------------------------------------------------------ */
+typedef struct { int rank; uint32_t psn; } pkt_t;
+
+int orc_allreduce_write_loopback(int R, const int32_t *const *src, uint32_t len,
+                                 int32_t *const *dst, int dup_every,
+                                 uint64_t *frames_out, int with_icrc)
+{
+    if (R < 1 || R > ORC_MAX_FAN_IN) return -1;
+    const int message_num = (int)(len / ORC_PAYLOAD_COUNT);                 /* api.c:406 */
+    const int window_msgs = ORC_WINDOW_SIZE / ORC_MESSAGE_SIZE;             /* api.c:408 */
+    if (message_num < window_msgs) return -1;   /* the reference would read past src */
+    const size_t buf_words = (size_t)message_num * ORC_PAYLOAD_COUNT;
+
+    uint32_t **send_payload = calloc((size_t)R, sizeof(*send_payload));
+    uint32_t **recv_payload = calloc((size_t)R, sizeof(*recv_payload));
+    uint8_t **delivered = calloc((size_t)R, sizeof(*delivered));   /* per (msg) packet bitmap */
+    int *send_num = calloc((size_t)R, sizeof(int));
+    int *recv_num = calloc((size_t)R, sizeof(int));
+    const size_t qcap = (size_t)R * (size_t)message_num * ORC_PKTS_PER_MSG * 2 + 16;
+    pkt_t *q = malloc(qcap * sizeof(pkt_t));
+    orc_switch *sw = malloc(sizeof(orc_switch));
+    uint32_t egress[ORC_LANES];
+    int32_t egress_host[ORC_LANES];
+    uint8_t frame[2048];
+    uint64_t frames = 0, ingress_count = 0;
+    size_t qh = 0, qt = 0;
+    int ok = 1;
+
+    for (int r = 0; r < R; ++r) {
+        send_payload[r] = malloc(buf_words * 4);
+        recv_payload[r] = calloc(buf_words, 4);
+        delivered[r] = calloc((size_t)message_num, 1);
+        if (!send_payload[r] || !recv_payload[r] || !delivered[r]) ok = 0;
+    }
+    if (!send_payload || !recv_payload || !delivered || !send_num || !recv_num || !q || !sw) ok = 0;
+    if (!ok) goto out;
+    orc_switch_init(sw, R);
+
+#define POST_SEND(r, idx)                                                                     \
+    do {                                                                                      \
+        orc_encode_be32(src[r] + (size_t)(idx) * ORC_PAYLOAD_COUNT,                           \
+                        send_payload[r] + (size_t)(idx) * ORC_PAYLOAD_COUNT, ORC_PAYLOAD_COUNT); \
+        for (int p_ = 0; p_ < ORC_PKTS_PER_MSG; ++p_) {                                       \
+            q[qt].rank = (r); q[qt].psn = (uint32_t)((idx) * ORC_PKTS_PER_MSG + p_); ++qt;    \
+        }                                                                                     \
+    } while (0)
+
+    for (int r = 0; r < R; ++r)
+        for (int i = 0; i < window_msgs; ++i) { POST_SEND(r, i); send_num[r]++; }   /* api.c:408-411 */
+
+    while (qh < qt) {
+        const pkt_t pk = q[qh++];
+        const uint32_t msg = pk.psn / ORC_PKTS_PER_MSG, part = pk.psn % ORC_PKTS_PER_MSG;
+        const uint32_t *payload = send_payload[pk.rank] + (size_t)pk.psn * ORC_LANES;
+        int passes = (dup_every > 0 && (++ingress_count % (uint64_t)dup_every) == 0) ? 2 : 1;
+        for (int pass = 0; pass < passes; ++pass) {      /* pass 1 = immediate retransmit */
+            const int rc = orc_switch_ingress(sw, pk.rank, pk.psn, payload, egress);
+            if (rc != ORC_SW_BROADCAST && rc != ORC_SW_REPLAY) continue;
+            const int c0 = (rc == ORC_SW_BROADCAST) ? 0 : pk.rank;
+            const int c1 = (rc == ORC_SW_BROADCAST) ? R : pk.rank + 1;
+            for (int c = c0; c < c1; ++c) {
+                if (with_icrc) {
+                    orc_frame_hdr h;
+                    memset(&h, 0, sizeof(h));
+                    h.qp = 0x11; h.psn = pk.psn; h.opcode = part == 0 ? 0x06 : (part == 3 ? 0x08 : 0x07);
+                    h.src_port = 4791; h.dst_port = 4791;
+                    orc_decode_be32(egress, egress_host, ORC_LANES);
+                    orc_build_data_frame(frame, &h, egress_host, ORC_LANES, part == 0, NULL);
+                }
+                frames++;
+                /* the NIC writes the payload at the RETH address = own receive_payload + idx*4096 */
+                memcpy(recv_payload[c] + (size_t)pk.psn * ORC_LANES, egress, ORC_PAYLOAD_LEN);
+                const uint8_t bit = (uint8_t)(1u << part);
+                if (delivered[c][msg] & bit) continue;
+                delivered[c][msg] |= bit;
+                if (delivered[c][msg] != 0x0F) continue;
+                /* completion of WRITE wr_id = msg: api.c:422-438 */
+                orc_decode_be32(recv_payload[c] + (size_t)msg * ORC_PAYLOAD_COUNT,
+                                dst[c] + (size_t)recv_num[c] * ORC_PAYLOAD_COUNT, ORC_PAYLOAD_COUNT);
+                recv_num[c]++;
+                if (send_num[c] < message_num) { POST_SEND(c, send_num[c]); send_num[c]++; }
+            }
+        }
+    }
+#undef POST_SEND
+    for (int r = 0; r < R; ++r)
+        if (recv_num[r] != message_num) ok = 0;
+
+out:
+    if (frames_out) *frames_out = frames;
+    for (int r = 0; r < R && send_payload && recv_payload && delivered; ++r) {
+        free(send_payload[r]); free(recv_payload[r]); free(delivered[r]);
+    }
+    free(send_payload); free(recv_payload); free(delivered);
+    free(send_num); free(recv_num); free(q); free(sw);
+    return ok ? message_num : -1;
+}

@@ -1,0 +1,145 @@
+/*
+ * inccl_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the host-side allreduce hot path of In-NetLab/container_inc
+ * (INCCL), written from scratch in plain C11.  It is the parity checker for the
+ * MI355X engine in container_inc_amd/: only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product library never links it.
+ *
+ * Every function cites the reference file:line it restates (paths relative to
+ * the reference checkout's repository/ directory).
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - integer sum + wire codec + windowed driver: pinned by the reference's own
+ *     known-answer test src/host.c:20-25,51-55 (in[i] = i*(rank+1), two ranks,
+ *     dst[i] == 3*i) -> tests/golden/host_known_answer.*
+ *   - ICRC: pinned by the canned RoCEv2 ACK frame in src/test.c:4-22 whose
+ *     captured ICRC bytes are kept at src/test.c:21 (e8 b0 bb 30).
+ *   - fp32 quantise / dequantise: NOT present in the reference (no float in its
+ *     data path).  Pinned by the spec below plus known-answer vectors
+ *     (powers of two, ties-to-even, saturation, NaN/Inf, denormals).
+ * The reference itself is unbuildable in this image (needs infiniband/verbs.h
+ * and pcap.h, both absent), so there is no oracle/_ref build.
+ */
+#ifndef INCCL_ORACLE_H
+#define INCCL_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Size constants of the reference (repository/include/api.h:38-40,
+ * repository/include/util.h:85, repository/src/non_termination_switch.c:21-24). */
+#define ORC_PAYLOAD_LEN      1024   /* bytes per RoCE packet payload  (util.h:85)        */
+#define ORC_LANES            256    /* int32 lanes per packet          (nts.c:55)         */
+#define ORC_MESSAGE_SIZE     4096   /* bytes per RDMA WRITE message    (api.h:39)         */
+#define ORC_PAYLOAD_COUNT    1024   /* int32 per message               (api.h:40)         */
+#define ORC_WINDOW_SIZE      8192   /* host window in bytes            (api.h:38)         */
+#define ORC_PKTS_PER_MSG     4      /* MESSAGE_SIZE / PAYLOAD_LEN                         */
+#define ORC_SW_WINDOW        8      /* switch window in packets        (nts.c:21)         */
+#define ORC_SW_SLOTS         16     /* N = 2*WINDOW_SIZE slots         (nts.c:22)         */
+#define ORC_MAX_FAN_IN       31     /* bitmap bit FAN_IN marks "result known" (nts.c:29-30,366) */
+#define ORC_ETH_HDR          14
+#define ORC_IP_HDR           20
+#define ORC_UDP_HDR          8
+#define ORC_BTH_HDR          12
+#define ORC_RETH_HDR         16
+#define ORC_AETH_HDR         4
+#define ORC_ICRC_LEN         4
+
+/* Quantiser scale exponents accepted by the engine (spec). */
+#define ORC_SCALE_MIN        (-64)
+#define ORC_SCALE_MAX        64
+
+/* ---------------- byte order (wire codec) ---------------- */
+/* api.c:300-302 post_send: send_payload[i] = htonl(src[i]) */
+void orc_encode_be32(const int32_t *src, uint32_t *wire, size_t n);
+/* api.c:428-430 / :377-379: dst[j] = ntohl(receive_payload[j]) */
+void orc_decode_be32(const uint32_t *wire, int32_t *dst, size_t n);
+
+/* ---------------- fp32 <-> fixed point (new front/back stages) ---------------- */
+/* q = sat_i32(round_half_even(x * 2^k)); NaN -> 0; +Inf -> INT32_MAX; -Inf -> INT32_MIN. */
+int32_t orc_quantise_one(float x, int k);
+void    orc_quantise_f32(const float *x, int32_t *q, size_t n, int k);
+/* f = (float)q * 2^-k  ((float)q rounds to nearest even; the scaling is exact). */
+float   orc_dequantise_one(int32_t q, int k);
+void    orc_dequantise_q32(const int32_t *q, float *f, size_t n, int k);
+
+/* ---------------- reduction ---------------- */
+/* nts.c:361-363: aggregator[slot][i] += ntohl(data[i]) -- two's-complement wrap
+ * (done in uint32 here: the reference's signed int accumulator is UB on overflow). */
+void orc_sum_q32(const int32_t *const *srcs, int R, int32_t *dst, size_t n);
+/* Fused spec of the engine's single-GPU path: dst = dequant(sum_r quant(src_r)). */
+void orc_reduce_f32(const float *const *srcs, int R, float *dst, size_t n, int k);
+/* Local quantise+sum to int32 (first stage of the multi-GPU path). */
+void orc_quant_sum(const float *const *srcs, int R, int32_t *dst, size_t n, int k);
+/* max |x| over R buckets; NaN lanes ignored. */
+float orc_absmax_f32(const float *const *srcs, int R, size_t n);
+/* Largest k with R*absmax*2^k <= 2^30 (one bit of headroom), clamped to
+ * [ORC_SCALE_MIN, ORC_SCALE_MAX]; absmax == 0 -> ORC_SCALE_MAX; Inf -> ORC_SCALE_MIN. */
+int   orc_choose_scale(float absmax, int R);
+/* Position-weighted linear checksum: sum_i (2i+1) * (uint32)q[i]  mod 2^32. */
+uint32_t orc_checksum_q32(const int32_t *q, size_t n, uint64_t index_base);
+
+/* ---------------- switch aggregation pipeline (root switch) ---------------- */
+/* State of nts.c:55-60 restated for one root switch with fan_in children. */
+typedef struct orc_switch {
+    int      fan_in;
+    int32_t  aggregator[ORC_SW_SLOTS][ORC_LANES];   /* nts.c:55 */
+    uint32_t arrival_state[ORC_SW_SLOTS];           /* nts.c:59 bitmap */
+    int      degree[ORC_SW_SLOTS];                  /* nts.c:60 */
+    uint64_t adds;                                  /* packets actually summed */
+    uint64_t replays;                               /* retransmits answered from the slot */
+} orc_switch;
+
+void orc_switch_init(orc_switch *sw, int fan_in);
+/* One UP data packet from child `port` with PSN `psn` and a big-endian payload of
+ * ORC_LANES words (nts.c:347-374 / :427-455, root branch).
+ * Returns:  ORC_SW_ABSORBED  first arrival, aggregate not complete yet
+ *           ORC_SW_BROADCAST first arrival completed the slot; egress_be holds the
+ *                            big-endian aggregate to send to EVERY child (nts.c:369-371)
+ *           ORC_SW_REPLAY    retransmit of a completed slot; egress_be holds the aggregate
+ *                            to send back to `port` only (nts.c:353-356)
+ *           ORC_SW_DROPPED   retransmit of an incomplete slot (nts.c:353 with no result) */
+enum { ORC_SW_ABSORBED = 0, ORC_SW_BROADCAST = 1, ORC_SW_REPLAY = 2, ORC_SW_DROPPED = 3 };
+int orc_switch_ingress(orc_switch *sw, int port, uint32_t psn,
+                       const uint32_t *payload_be, uint32_t *egress_be);
+
+/* ---------------- RoCEv2 framing + ICRC ---------------- */
+/* util.c:141-195: reflected CRC-32 (poly 0xEDB88320), init ~0, final ~. */
+uint32_t orc_crc32(const void *data, size_t len);
+/* util.c:250-286: ICRC over 8 x 0xFF || IP..payload with tos/ttl/ipcsum/udpcsum/qpn-low-byte masked. */
+uint32_t orc_icrc(const uint8_t *frame);
+/* util.c:106-127 */
+uint16_t orc_ipv4_checksum(const uint8_t *ip_hdr);
+/* util.c:331-442 build_eth_packet for PACKET_TYPE_DATA (reth == NULL, with_reth == 0)
+ * and PACKET_TYPE_RETH (with_reth != 0; reth may be NULL -> zeroed).  `payload_host`
+ * holds host-order words; they are written big-endian.  Returns the frame length. */
+typedef struct orc_frame_hdr {
+    uint8_t  src_mac[6], dst_mac[6];
+    uint32_t src_ip, dst_ip;      /* network order, as util.c:362-363 stores them */
+    uint16_t src_port, dst_port;  /* host order */
+    uint32_t qp, psn;
+    uint8_t  opcode;
+} orc_frame_hdr;
+size_t orc_build_data_frame(uint8_t *frame, const orc_frame_hdr *h, const int32_t *payload_host,
+                            int n_words, int with_reth, const uint8_t *reth16);
+
+/* ---------------- windowed host driver + switch, single-process loopback ---------------- */
+/* Drives R ranks through api.c:403-452 (inccl_allreduce_write: 2-message window,
+ * encode, completion-ordered decode) against one root switch (nts.c:303-501).
+ * Each RDMA WRITE of 4096 B is four 1 KiB packets with consecutive PSNs.
+ * `dup_every` > 0 re-injects every dup_every-th packet as a retransmit (idempotence).
+ * Elements [message_num*1024, len) of dst are left untouched, as in the reference.
+ * Returns the number of messages decoded per rank. */
+int orc_allreduce_write_loopback(int R, const int32_t *const *src, uint32_t len,
+                                 int32_t *const *dst, int dup_every,
+                                 uint64_t *frames_out, int with_icrc);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* INCCL_ORACLE_H */

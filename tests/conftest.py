@@ -1,0 +1,49 @@
+"""Shared test setup.
+
+Markers: ``gpu`` -- needs a real MI355X (run with ``-m gpu``).  Everything else
+runs on CPU: the oracle against the golden fixtures, the C-ABI surface of
+libinccl_amd.so (loads + exports, no compute), the TCP bootstrap, and the
+multi-rank shard plan over ``gloo``.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X GPU (HIP kernels / RCCL)")
+
+
+@pytest.fixture(scope="session")
+def orc():
+    from oracle import oracle as O
+    O.build()
+    return O
+
+
+@pytest.fixture(scope="session")
+def lib():
+    import container_inc_amd as cia
+    if not os.path.exists(cia.LIB_PATH):
+        cia.build()
+    return cia.load()
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but no GPU is visible")
+    import container_inc_amd as cia
+    if not os.path.exists(cia.LIB_PATH):
+        cia.build()
+    cia.load()
+    return torch.device("cuda:0")

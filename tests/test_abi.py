@@ -1,0 +1,91 @@
+"""The C-ABI boundary: libinccl_amd.so loads and exports exactly what
+include/api.h and include/inccl_amd.h declare; the headers compile as plain C
+with no HIP/RCCL/torch headers.  No compute calls (CPU only)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("api.h", "inccl_amd.h")]
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"\b(inccl_\w+)\s*\(", text):
+            names.add(m.group(1))
+    return names
+
+
+def exported_symbols(path):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", path], text=True)
+    return {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+
+
+def test_reference_six_entry_points_declared():
+    # repository/include/api.h:93-101
+    ref = {"inccl_group_create", "inccl_group_destroy", "inccl_communicator_create",
+           "inccl_communicator_destroy", "inccl_allreduce_sendrecv", "inccl_allreduce_write"}
+    assert ref <= declared_functions()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    import container_inc_amd as cia
+    decl = declared_functions()
+    exp = exported_symbols(cia.LIB_PATH)
+    missing = decl - exp
+    assert not missing, f"declared but not exported: {sorted(missing)}"
+    extra = {s for s in exp if s.startswith("inccl_")} - decl
+    assert not extra, f"exported but undeclared: {sorted(extra)}"
+    for name in decl:
+        assert hasattr(lib, name)
+
+
+def test_python_binding_covers_abi():
+    from container_inc_amd._lib import SIGNATURES
+    assert set(SIGNATURES) == declared_functions()
+
+
+def test_headers_compile_as_plain_c(tmp_path):
+    src = tmp_path / "t.c"
+    src.write_text('#include "api.h"\n#include "inccl_amd.h"\nint main(void){return INCCL_OK;}\n')
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Werror", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),
+                           str(src)])
+
+
+def test_host_example_links(tmp_path):
+    exe = tmp_path / "host_example"
+    subprocess.check_call(["gcc", "-O2", "-std=c11", "-Wall", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "c", "host_example.c"), "-o", str(exe),
+                           "-L", os.path.join(ROOT, "container_inc_amd"), "-linccl_amd", "-lpthread"])
+    assert exe.exists()
+
+
+def test_version_and_host_helpers(lib):
+    assert lib.inccl_version().startswith(b"inccl-amd")
+    from container_inc_amd import inccl
+    assert inccl.choose_scale(6.0, 8) == 24
+
+
+def test_choose_scale_host_matches_oracle(lib, orc):
+    from container_inc_amd import inccl
+    for amax in (0.0, 1e-30, 1e-3, 0.25, 0.5, 1.0, 6.0, 7.999, 1e6, 3e38, float("inf")):
+        for R in (1, 2, 3, 8, 64):
+            assert inccl.choose_scale(amax, R) == orc.choose_scale(amax, R), (amax, R)
+
+
+def test_no_device_means_loud_failure(lib):
+    """Without a GPU the product fails; it never computes on the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from container_inc_amd import inccl
+    g = inccl.inccl_group_create(1, 0, "127.0.0.1")
+    assert g is None
+    assert lib.inccl_last_error()

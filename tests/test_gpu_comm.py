@@ -1,0 +1,184 @@
+"""Communicator paths on the GPU (gpu): the reference's host API
+(inccl_allreduce_write / _sendrecv) and the fp32 allreduce, over the
+in-process transport (ranks = threads sharing one GPU, the GPU's sum kernel is
+the switch) and over RCCL at world size 1.  Checked against the oracle."""
+import os
+import subprocess
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+INT32_MIN, INT32_MAX = -(2 ** 31), 2 ** 31 - 1
+
+
+def _run_ranks(world, fn):
+    """Run fn(rank) on `world` threads; re-raise the first failure."""
+    errs = [None] * world
+    out = [None] * world
+
+    def body(r):
+        try:
+            out[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = e
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    for e in errs:
+        if e is not None:
+            raise e
+    return out
+
+
+def test_host_example_binary(gpu, tmp_path):
+    """tests/c/host_example.c: host.c's known answer through the C ABI alone."""
+    exe = tmp_path / "host_example"
+    subprocess.check_call(["gcc", "-O2", "-std=c11", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "c", "host_example.c"), "-o", str(exe),
+                           "-L", os.path.join(ROOT, "container_inc_amd"), "-linccl_amd", "-lpthread",
+                           "-Wl,-rpath," + os.path.join(ROOT, "container_inc_amd")])
+    for world in (2, 4):
+        r = subprocess.run([str(exe), str(world), "local"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "result ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("variant", ["write", "sendrecv"])
+def test_allreduce_write_known_answer(gpu, variant):
+    """host.c:20-25,41,47,51-55 with the reference's two ranks."""
+    from container_inc_amd import inccl
+    g = np.load(os.path.join(GOLDEN, "host_known_answer.npz"))
+    hub = f"known-{variant}"
+
+    def rank(r):
+        grp = inccl.inccl_group_create_local(2, r, hub)
+        comm = inccl.inccl_communicator_create(grp, int(g["comm_size_bytes"]))
+        dst = np.zeros_like(g["expected"])
+        fn = inccl.inccl_allreduce_write if variant == "write" else inccl.inccl_allreduce_sendrecv
+        fn(comm, g["inputs"][r].copy(), g["inputs"].shape[1], dst)
+        comm.destroy()
+        grp.destroy()
+        return dst
+
+    for dst in _run_ranks(2, rank):
+        np.testing.assert_array_equal(dst, g["expected"])
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_allreduce_write_random_ragged(gpu, orc, world):
+    """Random int32 with wrap, len not a multiple of 1024: tail untouched (api.c:406),
+    small staging (comm size 16 KiB) so the pinned ping-pong path runs many chunks."""
+    from container_inc_amd import inccl
+    n = 1024 * 37 + 500
+    rng = np.random.default_rng(world)
+    xs = [rng.integers(INT32_MIN, INT32_MAX, n, dtype=np.int64, endpoint=True).astype(np.int32) for _ in range(world)]
+    want = orc.sum_q32(xs)
+    hub = f"ragged-{world}"
+
+    def rank(r):
+        grp = inccl.inccl_group_create_local(world, r, hub)
+        comm = inccl.inccl_communicator_create(grp, 16384)
+        dst = np.full(n, 77, np.int32)
+        comm.allreduce_write(xs[r], n, dst)
+        comm.destroy()
+        grp.destroy()
+        return dst
+
+    for dst in _run_ranks(world, rank):
+        np.testing.assert_array_equal(dst[: 37 * 1024], want[: 37 * 1024])
+        assert np.all(dst[37 * 1024:] == 77)
+
+
+@pytest.mark.parametrize("world,R,n,chunks,k", [
+    (2, 2, 1 << 20, 1, 25),
+    (2, 2, (1 << 20) + 77, 3, 25),
+    (3, 1, 100_001, 1, 20),
+    (4, 2, 1 << 18, 4, "auto"),
+    (8, 1, 65_536, 2, 22),
+])
+def test_allreduce_f32_local(gpu, orc, world, R, n, chunks, k):
+    """quant+local sum -> reduce-scatter (the GPU sum kernel over every rank's
+    shard) -> dequant shard -> all-gather, vs oracle.reduce_f32 of all W*R buckets."""
+    import torch
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(world * 100 + R)
+    xs = [[(rng.standard_normal(n) * 2).astype(np.float32) for _ in range(R)] for _ in range(world)]
+    every = [x for per in xs for x in per]
+    kk = orc.choose_scale(orc.absmax(every), world * R) if k == "auto" else k
+    want = orc.reduce_f32(every, kk)
+    dev_in = [[torch.from_numpy(x).to(gpu) for x in per] for per in xs]
+    torch.cuda.synchronize()
+    hub = f"f32-{world}-{R}-{n}-{chunks}"
+
+    def rank(r):
+        grp = inccl.inccl_group_create_local(world, r, hub)
+        comm = inccl.inccl_communicator_create(grp, 0)
+        out = torch.empty(n, dtype=torch.float32, device=gpu)
+        comm.allreduce_f32(dev_in[r], out=out, scale_exp=inccl.SCALE_AUTO if k == "auto" else k, chunks=chunks,
+                           stream=comm.stream)
+        torch.cuda.synchronize()
+        comm.barrier()
+        res = out.cpu().numpy()
+        comm.destroy()
+        grp.destroy()
+        return res
+
+    for res in _run_ranks(world, rank):
+        np.testing.assert_array_equal(res.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.fixture()
+def force_rccl(monkeypatch):
+    monkeypatch.setenv("INCCL_FORCE_RCCL", "1")
+    monkeypatch.setenv("INCCL_FORCE_SHARDED", "1")
+    monkeypatch.setenv("INCCL_MASTER_PORT", "0")
+
+
+def test_rccl_world1_paths(gpu, orc, force_rccl):
+    """RCCL transport at world size 1: ncclReduceScatter / ncclAllGather /
+    ncclAllReduce are real RCCL calls on a one-rank communicator."""
+    import torch
+    from container_inc_amd import inccl
+    grp = inccl.inccl_group_create(1, 0, "127.0.0.1")
+    assert grp is not None and grp.transport == "rccl"
+    comm = inccl.inccl_communicator_create(grp, 1 << 20)
+    rng = np.random.default_rng(5)
+    for n, chunks in ((1 << 20, 1), ((1 << 20) + 5, 3)):
+        xs = [rng.standard_normal(n).astype(np.float32) for _ in range(2)]
+        out = comm.allreduce_f32([torch.from_numpy(x).to(gpu) for x in xs], scale_exp=25, chunks=chunks)
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), orc.reduce_f32(xs, 25).view(np.uint32))
+    q = rng.integers(INT32_MIN, INT32_MAX, 4096, dtype=np.int64, endpoint=True).astype(np.int32)
+    np.testing.assert_array_equal(comm.allreduce_q32(torch.from_numpy(q).to(gpu)).cpu().numpy(), q)
+    dst = np.zeros(4096, np.int32)
+    comm.allreduce_write(q, 4096, dst)
+    np.testing.assert_array_equal(dst, q)
+    comm.destroy()
+    grp.destroy()
+
+
+def test_allreduce_f32_host_buckets(gpu, orc):
+    """BASELINE config 3 shape (scaled down): host fp32 -> 3-stream pipeline -> host."""
+    import torch
+    from container_inc_amd import inccl
+    grp = inccl.inccl_group_create(1, 0, "127.0.0.1")
+    comm = inccl.inccl_communicator_create(grp, 0)
+    n = (16 << 20) // 4 + 333
+    x = torch.randn(n, dtype=torch.float32).pin_memory()
+    y = torch.empty(n, dtype=torch.float32).pin_memory()
+    comm.allreduce_f32_host(x, y, scale_exp=24, bucket_bytes=1 << 20)
+    want = orc.reduce_f32([x.numpy()], 24)
+    np.testing.assert_array_equal(y.numpy().view(np.uint32), want.view(np.uint32))
+    # pageable numpy buffers work too (synchronous staging)
+    xn = x.numpy().copy()
+    yn = np.empty_like(xn)
+    comm.allreduce_f32_host(xn, yn, scale_exp=24, bucket_bytes=3 << 20)
+    np.testing.assert_array_equal(yn.view(np.uint32), want.view(np.uint32))
+    comm.destroy()
+    grp.destroy()
