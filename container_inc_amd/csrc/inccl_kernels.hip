@@ -21,7 +21,8 @@
 // wave-instruction = exactly one reference packet payload of 256 lanes,
 // nts.c:55).  A workgroup of 256 lanes owns a tile of 256*U float4 per input and
 // issues all R*U loads before touching them (R*U*16 B in flight per lane), then
-// writes U nontemporal float4 stores.  Grid-stride over tiles.
+// writes U nontemporal float4 stores.  One workgroup per tile by default (a
+// grid-stride loop covers a capped grid).
 //
 // The horizontal reductions (absmax for automatic scaling, the position
 // weighted checksum) use wave64 __shfl_xor trees, an LDS stage across the
@@ -312,7 +313,9 @@ int launch_stream_R(const SrcPtrs& s, void* dst, int64_t n, const Scale& sc, hip
         if (n4 > 0) {
             constexpr int U = Unroll<R>::U;
             const int64_t tiles = (n4 + (int64_t)kBlock * U - 1) / ((int64_t)kBlock * U);
-            const int64_t cap = g_grid_cap > 0 ? g_grid_cap : (int64_t)num_cus() * 16;
+            // One workgroup per tile by default (measured on MI355X, 2 x 256 MiB
+            // fused: one-shot 6.51 TB/s vs 6.23 TB/s for a 16-per-CU grid-stride cap).
+            const int64_t cap = g_grid_cap > 0 ? g_grid_cap : (int64_t)0x7fffffff;
             const int grid = (int)(tiles < cap ? tiles : cap);
             if (g_nt_loads)
                 hipLaunchKernelGGL((k_stream_vec<IN, OUT, R, true>), dim3(grid), dim3(kBlock), 0, st, s, dst, n4, sc);
