@@ -39,7 +39,9 @@ def parse():
     p.add_argument("--bucket-mib", type=int, default=256)
     p.add_argument("--local-buckets", type=int, default=2)
     p.add_argument("--scale-exp", type=int, default=25)
-    p.add_argument("--chunks", type=int, default=int(os.environ.get("INCCL_BENCH_CHUNKS", "4")))
+    p.add_argument("--chunks", type=int, default=0, help="pipelined chunks for the rccl engine (0 = tune)")
+    p.add_argument("--engine", default="auto", choices=["auto", "rccl", "p2p"],
+                   help="N>1 exchange engine; auto = time every candidate during warmup, keep the fastest")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--grid-cap", type=int, default=0)
@@ -98,6 +100,13 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         print(f"warning: WORLD_SIZE={world} but --gpus={a.gpus}; using WORLD_SIZE", file=sys.stderr)
+    # rehearsal hook: every rank on device 0 (a one-GPU box running N>1 over the
+    # p2p engine; RCCL refuses two ranks on one GPU)
+    if os.environ.get("INCCL_BENCH_SAME_DEVICE") == "1":
+        local_rank = 0
+    os.environ.setdefault("INCCL_BOOT_TIMEOUT", "120")
+    if a.engine == "p2p":
+        os.environ["INCCL_ENGINE"] = "p2p"   # no eager RCCL communicator
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
@@ -120,7 +129,54 @@ def main():
         raise SystemExit("inccl_group_create failed: " + container_inc_amd.load().inccl_last_error().decode())
     comm = inccl.inccl_communicator_create(grp, 0)
     stream = torch.cuda.Stream(device=dev)
-    chunks = a.chunks if world > 1 else 1
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # N>1: pick the exchange engine / chunking during warmup (untimed).  Every
+    # candidate must produce a bit-identical result (integer sums are exact);
+    # any failure or mismatch on any rank drops that candidate on all ranks.
+    chosen = ("rccl", 1)
+    tuning = []
+    if world > 1:
+        cands = []
+        if a.engine in ("auto", "rccl"):
+            cands += [("rccl", c) for c in ([a.chunks] if a.chunks else [1, 4])]
+        if a.engine in ("auto", "p2p"):
+            cands.append(("p2p", 1))
+        ref = None
+        best = None
+        for eng, ch in cands:
+            ok, dt = 1, float("inf")
+            try:
+                comm.set_engine(eng)
+                for _ in range(3):
+                    comm.allreduce_f32(srcs, out=out, scale_exp=k, chunks=ch, stream=stream.cuda_stream)
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = out.clone()
+                elif not torch.equal(ref, out):
+                    ok = 0
+                barrier()
+                t0 = time.perf_counter()
+                for _ in range(5):
+                    comm.allreduce_f32(srcs, out=out, scale_exp=k, chunks=ch, stream=stream.cuda_stream)
+                torch.cuda.synchronize()
+                dt = time.perf_counter() - t0
+            except Exception as e:  # noqa: BLE001
+                print(f"rank {rank}: engine {eng} chunks {ch} failed: {e}", file=sys.stderr, flush=True)
+                ok = 0
+            v = torch.tensor([dt if ok else float("inf"), 0.0 if ok else 1.0], dtype=torch.float64)
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+            good = v[1].item() == 0.0
+            tuning.append({"engine": eng, "chunks": ch, "ok": good, "ms": round(v[0].item() * 200, 3) if good else None})
+            if good and (best is None or v[0].item() < best[0]):
+                best = (v[0].item(), eng, ch)
+        if best is not None:
+            chosen = (best[1], best[2])
+        comm.set_engine(chosen[0])
+    chunks = chosen[1]
 
     def step():
         comm.allreduce_f32(srcs, out=out, scale_exp=k, chunks=chunks, stream=stream.cuda_stream)
@@ -128,10 +184,6 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
 
     barrier()
     torch.cuda.synchronize()
@@ -175,8 +227,11 @@ def main():
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
     workload = (f"fused quantise+sum+dequantise of R={R} resident {a.bucket_mib} MiB fp32 buckets, 1 GPU"
                 if world == 1 else
-                f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: quant+local sum -> RCCL reduce-scatter "
-                f"int32 -> dequant shard -> RCCL all-gather fp32, {chunks} pipelined chunks")
+                (f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: quant+local sum -> RCCL reduce-scatter "
+                 f"int32 -> dequant shard -> RCCL all-gather fp32, {chunks} pipelined chunks")
+                if comm.engine == "rccl" else
+                (f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: quant+local sum -> p2p pull of every "
+                 f"peer's shard over xGMI with fused sum+dequant -> p2p gather of every result shard"))
     kname = "k_stream_vec<F32,F32,R>" if world == 1 else "k_stream_vec<F32,Q32,R>"
     traffic = load_traffic(kname + f" R={R} n={n}")
 
@@ -203,6 +258,8 @@ def main():
             "global_batch": world * R,
             "parallelism": f"dp{world}",
             "chunks": chunks,
+            "engine": comm.engine if world > 1 else "fused",
+            "engine_tuning": tuning or None,
             "shard_elems": chunk_plan(n, world, chunks)[0][2] if world > 1 else n,
         },
         "roofline": {

@@ -282,7 +282,14 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     INCCL_HIP(hipMalloc((void **)&c->d_words, 256));
     INCCL_HIP(hipMemset(c->d_words, 0, 256));
     c->comm_id = g->comm_seq++;
-    if (g->transport == INCCL_TRANSPORT_RCCL) {
+    const char *eng = getenv("INCCL_ENGINE");
+    if (eng && *eng && g->transport == INCCL_TRANSPORT_RCCL) {
+        int rc = inccl_comm_set_engine(c, eng);
+        if (rc) return rc;
+    }
+    /* RCCL communicator up front (errors surface at creation), unless the p2p
+     * engine was chosen: then RCCL is created on first use, if ever */
+    if (g->transport == INCCL_TRANSPORT_RCCL && c->engine == INCCL_ENGINE_RCCL) {
         const char *force = getenv("INCCL_FORCE_RCCL");
         if (g->world_size > 1 || (force && atoi(force) != 0)) {
             int rc = inccl_rccl_comm_init(c);
@@ -302,6 +309,10 @@ int inccl_communicator_destroy(struct inccl_communicator *comm)
     if (!comm) return 0;
     if (comm->group->device >= 0) hipSetDevice(comm->group->device);
     if (comm->stream) hipStreamSynchronize(comm->stream);
+    if (comm->p2p_part) {   /* peers may still be reading our shard buffers */
+        inccl_boot_barrier(comm->group);
+        inccl_p2p_release(comm);
+    }
     inccl_rccl_comm_destroy(comm);
     if (comm->d_q32) hipFree(comm->d_q32);
     if (comm->d_f32) hipFree(comm->d_f32);
@@ -338,6 +349,29 @@ struct inccl_communicator *inccl_communicator_create(struct inccl_group *group, 
 }
 
 void *inccl_comm_stream(struct inccl_communicator *comm) { return comm ? (void *)comm->stream : NULL; }
+
+int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name)
+{
+    if (!comm || !name) return inccl_set_error(INCCL_ERR_ARG, "bad set_engine args");
+    if (strcmp(name, "rccl") == 0) {
+        comm->engine = INCCL_ENGINE_RCCL;
+        return 0;
+    }
+    if (strcmp(name, "p2p") == 0) {
+        if (comm->group->transport != INCCL_TRANSPORT_RCCL)
+            return inccl_set_error(INCCL_ERR_ARG, "p2p engine needs a multi-process (rccl) group");
+        comm->engine = INCCL_ENGINE_P2P;
+        return 0;
+    }
+    return inccl_set_error(INCCL_ERR_ARG, "unknown engine '%s' (rccl | p2p)", name);
+}
+
+const char *inccl_comm_engine(const struct inccl_communicator *comm)
+{
+    if (!comm) return "";
+    if (comm->group->transport == INCCL_TRANSPORT_LOCAL) return "local";
+    return comm->engine == INCCL_ENGINE_P2P ? "p2p" : "rccl";
+}
 
 int inccl_comm_barrier(struct inccl_communicator *comm)
 {
@@ -430,6 +464,8 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
         return kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, k,
                                    amax, scale_R, st));
 
+    if (c->engine == INCCL_ENGINE_P2P && c->group->transport == INCCL_TRANSPORT_RCCL)
+        return inccl_p2p_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
     /* chunk boundaries: multiples of W*64 elements so every chunk's shards are
      * 256-B aligned inside dst; each chunk has its own workspace region */
     if (chunks < 1) chunks = 1;

@@ -176,6 +176,26 @@ int inccl_boot_bcast(struct inccl_group *g, void *buf, size_t bytes)
     return 0;
 }
 
+int inccl_boot_allgather(struct inccl_group *g, const void *mine, void *all, size_t bytes)
+{
+    char *out = (char *)all;
+    memcpy(out + (size_t)g->rank * bytes, mine, bytes);
+    if (g->world_size == 1) return 0;
+    if (g->rank == 0) {
+        for (int r = 1; r < g->world_size; ++r)
+            if (recv_all(g->peer_fds[r], out + (size_t)r * bytes, bytes) != 0)
+                return inccl_set_error(INCCL_ERR_SYS, "allgather: recv from rank %d failed", r);
+        for (int r = 1; r < g->world_size; ++r)
+            if (send_all(g->peer_fds[r], out, bytes * (size_t)g->world_size) != 0)
+                return inccl_set_error(INCCL_ERR_SYS, "allgather: send to rank %d failed", r);
+        return 0;
+    }
+    if (send_all(g->master_fd, mine, bytes) != 0 ||
+        recv_all(g->master_fd, out, bytes * (size_t)g->world_size) != 0)
+        return inccl_set_error(INCCL_ERR_SYS, "allgather: exchange with rank 0 failed");
+    return 0;
+}
+
 int inccl_boot_barrier(struct inccl_group *g)
 {
     if (g->world_size == 1) return 0;

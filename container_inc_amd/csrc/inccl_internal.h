@@ -17,6 +17,9 @@
 
 #define INCCL_TRANSPORT_RCCL 0
 #define INCCL_TRANSPORT_LOCAL 1
+/* communicator-level exchange engine (group transport RCCL only) */
+#define INCCL_ENGINE_RCCL 0
+#define INCCL_ENGINE_P2P 1
 
 struct inccl_local_hub;
 
@@ -55,6 +58,14 @@ struct inccl_communicator {
     void *d_stage;               /* host-path device staging (2 x in + 2 x out buckets) */
     size_t d_stage_bytes;
     uint32_t *d_words;           /* small scratch words: [0] absmax, [1] checksum */
+    /* p2p engine: library-owned buffers shared with every peer through HIP IPC
+     * handles; each GPU pulls its shard from all peers over xGMI */
+    int engine;                  /* INCCL_ENGINE_* */
+    size_t p2p_cap;              /* elements per buffer */
+    int32_t *p2p_part;           /* this rank's quantised partial sums (W * shard) */
+    float *p2p_res;              /* this rank's dequantised shard lives at rank * shard */
+    int32_t *p2p_peer_part[INCCL_MAX_LOCAL_INPUTS];
+    float *p2p_peer_res[INCCL_MAX_LOCAL_INPUTS];
     hipEvent_t ev[8];
 };
 
@@ -79,6 +90,11 @@ int inccl_rccl_allreduce_q32(struct inccl_communicator *c, const int32_t *send, 
                              hipStream_t st);
 int inccl_rccl_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st);
 
+/* p2p engine */
+int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
+                    const uint32_t *amax, int scale_R, hipStream_t st);
+void inccl_p2p_release(struct inccl_communicator *c);
+
 /* local transport */
 struct inccl_local_hub *inccl_hub_attach(const char *name, int world_size);
 void inccl_hub_detach(struct inccl_local_hub *hub);
@@ -96,6 +112,7 @@ int inccl_boot_master(struct inccl_group *g);
 int inccl_boot_worker(struct inccl_group *g);
 int inccl_boot_bcast(struct inccl_group *g, void *buf, size_t bytes);   /* from rank 0 */
 int inccl_boot_barrier(struct inccl_group *g);
+int inccl_boot_allgather(struct inccl_group *g, const void *mine, void *all, size_t bytes);
 void inccl_boot_close(struct inccl_group *g);
 
 /* errors */

@@ -19,6 +19,9 @@ int inccl_k_absmax(const float *const *srcs, int R, size_t n, uint32_t *amax_bit
 int inccl_k_checksum(const int32_t *q, size_t n, uint64_t index_base, uint32_t *out_dev, int zero_first,
                      void *stream);
 void inccl_k_set_tuning(int grid_cap, int nt_loads);
+/* dst[off[j] .. off[j]+cnt[j]) = src[j][0 .. cnt[j]) for j < nseg, 4-byte elements, one launch */
+int inccl_k_gather(const void *const *src, const int64_t *off, const int64_t *cnt, int nseg, void *dst,
+                   void *stream);
 
 #ifdef __cplusplus
 }

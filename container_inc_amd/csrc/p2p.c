@@ -1,0 +1,137 @@
+/* p2p.c -- the "p2p" exchange engine: reduce-scatter and all-gather as direct
+ * peer reads over xGMI with this library's own kernels (no RCCL on the data path).
+ *
+ * Every rank owns two library-allocated device buffers whose HIP IPC handles are
+ * exchanged once over the group's bootstrap sockets:
+ *   part  int32 [W * shard]  this rank's quantised local sums (W shards)
+ *   res   fp32  [W * shard]  this rank's dequantised result shard at rank * shard
+ * One bucket piece:
+ *   1. quant + local sum of the R buckets -> part            (HBM, local)
+ *   2. stream sync + group barrier                            (all parts ready)
+ *   3. res[me] = dequant( sum_j part_j[me] )  -- one kernel reading the W
+ *      peers' shard me concurrently (W-1 of them over xGMI): the reference's
+ *      switch aggregate (non_termination_switch.c:361-363) fused with the new
+ *      dequantise stage
+ *   4. stream sync + group barrier                            (all shards ready)
+ *   5. dst[j] = res_j[j] for every j -- one gather kernel pulling all W shards
+ * Buffer reuse is safe without a third barrier: a rank reaches the next
+ * call's step-2 barrier only after its own step 5 has drained (the sync in 2),
+ * so nobody still reads a `part` or `res` that the next call overwrites.
+ * Host barriers cost tens of microseconds; the step moves hundreds of MB. */
+#define _GNU_SOURCE
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "inccl_internal.h"
+#include "inccl_kernels.h"
+
+typedef struct {
+    hipIpcMemHandle_t part, res;
+} p2p_handles;
+
+void inccl_p2p_release(struct inccl_communicator *c)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    if (c->p2p_cap == 0 && !c->p2p_part) return;
+    hipDeviceSynchronize();
+    for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS; ++j) {
+        if (j == me) continue;
+        if (c->p2p_peer_part[j]) hipIpcCloseMemHandle(c->p2p_peer_part[j]);
+        if (c->p2p_peer_res[j]) hipIpcCloseMemHandle(c->p2p_peer_res[j]);
+        c->p2p_peer_part[j] = NULL;
+        c->p2p_peer_res[j] = NULL;
+    }
+    if (c->p2p_part) hipFree(c->p2p_part);
+    if (c->p2p_res) hipFree(c->p2p_res);
+    c->p2p_part = NULL;
+    c->p2p_res = NULL;
+    c->p2p_cap = 0;
+}
+
+/* collective: every rank calls it with the same `elems` */
+static int p2p_ensure(struct inccl_communicator *c, size_t elems)
+{
+    struct inccl_group *g = c->group;
+    const int W = g->world_size, me = g->rank;
+    if (c->p2p_cap >= elems && c->p2p_part) return 0;
+    /* peers may still read the old buffers until everyone is here */
+    int rc = inccl_boot_barrier(g);
+    if (rc) return rc;
+    inccl_p2p_release(c);
+    size_t cap = (elems + (1u << 19) - 1) & ~(size_t)((1u << 19) - 1);   /* 2 MiB granules */
+    INCCL_HIP(hipMalloc((void **)&c->p2p_part, cap * sizeof(int32_t)));
+    INCCL_HIP(hipMalloc((void **)&c->p2p_res, cap * sizeof(float)));
+    c->p2p_cap = cap;
+    p2p_handles mine, *all = (p2p_handles *)calloc((size_t)W, sizeof(p2p_handles));
+    if (!all) return inccl_set_error(INCCL_ERR_NOMEM, "p2p: out of memory");
+    memset(&mine, 0, sizeof(mine));
+    hipError_t e = hipIpcGetMemHandle(&mine.part, c->p2p_part);
+    if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.res, c->p2p_res);
+    if (e != hipSuccess) {
+        free(all);
+        return inccl_hip_check(e, "hipIpcGetMemHandle");
+    }
+    rc = inccl_boot_allgather(g, &mine, all, sizeof(p2p_handles));
+    for (int j = 0; rc == 0 && j < W; ++j) {
+        if (j == me) {
+            c->p2p_peer_part[j] = c->p2p_part;
+            c->p2p_peer_res[j] = c->p2p_res;
+            continue;
+        }
+        void *pp = NULL, *pr = NULL;
+        e = hipIpcOpenMemHandle(&pp, all[j].part, hipIpcMemLazyEnablePeerAccess);
+        if (e == hipSuccess) e = hipIpcOpenMemHandle(&pr, all[j].res, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) rc = inccl_hip_check(e, "hipIpcOpenMemHandle");
+        c->p2p_peer_part[j] = (int32_t *)pp;
+        c->p2p_peer_res[j] = (float *)pr;
+    }
+    free(all);
+    if (rc) return rc;
+    /* everyone mapped everyone before first use */
+    return inccl_boot_barrier(g);
+}
+
+static int sync_and_barrier(struct inccl_communicator *c, hipStream_t st)
+{
+    INCCL_HIP(hipStreamSynchronize(st));
+    return inccl_boot_barrier(c->group);
+}
+
+int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
+                    const uint32_t *amax, int scale_R, hipStream_t st)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    if (W > INCCL_MAX_LOCAL_INPUTS) return inccl_set_error(INCCL_ERR_ARG, "p2p engine supports up to %d GPUs",
+                                                          INCCL_MAX_LOCAL_INPUTS);
+    const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
+    int rc = p2p_ensure(c, total);
+    if (rc) return rc;
+    /* 1. local quantise + sum */
+    rc = inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_Q32, (const void *const *)srcs, R, c->p2p_part, n, k, amax,
+                        scale_R, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p quant+sum launch failed (%d)", rc);
+    if (total > n) INCCL_HIP(hipMemsetAsync(c->p2p_part + n, 0, (total - n) * sizeof(int32_t), st));
+    rc = sync_and_barrier(c, st);
+    if (rc) return rc;
+    /* 3. pull shard `me` from every peer, sum, dequantise */
+    const void *peer[INCCL_MAX_LOCAL_INPUTS];
+    for (int j = 0; j < W; ++j) peer[j] = c->p2p_peer_part[j] + (size_t)me * shard;
+    rc = inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_F32, peer, W, c->p2p_res + (size_t)me * shard, shard, k, amax,
+                        scale_R, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p reduce-scatter launch failed (%d)", rc);
+    rc = sync_and_barrier(c, st);
+    if (rc) return rc;
+    /* 5. gather every shard into dst (ragged last shard clamped to n) */
+    const void *src[INCCL_MAX_LOCAL_INPUTS];
+    int64_t off[INCCL_MAX_LOCAL_INPUTS], cnt[INCCL_MAX_LOCAL_INPUTS];
+    for (int j = 0; j < W; ++j) {
+        const size_t lo = (size_t)j * shard;
+        src[j] = c->p2p_peer_res[j] + lo;
+        off[j] = (int64_t)lo;
+        cnt[j] = lo >= n ? 0 : (int64_t)((n - lo) < shard ? (n - lo) : shard);
+    }
+    rc = inccl_k_gather(src, off, cnt, W, dst, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p gather launch failed (%d)", rc);
+    return 0;
+}

@@ -237,10 +237,36 @@ int inccl_local_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, s
 /* ------------------------------------------------------------------ */
 static int is_local(const struct inccl_communicator *c) { return c->group->transport == INCCL_TRANSPORT_LOCAL; }
 
+/* RCCL communicator on first use when the engine skipped the eager init (p2p) */
+static int ensure_rccl(struct inccl_communicator *c)
+{
+    if (c->nccl || c->group->world_size == 1) return 0;
+    return inccl_rccl_comm_init(c);
+}
+
+/* 4-byte max over the group through the bootstrap sockets (p2p engine) */
+static int host_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, hipStream_t st)
+{
+    struct inccl_group *g = c->group;
+    uint32_t v = 0, all[64];
+    if (g->world_size > 64) return inccl_set_error(INCCL_ERR_ARG, "host max-allreduce: world too large");
+    INCCL_HIP(hipMemcpyAsync(&v, buf, sizeof(v), hipMemcpyDeviceToHost, st));
+    INCCL_HIP(hipStreamSynchronize(st));
+    int rc = inccl_boot_allgather(g, &v, all, sizeof(v));
+    if (rc) return rc;
+    uint32_t m = 0;
+    for (int j = 0; j < g->world_size; ++j) m = all[j] > m ? all[j] : m;
+    INCCL_HIP(hipMemcpyAsync(buf, &m, sizeof(m), hipMemcpyHostToDevice, st));
+    INCCL_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
 int inccl_tp_reduce_scatter_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t shard,
                                 hipStream_t st)
 {
     if (is_local(c)) return inccl_local_reduce_scatter_q32(c, send, recv, shard, st);
+    int rc = ensure_rccl(c);
+    if (rc) return rc;
     if (!c->nccl) {   /* world 1 without RCCL: the reduce-scatter is a copy */
         if (send != recv) INCCL_HIP(hipMemcpyAsync(recv, send, shard * 4, hipMemcpyDeviceToDevice, st));
         return 0;
@@ -252,6 +278,8 @@ int inccl_tp_all_gather_f32(struct inccl_communicator *c, const float *send, flo
                             hipStream_t st)
 {
     if (is_local(c)) return inccl_local_all_gather_f32(c, send, recv, shard, st);
+    int rc = ensure_rccl(c);
+    if (rc) return rc;
     if (!c->nccl) {
         if (send != recv) INCCL_HIP(hipMemcpyAsync(recv, send, shard * 4, hipMemcpyDeviceToDevice, st));
         return 0;
@@ -263,6 +291,8 @@ int inccl_tp_allreduce_q32(struct inccl_communicator *c, const int32_t *send, in
                            hipStream_t st)
 {
     if (is_local(c)) return inccl_local_allreduce_q32(c, send, recv, n, st);
+    int rc = ensure_rccl(c);
+    if (rc) return rc;
     if (!c->nccl) {
         if (send != recv) INCCL_HIP(hipMemcpyAsync(recv, send, n * 4, hipMemcpyDeviceToDevice, st));
         return 0;
@@ -273,6 +303,9 @@ int inccl_tp_allreduce_q32(struct inccl_communicator *c, const int32_t *send, in
 int inccl_tp_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st)
 {
     if (is_local(c)) return inccl_local_allreduce_max_u32(c, buf, n, st);
+    if (c->engine == INCCL_ENGINE_P2P && n == 1) return host_allreduce_max_u32(c, buf, st);
+    int rc = ensure_rccl(c);
+    if (rc) return rc;
     if (!c->nccl) return 0;
     return inccl_rccl_allreduce_max_u32(c, buf, n, st);
 }

@@ -225,6 +225,13 @@ class Communicator:
     def stream(self) -> int:
         return load().inccl_comm_stream(self.handle)
 
+    @property
+    def engine(self) -> str:
+        return load().inccl_comm_engine(self.handle).decode()
+
+    def set_engine(self, name: str) -> None:
+        check(load().inccl_comm_set_engine(self.handle, name.encode()), "inccl_comm_set_engine")
+
     def barrier(self) -> None:
         check(load().inccl_comm_barrier(self.handle), "inccl_comm_barrier")
 

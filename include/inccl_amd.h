@@ -113,6 +113,14 @@ const char *inccl_group_transport(const struct inccl_group *group);
 /* The communicator's own HIP stream (void* hipStream_t). */
 void *inccl_comm_stream(struct inccl_communicator *comm);
 int inccl_comm_barrier(struct inccl_communicator *comm);
+/* Exchange engine of a multi-process communicator for inccl_allreduce_f32:
+ *   "rccl"  quant+sum -> ncclReduceScatter(int32) -> dequant -> ncclAllGather (default)
+ *   "p2p"   library buffers shared via HIP IPC; each GPU pulls its shard from every
+ *           peer over xGMI with the fused sum+dequantise kernel, then pulls every
+ *           peer's result shard (two group barriers per call)
+ * Every rank must select the same engine.  $INCCL_ENGINE sets it at creation. */
+int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name);
+const char *inccl_comm_engine(const struct inccl_communicator *comm);
 
 /* Device-resident fp32 allreduce of R local buckets per rank:
  *   dst = dequant( sum over ranks, sum over r<R  quant(srcs[r]) )
