@@ -19,10 +19,11 @@
 //
 // Layout: each lane moves 16 B per access (global_load_dwordx4 = one 1 KiB
 // wave-instruction = exactly one reference packet payload of 256 lanes,
-// nts.c:55).  A workgroup of 256 lanes owns a tile of 256*U float4 per input and
-// issues all R*U loads before touching them (R*U*16 B in flight per lane), then
-// writes U nontemporal float4 stores.  One workgroup per tile by default (a
-// grid-stride loop covers a capped grid).
+// nts.c:55).  A workgroup of BLOCK lanes owns a tile of BLOCK*U float4 per
+// input and issues all R*U loads before touching them, then writes U
+// nontemporal float4 stores; BLOCK/U per R come from a measured sweep
+// (Geometry<R> in inccl_stream.h: U = 1, BLOCK = 512 or 1024).  One workgroup
+// per tile by default (a grid-stride loop covers a capped grid).
 //
 // The horizontal reductions (absmax for automatic scaling, the position
 // weighted checksum) use wave64 __shfl_xor trees, an LDS stage across the
@@ -31,148 +32,11 @@
 #include <stdint.h>
 
 #include "inccl_kernels.h"
+#include "inccl_stream.h"
 
 namespace {
 
-constexpr int kBlock = 256;
-constexpr int kMaxR = INCCL_MAX_LOCAL_INPUTS;
-
-enum Kind { F32 = 0, Q32 = 1, Q32BE = 2 };
-
-struct SrcPtrs {
-    const void* p[kMaxR];
-};
-
-// Quantiser scale source: a static exponent, or the absmax word written by
-// k_absmax (auto scaling, spec = orc_choose_scale).
-struct Scale {
-    int k;
-    const uint32_t* amax_bits;  // nullptr -> use k
-    int scale_R;                // contributors for auto scale
-};
-
-__device__ __forceinline__ float pow2f(int k) { return __uint_as_float((uint32_t)(k + 127) << 23); }
-
-// Same arithmetic as orc_choose_scale (oracle/inccl_oracle.c).
-__device__ __forceinline__ int choose_scale(float amax, int R)
-{
-    if (!(amax > 0.0f)) return INCCL_SCALE_MAX;
-    if (__builtin_isinf(amax)) return INCCL_SCALE_MIN;
-    double t = (double)amax * (double)R;
-    int e;
-    double m = frexp(t, &e);
-    int k = (m == 0.5) ? (31 - e) : (30 - e);
-    k = k < INCCL_SCALE_MIN ? INCCL_SCALE_MIN : k;
-    k = k > INCCL_SCALE_MAX ? INCCL_SCALE_MAX : k;
-    return k;
-}
-
-__device__ __forceinline__ int resolve_k(const Scale& s)
-{
-    if (s.amax_bits == nullptr) return s.k;
-    const uint32_t bits = __builtin_nontemporal_load(s.amax_bits);
-    return choose_scale(__uint_as_float(bits), s.scale_R);
-}
-
-// q = sat_i32(rne(x * 2^k)), NaN -> 0  (orc_quantise_one)
-__device__ __forceinline__ uint32_t quant1(float x, float scale)
-{
-    float y = x * scale;
-    y = (y != y) ? 0.0f : y;
-    y = __builtin_rintf(y);
-    int32_t q = (y >= 2147483648.0f) ? INT32_MAX : ((y <= -2147483648.0f) ? INT32_MIN : (int32_t)y);
-    return (uint32_t)q;
-}
-
-template <int IN>
-__device__ __forceinline__ uint32_t load_xform(uint32_t raw, float scale)
-{
-    if constexpr (IN == F32) return quant1(__uint_as_float(raw), scale);
-    else if constexpr (IN == Q32BE) return __builtin_bswap32(raw);
-    else return raw;
-}
-
-template <int OUT>
-__device__ __forceinline__ uint32_t store_xform(uint32_t acc, float inv)
-{
-    if constexpr (OUT == F32) return __float_as_uint((float)(int32_t)acc * inv);
-    else if constexpr (OUT == Q32BE) return __builtin_bswap32(acc);
-    else return acc;
-}
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// Loads per lane per input in one tile; keeps R*U*16 B in flight per lane.
-template <int R>
-struct Unroll {
-    static constexpr int U = (R >= 8) ? 1 : ((R >= 4) ? 2 : ((R >= 2) ? 4 : 8));
-};
-
-template <int IN, int OUT, int R, bool NT>
-__global__ __launch_bounds__(kBlock) void k_stream_vec(SrcPtrs src, void* __restrict__ dst, int64_t n4,
-                                                       Scale sc)
-{
-    constexpr int U = Unroll<R>::U;
-    const int k = resolve_k(sc);
-    const float scale = pow2f(k);
-    const float inv = pow2f(-k);
-    const int64_t tile_elems = (int64_t)kBlock * U;
-    const int64_t stride = (int64_t)gridDim.x * tile_elems;
-    u32x4* __restrict__ out = reinterpret_cast<u32x4*>(dst);
-
-    for (int64_t base = (int64_t)blockIdx.x * tile_elems; base < n4; base += stride) {
-        const int64_t i0 = base + threadIdx.x;
-        if (base + tile_elems <= n4) {
-            u32x4 v[R][U];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const u32x4* p = reinterpret_cast<const u32x4*>(src.p[r]) + i0 + (int64_t)u * kBlock;
-                    v[r][u] = NT ? __builtin_nontemporal_load(p) : *p;
-                }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                u32x4 acc = {0u, 0u, 0u, 0u};
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    acc.x += load_xform<IN>(v[r][u].x, scale);
-                    acc.y += load_xform<IN>(v[r][u].y, scale);
-                    acc.z += load_xform<IN>(v[r][u].z, scale);
-                    acc.w += load_xform<IN>(v[r][u].w, scale);
-                }
-                u32x4 o;
-                o.x = store_xform<OUT>(acc.x, inv);
-                o.y = store_xform<OUT>(acc.y, inv);
-                o.z = store_xform<OUT>(acc.z, inv);
-                o.w = store_xform<OUT>(acc.w, inv);
-                __builtin_nontemporal_store(o, out + i0 + (int64_t)u * kBlock);
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t i = i0 + (int64_t)u * kBlock;
-                if (i < n4) {
-                    u32x4 acc = {0u, 0u, 0u, 0u};
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const u32x4 x = reinterpret_cast<const u32x4*>(src.p[r])[i];
-                        acc.x += load_xform<IN>(x.x, scale);
-                        acc.y += load_xform<IN>(x.y, scale);
-                        acc.z += load_xform<IN>(x.z, scale);
-                        acc.w += load_xform<IN>(x.w, scale);
-                    }
-                    u32x4 o;
-                    o.x = store_xform<OUT>(acc.x, inv);
-                    o.y = store_xform<OUT>(acc.y, inv);
-                    o.z = store_xform<OUT>(acc.z, inv);
-                    o.w = store_xform<OUT>(acc.w, inv);
-                    out[i] = o;
-                }
-            }
-        }
-    }
-}
+using namespace inccl_dev;
 
 // Element-granular variant: the scalar tail after the float4 body, and the whole
 // range when any pointer is not 16-B aligned.
@@ -351,16 +215,17 @@ int launch_stream_R(const SrcPtrs& s, void* dst, int64_t n, const Scale& sc, hip
     if (vec) {
         const int64_t n4 = n >> 2;
         if (n4 > 0) {
-            constexpr int U = Unroll<R>::U;
-            const int64_t tiles = (n4 + (int64_t)kBlock * U - 1) / ((int64_t)kBlock * U);
+            constexpr int U = Geometry<R>::U;
+            constexpr int B = Geometry<R>::BLOCK;
+            const int64_t tiles = (n4 + (int64_t)B * U - 1) / ((int64_t)B * U);
             // One workgroup per tile by default (measured on MI355X, 2 x 256 MiB
             // fused: one-shot 6.51 TB/s vs 6.23 TB/s for a 16-per-CU grid-stride cap).
             const int64_t cap = g_grid_cap > 0 ? g_grid_cap : (int64_t)0x7fffffff;
             const int grid = (int)(tiles < cap ? tiles : cap);
             if (g_nt_loads)
-                hipLaunchKernelGGL((k_stream_vec<IN, OUT, R, true>), dim3(grid), dim3(kBlock), 0, st, s, dst, n4, sc);
+                hipLaunchKernelGGL((k_stream_vec<IN, OUT, R, true, B, U>), dim3(grid), dim3(B), 0, st, s, dst, n4, sc);
             else
-                hipLaunchKernelGGL((k_stream_vec<IN, OUT, R, false>), dim3(grid), dim3(kBlock), 0, st, s, dst, n4, sc);
+                hipLaunchKernelGGL((k_stream_vec<IN, OUT, R, false, B, U>), dim3(grid), dim3(B), 0, st, s, dst, n4, sc);
         }
         done = n4 << 2;
     }

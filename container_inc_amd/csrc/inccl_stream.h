@@ -1,0 +1,164 @@
+// inccl_stream.h -- device code of the generic streaming kernel (HIP, gfx950).
+// Shared by the product (inccl_kernels.hip) and the variant tuner
+// (tools/tune/tune_stream.hip), so the tuner measures exactly this code.
+// See inccl_kernels.hip for the kernel family and the layout.
+#ifndef INCCL_STREAM_H
+#define INCCL_STREAM_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "inccl_amd.h"
+
+namespace inccl_dev {
+
+constexpr int kBlock = 256;   // default workgroup size
+constexpr int kMaxR = INCCL_MAX_LOCAL_INPUTS;
+
+enum Kind { F32 = 0, Q32 = 1, Q32BE = 2 };
+
+struct SrcPtrs {
+    const void* p[kMaxR];
+};
+
+// Quantiser scale source: a static exponent, or the absmax word written by
+// k_absmax (auto scaling, spec = orc_choose_scale).
+struct Scale {
+    int k;
+    const uint32_t* amax_bits;  // nullptr -> use k
+    int scale_R;                // contributors for auto scale
+};
+
+__device__ __forceinline__ float pow2f(int k) { return __uint_as_float((uint32_t)(k + 127) << 23); }
+
+// Same arithmetic as orc_choose_scale (oracle/inccl_oracle.c).
+__device__ __forceinline__ int choose_scale(float amax, int R)
+{
+    if (!(amax > 0.0f)) return INCCL_SCALE_MAX;
+    if (__builtin_isinf(amax)) return INCCL_SCALE_MIN;
+    double t = (double)amax * (double)R;
+    int e;
+    double m = frexp(t, &e);
+    int k = (m == 0.5) ? (31 - e) : (30 - e);
+    k = k < INCCL_SCALE_MIN ? INCCL_SCALE_MIN : k;
+    k = k > INCCL_SCALE_MAX ? INCCL_SCALE_MAX : k;
+    return k;
+}
+
+__device__ __forceinline__ int resolve_k(const Scale& s)
+{
+    if (s.amax_bits == nullptr) return s.k;
+    const uint32_t bits = __builtin_nontemporal_load(s.amax_bits);
+    return choose_scale(__uint_as_float(bits), s.scale_R);
+}
+
+// q = sat_i32(rne(x * 2^k)), NaN -> 0  (orc_quantise_one)
+__device__ __forceinline__ uint32_t quant1(float x, float scale)
+{
+    float y = x * scale;
+    y = (y != y) ? 0.0f : y;
+    y = __builtin_rintf(y);
+    int32_t q = (y >= 2147483648.0f) ? INT32_MAX : ((y <= -2147483648.0f) ? INT32_MIN : (int32_t)y);
+    return (uint32_t)q;
+}
+
+template <int IN>
+__device__ __forceinline__ uint32_t load_xform(uint32_t raw, float scale)
+{
+    if constexpr (IN == F32) return quant1(__uint_as_float(raw), scale);
+    else if constexpr (IN == Q32BE) return __builtin_bswap32(raw);
+    else return raw;
+}
+
+template <int OUT>
+__device__ __forceinline__ uint32_t store_xform(uint32_t acc, float inv)
+{
+    if constexpr (OUT == F32) return __float_as_uint((float)(int32_t)acc * inv);
+    else if constexpr (OUT == Q32BE) return __builtin_bswap32(acc);
+    else return acc;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Tile geometry per fan-in R, from the variant sweep on MI355X
+// (tools/tune/tune_stream.hip -> profiles/r01_tune_stream.jsonl, 2 x 256 MiB):
+// one float4 per lane per input (U = 1) beat deeper per-lane unrolling for
+// every R (e.g. R = 2: 6.96 TB/s at 512 x 1 vs 6.47 at 256 x 4); 512-lane
+// workgroups win at R = 2..3, 1024-lane ones at R = 1 and R >= 4.
+template <int R>
+struct Unroll {
+    static constexpr int U = 1;
+};
+template <int R>
+struct Geometry {
+    static constexpr int BLOCK = (R == 2 || R == 3) ? 512 : 1024;
+    static constexpr int U = Unroll<R>::U;
+};
+
+template <int IN, int OUT, int R, bool NT, int BLOCK = kBlock, int U = Unroll<R>::U>
+__global__ __launch_bounds__(BLOCK) void k_stream_vec(SrcPtrs src, void* __restrict__ dst, int64_t n4, Scale sc)
+{
+    const int k = resolve_k(sc);
+    const float scale = pow2f(k);
+    const float inv = pow2f(-k);
+    const int64_t tile_elems = (int64_t)BLOCK * U;
+    const int64_t stride = (int64_t)gridDim.x * tile_elems;
+    u32x4* __restrict__ out = reinterpret_cast<u32x4*>(dst);
+
+    for (int64_t base = (int64_t)blockIdx.x * tile_elems; base < n4; base += stride) {
+        const int64_t i0 = base + threadIdx.x;
+        if (base + tile_elems <= n4) {
+            u32x4 v[R][U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const u32x4* p = reinterpret_cast<const u32x4*>(src.p[r]) + i0 + (int64_t)u * BLOCK;
+                    v[r][u] = NT ? __builtin_nontemporal_load(p) : *p;
+                }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    acc.x += load_xform<IN>(v[r][u].x, scale);
+                    acc.y += load_xform<IN>(v[r][u].y, scale);
+                    acc.z += load_xform<IN>(v[r][u].z, scale);
+                    acc.w += load_xform<IN>(v[r][u].w, scale);
+                }
+                u32x4 o;
+                o.x = store_xform<OUT>(acc.x, inv);
+                o.y = store_xform<OUT>(acc.y, inv);
+                o.z = store_xform<OUT>(acc.z, inv);
+                o.w = store_xform<OUT>(acc.w, inv);
+                __builtin_nontemporal_store(o, out + i0 + (int64_t)u * BLOCK);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = i0 + (int64_t)u * BLOCK;
+                if (i < n4) {
+                    u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const u32x4 x = reinterpret_cast<const u32x4*>(src.p[r])[i];
+                        acc.x += load_xform<IN>(x.x, scale);
+                        acc.y += load_xform<IN>(x.y, scale);
+                        acc.z += load_xform<IN>(x.z, scale);
+                        acc.w += load_xform<IN>(x.w, scale);
+                    }
+                    u32x4 o;
+                    o.x = store_xform<OUT>(acc.x, inv);
+                    o.y = store_xform<OUT>(acc.y, inv);
+                    o.z = store_xform<OUT>(acc.z, inv);
+                    o.w = store_xform<OUT>(acc.w, inv);
+                    out[i] = o;
+                }
+            }
+        }
+    }
+}
+
+}  // namespace inccl_dev
+
+#endif

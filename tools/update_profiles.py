@@ -1,0 +1,70 @@
+"""Copy a GPU evidence pass (tools/gpu_round_profile.sh) from gpurun_out/ into
+profiles/ (tracked): bench JSON, rocprofv3 kernel stats, PMC counter CSVs, and
+the per-launch HBM traffic summary profiles/pmc_traffic.json that bench.py reads.
+
+    python tools/update_profiles.py --round 1 [--src gpurun_out]
+
+Traffic correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE and WRITE_SIZE are in
+KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide coalesced streaming
+read, so hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+"""
+import argparse
+import csv
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = {"fused": "k_stream_vec<F32,F32,R>", "quant_sum": "k_stream_vec<F32,Q32,R>"}
+
+
+def mean_counter(path):
+    rows = [r for r in csv.DictReader(open(path)) if "k_stream_vec" in r["Kernel_Name"]]
+    vals = [float(r["Counter_Value"]) for r in rows]
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--round", type=int, required=True)
+    p.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
+    p.add_argument("--mib", type=int, default=256)
+    p.add_argument("--R", type=int, default=2)
+    a = p.parse_args()
+    tag = f"r{a.round:02d}"
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(os.path.join(prof, f"{tag}_pmc"), exist_ok=True)
+    src = a.src
+    if os.path.exists(os.path.join(src, "bench.json")):
+        shutil.copy(os.path.join(src, "bench.json"), os.path.join(prof, f"{tag}_bench_n1.json"))
+    if os.path.exists(os.path.join(src, "prof", "run_kernel_stats.csv")):
+        shutil.copy(os.path.join(src, "prof", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_bench_n1_kernel_stats.csv"))
+    traffic_path = os.path.join(prof, "pmc_traffic.json")
+    traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
+    n = a.mib * (1 << 20) // 4
+    for k, kname in KERNELS.items():
+        f_csv = os.path.join(src, f"pmc_{k}_FETCH_SIZE", "pmc_counter_collection.csv")
+        w_csv = os.path.join(src, f"pmc_{k}_WRITE_SIZE", "pmc_counter_collection.csv")
+        if not (os.path.exists(f_csv) and os.path.exists(w_csv)):
+            continue
+        f, nf = mean_counter(f_csv)
+        w, nw = mean_counter(w_csv)
+        shutil.copy(f_csv, os.path.join(prof, f"{tag}_pmc", f"{k}_fetch_size.csv"))
+        shutil.copy(w_csv, os.path.join(prof, f"{tag}_pmc", f"{k}_write_size.csv"))
+        alg = (a.R + 1) * 4 * n
+        hbm = (2 * f + w) * 1024
+        traffic[f"{kname} R={a.R} n={n}"] = {
+            "hbm_bytes_per_launch": int(round(hbm)), "fetch_size_kib_raw": f, "write_size_kib": w,
+            "launches_averaged": [nf, nw],
+            "correction": "gfx950: FETCH_SIZE counts half the bytes of a wide coalesced stream -> x2 "
+                          "(MI355X_MICROARCH.md HBM); units KiB",
+            "alg_bytes_per_launch": alg, "ratio_to_alg": round(hbm / alg, 5),
+            "command": f"rocprofv3 --pmc <FETCH_SIZE|WRITE_SIZE> --output-format csv -- python tools/kernel_probe.py "
+                       f"--kernel {k} --R {a.R} --mib {a.mib} --iters 5",
+            "round": a.round}
+    json.dump(traffic, open(traffic_path, "w"), indent=1)
+    print(json.dumps(traffic, indent=1))
+
+
+if __name__ == "__main__":
+    main()
