@@ -1,0 +1,39 @@
+/* inccl_frames.h -- C-ABI shim between switch.c and the frame kernels in
+ * inccl_frames.hip (the reference's switch dataplane on the GPU).  Internal. */
+#ifndef INCCL_FRAMES_H
+#define INCCL_FRAMES_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "inccl_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* device-side state of one root switch (pointers into one allocation) */
+typedef struct InccSwitchState {
+    int32_t *agg;        /* [slots][256]        non_termination_switch.c:55 */
+    uint32_t *arrival;   /* [slots]             nts.c:59 */
+    int32_t *degree;     /* [slots]             nts.c:60 */
+    uint32_t *reth;      /* [slots][fan_in][4]  nts.c:57 */
+    uint32_t slots;      /* power of two */
+    int fan_in;
+} InccSwitchState;
+
+typedef struct inccl_frame_template InccFrameTemplate;
+
+int inccl_k_frames_init(void);
+int inccl_k_icrc(const uint8_t *frames, size_t stride, size_t count, uint32_t *out, void *stream);
+int inccl_k_switch_ingress(const InccSwitchState *s, const uint8_t *frames, size_t stride, size_t count,
+                           const int32_t *ports, int32_t *action, uint32_t *psn_out, void *stream);
+int inccl_k_switch_egress(const InccSwitchState *s, const uint8_t *in_frames, size_t in_stride, size_t count,
+                          const int32_t *ports, const int32_t *action, const uint32_t *psns,
+                          const InccFrameTemplate *tmpl, uint8_t *out, size_t out_stride, int32_t *out_len,
+                          void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,119 @@
+/* switch.c -- host side of the GPU switch dataplane (inccl_frames.hip).
+ *
+ * The reference's root switch keeps its aggregation state in globals
+ * (non_termination_switch.c:55-60) and processes one frame at a time on one
+ * CPU thread (nts.c:508-530).  Here the state lives in HBM and frames are
+ * processed in batches: one ingress launch (parse + idempotent add, nts.c:303-483),
+ * one egress launch (frame build + ICRC, util.c:331-442) and one recycle launch
+ * (clear_state_data(psn + window), nts.c:235-242, :367).  A batch must span
+ * fewer than slots/2 PSNs -- the reference's window of 8 packets over 16 slots
+ * (nts.c:21-22) has the same ratio. */
+#define _GNU_SOURCE
+#include <stdlib.h>
+#include <string.h>
+
+#include "inccl_frames.h"
+#include "inccl_internal.h"
+
+struct inccl_switch {
+    InccSwitchState st;
+    void *mem;
+    size_t bytes;
+    int device;
+};
+
+static int kerr2(int rc, const char *what)
+{
+    if (rc == 0) return 0;
+    if (rc == INCCL_ERR_ARG) return inccl_set_error(rc, "%s: invalid argument", what);
+    return inccl_set_error(INCCL_ERR_HIP, "%s: %s", what, hipGetErrorString((hipError_t)rc));
+}
+
+struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device)
+{
+    if (fan_in < 1 || fan_in > 31 || slots < 2 || (slots & (slots - 1)) != 0) {
+        inccl_set_error(INCCL_ERR_ARG, "switch: fan_in must be 1..31 and slots a power of two >= 2");
+        return NULL;
+    }
+    if (device >= 0 && hipSetDevice(device) != hipSuccess) {
+        inccl_set_error(INCCL_ERR_HIP, "switch: hipSetDevice(%d) failed", device);
+        return NULL;
+    }
+    struct inccl_switch *sw = (struct inccl_switch *)calloc(1, sizeof(*sw));
+    if (!sw) return NULL;
+    const size_t agg = (size_t)slots * 256 * sizeof(int32_t);
+    const size_t arr = (size_t)slots * sizeof(uint32_t);
+    const size_t deg = (size_t)slots * sizeof(int32_t);
+    const size_t reth = (size_t)slots * (size_t)fan_in * 16;
+    sw->bytes = agg + arr + deg + reth;
+    hipError_t e = hipMalloc(&sw->mem, sw->bytes);
+    if (e == hipSuccess) e = hipMemset(sw->mem, 0, sw->bytes);
+    if (e != hipSuccess) {
+        inccl_hip_check(e, "switch: hipMalloc");
+        if (sw->mem) hipFree(sw->mem);
+        free(sw);
+        return NULL;
+    }
+    char *p = (char *)sw->mem;
+    sw->st.agg = (int32_t *)p;
+    sw->st.arrival = (uint32_t *)(p + agg);
+    sw->st.degree = (int32_t *)(p + agg + arr);
+    sw->st.reth = (uint32_t *)(p + agg + arr + deg);
+    sw->st.slots = slots;
+    sw->st.fan_in = fan_in;
+    hipGetDevice(&sw->device);
+    if (kerr2(inccl_k_frames_init(), "switch: CRC tables")) {
+        hipFree(sw->mem);
+        free(sw);
+        return NULL;
+    }
+    return sw;
+}
+
+int inccl_switch_destroy(struct inccl_switch *sw)
+{
+    if (!sw) return 0;
+    hipSetDevice(sw->device);
+    hipDeviceSynchronize();
+    hipFree(sw->mem);
+    free(sw);
+    return 0;
+}
+
+int inccl_switch_reset(struct inccl_switch *sw, void *stream)
+{
+    if (!sw) return inccl_set_error(INCCL_ERR_ARG, "switch is NULL");
+    INCCL_HIP(hipMemsetAsync(sw->mem, 0, sw->bytes, (hipStream_t)stream));
+    return 0;
+}
+
+const int32_t *inccl_switch_slot(struct inccl_switch *sw, uint32_t psn)
+{
+    if (!sw) return NULL;
+    return sw->st.agg + (size_t)(psn & (sw->st.slots - 1)) * 256;
+}
+
+int inccl_switch_ingress(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
+                         const int32_t *ports_dev, int32_t *action_dev, uint32_t *psn_dev, void *stream)
+{
+    if (!sw) return inccl_set_error(INCCL_ERR_ARG, "switch is NULL");
+    return kerr2(inccl_k_switch_ingress(&sw->st, frames_dev, stride, count, ports_dev, action_dev, psn_dev, stream),
+                 "inccl_switch_ingress");
+}
+
+int inccl_switch_egress(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
+                        const int32_t *ports_dev, const int32_t *action_dev, const uint32_t *psn_dev,
+                        const struct inccl_frame_template *templates_dev, uint8_t *out_dev, size_t out_stride,
+                        int32_t *out_len_dev, void *stream)
+{
+    if (!sw) return inccl_set_error(INCCL_ERR_ARG, "switch is NULL");
+    (void)stride;
+    return kerr2(inccl_k_switch_egress(&sw->st, frames_dev, stride, count, ports_dev, action_dev, psn_dev,
+                                       templates_dev, out_dev, out_stride, out_len_dev, stream),
+                 "inccl_switch_egress");
+}
+
+int inccl_icrc_frames(const uint8_t *frames_dev, size_t stride, size_t count, uint32_t *icrc_dev, void *stream)
+{
+    return kerr2(inccl_k_icrc(frames_dev, stride, count, icrc_dev, stream), "inccl_icrc_frames");
+}

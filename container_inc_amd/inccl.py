@@ -342,3 +342,74 @@ def inccl_allreduce_write(comm: Communicator, src_data: np.ndarray, length: int,
 
 def inccl_allreduce_sendrecv(comm: Communicator, src_data: np.ndarray, length: int, dst_data: np.ndarray) -> None:
     comm.allreduce_sendrecv(src_data, length, dst_data)
+
+
+# ---------------------------------------------------------------------------
+# the reference switch's dataplane on the GPU (non_termination_switch.c:303-501,
+# util.c:331-442); frames are rows of a uint8 CUDA tensor [count, stride]
+# ---------------------------------------------------------------------------
+SW_IGNORED, SW_ABSORBED, SW_COMPLETED, SW_DROPPED, SW_REPLAY, SW_ACK, SW_INVALID = range(7)
+FRAME_TEMPLATE_DTYPE = np.dtype([("src_mac", np.uint8, 6), ("dst_mac", np.uint8, 6), ("src_ip", "<u4"),
+                                 ("dst_ip", "<u4"), ("src_port", "<u2"), ("dst_port", "<u2"), ("qp", "<u4")])
+assert FRAME_TEMPLATE_DTYPE.itemsize == 28
+
+
+def _frames_arg(frames, name="frames"):
+    torch = _torch()
+    if frames.dim() != 2:
+        raise ValueError(f"{name}: expected [count, stride] uint8")
+    if frames.shape[1] % 4:
+        raise ValueError(f"{name}: stride must be a multiple of 4")
+    return _dev_ptr(frames, torch.uint8, name), frames.shape[0], frames.shape[1]
+
+
+def icrc_frames(frames, stream=None):
+    """ICRC (util.c:250-286) of every frame row; returns an int32 tensor of the uint32 values."""
+    torch = _torch()
+    ptr, count, stride = _frames_arg(frames)
+    out = torch.empty(count, dtype=torch.int32, device=frames.device)
+    check(load().inccl_icrc_frames(ptr, stride, count, _dev_ptr(out, torch.int32, "out"), _stream_handle(stream)),
+          "inccl_icrc_frames")
+    return out
+
+
+class GpuSwitch:
+    """A root switch (fan_in children) whose state and dataplane live on the GPU."""
+
+    def __init__(self, fan_in: int, slots: int = 1024, device: int = -1):
+        self.fan_in = int(fan_in)
+        self.handle = load().inccl_switch_create(self.fan_in, int(slots), int(device))
+        if not self.handle:
+            raise IncclError(load().inccl_last_error().decode(errors="replace"))
+
+    def reset(self, stream=None):
+        check(load().inccl_switch_reset(self.handle, _stream_handle(stream)), "inccl_switch_reset")
+
+    def ingress(self, frames, ports, stream=None):
+        torch = _torch()
+        ptr, count, stride = _frames_arg(frames)
+        pp = _dev_ptr(ports, torch.int32, "ports", count)
+        action = torch.empty(count, dtype=torch.int32, device=frames.device)
+        psn = torch.empty(count, dtype=torch.int32, device=frames.device)
+        check(load().inccl_switch_ingress(self.handle, ptr, stride, count, pp, action.data_ptr(), psn.data_ptr(),
+                                          _stream_handle(stream)), "inccl_switch_ingress")
+        return action, psn
+
+    def egress(self, frames, ports, action, psn, templates, out_stride: int = 1152, stream=None):
+        torch = _torch()
+        ptr, count, stride = _frames_arg(frames)
+        if templates.dtype != torch.uint8 or templates.numel() != 28 * self.fan_in:
+            raise ValueError("templates: fan_in x 28-byte inccl_frame_template records (uint8)")
+        out = torch.zeros((count * self.fan_in, out_stride), dtype=torch.uint8, device=frames.device)
+        out_len = torch.empty(count * self.fan_in, dtype=torch.int32, device=frames.device)
+        check(load().inccl_switch_egress(self.handle, ptr, stride, count, _dev_ptr(ports, torch.int32, "ports", count),
+                                         _dev_ptr(action, torch.int32, "action", count),
+                                         _dev_ptr(psn, torch.int32, "psn", count),
+                                         _dev_ptr(templates, torch.uint8, "templates"), out.data_ptr(), out_stride,
+                                         out_len.data_ptr(), _stream_handle(stream)), "inccl_switch_egress")
+        return out, out_len
+
+    def destroy(self):
+        if self.handle:
+            load().inccl_switch_destroy(self.handle)
+            self.handle = None

@@ -145,6 +145,53 @@ int inccl_allreduce_q32(struct inccl_communicator *comm, const int32_t *src_dev,
 int inccl_allreduce_f32_host(struct inccl_communicator *comm, const float *src_host, float *dst_host, size_t n,
                              int scale_exp, size_t bucket_bytes);
 
+/* ---------- the reference switch's dataplane on the GPU ----------
+ * non_termination_switch.c:303-501 (parse, per-PSN first-arrival aggregation,
+ * broadcast / replay) and util.c:331-442 (egress frame build, payload htonl,
+ * RoCE ICRC), batched: a batch of ingress frames -> one ingress launch -> one
+ * egress launch.  Frames live in device memory at a fixed `stride` (multiple of
+ * 4 B).  Within one batch the arrival order is not defined: first arrivals of a
+ * (psn, port) pair are added once, later copies are DROPPED (slot incomplete
+ * before the batch) or REPLAYed (slot completed in an earlier batch).  A batch
+ * must span fewer than slots/2 PSNs (the reference: window 8 of 16 slots). */
+#define INCCL_SW_IGNORED 0    /* opcode the switch does not handle             */
+#define INCCL_SW_ABSORBED 1   /* first arrival, slot not complete (nts.c:359-363) */
+#define INCCL_SW_COMPLETED 2  /* first arrival completing the slot: broadcast (nts.c:365-372) */
+#define INCCL_SW_DROPPED 3    /* retransmit into an incomplete slot (nts.c:353) */
+#define INCCL_SW_REPLAY 4     /* retransmit of a completed slot: resend to its port (nts.c:354-356) */
+#define INCCL_SW_ACK 5        /* UP ACK: reflected by the host (nts.c:403-406) */
+#define INCCL_SW_INVALID 6    /* bad port or payload length (nts.c:350) */
+
+/* One child connection (the fields of util.h connection_t that egress uses). */
+struct inccl_frame_template {
+    uint8_t src_mac[6], dst_mac[6];
+    uint32_t src_ip, dst_ip;        /* as stored in the IP header */
+    uint16_t src_port, dst_port;    /* host order (util.c:368-370) */
+    uint32_t qp;                    /* peer QPN (util.c:384) */
+};
+struct inccl_switch;
+
+/* fan_in children (1..31), `slots` PSN slots (power of two), on `device` (-1 = current). */
+struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device);
+int inccl_switch_destroy(struct inccl_switch *sw);
+int inccl_switch_reset(struct inccl_switch *sw, void *stream);
+/* device pointer of the 256-lane aggregator slot of `psn` */
+const int32_t *inccl_switch_slot(struct inccl_switch *sw, uint32_t psn);
+/* ports_dev[i] = ingress port of frame i.  Writes action_dev[i] (INCCL_SW_*) and psn_dev[i]. */
+int inccl_switch_ingress(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
+                         const int32_t *ports_dev, int32_t *action_dev, uint32_t *psn_dev, void *stream);
+/* For every COMPLETED frame i: fan_in egress frames to children c at
+ * out_dev[(i*fan_in + c) * out_stride]; for every REPLAY frame: one frame to
+ * its port.  out_len_dev[i*fan_in + c] = frame bytes or 0.  Then recycles
+ * slot psn + slots/2 of every completed psn (nts.c:367).  templates_dev holds
+ * fan_in inccl_frame_template records (device memory). */
+int inccl_switch_egress(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
+                        const int32_t *ports_dev, const int32_t *action_dev, const uint32_t *psn_dev,
+                        const struct inccl_frame_template *templates_dev, uint8_t *out_dev, size_t out_stride,
+                        int32_t *out_len_dev, void *stream);
+/* RoCE ICRC (util.c:250-286) of `count` frames: icrc_dev[i] as the frame would store it (host order). */
+int inccl_icrc_frames(const uint8_t *frames_dev, size_t stride, size_t count, uint32_t *icrc_dev, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

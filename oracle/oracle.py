@@ -184,9 +184,13 @@ class FrameHdr(ctypes.Structure):
 
 def build_data_frame(payload_host: np.ndarray, psn: int, opcode: int, qp: int = 0x11,
                      with_reth: bool = False, reth: bytes | None = None,
-                     src_ip: int = 0, dst_ip: int = 0, src_port: int = 4791, dst_port: int = 4791) -> bytes:
+                     src_ip: int = 0, dst_ip: int = 0, src_port: int = 4791, dst_port: int = 4791,
+                     src_mac: bytes = bytes(6), dst_mac: bytes = bytes(6)) -> bytes:
     payload_host = np.ascontiguousarray(payload_host, dtype=np.int32)
     h = FrameHdr()
+    for i in range(6):
+        h.src_mac[i] = src_mac[i]
+        h.dst_mac[i] = dst_mac[i]
     h.src_ip, h.dst_ip, h.src_port, h.dst_port = src_ip, dst_ip, src_port, dst_port
     h.qp, h.psn, h.opcode = qp, psn, opcode
     frame = np.zeros(4096 + 128, np.uint8)

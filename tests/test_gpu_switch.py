@@ -1,0 +1,154 @@
+"""The reference switch's dataplane on the GPU vs the oracle (gpu): RoCE ICRC
+(util.c:250-286) against the captured frame of test.c and oracle-built frames;
+batched ingress (non_termination_switch.c:303-483: first-arrival add,
+retransmit drop / replay) and egress frames (util.c:331-442) byte-exact."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+STRIDE = 1152
+INT32_MIN, INT32_MAX = -(2 ** 31), 2 ** 31 - 1
+
+
+def _rows(frames, dev):
+    import torch
+    a = np.zeros((len(frames), STRIDE), np.uint8)
+    for i, f in enumerate(frames):
+        a[i, : len(f)] = np.frombuffer(f, np.uint8)
+    return torch.from_numpy(a).to(dev)
+
+
+def test_icrc_golden_frame(gpu):
+    from container_inc_amd import inccl
+    g = json.load(open(os.path.join(GOLDEN, "icrc_test_c.json")))
+    got = inccl.icrc_frames(_rows([bytes.fromhex(g["frame_hex"])], gpu)).cpu().numpy().view(np.uint32)
+    assert int(got[0]) == g["icrc_u32"]
+
+
+def test_icrc_random_frames(gpu, orc):
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(21)
+    frames = []
+    for i in range(300):
+        payload = rng.integers(INT32_MIN, INT32_MAX, 256, dtype=np.int64, endpoint=True).astype(np.int32)
+        wf = bool(i % 3 == 0)
+        frames.append(orc.build_data_frame(payload, psn=int(rng.integers(0, 1 << 24)), opcode=0x06 if wf else 0x07,
+                                           qp=int(rng.integers(0, 1 << 24)), with_reth=wf,
+                                           reth=rng.integers(0, 256, 16, dtype=np.uint8).tobytes() if wf else None,
+                                           src_ip=int(rng.integers(0, 1 << 32)), dst_ip=int(rng.integers(0, 1 << 32)),
+                                           src_port=int(rng.integers(0, 65536)), dst_port=4791))
+    got = inccl.icrc_frames(_rows(frames, gpu)).cpu().numpy().view(np.uint32)
+    for f, c in zip(frames, got):
+        assert int(c) == orc.icrc(f) == int.from_bytes(f[-4:], "little")
+
+
+def _templates(fan_in):
+    from container_inc_amd.inccl import FRAME_TEMPLATE_DTYPE
+    t = np.zeros(fan_in, FRAME_TEMPLATE_DTYPE)
+    for c in range(fan_in):
+        t[c]["src_mac"] = [0x52, 0x54, 0, 0xAA, 0, c]
+        t[c]["dst_mac"] = [0x52, 0x54, 0, 0xBB, 1, c]
+        t[c]["src_ip"] = 0x0132320A + (c << 24)
+        t[c]["dst_ip"] = 0x0232320A + (c << 24)
+        t[c]["src_port"] = 4791
+        t[c]["dst_port"] = 4791 + c
+        t[c]["qp"] = 0x100 + c
+    return t
+
+
+def _expected_frame(orc, t, c, agg, psn, op, reth):
+    wf = op in (0x06, 0x0A)
+    return orc.build_data_frame(agg, psn=psn, opcode=op, qp=int(t[c]["qp"]), with_reth=wf,
+                                reth=reth if wf else None, src_ip=int(t[c]["src_ip"]), dst_ip=int(t[c]["dst_ip"]),
+                                src_port=int(t[c]["src_port"]), dst_port=int(t[c]["dst_port"]),
+                                src_mac=bytes(t[c]["src_mac"]), dst_mac=bytes(t[c]["dst_mac"]))
+
+
+@pytest.mark.parametrize("fan_in", [2, 3, 8])
+def test_switch_batches(gpu, orc, fan_in):
+    import torch
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(100 + fan_in)
+    slots, per_batch, batches = 64, 8, 5
+    sw = inccl.GpuSwitch(fan_in, slots)
+    tmpl = _templates(fan_in)
+    tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
+    payload, reth, opcode = {}, {}, {}
+    completed = set()
+    for b in range(batches):
+        psns = list(range(b * per_batch, (b + 1) * per_batch))
+        frames, ports, keys = [], [], []
+        for p in psns:
+            opcode[p] = [0x06, 0x07, 0x07, 0x08][p % 4]
+            for port in range(fan_in):
+                payload[(p, port)] = rng.integers(INT32_MIN, INT32_MAX, 256, dtype=np.int64, endpoint=True).astype(np.int32)
+                reth[(p, port)] = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+                keys.append((p, port))
+        # retransmits: some of this batch's frames twice, and some of the previous batch's
+        dups = [keys[i] for i in rng.choice(len(keys), size=len(keys) // 4, replace=False)]
+        old = [(p, port) for (p, port) in payload if p < b * per_batch and p >= (b - 1) * per_batch]
+        olds = [old[i] for i in rng.choice(len(old), size=min(3, len(old)), replace=False)] if old else []
+        order = keys + dups + olds
+        perm = rng.permutation(len(order))
+        order = [order[i] for i in perm]
+        for (p, port) in order:
+            wf = opcode[p] in (0x06, 0x0A)
+            frames.append(orc.build_data_frame(payload[(p, port)], psn=p, opcode=opcode[p], qp=0x11, with_reth=wf,
+                                               reth=reth[(p, port)] if wf else None, src_ip=0x0A000001 + port))
+            ports.append(port)
+        fr = _rows(frames, gpu)
+        pt = torch.tensor(ports, dtype=torch.int32, device=gpu)
+        action, psn_out = sw.ingress(fr, pt)
+        out, out_len = sw.egress(fr, pt, action, psn_out, tmpl_dev)
+        torch.cuda.synchronize()
+        action, psn_out = action.cpu().numpy(), psn_out.cpu().numpy()
+        out, out_len = out.cpu().numpy(), out_len.cpu().numpy()
+        # which copy of a (psn, port) pair arrives first inside a batch is not
+        # defined: exactly one copy is added, the others are DROPPED; copies of a
+        # pair whose slot completed in an EARLIER batch are REPLAYed (nts.c:353-357)
+        groups = {}
+        for i, (p, port) in enumerate(order):
+            assert psn_out[i] == p
+            groups.setdefault((p, port), []).append(int(action[i]))
+        n_completed = {}
+        for (p, port), acts in groups.items():
+            if p in completed:
+                assert acts == [inccl.SW_REPLAY] * len(acts), (p, port, acts)
+                continue
+            firsts = [a for a in acts if a in (inccl.SW_ABSORBED, inccl.SW_COMPLETED)]
+            assert len(firsts) == 1 and acts.count(inccl.SW_DROPPED) == len(acts) - 1, (p, port, acts)
+            if firsts[0] == inccl.SW_COMPLETED:
+                n_completed[p] = n_completed.get(p, 0) + 1
+        assert all(n_completed.get(p, 0) == 1 for p in psns), n_completed
+        for i, (p, port) in enumerate(order):
+            agg = orc.sum_q32([payload[(p, c)] for c in range(fan_in)])
+            for c in range(fan_in):
+                row = i * fan_in + c
+                if action[i] == inccl.SW_COMPLETED or (action[i] == inccl.SW_REPLAY and c == port):
+                    want = _expected_frame(orc, tmpl, c, agg, p, opcode[p], reth[(p, c)])
+                    assert out_len[row] == len(want), (i, c)
+                    assert bytes(out[row, : len(want)]) == want, (i, c)
+                else:
+                    assert out_len[row] == 0
+        completed |= set(psns)
+    sw.destroy()
+
+
+def test_switch_rejects_bad_frames(gpu, orc):
+    import torch
+    from container_inc_amd import inccl
+    sw = inccl.GpuSwitch(2, 16)
+    good = orc.build_data_frame(np.ones(256, np.int32), psn=3, opcode=0x07)
+    short = orc.build_data_frame(np.ones(100, np.int32), psn=4, opcode=0x07)   # payload != 1024 B (nts.c:350)
+    ack = bytearray(good[:62])
+    ack[42] = 0x11
+    frames = _rows([good, short, bytes(ack), good], gpu)
+    ports = torch.tensor([0, 1, 0, 5], dtype=torch.int32, device=gpu)
+    action, _ = sw.ingress(frames, ports)
+    assert action.cpu().tolist() == [inccl.SW_ABSORBED, inccl.SW_INVALID, inccl.SW_ACK, inccl.SW_INVALID]
+    sw.destroy()
