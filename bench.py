@@ -74,6 +74,71 @@ def cpu_baseline(n_elems: int, R: int, k: int, seconds: float) -> dict:
                       f"(oracle/inccl_oracle.c orc_reduce_f32, 1 thread, {dt:.1f} s)"}
 
 
+def cpu_baseline_allcores(n_elems: int, R: int, k: int, seconds: float) -> dict:
+    """The same restatement on every host core: threads over disjoint 1 Mi-element
+    chunks of the sample (ctypes releases the GIL inside the C loop)."""
+    import threading
+
+    import numpy as np
+
+    from oracle import oracle as O
+    # the GPU box exposes the whole machine's CPUs; our share is $OMP_NUM_THREADS (16)
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 64))
+    m = min(n_elems, 1 << 24)
+    rng = np.random.default_rng(1000)
+    xs = [rng.standard_normal(m).astype(np.float32) for _ in range(R)]
+    out = np.empty(m, np.float32)
+    chunk = 1 << 20
+    jobs = [(o, min(m, o + chunk)) for o in range(0, m, chunk)]
+    L = O.lib()
+
+    def worker(tid, stop_at, counter):
+        while time.perf_counter() < stop_at:
+            for j in range(tid, len(jobs), cores):
+                lo, hi = jobs[j]
+                srcs = (O.ctypes.c_void_p * R)(*[x[lo:hi].ctypes.data for x in xs])
+                L.orc_reduce_f32(srcs, R, out[lo:hi].ctypes.data, hi - lo, k)
+                counter[tid] += hi - lo
+
+    counter = [0] * cores
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=worker, args=(t, t0 + seconds, counter)) for t in range(cores)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    dt = time.perf_counter() - t0
+    return {"value": round(sum(counter) * R * 4 / dt / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": "port",
+            "sample": f"orc_reduce_f32 over 1 Mi-element chunks of R={R} x {m * 4 >> 20} MiB buckets on {cores} "
+                      f"threads for {dt:.1f} s"}
+
+
+def cpu_reference_pipeline(seconds: float) -> dict:
+    """The reference's own per-element CPU path restated end to end, int32:
+    encode (api.c:300-302) -> root switch add per 1 KiB packet (nts.c:361-363) ->
+    egress frame build + ICRC per child (util.c:331-442) -> decode (api.c:428-430),
+    two ranks in one thread (oracle orc_allreduce_write_loopback with framing)."""
+    import numpy as np
+
+    from oracle import oracle as O
+    m = 1 << 20   # 4 MiB bucket per rank (BASELINE config 1)
+    rng = np.random.default_rng(1)
+    xs = [rng.integers(-2 ** 31, 2 ** 31 - 1, m, dtype=np.int64).astype(np.int32) for _ in range(2)]
+    t0 = time.perf_counter()
+    iters = 0
+    while True:
+        rc, _, _ = O.allreduce_write_loopback(xs, with_icrc=True)
+        assert rc == m // 1024
+        iters += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(iters * m * 4 / dt / 1e9, 4), "unit": "GB/s of one rank's int32 bucket", "cores": 1,
+            "kind": "port", "sample": f"{iters} x loopback inccl_allreduce_write of 2 ranks x 4 MiB int32 with "
+                                      f"switch aggregation and ICRC framing, {dt:.1f} s"}
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
     PMC summary (profiles/pmc_traffic.json), or None."""
@@ -277,6 +342,8 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(n, R, k, a.cpu_seconds)
+        res["cpu_baseline_allcores"] = cpu_baseline_allcores(n, R, k, min(a.cpu_seconds, 5.0))
+        res["cpu_reference_pipeline"] = cpu_reference_pipeline(min(a.cpu_seconds, 5.0))
     if rank == 0:
         line = json.dumps(res)
         print(line, flush=True)
