@@ -31,19 +31,22 @@ constexpr int kWin = 1088;            // 64 lanes x 17 bytes
 constexpr int kSeg = 17;
 constexpr int kFrameMax = 1152;       // staged frame bytes (>= 1098)
 constexpr int kWavesPerBlock = 4;
+constexpr int kEgressWaves = 8;       // 512-lane blocks, CU-sized persistent grid
 constexpr int kLanes = 256;           // int32 lanes per packet (nts.c:55)
 
-__device__ uint32_t g_crc_tab[256];
+__device__ uint32_t g_crc_tab[4][256];       // slice-by-4 tables (util.c:141-159 derives 8)
 __device__ uint32_t g_shift_tab[6][4][256];
 
 struct CrcLds {
-    uint32_t tab[256];
+    uint32_t tab[4][256];
     uint32_t sh[6][4][256];
 };
 
 __device__ __forceinline__ void load_tables(CrcLds& t)
 {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) t.tab[i] = g_crc_tab[i];
+    uint32_t* d0 = &t.tab[0][0];
+    const uint32_t* s0 = &g_crc_tab[0][0];
+    for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) d0[i] = s0[i];
     uint32_t* dst = &t.sh[0][0][0];
     const uint32_t* src = &g_shift_tab[0][0][0];
     for (int i = threadIdx.x; i < 6 * 4 * 256; i += blockDim.x) dst[i] = src[i];
@@ -62,27 +65,31 @@ __device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds& t, int lane)
     const int ip_total = ((int)fr[16] << 8) | fr[17];
     const int L = ip_total;                       // 4 (init) + ip_total - 4 (no ICRC)
     const int lead = kWin - L;                    // zero bytes before the message
-    uint32_t c = 0;
+    uint8_t b[kSeg];
 #pragma unroll
     for (int j = 0; j < kSeg; ++j) {
-        const int w = lane * kSeg + j;
-        const int m = w - lead;
-        uint8_t b = 0;
-        if (m >= 0) b = (m < 4) ? (uint8_t)0xFF : frame_byte(fr, 14 + m - 4);
-        c = (c >> 8) ^ t.tab[(c ^ b) & 0xFFu];
+        const int m = lane * kSeg + j - lead;
+        b[j] = (m < 0) ? (uint8_t)0 : ((m < 4) ? (uint8_t)0xFF : frame_byte(fr, 14 + m - 4));
     }
+    // slice-by-4 over bytes 0..15, then byte 16: a 5-step dependent chain
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+        c ^= (uint32_t)b[j] | ((uint32_t)b[j + 1] << 8) | ((uint32_t)b[j + 2] << 16) | ((uint32_t)b[j + 3] << 24);
+        c = t.tab[3][c & 0xFF] ^ t.tab[2][(c >> 8) & 0xFF] ^ t.tab[1][(c >> 16) & 0xFF] ^ t.tab[0][c >> 24];
+    }
+    c = (c >> 8) ^ t.tab[0][(c ^ b[16]) & 0xFFu];
+    // tree: at level l the block of lane L (low l bits zero) absorbs block L + 2^l:
+    // crc = shift(crc_left, |right| = 17 * 2^l bytes) ^ crc_right.  Only left lanes
+    // (the block representatives) are updated; lane 0 ends with the whole window.
 #pragma unroll
     for (int l = 0; l < 6; ++l) {
         const uint32_t other = (uint32_t)__shfl_xor((int)c, 1 << l, kWave);
-        const bool left = ((lane >> l) & 1) == 0;
-        const uint32_t mine_shifted =
+        const uint32_t shifted =
             t.sh[l][0][c & 0xFF] ^ t.sh[l][1][(c >> 8) & 0xFF] ^ t.sh[l][2][(c >> 16) & 0xFF] ^ t.sh[l][3][c >> 24];
-        const uint32_t other_shifted = t.sh[l][0][other & 0xFF] ^ t.sh[l][1][(other >> 8) & 0xFF] ^
-                                       t.sh[l][2][(other >> 16) & 0xFF] ^ t.sh[l][3][other >> 24];
-        // block [left | right]: crc = shift(crc_left, |right|) ^ crc_right
-        c = left ? (mine_shifted ^ other) : (other_shifted ^ c);
+        c = shifted ^ other;   // meaningful in left lanes only
     }
-    return ~c;
+    return ~(uint32_t)__shfl((int)c, 0, kWave);
 }
 
 // stage `bytes` of a global frame into LDS (dword loads; frames are 4-B aligned)
@@ -176,9 +183,11 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress(InccSwitchSta
                         (uint32_t)r[2 * lane] | ((uint32_t)r[2 * lane + 1] << 16);
                 }
                 int32_t* agg = s.agg + (size_t)slot * kLanes;
+                // word i = j*64 + lane: each wave-instruction adds 256 contiguous
+                // bytes (the full-rate atomic shape, MI355X_MICROARCH.md atomics)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {                    // nts.c:361-363 / :443-445
-                    const int i = lane * 4 + j;
+                    const int i = j * kWave + lane;
                     const uint32_t raw = (uint32_t)d16[2 * i] | ((uint32_t)d16[2 * i + 1] << 16);
                     atomicAdd(&agg[i], (int32_t)__builtin_bswap32(raw));
                 }
@@ -199,11 +208,49 @@ __device__ __forceinline__ void put16(uint8_t* p, uint32_t v)
     p[1] = (uint8_t)v;
 }
 
+// Header image of child c's egress frames (util.c:348-388) with opcode and PSN
+// left zero: identical for every frame of that child and RETH flag, so each
+// block builds the 2*fan_in images once into LDS and frames copy them word-wise.
+constexpr int kHdrImg = 72;   // 70 header bytes (with RETH slot) rounded to dwords
+
+__device__ void build_header_image(uint8_t* fr, const InccFrameTemplate& h, bool wf)
+{
+    const int total = 14 + 20 + 8 + 12 + (wf ? 16 : 0) + kLanes * 4 + 4;   // util.c:341-345
+    for (int i = 0; i < kHdrImg; ++i) fr[i] = 0;
+    for (int i = 0; i < 6; ++i) {                                    // util.c:348-351
+        fr[i] = h.dst_mac[i];
+        fr[6 + i] = h.src_mac[i];
+    }
+    fr[12] = 0x08; fr[13] = 0x00;
+    uint8_t* ip = fr + 14;                                           // util.c:354-364
+    ip[0] = 0x45; ip[1] = 0x00;
+    put16(ip + 2, (uint32_t)(total - 14));
+    ip[4] = 0x11; ip[5] = 0x11;
+    put16(ip + 6, 0x4000);
+    ip[8] = 0x40; ip[9] = 0x11;
+    for (int i = 0; i < 4; ++i) {
+        ip[12 + i] = (uint8_t)(h.src_ip >> (8 * i));                 // stored as-is (network order value)
+        ip[16 + i] = (uint8_t)(h.dst_ip >> (8 * i));
+    }
+    uint32_t sum = 0;                                                // util.c:106-127
+    for (int i = 0; i < 20; i += 2) sum += ((uint32_t)ip[i] << 8) | ip[i + 1];
+    while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
+    put16(ip + 10, (~sum) & 0xFFFF);
+    uint8_t* udp = ip + 20;                                          // util.c:367-372
+    put16(udp + 0, h.src_port);
+    put16(udp + 2, h.dst_port);
+    put16(udp + 4, (uint32_t)(total - 14 - 20));
+    uint8_t* bth = udp + 8;                                          // util.c:376-388
+    bth[2] = 0xFF; bth[3] = 0xFF;
+    const uint32_t q = h.qp & 0x00FFFFFFu;
+    bth[4] = (uint8_t)(q >> 24); bth[5] = (uint8_t)(q >> 16); bth[6] = (uint8_t)(q >> 8); bth[7] = (uint8_t)q;
+}
+
 __device__ void egress_one(const InccSwitchState& s, const uint8_t* __restrict__ in_frames, int64_t in_stride,
                            const int32_t* __restrict__ ports, const int32_t* __restrict__ action,
-                           const uint32_t* __restrict__ psns, const InccFrameTemplate* __restrict__ tmpl,
-                           uint8_t* __restrict__ out, int64_t out_stride, int32_t* __restrict__ out_len,
-                           const CrcLds& t, uint8_t* frbuf, int64_t g, int lane)
+                           const uint32_t* __restrict__ psns, const uint8_t (*himg)[kHdrImg],
+                           uint8_t* __restrict__ out, int64_t out_stride, bool out16,
+                           int32_t* __restrict__ out_len, const CrcLds& t, uint8_t* frbuf, int64_t g, int lane)
 {
     const int fan = s.fan_in;
     const int64_t f = g / fan;
@@ -218,44 +265,18 @@ __device__ void egress_one(const InccSwitchState& s, const uint8_t* __restrict__
     const uint32_t slot = psn & (s.slots - 1);
     const uint8_t op = in_frames[f * in_stride + 42];
     const bool wf = is_write_first(op);
-    const int data_len = kLanes * 4;
-    const int total = 14 + 20 + 8 + 12 + (wf ? 16 : 0) + data_len + 4;   // util.c:341-345
+    const int total = 14 + 20 + 8 + 12 + (wf ? 16 : 0) + kLanes * 4 + 4;   // util.c:341-345
     uint8_t* fr = frbuf;
-    const InccFrameTemplate& h = tmpl[c];
-    if (lane == 0) {
-        for (int i = 0; i < 6; ++i) {                               // util.c:348-351
-            fr[i] = h.dst_mac[i];
-            fr[6 + i] = h.src_mac[i];
-        }
-        fr[12] = 0x08; fr[13] = 0x00;
-        uint8_t* ip = fr + 14;                                      // util.c:354-364
-        ip[0] = 0x45; ip[1] = 0x00;
-        put16(ip + 2, (uint32_t)(total - 14));
-        ip[4] = 0x11; ip[5] = 0x11;
-        put16(ip + 6, 0x4000);
-        ip[8] = 0x40; ip[9] = 0x11;
-        ip[10] = 0; ip[11] = 0;
-        for (int i = 0; i < 4; ++i) {
-            ip[12 + i] = (uint8_t)(h.src_ip >> (8 * i));            // stored as-is (network order value)
-            ip[16 + i] = (uint8_t)(h.dst_ip >> (8 * i));
-        }
-        uint32_t sum = 0;                                           // util.c:106-127
-        for (int i = 0; i < 20; i += 2) sum += ((uint32_t)ip[i] << 8) | ip[i + 1];
-        while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
-        put16(ip + 10, (~sum) & 0xFFFF);
-        uint8_t* udp = ip + 20;                                     // util.c:367-372
-        put16(udp + 0, h.src_port);
-        put16(udp + 2, h.dst_port);
-        put16(udp + 4, (uint32_t)(total - 14 - 20));
-        udp[6] = 0; udp[7] = 0;
-        uint8_t* bth = udp + 8;                                     // util.c:376-388
-        bth[0] = op; bth[1] = 0; bth[2] = 0xFF; bth[3] = 0xFF;
-        const uint32_t q = h.qp & 0x00FFFFFFu, p = psn | 0x80000000u;
-        bth[4] = (uint8_t)(q >> 24); bth[5] = (uint8_t)(q >> 16); bth[6] = (uint8_t)(q >> 8); bth[7] = (uint8_t)q;
-        bth[8] = (uint8_t)(p >> 24); bth[9] = (uint8_t)(p >> 16); bth[10] = (uint8_t)(p >> 8); bth[11] = (uint8_t)p;
+    if (lane < kHdrImg / 4)
+        reinterpret_cast<uint32_t*>(fr)[lane] = reinterpret_cast<const uint32_t*>(himg[c * 2 + (wf ? 1 : 0)])[lane];
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {                                                 // util.c:378, :386
+        const uint32_t p = psn | 0x80000000u;
+        fr[42] = op;
+        fr[50] = (uint8_t)(p >> 24); fr[51] = (uint8_t)(p >> 16); fr[52] = (uint8_t)(p >> 8); fr[53] = (uint8_t)p;
     }
     // offsets 54 / 70 are 2-byte aligned: 16-bit LDS stores
-    if (wf && lane < 4) {                                           // util.c:409-417, reth_keeper[slot][c]
+    if (wf && lane < 4) {                                            // util.c:409-417, reth_keeper[slot][c]
         const uint32_t r = s.reth[((size_t)slot * fan + c) * 4 + lane];
         uint16_t* r16 = reinterpret_cast<uint16_t*>(fr + 54);
         r16[2 * lane] = (uint16_t)r;
@@ -265,24 +286,30 @@ __device__ void egress_one(const InccSwitchState& s, const uint8_t* __restrict__
     const int32_t* agg = s.agg + (size_t)slot * kLanes;
     uint16_t* d16 = reinterpret_cast<uint16_t*>(fr + doff);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {                                   // util.c:403-405 / :419-421 htonl
-        const int i = lane * 4 + j;
+    for (int j = 0; j < 4; ++j) {                                    // util.c:403-405 / :419-421 htonl
+        const int i = j * kWave + lane;
         const uint32_t be = __builtin_bswap32((uint32_t)agg[i]);
         d16[2 * i] = (uint16_t)be;
         d16[2 * i + 1] = (uint16_t)(be >> 16);
     }
     __builtin_amdgcn_wave_barrier();
-    const uint32_t crc = icrc_wave(fr, t, lane);                   // util.c:424-426
-    if (lane == 0) {                                                // stored host order (LE)
+    const uint32_t crc = icrc_wave(fr, t, lane);                    // util.c:424-426
+    if (lane == 0) {                                                 // stored host order (LE)
         fr[total - 4] = (uint8_t)crc;
         fr[total - 3] = (uint8_t)(crc >> 8);
         fr[total - 2] = (uint8_t)(crc >> 16);
         fr[total - 1] = (uint8_t)(crc >> 24);
     }
     __builtin_amdgcn_wave_barrier();
-    uint32_t* o = reinterpret_cast<uint32_t*>(out + g * out_stride);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(fr);
-    for (int i = lane; i < (total + 3) / 4; i += kWave) o[i] = src[i];
+    uint8_t* o = out + g * out_stride;
+    if (out16) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        for (int i = lane; i < (total + 15) / 16; i += kWave)
+            reinterpret_cast<u4*>(o)[i] = reinterpret_cast<const u4*>(fr)[i];
+    } else {
+        for (int i = lane; i < (total + 3) / 4; i += kWave)
+            reinterpret_cast<uint32_t*>(o)[i] = reinterpret_cast<const uint32_t*>(fr)[i];
+    }
     if (lane == 0) out_len[g] = total;
     // the result is known from now on: later retransmits replay (nts.c:366)
     if (act == INCCL_SW_COMPLETED && c == 0 && lane == 0) atomicOr(&s.arrival[slot], 1u << fan);
@@ -291,24 +318,27 @@ __device__ void egress_one(const InccSwitchState& s, const uint8_t* __restrict__
 
 // Egress (nts.c:365-372 / :447-453 broadcast, :353-356 / :435-438 replay;
 // frames per util.c:331-442): wave (f, c) builds child c's copy of frame f.
-__global__ __launch_bounds__(kWave* kWavesPerBlock) void k_egress(InccSwitchState s, const uint8_t* __restrict__ in_frames,
-                                                                  int64_t in_stride, int64_t count,
-                                                                  const int32_t* __restrict__ ports,
-                                                                  const int32_t* __restrict__ action,
-                                                                  const uint32_t* __restrict__ psns,
-                                                                  const InccFrameTemplate* __restrict__ tmpl,
-                                                                  uint8_t* __restrict__ out, int64_t out_stride,
-                                                                  int32_t* __restrict__ out_len)
+__global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState s, const uint8_t* __restrict__ in_frames,
+                                                               int64_t in_stride, int64_t count,
+                                                               const int32_t* __restrict__ ports,
+                                                               const int32_t* __restrict__ action,
+                                                               const uint32_t* __restrict__ psns,
+                                                               const InccFrameTemplate* __restrict__ tmpl,
+                                                               uint8_t* __restrict__ out, int64_t out_stride,
+                                                               int32_t* __restrict__ out_len)
 {
     __shared__ CrcLds t;
-    __shared__ __attribute__((aligned(16))) uint8_t buf[kWavesPerBlock][kFrameMax];
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kEgressWaves][kFrameMax];
+    __shared__ __attribute__((aligned(16))) uint8_t himg[2 * 31][kHdrImg];
     load_tables(t);
+    const int fan = s.fan_in;
+    for (int i = threadIdx.x; i < 2 * fan; i += blockDim.x) build_header_image(himg[i], tmpl[i >> 1], (i & 1) != 0);
     __syncthreads();
     const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    const int fan = s.fan_in;
-    for (int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + w; g < count * fan;
-         g += (int64_t)gridDim.x * kWavesPerBlock)
-        egress_one(s, in_frames, in_stride, ports, action, psns, tmpl, out, out_stride, out_len, t, buf[w], g, lane);
+    const bool out16 = ((out_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+    for (int64_t g = (int64_t)blockIdx.x * kEgressWaves + w; g < count * fan; g += (int64_t)gridDim.x * kEgressWaves)
+        egress_one(s, in_frames, in_stride, ports, action, psns, himg, out, out_stride, out16, out_len, t, buf[w], g,
+                   lane);
 }
 
 // clear_state_data(psn + WINDOW) for every slot completed in the batch (nts.c:235-242, :367)
@@ -330,14 +360,14 @@ __global__ void k_recycle(InccSwitchState s, int64_t count, const int32_t* __res
 // ---------------------------------------------------------------------------
 // host: CRC tables (util.c:141-159) and the zero-append operators per tree level
 // ---------------------------------------------------------------------------
-uint32_t host_tab[256];
+uint32_t host_tab[4][256];
 uint32_t host_shift[6][4][256];
 bool g_tables_ready[64];
 std::mutex g_tables_mu;
 
 uint32_t zeros_append(uint32_t c, int nbytes)
 {
-    for (int i = 0; i < nbytes; ++i) c = (c >> 8) ^ host_tab[c & 0xFF];
+    for (int i = 0; i < nbytes; ++i) c = (c >> 8) ^ host_tab[0][c & 0xFF];
     return c;
 }
 
@@ -351,8 +381,10 @@ int ensure_tables()
     for (uint32_t i = 0; i < 256; ++i) {
         uint32_t c = i;
         for (int j = 0; j < 8; ++j) c = (c >> 1) ^ ((c & 1u) ? 0xEDB88320u : 0u);
-        host_tab[i] = c;
+        host_tab[0][i] = c;
     }
+    for (int k = 1; k < 4; ++k)
+        for (int i = 0; i < 256; ++i) host_tab[k][i] = (host_tab[k - 1][i] >> 8) ^ host_tab[0][host_tab[k - 1][i] & 0xFF];
     for (int l = 0; l < 6; ++l)
         for (int b = 0; b < 4; ++b)
             for (uint32_t v = 0; v < 256; ++v) host_shift[l][b][v] = zeros_append(v << (8 * b), kSeg << l);
@@ -361,6 +393,20 @@ int ensure_tables()
     if (e != hipSuccess) return (int)e;
     if (dev >= 0 && dev < 64) g_tables_ready[dev] = true;
     return 0;
+}
+
+int num_cus()
+{
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            cus = v;
+        else
+            cus = 256;
+    }
+    return cus;
 }
 
 inline int grid_for(int64_t waves)
@@ -383,7 +429,8 @@ int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* o
     int rc = ensure_tables();
     if (rc) return rc;
     const int64_t blocks = ((int64_t)count + kWavesPerBlock - 1) / kWavesPerBlock;
-    const int grid = (int)(blocks < 2048 ? blocks : 2048);
+    const int64_t cap = (int64_t)num_cus() * 4;
+    const int grid = (int)(blocks < cap ? blocks : cap);
     hipLaunchKernelGGL(k_icrc, dim3(grid), dim3(kWave * kWavesPerBlock), 0, (hipStream_t)stream, frames,
                        (int64_t)stride, (int64_t)count, out);
     return (int)hipGetLastError();
@@ -411,8 +458,11 @@ int inccl_k_switch_egress(const InccSwitchState* s, const uint8_t* in_frames, si
     int rc = ensure_tables();
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    const int eg = grid_for((int64_t)count * s->fan_in);
-    hipLaunchKernelGGL(k_egress, dim3(eg < 2048 ? eg : 2048), dim3(kWave * kWavesPerBlock), 0, st, *s,
+    // persistent grid: the 25 KiB CRC tables are loaded once per block
+    const int64_t need = ((int64_t)count * s->fan_in + kEgressWaves - 1) / kEgressWaves;
+    const int64_t cap = (int64_t)num_cus() * 4;
+    const int eg = (int)(need < cap ? (need < 1 ? 1 : need) : cap);
+    hipLaunchKernelGGL(k_egress, dim3(eg), dim3(kWave * kEgressWaves), 0, st, *s,
                        in_frames, (int64_t)in_stride, (int64_t)count, ports, action, psns, tmpl, out,
                        (int64_t)out_stride, out_len);
     hipLaunchKernelGGL(k_recycle, dim3((unsigned)count), dim3(256), 0, st, *s, (int64_t)count, action, psns);

@@ -60,19 +60,23 @@ static int p2p_ensure(struct inccl_communicator *c, size_t elems)
     if (rc) return rc;
     inccl_p2p_release(c);
     size_t cap = (elems + (1u << 19) - 1) & ~(size_t)((1u << 19) - 1);   /* 2 MiB granules */
-    INCCL_HIP(hipMalloc((void **)&c->p2p_part, cap * sizeof(int32_t)));
-    INCCL_HIP(hipMalloc((void **)&c->p2p_res, cap * sizeof(float)));
-    c->p2p_cap = cap;
     p2p_handles mine, *all = (p2p_handles *)calloc((size_t)W, sizeof(p2p_handles));
     if (!all) return inccl_set_error(INCCL_ERR_NOMEM, "p2p: out of memory");
     memset(&mine, 0, sizeof(mine));
-    hipError_t e = hipIpcGetMemHandle(&mine.part, c->p2p_part);
-    if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.res, c->p2p_res);
-    if (e != hipSuccess) {
-        free(all);
-        return inccl_hip_check(e, "hipIpcGetMemHandle");
+    /* local failures are carried to the collective outcome check below */
+    hipError_t e = hipMalloc((void **)&c->p2p_part, cap * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&c->p2p_res, cap * sizeof(float));
+    if (e == hipSuccess) {
+        c->p2p_cap = cap;
+        e = hipIpcGetMemHandle(&mine.part, c->p2p_part);
+        if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.res, c->p2p_res);
     }
-    rc = inccl_boot_allgather(g, &mine, all, sizeof(p2p_handles));
+    if (e != hipSuccess) rc = inccl_hip_check(e, "p2p: hipMalloc/hipIpcGetMemHandle");
+    int rc_x = inccl_boot_allgather(g, &mine, all, sizeof(p2p_handles));
+    if (rc_x) {
+        free(all);
+        return rc_x;
+    }
     for (int j = 0; rc == 0 && j < W; ++j) {
         if (j == me) {
             c->p2p_peer_part[j] = c->p2p_part;
@@ -87,9 +91,20 @@ static int p2p_ensure(struct inccl_communicator *c, size_t elems)
         c->p2p_peer_res[j] = (float *)pr;
     }
     free(all);
-    if (rc) return rc;
-    /* everyone mapped everyone before first use */
-    return inccl_boot_barrier(g);
+    /* agree on the outcome: a rank whose IPC mapping failed must not leave its
+     * peers waiting in a barrier it never reaches, and everyone must see the
+     * failure so the caller can fall back on every rank alike */
+    int32_t mine_rc = rc ? 1 : 0, all_rc[64];
+    if (W > 64) return inccl_set_error(INCCL_ERR_ARG, "p2p: world too large");
+    int rc2 = inccl_boot_allgather(g, &mine_rc, all_rc, sizeof(int32_t));
+    if (rc2) return rc2;
+    for (int j = 0; j < W; ++j)
+        if (all_rc[j]) {
+            if (!rc) rc = inccl_set_error(INCCL_ERR_HIP, "p2p: rank %d could not map the peer buffers", j);
+            inccl_p2p_release(c);
+            return rc;
+        }
+    return 0;
 }
 
 static int sync_and_barrier(struct inccl_communicator *c, hipStream_t st)
