@@ -11,11 +11,16 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <fcntl.h>
 #include <poll.h>
+#include <sched.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -212,8 +217,89 @@ int inccl_boot_barrier(struct inccl_group *g)
     return 0;
 }
 
+/* ------------------------------------------------------------------ */
+/* same-node fast barrier: a sense-reversing counter in POSIX shared memory */
+/* ------------------------------------------------------------------ */
+struct inccl_shm_bar {
+    _Atomic uint32_t count;
+    _Atomic uint32_t generation;
+    uint32_t world;
+};
+
+int inccl_boot_shm_init(struct inccl_group *g)
+{
+    if (g->world_size == 1 || g->shm_bar) return 0;
+    char name[64];
+    memset(name, 0, sizeof(name));
+    if (g->rank == 0) {
+        struct timespec ts;
+        clock_gettime(CLOCK_REALTIME, &ts);
+        snprintf(name, sizeof(name), "/inccl-%d-%ld-%d", (int)getpid(), (long)ts.tv_nsec, g->port);
+        int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd >= 0) {
+            if (ftruncate(fd, sizeof(struct inccl_shm_bar)) != 0) name[0] = 0;
+            close(fd);
+        } else {
+            name[0] = 0;
+        }
+    }
+    int rc = inccl_boot_bcast(g, name, sizeof(name));
+    if (rc) return rc;
+    int32_t ok = 0;
+    void *p = MAP_FAILED;
+    if (name[0]) {
+        int fd = shm_open(name, O_RDWR, 0600);
+        if (fd >= 0) {
+            p = mmap(NULL, sizeof(struct inccl_shm_bar), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            close(fd);
+            ok = p != MAP_FAILED;
+        }
+    }
+    int32_t all[64];
+    if (g->world_size > 64) ok = 0;
+    rc = g->world_size <= 64 ? inccl_boot_allgather(g, &ok, all, sizeof(ok)) : 0;
+    int every = rc == 0 && g->world_size <= 64;
+    for (int j = 0; every && j < g->world_size; ++j) every = every && all[j];
+    /* the name is no longer needed once every rank has mapped it */
+    int rc2 = inccl_boot_barrier(g);
+    if (g->rank == 0 && name[0]) shm_unlink(name);
+    if (!every) {   /* not all on one node (or no /dev/shm): keep the TCP barrier */
+        if (p != MAP_FAILED) munmap(p, sizeof(struct inccl_shm_bar));
+        return rc ? rc : rc2;
+    }
+    struct inccl_shm_bar *b = (struct inccl_shm_bar *)p;
+    if (g->rank == 0) b->world = (uint32_t)g->world_size;
+    g->shm_bar = b;
+    return inccl_boot_barrier(g);
+}
+
+int inccl_group_barrier(struct inccl_group *g)
+{
+    struct inccl_shm_bar *b = g->shm_bar;
+    if (!b) return inccl_boot_barrier(g);
+    const uint32_t gen = atomic_load(&b->generation);
+    if (atomic_fetch_add(&b->count, 1) + 1 == (uint32_t)g->world_size) {
+        atomic_store(&b->count, 0);
+        atomic_store(&b->generation, gen + 1);
+        return 0;
+    }
+    const double deadline = now_s() + boot_timeout_s();
+    unsigned spins = 0;
+    while (atomic_load(&b->generation) == gen) {
+        if ((++spins & 1023) == 0) {
+            if (now_s() > deadline) return inccl_set_error(INCCL_ERR_SYS, "shm barrier timed out");
+            sched_yield();
+        }
+    }
+    return 0;
+}
+
 void inccl_boot_close(struct inccl_group *g)
 {
+    if (g->shm_bar) {
+        munmap(g->shm_bar, sizeof(struct inccl_shm_bar));
+        g->shm_bar = NULL;
+    }
     if (g->peer_fds) {
         for (int r = 0; r < g->world_size; ++r)
             if (g->peer_fds[r] >= 0) close(g->peer_fds[r]);

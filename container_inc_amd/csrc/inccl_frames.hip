@@ -34,19 +34,17 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kEgressWaves = 8;       // 512-lane blocks, CU-sized persistent grid
 constexpr int kLanes = 256;           // int32 lanes per packet (nts.c:55)
 
-__device__ uint32_t g_crc_tab[4][256];       // slice-by-4 tables (util.c:141-159 derives 8)
+__device__ uint32_t g_crc_tab[256];          // util.c:141-150 table 0
 __device__ uint32_t g_shift_tab[6][4][256];
 
 struct CrcLds {
-    uint32_t tab[4][256];
+    uint32_t tab[256];
     uint32_t sh[6][4][256];
 };
 
 __device__ __forceinline__ void load_tables(CrcLds& t)
 {
-    uint32_t* d0 = &t.tab[0][0];
-    const uint32_t* s0 = &g_crc_tab[0][0];
-    for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) d0[i] = s0[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) t.tab[i] = g_crc_tab[i];
     uint32_t* dst = &t.sh[0][0][0];
     const uint32_t* src = &g_shift_tab[0][0][0];
     for (int i = threadIdx.x; i < 6 * 4 * 256; i += blockDim.x) dst[i] = src[i];
@@ -71,14 +69,12 @@ __device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds& t, int lane)
         const int m = lane * kSeg + j - lead;
         b[j] = (m < 0) ? (uint8_t)0 : ((m < 4) ? (uint8_t)0xFF : frame_byte(fr, 14 + m - 4));
     }
-    // slice-by-4 over bytes 0..15, then byte 16: a 5-step dependent chain
+    // byte-table CRC (util.c:190-192 form).  The kernel is bound by LDS lookups,
+    // not by this chain's latency: a slice-by-4 variant (4 KiB of tables, one
+    // block fewer per CU) measured slower in k_egress (356 vs 289 us / 131k frames).
     uint32_t c = 0;
 #pragma unroll
-    for (int j = 0; j < 16; j += 4) {
-        c ^= (uint32_t)b[j] | ((uint32_t)b[j + 1] << 8) | ((uint32_t)b[j + 2] << 16) | ((uint32_t)b[j + 3] << 24);
-        c = t.tab[3][c & 0xFF] ^ t.tab[2][(c >> 8) & 0xFF] ^ t.tab[1][(c >> 16) & 0xFF] ^ t.tab[0][c >> 24];
-    }
-    c = (c >> 8) ^ t.tab[0][(c ^ b[16]) & 0xFFu];
+    for (int j = 0; j < kSeg; ++j) c = (c >> 8) ^ t.tab[(c ^ b[j]) & 0xFFu];
     // tree: at level l the block of lane L (low l bits zero) absorbs block L + 2^l:
     // crc = shift(crc_left, |right| = 17 * 2^l bytes) ^ crc_right.  Only left lanes
     // (the block representatives) are updated; lane 0 ends with the whole window.
@@ -360,14 +356,14 @@ __global__ void k_recycle(InccSwitchState s, int64_t count, const int32_t* __res
 // ---------------------------------------------------------------------------
 // host: CRC tables (util.c:141-159) and the zero-append operators per tree level
 // ---------------------------------------------------------------------------
-uint32_t host_tab[4][256];
+uint32_t host_tab[256];
 uint32_t host_shift[6][4][256];
 bool g_tables_ready[64];
 std::mutex g_tables_mu;
 
 uint32_t zeros_append(uint32_t c, int nbytes)
 {
-    for (int i = 0; i < nbytes; ++i) c = (c >> 8) ^ host_tab[0][c & 0xFF];
+    for (int i = 0; i < nbytes; ++i) c = (c >> 8) ^ host_tab[c & 0xFF];
     return c;
 }
 
@@ -381,10 +377,8 @@ int ensure_tables()
     for (uint32_t i = 0; i < 256; ++i) {
         uint32_t c = i;
         for (int j = 0; j < 8; ++j) c = (c >> 1) ^ ((c & 1u) ? 0xEDB88320u : 0u);
-        host_tab[0][i] = c;
+        host_tab[i] = c;
     }
-    for (int k = 1; k < 4; ++k)
-        for (int i = 0; i < 256; ++i) host_tab[k][i] = (host_tab[k - 1][i] >> 8) ^ host_tab[0][host_tab[k - 1][i] & 0xFF];
     for (int l = 0; l < 6; ++l)
         for (int b = 0; b < 4; ++b)
             for (uint32_t v = 0; v < 256; ++v) host_shift[l][b][v] = zeros_append(v << (8 * b), kSeg << l);

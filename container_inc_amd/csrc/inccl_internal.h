@@ -22,6 +22,7 @@
 #define INCCL_ENGINE_P2P 1
 
 struct inccl_local_hub;
+struct inccl_shm_bar;
 
 struct inccl_group {
     int rank;
@@ -34,6 +35,7 @@ struct inccl_group {
      * reference's group_fd_list, api.h:58); other ranks hold master_fd. */
     int master_fd;
     int *peer_fds;
+    struct inccl_shm_bar *shm_bar;   /* same-node fast barrier (NULL: TCP barrier) */
     /* local transport */
     struct inccl_local_hub *hub;
     int comm_seq;   /* communicators created so far (names the hub slot) */
@@ -113,6 +115,8 @@ int inccl_boot_worker(struct inccl_group *g);
 int inccl_boot_bcast(struct inccl_group *g, void *buf, size_t bytes);   /* from rank 0 */
 int inccl_boot_barrier(struct inccl_group *g);
 int inccl_boot_allgather(struct inccl_group *g, const void *mine, void *all, size_t bytes);
+int inccl_boot_shm_init(struct inccl_group *g);   /* collective; falls back silently */
+int inccl_group_barrier(struct inccl_group *g);   /* shm barrier if set up, else TCP */
 void inccl_boot_close(struct inccl_group *g);
 
 /* errors */

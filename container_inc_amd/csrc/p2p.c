@@ -58,6 +58,8 @@ static int p2p_ensure(struct inccl_communicator *c, size_t elems)
     /* peers may still read the old buffers until everyone is here */
     int rc = inccl_boot_barrier(g);
     if (rc) return rc;
+    rc = inccl_boot_shm_init(g);   /* same-node fast barrier for the per-call syncs */
+    if (rc) return rc;
     inccl_p2p_release(c);
     size_t cap = (elems + (1u << 19) - 1) & ~(size_t)((1u << 19) - 1);   /* 2 MiB granules */
     p2p_handles mine, *all = (p2p_handles *)calloc((size_t)W, sizeof(p2p_handles));
@@ -110,7 +112,7 @@ static int p2p_ensure(struct inccl_communicator *c, size_t elems)
 static int sync_and_barrier(struct inccl_communicator *c, hipStream_t st)
 {
     INCCL_HIP(hipStreamSynchronize(st));
-    return inccl_boot_barrier(c->group);
+    return inccl_group_barrier(c->group);
 }
 
 int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,

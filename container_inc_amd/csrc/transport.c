@@ -313,5 +313,5 @@ int inccl_tp_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size
 int inccl_tp_barrier(struct inccl_communicator *c)
 {
     if (is_local(c)) return inccl_local_barrier(c);
-    return inccl_boot_barrier(c->group);
+    return inccl_group_barrier(c->group);
 }
