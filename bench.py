@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--local-buckets", type=int, default=2)
     p.add_argument("--scale-exp", type=int, default=25)
     p.add_argument("--chunks", type=int, default=0, help="pipelined chunks for the rccl engine (0 = tune)")
-    p.add_argument("--engine", default="auto", choices=["auto", "rccl", "p2p"],
+    p.add_argument("--engine", default="auto", choices=["auto", "rccl", "a2a", "p2p"],
                    help="N>1 exchange engine; auto = time every candidate during warmup, keep the fastest")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -208,6 +208,8 @@ def main():
         cands = []
         if a.engine in ("auto", "rccl"):
             cands += [("rccl", c) for c in ([a.chunks] if a.chunks else [1, 4])]
+        if a.engine in ("auto", "a2a"):
+            cands.append(("a2a", 1))
         if a.engine in ("auto", "p2p"):
             cands.append(("p2p", 1))
         ref = None
@@ -295,6 +297,9 @@ def main():
                 (f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: quant+local sum -> RCCL reduce-scatter "
                  f"int32 -> dequant shard -> RCCL all-gather fp32, {chunks} pipelined chunks")
                 if comm.engine == "rccl" else
+                (f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: quant+local sum -> RCCL all-to-all of "
+                 f"int32 shards -> fused sum+dequant (HIP) -> RCCL all-gather fp32")
+                if comm.engine == "a2a" else
                 (f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: quant+local sum -> p2p pull of every "
                  f"peer's shard over xGMI with fused sum+dequant -> p2p gather of every result shard"))
     kname = "k_stream_vec<F32,F32,R>" if world == 1 else "k_stream_vec<F32,Q32,R>"

@@ -357,20 +357,26 @@ int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name)
         comm->engine = INCCL_ENGINE_RCCL;
         return 0;
     }
+    if (strcmp(name, "a2a") == 0) {
+        if (comm->group->transport != INCCL_TRANSPORT_RCCL)
+            return inccl_set_error(INCCL_ERR_ARG, "a2a engine needs a multi-process (rccl) group");
+        comm->engine = INCCL_ENGINE_A2A;
+        return 0;
+    }
     if (strcmp(name, "p2p") == 0) {
         if (comm->group->transport != INCCL_TRANSPORT_RCCL)
             return inccl_set_error(INCCL_ERR_ARG, "p2p engine needs a multi-process (rccl) group");
         comm->engine = INCCL_ENGINE_P2P;
         return 0;
     }
-    return inccl_set_error(INCCL_ERR_ARG, "unknown engine '%s' (rccl | p2p)", name);
+    return inccl_set_error(INCCL_ERR_ARG, "unknown engine '%s' (rccl | a2a | p2p)", name);
 }
 
 const char *inccl_comm_engine(const struct inccl_communicator *comm)
 {
     if (!comm) return "";
     if (comm->group->transport == INCCL_TRANSPORT_LOCAL) return "local";
-    return comm->engine == INCCL_ENGINE_P2P ? "p2p" : "rccl";
+    return comm->engine == INCCL_ENGINE_P2P ? "p2p" : (comm->engine == INCCL_ENGINE_A2A ? "a2a" : "rccl");
 }
 
 int inccl_comm_barrier(struct inccl_communicator *comm)
@@ -389,6 +395,36 @@ int inccl_allreduce_q32(struct inccl_communicator *c, const int32_t *src_dev, in
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     if (n == 0) return 0;
     return inccl_tp_allreduce_q32(c, src_dev, dst_dev, n, st);
+}
+
+/* Variant B: quant + local sum -> grouped ncclSend/Recv of
+ * int32 shards -> this library's fused sum over the W received shards +
+ * dequantise (the switch aggregate, non_termination_switch.c:361-363, fused with
+ * the back stage) -> ncclAllGather.  `ws` holds W*shard (send) + W*shard (recv). */
+static int allreduce_piece_a2a(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n,
+                               int k, const uint32_t *amax, int scale_R, int32_t *ws, float *fws, hipStream_t st)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
+    int32_t *qsend = ws, *qrecv = ws + total;
+    int rc = kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_Q32, (const void *const *)srcs, R, qsend, n, k, amax,
+                                 scale_R, st));
+    if (rc) return rc;
+    if (total > n) INCCL_HIP(hipMemsetAsync(qsend + n, 0, (total - n) * sizeof(int32_t), st));
+    rc = inccl_rccl_alltoall_q32(c, qsend, qrecv, shard, st);
+    if (rc) return rc;
+    const void *parts[INCCL_MAX_LOCAL_INPUTS];
+    for (int j = 0; j < W; ++j) parts[j] = (j == me) ? (const void *)(qsend + (size_t)me * shard)
+                                                      : (const void *)(qrecv + (size_t)j * shard);
+    const size_t lo = (size_t)me * shard;
+    const int in_place = (total == n);
+    float *gather = in_place ? dst : fws;
+    rc = kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_F32, parts, W, gather + lo, shard, k, amax, scale_R, st));
+    if (rc) return rc;
+    rc = inccl_tp_all_gather_f32(c, gather + lo, gather, shard, st);
+    if (rc) return rc;
+    if (!in_place) INCCL_HIP(hipMemcpyAsync(dst, fws, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    return 0;
 }
 
 /* One bucket piece: quant + local sum -> reduce-scatter -> dequant shard ->
@@ -466,6 +502,19 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
 
     if (c->engine == INCCL_ENGINE_P2P && c->group->transport == INCCL_TRANSPORT_RCCL)
         return inccl_p2p_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+    if (c->engine == INCCL_ENGINE_A2A && c->group->transport == INCCL_TRANSPORT_RCCL) {
+        if (W > INCCL_MAX_LOCAL_INPUTS)
+            return inccl_set_error(INCCL_ERR_ARG, "a2a engine sums at most %d shards", INCCL_MAX_LOCAL_INPUTS);
+        const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
+        rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, 2 * total * sizeof(int32_t));
+        if (rc) return rc;
+        if (total != n) {
+            rc = inccl_ensure_dev(&c->d_f32, &c->d_f32_bytes, total * sizeof(float));
+            if (rc) return rc;
+        }
+        return allreduce_piece_a2a(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, (int32_t *)c->d_q32,
+                                   (float *)c->d_f32, st);
+    }
     /* chunk boundaries: multiples of W*64 elements so every chunk's shards are
      * 256-B aligned inside dst; each chunk has its own workspace region */
     if (chunks < 1) chunks = 1;

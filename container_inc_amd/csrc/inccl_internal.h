@@ -20,6 +20,7 @@
 /* communicator-level exchange engine (group transport RCCL only) */
 #define INCCL_ENGINE_RCCL 0
 #define INCCL_ENGINE_P2P 1
+#define INCCL_ENGINE_A2A 2
 
 struct inccl_local_hub;
 struct inccl_shm_bar;
@@ -91,6 +92,9 @@ int inccl_rccl_all_gather_f32(struct inccl_communicator *c, const float *send, f
 int inccl_rccl_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
                              hipStream_t st);
 int inccl_rccl_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st);
+/* grouped send/recv: shard j of `send` to rank j, rank j's shard `me` into recv + j*shard */
+int inccl_rccl_alltoall_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t shard,
+                            hipStream_t st);
 
 /* p2p engine */
 int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,

@@ -80,6 +80,27 @@ int inccl_rccl_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, si
                       "ncclAllReduce(max)");
 }
 
+int inccl_rccl_alltoall_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t shard,
+                            hipStream_t st)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    if (!c->nccl && W > 1) {
+        int rc = inccl_rccl_comm_init(c);
+        if (rc) return rc;
+    }
+    if (W == 1) return 0;
+    int rc = nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (int j = 0; rc == 0 && j < W; ++j) {
+        if (j == me) continue;
+        rc = nccl_check(ncclSend(send + (size_t)j * shard, shard, ncclInt32, j, (ncclComm_t)c->nccl, st), "ncclSend");
+        if (rc == 0)
+            rc = nccl_check(ncclRecv(recv + (size_t)j * shard, shard, ncclInt32, j, (ncclComm_t)c->nccl, st),
+                            "ncclRecv");
+    }
+    int rc2 = nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    return rc ? rc : rc2;
+}
+
 /* ------------------------------------------------------------------ */
 /* local hub                                                            */
 /* ------------------------------------------------------------------ */

@@ -115,6 +115,8 @@ void *inccl_comm_stream(struct inccl_communicator *comm);
 int inccl_comm_barrier(struct inccl_communicator *comm);
 /* Exchange engine of a multi-process communicator for inccl_allreduce_f32:
  *   "rccl"  quant+sum -> ncclReduceScatter(int32) -> dequant -> ncclAllGather (default)
+ *   "a2a"   quant+sum -> grouped ncclSend/Recv of int32 shards -> this library's fused
+ *           sum + dequantise kernel over the W shards -> ncclAllGather
  *   "p2p"   library buffers shared via HIP IPC; each GPU pulls its shard from every
  *           peer over xGMI with the fused sum+dequantise kernel, then pulls every
  *           peer's result shard (two group barriers per call)
