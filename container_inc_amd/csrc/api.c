@@ -318,6 +318,7 @@ int inccl_communicator_destroy(struct inccl_communicator *comm)
     if (comm->d_f32) hipFree(comm->d_f32);
     if (comm->d_stage) hipFree(comm->d_stage);
     if (comm->d_words) hipFree(comm->d_words);
+    inccl_copy_pool_destroy(comm->pool);
     if (comm->send_payload) hipHostFree(comm->send_payload);
     if (comm->receive_payload) hipHostFree(comm->receive_payload);
     for (int i = 0; i < 8; ++i)
@@ -581,6 +582,33 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
  * become large chunks staged through the pinned send/receive buffers, the
  * sum runs on the GPU (RCCL or the local hub's sum kernel), and the same
  * "whole messages only" rule applies. */
+/* Grow the pinned staging (the reference's 2*size registered buffers) so each
+ * ping-pong half holds `half_bytes`. */
+static int ensure_staging(struct inccl_communicator *c, size_t half_bytes)
+{
+    if ((size_t)c->payload_buf_size >= 2 * half_bytes && c->send_payload) return 0;
+    INCCL_HIP(hipStreamSynchronize(c->copy_streams[0]));
+    INCCL_HIP(hipStreamSynchronize(c->copy_streams[1]));
+    if (c->send_payload) hipHostFree(c->send_payload);
+    if (c->receive_payload) hipHostFree(c->receive_payload);
+    c->send_payload = c->receive_payload = NULL;
+    c->payload_buf_size = 0;
+    INCCL_HIP(hipHostMalloc((void **)&c->send_payload, 2 * half_bytes, hipHostMallocDefault));
+    INCCL_HIP(hipHostMalloc((void **)&c->receive_payload, 2 * half_bytes, hipHostMallocDefault));
+    c->payload_buf_size = (uint32_t)(2 * half_bytes);
+    return 0;
+}
+
+/* Replaces api.c:403-452 / :330-401.  The reference encodes 1024-element
+ * messages into the registered buffer (api.c:300-302), lets the switch add
+ * them and decodes completions into dst (api.c:428-430), two messages in
+ * flight (api.c:408).  Here messages become chunks of up to 16 MiB that stream
+ * through a 5-stage pipeline, chunk i+1's copy-in overlapping chunk i's DMA,
+ * reduction and copy-out:
+ *   host copy-in (pool) -> H2D (copy stream 0) -> device allreduce (RCCL, or the
+ *   local hub's sum kernel) -> D2H (copy stream 1) -> host copy-out (pool)
+ * The pinned staging halves ping-pong as the reference's two-message window
+ * does.  The "whole messages only" rule (api.c:406) is kept. */
 static int allreduce_host_q32(struct inccl_communicator *c, const int32_t *src, uint32_t len, int32_t *dst)
 {
     const size_t message_num = len / PAYLOAD_COUNT;          /* api.c:406 */
@@ -588,49 +616,54 @@ static int allreduce_host_q32(struct inccl_communicator *c, const int32_t *src, 
     if (n == 0) return 0;
     if (!src || !dst) return inccl_set_error(INCCL_ERR_ARG, "NULL src/dst");
     INCCL_HIP(hipSetDevice(c->group->device));
-    hipStream_t st = c->stream;
-    int rc = inccl_ensure_dev(&c->d_stage, &c->d_stage_bytes, n * sizeof(int32_t));
+    /* chunk: what the reference buffers hold, at least 1 MiB, at most 16 MiB */
+    size_t chunk_bytes = c->payload_buf_size / 2;
+    if (chunk_bytes < ((size_t)1 << 20)) chunk_bytes = (size_t)1 << 20;
+    if (chunk_bytes > ((size_t)16 << 20)) chunk_bytes = (size_t)16 << 20;
+    if (chunk_bytes > n * sizeof(int32_t)) chunk_bytes = n * sizeof(int32_t);
+    chunk_bytes = chunk_bytes / MESSAGE_SIZE * MESSAGE_SIZE;
+    int rc = ensure_staging(c, chunk_bytes);
     if (rc) return rc;
-    int32_t *d = (int32_t *)c->d_stage;
-    /* two halves of each pinned buffer alternate (ping-pong) */
-    size_t chunk = c->payload_buf_size / 2 / sizeof(int32_t);
-    chunk = chunk / PAYLOAD_COUNT * PAYLOAD_COUNT;
-    if (chunk == 0) {
-        INCCL_HIP(hipMemcpyAsync(d, src, n * sizeof(int32_t), hipMemcpyHostToDevice, st));
-    } else {
-        for (size_t off = 0, i = 0; off < n; off += chunk, ++i) {
-            const size_t cnt = (n - off) < chunk ? (n - off) : chunk;
-            char *half = c->send_payload + (i & 1) * chunk * sizeof(int32_t);
-            INCCL_HIP(hipEventSynchronize(c->ev[2 + (i & 1)]));   /* the DMA that last read this half */
-            memcpy(half, src + off, cnt * sizeof(int32_t));
-            INCCL_HIP(hipMemcpyAsync(d + off, half, cnt * sizeof(int32_t), hipMemcpyHostToDevice, st));
-            INCCL_HIP(hipEventRecord(c->ev[2 + (i & 1)], st));
+    const size_t CH = chunk_bytes / sizeof(int32_t);
+    rc = inccl_ensure_dev(&c->d_stage, &c->d_stage_bytes, 2 * chunk_bytes);
+    if (rc) return rc;
+    if (!c->pool) {
+        const char *e = getenv("INCCL_COPY_THREADS");
+        c->pool = inccl_copy_pool_create(e && *e ? atoi(e) : 4);   /* NULL -> plain memcpy */
+    }
+    int32_t *d[2] = {(int32_t *)c->d_stage, (int32_t *)c->d_stage + CH};
+    char *in[2] = {c->send_payload, c->send_payload + chunk_bytes};
+    char *out[2] = {c->receive_payload, c->receive_payload + chunk_bytes};
+    hipStream_t h2d = c->copy_streams[0], d2h = c->copy_streams[1], ks = c->stream;
+    hipEvent_t e_h2d[2] = {c->ev[0], c->ev[1]}, e_ar[2] = {c->ev[2], c->ev[3]}, e_d2h[2] = {c->ev[4], c->ev[5]};
+    INCCL_HIP(hipStreamSynchronize(ks));
+    const size_t nch = (n + CH - 1) / CH;
+    for (size_t i = 0; i < nch; ++i) {
+        const int s = (int)(i & 1);
+        const size_t off = i * CH, cnt = (n - off) < CH ? (n - off) : CH;
+        if (i >= 2) INCCL_HIP(hipEventSynchronize(e_h2d[s]));           /* in[s] read by chunk i-2's DMA */
+        inccl_copy(c->pool, in[s], src + off, cnt * sizeof(int32_t));   /* api.c:300-302 (no byte swap) */
+        if (i >= 2) INCCL_HIP(hipStreamWaitEvent(h2d, e_d2h[s], 0));    /* d[s] drained by chunk i-2 */
+        INCCL_HIP(hipMemcpyAsync(d[s], in[s], cnt * sizeof(int32_t), hipMemcpyHostToDevice, h2d));
+        INCCL_HIP(hipEventRecord(e_h2d[s], h2d));
+        INCCL_HIP(hipStreamWaitEvent(ks, e_h2d[s], 0));
+        rc = inccl_tp_allreduce_q32(c, d[s], d[s], cnt, ks);            /* the switch's sum, nts.c:361-363 */
+        if (rc) return rc;
+        INCCL_HIP(hipEventRecord(e_ar[s], ks));
+        INCCL_HIP(hipStreamWaitEvent(d2h, e_ar[s], 0));
+        INCCL_HIP(hipMemcpyAsync(out[s], d[s], cnt * sizeof(int32_t), hipMemcpyDeviceToHost, d2h));
+        INCCL_HIP(hipEventRecord(e_d2h[s], d2h));
+        if (i >= 1) {   /* decode the previous completion while this chunk is in flight (api.c:428-430) */
+            const int ps = (int)((i - 1) & 1);
+            const size_t poff = (i - 1) * CH, pcnt = (n - poff) < CH ? (n - poff) : CH;
+            INCCL_HIP(hipEventSynchronize(e_d2h[ps]));
+            inccl_copy(c->pool, dst + poff, out[ps], pcnt * sizeof(int32_t));
         }
     }
-    rc = inccl_tp_allreduce_q32(c, d, d, n, st);
-    if (rc) return rc;
-    if (chunk == 0) {
-        INCCL_HIP(hipMemcpyAsync(dst, d, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        INCCL_HIP(hipStreamSynchronize(st));
-        return 0;
-    }
-    size_t prev_off = 0, prev_cnt = 0;
-    for (size_t off = 0, i = 0; off < n; off += chunk, ++i) {
-        const size_t cnt = (n - off) < chunk ? (n - off) : chunk;
-        char *half = c->receive_payload + (i & 1) * chunk * sizeof(int32_t);
-        INCCL_HIP(hipMemcpyAsync(half, d + off, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        INCCL_HIP(hipEventRecord(c->ev[4 + (i & 1)], st));
-        if (i > 0) {   /* decode the previous completion while this one is in flight (api.c:428-430) */
-            INCCL_HIP(hipEventSynchronize(c->ev[4 + ((i - 1) & 1)]));
-            memcpy(dst + prev_off, c->receive_payload + ((i - 1) & 1) * chunk * sizeof(int32_t),
-                   prev_cnt * sizeof(int32_t));
-        }
-        prev_off = off;
-        prev_cnt = cnt;
-    }
-    const size_t last = (n + chunk - 1) / chunk - 1;
-    INCCL_HIP(hipEventSynchronize(c->ev[4 + (last & 1)]));
-    memcpy(dst + prev_off, c->receive_payload + (last & 1) * chunk * sizeof(int32_t), prev_cnt * sizeof(int32_t));
+    const int ls = (int)((nch - 1) & 1);
+    const size_t loff = (nch - 1) * CH, lcnt = n - loff;
+    INCCL_HIP(hipEventSynchronize(e_d2h[ls]));
+    inccl_copy(c->pool, dst + loff, out[ls], lcnt * sizeof(int32_t));
     return 0;
 }
 

@@ -24,6 +24,7 @@
 
 struct inccl_local_hub;
 struct inccl_shm_bar;
+struct inccl_copy_pool;
 
 struct inccl_group {
     int rank;
@@ -69,6 +70,7 @@ struct inccl_communicator {
     float *p2p_res;              /* this rank's dequantised shard lives at rank * shard */
     int32_t *p2p_peer_part[INCCL_MAX_LOCAL_INPUTS];
     float *p2p_peer_res[INCCL_MAX_LOCAL_INPUTS];
+    struct inccl_copy_pool *pool;  /* host staging copies (copypool.c) */
     hipEvent_t ev[8];
 };
 
@@ -141,5 +143,10 @@ static inline size_t inccl_shard_elems(size_t n, int world)
 }
 
 int inccl_ensure_dev(void **p, size_t *cur, size_t need);
+
+/* copypool.c */
+struct inccl_copy_pool *inccl_copy_pool_create(int n);
+void inccl_copy_pool_destroy(struct inccl_copy_pool *p);
+void inccl_copy(struct inccl_copy_pool *p, void *dst, const void *src, size_t bytes);
 
 #endif
