@@ -318,14 +318,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32->int32 (fixed point, 2^-%d)" % k,
+        "dtype": "int32",
         "data": "synthetic N(0,1) fp32 buckets, torch.Generator seed 1000+rank",
         "config": {
             "workload": workload,
             "bucket_mib": a.bucket_mib,
             "local_buckets": R,
             "scale_exp": k,
-            "global_batch": world * R,
+            "numerics": f"fp32 in/out; quantised to int32 fixed point 2^-{k}; int32 wrap-around sum (exact)",
             "parallelism": f"dp{world}",
             "chunks": chunks,
             "engine": comm.engine if world > 1 else "fused",

@@ -95,7 +95,7 @@ struct Geometry {
     static constexpr int U = Unroll<R>::U;
 };
 
-template <int IN, int OUT, int R, bool NT, int BLOCK = kBlock, int U = Unroll<R>::U>
+template <int IN, int OUT, int R, bool NT, int BLOCK = kBlock, int U = Unroll<R>::U, bool NTS = true>
 __global__ __launch_bounds__(BLOCK) void k_stream_vec(SrcPtrs src, void* __restrict__ dst, int64_t n4, Scale sc)
 {
     const int k = resolve_k(sc);
@@ -131,7 +131,8 @@ __global__ __launch_bounds__(BLOCK) void k_stream_vec(SrcPtrs src, void* __restr
                 o.y = store_xform<OUT>(acc.y, inv);
                 o.z = store_xform<OUT>(acc.z, inv);
                 o.w = store_xform<OUT>(acc.w, inv);
-                __builtin_nontemporal_store(o, out + i0 + (int64_t)u * BLOCK);
+                if constexpr (NTS) __builtin_nontemporal_store(o, out + i0 + (int64_t)u * BLOCK);
+                else out[i0 + (int64_t)u * BLOCK] = o;
             }
         } else {
 #pragma unroll

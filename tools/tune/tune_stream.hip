@@ -86,6 +86,22 @@ static void variant(const SrcPtrs& s, void* out, int64_t n4, const char* name)
     fflush(stdout);
 }
 
+// cache-policy and grid-stride depth variants at the product geometry (R = 2: 512 x 1)
+template <bool NT, bool NTS>
+static void policy(const SrcPtrs& s, void* out, int64_t n4, int depth)
+{
+    Scale sc{25, nullptr, 2};
+    const int64_t tiles = n4 / 512;
+    const int64_t grid = tiles / depth;
+    float ms = time_ms([&] {
+        hipLaunchKernelGGL((k_stream_vec<F32, F32, 2, NT, 512, 1, NTS>), dim3((unsigned)grid), dim3(512), 0, 0, s, out,
+                           n4, sc);
+    });
+    printf("{\"kernel\": \"fused_policy\", \"R\": 2, \"nt_loads\": %d, \"nt_stores\": %d, \"tiles_per_block\": %d, "
+           "\"ms\": %.5f, \"GBs\": %.1f}\n", NT, NTS, depth, ms, 48.0 * n4 / (ms * 1e-3) / 1e9);
+    fflush(stdout);
+}
+
 template <int IN, int OUT, int R>
 static void sweep(const SrcPtrs& s, void* out, int64_t n4, const char* name)
 {
@@ -133,6 +149,16 @@ int main()
     s.p[0] = a;
     s.p[1] = b;
     for (int i = 0; i < 6; ++i) s.p[2 + i] = extra[i];
+    if (getenv("TUNE_POLICY")) {
+        for (int rep = 0; rep < 3; ++rep)
+            for (int depth : {1, 2, 4, 8}) {
+                policy<true, true>(s, o, n4, depth);
+                policy<false, true>(s, o, n4, depth);
+                policy<true, false>(s, o, n4, depth);
+                policy<false, false>(s, o, n4, depth);
+            }
+        return 0;
+    }
     for (int rep = 0; rep < 2; ++rep) {
         sweep<F32, F32, 2>(s, o, n4, "fused");
         sweep<F32, F32, 1>(s, o, n4, "fused");
