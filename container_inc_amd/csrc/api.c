@@ -266,7 +266,12 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     struct inccl_group *g = c->group;
     if (g->device < 0) return inccl_set_error(INCCL_ERR_STATE, "group has no device (bootstrap-only)");
     INCCL_HIP(hipSetDevice(g->device));
-    c->payload_buf_size = size * 2u;             /* api.c:164 */
+    /* api.c:164 registers 2*size bytes per direction.  The staging here streams
+     * chunks of at most 16 MiB per ping-pong half (allreduce_host_q32), so the
+     * pinned buffers are capped at 32 MiB each (this also keeps 2*size from
+     * overflowing the 32-bit field for size >= 2 GiB). */
+    const uint64_t want = 2ull * (uint64_t)size;
+    c->payload_buf_size = (uint32_t)(want < (32ull << 20) ? want : (32ull << 20));
     c->window_size = WINDOW_SIZE;                /* api.c:226 */
     if (c->payload_buf_size) {
         INCCL_HIP(hipHostMalloc((void **)&c->send_payload, c->payload_buf_size, hipHostMallocDefault));
