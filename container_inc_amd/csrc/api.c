@@ -315,7 +315,8 @@ int inccl_communicator_destroy(struct inccl_communicator *comm)
     if (comm->group->device >= 0) hipSetDevice(comm->group->device);
     if (comm->stream) hipStreamSynchronize(comm->stream);
     if (comm->p2p_part) {   /* peers may still be reading our shard buffers */
-        inccl_boot_barrier(comm->group);
+        hipDeviceSynchronize();   /* our queued reads of theirs have drained ... */
+        inccl_boot_barrier(comm->group);   /* ... and so have everyone else's */
         inccl_p2p_release(comm);
     }
     inccl_rccl_comm_destroy(comm);
@@ -382,7 +383,8 @@ const char *inccl_comm_engine(const struct inccl_communicator *comm)
 {
     if (!comm) return "";
     if (comm->group->transport == INCCL_TRANSPORT_LOCAL) return "local";
-    return comm->engine == INCCL_ENGINE_P2P ? "p2p" : (comm->engine == INCCL_ENGINE_A2A ? "a2a" : "rccl");
+    if (comm->engine == INCCL_ENGINE_P2P) return comm->p2p_cap == 0 ? "p2p" : (comm->p2p_async ? "p2p-async" : "p2p-sync");
+    return comm->engine == INCCL_ENGINE_A2A ? "a2a" : "rccl";
 }
 
 int inccl_comm_barrier(struct inccl_communicator *comm)

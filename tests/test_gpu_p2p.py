@@ -33,9 +33,11 @@ def _inputs(world, R, n, seed):
     return out
 
 
-def _rank_main(rank, world, port, cases, q):
+def _rank_main(rank, world, port, cases, q, sync=False):
     try:
         os.environ["INCCL_ENGINE"] = "p2p"
+        if sync:
+            os.environ["INCCL_P2P_SYNC"] = "1"
         os.environ["INCCL_DEVICE"] = "0"
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
         import sys
@@ -47,7 +49,7 @@ def _rank_main(rank, world, port, cases, q):
         grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port)
         assert grp is not None, "group create failed"
         comm = inccl.inccl_communicator_create(grp, 0)
-        assert comm is not None and comm.engine == "p2p"
+        assert comm is not None and comm.engine.startswith("p2p")
         results = []
         for (R, n, k, seed) in cases:
             xs = _inputs(world, R, n, seed)
@@ -56,26 +58,29 @@ def _rank_main(rank, world, port, cases, q):
             want = O.reduce_f32(every, kk)
             srcs = [torch.from_numpy(x).to(dev) for x in xs[rank]]
             out = torch.full((n,), float("nan"), device=dev)
-            for _ in range(2):   # twice: buffer reuse across calls
+            for _ in range(4):   # repeated: buffer reuse across calls (async: no host waits between them)
                 comm.allreduce_f32(srcs, out=out, scale_exp=inccl.SCALE_AUTO if k == "auto" else k,
                                    stream=comm.stream)
                 torch.cuda.synchronize()
                 got = out.cpu().numpy()
                 results.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
+        mode = comm.engine
         comm.destroy()
         grp.destroy()
-        q.put((rank, results, None))
+        q.put((rank, results, None if mode == ("p2p-sync" if sync else "p2p-async") else f"mode {mode}"))
     except BaseException as e:  # noqa: BLE001
         q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_p2p_engine_multiprocess(gpu, world):
+@pytest.mark.parametrize("world,sync", [(2, False), (3, False), (2, True)])
+def test_p2p_engine_multiprocess(gpu, world, sync):
+    """sync=False: interprocess-event ordering, no host waits on the GPU (default);
+    sync=True: stream synchronisation + barrier between the phases."""
     cases = [(2, 1 << 20, 25, 11), (1, 100_003, 20, 12), (2, 65_536 * 3 + 5, "auto", 13), (2, 4 << 20, 24, 14)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_rank_main, args=(r, world, port, cases, q)) for r in range(world)]
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, cases, q, sync)) for r in range(world)]
     for p in ps:
         p.start()
     res = {}
