@@ -383,8 +383,7 @@ const char *inccl_comm_engine(const struct inccl_communicator *comm)
 {
     if (!comm) return "";
     if (comm->group->transport == INCCL_TRANSPORT_LOCAL) return "local";
-    if (comm->engine == INCCL_ENGINE_P2P) return comm->p2p_cap == 0 ? "p2p" : (comm->p2p_async ? "p2p-async" : "p2p-sync");
-    return comm->engine == INCCL_ENGINE_A2A ? "a2a" : "rccl";
+    return comm->engine == INCCL_ENGINE_P2P ? "p2p" : (comm->engine == INCCL_ENGINE_A2A ? "a2a" : "rccl");
 }
 
 int inccl_comm_barrier(struct inccl_communicator *comm)

@@ -70,11 +70,6 @@ struct inccl_communicator {
     float *p2p_res;              /* this rank's dequantised shard lives at rank * shard */
     int32_t *p2p_peer_part[INCCL_MAX_LOCAL_INPUTS];
     float *p2p_peer_res[INCCL_MAX_LOCAL_INPUTS];
-    /* interprocess events: [0] partials ready, [1] shard reduced (peers' parts
-     * consumed), [2] gather done (peers' result shards consumed); own + peers' */
-    hipEvent_t p2p_ev[3];
-    hipEvent_t p2p_peer_ev[INCCL_MAX_LOCAL_INPUTS][3];
-    int p2p_async;
     struct inccl_copy_pool *pool;  /* host staging copies (copypool.c) */
     hipEvent_t ev[8];
 };

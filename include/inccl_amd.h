@@ -122,7 +122,7 @@ int inccl_comm_barrier(struct inccl_communicator *comm);
  *           peer's result shard (two group barriers per call)
  * Every rank must select the same engine.  $INCCL_ENGINE sets it at creation. */
 int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name);
-/* "rccl", "a2a", "p2p" (before first use), "p2p-async" or "p2p-sync", or "local" */
+/* "rccl", "a2a", "p2p" or "local" */
 const char *inccl_comm_engine(const struct inccl_communicator *comm);
 
 /* Device-resident fp32 allreduce of R local buckets per rank:
