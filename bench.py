@@ -345,6 +345,12 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if world > 1:
+        # nccl-tests convention (BASELINE config 4): algbw = one rank's bucket bytes
+        # / step time; busbw = algbw * 2(W-1)/W, the per-GPU link traffic of RS + AG
+        algbw = n * 4 / (ms_per_step * 1e-3) / 1e9
+        res["collective"] = {"algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2),
+                             "bytes_per_rank": n * 4}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(n, R, k, a.cpu_seconds)
         res["cpu_baseline_allcores"] = cpu_baseline_allcores(n, R, k, min(a.cpu_seconds, 5.0))

@@ -287,6 +287,8 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     INCCL_HIP(hipMalloc((void **)&c->d_words, 256));
     INCCL_HIP(hipMemset(c->d_words, 0, 256));
     c->comm_id = g->comm_seq++;
+    const char *llb = getenv("INCCL_LL_MAX_BYTES");   /* small-bucket one-kernel path; 0 disables */
+    c->ll_max_bytes = llb ? (size_t)strtoull(llb, NULL, 0) : ((size_t)1 << 20);
     const char *eng = getenv("INCCL_ENGINE");
     if (eng && *eng && g->transport == INCCL_TRANSPORT_RCCL) {
         int rc = inccl_comm_set_engine(c, eng);
@@ -314,10 +316,11 @@ int inccl_communicator_destroy(struct inccl_communicator *comm)
     if (!comm) return 0;
     if (comm->group->device >= 0) hipSetDevice(comm->group->device);
     if (comm->stream) hipStreamSynchronize(comm->stream);
-    if (comm->p2p_part) {   /* peers may still be reading our shard buffers */
+    if (comm->p2p_part || comm->ll_buf) {   /* peers may still be reading our IPC buffers */
         hipDeviceSynchronize();   /* our queued reads of theirs have drained ... */
         inccl_boot_barrier(comm->group);   /* ... and so have everyone else's */
         inccl_p2p_release(comm);
+        inccl_ll_release(comm);
     }
     inccl_rccl_comm_destroy(comm);
     if (comm->d_q32) hipFree(comm->d_q32);
@@ -376,14 +379,26 @@ int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name)
         comm->engine = INCCL_ENGINE_P2P;
         return 0;
     }
-    return inccl_set_error(INCCL_ERR_ARG, "unknown engine '%s' (rccl | a2a | p2p)", name);
+    if (strcmp(name, "ll") == 0) {
+        if (comm->group->transport != INCCL_TRANSPORT_RCCL)
+            return inccl_set_error(INCCL_ERR_ARG, "ll engine needs a multi-process (rccl) group");
+        if (comm->ll_max_bytes == 0) return inccl_set_error(INCCL_ERR_ARG, "ll engine disabled (INCCL_LL_MAX_BYTES=0)");
+        comm->engine = INCCL_ENGINE_LL;
+        return 0;
+    }
+    return inccl_set_error(INCCL_ERR_ARG, "unknown engine '%s' (rccl | a2a | p2p | ll)", name);
 }
 
 const char *inccl_comm_engine(const struct inccl_communicator *comm)
 {
     if (!comm) return "";
     if (comm->group->transport == INCCL_TRANSPORT_LOCAL) return "local";
-    return comm->engine == INCCL_ENGINE_P2P ? "p2p" : (comm->engine == INCCL_ENGINE_A2A ? "a2a" : "rccl");
+    switch (comm->engine) {
+        case INCCL_ENGINE_P2P: return "p2p";
+        case INCCL_ENGINE_A2A: return "a2a";
+        case INCCL_ENGINE_LL: return "ll";
+        default: return "rccl";
+    }
 }
 
 int inccl_comm_barrier(struct inccl_communicator *comm)
@@ -507,8 +522,12 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
         return kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, k,
                                    amax, scale_R, st));
 
-    if (c->engine == INCCL_ENGINE_P2P && c->group->transport == INCCL_TRANSPORT_RCCL)
+    /* the IPC engines: one kernel for small buckets (ll.c), else the sharded p2p exchange */
+    if ((c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL) && c->group->transport == INCCL_TRANSPORT_RCCL) {
+        if (n <= c->ll_max_bytes / sizeof(float))
+            return inccl_ll_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
         return inccl_p2p_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+    }
     if (c->engine == INCCL_ENGINE_A2A && c->group->transport == INCCL_TRANSPORT_RCCL) {
         if (W > INCCL_MAX_LOCAL_INPUTS)
             return inccl_set_error(INCCL_ERR_ARG, "a2a engine sums at most %d shards", INCCL_MAX_LOCAL_INPUTS);

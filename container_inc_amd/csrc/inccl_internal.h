@@ -21,6 +21,7 @@
 #define INCCL_ENGINE_RCCL 0
 #define INCCL_ENGINE_P2P 1
 #define INCCL_ENGINE_A2A 2
+#define INCCL_ENGINE_LL 3
 
 struct inccl_local_hub;
 struct inccl_shm_bar;
@@ -70,6 +71,17 @@ struct inccl_communicator {
     float *p2p_res;              /* this rank's dequantised shard lives at rank * shard */
     int32_t *p2p_peer_part[INCCL_MAX_LOCAL_INPUTS];
     float *p2p_peer_res[INCCL_MAX_LOCAL_INPUTS];
+    /* ll engine (small buckets, one kernel per call): one IPC buffer per rank =
+     * signal array + two parity data slots; epoch = calls so far */
+    char *ll_buf;
+    char *ll_peer[INCCL_MAX_LOCAL_INPUTS];
+    size_t ll_cap;               /* elements per data slot */
+    uint32_t ll_epoch;
+    uint32_t *ll_err_host;       /* host-mapped: set by a kernel whose peers timed out */
+    uint32_t *ll_err_dev;
+    uint64_t ll_timeout_ticks;
+    hipStream_t ll_last_stream;  /* ordering across caller streams (ev[7]) */
+    size_t ll_max_bytes;         /* buckets up to this size take the ll kernel */
     struct inccl_copy_pool *pool;  /* host staging copies (copypool.c) */
     hipEvent_t ev[8];
 };
@@ -102,6 +114,11 @@ int inccl_rccl_alltoall_q32(struct inccl_communicator *c, const int32_t *send, i
 int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
                     const uint32_t *amax, int scale_R, hipStream_t st);
 void inccl_p2p_release(struct inccl_communicator *c);
+
+/* ll engine (ll.c): n <= c->ll_max_bytes / 4 */
+int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
+                   const uint32_t *amax, int scale_R, hipStream_t st);
+void inccl_ll_release(struct inccl_communicator *c);
 
 /* local transport */
 struct inccl_local_hub *inccl_hub_attach(const char *name, int world_size);

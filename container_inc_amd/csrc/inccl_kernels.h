@@ -23,6 +23,28 @@ void inccl_k_set_tuning(int grid_cap, int nt_loads);
 int inccl_k_gather(const void *const *src, const int64_t *off, const int64_t *cnt, int nseg, void *dst,
                    void *stream);
 
+/* the one-kernel small-bucket allreduce (inccl_ll.hip) */
+#define INCCL_LL_MAX_BLOCKS 256   /* workgroups per call = flags per rank in a signal array */
+struct inccl_ll_launch {
+    const float *src[INCCL_MAX_LOCAL_INPUTS];
+    int R;
+    float *dst;
+    size_t n;
+    uint32_t *own_data;                                /* this call's parity slot */
+    const uint32_t *peer_data[INCCL_MAX_LOCAL_INPUTS]; /* per rank, [me] = own_data */
+    uint32_t *peer_sig[INCCL_MAX_LOCAL_INPUTS];        /* per rank signal arrays (W x MAX_BLOCKS words) */
+    const uint32_t *own_sig;
+    uint32_t *err;                                     /* device view of a host-mapped word */
+    uint32_t epoch;
+    int W, me;
+    uint64_t timeout_ticks;
+    int scale_exp;
+    const uint32_t *amax_bits;
+    int scale_R;
+};
+int inccl_k_ll_grid(size_t n);
+int inccl_k_ll_oneshot(const struct inccl_ll_launch *l, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -119,10 +119,14 @@ int inccl_comm_barrier(struct inccl_communicator *comm);
  *           sum + dequantise kernel over the W shards -> ncclAllGather
  *   "p2p"   library buffers shared via HIP IPC; each GPU pulls its shard from every
  *           peer over xGMI with the fused sum+dequantise kernel, then pulls every
- *           peer's result shard (two group barriers per call)
+ *           peer's result shard (two group barriers per call); buckets up to
+ *           $INCCL_LL_MAX_BYTES (default 1 MiB) take the "ll" kernel instead
+ *   "ll"    one kernel per call: quant + local sum into an IPC buffer, arrival flags
+ *           written into the peers' memory, every peer's bucket read over xGMI and
+ *           summed + dequantised; no host synchronisation (larger buckets: as "p2p")
  * Every rank must select the same engine.  $INCCL_ENGINE sets it at creation. */
 int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name);
-/* "rccl", "a2a", "p2p" or "local" */
+/* "rccl", "a2a", "p2p", "ll" or "local" */
 const char *inccl_comm_engine(const struct inccl_communicator *comm);
 
 /* Device-resident fp32 allreduce of R local buckets per rank:

@@ -33,9 +33,11 @@ def _inputs(world, R, n, seed):
     return out
 
 
-def _rank_main(rank, world, port, cases, q):
+def _rank_main(rank, world, port, cases, q, engine="p2p"):
     try:
-        os.environ["INCCL_ENGINE"] = "p2p"
+        os.environ["INCCL_ENGINE"] = engine
+        if engine == "p2p":
+            os.environ["INCCL_LL_MAX_BYTES"] = "0"   # the sharded exchange at every size
         os.environ["INCCL_DEVICE"] = "0"
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
         import sys
@@ -47,23 +49,27 @@ def _rank_main(rank, world, port, cases, q):
         grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port)
         assert grp is not None, "group create failed"
         comm = inccl.inccl_communicator_create(grp, 0)
-        assert comm is not None and comm.engine == "p2p"
+        assert comm is not None and comm.engine == engine
+        side = torch.cuda.Stream(device=dev)
         results = []
-        for (R, n, k, seed) in cases:
+        for case in cases:
+            R, n, k, seed = case[:4]
+            shift = case[4] if len(case) > 4 else 0   # element offset: unaligned src/dst
             xs = _inputs(world, R, n, seed)
             every = [x for per in xs for x in per]
             kk = O.choose_scale(O.absmax(every), world * R) if k == "auto" else k
             want = O.reduce_f32(every, kk)
-            srcs = [torch.from_numpy(x).to(dev) for x in xs[rank]]
-            out = torch.full((n,), float("nan"), device=dev)
-            for _ in range(4):   # repeated: buffer reuse across calls
+            srcs = [torch.from_numpy(np.concatenate([np.zeros(shift, np.float32), x])).to(dev)[shift:]
+                    for x in xs[rank]]
+            out = torch.full((n + shift,), float("nan"), device=dev)[shift:]
+            for it in range(4):   # repeated: buffer reuse across calls (and across two streams)
                 comm.allreduce_f32(srcs, out=out, scale_exp=inccl.SCALE_AUTO if k == "auto" else k,
-                                   stream=comm.stream)
+                                   stream=comm.stream if it % 2 == 0 else side.cuda_stream)
                 torch.cuda.synchronize()
                 got = out.cpu().numpy()
                 results.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
             # back to back with no host synchronisation in between (the bench's timed loop)
-            outs = [torch.full((n,), float("nan"), device=dev) for _ in range(12)]
+            outs = [torch.full((n + shift,), float("nan"), device=dev)[shift:] for _ in range(12)]
             for o in outs:
                 comm.allreduce_f32(srcs, out=o, scale_exp=inccl.SCALE_AUTO if k == "auto" else k,
                                    stream=comm.stream)
@@ -77,13 +83,23 @@ def _rank_main(rank, world, port, cases, q):
         q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_p2p_engine_multiprocess(gpu, world):
-    cases = [(2, 1 << 20, 25, 11), (1, 100_003, 20, 12), (2, 65_536 * 3 + 5, "auto", 13), (2, 4 << 20, 24, 14)]
+P2P_CASES = [(2, 1 << 20, 25, 11), (1, 100_003, 20, 12), (2, 65_536 * 3 + 5, "auto", 13), (2, 4 << 20, 24, 14),
+             (2, 300_001, 25, 15, 1)]
+# the ll kernel: tiny, ragged, unaligned, one workgroup, the 256-workgroup cap, the
+# 1 MiB slot exactly, and one bucket above it (served by the p2p exchange)
+LL_CASES = [(2, 1, 25, 21), (1, 1000, 20, 22), (3, 4099, 25, 23, 1), (2, 65_536 * 3 + 5, "auto", 24),
+            (8, 262_144, 22, 25), (2, 262_143, 25, 26, 3), (2, 300_000, 25, 27)]
+
+
+@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "ll"), (3, "ll")])
+def test_p2p_engine_multiprocess(gpu, world, engine):
+    """One process per rank on GPU 0 (IPC between processes; the same code as
+    across xGMI).  "p2p" at large buckets, "ll" (one kernel, device flags)."""
+    cases = P2P_CASES if engine == "p2p" else LL_CASES
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_rank_main, args=(r, world, port, cases, q)) for r in range(world)]
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, cases, q, engine)) for r in range(world)]
     for p in ps:
         p.start()
     res = {}
@@ -100,3 +116,60 @@ def test_p2p_engine_multiprocess(gpu, world):
         ok, err = res[r]
         assert err is None, f"rank {r}: {err}"
         assert all(ok), f"rank {r}: {ok}"
+
+
+def _timeout_main(rank, port, q):
+    """rank 1 skips the second call: rank 0's kernel must time out, finish, and
+    report the failure on the next call instead of hanging the GPU."""
+    try:
+        os.environ["INCCL_ENGINE"] = "ll"
+        os.environ["INCCL_DEVICE"] = "0"
+        os.environ["INCCL_BOOT_TIMEOUT"] = "120"
+        os.environ["INCCL_LL_TIMEOUT_MS"] = "300"
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        from container_inc_amd import inccl
+        dev = torch.device("cuda:0")
+        grp = inccl.inccl_group_create(2, rank, "127.0.0.1", port=port)
+        comm = inccl.inccl_communicator_create(grp, 0)
+        x = [torch.ones(4096, device=dev)]
+        out = torch.empty(4096, device=dev)
+        comm.allreduce_f32(x, out=out, scale_exp=20)
+        torch.cuda.synchronize()
+        first_ok = bool((out == 2).all().item())
+        err = None
+        if rank == 0:
+            comm.allreduce_f32(x, out=out, scale_exp=20)   # the peer never arrives
+            torch.cuda.synchronize()
+            try:
+                comm.allreduce_f32(x, out=out, scale_exp=20)
+            except Exception as e:  # noqa: BLE001
+                err = repr(e)
+        comm.destroy()
+        grp.destroy()
+        q.put((rank, first_ok, err))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, False, "crash " + repr(e)))
+
+
+def test_ll_engine_peer_timeout(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_timeout_main, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(2):
+            r, ok, err = q.get(timeout=240)
+            res[r] = (ok, err)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert res[0][0] and res[1][0], res
+    assert res[1][1] is None, res
+    assert res[0][1] is not None and "timed out" in res[0][1], res
