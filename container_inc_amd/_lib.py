@@ -58,6 +58,8 @@ SIGNATURES = {
     "inccl_allreduce_f32_pipelined": (_I, [_P, _P, _I, _P, _SZ, _I, _I, _P]),
     "inccl_allreduce_q32": (_I, [_P, _P, _P, _SZ, _P]),
     "inccl_allreduce_f32_host": (_I, [_P, _P, _P, _SZ, _I, _SZ]),
+    "inccl_host_register": (_I, [_P, _P, _SZ]),
+    "inccl_host_deregister": (_I, [_P, _P]),
     "inccl_switch_create": (_P, [_I, _U32, _I]),
     "inccl_switch_destroy": (_I, [_P]),
     "inccl_switch_reset": (_I, [_P, _P]),

@@ -323,6 +323,10 @@ int inccl_communicator_destroy(struct inccl_communicator *comm)
         inccl_ll_release(comm);
     }
     inccl_rccl_comm_destroy(comm);
+    if (comm->copy_streams[0]) hipStreamSynchronize(comm->copy_streams[0]);
+    if (comm->copy_streams[1]) hipStreamSynchronize(comm->copy_streams[1]);
+    for (int i = 0; i < comm->nreg; ++i) hipHostUnregister(comm->reg[i].p);
+    comm->nreg = 0;
     if (comm->d_q32) hipFree(comm->d_q32);
     if (comm->d_f32) hipFree(comm->d_f32);
     if (comm->d_stage) hipFree(comm->d_stage);
@@ -624,6 +628,74 @@ static int ensure_staging(struct inccl_communicator *c, size_t half_bytes)
     return 0;
 }
 
+int inccl_host_register(struct inccl_communicator *c, void *ptr, size_t bytes)
+{
+    if (!c || !ptr || !bytes) return inccl_set_error(INCCL_ERR_ARG, "bad host_register args");
+    if (c->nreg >= INCCL_MAX_HOST_REGIONS)
+        return inccl_set_error(INCCL_ERR_ARG, "host_register: at most %d ranges", INCCL_MAX_HOST_REGIONS);
+    for (int i = 0; i < c->nreg; ++i)
+        if ((char *)ptr < c->reg[i].p + c->reg[i].len && c->reg[i].p < (char *)ptr + bytes)
+            return inccl_set_error(INCCL_ERR_ARG, "host_register: range overlaps a registered one");
+    INCCL_HIP(hipSetDevice(c->group->device));
+    INCCL_HIP(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    c->reg[c->nreg].p = (char *)ptr;
+    c->reg[c->nreg].len = bytes;
+    c->nreg++;
+    return 0;
+}
+
+int inccl_host_deregister(struct inccl_communicator *c, void *ptr)
+{
+    if (!c || !ptr) return inccl_set_error(INCCL_ERR_ARG, "bad host_deregister args");
+    for (int i = 0; i < c->nreg; ++i)
+        if (c->reg[i].p == (char *)ptr) {
+            INCCL_HIP(hipStreamSynchronize(c->copy_streams[0]));
+            INCCL_HIP(hipStreamSynchronize(c->copy_streams[1]));
+            INCCL_HIP(hipHostUnregister(ptr));
+            c->reg[i] = c->reg[--c->nreg];
+            return 0;
+        }
+    return inccl_set_error(INCCL_ERR_ARG, "host_deregister: %p is not a registered range", ptr);
+}
+
+static int host_registered(const struct inccl_communicator *c, const void *p, size_t bytes)
+{
+    for (int i = 0; i < c->nreg; ++i)
+        if ((const char *)p >= c->reg[i].p && (const char *)p + bytes <= c->reg[i].p + c->reg[i].len) return 1;
+    return 0;
+}
+
+/* src and dst registered: no host copies, the DMA engines read and write the
+ * caller's memory.  Chunk i's H2D overlaps chunk i-1's D2H (PCIe is full
+ * duplex); two device buffers ping-pong. */
+static int allreduce_host_q32_registered(struct inccl_communicator *c, const int32_t *src, size_t n, int32_t *dst)
+{
+    const size_t CH = ((size_t)16 << 20) / sizeof(int32_t);
+    int rc = inccl_ensure_dev(&c->d_stage, &c->d_stage_bytes, 2 * CH * sizeof(int32_t));
+    if (rc) return rc;
+    int32_t *d[2] = {(int32_t *)c->d_stage, (int32_t *)c->d_stage + CH};
+    hipStream_t h2d = c->copy_streams[0], d2h = c->copy_streams[1], ks = c->stream;
+    hipEvent_t e_h2d[2] = {c->ev[0], c->ev[1]}, e_ar[2] = {c->ev[2], c->ev[3]}, e_d2h[2] = {c->ev[4], c->ev[5]};
+    INCCL_HIP(hipStreamSynchronize(ks));
+    const size_t nch = (n + CH - 1) / CH;
+    for (size_t i = 0; i < nch; ++i) {
+        const int s = (int)(i & 1);
+        const size_t off = i * CH, cnt = (n - off) < CH ? (n - off) : CH;
+        if (i >= 2) INCCL_HIP(hipStreamWaitEvent(h2d, e_d2h[s], 0));    /* d[s] drained by chunk i-2 */
+        INCCL_HIP(hipMemcpyAsync(d[s], src + off, cnt * sizeof(int32_t), hipMemcpyHostToDevice, h2d));
+        INCCL_HIP(hipEventRecord(e_h2d[s], h2d));
+        INCCL_HIP(hipStreamWaitEvent(ks, e_h2d[s], 0));
+        rc = inccl_tp_allreduce_q32(c, d[s], d[s], cnt, ks);            /* the switch's sum, nts.c:361-363 */
+        if (rc) return rc;
+        INCCL_HIP(hipEventRecord(e_ar[s], ks));
+        INCCL_HIP(hipStreamWaitEvent(d2h, e_ar[s], 0));
+        INCCL_HIP(hipMemcpyAsync(dst + off, d[s], cnt * sizeof(int32_t), hipMemcpyDeviceToHost, d2h));
+        INCCL_HIP(hipEventRecord(e_d2h[s], d2h));
+    }
+    INCCL_HIP(hipStreamSynchronize(d2h));
+    return 0;
+}
+
 /* Replaces api.c:403-452 / :330-401.  The reference encodes 1024-element
  * messages into the registered buffer (api.c:300-302), lets the switch add
  * them and decodes completions into dst (api.c:428-430), two messages in
@@ -641,6 +713,8 @@ static int allreduce_host_q32(struct inccl_communicator *c, const int32_t *src, 
     if (n == 0) return 0;
     if (!src || !dst) return inccl_set_error(INCCL_ERR_ARG, "NULL src/dst");
     INCCL_HIP(hipSetDevice(c->group->device));
+    if (host_registered(c, src, n * sizeof(int32_t)) && host_registered(c, dst, n * sizeof(int32_t)))
+        return allreduce_host_q32_registered(c, src, n, dst);
     /* chunk: what the reference buffers hold, at least 1 MiB, at most 16 MiB */
     size_t chunk_bytes = c->payload_buf_size / 2;
     if (chunk_bytes < ((size_t)1 << 20)) chunk_bytes = (size_t)1 << 20;

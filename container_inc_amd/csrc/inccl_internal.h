@@ -22,6 +22,7 @@
 #define INCCL_ENGINE_P2P 1
 #define INCCL_ENGINE_A2A 2
 #define INCCL_ENGINE_LL 3
+#define INCCL_MAX_HOST_REGIONS 16
 
 struct inccl_local_hub;
 struct inccl_shm_bar;
@@ -82,6 +83,10 @@ struct inccl_communicator {
     uint64_t ll_timeout_ticks;
     hipStream_t ll_last_stream;  /* ordering across caller streams (ev[7]) */
     size_t ll_max_bytes;         /* buckets up to this size take the ll kernel */
+    /* host memory registered by the caller (inccl_host_register, the ibv_reg_mr of
+     * api.c:170-176): the host collectives DMA such ranges directly */
+    struct { char *p; size_t len; } reg[INCCL_MAX_HOST_REGIONS];
+    int nreg;
     struct inccl_copy_pool *pool;  /* host staging copies (copypool.c) */
     hipEvent_t ev[8];
 };

@@ -242,6 +242,17 @@ class Communicator:
     def allreduce_sendrecv(self, src: np.ndarray, length: int, dst: np.ndarray) -> None:
         _host_int32_call(load().inccl_allreduce_sendrecv, self.handle, src, length, dst)
 
+    def host_register(self, a) -> None:
+        """Pin a host array for direct DMA by allreduce_write / _sendrecv (the
+        reference registers its payload buffers with ibv_reg_mr, api.c:170-176).
+        Keep `a` alive until host_deregister or destroy."""
+        p, nbytes = _host_buf(a)
+        check(load().inccl_host_register(self.handle, p, nbytes), "inccl_host_register")
+
+    def host_deregister(self, a) -> None:
+        p, _ = _host_buf(a)
+        check(load().inccl_host_deregister(self.handle, p), "inccl_host_deregister")
+
     # -- additive device API --
     def allreduce_f32(self, srcs, out=None, scale_exp: int = 25, chunks: int = 1, stream=None):
         torch = _torch()
@@ -283,6 +294,17 @@ class Communicator:
             rc = load().inccl_communicator_destroy(self.handle)
             self.handle = None
         return rc
+
+
+def _host_buf(a):
+    if isinstance(a, np.ndarray):
+        if not a.flags["C_CONTIGUOUS"]:
+            raise ValueError("expected a contiguous numpy array")
+        return a.ctypes.data, a.nbytes
+    torch = _torch()
+    if isinstance(a, torch.Tensor) and a.device.type == "cpu" and a.is_contiguous():
+        return a.data_ptr(), a.numel() * a.element_size()
+    raise ValueError("expected a contiguous numpy array or CPU tensor")
 
 
 def _host_ptr(a, np_dtype, name):

@@ -146,6 +146,16 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *comm, const float *
  * without the host copies. */
 int inccl_allreduce_q32(struct inccl_communicator *comm, const int32_t *src_dev, int32_t *dst_dev, size_t n,
                         void *stream);
+/* Register caller host memory with a communicator -- the analogue of the
+ * reference's ibv_reg_mr on its payload buffers (api.c:170-176).  It is pinned
+ * (hipHostRegister) until inccl_host_deregister or communicator destroy, and
+ * inccl_allreduce_write / _sendrecv whose src and dst both lie inside registered
+ * ranges DMA them directly instead of staging them through the communicator's
+ * pinned buffers (no host copies).  At most 16 ranges per communicator.
+ * The memory must stay allocated while registered. */
+int inccl_host_register(struct inccl_communicator *comm, void *ptr, size_t bytes);
+int inccl_host_deregister(struct inccl_communicator *comm, void *ptr);
+
 /* Host-memory fp32 allreduce (BASELINE config 3): src/dst in host memory,
  * pipelined H2D / reduce / D2H over `bucket_bytes` buckets on three streams.
  * Synchronous. */

@@ -96,6 +96,51 @@ def test_allreduce_write_random_ragged(gpu, orc, world):
         assert np.all(dst[37 * 1024:] == 77)
 
 
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_allreduce_write_registered(gpu, orc, world):
+    """Registered src/dst (the ibv_reg_mr analogue): direct DMA, several 16 MiB
+    chunks + a ragged tail, then the same arrays unregistered (staging path);
+    a partially registered call (dst only) also takes the staging path."""
+    from container_inc_amd import inccl
+    n = 1024 * (4096 * 9 + 3) + 77          # 9 chunks of 16 MiB + 3 messages + a partial one
+    m = n // 1024 * 1024
+    rng = np.random.default_rng(40 + world)
+    xs = [rng.integers(INT32_MIN, INT32_MAX, n, dtype=np.int64, endpoint=True).astype(np.int32) for _ in range(world)]
+    want = orc.sum_q32(xs)
+    hub = f"reg-{world}"
+
+    def rank(r):
+        grp = (inccl.inccl_group_create(1, 0, "127.0.0.1") if world == 1
+               else inccl.inccl_group_create_local(world, r, hub))
+        comm = inccl.inccl_communicator_create(grp, 1 << 20)
+        src = xs[r].copy()
+        dst = np.full(n, 5, np.int32)
+        comm.host_register(src)
+        comm.host_register(dst)
+        with pytest.raises(RuntimeError):
+            comm.host_register(dst[10:])          # overlaps a registered range
+        outs = []
+        comm.allreduce_write(src, n, dst)
+        outs.append(dst.copy())
+        comm.allreduce_write(src, n, dst)         # again: buffers reused
+        outs.append(dst.copy())
+        comm.host_deregister(src)
+        dst[:] = 5
+        comm.allreduce_write(src, n, dst)         # dst registered only -> staging
+        outs.append(dst.copy())
+        comm.host_deregister(dst)
+        with pytest.raises(RuntimeError):
+            comm.host_deregister(dst)
+        comm.destroy()
+        grp.destroy()
+        return outs
+
+    for outs in _run_ranks(world, rank):
+        for dst in outs:
+            np.testing.assert_array_equal(dst[:m], want[:m])
+            assert np.all(dst[m:] == 5)
+
+
 @pytest.mark.parametrize("world,R,n,chunks,k", [
     (2, 2, 1 << 20, 1, 25),
     (2, 2, (1 << 20) + 77, 3, 25),

@@ -78,17 +78,20 @@ def main():
 
     # reference API: inccl_allreduce_write on host int32
     for world, label in ((1, "rccl world 1"), (2, "local 2 ranks (threads, one GPU)")):
-        for mib in (4, 64, 256):
+        for reg, mib in [(reg, mib) for reg in (False, True) for mib in (4, 64, 256)]:
             ne = (mib << 20) // 4
             srcs = [np.arange(ne, dtype=np.int32) * (r + 1) for r in range(world)]
             times = [0.0] * world
-            hub = f"hb-{world}-{mib}"
+            hub = f"hb-{world}-{mib}-{int(reg)}"
 
             def rank(r):
                 g = (inccl.inccl_group_create(1, 0, "127.0.0.1") if world == 1
                      else inccl.inccl_group_create_local(world, r, hub))
                 c = inccl.inccl_communicator_create(g, 8 << 20)
                 dst = np.empty(ne, np.int32)
+                if reg:   # inccl_host_register: direct DMA, no staging copies
+                    c.host_register(srcs[r])
+                    c.host_register(dst)
                 c.allreduce_write(srcs[r], ne, dst)   # warm
                 t0 = time.perf_counter()
                 reps = 3
@@ -107,6 +110,7 @@ def main():
                 t.join()
             dt = max(t[0] for t in times)
             print(json.dumps({"what": "inccl_allreduce_write host int32", "transport": label, "bucket_mib": mib,
+                              "registered": reg,
                               "ms": round(dt * 1e3, 3), "GBs_per_rank": round((mib << 20) / dt / 1e9, 3),
                               "correct": all(t[1] for t in times)}), flush=True)
 
