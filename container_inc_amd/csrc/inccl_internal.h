@@ -73,11 +73,10 @@ struct inccl_communicator {
     int32_t *p2p_peer_part[INCCL_MAX_LOCAL_INPUTS];
     float *p2p_peer_res[INCCL_MAX_LOCAL_INPUTS];
     /* ll engine (small buckets, one kernel per call): one IPC buffer per rank =
-     * signal array + two parity data slots; epoch = calls so far */
+     * signal array + call counter + two parity data slots */
     char *ll_buf;
     char *ll_peer[INCCL_MAX_LOCAL_INPUTS];
     size_t ll_cap;               /* elements per data slot */
-    uint32_t ll_epoch;
     uint32_t *ll_err_host;       /* host-mapped: set by a kernel whose peers timed out */
     uint32_t *ll_err_dev;
     uint64_t ll_timeout_ticks;

@@ -30,12 +30,13 @@ struct inccl_ll_launch {
     int R;
     float *dst;
     size_t n;
-    uint32_t *own_data;                                /* this call's parity slot */
-    const uint32_t *peer_data[INCCL_MAX_LOCAL_INPUTS]; /* per rank, [me] = own_data */
+    uint32_t *own_data;                                /* own data slot 0; slot 1 at + slot_elems */
+    const uint32_t *peer_data[INCCL_MAX_LOCAL_INPUTS]; /* every rank's slot 0, [me] = own_data */
+    size_t slot_elems;
     uint32_t *peer_sig[INCCL_MAX_LOCAL_INPUTS];        /* per rank signal arrays (W x MAX_BLOCKS words) */
     const uint32_t *own_sig;
+    uint32_t *ctr;                                     /* own device words: [0] calls done, [1] workgroups retired */
     uint32_t *err;                                     /* device view of a host-mapped word */
-    uint32_t epoch;
     int W, me;
     uint64_t timeout_ticks;
     int scale_exp;

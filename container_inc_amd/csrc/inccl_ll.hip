@@ -17,12 +17,14 @@
 // Each rank reads the whole bucket from every peer ("one shot"), which is the
 // right trade while a call is latency-bound, i.e. for buckets up to ~1 MiB.
 //
-// Buffer reuse.  The data buffers alternate by call parity.  A rank writes the
-// parity-p buffer in call e only after its call e-1 saw every peer's flag for
+// Buffer reuse.  The data slots alternate by call parity.  A rank writes the
+// parity-p slot in call e only after its call e-1 saw every peer's flag for
 // call e-1, which those peers raise only after their call e-2 kernel (the last
-// reader of the parity-p buffer) completed: kernels of one rank are ordered on
+// reader of the parity-p slot) completed: kernels of one rank are ordered on
 // its stream (the host side adds an event wait when the caller switches
 // streams).  Flags carry the call number (epoch), so they never need resetting.
+// The epoch lives on the device (read by every workgroup at its start, advanced
+// by the last one to retire), so a captured hipGraph replays correctly.
 //
 // Termination.  Every wait is bounded by a wall-clock timeout; a rank whose
 // peers never arrive sets a host-visible error word and finishes the kernel,
@@ -45,12 +47,13 @@ struct LLArgs {
     SrcPtrs src;                    // R local fp32 buckets
     float* dst;
     int64_t n;                      // elements
-    uint32_t* own_data;             // this call's parity slot of the own buffer
-    const uint32_t* peer_data[kMaxR];   // every rank's parity slot ([me] = own_data)
+    uint32_t* own_data;             // own data slot 0 (slot 1 at + slot_elems)
+    const uint32_t* peer_data[kMaxR];   // every rank's slot 0 ([me] = own_data)
+    int64_t slot_elems;
     uint32_t* peer_sig[kMaxR];      // every rank's signal array ([me] unused)
     const uint32_t* own_sig;
+    uint32_t* ctr;                  // [0] calls completed on this rank, [1] workgroups retired
     uint32_t* err;                  // host-mapped error word
-    uint32_t epoch;
     int W, me;
     uint64_t timeout_ticks;         // s_memrealtime ticks
     Scale sc;
@@ -67,9 +70,12 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
     const int64_t nq = (a.n + 3) >> 2;
     const int64_t stride = (int64_t)gridDim.x * kLLBlock;
     const int tid = threadIdx.x;
+    // this call's number, kept on the device so that graph replays advance it too
+    const uint32_t epoch = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const int64_t slot = (int64_t)(epoch & 1u) * a.slot_elems;
 
-    // 1. quantise + local sum into the own data buffer (padding lanes are 0)
-    u32x4* own = reinterpret_cast<u32x4*>(a.own_data);
+    // 1. quantise + local sum into the own data slot (padding lanes are 0)
+    u32x4* own = reinterpret_cast<u32x4*>(a.own_data + slot);
     for (int64_t q = (int64_t)blockIdx.x * kLLBlock + tid; q < nq; q += stride) {
         u32x4 acc = {0u, 0u, 0u, 0u};
         if (vec_src && 4 * q + 4 <= a.n) {
@@ -102,13 +108,13 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
     // 2. arrival flag into every peer (release at system scope: L2 written back first)
     const int flag = a.me * INCCL_LL_MAX_BLOCKS + blockIdx.x;
     if (tid < a.W && tid != a.me)
-        __hip_atomic_store(a.peer_sig[tid] + flag, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.peer_sig[tid] + flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 
     // 3. wait for every peer's workgroup blockIdx.x (bounded)
     if (tid < a.W && tid != a.me) {
         const uint32_t* s = a.own_sig + tid * INCCL_LL_MAX_BLOCKS + blockIdx.x;
         const uint64_t t0 = now_ticks();
-        while ((int32_t)(__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
+        while ((int32_t)(__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
             if (now_ticks() - t0 > a.timeout_ticks) {
                 __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
@@ -124,7 +130,7 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
     for (int64_t q = (int64_t)blockIdx.x * kLLBlock + tid; q < nq; q += stride) {
         u32x4 acc = {0u, 0u, 0u, 0u};
         for (int j = 0; j < a.W; ++j) {
-            const u32x4 x = reinterpret_cast<const u32x4*>(a.peer_data[j])[q];
+            const u32x4 x = reinterpret_cast<const u32x4*>(a.peer_data[j] + slot)[q];
             acc.x += x.x;
             acc.y += x.y;
             acc.z += x.z;
@@ -141,6 +147,16 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
             const uint32_t v[4] = {o.x, o.y, o.z, o.w};
             for (int e = 0; e < 4; ++e)
                 if (4 * q + e < a.n) reinterpret_cast<uint32_t*>(a.dst)[4 * q + e] = v[e];
+        }
+    }
+
+    // 5. retire: the last workgroup advances the call counter for the next call
+    //    (every workgroup read it at its start, before retiring)
+    if (tid == 0) {
+        const uint32_t done = __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == gridDim.x - 1) {
+            __hip_atomic_store(a.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -184,13 +200,14 @@ extern "C" int inccl_k_ll_oneshot(const struct inccl_ll_launch* l, void* stream)
     a.dst = l->dst;
     a.n = (int64_t)l->n;
     a.own_data = l->own_data;
+    a.slot_elems = (int64_t)l->slot_elems;
     for (int j = 0; j < l->W; ++j) {
         a.peer_data[j] = l->peer_data[j];
         a.peer_sig[j] = l->peer_sig[j];
     }
     a.own_sig = l->own_sig;
+    a.ctr = l->ctr;
     a.err = l->err;
-    a.epoch = l->epoch;
     a.W = l->W;
     a.me = l->me;
     a.timeout_ticks = l->timeout_ticks;

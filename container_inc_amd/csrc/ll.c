@@ -8,10 +8,11 @@
  * (non_termination_switch.c:361-365) kept in HBM.
  *
  * Per rank, one device allocation shared over HIP IPC:
- *   [0, SIG)                     signal array: W x INCCL_LL_MAX_BLOCKS words,
+ *   [0, 32 KiB)                  signal array: W x INCCL_LL_MAX_BLOCKS words,
  *                                word [j][b] = last call whose block b of rank j arrived
- *   [SIG, SIG + cap*4)           data slot of even calls (int32 partial sums)
- *   [SIG + cap*4, SIG + 2*cap*4) data slot of odd calls
+ *   [32 KiB, +8)                 call counter + retired-workgroup count (own use)
+ *   [64 KiB, +cap*4)             data slot of even calls (int32 partial sums)
+ *   [64 KiB + cap*4, +cap*4)     data slot of odd calls
  * Created collectively on the first ll call (all ranks make the same calls). */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -21,7 +22,8 @@
 #include "inccl_internal.h"
 #include "inccl_kernels.h"
 
-#define LL_SIG_BYTES ((size_t)65536)   /* >= 8 x 256 words, keeps the data slots 64 KiB aligned */
+#define LL_SIG_BYTES ((size_t)65536)   /* signals + counters; keeps the data slots 64 KiB aligned */
+#define LL_CTR_OFFSET ((size_t)32768)  /* after the 8 x 256 signal words */
 
 void inccl_ll_release(struct inccl_communicator *c)
 {
@@ -85,7 +87,6 @@ static int ll_ensure(struct inccl_communicator *c)
             return rc;
         }
     c->ll_cap = cap;
-    c->ll_epoch = 0;
     c->ll_last_stream = NULL;
     if (c->ll_timeout_ticks == 0) {
         int khz = 0;
@@ -103,38 +104,49 @@ int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R
                    const uint32_t *amax, int scale_R, hipStream_t st)
 {
     const int W = c->group->world_size, me = c->group->rank;
+    if (!c->ll_buf) {   /* the collective setup cannot run inside a graph capture */
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        INCCL_HIP(hipStreamIsCapturing(st, &cap));
+        if (cap != hipStreamCaptureStatusNone)
+            return inccl_set_error(INCCL_ERR_STATE, "ll: make one call outside graph capture first (collective setup)");
+    }
     int rc = ll_ensure(c);
     if (rc) return rc;
     if (n > c->ll_cap) return inccl_set_error(INCCL_ERR_ARG, "ll: %zu elements exceed the slot (%zu)", n, c->ll_cap);
     if (*(volatile uint32_t *)c->ll_err_host)
         return inccl_set_error(INCCL_ERR_STATE, "ll: an earlier call timed out waiting for a peer (results invalid)");
-    const uint32_t epoch = ++c->ll_epoch;
-    const size_t slot = LL_SIG_BYTES + (size_t)(epoch & 1u) * c->ll_cap * sizeof(uint32_t);
     struct inccl_ll_launch l;
     memset(&l, 0, sizeof(l));
     for (int r = 0; r < R; ++r) l.src[r] = srcs[r];
     l.R = R;
     l.dst = dst;
     l.n = n;
-    l.own_data = (uint32_t *)(c->ll_buf + slot);
+    l.own_data = (uint32_t *)(c->ll_buf + LL_SIG_BYTES);
+    l.slot_elems = c->ll_cap;
     for (int j = 0; j < W; ++j) {
-        l.peer_data[j] = (const uint32_t *)(c->ll_peer[j] + slot);
+        l.peer_data[j] = (const uint32_t *)(c->ll_peer[j] + LL_SIG_BYTES);
         l.peer_sig[j] = (uint32_t *)c->ll_peer[j];
     }
     l.own_sig = (const uint32_t *)c->ll_buf;
+    l.ctr = (uint32_t *)(c->ll_buf + LL_CTR_OFFSET);
     l.err = c->ll_err_dev;
-    l.epoch = epoch;
     l.W = W;
     l.me = me;
     l.timeout_ticks = c->ll_timeout_ticks;
     l.scale_exp = k;
     l.amax_bits = amax;
     l.scale_R = scale_R;
-    /* the parity argument needs this rank's calls in order: chain across streams */
-    if (c->ll_last_stream && c->ll_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[7], 0));
+    /* the parity argument needs this rank's calls in order: chain across streams
+     * (inside a graph capture the caller's single capture stream orders them) */
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    INCCL_HIP(hipStreamIsCapturing(st, &cap));
+    const int capturing = cap != hipStreamCaptureStatusNone;
+    if (!capturing && c->ll_last_stream && c->ll_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[7], 0));
     rc = inccl_k_ll_oneshot(&l, st);
     if (rc) return inccl_set_error(INCCL_ERR_HIP, "ll kernel launch failed (%d)", rc);
-    INCCL_HIP(hipEventRecord(c->ev[7], st));
-    c->ll_last_stream = st;
+    if (!capturing) {
+        INCCL_HIP(hipEventRecord(c->ev[7], st));
+        c->ll_last_stream = st;
+    }
     return 0;
 }

@@ -76,6 +76,35 @@ def _rank_main(rank, world, port, cases, q, engine="p2p"):
             torch.cuda.synchronize()
             for o in outs:
                 results.append(bool(np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32))))
+        if engine == "ll":
+            # hipGraph: three calls captured once, replayed with fresh inputs (the
+            # call counter lives on the device, so every replay is a new call)
+            n = 5000
+            bufs = [torch.empty(n, device=dev) for _ in range(2)]
+            outs = [torch.empty(n, device=dev) for _ in range(3)]
+            cs = torch.cuda.Stream(device=dev)
+            graph = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(graph, stream=cs):
+                for o in outs:
+                    comm.allreduce_f32(bufs, out=o, scale_exp=24, stream=cs.cuda_stream)
+            for rep in range(5):
+                xs = _inputs(world, 2, n, 100 + rep)
+                want = O.reduce_f32([x for per in xs for x in per], 24)
+                for b, x in zip(bufs, xs[rank]):
+                    b.copy_(torch.from_numpy(x))
+                for o in outs:
+                    o.fill_(float("nan"))
+                torch.cuda.synchronize()
+                graph.replay()
+                torch.cuda.synchronize()
+                for o in outs:
+                    results.append(bool(np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32))))
+            # eager calls keep working after the replays
+            comm.allreduce_f32(bufs, out=outs[0], scale_exp=24, stream=comm.stream)
+            torch.cuda.synchronize()
+            results.append(bool(np.array_equal(outs[0].cpu().numpy().view(np.uint32), want.view(np.uint32))))
+            del graph
         comm.destroy()
         grp.destroy()
         q.put((rank, results, None))

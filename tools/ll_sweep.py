@@ -53,8 +53,27 @@ def rank_main(rank, port, q):
             torch.cuda.synchronize()
             res[eng] = round(e0.elapsed_time(e1) * 1e3 / iters, 2)
             outs[eng] = out.clone()
+            if eng == "ll":   # the same calls captured in a hipGraph and replayed
+                per = 20
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, stream=st):
+                    for _ in range(per):
+                        comm.allreduce_f32(srcs, out=out, scale_exp=25, stream=st.cuda_stream)
+                with torch.cuda.stream(st):   # replay() launches on the current stream
+                    graph.replay()
+                    torch.cuda.synchronize()
+                    comm.barrier()
+                    e0.record(st)
+                    for _ in range(iters // per):
+                        graph.replay()
+                    e1.record(st)
+                torch.cuda.synchronize()
+                res["ll_graph"] = round(e0.elapsed_time(e1) * 1e3 / (iters // per * per), 2)
+                outs["ll_graph"] = out.clone()
+                del graph
         rows.append({"bucket_bytes": b, "us_per_call_p2p": res["p2p"], "us_per_call_ll": res["ll"],
-                     "bit_equal": bool(torch.equal(outs["p2p"], outs["ll"]))})
+                     "us_per_call_ll_graph": res["ll_graph"],
+                     "bit_equal": bool(torch.equal(outs["p2p"], outs["ll"]) and torch.equal(outs["p2p"], outs["ll_graph"]))})
     for comm in comms.values():
         comm.destroy()
     grp.destroy()
@@ -87,6 +106,7 @@ def main():
         row = dict(row0)
         row["us_per_call_p2p"] = max(row0["us_per_call_p2p"], row1["us_per_call_p2p"])
         row["us_per_call_ll"] = max(row0["us_per_call_ll"], row1["us_per_call_ll"])
+        row["us_per_call_ll_graph"] = max(row0["us_per_call_ll_graph"], row1["us_per_call_ll_graph"])
         row["bit_equal"] = row0["bit_equal"] and row1["bit_equal"]
         row["setup"] = "2 processes sharing one MI355X (IPC on one device), R=2 fp32 buckets, k=25"
         row["ll_grid_cap"] = a.grid_cap or 64
