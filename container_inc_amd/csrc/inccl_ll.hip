@@ -61,7 +61,22 @@ struct LLArgs {
 
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
-template <int R>
+// System-scope (sc0 sc1) word access: write-through on store, cache-bypassing
+// on load -- the WT protocol's data path needs no L2 writeback or invalidate.
+__device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// WT = false: plain data accesses ordered by a system-scope release (buffer_wbl2)
+//             on the flag store and an acquire (buffer_inv) after the wait.
+// WT = true:  data written through and read around the caches (sc0 sc1), so the
+//             flag store only has to follow the data stores' completion.
+template <int R, bool WT>
 __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, int vec_dst)
 {
     const int k = resolve_k(a.sc);
@@ -101,14 +116,25 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
             acc.z = s[2];
             acc.w = s[3];
         }
-        own[q] = acc;
+        if constexpr (WT) {
+            uint32_t* w = a.own_data + slot + 4 * q;
+            st_sys(w, acc.x);
+            st_sys(w + 1, acc.y);
+            st_sys(w + 2, acc.z);
+            st_sys(w + 3, acc.w);
+        } else {
+            own[q] = acc;
+        }
     }
+    if constexpr (WT) __builtin_amdgcn_s_waitcnt(0);   // own stores acknowledged at system scope
     __syncthreads();   // every lane's stores issued and complete at workgroup scope
 
     // 2. arrival flag into every peer (release at system scope: L2 written back first)
     const int flag = a.me * INCCL_LL_MAX_BLOCKS + blockIdx.x;
-    if (tid < a.W && tid != a.me)
-        __hip_atomic_store(a.peer_sig[tid] + flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid < a.W && tid != a.me) {
+        if constexpr (WT) st_sys(a.peer_sig[tid] + flag, epoch);
+        else __hip_atomic_store(a.peer_sig[tid] + flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 
     // 3. wait for every peer's workgroup blockIdx.x (bounded)
     if (tid < a.W && tid != a.me) {
@@ -121,20 +147,28 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope: invalidates stale lines
+        if constexpr (!WT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope: invalidates stale lines
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // every wave, before reading peer memory
+    if constexpr (!WT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // every wave, before reading peer memory
 
     // 4. sum the W ranks' quads, dequantise into dst
     for (int64_t q = (int64_t)blockIdx.x * kLLBlock + tid; q < nq; q += stride) {
         u32x4 acc = {0u, 0u, 0u, 0u};
         for (int j = 0; j < a.W; ++j) {
-            const u32x4 x = reinterpret_cast<const u32x4*>(a.peer_data[j] + slot)[q];
-            acc.x += x.x;
-            acc.y += x.y;
-            acc.z += x.z;
-            acc.w += x.w;
+            if constexpr (WT) {
+                const uint32_t* w = a.peer_data[j] + slot + 4 * q;
+                acc.x += ld_sys(w);
+                acc.y += ld_sys(w + 1);
+                acc.z += ld_sys(w + 2);
+                acc.w += ld_sys(w + 3);
+            } else {
+                const u32x4 x = reinterpret_cast<const u32x4*>(a.peer_data[j] + slot)[q];
+                acc.x += x.x;
+                acc.y += x.y;
+                acc.z += x.z;
+                acc.w += x.w;
+            }
         }
         u32x4 o;
         o.x = __float_as_uint((float)(int32_t)acc.x * inv);
@@ -164,7 +198,13 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
 template <int R>
 hipError_t launch_R(const LLArgs& a, int grid, int vs, int vd, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_ll_oneshot<R>, dim3(grid), dim3(kLLBlock), 0, st, a, vs, vd);
+    static int wt = -1;   // $INCCL_LL_PROTOCOL: "wt" (default) or "fence"; same on every rank
+    if (wt < 0) {
+        const char* e = getenv("INCCL_LL_PROTOCOL");
+        wt = (e && e[0] == 'f') ? 0 : 1;
+    }
+    if (wt) hipLaunchKernelGGL((k_ll_oneshot<R, true>), dim3(grid), dim3(kLLBlock), 0, st, a, vs, vd);
+    else hipLaunchKernelGGL((k_ll_oneshot<R, false>), dim3(grid), dim3(kLLBlock), 0, st, a, vs, vd);
     return hipGetLastError();
 }
 
