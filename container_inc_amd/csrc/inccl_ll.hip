@@ -61,15 +61,22 @@ struct LLArgs {
 
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
-// System-scope (sc0 sc1) word access: write-through on store, cache-bypassing
-// on load -- the WT protocol's data path needs no L2 writeback or invalidate.
+// System-scope (sc0 sc1) access: write-through on store, L1-bypassing and
+// coherent on load -- the WT protocol's data path needs no L2 writeback or
+// invalidate.  16-B accesses: a 4-B sc1 store costs ~6x a 16-B one per byte
+// (MI355X_MICROARCH.md, store flavours).
 __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v)
 {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p)
+__device__ __forceinline__ void st_sys16(uint32_t* p, u32x4 v)
 {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+constexpr int kAuxSys = 1 | 16;   // buffer instruction cache policy: sc0 | sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 
 // WT = false: plain data accesses ordered by a system-scope release (buffer_wbl2)
@@ -117,11 +124,7 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
             acc.w = s[3];
         }
         if constexpr (WT) {
-            uint32_t* w = a.own_data + slot + 4 * q;
-            st_sys(w, acc.x);
-            st_sys(w + 1, acc.y);
-            st_sys(w + 2, acc.z);
-            st_sys(w + 3, acc.w);
+            st_sys16(a.own_data + slot + 4 * q, acc);
         } else {
             own[q] = acc;
         }
@@ -152,42 +155,61 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
     __syncthreads();
     if constexpr (!WT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // every wave, before reading peer memory
 
-    // 4. sum the W ranks' quads, dequantise into dst
-    for (int64_t q = (int64_t)blockIdx.x * kLLBlock + tid; q < nq; q += stride) {
-        u32x4 acc = {0u, 0u, 0u, 0u};
-        for (int j = 0; j < a.W; ++j) {
-            if constexpr (WT) {
-                const uint32_t* w = a.peer_data[j] + slot + 4 * q;
-                acc.x += ld_sys(w);
-                acc.y += ld_sys(w + 1);
-                acc.z += ld_sys(w + 2);
-                acc.w += ld_sys(w + 3);
-            } else {
-                const u32x4 x = reinterpret_cast<const u32x4*>(a.peer_data[j] + slot)[q];
-                acc.x += x.x;
-                acc.y += x.y;
-                acc.z += x.z;
-                acc.w += x.w;
+    // 4. sum the W ranks' quads, dequantise into dst: all W loads of up to kU
+    //    quads in flight before the first add
+    constexpr int kU = 4;
+    __amdgpu_buffer_rsrc_t peer[kMaxR];
+    if constexpr (WT) {
+#pragma unroll
+        for (int j = 0; j < kMaxR; ++j)
+            if (j < a.W) peer[j] = rsrc(a.peer_data[j] + slot, (uint32_t)(nq * 16));
+    }
+    for (int64_t q0 = (int64_t)blockIdx.x * kLLBlock + tid; q0 < nq; q0 += stride * kU) {
+        u32x4 x[kU][kMaxR];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t q = q0 + u * stride;
+#pragma unroll
+            for (int j = 0; j < kMaxR; ++j) {
+                if (j < a.W && q < nq) {
+                    if constexpr (WT) x[u][j] = __builtin_amdgcn_raw_buffer_load_b128(peer[j], (int)(q * 16), 0, kAuxSys);
+                    else x[u][j] = reinterpret_cast<const u32x4*>(a.peer_data[j] + slot)[q];
+                }
             }
         }
-        u32x4 o;
-        o.x = __float_as_uint((float)(int32_t)acc.x * inv);
-        o.y = __float_as_uint((float)(int32_t)acc.y * inv);
-        o.z = __float_as_uint((float)(int32_t)acc.z * inv);
-        o.w = __float_as_uint((float)(int32_t)acc.w * inv);
-        if (vec_dst && 4 * q + 4 <= a.n) {
-            reinterpret_cast<u32x4*>(a.dst)[q] = o;
-        } else {
-            const uint32_t v[4] = {o.x, o.y, o.z, o.w};
-            for (int e = 0; e < 4; ++e)
-                if (4 * q + e < a.n) reinterpret_cast<uint32_t*>(a.dst)[4 * q + e] = v[e];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t q = q0 + u * stride;
+            if (q >= nq) break;
+            u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < kMaxR; ++j)
+                if (j < a.W) {
+                    acc.x += x[u][j].x;
+                    acc.y += x[u][j].y;
+                    acc.z += x[u][j].z;
+                    acc.w += x[u][j].w;
+                }
+            u32x4 o;
+            o.x = __float_as_uint((float)(int32_t)acc.x * inv);
+            o.y = __float_as_uint((float)(int32_t)acc.y * inv);
+            o.z = __float_as_uint((float)(int32_t)acc.z * inv);
+            o.w = __float_as_uint((float)(int32_t)acc.w * inv);
+            if (vec_dst && 4 * q + 4 <= a.n) {
+                reinterpret_cast<u32x4*>(a.dst)[q] = o;
+            } else {
+                const uint32_t v[4] = {o.x, o.y, o.z, o.w};
+                for (int e = 0; e < 4; ++e)
+                    if (4 * q + e < a.n) reinterpret_cast<uint32_t*>(a.dst)[4 * q + e] = v[e];
+            }
         }
     }
 
     // 5. retire: the last workgroup advances the call counter for the next call
     //    (every workgroup read it at its start, before retiring)
     if (tid == 0) {
-        const uint32_t done = __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        // relaxed: only atomicity matters, the next kernel is ordered by the kernel boundary
+        const uint32_t done = __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (done == gridDim.x - 1) {
             __hip_atomic_store(a.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
