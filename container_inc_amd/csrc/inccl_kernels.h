@@ -19,9 +19,13 @@ int inccl_k_absmax(const float *const *srcs, int R, size_t n, uint32_t *amax_bit
 int inccl_k_checksum(const int32_t *q, size_t n, uint64_t index_base, uint32_t *out_dev, int zero_first,
                      void *stream);
 void inccl_k_set_tuning(int grid_cap, int nt_loads);
-/* dst[off[j] .. off[j]+cnt[j]) = src[j][0 .. cnt[j]) for j < nseg, 4-byte elements, one launch */
-int inccl_k_gather(const void *const *src, const int64_t *off, const int64_t *cnt, int nseg, void *dst,
-                   void *stream);
+/* p2p engine kernels reading peer memory with system-coherent loads (inccl_peer.hip):
+ * dst[i] = dequant(sum_j peers[j][i]), n % 4 == 0, 16-B aligned; and
+ * dst[off[j] .. off[j]+cnt[j]) = src[j][0 .. cnt[j]) for j < nseg, one launch */
+int inccl_k_peer_reduce(const void *const *peers, int W, float *dst, size_t n, int scale_exp,
+                        const uint32_t *amax_bits_dev, int scale_R, void *stream);
+int inccl_k_peer_gather(const void *const *src, const int64_t *off, const int64_t *cnt, int nseg, void *dst,
+                        void *stream);
 
 /* the one-kernel small-bucket allreduce (inccl_ll.hip) */
 #define INCCL_LL_MAX_BLOCKS 256   /* workgroups per call = flags per rank in a signal array */

@@ -56,46 +56,6 @@ __global__ __launch_bounds__(kBlock) void k_stream_scalar(SrcPtrs src, void* __r
     }
 }
 
-// ---- multi-source gather (p2p all-gather): segment j = blockIdx.y ----
-struct Segs {
-    const void* src[kMaxR];
-    int64_t off[kMaxR];
-    int64_t cnt[kMaxR];
-};
-
-constexpr int kGatherU = 4;   // float4 per lane per tile
-
-template <bool VEC>
-__global__ __launch_bounds__(kBlock) void k_gather(Segs s, uint32_t* __restrict__ dst)
-{
-    const int j = blockIdx.y;
-    const int64_t cnt = s.cnt[j];
-    uint32_t* __restrict__ d = dst + s.off[j];
-    const uint32_t* __restrict__ src = reinterpret_cast<const uint32_t*>(s.src[j]);
-    if constexpr (VEC) {
-        const int64_t n4 = cnt >> 2;
-        const int64_t tile = (int64_t)kBlock * kGatherU;
-        for (int64_t base = (int64_t)blockIdx.x * tile; base < n4; base += (int64_t)gridDim.x * tile) {
-            u32x4 v[kGatherU];
-#pragma unroll
-            for (int u = 0; u < kGatherU; ++u) {
-                const int64_t i = base + threadIdx.x + (int64_t)u * kBlock;
-                if (i < n4) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src) + i);
-            }
-#pragma unroll
-            for (int u = 0; u < kGatherU; ++u) {
-                const int64_t i = base + threadIdx.x + (int64_t)u * kBlock;
-                if (i < n4) __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(d) + i);
-            }
-        }
-        if (blockIdx.x == 0)
-            for (int64_t i = (n4 << 2) + threadIdx.x; i < cnt; i += kBlock) d[i] = src[i];
-    } else {
-        for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * kBlock)
-            d[i] = src[i];
-    }
-}
-
 // ---- horizontal reductions: wave64 shuffle -> LDS -> one atomic per block ----
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 {
@@ -328,34 +288,6 @@ int inccl_k_checksum(const int32_t* q, size_t n, uint64_t index_base, uint32_t* 
     const int grid = (int)(blocks < 1 ? 1 : (blocks < cap ? blocks : cap));
     hipLaunchKernelGGL(k_checksum, dim3(grid), dim3(kBlock), 0, st, reinterpret_cast<const uint32_t*>(q),
                        (int64_t)n, index_base, out_dev);
-    return (int)hipGetLastError();
-}
-
-int inccl_k_gather(const void* const* src, const int64_t* off, const int64_t* cnt, int nseg, void* dst, void* stream)
-{
-    if (nseg < 1 || nseg > kMaxR || dst == nullptr) return INCCL_ERR_ARG;
-    Segs s = {};
-    int64_t maxcnt = 0;
-    bool vec = true;
-    for (int j = 0; j < nseg; ++j) {
-        s.src[j] = src[j];
-        s.off[j] = off[j];
-        s.cnt[j] = cnt[j] > 0 ? cnt[j] : 0;
-        if (s.cnt[j] > 0 && src[j] == nullptr) return INCCL_ERR_ARG;
-        maxcnt = s.cnt[j] > maxcnt ? s.cnt[j] : maxcnt;
-        vec = vec && aligned16(src[j]) && aligned16(static_cast<uint32_t*>(dst) + off[j]);
-    }
-    if (maxcnt == 0) return 0;
-    hipStream_t st = (hipStream_t)stream;
-    if (vec) {
-        const int64_t tiles = ((maxcnt >> 2) + (int64_t)kBlock * kGatherU - 1) / ((int64_t)kBlock * kGatherU);
-        const int gx = (int)(tiles < 1 ? 1 : (tiles < 65535 ? tiles : 65535));
-        hipLaunchKernelGGL(k_gather<true>, dim3(gx, nseg), dim3(kBlock), 0, st, s, static_cast<uint32_t*>(dst));
-    } else {
-        const int64_t blocks = (maxcnt + kBlock - 1) / kBlock;
-        const int gx = (int)(blocks < 4096 ? blocks : 4096);
-        hipLaunchKernelGGL(k_gather<false>, dim3(gx, nseg), dim3(kBlock), 0, st, s, static_cast<uint32_t*>(dst));
-    }
     return (int)hipGetLastError();
 }
 

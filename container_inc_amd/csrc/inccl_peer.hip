@@ -1,0 +1,177 @@
+// inccl_peer.hip -- the p2p engine's two kernels that read other GPUs' memory
+// (csrc/p2p.c): the pull reduce-scatter and the all-gather.
+//
+// Peer buffers are mapped over HIP IPC.  Remote VRAM may be cached
+// non-coherently in this GPU's L2, and these kernels re-read the same peer
+// addresses on every call.  So every load of peer memory is a system-scope
+// `buffer_load_dwordx4 ... sc0 sc1`: coherent, L1-bypassing, and 0-3 % slower
+// than a plain 16-B load (MI355X_MICROARCH.md, load flavours).  The producers'
+// plain stores reach memory at their kernel's end-of-kernel release, before
+// the host barrier that separates the phases.
+//
+//   k_peer_reduce<R>:  out[i] = dequant( sum_{j<R} peer_j[i] )   int32 -> fp32
+//       the reference switch's aggregate (non_termination_switch.c:361-363)
+//       over the W ranks' shards, fused with the new dequantise stage
+//   k_peer_gather:     dst[off_j + i] = src_j[i]  for every rank j (blockIdx.y)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "inccl_kernels.h"
+#include "inccl_stream.h"
+
+namespace {
+
+using namespace inccl_dev;
+
+constexpr int kAuxSys = 1 | 16;   // buffer instruction cache policy: sc0 | sc1
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ u32x4 ld_sys16(const void* tile_base, uint32_t tile_bytes, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(rsrc(tile_base, tile_bytes), (int)off, 0, kAuxSys);
+}
+
+template <int R, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_peer_reduce(SrcPtrs src, float* __restrict__ dst, int64_t n4, Scale sc)
+{
+    const float inv = pow2f(-resolve_k(sc));
+    u32x4* __restrict__ out = reinterpret_cast<u32x4*>(dst);
+    for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n4; base += (int64_t)gridDim.x * BLOCK) {
+        const int64_t i = base + threadIdx.x;
+        const int64_t left = n4 - base;
+        const uint32_t tile_bytes = (uint32_t)((left < BLOCK ? left : BLOCK) * 16);
+        u32x4 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r)   // out-of-range lanes read 0 (buffer range check)
+            v[r] = ld_sys16(reinterpret_cast<const u32x4*>(src.p[r]) + base, tile_bytes, threadIdx.x * 16u);
+        if (i < n4) {
+            u32x4 acc = v[0];
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                acc.x += v[r].x;
+                acc.y += v[r].y;
+                acc.z += v[r].z;
+                acc.w += v[r].w;
+            }
+            u32x4 o;
+            o.x = __float_as_uint((float)(int32_t)acc.x * inv);
+            o.y = __float_as_uint((float)(int32_t)acc.y * inv);
+            o.z = __float_as_uint((float)(int32_t)acc.z * inv);
+            o.w = __float_as_uint((float)(int32_t)acc.w * inv);
+            __builtin_nontemporal_store(o, out + i);
+        }
+    }
+}
+
+struct Segs {
+    const void* src[kMaxR];
+    int64_t off[kMaxR];
+    int64_t cnt[kMaxR];
+};
+
+constexpr int kGatherBlock = 256;
+constexpr int kGatherU = 4;   // float4 per lane per tile
+
+__global__ __launch_bounds__(kGatherBlock) void k_peer_gather(Segs s, uint32_t* __restrict__ dst)
+{
+    const int j = blockIdx.y;
+    const int64_t cnt = s.cnt[j];
+    uint32_t* __restrict__ d = dst + s.off[j];
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(s.src[j]);
+    const int64_t n4 = cnt >> 2;
+    const int64_t tile = (int64_t)kGatherBlock * kGatherU;
+    const bool dvec = (reinterpret_cast<uintptr_t>(d) & 15u) == 0;
+    for (int64_t base = (int64_t)blockIdx.x * tile; base < n4; base += (int64_t)gridDim.x * tile) {
+        const int64_t left = n4 - base;
+        const uint32_t tile_bytes = (uint32_t)((left < tile ? left : tile) * 16);
+        const u32x4* tb = reinterpret_cast<const u32x4*>(src) + base;
+        u32x4 v[kGatherU];
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u)
+            v[u] = ld_sys16(tb, tile_bytes, (threadIdx.x + u * kGatherBlock) * 16u);
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u) {
+            const int64_t i = base + threadIdx.x + (int64_t)u * kGatherBlock;
+            if (i < n4) {
+                if (dvec) {
+                    __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(d) + i);
+                } else {
+                    d[4 * i] = v[u].x;
+                    d[4 * i + 1] = v[u].y;
+                    d[4 * i + 2] = v[u].z;
+                    d[4 * i + 3] = v[u].w;
+                }
+            }
+        }
+    }
+    if (blockIdx.x == 0)   // ragged tail of the last shard
+        for (int64_t i = (n4 << 2) + threadIdx.x; i < cnt; i += kGatherBlock)
+            d[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int R>
+hipError_t launch_reduce_R(const SrcPtrs& s, float* dst, int64_t n4, const Scale& sc, hipStream_t st)
+{
+    constexpr int B = Geometry<R>::BLOCK;
+    const int64_t grid = (n4 + B - 1) / B;
+    hipLaunchKernelGGL((k_peer_reduce<R, B>), dim3((unsigned)grid), dim3(B), 0, st, s, dst, n4, sc);
+    return hipGetLastError();
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+extern "C" int inccl_k_peer_reduce(const void* const* peers, int W, float* dst, size_t n, int scale_exp,
+                                   const uint32_t* amax_bits_dev, int scale_R, void* stream)
+{
+    if (W < 1 || W > kMaxR || dst == nullptr || (n & 3) != 0 || !aligned16(dst)) return INCCL_ERR_ARG;
+    if (n == 0) return 0;
+    SrcPtrs s = {};
+    for (int j = 0; j < W; ++j) {
+        if (peers[j] == nullptr || !aligned16(peers[j])) return INCCL_ERR_ARG;
+        s.p[j] = peers[j];
+    }
+    Scale sc{scale_exp, amax_bits_dev, scale_R > 0 ? scale_R : W};
+    const int64_t n4 = (int64_t)(n >> 2);
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    switch (W) {
+        case 1: e = launch_reduce_R<1>(s, dst, n4, sc, st); break;
+        case 2: e = launch_reduce_R<2>(s, dst, n4, sc, st); break;
+        case 3: e = launch_reduce_R<3>(s, dst, n4, sc, st); break;
+        case 4: e = launch_reduce_R<4>(s, dst, n4, sc, st); break;
+        case 5: e = launch_reduce_R<5>(s, dst, n4, sc, st); break;
+        case 6: e = launch_reduce_R<6>(s, dst, n4, sc, st); break;
+        case 7: e = launch_reduce_R<7>(s, dst, n4, sc, st); break;
+        default: e = launch_reduce_R<8>(s, dst, n4, sc, st); break;
+    }
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int inccl_k_peer_gather(const void* const* src, const int64_t* off, const int64_t* cnt, int nseg, void* dst,
+                                   void* stream)
+{
+    if (nseg < 1 || nseg > kMaxR || dst == nullptr) return INCCL_ERR_ARG;
+    Segs s = {};
+    int64_t maxc = 0;
+    for (int j = 0; j < nseg; ++j) {
+        if ((src[j] == nullptr && cnt[j] > 0) || cnt[j] < 0 || !aligned16(src[j])) return INCCL_ERR_ARG;
+        s.src[j] = src[j];
+        s.off[j] = off[j];
+        s.cnt[j] = cnt[j];
+        maxc = cnt[j] > maxc ? cnt[j] : maxc;
+    }
+    if (maxc == 0) return 0;
+    const int64_t tile = (int64_t)kGatherBlock * kGatherU * 4;
+    int64_t gx = (maxc + tile - 1) / tile;
+    if (gx < 1) gx = 1;
+    hipLaunchKernelGGL(k_peer_gather, dim3((unsigned)gx, (unsigned)nseg), dim3(kGatherBlock), 0, (hipStream_t)stream, s,
+                       reinterpret_cast<uint32_t*>(dst));
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}

@@ -17,7 +17,10 @@
  * Buffer reuse is safe without a third barrier: a rank reaches the next
  * call's step-2 barrier only after its own step 5 has drained (the sync in 2),
  * so nobody still reads a `part` or `res` that the next call overwrites.
- * Host barriers cost tens of microseconds; the step moves hundreds of MB. */
+ * Host barriers cost tens of microseconds; the step moves hundreds of MB.
+ * Steps 3 and 5 read peer memory with system-coherent loads (inccl_peer.hip):
+ * IPC-mapped remote VRAM may sit non-coherently in this GPU's L2 from the
+ * previous call. */
 #define _GNU_SOURCE
 #include <stdio.h>
 #include <stdlib.h>
@@ -134,8 +137,7 @@ int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int 
     /* 3. pull shard `me` from every peer, sum, dequantise */
     const void *peer[INCCL_MAX_LOCAL_INPUTS];
     for (int j = 0; j < W; ++j) peer[j] = c->p2p_peer_part[j] + (size_t)me * shard;
-    rc = inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_F32, peer, W, c->p2p_res + (size_t)me * shard, shard, k, amax,
-                        scale_R, st);
+    rc = inccl_k_peer_reduce(peer, W, c->p2p_res + (size_t)me * shard, shard, k, amax, scale_R, st);
     if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p reduce-scatter launch failed (%d)", rc);
     rc = sync_and_barrier(c, st);
     if (rc) return rc;
@@ -148,7 +150,7 @@ int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int 
         off[j] = (int64_t)lo;
         cnt[j] = lo >= n ? 0 : (int64_t)((n - lo) < shard ? (n - lo) : shard);
     }
-    rc = inccl_k_gather(src, off, cnt, W, dst, st);
+    rc = inccl_k_peer_gather(src, off, cnt, W, dst, st);
     if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p gather launch failed (%d)", rc);
     return 0;
 }
