@@ -40,8 +40,9 @@ def parse():
     p.add_argument("--local-buckets", type=int, default=2)
     p.add_argument("--scale-exp", type=int, default=25)
     p.add_argument("--chunks", type=int, default=0, help="pipelined chunks for the rccl engine (0 = tune)")
-    p.add_argument("--engine", default="auto", choices=["auto", "rccl", "a2a", "p2p"],
+    p.add_argument("--engine", default="auto", choices=["auto", "rccl", "ar", "a2a", "p2p", "mesh"],
                    help="N>1 exchange engine; auto = time every candidate during warmup, keep the fastest")
+    p.add_argument("--no-sweep", action="store_true", help="N>1: skip the bucket-size sweep (BASELINE config 5)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--grid-cap", type=int, default=0)
@@ -139,6 +140,56 @@ def cpu_reference_pipeline(seconds: float) -> dict:
                                       f"switch aggregation and ICRC framing, {dt:.1f} s"}
 
 
+def size_sweep(comm, dev, R: int, k: int, rank: int) -> list:
+    """BASELINE config 5 at N > 1: bucket sizes 4 KiB (one reference message,
+    api.h:39) to 64 MiB, per engine: host wall time per call over back-to-back
+    calls (max over ranks), and whether the output is bit-identical to the
+    first engine's.  Buckets up to the ll threshold (1 MiB) take the one-kernel
+    ll engine; rccl / ar run everywhere for comparison."""
+    import torch
+    import torch.distributed as dist
+    rows = []
+    for b in (4 << 10, 64 << 10, 1 << 20, 16 << 20, 64 << 20):
+        n = b // 4
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(7000 + rank)
+        xs = [torch.randn(n, generator=gen, device=dev) for _ in range(R)]
+        out = torch.empty(n, device=dev)
+        st = torch.cuda.Stream(device=dev)
+        ref = None
+        iters = 50 if b <= (1 << 20) else 10
+        for eng in (("rccl", "ar", "ll") if b <= (1 << 20) else ("rccl", "ar", "p2p", "mesh")):
+            ok, dt, same = 1, float("inf"), True
+            try:
+                comm.set_engine(eng)
+                for _ in range(3):
+                    comm.allreduce_f32(xs, out=out, scale_exp=k, stream=st.cuda_stream)
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = out.clone()
+                else:
+                    same = bool(torch.equal(ref, out))
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    comm.allreduce_f32(xs, out=out, scale_exp=k, stream=st.cuda_stream)
+                torch.cuda.synchronize()
+                dt = (time.perf_counter() - t0) / iters
+            except Exception as e:  # noqa: BLE001
+                print(f"rank {rank}: sweep {b} B engine {eng} failed: {e}", file=sys.stderr, flush=True)
+                ok = 0
+            v = torch.tensor([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0],
+                             dtype=torch.float64)
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+            good = v[1].item() == 0.0
+            rows.append({"bucket_bytes": b, "engine": eng, "ok": good,
+                         "us": round(v[0].item() * 1e6, 2) if good else None,
+                         "algbw_GBps": round(b / v[0].item() / 1e9, 2) if good else None,
+                         "bit_identical": v[2].item() == 0.0})
+        del xs, out
+    return rows
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
     PMC summary (profiles/pmc_traffic.json), or None."""
@@ -170,8 +221,8 @@ def main():
     if os.environ.get("INCCL_BENCH_SAME_DEVICE") == "1":
         local_rank = 0
     os.environ.setdefault("INCCL_BOOT_TIMEOUT", "120")
-    if a.engine == "p2p":
-        os.environ["INCCL_ENGINE"] = "p2p"   # no eager RCCL communicator
+    if a.engine in ("p2p", "mesh"):
+        os.environ["INCCL_ENGINE"] = a.engine   # no eager RCCL communicator
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
@@ -208,10 +259,14 @@ def main():
         cands = []
         if a.engine in ("auto", "rccl"):
             cands += [("rccl", c) for c in ([a.chunks] if a.chunks else [1, 4])]
+        if a.engine in ("auto", "ar"):
+            cands.append(("ar", 1))
         if a.engine in ("auto", "a2a"):
             cands.append(("a2a", 1))
         if a.engine in ("auto", "p2p"):
             cands.append(("p2p", 1))
+        if a.engine in ("auto", "mesh"):
+            cands.append(("mesh", 1))
         ref = None
         best = None
         for eng, ch in cands:
@@ -292,16 +347,19 @@ def main():
     k_ms = kev0.elapsed_time(kev1) / kiters
     alg_bytes = (R + 1) * 4 * n
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    per_rank = f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: "
     workload = (f"fused quantise+sum+dequantise of R={R} resident {a.bucket_mib} MiB fp32 buckets, 1 GPU"
-                if world == 1 else
-                (f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: quant+local sum -> RCCL reduce-scatter "
-                 f"int32 -> dequant shard -> RCCL all-gather fp32, {chunks} pipelined chunks")
-                if comm.engine == "rccl" else
-                (f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: quant+local sum -> RCCL all-to-all of "
-                 f"int32 shards -> fused sum+dequant (HIP) -> RCCL all-gather fp32")
-                if comm.engine == "a2a" else
-                (f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: quant+local sum -> p2p pull of every "
-                 f"peer's shard over xGMI with fused sum+dequant -> p2p gather of every result shard"))
+                if world == 1 else per_rank + {
+                    "rccl": f"quant+local sum -> RCCL reduce-scatter int32 -> dequant shard -> RCCL all-gather fp32, "
+                            f"{chunks} pipelined chunks",
+                    "ar": "quant+local sum -> RCCL all-reduce int32 in place -> dequant",
+                    "a2a": "quant+local sum -> RCCL all-to-all of int32 shards -> fused sum+dequant (HIP) -> RCCL "
+                           "all-gather fp32",
+                    "p2p": "quant+local sum -> p2p pull of every peer's shard over xGMI with fused sum+dequant -> p2p "
+                           "gather of every result shard",
+                    "mesh": "one persistent HIP kernel: per-chunk quant+local sum pushed into the owner's inbox over "
+                            "xGMI -> owner's sum+dequant on arrival flags -> pull of every result chunk",
+                }.get(comm.engine, comm.engine))
     kname = "k_stream_vec<F32,F32,R>" if world == 1 else "k_stream_vec<F32,Q32,R>"
     traffic = load_traffic(kname + f" R={R} n={n}")
 
@@ -351,6 +409,9 @@ def main():
         algbw = n * 4 / (ms_per_step * 1e-3) / 1e9
         res["collective"] = {"algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2),
                              "bytes_per_rank": n * 4}
+    if world > 1 and not a.no_sweep:
+        res["sweep"] = size_sweep(comm, dev, R, k, rank)
+        comm.set_engine(chosen[0])
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(n, R, k, a.cpu_seconds)
         res["cpu_baseline_allcores"] = cpu_baseline_allcores(n, R, k, min(a.cpu_seconds, 5.0))

@@ -289,6 +289,7 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     c->comm_id = g->comm_seq++;
     const char *llb = getenv("INCCL_LL_MAX_BYTES");   /* small-bucket one-kernel path; 0 disables */
     c->ll_max_bytes = llb ? (size_t)strtoull(llb, NULL, 0) : ((size_t)1 << 20);
+    if (c->ll_max_bytes > ((size_t)1 << 30)) c->ll_max_bytes = (size_t)1 << 30;   /* 32-bit buffer offsets */
     const char *eng = getenv("INCCL_ENGINE");
     if (eng && *eng && g->transport == INCCL_TRANSPORT_RCCL) {
         int rc = inccl_comm_set_engine(c, eng);
@@ -316,11 +317,12 @@ int inccl_communicator_destroy(struct inccl_communicator *comm)
     if (!comm) return 0;
     if (comm->group->device >= 0) hipSetDevice(comm->group->device);
     if (comm->stream) hipStreamSynchronize(comm->stream);
-    if (comm->p2p_part || comm->ll_buf) {   /* peers may still be reading our IPC buffers */
+    if (comm->p2p_part || comm->ll_buf || comm->mesh_buf) {   /* peers may still be reading our IPC buffers */
         hipDeviceSynchronize();   /* our queued reads of theirs have drained ... */
         inccl_boot_barrier(comm->group);   /* ... and so have everyone else's */
         inccl_p2p_release(comm);
         inccl_ll_release(comm);
+        inccl_mesh_release(comm);
     }
     inccl_rccl_comm_destroy(comm);
     if (comm->copy_streams[0]) hipStreamSynchronize(comm->copy_streams[0]);
@@ -383,6 +385,16 @@ int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name)
         comm->engine = INCCL_ENGINE_P2P;
         return 0;
     }
+    if (strcmp(name, "mesh") == 0) {
+        if (comm->group->transport != INCCL_TRANSPORT_RCCL)
+            return inccl_set_error(INCCL_ERR_ARG, "mesh engine needs a multi-process (rccl) group");
+        comm->engine = INCCL_ENGINE_MESH;
+        return 0;
+    }
+    if (strcmp(name, "ar") == 0) {
+        comm->engine = INCCL_ENGINE_AR;
+        return 0;
+    }
     if (strcmp(name, "ll") == 0) {
         if (comm->group->transport != INCCL_TRANSPORT_RCCL)
             return inccl_set_error(INCCL_ERR_ARG, "ll engine needs a multi-process (rccl) group");
@@ -390,7 +402,7 @@ int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name)
         comm->engine = INCCL_ENGINE_LL;
         return 0;
     }
-    return inccl_set_error(INCCL_ERR_ARG, "unknown engine '%s' (rccl | a2a | p2p | ll)", name);
+    return inccl_set_error(INCCL_ERR_ARG, "unknown engine '%s' (rccl | ar | a2a | p2p | ll | mesh)", name);
 }
 
 const char *inccl_comm_engine(const struct inccl_communicator *comm)
@@ -401,6 +413,8 @@ const char *inccl_comm_engine(const struct inccl_communicator *comm)
         case INCCL_ENGINE_P2P: return "p2p";
         case INCCL_ENGINE_A2A: return "a2a";
         case INCCL_ENGINE_LL: return "ll";
+        case INCCL_ENGINE_MESH: return "mesh";
+        case INCCL_ENGINE_AR: return "ar";
         default: return "rccl";
     }
 }
@@ -526,11 +540,28 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
         return kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, k,
                                    amax, scale_R, st));
 
-    /* the IPC engines: one kernel for small buckets (ll.c), else the sharded p2p exchange */
-    if ((c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL) && c->group->transport == INCCL_TRANSPORT_RCCL) {
-        if (n <= c->ll_max_bytes / sizeof(float))
+    /* the IPC engines: one kernel for small buckets (ll.c), else the one-kernel
+     * mesh exchange (mesh.c) or the host-synchronised p2p exchange (p2p.c) */
+    if ((c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH) &&
+        c->group->transport == INCCL_TRANSPORT_RCCL) {
+        if (n <= c->ll_max_bytes / sizeof(float) && W > 1)
             return inccl_ll_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+        if (c->engine == INCCL_ENGINE_MESH) return inccl_mesh_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
         return inccl_p2p_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+    }
+    /* RCCL's own allreduce on the int32 partials: quant + local sum -> in-place
+     * ncclAllReduce(int32, sum) -> dequantise (the switch aggregate inside RCCL) */
+    if (c->engine == INCCL_ENGINE_AR) {
+        rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
+        if (rc) return rc;
+        int32_t *q = (int32_t *)c->d_q32;
+        rc = kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_Q32, (const void *const *)srcs_dev, R, q, n, k, amax,
+                                 scale_R, st));
+        if (rc) return rc;
+        rc = inccl_tp_allreduce_q32(c, q, q, n, st);
+        if (rc) return rc;
+        const void *s1[1] = {q};
+        return kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, dst_dev, n, k, amax, scale_R, st));
     }
     if (c->engine == INCCL_ENGINE_A2A && c->group->transport == INCCL_TRANSPORT_RCCL) {
         if (W > INCCL_MAX_LOCAL_INPUTS)

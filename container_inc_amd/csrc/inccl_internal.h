@@ -22,6 +22,8 @@
 #define INCCL_ENGINE_P2P 1
 #define INCCL_ENGINE_A2A 2
 #define INCCL_ENGINE_LL 3
+#define INCCL_ENGINE_MESH 4
+#define INCCL_ENGINE_AR 5
 #define INCCL_MAX_HOST_REGIONS 16
 
 struct inccl_local_hub;
@@ -82,6 +84,16 @@ struct inccl_communicator {
     uint64_t ll_timeout_ticks;
     hipStream_t ll_last_stream;  /* ordering across caller streams (ev[7]) */
     size_t ll_max_bytes;         /* buckets up to this size take the ll kernel */
+    /* mesh engine (large buckets, one persistent kernel per call): one IPC buffer
+     * per rank = signal array + counters + inbox (W partial shards) + result shard */
+    char *mesh_buf;
+    char *mesh_peer[INCCL_MAX_LOCAL_INPUTS];
+    size_t mesh_cap;             /* elements per inbox slot / result shard */
+    int mesh_grid;               /* this rank's workgroups per call */
+    uint32_t *mesh_err_host;     /* host-mapped: set by a kernel whose peers timed out */
+    uint32_t *mesh_err_dev;
+    uint64_t mesh_timeout_ticks;
+    hipStream_t mesh_last_stream;  /* ordering across caller streams (ev[6]) */
     /* host memory registered by the caller (inccl_host_register, the ibv_reg_mr of
      * api.c:170-176): the host collectives DMA such ranges directly */
     struct { char *p; size_t len; } reg[INCCL_MAX_HOST_REGIONS];
@@ -123,6 +135,12 @@ void inccl_p2p_release(struct inccl_communicator *c);
 int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
                    const uint32_t *amax, int scale_R, hipStream_t st);
 void inccl_ll_release(struct inccl_communicator *c);
+uint64_t inccl_wait_ticks(struct inccl_group *g);   /* bound of an in-kernel wait */
+
+/* mesh engine (mesh.c) */
+int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
+                     const uint32_t *amax, int scale_R, hipStream_t st);
+void inccl_mesh_release(struct inccl_communicator *c);
 
 /* local transport */
 struct inccl_local_hub *inccl_hub_attach(const char *name, int world_size);

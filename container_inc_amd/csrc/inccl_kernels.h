@@ -50,6 +50,34 @@ struct inccl_ll_launch {
 int inccl_k_ll_grid(size_t n);
 int inccl_k_ll_oneshot(const struct inccl_ll_launch *l, void *stream);
 
+/* the one-kernel large-bucket allreduce (inccl_mesh.hip): push reduce-scatter,
+ * per-chunk arrival flags, pull all-gather */
+#define INCCL_MESH_MAX_CHUNKS 1024   /* chunks per shard = flags per source rank */
+struct inccl_mesh_launch {
+    const float *src[INCCL_MAX_LOCAL_INPUTS];
+    int R;
+    float *dst;
+    size_t n;
+    size_t shard;                                      /* elements per rank's shard, multiple of 64 */
+    size_t chunk;                                      /* elements per chunk, multiple of 64 */
+    size_t inbox_stride;                               /* elements per source slot of an inbox */
+    int nchunks, lag, grid;
+    uint32_t *peer_inbox[INCCL_MAX_LOCAL_INPUTS];      /* every rank's inbox ([me] = own) */
+    const uint32_t *own_inbox;
+    uint32_t *own_res;
+    const uint32_t *peer_res[INCCL_MAX_LOCAL_INPUTS];  /* every rank's result shard */
+    uint32_t *peer_sig[INCCL_MAX_LOCAL_INPUTS];        /* every rank's signal array */
+    const uint32_t *own_sig;
+    uint32_t *ctr;                                     /* own words: calls, retired, ticket, abort */
+    uint32_t *err;                                     /* device view of a host-mapped word */
+    int W, me;
+    uint64_t timeout_ticks;
+    int scale_exp;
+    const uint32_t *amax_bits;
+    int scale_R;
+};
+int inccl_k_mesh(const struct inccl_mesh_launch *l, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -69,14 +69,17 @@ __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v)
 {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ void st_sys16(uint32_t* p, u32x4 v)
-{
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
-}
 constexpr int kAuxSys = 1 | 16;   // buffer instruction cache policy: sc0 | sc1
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes)
 {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+// 16-B system-scope store through a (wave-uniform) buffer resource.  A builtin,
+// not inline asm: the compiler's hazard recognizer must see the store, or it may
+// overwrite the data VGPRs of a >64-bit store before the store has read them.
+__device__ __forceinline__ void st_sys16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, u32x4 v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)byte_off, 0, kAuxSys);
 }
 
 // WT = false: plain data accesses ordered by a system-scope release (buffer_wbl2)
@@ -98,6 +101,7 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
 
     // 1. quantise + local sum into the own data slot (padding lanes are 0)
     u32x4* own = reinterpret_cast<u32x4*>(a.own_data + slot);
+    const __amdgpu_buffer_rsrc_t own_rs = rsrc(a.own_data + slot, (uint32_t)(nq * 16));
     for (int64_t q = (int64_t)blockIdx.x * kLLBlock + tid; q < nq; q += stride) {
         u32x4 acc = {0u, 0u, 0u, 0u};
         if (vec_src && 4 * q + 4 <= a.n) {
@@ -124,7 +128,7 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
             acc.w = s[3];
         }
         if constexpr (WT) {
-            st_sys16(a.own_data + slot + 4 * q, acc);
+            st_sys16(own_rs, (uint32_t)(q * 16), acc);
         } else {
             own[q] = acc;
         }

@@ -1,0 +1,371 @@
+// inccl_mesh.hip -- the "mesh" engine: a whole large-bucket allreduce as ONE
+// persistent kernel per rank, with no host synchronisation and no RCCL.
+//
+// Every GPU is the aggregation switch for its own shard of the bucket
+// (non_termination_switch.c:303-501 keeps one switch per tree; on a fully
+// connected xGMI mesh every rank can be one).  A shard is cut into chunks, and
+// one call is three kinds of work item per chunk c:
+//
+//   push(c, j)   quantise + sum the R local buckets over chunk c of shard j and
+//                write the int32 partial straight into rank j's inbox over xGMI
+//                (the host's encode + RDMA WRITE of api.c:293-327), then raise
+//                arrive[me][c] in rank j's signal array;
+//   reduce(c)    wait until every rank's partial of chunk c of MY shard has
+//                arrived (the switch's arrival bitmap, nts.c:361-365), sum the W
+//                partials from local HBM, dequantise into my result shard, and
+//                raise ready[me][c] in every rank's signal array (the broadcast,
+//                nts.c:447-453);
+//   gather(c, j) wait for ready[j][c], then pull rank j's result chunk over xGMI
+//                into dst (the host's decode, api.c:428-430).
+//
+// Scheduling.  Items are numbered in one global order that every rank shares:
+// slot s holds push(s, *), reduce(s - lag) and gather(s - 2 lag, *).  Workgroups
+// take tickets from a device counter, so items start in that order on every
+// rank, and every item waits only for items of strictly earlier tickets on
+// other ranks.  Hence the earliest unfinished item anywhere never waits, and
+// the call always completes, whatever the grid size and residency (ranks on
+// separate GPUs; ranks sharing one GPU are sized so their grids co-reside).
+// A waiting workgroup holds its CU slot idle, so the host picks `lag` large
+// (default: the whole shard -- every push is taken before the first reduce);
+// the phases still overlap at their seams, quantisation overlaps the pushes'
+// xGMI writes, and both link directions are busy while pushing and gathering.
+//
+// Coherence.  Data crossing GPUs is written with system-scope 16-B stores
+// (`buffer_store_dwordx4 ... sc0 sc1`, write-through) and read with
+// system-scope 16-B buffer loads (`sc0 sc1`), so neither side needs an L2
+// writeback or invalidate; a flag is stored only after the workgroup's data
+// stores are acknowledged (s_waitcnt + barrier).  Flags carry the call number
+// (a device-resident counter, so a captured hipGraph replays correctly) and
+// never need resetting.
+//
+// Buffer reuse without double buffering: rank j pushes call e+1's partial of
+// chunk c into my inbox only after its call e finished, including its gather of
+// my result chunk c, which I raised only after reading that inbox chunk.
+// dst may alias srcs[0]: gather(c, j) waits for ready[j][c], which follows my
+// own push(c, j) -- the last reader of that source range.
+//
+// Termination.  Every wait is bounded by a wall-clock timeout; on expiry the
+// kernel sets a host-mapped error word and a local abort word, and every
+// workgroup leaves its loop: a missing peer costs a reported error, never a
+// hung GPU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "inccl_kernels.h"
+#include "inccl_stream.h"
+
+namespace {
+
+using namespace inccl_dev;
+
+constexpr int kMeshBlock = 256;
+constexpr int kMeshU = 4;   // quads per lane per pass (all loads in flight before the first add)
+constexpr int kAuxSys = 1 | 16;   // buffer instruction cache policy: sc0 | sc1
+
+struct MeshArgs {
+    SrcPtrs src;
+    float* dst;
+    int64_t n;
+    int64_t shard;                       // elements per rank's shard (multiple of 64)
+    int64_t chunk;                       // elements per chunk (multiple of 64)
+    int64_t inbox_stride;                // elements per source slot of an inbox
+    uint32_t* peer_inbox[kMaxR];         // rank j's inbox; my slot at + me * inbox_stride
+    const uint32_t* own_inbox;
+    uint32_t* own_res;
+    const uint32_t* peer_res[kMaxR];
+    uint32_t* peer_sig[kMaxR];           // rank j's signal array ([me] = own)
+    const uint32_t* own_sig;
+    uint32_t* ctr;                       // [0] calls done, [1] retired, [2] ticket, [3] abort
+    uint32_t* err;                       // host-mapped error word
+    uint64_t timeout_ticks;
+    int nchunks, W, me, lag, vec_src, vec_dst;
+    Scale sc;
+};
+
+__device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+// 16-B system-scope store through a (wave-uniform) buffer resource.  A builtin,
+// not inline asm: the compiler's hazard recognizer must see the store, or it may
+// overwrite the data VGPRs of a >64-bit store before the store has read them.
+__device__ __forceinline__ void st_sys16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, u32x4 v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)byte_off, 0, kAuxSys);
+}
+
+__device__ __forceinline__ int arrive_idx(int j, int c) { return j * INCCL_MESH_MAX_CHUNKS + c; }
+__device__ __forceinline__ int ready_idx(int j, int c) { return (kMaxR + j) * INCCL_MESH_MAX_CHUNKS + c; }
+
+// Bounded wait for *f >= epoch (serial-number order).  false: timed out or aborted.
+__device__ bool wait_flag(const MeshArgs& a, const uint32_t* f, uint32_t epoch)
+{
+    const uint64_t t0 = now_ticks();
+    while ((int32_t)(ld_sys(f) - epoch) < 0) {
+        if (__hip_atomic_load(a.ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+        if (now_ticks() - t0 > a.timeout_ticks) {
+            __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+}
+
+__device__ __forceinline__ int64_t chunk_len(const MeshArgs& a, int c)
+{
+    const int64_t rest = a.shard - (int64_t)c * a.chunk;
+    return rest < a.chunk ? rest : a.chunk;
+}
+
+// push(c, j): partial sums of chunk c of shard j -> rank j's inbox, slot me
+template <int R>
+__device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float scale)
+{
+    const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;   // global element index
+    const int64_t nq = chunk_len(a, c) >> 2;
+    const __amdgpu_buffer_rsrc_t out =
+        rsrc(a.peer_inbox[j] + (int64_t)a.me * a.inbox_stride + (int64_t)c * a.chunk, (uint32_t)(nq * 16));
+    const bool full = a.vec_src && lo + 4 * nq <= a.n;
+    for (int64_t q0 = threadIdx.x; q0 < nq; q0 += (int64_t)kMeshBlock * kMeshU) {
+        u32x4 acc[kMeshU];
+        if (full) {
+            u32x4 x[kMeshU][R];
+#pragma unroll
+            for (int u = 0; u < kMeshU; ++u) {
+                const int64_t q = q0 + (int64_t)u * kMeshBlock;
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    x[u][r] = q < nq ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.src.p[r]) + (lo >> 2) + q)
+                                     : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < kMeshU; ++u) {
+                acc[u] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    acc[u].x += quant1(__uint_as_float(x[u][r].x), scale);
+                    acc[u].y += quant1(__uint_as_float(x[u][r].y), scale);
+                    acc[u].z += quant1(__uint_as_float(x[u][r].z), scale);
+                    acc[u].w += quant1(__uint_as_float(x[u][r].w), scale);
+                }
+            }
+        } else {   // ragged end of the bucket / unaligned sources: element-granular, zero past n
+#pragma unroll
+            for (int u = 0; u < kMeshU; ++u) {
+                const int64_t q = q0 + (int64_t)u * kMeshBlock;
+                uint32_t s[4] = {0u, 0u, 0u, 0u};
+                if (q < nq)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int64_t i = lo + 4 * q + e;
+                        if (i < a.n)
+#pragma unroll
+                            for (int r = 0; r < R; ++r) s[e] += quant1(reinterpret_cast<const float*>(a.src.p[r])[i], scale);
+                    }
+                acc[u] = u32x4{s[0], s[1], s[2], s[3]};
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kMeshU; ++u) {
+            const int64_t q = q0 + (int64_t)u * kMeshBlock;
+            if (q < nq) st_sys16(out, (uint32_t)(q * 16), acc[u]);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);   // this lane's stores acknowledged at system scope
+    __syncthreads();                 // ... and every lane's
+    if (threadIdx.x == 0) st_sys(a.peer_sig[j] + arrive_idx(a.me, c), epoch);
+}
+
+// reduce(c): my shard's chunk c = dequant(sum over the W inbox slots)
+__device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
+{
+    bool ok = true;
+    if (threadIdx.x < a.W) ok = wait_flag(a, a.own_sig + arrive_idx(threadIdx.x, c), epoch);
+    if (!__syncthreads_and(ok)) return false;
+    const int64_t nq = chunk_len(a, c) >> 2;
+    const uint32_t bytes = (uint32_t)(nq * 16);
+    __amdgpu_buffer_rsrc_t in[kMaxR];
+#pragma unroll
+    for (int j = 0; j < kMaxR; ++j)
+        in[j] = rsrc(a.own_inbox + (int64_t)(j < a.W ? j : 0) * a.inbox_stride + (int64_t)c * a.chunk, bytes);
+    const __amdgpu_buffer_rsrc_t res = rsrc(a.own_res + (int64_t)c * a.chunk, bytes);
+    for (int64_t q0 = threadIdx.x; q0 < nq; q0 += (int64_t)kMeshBlock * 2) {
+        u32x4 x[2][kMaxR];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int j = 0; j < kMaxR; ++j)   // out-of-range lanes read 0 (buffer range check)
+                x[u][j] = j < a.W ? __builtin_amdgcn_raw_buffer_load_b128(in[j], (int)((q0 + u * kMeshBlock) * 16), 0, kAuxSys)
+                                  : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int64_t q = q0 + (int64_t)u * kMeshBlock;
+            if (q >= nq) break;
+            u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < kMaxR; ++j) {
+                acc.x += x[u][j].x;
+                acc.y += x[u][j].y;
+                acc.z += x[u][j].z;
+                acc.w += x[u][j].w;
+            }
+            u32x4 o;
+            o.x = __float_as_uint((float)(int32_t)acc.x * inv);
+            o.y = __float_as_uint((float)(int32_t)acc.y * inv);
+            o.z = __float_as_uint((float)(int32_t)acc.z * inv);
+            o.w = __float_as_uint((float)(int32_t)acc.w * inv);
+            st_sys16(res, (uint32_t)(q * 16), o);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x < a.W) st_sys(a.peer_sig[threadIdx.x] + ready_idx(a.me, c), epoch);
+    return true;
+}
+
+// gather(c, j): rank j's result chunk c -> dst (clipped to n)
+__device__ bool do_gather(const MeshArgs& a, int c, int j, uint32_t epoch)
+{
+    bool ok = true;
+    if (threadIdx.x == 0) ok = wait_flag(a, a.own_sig + ready_idx(j, c), epoch);
+    if (!__syncthreads_and(ok)) return false;
+    const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;
+    if (lo >= a.n) return true;
+    int64_t cnt = chunk_len(a, c);
+    if (lo + cnt > a.n) cnt = a.n - lo;
+    const int64_t nq = cnt >> 2;
+    const __amdgpu_buffer_rsrc_t src = rsrc(a.peer_res[j] + (int64_t)c * a.chunk, (uint32_t)(chunk_len(a, c) * 4));
+    uint32_t* d = reinterpret_cast<uint32_t*>(a.dst) + lo;
+    for (int64_t q0 = threadIdx.x; q0 < nq; q0 += (int64_t)kMeshBlock * kMeshU) {
+        u32x4 v[kMeshU];
+#pragma unroll
+        for (int u = 0; u < kMeshU; ++u)
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(src, (int)((q0 + u * kMeshBlock) * 16), 0, kAuxSys);
+#pragma unroll
+        for (int u = 0; u < kMeshU; ++u) {
+            const int64_t q = q0 + (int64_t)u * kMeshBlock;
+            if (q < nq) {
+                if (a.vec_dst) {
+                    __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(d) + q);
+                } else {
+                    d[4 * q] = v[u].x;
+                    d[4 * q + 1] = v[u].y;
+                    d[4 * q + 2] = v[u].z;
+                    d[4 * q + 3] = v[u].w;
+                }
+            }
+        }
+    }
+    for (int64_t i = 4 * nq + threadIdx.x; i < cnt; i += kMeshBlock)   // ragged end of the bucket
+        d[i] = __builtin_amdgcn_raw_buffer_load_b32(src, (int)(i * 4), 0, kAuxSys);
+    return true;
+}
+
+template <int R>
+__global__ __launch_bounds__(kMeshBlock) void k_mesh(MeshArgs a)
+{
+    __shared__ int s_ticket;
+    const int k = resolve_k(a.sc);
+    const float scale = pow2f(k);
+    const float inv = pow2f(-k);
+    // this call's number, kept on the device so that graph replays advance it too
+    const uint32_t epoch = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const int W = a.W;
+    const int per_slot = 2 * W + 1;
+    const int total = (a.nchunks + 2 * a.lag) * per_slot;
+    for (;;) {
+        if (threadIdx.x == 0)
+            s_ticket = (int)__hip_atomic_fetch_add(a.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int t = s_ticket;
+        __syncthreads();   // everyone has read s_ticket before it is rewritten
+        if (t >= total) break;
+        const int s = t / per_slot, pos = t - s * per_slot;
+        if (pos < W) {
+            if (s < a.nchunks) do_push<R>(a, s, (a.me + 1 + pos) % W, epoch, scale);
+        } else if (pos == W) {
+            const int c = s - a.lag;
+            if (c >= 0 && c < a.nchunks && !do_reduce(a, c, epoch, inv)) break;
+        } else {
+            const int c = s - 2 * a.lag;
+            if (c >= 0 && c < a.nchunks && !do_gather(a, c, (a.me + pos - W) % W, epoch)) break;
+        }
+    }
+    // retire: the last workgroup resets the ticket and advances the call counter
+    if (threadIdx.x == 0) {
+        const uint32_t done = __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == gridDim.x - 1) {
+            __hip_atomic_store(a.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.ctr + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
+{
+    if (!l || l->R < 1 || l->R > kMaxR || l->W < 1 || l->W > kMaxR || l->me < 0 || l->me >= l->W || l->grid < 1 ||
+        l->nchunks < 1 || l->nchunks > INCCL_MESH_MAX_CHUNKS || l->lag < 1 || (l->shard & 63) || (l->chunk & 63) ||
+        l->chunk == 0 || (size_t)l->nchunks * l->chunk < l->shard || l->shard > l->inbox_stride ||
+        (size_t)l->W * l->shard < l->n || l->chunk > ((size_t)1 << 26))
+        return INCCL_ERR_ARG;
+    MeshArgs a{};
+    for (int r = 0; r < l->R; ++r) a.src.p[r] = l->src[r];
+    a.dst = l->dst;
+    a.n = (int64_t)l->n;
+    a.shard = (int64_t)l->shard;
+    a.chunk = (int64_t)l->chunk;
+    a.inbox_stride = (int64_t)l->inbox_stride;
+    for (int j = 0; j < l->W; ++j) {
+        a.peer_inbox[j] = l->peer_inbox[j];
+        a.peer_res[j] = l->peer_res[j];
+        a.peer_sig[j] = l->peer_sig[j];
+    }
+    a.own_inbox = l->own_inbox;
+    a.own_res = l->own_res;
+    a.own_sig = l->own_sig;
+    a.ctr = l->ctr;
+    a.err = l->err;
+    a.timeout_ticks = l->timeout_ticks;
+    a.nchunks = l->nchunks;
+    a.W = l->W;
+    a.me = l->me;
+    a.lag = l->lag;
+    int vs = 1;
+    for (int r = 0; r < l->R; ++r) vs &= aligned16(l->src[r]) ? 1 : 0;
+    a.vec_src = vs;
+    a.vec_dst = aligned16(l->dst) ? 1 : 0;
+    a.sc.k = l->scale_exp;
+    a.sc.amax_bits = l->amax_bits;
+    a.sc.scale_R = l->scale_R;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 g((unsigned)l->grid), b(kMeshBlock);
+    switch (l->R) {
+        case 1: hipLaunchKernelGGL(k_mesh<1>, g, b, 0, st, a); break;
+        case 2: hipLaunchKernelGGL(k_mesh<2>, g, b, 0, st, a); break;
+        case 3: hipLaunchKernelGGL(k_mesh<3>, g, b, 0, st, a); break;
+        case 4: hipLaunchKernelGGL(k_mesh<4>, g, b, 0, st, a); break;
+        case 5: hipLaunchKernelGGL(k_mesh<5>, g, b, 0, st, a); break;
+        case 6: hipLaunchKernelGGL(k_mesh<6>, g, b, 0, st, a); break;
+        case 7: hipLaunchKernelGGL(k_mesh<7>, g, b, 0, st, a); break;
+        default: hipLaunchKernelGGL(k_mesh<8>, g, b, 0, st, a); break;
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}

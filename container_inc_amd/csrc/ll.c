@@ -88,16 +88,20 @@ static int ll_ensure(struct inccl_communicator *c)
         }
     c->ll_cap = cap;
     c->ll_last_stream = NULL;
-    if (c->ll_timeout_ticks == 0) {
-        int khz = 0;
-        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, g->device >= 0 ? g->device : 0) != hipSuccess ||
-            khz <= 0)
-            khz = 100000;   /* 100 MHz, the CDNA constant clock */
-        const char *t = getenv("INCCL_LL_TIMEOUT_MS");
-        const double ms = t ? atof(t) : 5000.0;
-        c->ll_timeout_ticks = (uint64_t)(ms * (double)khz);
-    }
+    if (c->ll_timeout_ticks == 0) c->ll_timeout_ticks = inccl_wait_ticks(g);
     return 0;
+}
+
+/* device wall-clock ticks of a bounded in-kernel wait: $INCCL_LL_TIMEOUT_MS (5 s) */
+uint64_t inccl_wait_ticks(struct inccl_group *g)
+{
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, g->device >= 0 ? g->device : 0) != hipSuccess ||
+        khz <= 0)
+        khz = 100000;   /* 100 MHz, the CDNA constant clock */
+    const char *t = getenv("INCCL_LL_TIMEOUT_MS");
+    const double ms = t ? atof(t) : 5000.0;
+    return (uint64_t)(ms * (double)khz);
 }
 
 int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,

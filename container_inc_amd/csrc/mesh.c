@@ -1,0 +1,219 @@
+/* mesh.c -- host side of the "mesh" engine: a large-bucket allreduce as one
+ * persistent kernel per rank (work items, schedule and protocol in
+ * inccl_mesh.hip).
+ *
+ * The p2p engine (p2p.c) runs quantise -> barrier -> pull reduce-scatter ->
+ * barrier -> pull all-gather, with two host stream synchronisations per call
+ * and no overlap between the phases.  Here one kernel does the whole call: its
+ * push / reduce / gather items of different chunks meet through flags in HBM,
+ * so quantisation, the local sums and the xGMI traffic in both directions
+ * overlap, and the host never waits.
+ *
+ * Per rank, one device allocation shared over HIP IPC:
+ *   [0, 64 KiB)              signal array: arrive[8][1024] and ready[8][1024] words
+ *   [64 KiB, +16)            call counter, retired workgroups, ticket, abort word
+ *   [128 KiB, +W*cap*4)      inbox: slot j holds rank j's int32 partial of my shard
+ *   [.., +cap*4)             my dequantised result shard (fp32)
+ * Created collectively on the first call, regrown collectively when a larger
+ * bucket arrives (all ranks make the same calls, as with RCCL). */
+#define _GNU_SOURCE
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "inccl_internal.h"
+#include "inccl_kernels.h"
+
+#define MESH_SIG_BYTES ((size_t)2 * INCCL_MAX_LOCAL_INPUTS * INCCL_MESH_MAX_CHUNKS * sizeof(uint32_t))
+#define MESH_CTR_OFFSET MESH_SIG_BYTES
+#define MESH_DATA_OFFSET (MESH_SIG_BYTES + (size_t)65536)
+
+typedef struct {
+    hipIpcMemHandle_t h;
+    int pci_domain, pci_bus, pci_dev;   /* ranks sharing a GPU split its workgroup slots */
+} mesh_peer_info;
+
+void inccl_mesh_release(struct inccl_communicator *c)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    if (!c->mesh_buf) return;
+    hipDeviceSynchronize();
+    for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS; ++j) {
+        if (j != me && c->mesh_peer[j]) hipIpcCloseMemHandle(c->mesh_peer[j]);
+        c->mesh_peer[j] = NULL;
+    }
+    hipFree(c->mesh_buf);
+    c->mesh_buf = NULL;
+    if (c->mesh_err_host) hipHostFree(c->mesh_err_host);
+    c->mesh_err_host = NULL;
+    c->mesh_err_dev = NULL;
+    c->mesh_cap = 0;
+}
+
+/* collective: every rank calls it with the same shard size */
+static int mesh_ensure(struct inccl_communicator *c, size_t shard)
+{
+    struct inccl_group *g = c->group;
+    const int W = g->world_size, me = g->rank;
+    if (c->mesh_buf && c->mesh_cap >= shard) return 0;
+    if (W > INCCL_MAX_LOCAL_INPUTS)
+        return inccl_set_error(INCCL_ERR_ARG, "mesh engine supports up to %d GPUs", INCCL_MAX_LOCAL_INPUTS);
+    if (c->mesh_buf) {   /* peers may still read the old buffers until everyone is here */
+        INCCL_HIP(hipDeviceSynchronize());
+        int rc = inccl_boot_barrier(g);
+        if (rc) return rc;
+        inccl_mesh_release(c);
+    }
+    const size_t cap = (shard + ((size_t)1 << 19) - 1) & ~(((size_t)1 << 19) - 1);   /* 2 MiB granules */
+    const int dev = g->device >= 0 ? g->device : 0;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    mesh_peer_info mine, *all = (mesh_peer_info *)calloc((size_t)W, sizeof(mesh_peer_info));
+    if (!all) return inccl_set_error(INCCL_ERR_NOMEM, "mesh: out of memory");
+    memset(&mine, 0, sizeof(mine));
+    int rc = 0;
+    /* local failures are carried to the collective outcome check below */
+    hipError_t e = hipMalloc((void **)&c->mesh_buf, MESH_DATA_OFFSET + ((size_t)W + 1) * cap * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(c->mesh_buf, 0, MESH_DATA_OFFSET);   /* flags + counters */
+    if (e == hipSuccess) e = hipDeviceSynchronize();   /* zeroed before any peer maps it */
+    if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.h, c->mesh_buf);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&c->mesh_err_host, sizeof(uint32_t), hipHostMallocMapped);
+    if (e == hipSuccess) {
+        *(volatile uint32_t *)c->mesh_err_host = 0;
+        e = hipHostGetDevicePointer((void **)&c->mesh_err_dev, c->mesh_err_host, 0);
+    }
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&mine.pci_domain, hipDeviceAttributePciDomainID, dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&mine.pci_bus, hipDeviceAttributePciBusId, dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&mine.pci_dev, hipDeviceAttributePciDeviceId, dev);
+    if (e != hipSuccess) rc = inccl_hip_check(e, "mesh: buffer setup");
+    /* where everyone is: ranks sharing a GPU size their grids together */
+    int rc_x = inccl_boot_allgather(g, &mine, all, sizeof(mesh_peer_info));
+    if (rc_x) {
+        free(all);
+        return rc_x;
+    }
+    int sharing = 0;
+    for (int j = 0; j < W; ++j)
+        sharing += all[j].pci_domain == mine.pci_domain && all[j].pci_bus == mine.pci_bus &&
+                   all[j].pci_dev == mine.pci_dev;
+    /* two workgroups per CU; ranks sharing one GPU split those slots, so that
+     * their grids co-reside (every k_mesh<R> fits two 256-lane workgroups per CU;
+     * the schedule's progress argument needs each rank to keep one running) */
+    const char *ge = getenv("INCCL_MESH_GRID");
+    int grid = ge ? atoi(ge) : 0;
+    if (grid <= 0) grid = 2 * cus / (sharing > 0 ? sharing : 1);
+    if (grid < 4) grid = 4;
+    for (int j = 0; j < W; ++j) {
+        if (j == me) {
+            c->mesh_peer[j] = c->mesh_buf;
+            continue;
+        }
+        if (rc) continue;
+        void *p = NULL;
+        e = hipIpcOpenMemHandle(&p, all[j].h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) rc = inccl_hip_check(e, "mesh: hipIpcOpenMemHandle");
+        c->mesh_peer[j] = (char *)p;
+    }
+    free(all);
+    /* agree on the outcome, so that every rank falls back alike */
+    int32_t mine_rc = rc ? 1 : 0, all_rc[INCCL_MAX_LOCAL_INPUTS];
+    int rc2 = inccl_boot_allgather(g, &mine_rc, all_rc, sizeof(int32_t));
+    if (rc2) return rc2;
+    for (int j = 0; j < W; ++j)
+        if (all_rc[j]) {
+            if (!rc) rc = inccl_set_error(INCCL_ERR_HIP, "mesh: rank %d could not map the peer buffers", j);
+            inccl_mesh_release(c);
+            return rc;
+        }
+    c->mesh_cap = cap;
+    c->mesh_grid = grid;
+    c->mesh_last_stream = NULL;
+    if (c->mesh_timeout_ticks == 0) c->mesh_timeout_ticks = inccl_wait_ticks(g);
+    return 0;
+}
+
+/* Chunk size: about 256 chunks per shard for overlap, 16-256 KiB each
+ * ($INCCL_MESH_CHUNK elements overrides; same on every rank). */
+static size_t mesh_chunk(size_t shard)
+{
+    const char *ce = getenv("INCCL_MESH_CHUNK");
+    size_t ch = ce ? (size_t)strtoull(ce, NULL, 0) : 0;
+    if (ch == 0) {
+        ch = (shard + 255) / 256;
+        ch = (ch + 4095) & ~(size_t)4095;
+        if (ch > 65536) ch = 65536;
+    }
+    ch = (ch + 63) & ~(size_t)63;
+    if ((shard + ch - 1) / ch > INCCL_MESH_MAX_CHUNKS)
+        ch = ((shard + INCCL_MESH_MAX_CHUNKS - 1) / INCCL_MESH_MAX_CHUNKS + 63) & ~(size_t)63;
+    if (ch > shard) ch = shard;
+    return ch;
+}
+
+int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
+                     const uint32_t *amax, int scale_R, hipStream_t st)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    const size_t shard = inccl_shard_elems(n, W);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    INCCL_HIP(hipStreamIsCapturing(st, &cap));
+    const int capturing = cap != hipStreamCaptureStatusNone;
+    if (capturing && (!c->mesh_buf || c->mesh_cap < shard))   /* collective setup cannot run in a capture */
+        return inccl_set_error(INCCL_ERR_STATE, "mesh: make one call of this size outside graph capture first");
+    int rc = mesh_ensure(c, shard);
+    if (rc) return rc;
+    if (*(volatile uint32_t *)c->mesh_err_host)
+        return inccl_set_error(INCCL_ERR_STATE, "mesh: an earlier call timed out waiting for a peer (results invalid)");
+    const size_t chunk = mesh_chunk(shard);
+    const int nchunks = (int)((shard + chunk - 1) / chunk);
+    /* a reduce / gather starts `lag` slots after what it waits for.  Default: the
+     * whole shard, i.e. every push is taken before the first reduce and every
+     * reduce before the first gather -- a workgroup waiting on a flag holds its
+     * CU slot idle, and on one GPU (256 MiB, R = 2) lag = 1 / 171 / 400 / all
+     * chunks ran 823 / 668 / 474 / 402 us.  Phases still overlap at their
+     * seams, and both xGMI directions are busy in the push and gather phases.
+     * ($INCCL_MESH_LAG slots overrides; same on every rank.) */
+    const char *le = getenv("INCCL_MESH_LAG");
+    int lag = le ? atoi(le) : nchunks;
+    if (lag < 1) lag = 1;
+    if (lag > nchunks) lag = nchunks;
+    struct inccl_mesh_launch l;
+    memset(&l, 0, sizeof(l));
+    for (int r = 0; r < R; ++r) l.src[r] = srcs[r];
+    l.R = R;
+    l.dst = dst;
+    l.n = n;
+    l.shard = shard;
+    l.chunk = chunk;
+    l.inbox_stride = c->mesh_cap;
+    l.nchunks = nchunks;
+    l.lag = lag;
+    l.grid = c->mesh_grid;
+    for (int j = 0; j < W; ++j) {
+        char *base = c->mesh_peer[j];
+        l.peer_inbox[j] = (uint32_t *)(base + MESH_DATA_OFFSET);
+        l.peer_res[j] = (const uint32_t *)(base + MESH_DATA_OFFSET + (size_t)W * c->mesh_cap * sizeof(uint32_t));
+        l.peer_sig[j] = (uint32_t *)base;
+    }
+    l.own_inbox = l.peer_inbox[me];
+    l.own_res = (uint32_t *)l.peer_res[me];
+    l.own_sig = (const uint32_t *)c->mesh_buf;
+    l.ctr = (uint32_t *)(c->mesh_buf + MESH_CTR_OFFSET);
+    l.err = c->mesh_err_dev;
+    l.W = W;
+    l.me = me;
+    l.timeout_ticks = c->mesh_timeout_ticks;
+    l.scale_exp = k;
+    l.amax_bits = amax;
+    l.scale_R = scale_R;
+    /* the buffer-reuse argument needs this rank's calls in order: chain across
+     * streams (inside a capture the caller's capture stream orders them) */
+    if (!capturing && c->mesh_last_stream && c->mesh_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[6], 0));
+    rc = inccl_k_mesh(&l, st);
+    if (rc) return inccl_set_error(rc == INCCL_ERR_ARG ? INCCL_ERR_ARG : INCCL_ERR_HIP, "mesh kernel launch failed (%d)", rc);
+    if (!capturing) {
+        INCCL_HIP(hipEventRecord(c->ev[6], st));
+        c->mesh_last_stream = st;
+    }
+    return 0;
+}

@@ -324,7 +324,7 @@ int inccl_tp_allreduce_q32(struct inccl_communicator *c, const int32_t *send, in
 int inccl_tp_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st)
 {
     if (is_local(c)) return inccl_local_allreduce_max_u32(c, buf, n, st);
-    if ((c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL) && n == 1)
+    if ((c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH) && n == 1)
         return host_allreduce_max_u32(c, buf, st);
     int rc = ensure_rccl(c);
     if (rc) return rc;

@@ -124,9 +124,15 @@ int inccl_comm_barrier(struct inccl_communicator *comm);
  *   "ll"    one kernel per call: quant + local sum into an IPC buffer, arrival flags
  *           written into the peers' memory, every peer's bucket read over xGMI and
  *           summed + dequantised; no host synchronisation (larger buckets: as "p2p")
+ *   "mesh"  one persistent kernel per call for large buckets: each chunk's quantised
+ *           partial is pushed into its owner's IPC inbox over xGMI, the owner sums +
+ *           dequantises it once every rank's arrival flag is up, and every rank pulls
+ *           the result chunks; phases of different chunks overlap, no host
+ *           synchronisation (buckets up to $INCCL_LL_MAX_BYTES: the "ll" kernel)
+ *   "ar"    quant+sum -> ncclAllReduce(int32, sum) in place -> dequant
  * Every rank must select the same engine.  $INCCL_ENGINE sets it at creation. */
 int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name);
-/* "rccl", "a2a", "p2p", "ll" or "local" */
+/* "rccl", "ar", "a2a", "p2p", "ll", "mesh" or "local" */
 const char *inccl_comm_engine(const struct inccl_communicator *comm);
 
 /* Device-resident fp32 allreduce of R local buckets per rank:

@@ -195,17 +195,20 @@ def test_rccl_world1_paths(gpu, orc, force_rccl):
     assert grp is not None and grp.transport == "rccl"
     comm = inccl.inccl_communicator_create(grp, 1 << 20)
     rng = np.random.default_rng(5)
-    for engine in ("rccl", "a2a", "p2p"):
+    for engine in ("rccl", "ar", "a2a", "p2p", "mesh"):
         comm.set_engine(engine)
         assert comm.engine == engine
         for n, chunks in ((1 << 20, 1), ((1 << 20) + 5, 3)):
             xs = [rng.standard_normal(n).astype(np.float32) for _ in range(2)]
             out = comm.allreduce_f32([torch.from_numpy(x).to(gpu) for x in xs], scale_exp=25, chunks=chunks)
+            torch.cuda.synchronize()   # the call ran on the communicator's own (non-blocking) stream
             np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32),
                                           orc.reduce_f32(xs, 25).view(np.uint32), err_msg=engine)
     comm.set_engine("rccl")
     q = rng.integers(INT32_MIN, INT32_MAX, 4096, dtype=np.int64, endpoint=True).astype(np.int32)
-    np.testing.assert_array_equal(comm.allreduce_q32(torch.from_numpy(q).to(gpu)).cpu().numpy(), q)
+    qa = comm.allreduce_q32(torch.from_numpy(q).to(gpu))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(qa.cpu().numpy(), q)
     dst = np.zeros(4096, np.int32)
     comm.allreduce_write(q, 4096, dst)
     np.testing.assert_array_equal(dst, q)

@@ -36,7 +36,7 @@ def _inputs(world, R, n, seed):
 def _rank_main(rank, world, port, cases, q, engine="p2p"):
     try:
         os.environ["INCCL_ENGINE"] = engine
-        if engine == "p2p":
+        if engine in ("p2p", "mesh"):
             os.environ["INCCL_LL_MAX_BYTES"] = "0"   # the sharded exchange at every size
         os.environ["INCCL_DEVICE"] = "0"
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
@@ -76,7 +76,7 @@ def _rank_main(rank, world, port, cases, q, engine="p2p"):
             torch.cuda.synchronize()
             for o in outs:
                 results.append(bool(np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32))))
-        if engine == "ll":
+        if engine in ("ll", "mesh"):
             # hipGraph: three calls captured once, replayed with fresh inputs (the
             # call counter lives on the device, so every replay is a new call)
             n = 5000
@@ -120,11 +120,18 @@ LL_CASES = [(2, 1, 25, 21), (1, 1000, 20, 22), (3, 4099, 25, 23, 1), (2, 65_536 
             (8, 262_144, 22, 25), (2, 262_143, 25, 26, 3), (2, 300_000, 25, 27)]
 
 
-@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "ll"), (3, "ll")])
+# the mesh kernel: one chunk, many chunks (256 per shard), ragged ends inside and
+# beyond the last shard, unaligned buffers, R = 8 local buckets, a 1-element bucket
+MESH_CASES = P2P_CASES + [(1, 1, 25, 31), (8, 3_000_017, 22, 32), (2, (8 << 20) + 3, 25, 33, 2),
+                          (3, 64 * 3 - 1, 24, 34)]
+
+
+@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "ll"), (3, "ll"), (2, "mesh"), (3, "mesh")])
 def test_p2p_engine_multiprocess(gpu, world, engine):
     """One process per rank on GPU 0 (IPC between processes; the same code as
-    across xGMI).  "p2p" at large buckets, "ll" (one kernel, device flags)."""
-    cases = P2P_CASES if engine == "p2p" else LL_CASES
+    across xGMI).  "p2p" at large buckets, "ll" (one kernel, device flags),
+    "mesh" (one persistent kernel, per-chunk flags, push + pull)."""
+    cases = {"p2p": P2P_CASES, "ll": LL_CASES, "mesh": MESH_CASES}[engine]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -147,11 +154,13 @@ def test_p2p_engine_multiprocess(gpu, world, engine):
         assert all(ok), f"rank {r}: {ok}"
 
 
-def _timeout_main(rank, port, q):
+def _timeout_main(rank, port, q, engine="ll"):
     """rank 1 skips the second call: rank 0's kernel must time out, finish, and
     report the failure on the next call instead of hanging the GPU."""
     try:
-        os.environ["INCCL_ENGINE"] = "ll"
+        os.environ["INCCL_ENGINE"] = engine
+        if engine == "mesh":
+            os.environ["INCCL_LL_MAX_BYTES"] = "0"
         os.environ["INCCL_DEVICE"] = "0"
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
         os.environ["INCCL_LL_TIMEOUT_MS"] = "300"
@@ -182,11 +191,12 @@ def _timeout_main(rank, port, q):
         q.put((rank, False, "crash " + repr(e)))
 
 
-def test_ll_engine_peer_timeout(gpu):
+@pytest.mark.parametrize("engine", ["ll", "mesh"])
+def test_engine_peer_timeout(gpu, engine):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_timeout_main, args=(r, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_timeout_main, args=(r, port, q, engine)) for r in range(2)]
     for p in ps:
         p.start()
     res = {}
