@@ -301,7 +301,29 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
         const char *force = getenv("INCCL_FORCE_RCCL");
         if (g->world_size > 1 || (force && atoi(force) != 0)) {
             int rc = inccl_rccl_comm_init(c);
-            if (rc) return rc;
+            if (g->world_size > 1) {
+                /* agree on the outcome: if RCCL cannot come up on every rank (e.g.
+                 * ranks sharing one GPU), every rank switches to the IPC p2p
+                 * engine alike; the rccl engine can still be selected later and
+                 * then reports its own error */
+                int32_t mine = rc ? 1 : 0;
+                int32_t *all = (int32_t *)calloc((size_t)g->world_size, sizeof(int32_t));
+                if (!all) return inccl_set_error(INCCL_ERR_NOMEM, "communicator: out of memory");
+                int rc2 = inccl_boot_allgather(g, &mine, all, sizeof(int32_t));
+                int failed = -1;
+                for (int j = 0; !rc2 && j < g->world_size; ++j)
+                    if (all[j] && failed < 0) failed = j;
+                free(all);
+                if (rc2) return rc2;
+                if (failed >= 0) {
+                    fprintf(stderr, "inccl: RCCL communicator unavailable on rank %d%s%s; using the p2p engine\n",
+                            failed, rc ? ": " : "", rc ? inccl_last_error() : "");
+                    inccl_rccl_comm_destroy(c);
+                    c->engine = INCCL_ENGINE_P2P;
+                }
+            } else if (rc) {
+                return rc;
+            }
         }
     }
     /* int32 workspace of one bucket of `size` bytes up front */

@@ -32,16 +32,23 @@ static int nccl_check(ncclResult_t r, const char *what)
 int inccl_rccl_comm_init(struct inccl_communicator *c)
 {
     struct inccl_group *g = c->group;
-    ncclUniqueId id;
-    memset(&id, 0, sizeof(id));
+    /* rank 0 broadcasts even when it has no id, so that no peer waits on it */
+    struct {
+        int32_t ok;
+        ncclUniqueId id;
+    } u;
+    memset(&u, 0, sizeof(u));
+    int rc0 = 0;
     if (g->rank == 0) {
-        int rc = nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
-        if (rc) return rc;
+        rc0 = nccl_check(ncclGetUniqueId(&u.id), "ncclGetUniqueId");
+        u.ok = rc0 == 0;
     }
-    int rc = inccl_boot_bcast(g, &id, sizeof(id));
+    int rc = inccl_boot_bcast(g, &u, sizeof(u));
     if (rc) return rc;
+    if (rc0) return rc0;
+    if (!u.ok) return inccl_set_error(INCCL_ERR_NCCL, "ncclGetUniqueId failed on rank 0");
     ncclComm_t comm = NULL;
-    rc = nccl_check(ncclCommInitRank(&comm, g->world_size, id, g->rank), "ncclCommInitRank");
+    rc = nccl_check(ncclCommInitRank(&comm, g->world_size, u.id, g->rank), "ncclCommInitRank");
     if (rc) return rc;
     c->nccl = comm;
     return 0;
