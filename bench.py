@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--local-buckets", type=int, default=2)
     p.add_argument("--scale-exp", type=int, default=25)
     p.add_argument("--chunks", type=int, default=0, help="pipelined chunks for the rccl engine (0 = tune)")
-    p.add_argument("--engine", default="auto", choices=["auto", "rccl", "ar", "a2a", "p2p", "mesh"],
+    p.add_argument("--engine", default="auto", choices=["auto", "rccl", "ar", "a2a", "p2p", "mesh", "meshw"],
                    help="N>1 exchange engine; auto = time every candidate during warmup, keep the fastest")
     p.add_argument("--no-sweep", action="store_true", help="N>1: skip the bucket-size sweep (BASELINE config 5)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -156,9 +156,10 @@ def size_sweep(comm, dev, R: int, k: int, rank: int) -> list:
         xs = [torch.randn(n, generator=gen, device=dev) for _ in range(R)]
         out = torch.empty(n, device=dev)
         st = torch.cuda.Stream(device=dev)
+        torch.cuda.synchronize()   # inputs made on torch's stream; the calls run on st
         ref = None
         iters = 50 if b <= (1 << 20) else 10
-        for eng in (("rccl", "ar", "ll") if b <= (1 << 20) else ("rccl", "ar", "p2p", "mesh")):
+        for eng in (("rccl", "ar", "ll") if b <= (1 << 20) else ("rccl", "ar", "p2p", "mesh", "meshw")):
             ok, dt, same = 1, float("inf"), True
             try:
                 comm.set_engine(eng)
@@ -221,7 +222,7 @@ def main():
     if os.environ.get("INCCL_BENCH_SAME_DEVICE") == "1":
         local_rank = 0
     os.environ.setdefault("INCCL_BOOT_TIMEOUT", "120")
-    if a.engine in ("p2p", "mesh"):
+    if a.engine in ("p2p", "mesh", "meshw"):
         os.environ["INCCL_ENGINE"] = a.engine   # no eager RCCL communicator
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -237,6 +238,7 @@ def main():
     gen.manual_seed(1000 + rank)
     srcs = [torch.randn(n, generator=gen, device=dev, dtype=torch.float32) for _ in range(R)]
     out = torch.empty(n, device=dev, dtype=torch.float32)
+    torch.cuda.synchronize()   # inputs made on torch's stream; the library runs on its own
 
     master = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = int(os.environ.get("MASTER_PORT", "29500")) + 17
@@ -267,6 +269,8 @@ def main():
             cands.append(("p2p", 1))
         if a.engine in ("auto", "mesh"):
             cands.append(("mesh", 1))
+        if a.engine in ("auto", "meshw"):
+            cands.append(("meshw", 1))
         ref = None
         best = None
         for eng, ch in cands:
@@ -359,6 +363,9 @@ def main():
                            "gather of every result shard",
                     "mesh": "one persistent HIP kernel: per-chunk quant+local sum pushed into the owner's inbox over "
                             "xGMI -> owner's sum+dequant on arrival flags -> pull of every result chunk",
+                    "meshw": "one persistent HIP kernel: per-chunk quant+local sum pushed into the owner's inbox over "
+                             "xGMI -> owner's sum+dequant on arrival flags, result chunk pushed into every rank's "
+                             "inbox (all xGMI transfers are writes) -> local copy into dst",
                 }.get(comm.engine, comm.engine))
     kname = "k_stream_vec<F32,F32,R>" if world == 1 else "k_stream_vec<F32,Q32,R>"
     traffic = load_traffic(kname + f" R={R} n={n}")

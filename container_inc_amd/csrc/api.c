@@ -283,7 +283,7 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     INCCL_HIP(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
     INCCL_HIP(hipStreamCreateWithFlags(&c->copy_streams[0], hipStreamNonBlocking));
     INCCL_HIP(hipStreamCreateWithFlags(&c->copy_streams[1], hipStreamNonBlocking));
-    for (int i = 0; i < 8; ++i) INCCL_HIP(hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming));
+    for (int i = 0; i < 9; ++i) INCCL_HIP(hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming));
     INCCL_HIP(hipMalloc((void **)&c->d_words, 256));
     INCCL_HIP(hipMemset(c->d_words, 0, 256));
     c->comm_id = g->comm_seq++;
@@ -358,7 +358,7 @@ int inccl_communicator_destroy(struct inccl_communicator *comm)
     inccl_copy_pool_destroy(comm->pool);
     if (comm->send_payload) hipHostFree(comm->send_payload);
     if (comm->receive_payload) hipHostFree(comm->receive_payload);
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 9; ++i)
         if (comm->ev[i]) hipEventDestroy(comm->ev[i]);
     if (comm->copy_streams[0]) hipStreamDestroy(comm->copy_streams[0]);
     if (comm->copy_streams[1]) hipStreamDestroy(comm->copy_streams[1]);
@@ -407,10 +407,11 @@ int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name)
         comm->engine = INCCL_ENGINE_P2P;
         return 0;
     }
-    if (strcmp(name, "mesh") == 0) {
+    if (strcmp(name, "mesh") == 0 || strcmp(name, "meshw") == 0) {
         if (comm->group->transport != INCCL_TRANSPORT_RCCL)
             return inccl_set_error(INCCL_ERR_ARG, "mesh engine needs a multi-process (rccl) group");
         comm->engine = INCCL_ENGINE_MESH;
+        comm->mesh_push = name[4] == 'w';
         return 0;
     }
     if (strcmp(name, "ar") == 0) {
@@ -424,7 +425,7 @@ int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name)
         comm->engine = INCCL_ENGINE_LL;
         return 0;
     }
-    return inccl_set_error(INCCL_ERR_ARG, "unknown engine '%s' (rccl | ar | a2a | p2p | ll | mesh)", name);
+    return inccl_set_error(INCCL_ERR_ARG, "unknown engine '%s' (rccl | ar | a2a | p2p | ll | mesh | meshw)", name);
 }
 
 const char *inccl_comm_engine(const struct inccl_communicator *comm)
@@ -435,7 +436,7 @@ const char *inccl_comm_engine(const struct inccl_communicator *comm)
         case INCCL_ENGINE_P2P: return "p2p";
         case INCCL_ENGINE_A2A: return "a2a";
         case INCCL_ENGINE_LL: return "ll";
-        case INCCL_ENGINE_MESH: return "mesh";
+        case INCCL_ENGINE_MESH: return comm->mesh_push ? "meshw" : "mesh";
         case INCCL_ENGINE_AR: return "ar";
         default: return "rccl";
     }

@@ -5,12 +5,18 @@
 // repository/src/util.c:331-442 (build_eth_packet), :250-286 (compute_icrc),
 // :141-195 (crc32), :106-127 (ipv4_checksum).
 //
-// One wave64 per frame.  A frame is staged in LDS with dword loads; the ICRC
-// input (4 x 0xFF -- the CRC init folded into the message -- then the masked IP
-// .. payload bytes) is right-aligned in a 1088-byte window (64 lanes x 17 B) so
-// leading zeros do not change the raw CRC.  Each lane runs a byte-table CRC over
-// its 17 bytes; a 6-level shuffle tree combines lane CRCs with "append N zero
-// bytes" operators held as 4 x 256-entry tables per level in LDS.
+// One wave64 per frame.  A frame is staged in LDS; the ICRC input (4 x 0xFF --
+// the CRC init folded into the message -- then the masked IP .. payload bytes)
+// is the frame from byte 10 on, with bytes 10-13 and the masked fields set to
+// 0xFF in LDS while the CRC runs.  It is right-aligned in a 1088-byte window
+// (64 lanes x 17 B), so leading zeros do not change the raw CRC.  CRC-32 is
+// linear over GF(2): the window's raw CRC is the XOR over lanes of
+// Z_{17 (63 - lane)}(crc(segment)), Z_n = "append n zero bytes".  Each lane
+// (1) reads its 17 bytes as 6 dwords + byte-aligns them, (2) runs a byte-table
+// CRC through a 32-way replicated table (one copy per ds_read_b32 bank, so the
+// 64 data-dependent lookups of a wave-instruction never conflict), (3) applies
+// its own fixed Z as 8 nibble lookups in a lane-major table (bank = lane), and
+// (4) the wave XOR-reduces.  64 KiB of tables per block.
 //
 // State on the GPU (slots = PSN ring size, power of two; the reference uses 16):
 //   agg[slots][256] int32        aggregator        (nts.c:55)
@@ -31,61 +37,83 @@ constexpr int kWin = 1088;            // 64 lanes x 17 bytes
 constexpr int kSeg = 17;
 constexpr int kFrameMax = 1152;       // staged frame bytes (>= 1098)
 constexpr int kWavesPerBlock = 4;
+constexpr int kIcrcWaves = 8;        // 512-lane blocks, two per CU (74 KiB of LDS each)
 constexpr int kEgressWaves = 8;       // 512-lane blocks, CU-sized persistent grid
 constexpr int kLanes = 256;           // int32 lanes per packet (nts.c:55)
 
 __device__ uint32_t g_crc_tab[256];          // util.c:141-150 table 0
-__device__ uint32_t g_shift_tab[6][4][256];
+__device__ uint32_t g_lane_shift[8][16][kWave];   // [nibble][value][lane] = Z_{17 (63 - lane)}(value << 4 nibble)
 
 struct CrcLds {
-    uint32_t tab[256];
-    uint32_t sh[6][4][256];
+    uint32_t rep[256][32];          // byte table, one copy per ds_read_b32 bank
+    uint32_t lane_sh[8][16][kWave]; // per-lane zero-append operator, nibble-sliced
 };
 
 __device__ __forceinline__ void load_tables(CrcLds& t)
 {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) t.tab[i] = g_crc_tab[i];
-    uint32_t* dst = &t.sh[0][0][0];
-    const uint32_t* src = &g_shift_tab[0][0][0];
-    for (int i = threadIdx.x; i < 6 * 4 * 256; i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) (&t.rep[0][0])[i] = g_crc_tab[i >> 5];
+    uint32_t* dst = &t.lane_sh[0][0][0];
+    const uint32_t* src = &g_lane_shift[0][0][0];
+    for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) dst[i] = src[i];
 }
 
-__device__ __forceinline__ uint8_t frame_byte(const uint8_t* fr, int off)
+// frame bytes that read as 0xFF while the ICRC runs: 10-13 carry the CRC init
+// (the 4 x 0xFF prefix), the rest are the ICRC masks of util.c:266-270 (tos,
+// ttl, IP checksum, UDP checksum, BTH resv8a)
+constexpr int kNumMasked = 11;
+__device__ __forceinline__ int masked_pos(int i)
 {
-    // ICRC masks (util.c:266-270): tos, ttl, IP checksum, UDP checksum, BTH resv8a
-    if (off == 15 || off == 22 || off == 24 || off == 25 || off == 40 || off == 41 || off == 46) return 0xFF;
-    return fr[off];
+    constexpr uint64_t lo = 10ull | 11ull << 8 | 12ull << 16 | 13ull << 24 | 15ull << 32 | 22ull << 40 | 24ull << 48 |
+                            25ull << 56;
+    constexpr uint32_t hi = 40u | 41u << 8 | 46u << 16;
+    return i < 8 ? (int)((lo >> (8 * i)) & 0xFF) : (int)((hi >> (8 * (i - 8))) & 0xFF);
 }
 
-// ICRC of the frame staged at `fr` (LDS); result valid in every lane.
+// ICRC of the frame staged at `fr` (LDS, at least 1152 B, 4-B aligned), whose
+// masked bytes are already 0xFF; result valid in every lane.
 __device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds& t, int lane)
 {
-    const int ip_total = ((int)fr[16] << 8) | fr[17];
-    const int L = ip_total;                       // 4 (init) + ip_total - 4 (no ICRC)
-    const int lead = kWin - L;                    // zero bytes before the message
-    uint8_t b[kSeg];
-#pragma unroll
-    for (int j = 0; j < kSeg; ++j) {
-        const int m = lane * kSeg + j - lead;
-        b[j] = (m < 0) ? (uint8_t)0 : ((m < 4) ? (uint8_t)0xFF : frame_byte(fr, 14 + m - 4));
-    }
-    // byte-table CRC (util.c:190-192 form).  The kernel is bound by LDS lookups,
-    // not by this chain's latency: a slice-by-4 variant (4 KiB of tables, one
-    // block fewer per CU) measured slower in k_egress (356 vs 289 us / 131k frames).
+    const int ip_total = ((int)fr[16] << 8) | fr[17];   // message = 4 (init) + ip_total - 4 (no ICRC) bytes
+    const int lead = kWin - ip_total;                   // zero bytes before the message
+    const int o = 10 + lane * kSeg - lead;              // frame offset of this lane's first byte
     uint32_t c = 0;
+    if (o + kSeg > 10) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(fr);
+        const int d0 = o >> 2;   // floor division (o may be negative)
+        uint32_t dw[6];
 #pragma unroll
-    for (int j = 0; j < kSeg; ++j) c = (c >> 8) ^ t.tab[(c ^ b[j]) & 0xFFu];
-    // tree: at level l the block of lane L (low l bits zero) absorbs block L + 2^l:
-    // crc = shift(crc_left, |right| = 17 * 2^l bytes) ^ crc_right.  Only left lanes
-    // (the block representatives) are updated; lane 0 ends with the whole window.
+        for (int k = 0; k < 6; ++k) dw[k] = d0 + k >= 0 ? w[d0 + k] : 0u;
+        const uint32_t sh = (uint32_t)o & 3u;
+        uint32_t a[5];
 #pragma unroll
-    for (int l = 0; l < 6; ++l) {
-        const uint32_t other = (uint32_t)__shfl_xor((int)c, 1 << l, kWave);
-        const uint32_t shifted =
-            t.sh[l][0][c & 0xFF] ^ t.sh[l][1][(c >> 8) & 0xFF] ^ t.sh[l][2][(c >> 16) & 0xFF] ^ t.sh[l][3][c >> 24];
-        c = shifted ^ other;   // meaningful in left lanes only
+        for (int k = 0; k < 5; ++k) a[k] = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
+        const int nz = 10 - o;   // leading bytes of this lane before the message: zero
+        if (nz > 0) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const int z = nz - 4 * k;
+                a[k] = z >= 4 ? 0u : (z > 0 ? a[k] & (0xFFFFFFFFu << (8 * z)) : a[k]);
+            }
+        }
+        const uint32_t* rep = &t.rep[0][0] + (lane & 31);
+        // byte-table CRC (util.c:190-192 form), a dword at a time
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            c ^= a[k];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) c = (c >> 8) ^ rep[(c & 0xFFu) << 5];
+        }
+        c ^= a[4] & 0xFFu;
+        c = (c >> 8) ^ rep[(c & 0xFFu) << 5];
+        // shift to the window's end: Z_{17 (63 - lane)}(c)
+        uint32_t r = 0;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) r ^= t.lane_sh[n][(c >> (4 * n)) & 15u][lane];
+        c = r;
     }
-    return ~(uint32_t)__shfl((int)c, 0, kWave);
+#pragma unroll
+    for (int l = 0; l < 6; ++l) c ^= (uint32_t)__shfl_xor((int)c, 1 << l, kWave);
+    return ~c;
 }
 
 // stage `bytes` of a global frame into LDS (dword loads; frames are 4-B aligned)
@@ -97,15 +125,15 @@ __device__ __forceinline__ void stage_frame(uint8_t* lds, const uint8_t* g, int 
     for (int i = lane; i < words; i += kWave) dst[i] = src[i];
 }
 
-__global__ __launch_bounds__(kWave* kWavesPerBlock) void k_icrc(const uint8_t* __restrict__ frames, int64_t stride,
+__global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __restrict__ frames, int64_t stride,
                                                                 int64_t count, uint32_t* __restrict__ out)
 {
     __shared__ CrcLds t;
-    __shared__ __attribute__((aligned(16))) uint8_t buf[kWavesPerBlock][kFrameMax];
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kIcrcWaves][kFrameMax];
     load_tables(t);
     __syncthreads();
     const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    for (int64_t f0 = (int64_t)blockIdx.x * kWavesPerBlock; f0 < count; f0 += (int64_t)gridDim.x * kWavesPerBlock) {
+    for (int64_t f0 = (int64_t)blockIdx.x * kIcrcWaves; f0 < count; f0 += (int64_t)gridDim.x * kIcrcWaves) {
         const int64_t f = f0 + w;
         if (f < count) {
             const uint8_t* g = frames + f * stride;
@@ -115,6 +143,8 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_icrc(const uint8_t* _
                 if (lane == 0) out[f] = 0;
             } else {
                 stage_frame(buf[w], g, bytes, lane);
+                __builtin_amdgcn_wave_barrier();
+                if (lane < kNumMasked) buf[w][masked_pos(lane)] = 0xFF;
                 __builtin_amdgcn_wave_barrier();
                 const uint32_t crc = icrc_wave(buf[w], t, lane);
                 if (lane == 0) out[f] = crc;
@@ -242,54 +272,92 @@ __device__ void build_header_image(uint8_t* fr, const InccFrameTemplate& h, bool
     bth[4] = (uint8_t)(q >> 24); bth[5] = (uint8_t)(q >> 16); bth[6] = (uint8_t)(q >> 8); bth[7] = (uint8_t)q;
 }
 
-__device__ void egress_one(const InccSwitchState& s, const uint8_t* __restrict__ in_frames, int64_t in_stride,
-                           const int32_t* __restrict__ ports, const int32_t* __restrict__ action,
-                           const uint32_t* __restrict__ psns, const uint8_t (*himg)[kHdrImg],
-                           uint8_t* __restrict__ out, int64_t out_stride, bool out16,
-                           int32_t* __restrict__ out_len, const CrcLds& t, uint8_t* frbuf, int64_t g, int lane)
+// What one egress wave needs from global memory for output frame g: loaded one
+// frame ahead of its use (k_egress), so these dependent loads overlap the
+// previous frame's build + CRC instead of stalling the wave.
+struct EgressIn {
+    int act, port, c;
+    uint32_t psn, slot;
+    uint32_t op;
+    uint32_t reth;      // lanes 0-3: RETH word (used for WRITE_FIRST)
+    int32_t agg[4];     // word j * 64 + lane of the slot's aggregate
+};
+
+// Branch-free, so that no wait is needed until egress_emit uses the values: the
+// RETH and aggregate words are loaded whatever the action (the slot index is in
+// range for any PSN).
+__device__ __forceinline__ EgressIn egress_fetch(const InccSwitchState& s, const uint8_t* __restrict__ in_frames,
+                                                 int64_t in_stride, const int32_t* __restrict__ ports,
+                                                 const int32_t* __restrict__ action,
+                                                 const uint32_t* __restrict__ psns, int64_t g, int lane)
 {
+    EgressIn e;
     const int fan = s.fan_in;
     const int64_t f = g / fan;
-    const int c = (int)(g % fan);
-    const int act = action[f];
-    const bool emit = (act == INCCL_SW_COMPLETED) || (act == INCCL_SW_REPLAY && ports[f] == c);
+    e.c = (int)(g % fan);
+    e.act = action[f];
+    e.port = ports[f];
+    e.psn = psns[f];
+    // bytes 40-43 across lanes (the opcode is byte 42): a lane-varying load stays
+    // in a VGPR, where a uniform one would be read into an SGPR at once -- and
+    // that wait would also drain the previous frame's stores
+    e.op = in_frames[f * in_stride + 40 + (lane & 3)];
+    e.slot = e.psn & (s.slots - 1);
+    e.reth = lane < 4 ? s.reth[((size_t)e.slot * fan + e.c) * 4 + lane] : 0u;
+    const int32_t* agg = s.agg + (size_t)e.slot * kLanes;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e.agg[j] = agg[j * kWave + lane];
+    return e;
+}
+
+__device__ void egress_emit(const InccSwitchState& s, const EgressIn& e, const uint8_t (*himg)[kHdrImg],
+                            uint8_t* __restrict__ out, int64_t out_stride, bool out16, int32_t* __restrict__ out_len,
+                            const CrcLds& t, uint8_t* frbuf, int64_t g, int lane)
+{
+    const bool emit = (e.act == INCCL_SW_COMPLETED) || (e.act == INCCL_SW_REPLAY && e.port == e.c);
     if (!emit) {
         if (lane == 0) out_len[g] = 0;
         return;
     }
-    const uint32_t psn = psns[f];
-    const uint32_t slot = psn & (s.slots - 1);
-    const uint8_t op = in_frames[f * in_stride + 42];
-    const bool wf = is_write_first(op);
+    const int fan = s.fan_in;
+    const uint32_t op = (uint32_t)__shfl((int)e.op, 2, kWave);
+    const bool wf = is_write_first((uint8_t)op);
     const int total = 14 + 20 + 8 + 12 + (wf ? 16 : 0) + kLanes * 4 + 4;   // util.c:341-345
     uint8_t* fr = frbuf;
     if (lane < kHdrImg / 4)
-        reinterpret_cast<uint32_t*>(fr)[lane] = reinterpret_cast<const uint32_t*>(himg[c * 2 + (wf ? 1 : 0)])[lane];
+        reinterpret_cast<uint32_t*>(fr)[lane] = reinterpret_cast<const uint32_t*>(himg[e.c * 2 + (wf ? 1 : 0)])[lane];
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {                                                 // util.c:378, :386
-        const uint32_t p = psn | 0x80000000u;
-        fr[42] = op;
+        const uint32_t p = e.psn | 0x80000000u;
+        fr[42] = (uint8_t)op;
         fr[50] = (uint8_t)(p >> 24); fr[51] = (uint8_t)(p >> 16); fr[52] = (uint8_t)(p >> 8); fr[53] = (uint8_t)p;
     }
     // offsets 54 / 70 are 2-byte aligned: 16-bit LDS stores
-    if (wf && lane < 4) {                                            // util.c:409-417, reth_keeper[slot][c]
-        const uint32_t r = s.reth[((size_t)slot * fan + c) * 4 + lane];
+    if (wf && lane < 4) {                                          // util.c:409-417, reth_keeper[slot][c]
         uint16_t* r16 = reinterpret_cast<uint16_t*>(fr + 54);
-        r16[2 * lane] = (uint16_t)r;
-        r16[2 * lane + 1] = (uint16_t)(r >> 16);
+        r16[2 * lane] = (uint16_t)e.reth;
+        r16[2 * lane + 1] = (uint16_t)(e.reth >> 16);
     }
     const int doff = 54 + (wf ? 16 : 0);
-    const int32_t* agg = s.agg + (size_t)slot * kLanes;
     uint16_t* d16 = reinterpret_cast<uint16_t*>(fr + doff);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {                                    // util.c:403-405 / :419-421 htonl
         const int i = j * kWave + lane;
-        const uint32_t be = __builtin_bswap32((uint32_t)agg[i]);
+        const uint32_t be = __builtin_bswap32((uint32_t)e.agg[j]);
         d16[2 * i] = (uint16_t)be;
         d16[2 * i + 1] = (uint16_t)(be >> 16);
     }
     __builtin_amdgcn_wave_barrier();
+    uint8_t saved = 0;
+    if (lane < kNumMasked) {
+        saved = fr[masked_pos(lane)];
+        fr[masked_pos(lane)] = 0xFF;
+    }
+    __builtin_amdgcn_wave_barrier();
     const uint32_t crc = icrc_wave(fr, t, lane);                    // util.c:424-426
+    __builtin_amdgcn_wave_barrier();
+    if (lane < kNumMasked) fr[masked_pos(lane)] = saved;
+    __builtin_amdgcn_wave_barrier();
     if (lane == 0) {                                                 // stored host order (LE)
         fr[total - 4] = (uint8_t)crc;
         fr[total - 3] = (uint8_t)(crc >> 8);
@@ -298,22 +366,33 @@ __device__ void egress_one(const InccSwitchState& s, const uint8_t* __restrict__
     }
     __builtin_amdgcn_wave_barrier();
     uint8_t* o = out + g * out_stride;
+    // fixed trip counts (total <= 1098 B): the compiler can then count this
+    // wave's outstanding stores, and the next frame's prefetched loads are not
+    // held behind them by a conservative vmcnt(0)
     if (out16) {
         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-        for (int i = lane; i < (total + 15) / 16; i += kWave)
-            reinterpret_cast<u4*>(o)[i] = reinterpret_cast<const u4*>(fr)[i];
+#pragma unroll
+        for (int k = 0; k < (kFrameMax / 16 + kWave - 1) / kWave; ++k) {
+            const int i = lane + k * kWave;
+            if (i < (total + 15) / 16) reinterpret_cast<u4*>(o)[i] = reinterpret_cast<const u4*>(fr)[i];
+        }
     } else {
-        for (int i = lane; i < (total + 3) / 4; i += kWave)
-            reinterpret_cast<uint32_t*>(o)[i] = reinterpret_cast<const uint32_t*>(fr)[i];
+#pragma unroll
+        for (int k = 0; k < (kFrameMax / 4 + kWave - 1) / kWave; ++k) {
+            const int i = lane + k * kWave;
+            if (i < (total + 3) / 4) reinterpret_cast<uint32_t*>(o)[i] = reinterpret_cast<const uint32_t*>(fr)[i];
+        }
     }
     if (lane == 0) out_len[g] = total;
     // the result is known from now on: later retransmits replay (nts.c:366)
-    if (act == INCCL_SW_COMPLETED && c == 0 && lane == 0) atomicOr(&s.arrival[slot], 1u << fan);
+    if (e.act == INCCL_SW_COMPLETED && e.c == 0 && lane == 0) atomicOr(&s.arrival[e.slot], 1u << fan);
     __builtin_amdgcn_wave_barrier();
 }
 
 // Egress (nts.c:365-372 / :447-453 broadcast, :353-356 / :435-438 replay;
 // frames per util.c:331-442): wave (f, c) builds child c's copy of frame f.
+// Persistent: each wave walks its output frames with the next one's inputs in
+// flight.
 __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState s, const uint8_t* __restrict__ in_frames,
                                                                int64_t in_stride, int64_t count,
                                                                const int32_t* __restrict__ ports,
@@ -330,24 +409,39 @@ __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState 
     const int fan = s.fan_in;
     for (int i = threadIdx.x; i < 2 * fan; i += blockDim.x) build_header_image(himg[i], tmpl[i >> 1], (i & 1) != 0);
     __syncthreads();
-    const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     const bool out16 = ((out_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
-    for (int64_t g = (int64_t)blockIdx.x * kEgressWaves + w; g < count * fan; g += (int64_t)gridDim.x * kEgressWaves)
-        egress_one(s, in_frames, in_stride, ports, action, psns, himg, out, out_stride, out16, out_len, t, buf[w], g,
-                   lane);
+    const int64_t total = count * fan, step = (int64_t)gridDim.x * kEgressWaves;
+    int64_t g = (int64_t)blockIdx.x * kEgressWaves + w;
+    if (g >= total) return;
+    // two register sets used alternately (no copy between them: a copy would
+    // wait on every outstanding store of the previous frame too)
+    EgressIn a = egress_fetch(s, in_frames, in_stride, ports, action, psns, g, lane), b;
+    for (;;) {
+        if (g + step < total) b = egress_fetch(s, in_frames, in_stride, ports, action, psns, g + step, lane);
+        egress_emit(s, a, himg, out, out_stride, out16, out_len, t, buf[w], g, lane);
+        g += step;
+        if (g >= total) break;
+        if (g + step < total) a = egress_fetch(s, in_frames, in_stride, ports, action, psns, g + step, lane);
+        egress_emit(s, b, himg, out, out_stride, out16, out_len, t, buf[w], g, lane);
+        g += step;
+        if (g >= total) break;
+    }
 }
 
 // clear_state_data(psn + WINDOW) for every slot completed in the batch (nts.c:235-242, :367)
-__global__ void k_recycle(InccSwitchState s, int64_t count, const int32_t* __restrict__ action,
-                          const uint32_t* __restrict__ psns)
+__global__ __launch_bounds__(kWave* kWavesPerBlock) void k_recycle(InccSwitchState s, int64_t count,
+                                                                  const int32_t* __restrict__ action,
+                                                                  const uint32_t* __restrict__ psns)
 {
-    const int64_t f = blockIdx.x;
+    const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    const int64_t f = (int64_t)blockIdx.x * kWavesPerBlock + w;
     if (f >= count || action[f] != INCCL_SW_COMPLETED) return;
     const uint32_t slot = (psns[f] + (s.slots >> 1)) & (s.slots - 1);
-    int32_t* agg = s.agg + (size_t)slot * kLanes;
-    for (int i = threadIdx.x; i < kLanes; i += blockDim.x) agg[i] = 0;
-    for (int i = threadIdx.x; i < s.fan_in * 4; i += blockDim.x) s.reth[(size_t)slot * s.fan_in * 4 + i] = 0;
-    if (threadIdx.x == 0) {
+    typedef int32_t i4 __attribute__((ext_vector_type(4)));
+    reinterpret_cast<i4*>(s.agg + (size_t)slot * kLanes)[lane] = i4{0, 0, 0, 0};   // 64 lanes x 16 B = one slot
+    for (int i = lane; i < s.fan_in * 4; i += kWave) s.reth[(size_t)slot * s.fan_in * 4 + i] = 0;
+    if (lane == 0) {
         s.arrival[slot] = 0;
         s.degree[slot] = 0;
     }
@@ -357,7 +451,7 @@ __global__ void k_recycle(InccSwitchState s, int64_t count, const int32_t* __res
 // host: CRC tables (util.c:141-159) and the zero-append operators per tree level
 // ---------------------------------------------------------------------------
 uint32_t host_tab[256];
-uint32_t host_shift[6][4][256];
+uint32_t host_lane_shift[8][16][kWave];
 bool g_tables_ready[64];
 std::mutex g_tables_mu;
 
@@ -379,11 +473,17 @@ int ensure_tables()
         for (int j = 0; j < 8; ++j) c = (c >> 1) ^ ((c & 1u) ? 0xEDB88320u : 0u);
         host_tab[i] = c;
     }
-    for (int l = 0; l < 6; ++l)
-        for (int b = 0; b < 4; ++b)
-            for (uint32_t v = 0; v < 256; ++v) host_shift[l][b][v] = zeros_append(v << (8 * b), kSeg << l);
+    // Z_n is linear: Z_{n+17}(x) = Z_17(Z_n(x)), so lanes are filled from 63 down
+    for (int n = 0; n < 8; ++n)
+        for (uint32_t v = 0; v < 16; ++v) {
+            uint32_t x = v << (4 * n);
+            for (int lane = kWave - 1; lane >= 0; --lane) {
+                host_lane_shift[n][v][lane] = x;
+                x = zeros_append(x, kSeg);
+            }
+        }
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc_tab), host_tab, sizeof(host_tab));
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_shift_tab), host_shift, sizeof(host_shift));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane_shift), host_lane_shift, sizeof(host_lane_shift));
     if (e != hipSuccess) return (int)e;
     if (dev >= 0 && dev < 64) g_tables_ready[dev] = true;
     return 0;
@@ -422,10 +522,10 @@ int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* o
     if (count == 0) return 0;
     int rc = ensure_tables();
     if (rc) return rc;
-    const int64_t blocks = ((int64_t)count + kWavesPerBlock - 1) / kWavesPerBlock;
-    const int64_t cap = (int64_t)num_cus() * 4;
+    const int64_t blocks = ((int64_t)count + kIcrcWaves - 1) / kIcrcWaves;
+    const int64_t cap = (int64_t)num_cus() * 2;   // persistent: the 64 KiB of tables are loaded once per block
     const int grid = (int)(blocks < cap ? blocks : cap);
-    hipLaunchKernelGGL(k_icrc, dim3(grid), dim3(kWave * kWavesPerBlock), 0, (hipStream_t)stream, frames,
+    hipLaunchKernelGGL(k_icrc, dim3(grid), dim3(kWave * kIcrcWaves), 0, (hipStream_t)stream, frames,
                        (int64_t)stride, (int64_t)count, out);
     return (int)hipGetLastError();
 }
@@ -452,14 +552,15 @@ int inccl_k_switch_egress(const InccSwitchState* s, const uint8_t* in_frames, si
     int rc = ensure_tables();
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    // persistent grid: the 25 KiB CRC tables are loaded once per block
+    // persistent grid, two blocks per CU: the 64 KiB CRC tables are loaded once per block
     const int64_t need = ((int64_t)count * s->fan_in + kEgressWaves - 1) / kEgressWaves;
-    const int64_t cap = (int64_t)num_cus() * 4;
+    const int64_t cap = (int64_t)num_cus() * 2;
     const int eg = (int)(need < cap ? (need < 1 ? 1 : need) : cap);
     hipLaunchKernelGGL(k_egress, dim3(eg), dim3(kWave * kEgressWaves), 0, st, *s,
                        in_frames, (int64_t)in_stride, (int64_t)count, ports, action, psns, tmpl, out,
                        (int64_t)out_stride, out_len);
-    hipLaunchKernelGGL(k_recycle, dim3((unsigned)count), dim3(256), 0, st, *s, (int64_t)count, action, psns);
+    hipLaunchKernelGGL(k_recycle, dim3(grid_for((int64_t)count)), dim3(kWave * kWavesPerBlock), 0, st, *s,
+                       (int64_t)count, action, psns);
     return (int)hipGetLastError();
 }
 

@@ -94,12 +94,14 @@ struct inccl_communicator {
     uint32_t *mesh_err_dev;
     uint64_t mesh_timeout_ticks;
     hipStream_t mesh_last_stream;  /* ordering across caller streams (ev[6]) */
+    int mesh_push;               /* "meshw": result chunks pushed into every rank's result inbox */
     /* host memory registered by the caller (inccl_host_register, the ibv_reg_mr of
      * api.c:170-176): the host collectives DMA such ranges directly */
     struct { char *p; size_t len; } reg[INCCL_MAX_HOST_REGIONS];
     int nreg;
     struct inccl_copy_pool *pool;  /* host staging copies (copypool.c) */
-    hipEvent_t ev[8];
+    hipEvent_t ev[9];            /* [8]: p2p ordering across caller streams */
+    hipStream_t p2p_last_stream;
 };
 
 /* transport operations; all stream-ordered on `st` */

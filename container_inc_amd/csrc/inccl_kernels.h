@@ -66,6 +66,9 @@ struct inccl_mesh_launch {
     const uint32_t *own_inbox;
     uint32_t *own_res;
     const uint32_t *peer_res[INCCL_MAX_LOCAL_INPUTS];  /* every rank's result shard */
+    uint32_t *peer_resin[INCCL_MAX_LOCAL_INPUTS];      /* every rank's result inbox (push_res) */
+    const uint32_t *own_resin;
+    int push_res;                                      /* 1: reduce pushes results, gather copies locally */
     uint32_t *peer_sig[INCCL_MAX_LOCAL_INPUTS];        /* every rank's signal array */
     const uint32_t *own_sig;
     uint32_t *ctr;                                     /* own words: calls, retired, ticket, abort */

@@ -18,6 +18,13 @@
 //   gather(c, j) wait for ready[j][c], then pull rank j's result chunk over xGMI
 //                into dst (the host's decode, api.c:428-430).
 //
+// "meshw" (push_res): reduce(c) also writes the result chunk into slot `me` of
+// every rank's result inbox before raising ready, and gather(c, j) copies it
+// from the local inbox -- every xGMI transfer of the call is then a write.  The
+// inbox reuse argument below holds for the result inbox as it does for the
+// partial inbox (rank j rewrites my slot j of chunk c only after my next
+// push(c, j), i.e. after my previous call, gathers included, has finished).
+//
 // Scheduling.  Items are numbered in one global order that every rank shares:
 // slot s holds push(s, *), reduce(s - lag) and gather(s - 2 lag, *).  Workgroups
 // take tickets from a device counter, so items start in that order on every
@@ -73,12 +80,14 @@ struct MeshArgs {
     const uint32_t* own_inbox;
     uint32_t* own_res;
     const uint32_t* peer_res[kMaxR];
+    uint32_t* peer_resin[kMaxR];         // rank j's result inbox (push_res): slot i at + i * inbox_stride
+    const uint32_t* own_resin;
     uint32_t* peer_sig[kMaxR];           // rank j's signal array ([me] = own)
     const uint32_t* own_sig;
     uint32_t* ctr;                       // [0] calls done, [1] retired, [2] ticket, [3] abort
     uint32_t* err;                       // host-mapped error word
     uint64_t timeout_ticks;
-    int nchunks, W, me, lag, vec_src, vec_dst;
+    int nchunks, W, me, lag, vec_src, vec_dst, push_res;
     Scale sc;
 };
 
@@ -201,6 +210,12 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
     for (int j = 0; j < kMaxR; ++j)
         in[j] = rsrc(a.own_inbox + (int64_t)(j < a.W ? j : 0) * a.inbox_stride + (int64_t)c * a.chunk, bytes);
     const __amdgpu_buffer_rsrc_t res = rsrc(a.own_res + (int64_t)c * a.chunk, bytes);
+    __amdgpu_buffer_rsrc_t outs[kMaxR];   // push_res: my slot of every rank's result inbox
+    if (a.push_res) {
+#pragma unroll
+        for (int j = 0; j < kMaxR; ++j)
+            outs[j] = rsrc(a.peer_resin[j < a.W ? j : 0] + (int64_t)a.me * a.inbox_stride + (int64_t)c * a.chunk, bytes);
+    }
     for (int64_t q0 = threadIdx.x; q0 < nq; q0 += (int64_t)kMeshBlock * 2) {
         u32x4 x[2][kMaxR];
 #pragma unroll
@@ -226,7 +241,13 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
             o.y = __float_as_uint((float)(int32_t)acc.y * inv);
             o.z = __float_as_uint((float)(int32_t)acc.z * inv);
             o.w = __float_as_uint((float)(int32_t)acc.w * inv);
-            st_sys16(res, (uint32_t)(q * 16), o);
+            if (a.push_res) {
+#pragma unroll
+                for (int j = 0; j < kMaxR; ++j)
+                    if (j < a.W) st_sys16(outs[j], (uint32_t)(q * 16), o);
+            } else {
+                st_sys16(res, (uint32_t)(q * 16), o);
+            }
         }
     }
     __builtin_amdgcn_s_waitcnt(0);
@@ -246,7 +267,11 @@ __device__ bool do_gather(const MeshArgs& a, int c, int j, uint32_t epoch)
     int64_t cnt = chunk_len(a, c);
     if (lo + cnt > a.n) cnt = a.n - lo;
     const int64_t nq = cnt >> 2;
-    const __amdgpu_buffer_rsrc_t src = rsrc(a.peer_res[j] + (int64_t)c * a.chunk, (uint32_t)(chunk_len(a, c) * 4));
+    // pull rank j's result chunk over xGMI, or (push_res) copy what rank j pushed
+    // into my result inbox
+    const uint32_t* sbase = a.push_res ? a.own_resin + (int64_t)j * a.inbox_stride + (int64_t)c * a.chunk
+                                       : a.peer_res[j] + (int64_t)c * a.chunk;
+    const __amdgpu_buffer_rsrc_t src = rsrc(sbase, (uint32_t)(chunk_len(a, c) * 4));
     uint32_t* d = reinterpret_cast<uint32_t*>(a.dst) + lo;
     for (int64_t q0 = threadIdx.x; q0 < nq; q0 += (int64_t)kMeshBlock * kMeshU) {
         u32x4 v[kMeshU];
@@ -335,8 +360,12 @@ extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
     for (int j = 0; j < l->W; ++j) {
         a.peer_inbox[j] = l->peer_inbox[j];
         a.peer_res[j] = l->peer_res[j];
+        a.peer_resin[j] = l->peer_resin[j];
         a.peer_sig[j] = l->peer_sig[j];
     }
+    a.own_resin = l->own_resin;
+    a.push_res = l->push_res ? 1 : 0;
+    if (a.push_res && (l->own_resin == nullptr || l->peer_resin[0] == nullptr)) return INCCL_ERR_ARG;
     a.own_inbox = l->own_inbox;
     a.own_res = l->own_res;
     a.own_sig = l->own_sig;

@@ -14,6 +14,7 @@
  *   [64 KiB, +16)            call counter, retired workgroups, ticket, abort word
  *   [128 KiB, +W*cap*4)      inbox: slot j holds rank j's int32 partial of my shard
  *   [.., +cap*4)             my dequantised result shard (fp32)
+ *   [.., +W*cap*4)           result inbox ("meshw"): slot j holds rank j's result shard
  * Created collectively on the first call, regrown collectively when a larger
  * bucket arrives (all ranks make the same calls, as with RCCL). */
 #define _GNU_SOURCE
@@ -58,22 +59,32 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     if (c->mesh_buf && c->mesh_cap >= shard) return 0;
     if (W > INCCL_MAX_LOCAL_INPUTS)
         return inccl_set_error(INCCL_ERR_ARG, "mesh engine supports up to %d GPUs", INCCL_MAX_LOCAL_INPUTS);
-    if (c->mesh_buf) {   /* peers may still read the old buffers until everyone is here */
+    /* make before break (as p2p_ensure): the old buffer stays alive, and mapped
+     * by the peers, until every rank has mapped the new one */
+    struct inccl_communicator old = *c;
+    if (c->mesh_buf) {   /* everyone's queued accesses to the old buffers drain first */
         INCCL_HIP(hipDeviceSynchronize());
         int rc = inccl_boot_barrier(g);
         if (rc) return rc;
-        inccl_mesh_release(c);
+        c->mesh_buf = NULL;
+        c->mesh_err_host = NULL;
+        c->mesh_err_dev = NULL;
+        c->mesh_cap = 0;
+        for (int j = 0; j < INCCL_MAX_LOCAL_INPUTS; ++j) c->mesh_peer[j] = NULL;
     }
     const size_t cap = (shard + ((size_t)1 << 19) - 1) & ~(((size_t)1 << 19) - 1);   /* 2 MiB granules */
     const int dev = g->device >= 0 ? g->device : 0;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     mesh_peer_info mine, *all = (mesh_peer_info *)calloc((size_t)W, sizeof(mesh_peer_info));
-    if (!all) return inccl_set_error(INCCL_ERR_NOMEM, "mesh: out of memory");
+    if (!all) {
+        inccl_mesh_release(&old);
+        return inccl_set_error(INCCL_ERR_NOMEM, "mesh: out of memory");
+    }
     memset(&mine, 0, sizeof(mine));
     int rc = 0;
     /* local failures are carried to the collective outcome check below */
-    hipError_t e = hipMalloc((void **)&c->mesh_buf, MESH_DATA_OFFSET + ((size_t)W + 1) * cap * sizeof(uint32_t));
+    hipError_t e = hipMalloc((void **)&c->mesh_buf, MESH_DATA_OFFSET + ((size_t)2 * W + 1) * cap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(c->mesh_buf, 0, MESH_DATA_OFFSET);   /* flags + counters */
     if (e == hipSuccess) e = hipDeviceSynchronize();   /* zeroed before any peer maps it */
     if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.h, c->mesh_buf);
@@ -90,6 +101,7 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     int rc_x = inccl_boot_allgather(g, &mine, all, sizeof(mesh_peer_info));
     if (rc_x) {
         free(all);
+        inccl_mesh_release(&old);
         return rc_x;
     }
     int sharing = 0;
@@ -118,13 +130,23 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     /* agree on the outcome, so that every rank falls back alike */
     int32_t mine_rc = rc ? 1 : 0, all_rc[INCCL_MAX_LOCAL_INPUTS];
     int rc2 = inccl_boot_allgather(g, &mine_rc, all_rc, sizeof(int32_t));
-    if (rc2) return rc2;
+    if (rc2) {
+        inccl_mesh_release(&old);
+        return rc2;
+    }
     for (int j = 0; j < W; ++j)
         if (all_rc[j]) {
             if (!rc) rc = inccl_set_error(INCCL_ERR_HIP, "mesh: rank %d could not map the peer buffers", j);
             inccl_mesh_release(c);
+            inccl_mesh_release(&old);
             return rc;
         }
+    /* every peer has mapped the new buffer: the old one can go */
+    if (old.mesh_buf) {
+        int rc_b = inccl_boot_barrier(g);
+        inccl_mesh_release(&old);
+        if (rc_b) return rc_b;
+    }
     c->mesh_cap = cap;
     c->mesh_grid = grid;
     c->mesh_last_stream = NULL;
@@ -193,8 +215,11 @@ int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int
         char *base = c->mesh_peer[j];
         l.peer_inbox[j] = (uint32_t *)(base + MESH_DATA_OFFSET);
         l.peer_res[j] = (const uint32_t *)(base + MESH_DATA_OFFSET + (size_t)W * c->mesh_cap * sizeof(uint32_t));
+        l.peer_resin[j] = (uint32_t *)(base + MESH_DATA_OFFSET + ((size_t)W + 1) * c->mesh_cap * sizeof(uint32_t));
         l.peer_sig[j] = (uint32_t *)base;
     }
+    l.own_resin = l.peer_resin[me];
+    l.push_res = c->mesh_push;
     l.own_inbox = l.peer_inbox[me];
     l.own_res = (uint32_t *)l.peer_res[me];
     l.own_sig = (const uint32_t *)c->mesh_buf;

@@ -58,15 +58,33 @@ static int p2p_ensure(struct inccl_communicator *c, size_t elems)
     struct inccl_group *g = c->group;
     const int W = g->world_size, me = g->rank;
     if (c->p2p_cap >= elems && c->p2p_part) return 0;
-    /* peers may still read the old buffers until everyone is here */
+    /* this rank's queued reads of the peers' buffers (the previous call's gather)
+     * drain before anyone may drop them */
+    INCCL_HIP(hipDeviceSynchronize());
     int rc = inccl_boot_barrier(g);
     if (rc) return rc;
     rc = inccl_boot_shm_init(g);   /* same-node fast barrier for the per-call syncs */
     if (rc) return rc;
-    inccl_p2p_release(c);
+    /* Make before break: the new buffers are allocated, exported and mapped by
+     * every peer while the old ones are still alive, and the old ones go only
+     * after a barrier.  Freeing first lets a new export reuse the old one's
+     * identity (a dmabuf fd number) while a peer's runtime may still resolve it
+     * to the old import: a regrowth then, intermittently, left one rank reading
+     * a peer's old buffer on every later call. */
+    struct inccl_communicator old = *c;
+    c->p2p_part = NULL;
+    c->p2p_res = NULL;
+    c->p2p_cap = 0;
+    for (int j = 0; j < INCCL_MAX_LOCAL_INPUTS; ++j) {
+        c->p2p_peer_part[j] = NULL;
+        c->p2p_peer_res[j] = NULL;
+    }
     size_t cap = (elems + (1u << 19) - 1) & ~(size_t)((1u << 19) - 1);   /* 2 MiB granules */
     p2p_handles mine, *all = (p2p_handles *)calloc((size_t)W, sizeof(p2p_handles));
-    if (!all) return inccl_set_error(INCCL_ERR_NOMEM, "p2p: out of memory");
+    if (!all) {
+        inccl_p2p_release(&old);
+        return inccl_set_error(INCCL_ERR_NOMEM, "p2p: out of memory");
+    }
     memset(&mine, 0, sizeof(mine));
     /* local failures are carried to the collective outcome check below */
     hipError_t e = hipMalloc((void **)&c->p2p_part, cap * sizeof(int32_t));
@@ -80,6 +98,7 @@ static int p2p_ensure(struct inccl_communicator *c, size_t elems)
     int rc_x = inccl_boot_allgather(g, &mine, all, sizeof(p2p_handles));
     if (rc_x) {
         free(all);
+        inccl_p2p_release(&old);
         return rc_x;
     }
     for (int j = 0; rc == 0 && j < W; ++j) {
@@ -96,6 +115,10 @@ static int p2p_ensure(struct inccl_communicator *c, size_t elems)
         c->p2p_peer_res[j] = (float *)pr;
     }
     free(all);
+    /* every peer has mapped the new buffers: the old ones can go */
+    int rc_b = inccl_boot_barrier(g);
+    inccl_p2p_release(&old);
+    if (rc_b) return rc_b;
     /* agree on the outcome: a rank whose IPC mapping failed must not leave its
      * peers waiting in a barrier it never reaches, and everyone must see the
      * failure so the caller can fall back on every rank alike */
@@ -127,6 +150,10 @@ int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int 
     const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
     int rc = p2p_ensure(c, total);
     if (rc) return rc;
+    /* the previous call's gather may still be reading the peers' result shards,
+     * which the peers rewrite once this call's first barrier has passed: order
+     * it before that barrier's host sync when the caller switches streams */
+    if (c->p2p_last_stream && c->p2p_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[8], 0));
     /* 1. local quantise + sum */
     rc = inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_Q32, (const void *const *)srcs, R, c->p2p_part, n, k, amax,
                         scale_R, st);
@@ -152,5 +179,7 @@ int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int 
     }
     rc = inccl_k_peer_gather(src, off, cnt, W, dst, st);
     if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p gather launch failed (%d)", rc);
+    INCCL_HIP(hipEventRecord(c->ev[8], st));
+    c->p2p_last_stream = st;
     return 0;
 }

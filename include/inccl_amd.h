@@ -129,10 +129,13 @@ int inccl_comm_barrier(struct inccl_communicator *comm);
  *           dequantises it once every rank's arrival flag is up, and every rank pulls
  *           the result chunks; phases of different chunks overlap, no host
  *           synchronisation (buckets up to $INCCL_LL_MAX_BYTES: the "ll" kernel)
+ *   "meshw" as "mesh", but the owner also pushes each result chunk into every
+ *           rank's IPC result inbox, so that every xGMI transfer is a write; each
+ *           rank then copies the chunks locally into dst
  *   "ar"    quant+sum -> ncclAllReduce(int32, sum) in place -> dequant
  * Every rank must select the same engine.  $INCCL_ENGINE sets it at creation. */
 int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name);
-/* "rccl", "ar", "a2a", "p2p", "ll", "mesh" or "local" */
+/* "rccl", "ar", "a2a", "p2p", "ll", "mesh", "meshw" or "local" */
 const char *inccl_comm_engine(const struct inccl_communicator *comm);
 
 /* Device-resident fp32 allreduce of R local buckets per rank:

@@ -195,7 +195,7 @@ def test_rccl_world1_paths(gpu, orc, force_rccl):
     assert grp is not None and grp.transport == "rccl"
     comm = inccl.inccl_communicator_create(grp, 1 << 20)
     rng = np.random.default_rng(5)
-    for engine in ("rccl", "ar", "a2a", "p2p", "mesh"):
+    for engine in ("rccl", "ar", "a2a", "p2p", "mesh", "meshw"):
         comm.set_engine(engine)
         assert comm.engine == engine
         for n, chunks in ((1 << 20, 1), ((1 << 20) + 5, 3)):

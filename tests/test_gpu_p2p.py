@@ -36,7 +36,7 @@ def _inputs(world, R, n, seed):
 def _rank_main(rank, world, port, cases, q, engine="p2p"):
     try:
         os.environ["INCCL_ENGINE"] = engine
-        if engine in ("p2p", "mesh"):
+        if engine in ("p2p", "mesh", "meshw"):
             os.environ["INCCL_LL_MAX_BYTES"] = "0"   # the sharded exchange at every size
         os.environ["INCCL_DEVICE"] = "0"
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
@@ -62,6 +62,9 @@ def _rank_main(rank, world, port, cases, q, engine="p2p"):
             srcs = [torch.from_numpy(np.concatenate([np.zeros(shift, np.float32), x])).to(dev)[shift:]
                     for x in xs[rank]]
             out = torch.full((n + shift,), float("nan"), device=dev)[shift:]
+            # the inputs and the NaN fill were made on torch's stream; the library
+            # runs on its own non-blocking streams, so order them explicitly
+            torch.cuda.synchronize()
             for it in range(4):   # repeated: buffer reuse across calls (and across two streams)
                 comm.allreduce_f32(srcs, out=out, scale_exp=inccl.SCALE_AUTO if k == "auto" else k,
                                    stream=comm.stream if it % 2 == 0 else side.cuda_stream)
@@ -70,13 +73,14 @@ def _rank_main(rank, world, port, cases, q, engine="p2p"):
                 results.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
             # back to back with no host synchronisation in between (the bench's timed loop)
             outs = [torch.full((n + shift,), float("nan"), device=dev)[shift:] for _ in range(12)]
+            torch.cuda.synchronize()
             for o in outs:
                 comm.allreduce_f32(srcs, out=o, scale_exp=inccl.SCALE_AUTO if k == "auto" else k,
                                    stream=comm.stream)
             torch.cuda.synchronize()
             for o in outs:
                 results.append(bool(np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32))))
-        if engine in ("ll", "mesh"):
+        if engine in ("ll", "mesh", "meshw"):
             # hipGraph: three calls captured once, replayed with fresh inputs (the
             # call counter lives on the device, so every replay is a new call)
             n = 5000
@@ -127,12 +131,13 @@ MESH_CASES = P2P_CASES + [(1, 1, 25, 31), (8, 3_000_017, 22, 32), (2, (8 << 20) 
 
 
 @pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (4, "p2p"), (2, "ll"), (3, "ll"), (4, "ll"),
-                                          (2, "mesh"), (3, "mesh"), (4, "mesh")])
+                                          (2, "mesh"), (3, "mesh"), (4, "mesh"), (2, "meshw"), (3, "meshw"),
+                                          (4, "meshw")])
 def test_p2p_engine_multiprocess(gpu, world, engine):
     """One process per rank on GPU 0 (IPC between processes; the same code as
     across xGMI).  "p2p" at large buckets, "ll" (one kernel, device flags),
     "mesh" (one persistent kernel, per-chunk flags, push + pull)."""
-    cases = {"p2p": P2P_CASES, "ll": LL_CASES, "mesh": MESH_CASES}[engine]
+    cases = {"p2p": P2P_CASES, "ll": LL_CASES, "mesh": MESH_CASES, "meshw": MESH_CASES}[engine]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -160,7 +165,7 @@ def _timeout_main(rank, port, q, engine="ll"):
     report the failure on the next call instead of hanging the GPU."""
     try:
         os.environ["INCCL_ENGINE"] = engine
-        if engine == "mesh":
+        if engine in ("mesh", "meshw"):
             os.environ["INCCL_LL_MAX_BYTES"] = "0"
         os.environ["INCCL_DEVICE"] = "0"
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
@@ -192,7 +197,7 @@ def _timeout_main(rank, port, q, engine="ll"):
         q.put((rank, False, "crash " + repr(e)))
 
 
-@pytest.mark.parametrize("engine", ["ll", "mesh"])
+@pytest.mark.parametrize("engine", ["ll", "mesh", "meshw"])
 def test_engine_peer_timeout(gpu, engine):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -47,6 +47,23 @@ def test_icrc_random_frames(gpu, orc):
         assert int(c) == orc.icrc(f) == int.from_bytes(f[-4:], "little")
 
 
+def test_icrc_any_length(gpu, orc):
+    """Random bytes at every IP length class the window covers: 28..60, random
+    lengths, and the last few before the 1088-byte window is full (the leading
+    zero region then ends inside lane 0, at a lane boundary, or not at all)."""
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(22)
+    lens = list(range(28, 61)) + [int(x) for x in rng.integers(28, 1089, 60)] + list(range(1060, 1089))
+    frames = []
+    for ipt in lens:
+        f = bytearray(rng.integers(0, 256, 14 + ipt, dtype=np.uint8).tobytes())
+        f[16], f[17] = ipt >> 8, ipt & 0xFF
+        frames.append(bytes(f))
+    got = inccl.icrc_frames(_rows(frames, gpu)).cpu().numpy().view(np.uint32)
+    for ipt, f, c in zip(lens, frames, got):
+        assert int(c) == orc.icrc(f), ipt
+
+
 def _templates(fan_in):
     from container_inc_amd.inccl import FRAME_TEMPLATE_DTYPE
     t = np.zeros(fan_in, FRAME_TEMPLATE_DTYPE)

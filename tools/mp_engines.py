@@ -22,7 +22,7 @@ def main():
     engines = sys.argv[2:] or ["p2p", "ll", "mesh"]
     bad = 0
     for engine in engines:
-        cases = {"p2p": T.P2P_CASES, "ll": T.LL_CASES, "mesh": T.MESH_CASES}[engine]
+        cases = {"p2p": T.P2P_CASES, "ll": T.LL_CASES, "mesh": T.MESH_CASES, "meshw": T.MESH_CASES}[engine]
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
         port = T._free_port()
