@@ -130,9 +130,10 @@ MESH_CASES = P2P_CASES + [(1, 1, 25, 31), (8, 3_000_017, 22, 32), (2, (8 << 20) 
                           (3, 64 * 3 - 1, 24, 34)]
 
 
-@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (4, "p2p"), (2, "ll"), (3, "ll"), (4, "ll"),
-                                          (2, "mesh"), (3, "mesh"), (4, "mesh"), (2, "meshw"), (3, "meshw"),
-                                          (4, "meshw")])
+# W = 8 is the 8-GPU bench's world size: all eight ranks on GPU 0 here
+@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (4, "p2p"), (8, "p2p"), (2, "ll"), (3, "ll"),
+                                          (4, "ll"), (8, "ll"), (2, "mesh"), (3, "mesh"), (4, "mesh"), (8, "mesh"),
+                                          (2, "meshw"), (3, "meshw"), (4, "meshw"), (8, "meshw")])
 def test_p2p_engine_multiprocess(gpu, world, engine):
     """One process per rank on GPU 0 (IPC between processes; the same code as
     across xGMI).  "p2p" at large buckets, "ll" (one kernel, device flags),
