@@ -8,8 +8,10 @@ Workload (one "step"): every rank holds R = 2 resident 256 MiB fp32 buckets
 (the reference's FAN_IN = 2 children per switch, non_termination_switch.c:23)
 and produces their allreduce over all ranks into a third buffer:
   N = 1   one fused HIP kernel: dequant(sum_r quant(x_r))          (config 2)
-  N > 1   quant + local sum (HIP) -> RCCL reduce-scatter int32 -> dequant own
-          shard (HIP) -> RCCL all-gather fp32                       (config 4)
+  N > 1   the exchange engine that is fastest during warmup among rccl
+          (quant + local sum -> RCCL reduce-scatter int32 -> dequant shard ->
+          RCCL all-gather), ar, a2a, p2p, mesh and meshw, all bit-identical
+          (config 4; DESIGN.md "Multi-GPU"); then the config 5 size sweep
 value = bucket bytes reduced per second over the whole job = N * R * 256 MiB / t.
 
 Extra JSON fields: ``roofline`` for the dominant kernel (the fused / quant+sum
@@ -142,14 +144,14 @@ def cpu_reference_pipeline(seconds: float) -> dict:
 
 def size_sweep(comm, dev, R: int, k: int, rank: int) -> list:
     """BASELINE config 5 at N > 1: bucket sizes 4 KiB (one reference message,
-    api.h:39) to 64 MiB, per engine: host wall time per call over back-to-back
+    api.h:39) to 256 MiB in x4 steps, per engine: host wall time per call over back-to-back
     calls (max over ranks), and whether the output is bit-identical to the
     first engine's.  Buckets up to the ll threshold (1 MiB) take the one-kernel
     ll engine; rccl / ar run everywhere for comparison."""
     import torch
     import torch.distributed as dist
     rows = []
-    for b in (4 << 10, 64 << 10, 1 << 20, 16 << 20, 64 << 20):
+    for b in [(4 << 10) << (2 * i) for i in range(9)]:   # 4 KiB .. 256 MiB in x4 steps (BASELINE config 5)
         n = b // 4
         gen = torch.Generator(device=dev)
         gen.manual_seed(7000 + rank)
