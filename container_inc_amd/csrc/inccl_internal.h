@@ -132,6 +132,10 @@ int inccl_rccl_alltoall_q32(struct inccl_communicator *c, const int32_t *send, i
 int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
                     const uint32_t *amax, int scale_R, hipStream_t st);
 void inccl_p2p_release(struct inccl_communicator *c);
+/* int32 allreduce (wrapping sum) over the p2p engine's IPC buffers: the
+ * reference API's inccl_allreduce_write on a multi-process group without RCCL */
+int inccl_p2p_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
+                            hipStream_t st);
 
 /* ll engine (ll.c): n <= c->ll_max_bytes / 4 */
 int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,

@@ -12,6 +12,7 @@
 //   k_peer_reduce<R>:  out[i] = dequant( sum_{j<R} peer_j[i] )   int32 -> fp32
 //       the reference switch's aggregate (non_termination_switch.c:361-363)
 //       over the W ranks' shards, fused with the new dequantise stage
+//       (DEQ = false: the plain int32 sum, for the int32 allreduce)
 //   k_peer_gather:     dst[off_j + i] = src_j[i]  for every rank j (blockIdx.y)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -35,10 +36,12 @@ __device__ __forceinline__ u32x4 ld_sys16(const void* tile_base, uint32_t tile_b
     return __builtin_amdgcn_raw_buffer_load_b128(rsrc(tile_base, tile_bytes), (int)off, 0, kAuxSys);
 }
 
-template <int R, int BLOCK>
+// DEQ = false: the int32 sum itself (the reference's int32 allreduce,
+// inccl_allreduce_write over the IPC engines), no dequantise stage
+template <int R, int BLOCK, bool DEQ>
 __global__ __launch_bounds__(BLOCK) void k_peer_reduce(SrcPtrs src, float* __restrict__ dst, int64_t n4, Scale sc)
 {
-    const float inv = pow2f(-resolve_k(sc));
+    const float inv = DEQ ? pow2f(-resolve_k(sc)) : 1.0f;
     u32x4* __restrict__ out = reinterpret_cast<u32x4*>(dst);
     for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n4; base += (int64_t)gridDim.x * BLOCK) {
         const int64_t i = base + threadIdx.x;
@@ -57,11 +60,13 @@ __global__ __launch_bounds__(BLOCK) void k_peer_reduce(SrcPtrs src, float* __res
                 acc.z += v[r].z;
                 acc.w += v[r].w;
             }
-            u32x4 o;
-            o.x = __float_as_uint((float)(int32_t)acc.x * inv);
-            o.y = __float_as_uint((float)(int32_t)acc.y * inv);
-            o.z = __float_as_uint((float)(int32_t)acc.z * inv);
-            o.w = __float_as_uint((float)(int32_t)acc.w * inv);
+            u32x4 o = acc;
+            if constexpr (DEQ) {
+                o.x = __float_as_uint((float)(int32_t)acc.x * inv);
+                o.y = __float_as_uint((float)(int32_t)acc.y * inv);
+                o.z = __float_as_uint((float)(int32_t)acc.z * inv);
+                o.w = __float_as_uint((float)(int32_t)acc.w * inv);
+            }
             __builtin_nontemporal_store(o, out + i);
         }
     }
@@ -113,12 +118,12 @@ __global__ __launch_bounds__(kGatherBlock) void k_peer_gather(Segs s, uint32_t* 
             d[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <int R>
+template <int R, bool DEQ = true>
 hipError_t launch_reduce_R(const SrcPtrs& s, float* dst, int64_t n4, const Scale& sc, hipStream_t st)
 {
     constexpr int B = Geometry<R>::BLOCK;
     const int64_t grid = (n4 + B - 1) / B;
-    hipLaunchKernelGGL((k_peer_reduce<R, B>), dim3((unsigned)grid), dim3(B), 0, st, s, dst, n4, sc);
+    hipLaunchKernelGGL((k_peer_reduce<R, B, DEQ>), dim3((unsigned)grid), dim3(B), 0, st, s, dst, n4, sc);
     return hipGetLastError();
 }
 
@@ -149,6 +154,33 @@ extern "C" int inccl_k_peer_reduce(const void* const* peers, int W, float* dst, 
         case 6: e = launch_reduce_R<6>(s, dst, n4, sc, st); break;
         case 7: e = launch_reduce_R<7>(s, dst, n4, sc, st); break;
         default: e = launch_reduce_R<8>(s, dst, n4, sc, st); break;
+    }
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int inccl_k_peer_sum_q32(const void* const* peers, int W, int32_t* dst, size_t n, void* stream)
+{
+    if (W < 1 || W > kMaxR || dst == nullptr || (n & 3) != 0 || !aligned16(dst)) return INCCL_ERR_ARG;
+    if (n == 0) return 0;
+    SrcPtrs s = {};
+    for (int j = 0; j < W; ++j) {
+        if (peers[j] == nullptr || !aligned16(peers[j])) return INCCL_ERR_ARG;
+        s.p[j] = peers[j];
+    }
+    const Scale sc{0, nullptr, W};
+    const int64_t n4 = (int64_t)(n >> 2);
+    float* d = reinterpret_cast<float*>(dst);   // 32-bit words; no float arithmetic without DEQ
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    switch (W) {
+        case 1: e = launch_reduce_R<1, false>(s, d, n4, sc, st); break;
+        case 2: e = launch_reduce_R<2, false>(s, d, n4, sc, st); break;
+        case 3: e = launch_reduce_R<3, false>(s, d, n4, sc, st); break;
+        case 4: e = launch_reduce_R<4, false>(s, d, n4, sc, st); break;
+        case 5: e = launch_reduce_R<5, false>(s, d, n4, sc, st); break;
+        case 6: e = launch_reduce_R<6, false>(s, d, n4, sc, st); break;
+        case 7: e = launch_reduce_R<7, false>(s, d, n4, sc, st); break;
+        default: e = launch_reduce_R<8, false>(s, d, n4, sc, st); break;
     }
     return e == hipSuccess ? 0 : (int)e;
 }

@@ -183,3 +183,43 @@ int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int 
     c->p2p_last_stream = st;
     return 0;
 }
+
+/* The int32 allreduce over the same buffers and barriers as inccl_p2p_piece,
+ * with the sum left in int32 (the reference's switch add, nts.c:361-363, and
+ * nothing else): copy in -> barrier -> pull + sum shard `me` from every peer ->
+ * barrier -> gather every shard.  send may alias recv. */
+int inccl_p2p_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
+                            hipStream_t st)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    if (W > INCCL_MAX_LOCAL_INPUTS) return inccl_set_error(INCCL_ERR_ARG, "p2p engine supports up to %d GPUs",
+                                                          INCCL_MAX_LOCAL_INPUTS);
+    if (n == 0) return 0;
+    const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
+    int rc = p2p_ensure(c, total);
+    if (rc) return rc;
+    if (c->p2p_last_stream && c->p2p_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[8], 0));
+    INCCL_HIP(hipMemcpyAsync(c->p2p_part, send, n * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    if (total > n) INCCL_HIP(hipMemsetAsync(c->p2p_part + n, 0, (total - n) * sizeof(int32_t), st));
+    rc = sync_and_barrier(c, st);
+    if (rc) return rc;
+    const void *peer[INCCL_MAX_LOCAL_INPUTS];
+    for (int j = 0; j < W; ++j) peer[j] = c->p2p_peer_part[j] + (size_t)me * shard;
+    rc = inccl_k_peer_sum_q32(peer, W, (int32_t *)(c->p2p_res + (size_t)me * shard), shard, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p int32 reduce-scatter launch failed (%d)", rc);
+    rc = sync_and_barrier(c, st);
+    if (rc) return rc;
+    const void *src[INCCL_MAX_LOCAL_INPUTS];
+    int64_t off[INCCL_MAX_LOCAL_INPUTS], cnt[INCCL_MAX_LOCAL_INPUTS];
+    for (int j = 0; j < W; ++j) {
+        const size_t lo = (size_t)j * shard;
+        src[j] = c->p2p_peer_res[j] + lo;
+        off[j] = (int64_t)lo;
+        cnt[j] = lo >= n ? 0 : (int64_t)((n - lo) < shard ? (n - lo) : shard);
+    }
+    rc = inccl_k_peer_gather(src, off, cnt, W, recv, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p int32 gather launch failed (%d)", rc);
+    INCCL_HIP(hipEventRecord(c->ev[8], st));
+    c->p2p_last_stream = st;
+    return 0;
+}

@@ -319,6 +319,10 @@ int inccl_tp_allreduce_q32(struct inccl_communicator *c, const int32_t *send, in
                            hipStream_t st)
 {
     if (is_local(c)) return inccl_local_allreduce_q32(c, send, recv, n, st);
+    /* the IPC engines carry the int32 allreduce without RCCL */
+    if ((c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH) &&
+        c->group->world_size > 1)
+        return inccl_p2p_allreduce_q32(c, send, recv, n, st);
     int rc = ensure_rccl(c);
     if (rc) return rc;
     if (!c->nccl) {

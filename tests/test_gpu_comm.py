@@ -3,6 +3,7 @@
 in-process transport (ranks = threads sharing one GPU, the GPU's sum kernel is
 the switch) and over RCCL at world size 1.  Checked against the oracle."""
 import os
+import socket
 import subprocess
 import threading
 
@@ -48,6 +49,18 @@ def test_host_example_binary(gpu, tmp_path):
     for world in (2, 4):
         r = subprocess.run([str(exe), str(world), "local"], capture_output=True, text=True, timeout=300)
         assert r.returncode == 0 and "result ok" in r.stdout, r.stdout + r.stderr
+    # exactly as host.c is run: one process per rank, rank 0 the TCP master
+    # (both on GPU 0 here, so RCCL refuses and the ranks fall back to p2p together)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, INCCL_MASTER_PORT=str(port), INCCL_DEVICE="0", INCCL_BOOT_TIMEOUT="120")
+    ps = [subprocess.Popen([str(exe), "2", "127.0.0.1", str(r)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True, env=env) for r in range(2)]
+    outs = [p.communicate(timeout=240) for p in ps]
+    for p, (out, err) in zip(ps, outs):
+        assert p.returncode == 0 and "result ok" in out, out + err
 
 
 @pytest.mark.parametrize("variant", ["write", "sendrecv"])

@@ -219,3 +219,84 @@ def test_engine_peer_timeout(gpu, engine):
     assert res[0][0] and res[1][0], res
     assert res[1][1] is None, res
     assert res[0][1] is not None and "timed out" in res[0][1], res
+
+
+def _refapi_main(rank, world, port, q, engine):
+    """The reference's own caller, one process per rank (host.c:28-59): group +
+    communicator create, inccl_allreduce_write / _sendrecv on host int32 arrays,
+    plus the device int32 allreduce -- over the IPC engines, no RCCL."""
+    try:
+        if engine != "default":
+            os.environ["INCCL_ENGINE"] = engine
+        os.environ["INCCL_DEVICE"] = "0"
+        os.environ["INCCL_BOOT_TIMEOUT"] = "120"
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        from container_inc_amd import inccl
+        grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port)
+        assert grp is not None, "group create failed"
+        comm = inccl.inccl_communicator_create(grp, 4096 * 4)       # host.c:41
+        assert comm is not None
+        res = {"engine": comm.engine}
+        n = 4096                                                     # host.c:20-25
+        src = (np.arange(n, dtype=np.int64) * (rank + 1)).astype(np.int32)
+        for name, fn in (("write", inccl.inccl_allreduce_write), ("sendrecv", inccl.inccl_allreduce_sendrecv)):
+            dst = np.zeros(n, np.int32)
+            fn(comm, src, n, dst)
+            res[name] = bool(np.array_equal(dst, np.arange(n, dtype=np.int64).astype(np.int32)
+                                            * (world * (world + 1) // 2)))   # host.c:51-55 at world 2: 3*i
+        m = 1024 * 37                                                # whole messages, int32 wrap-around
+        xs = [np.random.default_rng(900 + r).integers(-2 ** 31, 2 ** 31, m, dtype=np.int64).astype(np.int32)
+              for r in range(world)]
+        xs[0][:4] = [2 ** 31 - 1, -2 ** 31, -1, 0]
+        want = np.sum([x.astype(np.uint32) for x in xs], axis=0, dtype=np.uint32).view(np.int32)
+        dst = np.zeros(m, np.int32)
+        comm.allreduce_write(xs[rank], m, dst)
+        res["random"] = bool(np.array_equal(dst, want))
+        reg_src, reg_dst = xs[rank].copy(), np.zeros(m, np.int32)
+        comm.host_register(reg_src)
+        comm.host_register(reg_dst)
+        comm.allreduce_write(reg_src, m, reg_dst)
+        res["registered"] = bool(np.array_equal(reg_dst, want))
+        k = 100_003                                                  # device int32 allreduce, ragged
+        dev = torch.device("cuda:0")
+        qs = [np.random.default_rng(950 + r).integers(-2 ** 31, 2 ** 31, k, dtype=np.int64).astype(np.int32)
+              for r in range(world)]
+        got = comm.allreduce_q32(torch.from_numpy(qs[rank]).to(dev))
+        torch.cuda.synchronize()
+        want_q = np.sum([x.astype(np.uint32) for x in qs], axis=0, dtype=np.uint32).view(np.int32)
+        res["device"] = bool(np.array_equal(got.cpu().numpy(), want_q))
+        comm.destroy()
+        grp.destroy()
+        q.put((rank, res, None))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "default")])
+def test_reference_api_multiprocess(gpu, world, engine):
+    """host.c's known answer with one process per rank on GPU 0.  "default"
+    leaves the engine to the communicator: RCCL refuses ranks sharing a GPU, so
+    every rank must agree to fall back to the p2p engine."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_refapi_main, args=(r, world, port, q, engine)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, ok, err = q.get(timeout=240)
+            res[r] = (ok, err)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        ok, err = res[r]
+        assert err is None, f"rank {r}: {err}"
+        assert ok.pop("engine") == "p2p", ok
+        assert all(ok.values()), f"rank {r}: {ok}"
