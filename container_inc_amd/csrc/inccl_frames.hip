@@ -272,14 +272,14 @@ __device__ void build_header_image(uint8_t* fr, const InccFrameTemplate& h, bool
     bth[4] = (uint8_t)(q >> 24); bth[5] = (uint8_t)(q >> 16); bth[6] = (uint8_t)(q >> 8); bth[7] = (uint8_t)q;
 }
 
-// What one egress wave needs from global memory for output frame g: loaded one
+// What one egress wave needs from global memory for input frame f: loaded one
 // frame ahead of its use (k_egress), so these dependent loads overlap the
 // previous frame's build + CRC instead of stalling the wave.
 struct EgressIn {
-    int act, port, c;
+    int act, port;
     uint32_t psn, slot;
-    uint32_t op;
-    uint32_t reth;      // lanes 0-3: RETH word (used for WRITE_FIRST)
+    uint32_t op;        // bytes 40-43 of the input frame across lanes (opcode: lane 2)
+    uint32_t reth;      // lane 4c+i: word i of child c's RETH (c < 16)
     int32_t agg[4];     // word j * 64 + lane of the slot's aggregate
 };
 
@@ -289,109 +289,118 @@ struct EgressIn {
 __device__ __forceinline__ EgressIn egress_fetch(const InccSwitchState& s, const uint8_t* __restrict__ in_frames,
                                                  int64_t in_stride, const int32_t* __restrict__ ports,
                                                  const int32_t* __restrict__ action,
-                                                 const uint32_t* __restrict__ psns, int64_t g, int lane)
+                                                 const uint32_t* __restrict__ psns, int64_t f, int lane)
 {
     EgressIn e;
     const int fan = s.fan_in;
-    const int64_t f = g / fan;
-    e.c = (int)(g % fan);
     e.act = action[f];
     e.port = ports[f];
     e.psn = psns[f];
-    // bytes 40-43 across lanes (the opcode is byte 42): a lane-varying load stays
-    // in a VGPR, where a uniform one would be read into an SGPR at once -- and
-    // that wait would also drain the previous frame's stores
+    // a lane-varying load stays in a VGPR, where a uniform one would be read into
+    // an SGPR at once -- and that wait would also drain the previous frame's stores
     e.op = in_frames[f * in_stride + 40 + (lane & 3)];
     e.slot = e.psn & (s.slots - 1);
-    e.reth = lane < 4 ? s.reth[((size_t)e.slot * fan + e.c) * 4 + lane] : 0u;
+    e.reth = lane < 4 * fan ? s.reth[(size_t)e.slot * fan * 4 + lane] : 0u;
     const int32_t* agg = s.agg + (size_t)e.slot * kLanes;
 #pragma unroll
     for (int j = 0; j < 4; ++j) e.agg[j] = agg[j * kWave + lane];
     return e;
 }
 
+// Every output frame of input frame f (rows f * fan_in + c): all fan_in children
+// on COMPLETED (the broadcast, nts.c:368-371), the sender's child on REPLAY
+// (nts.c:353-356).  The payload (htonl of the aggregate, util.c:403-405 /
+// :419-421) is written into the LDS frame once and shared by the children; each
+// child rewrites only the header bytes before its ICRC and copy-out.
 __device__ void egress_emit(const InccSwitchState& s, const EgressIn& e, const uint8_t (*himg)[kHdrImg],
                             uint8_t* __restrict__ out, int64_t out_stride, bool out16, int32_t* __restrict__ out_len,
-                            const CrcLds& t, uint8_t* frbuf, int64_t g, int lane)
+                            const CrcLds& t, uint8_t* frbuf, int64_t f, int lane)
 {
-    const bool emit = (e.act == INCCL_SW_COMPLETED) || (e.act == INCCL_SW_REPLAY && e.port == e.c);
-    if (!emit) {
-        if (lane == 0) out_len[g] = 0;
-        return;
-    }
     const int fan = s.fan_in;
+    const bool all = e.act == INCCL_SW_COMPLETED;
+    const bool one = e.act == INCCL_SW_REPLAY && e.port >= 0 && e.port < fan;
     const uint32_t op = (uint32_t)__shfl((int)e.op, 2, kWave);
     const bool wf = is_write_first((uint8_t)op);
     const int total = 14 + 20 + 8 + 12 + (wf ? 16 : 0) + kLanes * 4 + 4;   // util.c:341-345
+    if (lane < fan) out_len[f * fan + lane] = (all || (one && lane == e.port)) ? total : 0;
+    if (!all && !one) return;
     uint8_t* fr = frbuf;
-    if (lane < kHdrImg / 4)
-        reinterpret_cast<uint32_t*>(fr)[lane] = reinterpret_cast<const uint32_t*>(himg[e.c * 2 + (wf ? 1 : 0)])[lane];
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {                                                 // util.c:378, :386
-        const uint32_t p = e.psn | 0x80000000u;
-        fr[42] = (uint8_t)op;
-        fr[50] = (uint8_t)(p >> 24); fr[51] = (uint8_t)(p >> 16); fr[52] = (uint8_t)(p >> 8); fr[53] = (uint8_t)p;
-    }
-    // offsets 54 / 70 are 2-byte aligned: 16-bit LDS stores
-    if (wf && lane < 4) {                                          // util.c:409-417, reth_keeper[slot][c]
-        uint16_t* r16 = reinterpret_cast<uint16_t*>(fr + 54);
-        r16[2 * lane] = (uint16_t)e.reth;
-        r16[2 * lane + 1] = (uint16_t)(e.reth >> 16);
-    }
     const int doff = 54 + (wf ? 16 : 0);
+    // offsets 54 / 70 are 2-byte aligned: 16-bit LDS stores
     uint16_t* d16 = reinterpret_cast<uint16_t*>(fr + doff);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {                                    // util.c:403-405 / :419-421 htonl
+    for (int j = 0; j < 4; ++j) {
         const int i = j * kWave + lane;
         const uint32_t be = __builtin_bswap32((uint32_t)e.agg[j]);
         d16[2 * i] = (uint16_t)be;
         d16[2 * i + 1] = (uint16_t)(be >> 16);
     }
-    __builtin_amdgcn_wave_barrier();
-    uint8_t saved = 0;
-    if (lane < kNumMasked) {
-        saved = fr[masked_pos(lane)];
-        fr[masked_pos(lane)] = 0xFF;
-    }
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t crc = icrc_wave(fr, t, lane);                    // util.c:424-426
-    __builtin_amdgcn_wave_barrier();
-    if (lane < kNumMasked) fr[masked_pos(lane)] = saved;
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {                                                 // stored host order (LE)
-        fr[total - 4] = (uint8_t)crc;
-        fr[total - 3] = (uint8_t)(crc >> 8);
-        fr[total - 2] = (uint8_t)(crc >> 16);
-        fr[total - 1] = (uint8_t)(crc >> 24);
-    }
-    __builtin_amdgcn_wave_barrier();
-    uint8_t* o = out + g * out_stride;
-    // fixed trip counts (total <= 1098 B): the compiler can then count this
-    // wave's outstanding stores, and the next frame's prefetched loads are not
-    // held behind them by a conservative vmcnt(0)
-    if (out16) {
-        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-        for (int k = 0; k < (kFrameMax / 16 + kWave - 1) / kWave; ++k) {
-            const int i = lane + k * kWave;
-            if (i < (total + 15) / 16) reinterpret_cast<u4*>(o)[i] = reinterpret_cast<const u4*>(fr)[i];
+    const int c0 = all ? 0 : e.port, c1 = all ? fan : e.port + 1;
+    for (int c = c0; c < c1; ++c) {
+        // header bytes 0-49 from the image (50-53 are the PSN, below; the image's
+        // bytes past 53 would overlap the shared payload)
+        if (lane < 13)
+            reinterpret_cast<uint32_t*>(fr)[lane] = reinterpret_cast<const uint32_t*>(himg[c * 2 + (wf ? 1 : 0)])[lane];
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {                                             // util.c:378, :386
+            const uint32_t p = e.psn | 0x80000000u;
+            fr[42] = (uint8_t)op;
+            fr[50] = (uint8_t)(p >> 24); fr[51] = (uint8_t)(p >> 16); fr[52] = (uint8_t)(p >> 8); fr[53] = (uint8_t)p;
         }
-    } else {
-#pragma unroll
-        for (int k = 0; k < (kFrameMax / 4 + kWave - 1) / kWave; ++k) {
-            const int i = lane + k * kWave;
-            if (i < (total + 3) / 4) reinterpret_cast<uint32_t*>(o)[i] = reinterpret_cast<const uint32_t*>(fr)[i];
+        if (wf) {                                                    // util.c:409-417, reth_keeper[slot][c]
+            uint32_t r = (uint32_t)__shfl((int)e.reth, (4 * c + (lane & 3)) & (kWave - 1), kWave);
+            if (c >= kWave / 4 && lane < 4) r = s.reth[((size_t)e.slot * fan + c) * 4 + lane];
+            if (lane < 4) {
+                uint16_t* r16 = reinterpret_cast<uint16_t*>(fr + 54);
+                r16[2 * lane] = (uint16_t)r;
+                r16[2 * lane + 1] = (uint16_t)(r >> 16);
+            }
         }
+        __builtin_amdgcn_wave_barrier();
+        uint8_t saved = 0;
+        if (lane < kNumMasked) {
+            saved = fr[masked_pos(lane)];
+            fr[masked_pos(lane)] = 0xFF;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t crc = icrc_wave(fr, t, lane);                // util.c:424-426
+        __builtin_amdgcn_wave_barrier();
+        if (lane < kNumMasked) fr[masked_pos(lane)] = saved;
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {                                             // stored host order (LE)
+            fr[total - 4] = (uint8_t)crc;
+            fr[total - 3] = (uint8_t)(crc >> 8);
+            fr[total - 2] = (uint8_t)(crc >> 16);
+            fr[total - 1] = (uint8_t)(crc >> 24);
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint8_t* o = out + (f * fan + c) * out_stride;
+        // fixed trip counts (total <= 1098 B): the compiler can then count this
+        // wave's outstanding stores, and the next frame's prefetched loads are
+        // not held behind them by a conservative vmcnt(0)
+        if (out16) {
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+            for (int k = 0; k < (kFrameMax / 16 + kWave - 1) / kWave; ++k) {
+                const int i = lane + k * kWave;
+                if (i < (total + 15) / 16) reinterpret_cast<u4*>(o)[i] = reinterpret_cast<const u4*>(fr)[i];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < (kFrameMax / 4 + kWave - 1) / kWave; ++k) {
+                const int i = lane + k * kWave;
+                if (i < (total + 3) / 4) reinterpret_cast<uint32_t*>(o)[i] = reinterpret_cast<const uint32_t*>(fr)[i];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
-    if (lane == 0) out_len[g] = total;
     // the result is known from now on: later retransmits replay (nts.c:366)
-    if (e.act == INCCL_SW_COMPLETED && e.c == 0 && lane == 0) atomicOr(&s.arrival[e.slot], 1u << fan);
-    __builtin_amdgcn_wave_barrier();
+    if (all && lane == 0) atomicOr(&s.arrival[e.slot], 1u << fan);
 }
 
 // Egress (nts.c:365-372 / :447-453 broadcast, :353-356 / :435-438 replay;
-// frames per util.c:331-442): wave (f, c) builds child c's copy of frame f.
-// Persistent: each wave walks its output frames with the next one's inputs in
+// frames per util.c:331-442): wave f builds input frame f's output frames.
+// Persistent: each wave walks its input frames with the next one's inputs in
 // flight.
 __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState s, const uint8_t* __restrict__ in_frames,
                                                                int64_t in_stride, int64_t count,
@@ -411,21 +420,21 @@ __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState 
     __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     const bool out16 = ((out_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
-    const int64_t total = count * fan, step = (int64_t)gridDim.x * kEgressWaves;
-    int64_t g = (int64_t)blockIdx.x * kEgressWaves + w;
-    if (g >= total) return;
+    const int64_t step = (int64_t)gridDim.x * kEgressWaves;
+    int64_t f = (int64_t)blockIdx.x * kEgressWaves + w;
+    if (f >= count) return;
     // two register sets used alternately (no copy between them: a copy would
     // wait on every outstanding store of the previous frame too)
-    EgressIn a = egress_fetch(s, in_frames, in_stride, ports, action, psns, g, lane), b;
+    EgressIn a = egress_fetch(s, in_frames, in_stride, ports, action, psns, f, lane), b;
     for (;;) {
-        if (g + step < total) b = egress_fetch(s, in_frames, in_stride, ports, action, psns, g + step, lane);
-        egress_emit(s, a, himg, out, out_stride, out16, out_len, t, buf[w], g, lane);
-        g += step;
-        if (g >= total) break;
-        if (g + step < total) a = egress_fetch(s, in_frames, in_stride, ports, action, psns, g + step, lane);
-        egress_emit(s, b, himg, out, out_stride, out16, out_len, t, buf[w], g, lane);
-        g += step;
-        if (g >= total) break;
+        if (f + step < count) b = egress_fetch(s, in_frames, in_stride, ports, action, psns, f + step, lane);
+        egress_emit(s, a, himg, out, out_stride, out16, out_len, t, buf[w], f, lane);
+        f += step;
+        if (f >= count) break;
+        if (f + step < count) a = egress_fetch(s, in_frames, in_stride, ports, action, psns, f + step, lane);
+        egress_emit(s, b, himg, out, out_stride, out16, out_len, t, buf[w], f, lane);
+        f += step;
+        if (f >= count) break;
     }
 }
 
@@ -553,7 +562,7 @@ int inccl_k_switch_egress(const InccSwitchState* s, const uint8_t* in_frames, si
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     // persistent grid, two blocks per CU: the 64 KiB CRC tables are loaded once per block
-    const int64_t need = ((int64_t)count * s->fan_in + kEgressWaves - 1) / kEgressWaves;
+    const int64_t need = ((int64_t)count + kEgressWaves - 1) / kEgressWaves;
     const int64_t cap = (int64_t)num_cus() * 2;
     const int eg = (int)(need < cap ? (need < 1 ? 1 : need) : cap);
     hipLaunchKernelGGL(k_egress, dim3(eg), dim3(kWave * kEgressWaves), 0, st, *s,
