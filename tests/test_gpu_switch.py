@@ -86,7 +86,8 @@ def _expected_frame(orc, t, c, agg, psn, op, reth):
                                 src_mac=bytes(t[c]["src_mac"]), dst_mac=bytes(t[c]["dst_mac"]))
 
 
-@pytest.mark.parametrize("fan_in", [2, 3, 8])
+# 20 children: RETH words of children 16+ are loaded directly, not shuffled from the prefetch
+@pytest.mark.parametrize("fan_in", [2, 3, 8, 20])
 def test_switch_batches(gpu, orc, fan_in):
     import torch
     from container_inc_amd import inccl
