@@ -257,26 +257,29 @@ def main():
     # N>1: pick the exchange engine / chunking during warmup (untimed).  Every
     # candidate must produce a bit-identical result (integer sums are exact);
     # any failure or mismatch on any rank drops that candidate on all ranks.
-    chosen = ("rccl", 1)
+    chosen = ("rccl", 1, {})
     tuning = []
     if world > 1:
+        # (engine, rccl chunks, environment of the candidate): the mesh engines'
+        # phase lag is a scheduling knob whose best value depends on the fabric
+        # (DESIGN.md "Engine mesh"), so both the default and a short lag run
         cands = []
         if a.engine in ("auto", "rccl"):
-            cands += [("rccl", c) for c in ([a.chunks] if a.chunks else [1, 4])]
+            cands += [("rccl", c, {}) for c in ([a.chunks] if a.chunks else [1, 4])]
         if a.engine in ("auto", "ar"):
-            cands.append(("ar", 1))
+            cands.append(("ar", 1, {}))
         if a.engine in ("auto", "a2a"):
-            cands.append(("a2a", 1))
+            cands.append(("a2a", 1, {}))
         if a.engine in ("auto", "p2p"):
-            cands.append(("p2p", 1))
-        if a.engine in ("auto", "mesh"):
-            cands.append(("mesh", 1))
-        if a.engine in ("auto", "meshw"):
-            cands.append(("meshw", 1))
+            cands.append(("p2p", 1, {}))
+        for eng in ("mesh", "meshw"):
+            if a.engine in ("auto", eng):
+                cands += [(eng, 1, {}), (eng, 1, {"INCCL_MESH_LAG": "32"})]
         ref = None
         best = None
-        for eng, ch in cands:
+        for eng, ch, env in cands:
             ok, dt = 1, float("inf")
+            os.environ.update(env)
             try:
                 comm.set_engine(eng)
                 for _ in range(3):
@@ -293,17 +296,21 @@ def main():
                 torch.cuda.synchronize()
                 dt = time.perf_counter() - t0
             except Exception as e:  # noqa: BLE001
-                print(f"rank {rank}: engine {eng} chunks {ch} failed: {e}", file=sys.stderr, flush=True)
+                print(f"rank {rank}: engine {eng} chunks {ch} {env} failed: {e}", file=sys.stderr, flush=True)
                 ok = 0
+            for key in env:
+                os.environ.pop(key, None)
             v = torch.tensor([dt if ok else float("inf"), 0.0 if ok else 1.0], dtype=torch.float64)
             dist.all_reduce(v, op=dist.ReduceOp.MAX)
             good = v[1].item() == 0.0
-            tuning.append({"engine": eng, "chunks": ch, "ok": good, "ms": round(v[0].item() * 200, 3) if good else None})
+            tuning.append({"engine": eng, "chunks": ch, "env": env or None, "ok": good,
+                           "ms": round(v[0].item() * 200, 3) if good else None})
             if good and (best is None or v[0].item() < best[0]):
-                best = (v[0].item(), eng, ch)
+                best = (v[0].item(), eng, ch, env)
         if best is not None:
-            chosen = (best[1], best[2])
+            chosen = (best[1], best[2], best[3])
         comm.set_engine(chosen[0])
+        os.environ.update(chosen[2])
     chunks = chosen[1]
 
     def step():
@@ -396,6 +403,7 @@ def main():
             "parallelism": f"dp{world}",
             "chunks": chunks,
             "engine": comm.engine if world > 1 else "fused",
+            "engine_env": (chosen[2] or None) if world > 1 else None,
             "engine_tuning": tuning or None,
             "shard_elems": chunk_plan(n, world, chunks)[0][2] if world > 1 else n,
         },
@@ -419,6 +427,8 @@ def main():
         res["collective"] = {"algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2),
                              "bytes_per_rank": n * 4}
     if world > 1 and not a.no_sweep:
+        for key in chosen[2]:   # the sweep runs every engine with its defaults
+            os.environ.pop(key, None)
         res["sweep"] = size_sweep(comm, dev, R, k, rank)
         comm.set_engine(chosen[0])
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
