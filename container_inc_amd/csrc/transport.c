@@ -29,6 +29,19 @@ static int nccl_check(ncclResult_t r, const char *what)
     return inccl_set_error(INCCL_ERR_NCCL, "%s: %s", what, ncclGetErrorString(r));
 }
 
+/* a collective's own return code, then the communicator's asynchronous error
+ * (a peer that died, a network failure): RCCL reports those only this way */
+static int nccl_call(struct inccl_communicator *c, ncclResult_t r, const char *what)
+{
+    int rc = nccl_check(r, what);
+    if (rc) return rc;
+    ncclResult_t ae = ncclSuccess;
+    if (c->nccl && ncclCommGetAsyncError((ncclComm_t)c->nccl, &ae) == ncclSuccess && ae != ncclSuccess &&
+        ae != ncclInProgress)
+        return inccl_set_error(INCCL_ERR_NCCL, "%s: asynchronous RCCL error: %s", what, ncclGetErrorString(ae));
+    return 0;
+}
+
 int inccl_rccl_comm_init(struct inccl_communicator *c)
 {
     struct inccl_group *g = c->group;
@@ -65,25 +78,25 @@ void inccl_rccl_comm_destroy(struct inccl_communicator *c)
 int inccl_rccl_reduce_scatter_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t shard,
                                   hipStream_t st)
 {
-    return nccl_check(ncclReduceScatter(send, recv, shard, ncclInt32, ncclSum, (ncclComm_t)c->nccl, st),
+    return nccl_call(c, ncclReduceScatter(send, recv, shard, ncclInt32, ncclSum, (ncclComm_t)c->nccl, st),
                       "ncclReduceScatter");
 }
 
 int inccl_rccl_all_gather_f32(struct inccl_communicator *c, const float *send, float *recv, size_t shard,
                               hipStream_t st)
 {
-    return nccl_check(ncclAllGather(send, recv, shard, ncclFloat32, (ncclComm_t)c->nccl, st), "ncclAllGather");
+    return nccl_call(c, ncclAllGather(send, recv, shard, ncclFloat32, (ncclComm_t)c->nccl, st), "ncclAllGather");
 }
 
 int inccl_rccl_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
                              hipStream_t st)
 {
-    return nccl_check(ncclAllReduce(send, recv, n, ncclInt32, ncclSum, (ncclComm_t)c->nccl, st), "ncclAllReduce");
+    return nccl_call(c, ncclAllReduce(send, recv, n, ncclInt32, ncclSum, (ncclComm_t)c->nccl, st), "ncclAllReduce");
 }
 
 int inccl_rccl_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st)
 {
-    return nccl_check(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, (ncclComm_t)c->nccl, st),
+    return nccl_call(c, ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, (ncclComm_t)c->nccl, st),
                       "ncclAllReduce(max)");
 }
 
@@ -104,7 +117,7 @@ int inccl_rccl_alltoall_q32(struct inccl_communicator *c, const int32_t *send, i
             rc = nccl_check(ncclRecv(recv + (size_t)j * shard, shard, ncclInt32, j, (ncclComm_t)c->nccl, st),
                             "ncclRecv");
     }
-    int rc2 = nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    int rc2 = nccl_call(c, ncclGroupEnd(), "ncclGroupEnd");
     return rc ? rc : rc2;
 }
 
