@@ -111,9 +111,16 @@ __device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds& t, int lane)
         for (int n = 0; n < 8; ++n) r ^= t.lane_sh[n][(c >> (4 * n)) & 15u][lane];
         c = r;
     }
-#pragma unroll
-    for (int l = 0; l < 6; ++l) c ^= (uint32_t)__shfl_xor((int)c, 1 << l, kWave);
-    return ~c;
+    // XOR-reduce the 64 lane contributions with DPP (one VALU op per step, no
+    // LDS): quads, half-rows, rows, then the row broadcasts; lane 63 ends with
+    // the whole window
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x140, 0xF, 0xF, false);   // row_mirror
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x142, 0xA, 0xF, false);   // row_bcast15 -> rows 1, 3
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x143, 0xC, 0xF, false);   // row_bcast31 -> rows 2, 3
+    return ~(uint32_t)__builtin_amdgcn_readlane((int)c, 63);
 }
 
 // stage `bytes` of a global frame into LDS (dword loads; frames are 4-B aligned)
