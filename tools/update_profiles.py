@@ -39,6 +39,8 @@ def main():
         shutil.copy(os.path.join(src, "bench.json"), os.path.join(prof, f"{tag}_bench_n1.json"))
     if os.path.exists(os.path.join(src, "prof", "run_kernel_stats.csv")):
         shutil.copy(os.path.join(src, "prof", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_bench_n1_kernel_stats.csv"))
+    if os.path.exists(os.path.join(src, "bench_profiled.json")):
+        shutil.copy(os.path.join(src, "bench_profiled.json"), os.path.join(prof, f"{tag}_bench_n1_under_rocprof.json"))
     traffic_path = os.path.join(prof, "pmc_traffic.json")
     traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
     n = a.mib * (1 << 20) // 4
