@@ -12,11 +12,12 @@
 // (64 lanes x 17 B), so leading zeros do not change the raw CRC.  CRC-32 is
 // linear over GF(2): the window's raw CRC is the XOR over lanes of
 // Z_{17 (63 - lane)}(crc(segment)), Z_n = "append n zero bytes".  Each lane
-// (1) reads its 17 bytes as 6 dwords + byte-aligns them, (2) runs a byte-table
-// CRC through a 32-way replicated table (one copy per ds_read_b32 bank, so the
-// 64 data-dependent lookups of a wave-instruction never conflict), (3) applies
+// (1) reads its 17 bytes as 6 dwords + byte-aligns them, (2) computes the
+// segment's CRC as 34 independent nibble lookups (byte j's contribution is
+// Z_{16-j}(T[b_j]); a 2.2 KiB table whose 16 entries per lookup sit in 16
+// distinct banks, so no dependency chain and no bank conflicts), (3) applies
 // its own fixed Z as 8 nibble lookups in a lane-major table (bank = lane), and
-// (4) the wave XOR-reduces.  64 KiB of tables per block.
+// (4) the wave XOR-reduces.  34 KiB of tables per block.
 //
 // State on the GPU (slots = PSN ring size, power of two; the reference uses 16):
 //   agg[slots][256] int32        aggregator        (nts.c:55)
@@ -25,6 +26,7 @@
 //   reth[slots][fan_in][16 B]    RETH of each child's WRITE_FIRST (nts.c:57, :442)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <mutex>
 
@@ -37,21 +39,21 @@ constexpr int kWin = 1088;            // 64 lanes x 17 bytes
 constexpr int kSeg = 17;
 constexpr int kFrameMax = 1152;       // staged frame bytes (>= 1098)
 constexpr int kWavesPerBlock = 4;
-constexpr int kIcrcWaves = 8;        // 512-lane blocks, two per CU (74 KiB of LDS each)
-constexpr int kEgressWaves = 8;       // 512-lane blocks, CU-sized persistent grid
+constexpr int kIcrcWaves = 8;        // 512-lane blocks, three per CU (43 KiB of LDS each)
+constexpr int kEgressWaves = 8;       // 512-lane blocks, two per CU, persistent grid
 constexpr int kLanes = 256;           // int32 lanes per packet (nts.c:55)
 
-__device__ uint32_t g_crc_tab[256];          // util.c:141-150 table 0
+__device__ uint32_t g_seg[kSeg][2][16];       // [byte j][nibble][value] = Z_{16-j}(T[value << 4 nibble]), T = util.c:141-150
 __device__ uint32_t g_lane_shift[8][16][kWave];   // [nibble][value][lane] = Z_{17 (63 - lane)}(value << 4 nibble)
 
 struct CrcLds {
-    uint32_t rep[256][32];          // byte table, one copy per ds_read_b32 bank
+    uint32_t seg[kSeg][2][16];      // a lane's segment CRC as 34 independent nibble lookups (2.2 KiB)
     uint32_t lane_sh[8][16][kWave]; // per-lane zero-append operator, nibble-sliced
 };
 
 __device__ __forceinline__ void load_tables(CrcLds& t)
 {
-    for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) (&t.rep[0][0])[i] = g_crc_tab[i >> 5];
+    for (int i = threadIdx.x; i < kSeg * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg[0][0][0])[i];
     uint32_t* dst = &t.lane_sh[0][0][0];
     const uint32_t* src = &g_lane_shift[0][0][0];
     for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) dst[i] = src[i];
@@ -95,16 +97,16 @@ __device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds& t, int lane)
                 a[k] = z >= 4 ? 0u : (z > 0 ? a[k] & (0xFFFFFFFFu << (8 * z)) : a[k]);
             }
         }
-        const uint32_t* rep = &t.rep[0][0] + (lane & 31);
-        // byte-table CRC (util.c:190-192 form), a dword at a time
+        // the segment's CRC register (util.c:190-192 run from 0) is linear in its
+        // bytes: XOR over byte j of Z_{16-j}(T[b_j]), each split into two nibble
+        // lookups.  No lookup depends on another, and the 16 entries one
+        // ds_read_b32 can touch sit in 16 distinct banks (no conflicts).
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            c ^= a[k];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) c = (c >> 8) ^ rep[(c & 0xFFu) << 5];
+            for (int i = 0; i < 8; ++i) c ^= t.seg[4 * k + (i >> 1)][i & 1][(a[k] >> (4 * i)) & 15u];
         }
-        c ^= a[4] & 0xFFu;
-        c = (c >> 8) ^ rep[(c & 0xFFu) << 5];
+        c ^= t.seg[16][0][a[4] & 15u] ^ t.seg[16][1][(a[4] >> 4) & 15u];
         // shift to the window's end: Z_{17 (63 - lane)}(c)
         uint32_t r = 0;
 #pragma unroll
@@ -467,6 +469,7 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_recycle(InccSwitchSta
 // host: CRC tables (util.c:141-159) and the zero-append operators per tree level
 // ---------------------------------------------------------------------------
 uint32_t host_tab[256];
+uint32_t host_seg[kSeg][2][16];
 uint32_t host_lane_shift[8][16][kWave];
 bool g_tables_ready[64];
 std::mutex g_tables_mu;
@@ -489,6 +492,9 @@ int ensure_tables()
         for (int j = 0; j < 8; ++j) c = (c >> 1) ^ ((c & 1u) ? 0xEDB88320u : 0u);
         host_tab[i] = c;
     }
+    for (int j = 0; j < kSeg; ++j)
+        for (int h = 0; h < 2; ++h)
+            for (uint32_t v = 0; v < 16; ++v) host_seg[j][h][v] = zeros_append(host_tab[v << (4 * h)], kSeg - 1 - j);
     // Z_n is linear: Z_{n+17}(x) = Z_17(Z_n(x)), so lanes are filled from 63 down
     for (int n = 0; n < 8; ++n)
         for (uint32_t v = 0; v < 16; ++v) {
@@ -498,7 +504,7 @@ int ensure_tables()
                 x = zeros_append(x, kSeg);
             }
         }
-    e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc_tab), host_tab, sizeof(host_tab));
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg), host_seg, sizeof(host_seg));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane_shift), host_lane_shift, sizeof(host_lane_shift));
     if (e != hipSuccess) return (int)e;
     if (dev >= 0 && dev < 64) g_tables_ready[dev] = true;
@@ -517,6 +523,17 @@ int num_cus()
             cus = 256;
     }
     return cus;
+}
+
+// persistent blocks per CU (43-48 KiB of LDS each, so up to three fit).  The
+// ICRC kernel is fastest at three (65.9 vs 78.4 us per 131 072 frames at two),
+// egress at two (189 us at three: its stores and prefetches contend).
+// INCCL_ICRC_BLOCKS_PER_CU / INCCL_EGRESS_BLOCKS_PER_CU override for sweeps.
+int blocks_per_cu(const char* env, int dflt)
+{
+    const char* e = getenv(env);
+    const int v = e ? atoi(e) : 0;
+    return (v >= 1 && v <= 3) ? v : dflt;
 }
 
 inline int grid_for(int64_t waves)
@@ -539,7 +556,7 @@ int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* o
     int rc = ensure_tables();
     if (rc) return rc;
     const int64_t blocks = ((int64_t)count + kIcrcWaves - 1) / kIcrcWaves;
-    const int64_t cap = (int64_t)num_cus() * 2;   // persistent: the 64 KiB of tables are loaded once per block
+    const int64_t cap = (int64_t)num_cus() * blocks_per_cu("INCCL_ICRC_BLOCKS_PER_CU", 3);   // persistent: tables loaded once per block
     const int grid = (int)(blocks < cap ? blocks : cap);
     hipLaunchKernelGGL(k_icrc, dim3(grid), dim3(kWave * kIcrcWaves), 0, (hipStream_t)stream, frames,
                        (int64_t)stride, (int64_t)count, out);
@@ -568,9 +585,9 @@ int inccl_k_switch_egress(const InccSwitchState* s, const uint8_t* in_frames, si
     int rc = ensure_tables();
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    // persistent grid, two blocks per CU: the 64 KiB CRC tables are loaded once per block
+    // persistent grid: the CRC tables are loaded once per block
     const int64_t need = ((int64_t)count + kEgressWaves - 1) / kEgressWaves;
-    const int64_t cap = (int64_t)num_cus() * 2;
+    const int64_t cap = (int64_t)num_cus() * blocks_per_cu("INCCL_EGRESS_BLOCKS_PER_CU", 2);
     const int eg = (int)(need < cap ? (need < 1 ? 1 : need) : cap);
     hipLaunchKernelGGL(k_egress, dim3(eg), dim3(kWave * kEgressWaves), 0, st, *s,
                        in_frames, (int64_t)in_stride, (int64_t)count, ports, action, psns, tmpl, out,
