@@ -429,20 +429,34 @@ __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState 
     __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     const bool out16 = ((out_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+    // Round r covers frames [r * step, (r + 1) * step); in round r this wave
+    // takes frame r * step + (wave + r) mod step.  Rotating the offset by one per
+    // round balances the waves: only every fan_in-th input frame of a PSN
+    // completes it and emits, and with a fixed offset (step is even) the waves of
+    // the other residues would idle while the rest built every output frame.
+    // Once a round's frame is past count, every later round's is too.
     const int64_t step = (int64_t)gridDim.x * kEgressWaves;
-    int64_t f = (int64_t)blockIdx.x * kEgressWaves + w;
+    int64_t rot = (int64_t)blockIdx.x * kEgressWaves + w, base = 0;
+    int64_t f = rot;
     if (f >= count) return;
+    auto next = [&]() {
+        base += step;
+        rot = rot + 1 == step ? 0 : rot + 1;
+        return base + rot;
+    };
     // two register sets used alternately (no copy between them: a copy would
     // wait on every outstanding store of the previous frame too)
     EgressIn a = egress_fetch(s, in_frames, in_stride, ports, action, psns, f, lane), b;
     for (;;) {
-        if (f + step < count) b = egress_fetch(s, in_frames, in_stride, ports, action, psns, f + step, lane);
+        int64_t fn = next();
+        if (fn < count) b = egress_fetch(s, in_frames, in_stride, ports, action, psns, fn, lane);
         egress_emit(s, a, himg, out, out_stride, out16, out_len, t, buf[w], f, lane);
-        f += step;
+        f = fn;
         if (f >= count) break;
-        if (f + step < count) a = egress_fetch(s, in_frames, in_stride, ports, action, psns, f + step, lane);
+        fn = next();
+        if (fn < count) a = egress_fetch(s, in_frames, in_stride, ports, action, psns, fn, lane);
         egress_emit(s, b, himg, out, out_stride, out16, out_len, t, buf[w], f, lane);
-        f += step;
+        f = fn;
         if (f >= count) break;
     }
 }
