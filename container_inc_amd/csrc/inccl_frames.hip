@@ -125,15 +125,25 @@ __device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds& t, int lane)
     return ~(uint32_t)__builtin_amdgcn_readlane((int)c, 63);
 }
 
-// stage `bytes` of a global frame into LDS (dword loads; frames are 4-B aligned)
-__device__ __forceinline__ void stage_frame(uint8_t* lds, const uint8_t* g, int bytes, int lane)
+// Header word of a frame (bytes 16-19), loaded lane-varying so that it stays a
+// vector load: a uniform one would go through the scalar cache, and the LDS
+// waits of the running CRC (lgkmcnt) would then wait for it too.
+__device__ __forceinline__ uint32_t icrc_hdr_load(const uint8_t* g, int lane)
 {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(lds);
-    const int words = (bytes + 3) >> 2;
-    for (int i = lane; i < words; i += kWave) dst[i] = src[i];
+    return reinterpret_cast<const uint32_t*>(g)[4 + (lane & 1)];
 }
 
+__device__ __forceinline__ int icrc_ip_total(uint32_t hdr_lane)
+{
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)hdr_lane, 0);
+    return (int)(((h & 0xFFu) << 8) | ((h >> 8) & 0xFFu));
+}
+
+__device__ __forceinline__ bool icrc_len_ok(int ipt) { return ipt >= 28 && ipt <= kWin && 14 + ipt <= kFrameMax; }
+
+// Persistent: each wave walks its frames with the next frame's words (5 dwords
+// a lane, coalesced) and the one after's header in flight while the current
+// frame's CRC runs from LDS.
 __global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __restrict__ frames, int64_t stride,
                                                                 int64_t count, uint32_t* __restrict__ out)
 {
@@ -141,25 +151,45 @@ __global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __res
     __shared__ __attribute__((aligned(16))) uint8_t buf[kIcrcWaves][kFrameMax];
     load_tables(t);
     __syncthreads();
-    const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    for (int64_t f0 = (int64_t)blockIdx.x * kIcrcWaves; f0 < count; f0 += (int64_t)gridDim.x * kIcrcWaves) {
-        const int64_t f = f0 + w;
-        if (f < count) {
-            const uint8_t* g = frames + f * stride;
-            const int ip_total = ((int)g[16] << 8) | g[17];
-            const int bytes = 14 + ip_total;
-            if (ip_total < 28 || ip_total > kWin || bytes > kFrameMax) {
-                if (lane == 0) out[f] = 0;
-            } else {
-                stage_frame(buf[w], g, bytes, lane);
-                __builtin_amdgcn_wave_barrier();
-                if (lane < kNumMasked) buf[w][masked_pos(lane)] = 0xFF;
-                __builtin_amdgcn_wave_barrier();
-                const uint32_t crc = icrc_wave(buf[w], t, lane);
-                if (lane == 0) out[f] = crc;
-            }
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    constexpr int kWords = (kFrameMax / 4 + kWave - 1) / kWave;   // 5
+    const int64_t step = (int64_t)gridDim.x * kIcrcWaves;
+    int64_t f = (int64_t)blockIdx.x * kIcrcWaves + w;
+    if (f >= count) return;
+    uint32_t* lds = reinterpret_cast<uint32_t*>(buf[w]);
+    auto fetch = [&](int64_t fr, int ipt, uint32_t (&v)[kWords]) {
+        const uint32_t* g = reinterpret_cast<const uint32_t*>(frames + fr * stride);
+        const int words = icrc_len_ok(ipt) ? (14 + ipt + 3) >> 2 : 0;
+#pragma unroll
+        for (int k = 0; k < kWords; ++k) {
+            const int i = lane + k * kWave;
+            v[k] = i < words ? g[i] : 0u;
         }
+    };
+    int ip = icrc_ip_total(icrc_hdr_load(frames + f * stride, lane));
+    uint32_t cur[kWords];
+    fetch(f, ip, cur);
+    uint32_t hdrN = f + step < count ? icrc_hdr_load(frames + (f + step) * stride, lane) : 0u;
+    for (;;) {
+#pragma unroll
+        for (int k = 0; k < kWords; ++k)
+            if (lane + k * kWave < kFrameMax / 4) lds[lane + k * kWave] = cur[k];
         __builtin_amdgcn_wave_barrier();
+        if (lane < kNumMasked) buf[w][masked_pos(lane)] = 0xFF;
+        __builtin_amdgcn_wave_barrier();
+        const int64_t fn = f + step;
+        int ipn = 0;
+        if (fn < count) {
+            ipn = icrc_ip_total(hdrN);
+            fetch(fn, ipn, cur);
+            hdrN = fn + step < count ? icrc_hdr_load(frames + (fn + step) * stride, lane) : 0u;
+        }
+        const uint32_t crc = icrc_len_ok(ip) ? icrc_wave(buf[w], t, lane) : 0u;
+        if (lane == 0) out[f] = crc;
+        __builtin_amdgcn_wave_barrier();
+        f = fn;
+        ip = ipn;
+        if (f >= count) break;
     }
 }
 
