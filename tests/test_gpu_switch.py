@@ -170,3 +170,80 @@ def test_switch_rejects_bad_frames(gpu, orc):
     action, _ = sw.ingress(frames, ports)
     assert action.cpu().tolist() == [inccl.SW_ABSORBED, inccl.SW_INVALID, inccl.SW_ACK, inccl.SW_INVALID]
     sw.destroy()
+
+
+# Batches far larger than one round of the persistent egress grid (about 4096
+# waves): many rounds, load batches of several rounds, a partial last round, and
+# the per-round rotation of each wave's frame offset wrapping.  Every emitted
+# row is checked (length, payload = htonl of the wrap-around sum, ICRC), and a
+# sample of rows including the batch's last ones byte-exact against the oracle.
+@pytest.mark.parametrize("fan_in,P", [(2, 40000), (3, 21111)])
+def test_switch_large_batch_all_frames(gpu, orc, fan_in, P):
+    import torch
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(300 + fan_in)
+    n = fan_in * P
+    base = {op: np.frombuffer(orc.build_data_frame(np.zeros(256, np.int32), psn=0, opcode=op, qp=0x11,
+                                                   with_reth=(op == 0x06), reth=bytes(16) if op == 0x06 else None),
+                              np.uint8) for op in (0x06, 0x07, 0x08)}
+    psn = np.repeat(np.arange(P, dtype=np.uint32), fan_in)
+    port = np.tile(np.arange(fan_in, dtype=np.int32), P)
+    perm = rng.permutation(n)                      # arrivals interleaved across PSNs and ports
+    psn, port = psn[perm], port[perm]
+    op_of = np.array([0x06, 0x07, 0x07, 0x08], np.uint8)[psn % 4]
+    pay = rng.integers(INT32_MIN, INT32_MAX, (n, 256), dtype=np.int64, endpoint=True).astype(np.int32)
+    reth = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    frames = np.zeros((n, STRIDE), np.uint8)
+    for op in (0x06, 0x07, 0x08):
+        idx = np.nonzero(op_of == op)[0]
+        frames[idx, : len(base[op])] = base[op]
+        off = 70 if op == 0x06 else 54
+        if op == 0x06:
+            frames[idx, 54:70] = reth[idx]
+        frames[idx, off:off + 1024] = pay[idx].astype(">i4").view(np.uint8).reshape(len(idx), 1024)
+        frames[idx, 50:54] = (psn[idx] | 0x80000000).astype(">u4").view(np.uint8).reshape(len(idx), 4)
+    sw = inccl.GpuSwitch(fan_in, 1 << (int(np.ceil(np.log2(P))) + 1))
+    tmpl = _templates(fan_in)
+    tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
+    fr = torch.from_numpy(frames).to(gpu)
+    pt = torch.from_numpy(port).to(gpu)
+    action, psn_out = sw.ingress(fr, pt)
+    out, out_len = sw.egress(fr, pt, action, psn_out, tmpl_dev)
+    torch.cuda.synchronize()
+    act = action.cpu().numpy()
+    assert np.array_equal(psn_out.cpu().numpy(), psn)
+    done = act == inccl.SW_COMPLETED
+    assert done.sum() == P and np.array_equal(np.sort(psn[done]), np.arange(P))
+    assert (act[~done] == inccl.SW_ABSORBED).all()
+    # the wrap-around sum of every PSN (nts.c:361-363)
+    agg = np.zeros((P, 256), np.uint32)
+    np.add.at(agg, psn, pay.view(np.uint32))
+    ln = out_len.cpu().numpy().reshape(n, fan_in)
+    wf = op_of == 0x06
+    want_len = np.where(wf, 1098, 1082)
+    assert (ln[~done] == 0).all()
+    assert (ln[done] == want_len[done][:, None]).all()
+    rows = (np.nonzero(done)[0][:, None] * fan_in + np.arange(fan_in)[None, :]).reshape(-1)
+    o = out.view(-1, out.shape[-1])[torch.from_numpy(rows).to(gpu)]
+    oc = o.cpu().numpy()
+    row_frame = rows // fan_in
+    off = np.where(wf[row_frame], 70, 54)
+    for d in (54, 70):
+        sel = off == d
+        got = oc[sel, d:d + 1024].copy().view(">u4").astype(np.uint32)
+        assert np.array_equal(got, agg[psn[row_frame[sel]]])
+    lens = want_len[row_frame]
+    crc_stored = np.array([int.from_bytes(oc[i, lens[i] - 4:lens[i]].tobytes(), "little") for i in range(len(rows))],
+                          np.uint32)
+    crc = inccl.icrc_frames(o).cpu().numpy().view(np.uint32)
+    assert np.array_equal(crc, crc_stored)
+    # byte-exact sample: the batch's last emitted rows and random ones
+    src_row = {(int(p), int(c)): i for i, (p, c) in enumerate(zip(psn, port))}
+    sample = list(range(len(rows) - 2 * fan_in, len(rows))) + [int(x) for x in rng.choice(len(rows), 40, replace=False)]
+    for j in sample:
+        f, c = int(row_frame[j]), int(rows[j] % fan_in)
+        p = int(psn[f])
+        want = _expected_frame(orc, tmpl, c, agg[p].view(np.int32), p, int(op_of[f]),
+                               reth[src_row[(p, c)]].tobytes())
+        assert bytes(oc[j, : len(want)]) == want, (j, f, c)
+    sw.destroy()
