@@ -14,10 +14,19 @@ and produces their allreduce over all ranks into a third buffer:
           (config 4; DESIGN.md "Multi-GPU"); then the config 5 size sweep
 value = bucket bytes reduced per second over the whole job = N * R * 256 MiB / t.
 
-Extra JSON fields: ``roofline`` for the dominant kernel (the fused / quant+sum
-kernel, algorithmic bytes (R+1)*4*n per launch, timed with HIP events on its
-own stream) and ``cpu_baseline`` (the C oracle on a bounded sample, rank 0 at
-N = 1 only).
+Extra JSON fields:
+  roofline          N = 1: the fused kernel's HBM roofline (algorithmic bytes
+                    (R+1)*4*n per launch, timed with HIP events on its own stream).
+                    N > 1: the step's xGMI link roofline; the quant+sum kernel's
+                    HBM figure is roofline_hbm_kernel
+  cpu_baseline      the C oracle on a bounded sample, rank 0 at N = 1 only
+  sizes             N = 1: north_star's 4/64/256/1024 MiB buckets, kernel GB/s + HBM fraction
+  roofline_cold     N = 1: the fused kernel rotating through input sets far larger
+                    than the 256 MiB Infinity Cache
+  numerics_vs_exact N = 1: error vs the exact (fp64) sum, R = 2 and 8, k = 25 and auto
+  host_e2e          N = 1: BASELINE config 3, 1 GiB pinned host fp32 in 64 MiB buckets
+  sweep             N > 1: 4 KiB .. 256 MiB and 1 GiB per engine, verified with
+                    alternating input sets
 """
 from __future__ import annotations
 
@@ -47,6 +56,8 @@ def parse():
     p.add_argument("--no-sweep", action="store_true", help="N>1: skip the bucket-size sweep (BASELINE config 5)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extras", action="store_true",
+                   help="N=1: skip the size list, cold-input run, numerics and host-memory (config 3) keys")
     p.add_argument("--grid-cap", type=int, default=0)
     p.add_argument("--json-out", default="")
     return p.parse_args()
@@ -142,54 +153,247 @@ def cpu_reference_pipeline(seconds: float) -> dict:
                                       f"switch aggregation and ICRC framing, {dt:.1f} s"}
 
 
-def size_sweep(comm, dev, R: int, k: int, rank: int) -> list:
-    """BASELINE config 5 at N > 1: bucket sizes 4 KiB (one reference message,
-    api.h:39) to 256 MiB in x4 steps, per engine: host wall time per call over back-to-back
-    calls (max over ranks), and whether the output is bit-identical to the
-    first engine's.  Buckets up to the ll threshold (1 MiB) take the one-kernel
-    ll engine; rccl / ar run everywhere for comparison."""
+# 4 KiB (one reference message, api.h:39) .. 256 MiB in x4 steps (BASELINE config 5),
+# plus north_star's 1024 MiB point
+SWEEP_BYTES = [(4 << 10) << (2 * i) for i in range(9)] + [1 << 30]
+# xGMI: 7 links per MI355X, 153.6 GB/s per link counting both directions (AMD's
+# per-link figure; 76.8 GB/s each way).  A rank of a W-GPU full mesh has W-1 links.
+XGMI_LINK_GBS_BIDIR = 153.6
+
+
+def xgmi_roofline(world: int, bucket_bytes: int, seconds: float) -> dict:
+    """Link roofline of one N>1 step: RS + AG move (W-1)/W of the bucket out of
+    every rank and (W-1)/W into it, twice (int32 partials, fp32 results):
+    4 (W-1)/W B bytes across the rank's W-1 links, both directions counted,
+    against (W-1) x 153.6 GB/s."""
+    link_bytes = 4 * (world - 1) * bucket_bytes // world
+    achieved = link_bytes / seconds / 1e9
+    peak = (world - 1) * XGMI_LINK_GBS_BIDIR
+    return {"bound": "xgmi", "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "GB/s",
+            "frac": round(achieved / peak, 4), "traffic": None, "link_bytes_per_rank_per_step": link_bytes,
+            "peak_source": f"{world - 1} xGMI links x 153.6 GB/s (both directions; 76.8 GB/s each way)"}
+
+
+def run_verified(comm, eng: str, ch: int, inputs, out, k: int, stream, refs):
+    """Three calls alternating two input sets (A, B, A), each compared with the
+    reference engine's results.  Identical inputs on every call would hide a
+    buffer that is read stale; alternating them cannot.  Returns the three
+    outputs and whether they match `refs` (or, with no refs yet, whether the
+    two A calls agree with each other)."""
+    import torch
+    got = []
+    for xs in (inputs[0], inputs[1], inputs[0]):
+        comm.allreduce_f32(xs, out=out, scale_exp=k, chunks=ch, stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        got.append(out.clone())
+    if refs is None:
+        same = bool(torch.equal(got[0], got[2]))
+    else:
+        same = all(bool(torch.equal(g, refs[i % 2])) for i, g in enumerate(got))
+    return got, same
+
+
+def agree(values, world: int):
+    """Max over ranks of a list of floats (gloo)."""
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor(values, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    return v.tolist()
+
+
+def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
+    """BASELINE config 5 at N > 1 (and north_star's 1024 MiB point): per bucket
+    size and engine, host wall time per call over back-to-back calls (max over
+    ranks), GB/s, the xGMI link fraction, and whether the results of two
+    alternating input sets are bit-identical to the first engine's."""
     import torch
     import torch.distributed as dist
     rows = []
-    for b in [(4 << 10) << (2 * i) for i in range(9)]:   # 4 KiB .. 256 MiB in x4 steps (BASELINE config 5)
+    for b in SWEEP_BYTES:
         n = b // 4
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(7000 + rank)
-        xs = [torch.randn(n, generator=gen, device=dev) for _ in range(R)]
+        inputs = []
+        for seed in (7000, 8000):
+            gen = torch.Generator(device=dev)
+            gen.manual_seed(seed + rank)
+            inputs.append([torch.randn(n, generator=gen, device=dev) for _ in range(R)])
         out = torch.empty(n, device=dev)
         st = torch.cuda.Stream(device=dev)
         torch.cuda.synchronize()   # inputs made on torch's stream; the calls run on st
-        ref = None
-        iters = 50 if b <= (1 << 20) else 10
-        for eng in (("rccl", "ar", "ll") if b <= (1 << 20) else ("rccl", "ar", "p2p", "mesh", "meshw")):
-            ok, dt, same = 1, float("inf"), True
+        refs = None
+        iters = 50 if b <= (1 << 20) else (10 if b <= (256 << 20) else 4)
+        engines = ("rccl", "ar", "ll", "p2p") if b <= (1 << 20) else ("rccl", "ar", "a2a", "p2p", "mesh", "meshw")
+        for eng in engines:
+            ok, dt, same, got = 1, float("inf"), False, None
             try:
                 comm.set_engine(eng)
-                for _ in range(3):
-                    comm.allreduce_f32(xs, out=out, scale_exp=k, stream=st.cuda_stream)
-                torch.cuda.synchronize()
-                if ref is None:
-                    ref = out.clone()
-                else:
-                    same = bool(torch.equal(ref, out))
+                got, same = run_verified(comm, eng, 1, inputs, out, k, st, refs)
                 dist.barrier()
                 t0 = time.perf_counter()
                 for _ in range(iters):
-                    comm.allreduce_f32(xs, out=out, scale_exp=k, stream=st.cuda_stream)
+                    comm.allreduce_f32(inputs[0], out=out, scale_exp=k, stream=st.cuda_stream)
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) / iters
             except Exception as e:  # noqa: BLE001
                 print(f"rank {rank}: sweep {b} B engine {eng} failed: {e}", file=sys.stderr, flush=True)
                 ok = 0
-            v = torch.tensor([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0],
-                             dtype=torch.float64)
-            dist.all_reduce(v, op=dist.ReduceOp.MAX)
-            good = v[1].item() == 0.0
-            rows.append({"bucket_bytes": b, "engine": eng, "ok": good,
-                         "us": round(v[0].item() * 1e6, 2) if good else None,
-                         "algbw_GBps": round(b / v[0].item() / 1e9, 2) if good else None,
-                         "bit_identical": v[2].item() == 0.0})
+            v = agree([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0], world)
+            good, ident = v[1] == 0.0, v[2] == 0.0
+            if good and ident and refs is None:
+                refs = (got[0], got[1])
+            row = {"bucket_bytes": b, "engine": eng, "ok": good, "bit_identical": good and ident,
+                   "us": round(v[0] * 1e6, 2) if good else None,
+                   "algbw_GBps": round(b / v[0] / 1e9, 2) if good else None,
+                   "value_GBps": round(world * R * b / v[0] / 1e9, 2) if good else None}
+            if good:
+                row["xgmi_frac"] = xgmi_roofline(world, b, v[0])["frac"]
+            rows.append(row)
+            del got
+        del inputs, out, refs
+        torch.cuda.empty_cache()
+    return rows
+
+
+def kernel_time_ms(fn, stream, iters: int) -> float:
+    """Mean device time of fn() (one launch on `stream`) from HIP events on that stream."""
+    import torch
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def n1_sizes(dev, R: int, k: int, sizes_mib=(4, 64, 256, 1024)) -> list:
+    """north_star's bucket sizes at N = 1: the fused kernel on R resident buckets
+    of each size, GB/s of buckets reduced and the kernel's HBM roofline fraction."""
+    import torch
+
+    from container_inc_amd import inccl
+    rows = []
+    st = torch.cuda.Stream(device=dev)
+    for mib in sizes_mib:
+        n = mib * (1 << 20) // 4
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1000)
+        xs = [torch.randn(n, generator=gen, device=dev) for _ in range(R)]
+        out = torch.empty(n, device=dev)
+        torch.cuda.synchronize()
+        iters = max(10, min(400, (4 << 30) // (mib << 20)))
+        ms = kernel_time_ms(lambda: inccl.reduce_f32(xs, k, out=out, stream=st.cuda_stream), st, iters)
+        alg = (R + 1) * 4 * n
+        rows.append({"bucket_mib": mib, "kernel_us": round(ms * 1e3, 2),
+                     "GBps_buckets": round(R * 4 * n / (ms * 1e-3) / 1e9, 1),
+                     "hbm_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
+                     "hbm_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
         del xs, out
+    torch.cuda.empty_cache()
+    return rows
+
+
+def cold_run(dev, R: int, k: int, n: int, sets: int = 4) -> dict:
+    """The fused kernel rotating through `sets` independent input/output sets
+    (sets * (R+1) * 4n bytes, far beyond the 256 MiB Infinity Cache), so no launch
+    finds its inputs left on die by the previous one: an HBM figure by construction."""
+    import torch
+
+    from container_inc_amd import inccl
+    st = torch.cuda.Stream(device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2000)
+    groups = [([torch.randn(n, generator=gen, device=dev) for _ in range(R)], torch.empty(n, device=dev))
+              for _ in range(sets)]
+    torch.cuda.synchronize()
+    it = [0]
+
+    def one():
+        xs, out = groups[it[0] % sets]
+        it[0] += 1
+        inccl.reduce_f32(xs, k, out=out, stream=st.cuda_stream)
+
+    ms = kernel_time_ms(one, st, 40)
+    alg = (R + 1) * 4 * n
+    del groups
+    torch.cuda.empty_cache()
+    return {"sets": sets, "working_set_MiB": sets * alg >> 20, "kernel_us": round(ms * 1e3, 2),
+            "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
+            "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def host_e2e(comm, k: int, gib: int = 1, bucket_mib: int = 64) -> dict:
+    """BASELINE config 3: a `gib` GiB fp32 gradient in pinned host memory through
+    inccl_allreduce_f32_host (bucket_mib buckets, H2D / reduce / D2H on three
+    streams).  PCIe-inclusive; reported beside `value`, never as it."""
+    import torch
+    n = (gib << 30) // 4
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(n, generator=gen, dtype=torch.float32).pin_memory()
+    y = torch.empty(n, dtype=torch.float32).pin_memory()
+    comm.allreduce_f32_host(x, y, scale_exp=k, bucket_bytes=bucket_mib << 20)   # warm
+    reps = 4
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        comm.allreduce_f32_host(x, y, scale_exp=k, bucket_bytes=bucket_mib << 20)
+    dt = (time.perf_counter() - t0) / reps
+    del x, y
+    return {"gradient_GiB": gib, "bucket_MiB": bucket_mib, "streams": 3, "ms": round(dt * 1e3, 2),
+            "GBps": round((gib << 30) / dt / 1e9, 2),
+            "pcie_GBps_both_directions": round(2 * (gib << 30) / dt / 1e9, 2),
+            "what": "pinned host fp32 -> H2D -> fused quantise+sum+dequantise -> D2H, wall clock"}
+
+
+def numerics_vs_exact(dev, n: int) -> list:
+    """Error of the engine's result against the exact sum (fp64 of the fp32
+    inputs) on config-2 data (N(0,1), seeds 1000+r), per (R, scale):
+    max abs error, max relative error, and the fraction of lanes whose relative
+    error exceeds north_star's 1e-6.  The engine is bit-exact vs its own spec
+    (the oracle); this is the spec's distance from the true sum."""
+    import torch
+
+    from container_inc_amd import inccl
+    rows = []
+    for R in (2, 8):
+        gen = torch.Generator(device=dev)
+        xs = []
+        for r in range(R):
+            gen.manual_seed(1000 + r)
+            xs.append(torch.randn(n, generator=gen, device=dev))
+        exact = torch.zeros(n, dtype=torch.float64, device=dev)
+        for x in xs:
+            exact += x.double()
+        fp32_naive = xs[0].clone()
+        for x in xs[1:]:
+            fp32_naive += x
+        absx = exact.abs()
+        nz = absx > 0
+        for k in (25, "auto"):
+            if k == "auto":
+                word = torch.zeros(4, dtype=torch.int32, device=dev)
+                out = inccl.reduce_f32_auto(xs, word=word)
+                amax = float(word[:1].view(torch.float32).item())
+                kk = inccl.choose_scale(amax, R)
+            else:
+                out = inccl.reduce_f32(xs, k)
+                kk = k
+            torch.cuda.synchronize()
+            err = (out.double() - exact).abs()
+            rel = torch.where(nz, err / absx.clamp_min(1e-300), torch.zeros_like(err))
+            nerr = (fp32_naive.double() - exact).abs()
+            nrel = torch.where(nz, nerr / absx.clamp_min(1e-300), torch.zeros_like(nerr))
+            rows.append({"R": R, "scale_exp": kk, "auto": k == "auto", "lanes": n,
+                         "max_abs_err": float(err.max().item()),
+                         "bound_abs": R * 2.0 ** -(kk + 1),
+                         "max_rel_err": float(rel.max().item()),
+                         "frac_rel_gt_1e-6": float((rel > 1e-6).double().mean().item()),
+                         "frac_rel_gt_1e-6_fp32_naive_sum": float((nrel > 1e-6).double().mean().item())})
+            del out, err, rel, nerr, nrel
+        del xs, exact, fp32_naive, absx, nz
+    torch.cuda.empty_cache()
     return rows
 
 
@@ -206,7 +410,6 @@ def load_traffic(workload: str):
 
 def main():
     a = parse()
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -224,6 +427,8 @@ def main():
     if os.environ.get("INCCL_BENCH_SAME_DEVICE") == "1":
         local_rank = 0
     os.environ.setdefault("INCCL_BOOT_TIMEOUT", "120")
+    # an ll / mesh candidate whose peer never arrives costs 2 s, not 5
+    os.environ.setdefault("INCCL_LL_TIMEOUT_MS", "2000")
     if a.engine in ("p2p", "mesh", "meshw"):
         os.environ["INCCL_ENGINE"] = a.engine   # no eager RCCL communicator
     torch.cuda.set_device(local_rank)
@@ -255,14 +460,19 @@ def main():
             dist.barrier()
 
     # N>1: pick the exchange engine / chunking during warmup (untimed).  Every
-    # candidate must produce a bit-identical result (integer sums are exact);
-    # any failure or mismatch on any rank drops that candidate on all ranks.
+    # candidate runs alternating input sets A, B, A and must reproduce the
+    # reference engine's results bit for bit (integer sums are exact); any
+    # failure or mismatch on any rank drops that candidate on all ranks.  The
+    # first candidate that passes on every rank (rccl when RCCL is up) is the
+    # reference.
     chosen = ("rccl", 1, {})
     tuning = []
+    refs = None
     if world > 1:
-        # (engine, rccl chunks, environment of the candidate): the mesh engines'
-        # phase lag is a scheduling knob whose best value depends on the fabric
-        # (DESIGN.md "Engine mesh"), so both the default and a short lag run
+        gen_b = torch.Generator(device=dev)
+        gen_b.manual_seed(5000 + rank)
+        srcs_b = [torch.randn(n, generator=gen_b, device=dev, dtype=torch.float32) for _ in range(R)]
+        torch.cuda.synchronize()
         cands = []
         if a.engine in ("auto", "rccl"):
             cands += [("rccl", c, {}) for c in ([a.chunks] if a.chunks else [1, 4])]
@@ -275,20 +485,13 @@ def main():
         for eng in ("mesh", "meshw"):
             if a.engine in ("auto", eng):
                 cands += [(eng, 1, {}), (eng, 1, {"INCCL_MESH_LAG": "32"})]
-        ref = None
         best = None
         for eng, ch, env in cands:
-            ok, dt = 1, float("inf")
+            ok, dt, same, got = 1, float("inf"), False, None
             os.environ.update(env)
             try:
                 comm.set_engine(eng)
-                for _ in range(3):
-                    comm.allreduce_f32(srcs, out=out, scale_exp=k, chunks=ch, stream=stream.cuda_stream)
-                torch.cuda.synchronize()
-                if ref is None:
-                    ref = out.clone()
-                elif not torch.equal(ref, out):
-                    ok = 0
+                got, same = run_verified(comm, eng, ch, (srcs, srcs_b), out, k, stream, refs)
                 barrier()
                 t0 = time.perf_counter()
                 for _ in range(5):
@@ -300,17 +503,22 @@ def main():
                 ok = 0
             for key in env:
                 os.environ.pop(key, None)
-            v = torch.tensor([dt if ok else float("inf"), 0.0 if ok else 1.0], dtype=torch.float64)
-            dist.all_reduce(v, op=dist.ReduceOp.MAX)
-            good = v[1].item() == 0.0
-            tuning.append({"engine": eng, "chunks": ch, "env": env or None, "ok": good,
-                           "ms": round(v[0].item() * 200, 3) if good else None})
-            if good and (best is None or v[0].item() < best[0]):
-                best = (v[0].item(), eng, ch, env)
-        if best is not None:
-            chosen = (best[1], best[2], best[3])
+            v = agree([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0], world)
+            good = v[1] == 0.0 and v[2] == 0.0
+            if good and refs is None:
+                refs = (got[0], got[1])
+            tuning.append({"engine": eng, "chunks": ch, "env": env or None, "ok": v[1] == 0.0,
+                           "bit_identical": v[1] == 0.0 and v[2] == 0.0,
+                           "ms": round(v[0] * 200, 3) if v[1] == 0.0 else None})
+            if good and (best is None or v[0] < best[0]):
+                best = (v[0], eng, ch, env)
+            del got
+        if best is None:
+            raise SystemExit("no exchange engine produced verified results on every rank")
+        chosen = (best[1], best[2], best[3])
         comm.set_engine(chosen[0])
         os.environ.update(chosen[2])
+        del srcs_b
     chunks = chosen[1]
 
     def step():
@@ -332,11 +540,13 @@ def main():
     barrier()
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1)
-    t = torch.tensor([wall], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t.item())
+    wall = agree([wall], world)[0]
     ms_per_step = wall * 1e3 / a.steps
+    # the timed steps' output against the reference engine's (N>1)
+    verified = None
+    if refs is not None:
+        verified = agree([0.0 if torch.equal(out, refs[0]) else 1.0], world)[0] == 0.0
+        del refs
 
     # dominant kernel alone: fused (N=1) or quant + local sum (N>1), HIP events on its stream
     kstream = torch.cuda.Stream(device=dev)
@@ -348,16 +558,7 @@ def main():
         else:
             inccl.quant_sum(srcs, k, out=qbuf, stream=kstream.cuda_stream)
 
-    for _ in range(3):
-        kernel()
-    kev0, kev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    kiters = max(a.steps, 20)
-    kev0.record(kstream)
-    for _ in range(kiters):
-        kernel()
-    kev1.record(kstream)
-    torch.cuda.synchronize()
-    k_ms = kev0.elapsed_time(kev1) / kiters
+    k_ms = kernel_time_ms(kernel, kstream, max(a.steps, 20))
     alg_bytes = (R + 1) * 4 * n
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
     per_rank = f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: "
@@ -378,6 +579,20 @@ def main():
                 }.get(comm.engine, comm.engine))
     kname = "k_stream_vec<F32,F32,R>" if world == 1 else "k_stream_vec<F32,Q32,R>"
     traffic = load_traffic(kname + f" R={R} n={n}")
+    hbm_roofline = {
+        "kernel": kname,
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "traffic_source": ("profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE "
+                           "of this kernel and size, recorded in round 1 (not re-measured in this run)")
+        if traffic is not None else None,
+        "alg_bytes_per_launch": alg_bytes,
+        "kernel_ms": round(k_ms, 5),
+    }
 
     value = world * R * n * 4 / (ms_per_step * 1e-3) / 1e9
     res = {
@@ -407,20 +622,15 @@ def main():
             "engine_tuning": tuning or None,
             "shard_elems": chunk_plan(n, world, chunks)[0][2] if world > 1 else n,
         },
-        "roofline": {
-            "kernel": kname,
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "alg_bytes_per_launch": alg_bytes,
-            "kernel_ms": round(k_ms, 5),
-        },
+        # N = 1: the fused kernel's HBM roofline.  N > 1: the step is bound by the
+        # xGMI links, so `roofline` is the link fraction of the whole step and the
+        # dominant HBM kernel's figure moves to `roofline_hbm_kernel`.
+        "roofline": hbm_roofline if world == 1 else xgmi_roofline(world, n * 4, ms_per_step * 1e-3),
         "cpu_baseline": None,
     }
     if world > 1:
+        res["roofline_hbm_kernel"] = hbm_roofline
+        res["verified_vs_reference_engine"] = verified
         # nccl-tests convention (BASELINE config 4): algbw = one rank's bucket bytes
         # / step time; busbw = algbw * 2(W-1)/W, the per-GPU link traffic of RS + AG
         algbw = n * 4 / (ms_per_step * 1e-3) / 1e9
@@ -429,8 +639,13 @@ def main():
     if world > 1 and not a.no_sweep:
         for key in chosen[2]:   # the sweep runs every engine with its defaults
             os.environ.pop(key, None)
-        res["sweep"] = size_sweep(comm, dev, R, k, rank)
+        res["sweep"] = size_sweep(comm, dev, R, k, rank, world)
         comm.set_engine(chosen[0])
+    if world == 1 and not a.no_extras:
+        res["sizes"] = n1_sizes(dev, R, k)
+        res["roofline_cold"] = cold_run(dev, R, k, n)
+        res["numerics_vs_exact"] = numerics_vs_exact(dev, n)
+        res["host_e2e"] = host_e2e(comm, k)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(n, R, k, a.cpu_seconds)
         res["cpu_baseline_allcores"] = cpu_baseline_allcores(n, R, k, min(a.cpu_seconds, 5.0))

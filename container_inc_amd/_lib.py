@@ -54,6 +54,8 @@ SIGNATURES = {
     "inccl_comm_barrier": (_I, [_P]),
     "inccl_comm_set_engine": (_I, [_P, _S]),
     "inccl_comm_engine": (_S, [_P]),
+    "inccl_comm_ipc_mem_kind": (_I, [_P, _S]),
+    "inccl_comm_clear_error": (_I, [_P]),
     "inccl_allreduce_f32": (_I, [_P, _P, _I, _P, _SZ, _I, _P]),
     "inccl_allreduce_f32_pipelined": (_I, [_P, _P, _I, _P, _SZ, _I, _I, _P]),
     "inccl_allreduce_q32": (_I, [_P, _P, _P, _SZ, _P]),

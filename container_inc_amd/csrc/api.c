@@ -53,6 +53,38 @@ int inccl_ensure_dev(void **p, size_t *cur, size_t need)
     return 0;
 }
 
+/* Device memory that peers map over HIP IPC and that a running kernel polls or
+ * reads after a flag (the ll and mesh engines).  Default "uncached"
+ * (hipDeviceMallocUncached): every access bypasses the L2, so a remote GPU's
+ * xGMI store into this HBM cannot hide behind a line this GPU's L2 cached
+ * before it.  Coarse-grained hipMalloc memory is only guaranteed coherent with
+ * other agents at kernel boundaries.  $INCCL_IPC_MEM = uncached | finegrained |
+ * coarse selects the kind (same on every rank). */
+unsigned inccl_ipc_mem_flags(void)
+{
+    const char *e = getenv("INCCL_IPC_MEM");
+    if (e && strcmp(e, "coarse") == 0) return hipDeviceMallocDefault;
+    if (e && strcmp(e, "finegrained") == 0) return hipDeviceMallocFinegrained;
+    return hipDeviceMallocUncached;
+}
+
+hipError_t inccl_ipc_malloc(void **p, size_t bytes)
+{
+    const unsigned f = inccl_ipc_mem_flags();
+    if (f == hipDeviceMallocDefault) return hipMalloc(p, bytes);
+    return hipExtMallocWithFlags(p, bytes, f);
+}
+
+int inccl_mem_kind(const void *p)
+{
+    if (!p) return inccl_set_error(INCCL_ERR_ARG, "mem_kind: NULL pointer");
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof(a));
+    INCCL_HIP(hipPointerGetAttributes(&a, p));
+    if (a.type != hipMemoryTypeDevice) return inccl_set_error(INCCL_ERR_ARG, "mem_kind: not device memory");
+    return (int)a.allocationFlags;
+}
+
 /* ------------------------------------------------------------------ */
 /* stateless device API                                                 */
 /* ------------------------------------------------------------------ */
@@ -448,6 +480,39 @@ int inccl_comm_barrier(struct inccl_communicator *comm)
     return inccl_tp_barrier(comm);
 }
 
+int inccl_comm_ipc_mem_kind(struct inccl_communicator *comm, const char *engine)
+{
+    if (!comm || !engine) return inccl_set_error(INCCL_ERR_ARG, "bad ipc_mem_kind args");
+    const void *p = NULL;
+    if (strcmp(engine, "ll") == 0) p = comm->ll_buf;
+    else if (strcmp(engine, "mesh") == 0 || strcmp(engine, "meshw") == 0) p = comm->mesh_buf;
+    else if (strcmp(engine, "p2p") == 0) p = comm->p2p_part;
+    else return inccl_set_error(INCCL_ERR_ARG, "ipc_mem_kind: unknown engine '%s' (ll | mesh | p2p)", engine);
+    if (!p) return inccl_set_error(INCCL_ERR_STATE, "ipc_mem_kind: engine '%s' has no IPC buffer yet", engine);
+    if (comm->group->device >= 0) INCCL_HIP(hipSetDevice(comm->group->device));
+    return inccl_mem_kind(p);
+}
+
+int inccl_comm_clear_error(struct inccl_communicator *comm)
+{
+    if (!comm) return inccl_set_error(INCCL_ERR_ARG, "comm is NULL");
+    if (comm->group->transport != INCCL_TRANSPORT_RCCL || comm->group->world_size == 1) return 0;
+    INCCL_HIP(hipSetDevice(comm->group->device));
+    const int had = (comm->ll_err_host && *(volatile uint32_t *)comm->ll_err_host) ||
+                    (comm->mesh_err_host && *(volatile uint32_t *)comm->mesh_err_host);
+    /* every rank's kernels have finished (a timed-out kernel finishes by itself)
+     * and nobody reads a peer's buffer any more: drop them; the next ll / mesh
+     * call allocates, zeroes and exchanges fresh ones */
+    INCCL_HIP(hipDeviceSynchronize());
+    int rc = inccl_boot_barrier(comm->group);
+    if (rc) return rc;
+    inccl_ll_release(comm);
+    inccl_mesh_release(comm);
+    rc = inccl_boot_barrier(comm->group);
+    if (rc) return rc;
+    return had;
+}
+
 /* ------------------------------------------------------------------ */
 /* device-resident collectives                                          */
 /* ------------------------------------------------------------------ */
@@ -563,11 +628,13 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
         return kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, k,
                                    amax, scale_R, st));
 
-    /* the IPC engines: one kernel for small buckets (ll.c), else the one-kernel
-     * mesh exchange (mesh.c) or the host-synchronised p2p exchange (p2p.c) */
+    /* the IPC engines: the ll kernel for small buckets when the ll engine was
+     * chosen explicitly (ll.c), else the one-kernel mesh exchange (mesh.c) or the
+     * host-synchronised p2p exchange (p2p.c).  The p2p engine (and the automatic
+     * fallback to it when RCCL is unavailable) never routes to ll by itself. */
     if ((c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH) &&
         c->group->transport == INCCL_TRANSPORT_RCCL) {
-        if (n <= c->ll_max_bytes / sizeof(float) && W > 1)
+        if (c->engine == INCCL_ENGINE_LL && n <= c->ll_max_bytes / sizeof(float) && W > 1)
             return inccl_ll_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
         if (c->engine == INCCL_ENGINE_MESH) return inccl_mesh_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
         return inccl_p2p_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);

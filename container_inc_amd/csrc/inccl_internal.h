@@ -188,6 +188,10 @@ static inline size_t inccl_shard_elems(size_t n, int world)
 }
 
 int inccl_ensure_dev(void **p, size_t *cur, size_t need);
+/* IPC-shared device memory polled by running kernels (ll, mesh): $INCCL_IPC_MEM */
+unsigned inccl_ipc_mem_flags(void);
+hipError_t inccl_ipc_malloc(void **p, size_t bytes);
+int inccl_mem_kind(const void *p);   /* hipPointerAttribute_t.allocationFlags */
 
 /* copypool.c */
 struct inccl_copy_pool *inccl_copy_pool_create(int n);

@@ -54,7 +54,7 @@ static int ll_ensure(struct inccl_communicator *c)
     hipIpcMemHandle_t mine, all[INCCL_MAX_LOCAL_INPUTS];
     memset(&mine, 0, sizeof(mine));
     /* local failures are carried to the collective outcome check below */
-    hipError_t e = hipMalloc((void **)&c->ll_buf, LL_SIG_BYTES + 2 * cap * sizeof(uint32_t));
+    hipError_t e = inccl_ipc_malloc((void **)&c->ll_buf, LL_SIG_BYTES + 2 * cap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(c->ll_buf, 0, LL_SIG_BYTES);   /* synchronous: zero before any peer maps it */
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipIpcGetMemHandle(&mine, c->ll_buf);
@@ -65,7 +65,10 @@ static int ll_ensure(struct inccl_communicator *c)
     }
     if (e != hipSuccess) rc = inccl_hip_check(e, "ll: buffer setup");
     int rc_x = inccl_boot_allgather(g, &mine, all, sizeof(hipIpcMemHandle_t));
-    if (rc_x) return rc_x;
+    if (rc_x) {
+        inccl_ll_release(c);   /* back to a clean state: the next call starts over */
+        return rc_x;
+    }
     for (int j = 0; rc == 0 && j < W; ++j) {
         if (j == me) {
             c->ll_peer[j] = c->ll_buf;

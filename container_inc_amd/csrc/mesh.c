@@ -84,7 +84,7 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     memset(&mine, 0, sizeof(mine));
     int rc = 0;
     /* local failures are carried to the collective outcome check below */
-    hipError_t e = hipMalloc((void **)&c->mesh_buf, MESH_DATA_OFFSET + ((size_t)2 * W + 1) * cap * sizeof(uint32_t));
+    hipError_t e = inccl_ipc_malloc((void **)&c->mesh_buf, MESH_DATA_OFFSET + ((size_t)2 * W + 1) * cap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(c->mesh_buf, 0, MESH_DATA_OFFSET);   /* flags + counters */
     if (e == hipSuccess) e = hipDeviceSynchronize();   /* zeroed before any peer maps it */
     if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.h, c->mesh_buf);
@@ -101,6 +101,7 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     int rc_x = inccl_boot_allgather(g, &mine, all, sizeof(mesh_peer_info));
     if (rc_x) {
         free(all);
+        inccl_mesh_release(c);   /* back to a clean state: the next call starts over */
         inccl_mesh_release(&old);
         return rc_x;
     }
@@ -131,6 +132,7 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     int32_t mine_rc = rc ? 1 : 0, all_rc[INCCL_MAX_LOCAL_INPUTS];
     int rc2 = inccl_boot_allgather(g, &mine_rc, all_rc, sizeof(int32_t));
     if (rc2) {
+        inccl_mesh_release(c);
         inccl_mesh_release(&old);
         return rc2;
     }

@@ -235,6 +235,20 @@ class Communicator:
     def barrier(self) -> None:
         check(load().inccl_comm_barrier(self.handle), "inccl_comm_barrier")
 
+    def ipc_mem_kind(self, engine: str) -> int:
+        """hipDeviceMalloc* flags of the engine's IPC buffer (0 coarse, 1 fine-grained, 3 uncached)."""
+        rc = load().inccl_comm_ipc_mem_kind(self.handle, engine.encode())
+        if rc < 0:
+            check(rc, "inccl_comm_ipc_mem_kind")
+        return rc
+
+    def clear_error(self) -> bool:
+        """Collective: True if an ll / mesh wait had timed out; rebuilds their buffers."""
+        rc = load().inccl_comm_clear_error(self.handle)
+        if rc < 0:
+            check(rc, "inccl_comm_clear_error")
+        return rc == 1
+
     # -- reference collectives on host int32 arrays (api.c:330-452) --
     def allreduce_write(self, src: np.ndarray, length: int, dst: np.ndarray) -> None:
         _host_int32_call(load().inccl_allreduce_write, self.handle, src, length, dst)

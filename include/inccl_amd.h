@@ -119,16 +119,20 @@ int inccl_comm_barrier(struct inccl_communicator *comm);
  *           sum + dequantise kernel over the W shards -> ncclAllGather
  *   "p2p"   library buffers shared via HIP IPC; each GPU pulls its shard from every
  *           peer over xGMI with the fused sum+dequantise kernel, then pulls every
- *           peer's result shard (two group barriers per call); buckets up to
- *           $INCCL_LL_MAX_BYTES (default 1 MiB) take the "ll" kernel instead
- *   "ll"    one kernel per call: quant + local sum into an IPC buffer, arrival flags
- *           written into the peers' memory, every peer's bucket read over xGMI and
- *           summed + dequantised; no host synchronisation (larger buckets: as "p2p")
- *   "mesh"  one persistent kernel per call for large buckets: each chunk's quantised
- *           partial is pushed into its owner's IPC inbox over xGMI, the owner sums +
+ *           peer's result shard (two group barriers per call).  Also the automatic
+ *           fallback when RCCL cannot come up on every rank.
+ *   "ll"    one kernel per call for buckets up to $INCCL_LL_MAX_BYTES (default
+ *           1 MiB): quant + local sum into an IPC buffer, arrival flags written into
+ *           the peers' memory, every peer's bucket read over xGMI and summed +
+ *           dequantised; no host synchronisation (larger buckets: as "p2p")
+ *   "mesh"  one persistent kernel per call: each chunk's quantised partial is
+ *           pushed into its owner's IPC inbox over xGMI, the owner sums +
  *           dequantises it once every rank's arrival flag is up, and every rank pulls
  *           the result chunks; phases of different chunks overlap, no host
- *           synchronisation (buckets up to $INCCL_LL_MAX_BYTES: the "ll" kernel)
+ *           synchronisation
+ *   The ll and mesh buffers are fine-grained uncached device memory by default
+ *   ($INCCL_IPC_MEM = uncached | finegrained | coarse): their kernels poll flags
+ *   that peers write over xGMI while they run.
  *   "meshw" as "mesh", but the owner also pushes each result chunk into every
  *           rank's IPC result inbox, so that every xGMI transfer is a write; each
  *           rank then copies the chunks locally into dst
@@ -137,6 +141,18 @@ int inccl_comm_barrier(struct inccl_communicator *comm);
 int inccl_comm_set_engine(struct inccl_communicator *comm, const char *name);
 /* "rccl", "ar", "a2a", "p2p", "ll", "mesh", "meshw" or "local" */
 const char *inccl_comm_engine(const struct inccl_communicator *comm);
+/* Allocation flags (hipDeviceMallocDefault 0 / Finegrained 1 / Uncached 3) of the
+ * IPC buffer the named engine ("ll", "mesh" or "p2p") has allocated, or a
+ * negative INCCL_ERR_* code if it has none yet. */
+int inccl_comm_ipc_mem_kind(struct inccl_communicator *comm, const char *engine);
+/* Collective (every rank calls it).  An ll or mesh wait that timed out leaves
+ * its call's dst undefined and makes every later call of that engine fail with
+ * "timed out".  This returns 1 if such a timeout had been recorded on this rank
+ * (0 if not, negative on error) and drops the engines' IPC buffers after a
+ * device synchronisation and a group barrier, so that the next call rebuilds
+ * them from a clean state.  Check a call's outcome after synchronising its
+ * stream: a timeout is reported by the NEXT call or by this function. */
+int inccl_comm_clear_error(struct inccl_communicator *comm);
 
 /* Device-resident fp32 allreduce of R local buckets per rank:
  *   dst = dequant( sum over ranks, sum over r<R  quant(srcs[r]) )

@@ -248,3 +248,28 @@ def test_allreduce_f32_host_buckets(gpu, orc):
     np.testing.assert_array_equal(yn.view(np.uint32), want.view(np.uint32))
     comm.destroy()
     grp.destroy()
+
+
+def test_allreduce_f32_host_config3_full_size(gpu, orc):
+    """BASELINE config 3 at its real size: a 1 GiB fp32 gradient in pinned host
+    memory, 16 buckets of 64 MiB through the three-stream H2D / reduce / D2H
+    pipeline (the reference's registered staging buffers, api.c:164-176), plus a
+    ragged tail bucket; every lane bit-exact vs the oracle."""
+    import torch
+    from container_inc_amd import inccl
+    grp = inccl.inccl_group_create(1, 0, "127.0.0.1")
+    comm = inccl.inccl_communicator_create(grp, 0)
+    n = (1 << 30) // 4 + 4099   # 16 full 64 MiB buckets + a ragged 17th
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(n, generator=gen, dtype=torch.float32).pin_memory()
+    y = torch.full((n,), float("nan"), dtype=torch.float32).pin_memory()
+    comm.allreduce_f32_host(x, y, scale_exp=25, bucket_bytes=64 << 20)
+    want = orc.reduce_f32([x.numpy()], 25)
+    bad = np.flatnonzero(y.numpy().view(np.uint32) != want.view(np.uint32))
+    assert bad.size == 0, f"{bad.size} lanes differ, first at {bad[:8]}"
+    # a second call over the same buffers (pipeline state and events reused)
+    y.fill_(float("nan"))
+    comm.allreduce_f32_host(x, y, scale_exp=25, bucket_bytes=64 << 20)
+    assert np.array_equal(y.numpy().view(np.uint32), want.view(np.uint32))
+    comm.destroy()
+    grp.destroy()

@@ -109,6 +109,10 @@ def _rank_main(rank, world, port, cases, q, engine="p2p"):
             torch.cuda.synchronize()
             results.append(bool(np.array_equal(outs[0].cpu().numpy().view(np.uint32), want.view(np.uint32))))
             del graph
+        # the IPC buffer kind: the ll / mesh kernels poll memory that peers write
+        # over xGMI while they run, so it is fine-grained uncached; p2p's
+        # buffers are only read after a kernel boundary and a barrier
+        results.append(comm.ipc_mem_kind(engine) == (0 if engine == "p2p" else 3))
         comm.destroy()
         grp.destroy()
         q.put((rank, results, None))
@@ -191,11 +195,21 @@ def _timeout_main(rank, port, q, engine="ll"):
                 comm.allreduce_f32(x, out=out, scale_exp=20)
             except Exception as e:  # noqa: BLE001
                 err = repr(e)
+        # collective recovery: the timed-out rank reports it, both rebuild the
+        # engine's IPC buffers, and the communicator works again
+        had = comm.clear_error()
+        out.fill_(0)
+        torch.cuda.synchronize()
+        comm.allreduce_f32(x, out=out, scale_exp=20)
+        torch.cuda.synchronize()
+        after_ok = bool((out == 2).all().item())
+        kind = comm.ipc_mem_kind(engine)
         comm.destroy()
         grp.destroy()
-        q.put((rank, first_ok, err))
+        q.put((rank, {"first": first_ok, "after_clear": after_ok, "had": had == (rank == 0),
+                      "uncached": kind == 3}, err))
     except BaseException as e:  # noqa: BLE001
-        q.put((rank, False, "crash " + repr(e)))
+        q.put((rank, {"crash": False}, "crash " + repr(e)))
 
 
 @pytest.mark.parametrize("engine", ["ll", "mesh", "meshw"])
@@ -216,7 +230,7 @@ def test_engine_peer_timeout(gpu, engine):
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
-    assert res[0][0] and res[1][0], res
+    assert all(res[0][0].values()) and all(res[1][0].values()), res
     assert res[1][1] is None, res
     assert res[0][1] is not None and "timed out" in res[0][1], res
 
