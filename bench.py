@@ -242,6 +242,9 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
             good, ident = v[1] == 0.0, v[2] == 0.0
             if good and ident and refs is None:
                 refs = (got[0], got[1])
+            if rank == 0:
+                print(f"sweep {b} B {eng}: ok={good} identical={ident} us={v[0] * 1e6:.1f}", file=sys.stderr,
+                      flush=True)
             row = {"bucket_bytes": b, "engine": eng, "ok": good, "bit_identical": good and ident,
                    "us": round(v[0] * 1e6, 2) if good else None,
                    "algbw_GBps": round(b / v[0] / 1e9, 2) if good else None,
@@ -417,6 +420,9 @@ def main():
     from container_inc_amd import inccl
     from container_inc_amd.plan import chunk_plan
 
+    if os.environ.get("INCCL_BENCH_WATCHDOG"):   # debugging aid: dump every thread's stack when stuck
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["INCCL_BENCH_WATCHDOG"]), repeat=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -507,6 +513,9 @@ def main():
             good = v[1] == 0.0 and v[2] == 0.0
             if good and refs is None:
                 refs = (got[0], got[1])
+            if rank == 0:
+                print(f"tune {eng} chunks={ch} {env or ''}: ok={v[1] == 0.0} identical={v[2] == 0.0} "
+                      f"ms={v[0] * 200:.3f}", file=sys.stderr, flush=True)
             tuning.append({"engine": eng, "chunks": ch, "env": env or None, "ok": v[1] == 0.0,
                            "bit_identical": v[1] == 0.0 and v[2] == 0.0,
                            "ms": round(v[0] * 200, 3) if v[1] == 0.0 else None})

@@ -485,7 +485,7 @@ int inccl_comm_ipc_mem_kind(struct inccl_communicator *comm, const char *engine)
     if (!comm || !engine) return inccl_set_error(INCCL_ERR_ARG, "bad ipc_mem_kind args");
     const void *p = NULL;
     if (strcmp(engine, "ll") == 0) p = comm->ll_buf;
-    else if (strcmp(engine, "mesh") == 0 || strcmp(engine, "meshw") == 0) p = comm->mesh_buf;
+    else if (strcmp(engine, "mesh") == 0 || strcmp(engine, "meshw") == 0) p = comm->mesh_reg[1];   /* the inbox */
     else if (strcmp(engine, "p2p") == 0) p = comm->p2p_part;
     else return inccl_set_error(INCCL_ERR_ARG, "ipc_mem_kind: unknown engine '%s' (ll | mesh | p2p)", engine);
     if (!p) return inccl_set_error(INCCL_ERR_STATE, "ipc_mem_kind: engine '%s' has no IPC buffer yet", engine);

@@ -25,6 +25,12 @@
 #define INCCL_ENGINE_MESH 4
 #define INCCL_ENGINE_AR 5
 #define INCCL_MAX_HOST_REGIONS 16
+#define INCCL_MESH_REGIONS 4
+/* Largest single allocation exported over HIP IPC.  hipIpcOpenMemHandle of a
+ * 2.5 GiB allocation never returned under the HIP runtime torch bundles (ROCm
+ * 7.0; measured: tools/mesh_size_probe.py, DESIGN.md "IPC buffer lifecycle"),
+ * so every IPC buffer is split or refused below 2 GiB. */
+#define INCCL_IPC_MAX_BYTES (((size_t)2 << 30) - ((size_t)2 << 20))
 
 struct inccl_local_hub;
 struct inccl_shm_bar;
@@ -86,8 +92,9 @@ struct inccl_communicator {
     size_t ll_max_bytes;         /* buckets up to this size take the ll kernel */
     /* mesh engine (large buckets, one persistent kernel per call): one IPC buffer
      * per rank = signal array + counters + inbox (W partial shards) + result shard */
-    char *mesh_buf;
-    char *mesh_peer[INCCL_MAX_LOCAL_INPUTS];
+    char *mesh_buf;                                        /* = mesh_reg[0]: signals + counters */
+    char *mesh_reg[INCCL_MESH_REGIONS];                    /* sig, inbox, result shard, result inbox */
+    char *mesh_peer[INCCL_MESH_REGIONS][INCCL_MAX_LOCAL_INPUTS];   /* rank j's regions ([r][me] = own) */
     size_t mesh_cap;             /* elements per inbox slot / result shard */
     int mesh_grid;               /* this rank's workgroups per call */
     uint32_t *mesh_err_host;     /* host-mapped: set by a kernel whose peers timed out */

@@ -9,18 +9,20 @@
  * so quantisation, the local sums and the xGMI traffic in both directions
  * overlap, and the host never waits.
  *
- * Per rank, one device allocation shared over HIP IPC:
- *   [0, 64 KiB)              signal array: arrive[8][1024] and ready[8][1024] words
- *   [64 KiB, +16)            call counter, retired workgroups, ticket, abort word
- *   [128 KiB, +W*cap*4)      inbox: slot j holds rank j's int32 partial of my shard
- *   [.., +cap*4)             my dequantised result shard (fp32)
- *   [.., +W*cap*4)           result inbox ("meshw"): slot j holds rank j's result shard
+ * Per rank, four device allocations shared over HIP IPC (separate, so that no
+ * single export reaches 2 GiB; see INCCL_IPC_MAX_BYTES):
+ *   sig    [0, 64 KiB) signal array: arrive[8][1024] and ready[8][1024] words;
+ *          [64 KiB, +16) call counter, retired workgroups, ticket, abort word
+ *   inbox  W * cap int32: slot j holds rank j's partial of my shard
+ *   res    cap fp32: my dequantised result shard
+ *   resin  W * cap fp32 ("meshw"): slot j holds rank j's result shard
  * Created collectively on the first call, regrown collectively when a larger
  * bucket arrives (all ranks make the same calls, as with RCCL). */
 #define _GNU_SOURCE
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "inccl_internal.h"
 #include "inccl_kernels.h"
@@ -29,26 +31,52 @@
 #define MESH_CTR_OFFSET MESH_SIG_BYTES
 #define MESH_DATA_OFFSET (MESH_SIG_BYTES + (size_t)65536)
 
+/* $INCCL_TRACE: one timestamped line per setup step (debugging aid) */
+#define MTRACE(...)                                                                      \
+    do {                                                                                 \
+        if (getenv("INCCL_TRACE")) {                                                     \
+            struct timespec ts_;                                                         \
+            clock_gettime(CLOCK_MONOTONIC, &ts_);                                        \
+            fprintf(stderr, "[inccl %d %ld.%06ld] ", c->group->rank, (long)ts_.tv_sec,   \
+                    ts_.tv_nsec / 1000);                                                 \
+            fprintf(stderr, __VA_ARGS__);                                                \
+            fputc('\n', stderr);                                                         \
+        }                                                                                \
+    } while (0)
+
 typedef struct {
-    hipIpcMemHandle_t h;
+    hipIpcMemHandle_t h[INCCL_MESH_REGIONS];
     int pci_domain, pci_bus, pci_dev;   /* ranks sharing a GPU split its workgroup slots */
 } mesh_peer_info;
 
 void inccl_mesh_release(struct inccl_communicator *c)
 {
     const int W = c->group->world_size, me = c->group->rank;
-    if (!c->mesh_buf) return;
+    if (!c->mesh_buf && !c->mesh_reg[1] && !c->mesh_reg[2] && !c->mesh_reg[3]) return;
     hipDeviceSynchronize();
-    for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS; ++j) {
-        if (j != me && c->mesh_peer[j]) hipIpcCloseMemHandle(c->mesh_peer[j]);
-        c->mesh_peer[j] = NULL;
+    for (int r = 0; r < INCCL_MESH_REGIONS; ++r) {
+        for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS; ++j) {
+            if (j != me && c->mesh_peer[r][j]) hipIpcCloseMemHandle(c->mesh_peer[r][j]);
+            c->mesh_peer[r][j] = NULL;
+        }
+        if (c->mesh_reg[r]) hipFree(c->mesh_reg[r]);
+        c->mesh_reg[r] = NULL;
     }
-    hipFree(c->mesh_buf);
     c->mesh_buf = NULL;
     if (c->mesh_err_host) hipHostFree(c->mesh_err_host);
     c->mesh_err_host = NULL;
     c->mesh_err_dev = NULL;
     c->mesh_cap = 0;
+}
+
+/* bytes of region r for W ranks and `cap` elements per slot */
+static size_t mesh_region_bytes(int r, int W, size_t cap)
+{
+    switch (r) {
+        case 0: return MESH_DATA_OFFSET;                          /* signals + counters */
+        case 2: return cap * sizeof(uint32_t);                    /* my result shard */
+        default: return (size_t)W * cap * sizeof(uint32_t);       /* inbox / result inbox */
+    }
 }
 
 /* collective: every rank calls it with the same shard size */
@@ -59,10 +87,16 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     if (c->mesh_buf && c->mesh_cap >= shard) return 0;
     if (W > INCCL_MAX_LOCAL_INPUTS)
         return inccl_set_error(INCCL_ERR_ARG, "mesh engine supports up to %d GPUs", INCCL_MAX_LOCAL_INPUTS);
-    /* make before break (as p2p_ensure): the old buffer stays alive, and mapped
-     * by the peers, until every rank has mapped the new one */
+    const size_t cap = (shard + ((size_t)1 << 19) - 1) & ~(((size_t)1 << 19) - 1);   /* 2 MiB granules */
+    /* every rank computes the same sizes, so every rank refuses alike */
+    if (mesh_region_bytes(1, W, cap) > INCCL_IPC_MAX_BYTES)
+        return inccl_set_error(INCCL_ERR_ARG, "mesh: a %zu-element shard needs a %zu-byte inbox; IPC buffers stay below "
+                               "2 GiB (hipIpcOpenMemHandle of larger ones hangs)", shard, mesh_region_bytes(1, W, cap));
+    /* make before break (as p2p_ensure): the old buffers stay alive, and mapped
+     * by the peers, until every rank has mapped the new ones */
     struct inccl_communicator old = *c;
     if (c->mesh_buf) {   /* everyone's queued accesses to the old buffers drain first */
+        MTRACE("mesh regrow %zu -> %zu: device sync", c->mesh_cap, shard);
         INCCL_HIP(hipDeviceSynchronize());
         int rc = inccl_boot_barrier(g);
         if (rc) return rc;
@@ -70,9 +104,9 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
         c->mesh_err_host = NULL;
         c->mesh_err_dev = NULL;
         c->mesh_cap = 0;
-        for (int j = 0; j < INCCL_MAX_LOCAL_INPUTS; ++j) c->mesh_peer[j] = NULL;
+        memset(c->mesh_reg, 0, sizeof(c->mesh_reg));
+        memset(c->mesh_peer, 0, sizeof(c->mesh_peer));
     }
-    const size_t cap = (shard + ((size_t)1 << 19) - 1) & ~(((size_t)1 << 19) - 1);   /* 2 MiB granules */
     const int dev = g->device >= 0 ? g->device : 0;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
@@ -83,11 +117,17 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     }
     memset(&mine, 0, sizeof(mine));
     int rc = 0;
-    /* local failures are carried to the collective outcome check below */
-    hipError_t e = inccl_ipc_malloc((void **)&c->mesh_buf, MESH_DATA_OFFSET + ((size_t)2 * W + 1) * cap * sizeof(uint32_t));
+    /* local failures are carried to the collective outcome check below.  Four
+     * separate allocations, so that no single IPC export reaches 2 GiB for
+     * buckets up to ~2 GiB at any W */
+    hipError_t e = hipSuccess;
+    for (int r = 0; r < INCCL_MESH_REGIONS && e == hipSuccess; ++r) {
+        e = inccl_ipc_malloc((void **)&c->mesh_reg[r], mesh_region_bytes(r, W, cap));
+        if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.h[r], c->mesh_reg[r]);
+    }
+    c->mesh_buf = c->mesh_reg[0];
     if (e == hipSuccess) e = hipMemset(c->mesh_buf, 0, MESH_DATA_OFFSET);   /* flags + counters */
     if (e == hipSuccess) e = hipDeviceSynchronize();   /* zeroed before any peer maps it */
-    if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.h, c->mesh_buf);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->mesh_err_host, sizeof(uint32_t), hipHostMallocMapped);
     if (e == hipSuccess) {
         *(volatile uint32_t *)c->mesh_err_host = 0;
@@ -97,6 +137,8 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     if (e == hipSuccess) e = hipDeviceGetAttribute(&mine.pci_bus, hipDeviceAttributePciBusId, dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&mine.pci_dev, hipDeviceAttributePciDeviceId, dev);
     if (e != hipSuccess) rc = inccl_hip_check(e, "mesh: buffer setup");
+    MTRACE("mesh alloc 4 regions, inbox %zu B (%s): allgather", mesh_region_bytes(1, W, cap),
+           e == hipSuccess ? "ok" : hipGetErrorString(e));
     /* where everyone is: ranks sharing a GPU size their grids together */
     int rc_x = inccl_boot_allgather(g, &mine, all, sizeof(mesh_peer_info));
     if (rc_x) {
@@ -116,20 +158,22 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     int grid = ge ? atoi(ge) : 0;
     if (grid <= 0) grid = 2 * cus / (sharing > 0 ? sharing : 1);
     if (grid < 4) grid = 4;
-    for (int j = 0; j < W; ++j) {
-        if (j == me) {
-            c->mesh_peer[j] = c->mesh_buf;
-            continue;
+    for (int j = 0; j < W; ++j)
+        for (int r = 0; r < INCCL_MESH_REGIONS; ++r) {
+            if (j == me) {
+                c->mesh_peer[r][j] = c->mesh_reg[r];
+                continue;
+            }
+            if (rc) continue;
+            void *p = NULL;
+            e = hipIpcOpenMemHandle(&p, all[j].h[r], hipIpcMemLazyEnablePeerAccess);
+            if (e != hipSuccess) rc = inccl_hip_check(e, "mesh: hipIpcOpenMemHandle");
+            c->mesh_peer[r][j] = (char *)p;
         }
-        if (rc) continue;
-        void *p = NULL;
-        e = hipIpcOpenMemHandle(&p, all[j].h, hipIpcMemLazyEnablePeerAccess);
-        if (e != hipSuccess) rc = inccl_hip_check(e, "mesh: hipIpcOpenMemHandle");
-        c->mesh_peer[j] = (char *)p;
-    }
     free(all);
     /* agree on the outcome, so that every rank falls back alike */
     int32_t mine_rc = rc ? 1 : 0, all_rc[INCCL_MAX_LOCAL_INPUTS];
+    MTRACE("mesh peers mapped (rc %d): agree", rc);
     int rc2 = inccl_boot_allgather(g, &mine_rc, all_rc, sizeof(int32_t));
     if (rc2) {
         inccl_mesh_release(c);
@@ -143,10 +187,11 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
             inccl_mesh_release(&old);
             return rc;
         }
-    /* every peer has mapped the new buffer: the old one can go */
+    /* every peer has mapped the new buffers: the old ones can go */
     if (old.mesh_buf) {
         int rc_b = inccl_boot_barrier(g);
         inccl_mesh_release(&old);
+        MTRACE("mesh: old buffers released");
         if (rc_b) return rc_b;
     }
     c->mesh_cap = cap;
@@ -214,11 +259,10 @@ int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int
     l.lag = lag;
     l.grid = c->mesh_grid;
     for (int j = 0; j < W; ++j) {
-        char *base = c->mesh_peer[j];
-        l.peer_inbox[j] = (uint32_t *)(base + MESH_DATA_OFFSET);
-        l.peer_res[j] = (const uint32_t *)(base + MESH_DATA_OFFSET + (size_t)W * c->mesh_cap * sizeof(uint32_t));
-        l.peer_resin[j] = (uint32_t *)(base + MESH_DATA_OFFSET + ((size_t)W + 1) * c->mesh_cap * sizeof(uint32_t));
-        l.peer_sig[j] = (uint32_t *)base;
+        l.peer_sig[j] = (uint32_t *)c->mesh_peer[0][j];
+        l.peer_inbox[j] = (uint32_t *)c->mesh_peer[1][j];
+        l.peer_res[j] = (const uint32_t *)c->mesh_peer[2][j];
+        l.peer_resin[j] = (uint32_t *)c->mesh_peer[3][j];
     }
     l.own_resin = l.peer_resin[me];
     l.push_res = c->mesh_push;
@@ -236,6 +280,7 @@ int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int
     /* the buffer-reuse argument needs this rank's calls in order: chain across
      * streams (inside a capture the caller's capture stream orders them) */
     if (!capturing && c->mesh_last_stream && c->mesh_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[6], 0));
+    MTRACE("mesh launch n %zu shard %zu chunk %zu nchunks %d lag %d grid %d", n, shard, chunk, nchunks, lag, l.grid);
     rc = inccl_k_mesh(&l, st);
     if (rc) return inccl_set_error(rc == INCCL_ERR_ARG ? INCCL_ERR_ARG : INCCL_ERR_HIP, "mesh kernel launch failed (%d)", rc);
     if (!capturing) {
