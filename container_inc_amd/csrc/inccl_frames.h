@@ -18,9 +18,14 @@ typedef struct InccSwitchState {
     uint32_t *arrival;   /* [slots]             nts.c:59 */
     int32_t *degree;     /* [slots]             nts.c:60 */
     uint32_t *reth;      /* [slots][fan_in][4]  nts.c:57 */
+    uint64_t *first;     /* [slots][fan_in]     batch-tagged index of the first copy in a batch:
+                          * (~gen << 32) | frame, atomicMin -> the earliest frame of the newest batch */
     uint32_t slots;      /* power of two */
     int fan_in;
+    uint32_t gen;        /* batch generation (host counter, advanced per ingress call) */
 } InccSwitchState;
+
+#define INCCL_FRAME_MIN_STRIDE 64   /* a row must hold the 62-B ACK frame (headers through the BTH) */
 
 typedef struct inccl_frame_template InccFrameTemplate;
 

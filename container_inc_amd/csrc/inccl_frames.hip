@@ -139,7 +139,13 @@ __device__ __forceinline__ int icrc_ip_total(uint32_t hdr_lane)
     return (int)(((h & 0xFFu) << 8) | ((h >> 8) & 0xFFu));
 }
 
-__device__ __forceinline__ bool icrc_len_ok(int ipt) { return ipt >= 28 && ipt <= kWin && 14 + ipt <= kFrameMax; }
+// an ICRC is computed only for an IP length the window holds and whose frame
+// lies inside its row: a header claiming more bytes than the row has reads as
+// malformed (ICRC 0), never as the next row's bytes
+__device__ __forceinline__ bool icrc_len_ok(int ipt, int64_t stride)
+{
+    return ipt >= 28 && ipt <= kWin && 14 + ipt <= kFrameMax && 14 + ipt <= stride;
+}
 
 // Persistent: each wave walks its frames with the next frame's words (5 dwords
 // a lane, coalesced) and the one after's header in flight while the current
@@ -159,7 +165,7 @@ __global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __res
     uint32_t* lds = reinterpret_cast<uint32_t*>(buf[w]);
     auto fetch = [&](int64_t fr, int ipt, uint32_t (&v)[kWords]) {
         const uint32_t* g = reinterpret_cast<const uint32_t*>(frames + fr * stride);
-        const int words = icrc_len_ok(ipt) ? (14 + ipt + 3) >> 2 : 0;
+        const int words = icrc_len_ok(ipt, stride) ? (14 + ipt + 3) >> 2 : 0;
 #pragma unroll
         for (int k = 0; k < kWords; ++k) {
             const int i = lane + k * kWave;
@@ -184,7 +190,7 @@ __global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __res
             fetch(fn, ipn, cur);
             hdrN = fn + step < count ? icrc_hdr_load(frames + (fn + step) * stride, lane) : 0u;
         }
-        const uint32_t crc = icrc_len_ok(ip) ? icrc_wave(buf[w], t, lane) : 0u;
+        const uint32_t crc = icrc_len_ok(ip, stride) ? icrc_wave(buf[w], t, lane) : 0u;
         if (lane == 0) out[f] = crc;
         __builtin_amdgcn_wave_barrier();
         f = fn;
@@ -204,15 +210,40 @@ __device__ __forceinline__ bool is_data_opcode(uint8_t op)
 }
 __device__ __forceinline__ bool is_write_first(uint8_t op) { return op == 0x06 || op == 0x0A; }   // nts.c:327-328
 
-// Ingress (nts.c:303-483, root branch): one wave per frame.
-__global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress(InccSwitchState s, const uint8_t* __restrict__ frames,
-                                                                   int64_t stride, int64_t count,
-                                                                   const int32_t* __restrict__ ports,
-                                                                   int32_t* __restrict__ action,
-                                                                   uint32_t* __restrict__ psn_out)
+// Ingress (nts.c:303-483, root branch) in three passes that reproduce the
+// reference's one-frame-at-a-time order: frame index within the batch = arrival
+// order.  What a serial switch decides for frame f depends on which copies of
+// its (psn, port) and of its PSN's other ports came BEFORE f, so:
+//   claim   (a lane per frame) parse + validate; per (slot, port) an atomicMin
+//           of a batch-tagged frame index finds the first copy in the batch
+//   apply   (a wave per frame) the first copy of a pair whose port bit was not
+//           set before the batch is the arrival that counts: it adds its payload
+//           (nts.c:359-363) and keeps its RETH (:442).  The PSN completes at the
+//           LAST of its ports' counted arrivals (the max over ports of the first
+//           index; ports already in before the batch count as earlier than
+//           every frame): that frame is COMPLETED (:365-372), the others
+//           ABSORBED.  Every other copy is a retransmit (:353): REPLAY if the
+//           slot completed before the batch or at an earlier frame of it
+//           (:354-356), else DROPPED.
+//   commit  (a lane per frame) the arrival bitmap: port bits of the counted
+//           arrivals, and the result bit (:366) of the completing ones.
+// The arrival bitmap is read (apply) and written (commit) in different
+// launches, so every frame sees the state from before the batch.
+constexpr int kActPending = 100;   // claim -> apply: a data frame still to classify
+constexpr int kClaimBlock = 256;
+
+__device__ __forceinline__ uint64_t first_key(uint32_t gen, int64_t f)
 {
-    const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    const int64_t f = (int64_t)blockIdx.x * kWavesPerBlock + w;
+    return ((uint64_t)(~gen) << 32) | (uint64_t)(uint32_t)f;
+}
+
+__global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s, const uint8_t* __restrict__ frames,
+                                                               int64_t stride, int64_t count,
+                                                               const int32_t* __restrict__ ports,
+                                                               int32_t* __restrict__ action,
+                                                               uint32_t* __restrict__ psn_out)
+{
+    const int64_t f = (int64_t)blockIdx.x * kClaimBlock + threadIdx.x;
     if (f >= count) return;
     const uint8_t* fr = frames + f * stride;
     const int port = ports[f];
@@ -225,46 +256,95 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress(InccSwitchSta
     else if (is_data_opcode(op) || is_write_first(op)) {
         const bool wf = is_write_first(op);
         const int data_len = udp_len - 12 - 8 - 4 - (wf ? 16 : 0);   // nts.c:349, :429
-        if (data_len != kLanes * 4) act = INCCL_SW_INVALID;     // nts.c:350 assert
+        // nts.c:350 asserts the length; the payload must also lie inside the row
+        if (data_len != kLanes * 4 || 54 + (wf ? 16 : 0) + kLanes * 4 > stride) act = INCCL_SW_INVALID;
         else {
             const uint32_t slot = psn & (s.slots - 1);
-            const uint32_t bit = 1u << port;
-            const uint32_t result_bit = 1u << s.fan_in;
-            uint32_t old = 0;
-            if (lane == 0) {
-                atomicAdd(&s.degree[slot], 1);                   // nts.c:351 / :431
-                old = atomicOr(&s.arrival[slot], bit);           // nts.c:359 / :441
-            }
-            old = (uint32_t)__shfl((int)old, 0, kWave);
-            if (old & bit) {
-                act = (old & result_bit) ? INCCL_SW_REPLAY : INCCL_SW_DROPPED;   // nts.c:353-357
-            } else {
-                const uint8_t* data = fr + 54 + (wf ? 16 : 0);
-                // the payload starts at byte 54 (70 with RETH): 2-byte aligned only
-                const uint16_t* d16 = reinterpret_cast<const uint16_t*>(data);
-                if (wf && lane < 4) {                            // reth_keeper, nts.c:442
-                    const uint16_t* r = reinterpret_cast<const uint16_t*>(fr + 54);
-                    s.reth[((size_t)slot * s.fan_in + port) * 4 + lane] =
-                        (uint32_t)r[2 * lane] | ((uint32_t)r[2 * lane + 1] << 16);
-                }
-                int32_t* agg = s.agg + (size_t)slot * kLanes;
-                // word i = j*64 + lane: each wave-instruction adds 256 contiguous
-                // bytes (the full-rate atomic shape, MI355X_MICROARCH.md atomics)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {                    // nts.c:361-363 / :443-445
-                    const int i = j * kWave + lane;
-                    const uint32_t raw = (uint32_t)d16[2 * i] | ((uint32_t)d16[2 * i + 1] << 16);
-                    atomicAdd(&agg[i], (int32_t)__builtin_bswap32(raw));
-                }
-                const uint32_t mask = 0xffffffffu >> (32 - s.fan_in);
-                act = (((old | bit) & mask) == mask) ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
-            }
+            atomicAdd(&s.degree[slot], 1);                       // nts.c:351 / :431
+            atomicMin(reinterpret_cast<unsigned long long*>(&s.first[(size_t)slot * s.fan_in + port]),
+                      (unsigned long long)first_key(s.gen, f));
+            act = kActPending;
         }
     }
-    if (lane == 0) {
-        action[f] = act;
-        psn_out[f] = psn;
+    action[f] = act;
+    psn_out[f] = psn;
+}
+
+__global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwitchState s,
+                                                                         const uint8_t* __restrict__ frames,
+                                                                         int64_t stride, int64_t count,
+                                                                         const int32_t* __restrict__ ports,
+                                                                         int32_t* __restrict__ action,
+                                                                         const uint32_t* __restrict__ psns)
+{
+    const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    const int64_t f = (int64_t)blockIdx.x * kWavesPerBlock + w;
+    if (f >= count || action[f] != kActPending) return;
+    const uint8_t* fr = frames + f * stride;
+    const int port = ports[f];
+    const uint32_t psn = psns[f];
+    const uint32_t slot = psn & (s.slots - 1);
+    const uint32_t bit = 1u << port, result_bit = 1u << s.fan_in;
+    const uint32_t pre = s.arrival[slot];                       // the slot before this batch
+    const uint32_t tag = ~s.gen;
+    // lane p < fan_in: when port p's counted arrival happens, as 1 + frame index;
+    // 0 = before the batch, ~0 = not by the end of the batch
+    uint32_t at = 0;
+    uint32_t mine = 0xFFFFFFFFu;                                // frame index of my pair's first copy
+    if (lane < s.fan_in) {
+        const uint64_t e = s.first[(size_t)slot * s.fan_in + lane];
+        const bool in_batch = (uint32_t)(e >> 32) == tag;
+        at = (pre & (1u << lane)) ? 0u : (in_batch ? (uint32_t)e + 1u : 0xFFFFFFFFu);
+        mine = in_batch ? (uint32_t)e : 0xFFFFFFFFu;
     }
+    mine = (uint32_t)__shfl((int)mine, port, kWave);
+    uint32_t done_at = at;                                      // max over ports: the completing arrival
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) {
+        const uint32_t v = (uint32_t)__shfl_xor((int)done_at, o, kWave);
+        done_at = v > done_at ? v : done_at;
+    }
+    done_at = (uint32_t)__shfl((int)done_at, 0, kWave);
+    int act;
+    if (!(pre & bit) && mine == (uint32_t)f) {                  // the counted arrival: nts.c:359-363
+        const bool wf = is_write_first(fr[42]);
+        const uint8_t* data = fr + 54 + (wf ? 16 : 0);
+        // the payload starts at byte 54 (70 with RETH): 2-byte aligned only
+        const uint16_t* d16 = reinterpret_cast<const uint16_t*>(data);
+        if (wf && lane < 4) {                                    // reth_keeper, nts.c:442
+            const uint16_t* r = reinterpret_cast<const uint16_t*>(fr + 54);
+            s.reth[((size_t)slot * s.fan_in + port) * 4 + lane] =
+                (uint32_t)r[2 * lane] | ((uint32_t)r[2 * lane + 1] << 16);
+        }
+        int32_t* agg = s.agg + (size_t)slot * kLanes;
+        // word i = j*64 + lane: each wave-instruction adds 256 contiguous
+        // bytes (the full-rate atomic shape, MI355X_MICROARCH.md atomics)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {                            // nts.c:361-363 / :443-445
+            const int i = j * kWave + lane;
+            const uint32_t raw = (uint32_t)d16[2 * i] | ((uint32_t)d16[2 * i + 1] << 16);
+            atomicAdd(&agg[i], (int32_t)__builtin_bswap32(raw));
+        }
+        act = (done_at == (uint32_t)f + 1u) ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
+    } else {                                                     // retransmit: nts.c:353-357
+        const bool done_before = (pre & result_bit) != 0;
+        const bool done_earlier = done_at != 0u && done_at != 0xFFFFFFFFu && done_at - 1u < (uint32_t)f;
+        act = (done_before || done_earlier) ? INCCL_SW_REPLAY : INCCL_SW_DROPPED;
+    }
+    if (lane == 0) action[f] = act;
+}
+
+__global__ __launch_bounds__(kClaimBlock) void k_ingress_commit(InccSwitchState s, int64_t count,
+                                                                const int32_t* __restrict__ ports,
+                                                                const int32_t* __restrict__ action,
+                                                                const uint32_t* __restrict__ psns)
+{
+    const int64_t f = (int64_t)blockIdx.x * kClaimBlock + threadIdx.x;
+    if (f >= count) return;
+    const int act = action[f];
+    if (act != INCCL_SW_ABSORBED && act != INCCL_SW_COMPLETED) return;
+    const uint32_t slot = psns[f] & (s.slots - 1);
+    atomicOr(&s.arrival[slot], (1u << ports[f]) | (act == INCCL_SW_COMPLETED ? 1u << s.fan_in : 0u));   // nts.c:359, :366
 }
 
 __device__ __forceinline__ void put16(uint8_t* p, uint32_t v)
@@ -433,8 +513,6 @@ __device__ void egress_emit(const InccSwitchState& s, const EgressIn& e, const u
         }
         __builtin_amdgcn_wave_barrier();
     }
-    // the result is known from now on: later retransmits replay (nts.c:366)
-    if (all && lane == 0) atomicOr(&s.arrival[e.slot], 1u << fan);
 }
 
 // Egress (nts.c:365-372 / :447-453 broadcast, :353-356 / :435-438 replay;
@@ -595,8 +673,8 @@ int inccl_k_frames_init(void) { return ensure_tables(); }
 int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* out, void* stream)
 {
     if ((frames == nullptr || out == nullptr) && count) return INCCL_ERR_ARG;
-    if ((stride & 3) || ((uintptr_t)frames & 3)) return INCCL_ERR_ARG;
     if (count == 0) return 0;
+    if ((stride & 3) || stride < INCCL_FRAME_MIN_STRIDE || ((uintptr_t)frames & 3)) return INCCL_ERR_ARG;
     int rc = ensure_tables();
     if (rc) return rc;
     const int64_t blocks = ((int64_t)count + kIcrcWaves - 1) / kIcrcWaves;
@@ -611,9 +689,16 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
                            const int32_t* ports, int32_t* action, uint32_t* psn_out, void* stream)
 {
     if (count == 0) return 0;
-    if (!s || !frames || !ports || !action || !psn_out || (stride & 3) || ((uintptr_t)frames & 3)) return INCCL_ERR_ARG;
-    hipLaunchKernelGGL(k_ingress, dim3(grid_for((int64_t)count)), dim3(kWave * kWavesPerBlock), 0,
-                       (hipStream_t)stream, *s, frames, (int64_t)stride, (int64_t)count, ports, action, psn_out);
+    if (!s || !frames || !ports || !action || !psn_out || (stride & 3) || stride < INCCL_FRAME_MIN_STRIDE ||
+        ((uintptr_t)frames & 3) || count >= 0xFFFFFFFFull)
+        return INCCL_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 lanes((unsigned)(((int64_t)count + kClaimBlock - 1) / kClaimBlock));
+    hipLaunchKernelGGL(k_ingress_claim, lanes, dim3(kClaimBlock), 0, st, *s, frames, (int64_t)stride, (int64_t)count,
+                       ports, action, psn_out);
+    hipLaunchKernelGGL(k_ingress_apply, dim3(grid_for((int64_t)count)), dim3(kWave * kWavesPerBlock), 0, st, *s,
+                       frames, (int64_t)stride, (int64_t)count, ports, action, psn_out);
+    hipLaunchKernelGGL(k_ingress_commit, lanes, dim3(kClaimBlock), 0, st, *s, (int64_t)count, ports, action, psn_out);
     return (int)hipGetLastError();
 }
 

@@ -19,6 +19,7 @@ struct inccl_switch {
     InccSwitchState st;
     void *mem;
     size_t bytes;
+    size_t first_off;   /* the first-arrival table: all-ones = "no copy seen" */
     int device;
 };
 
@@ -45,9 +46,12 @@ struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device)
     const size_t arr = (size_t)slots * sizeof(uint32_t);
     const size_t deg = (size_t)slots * sizeof(int32_t);
     const size_t reth = (size_t)slots * (size_t)fan_in * 16;
-    sw->bytes = agg + arr + deg + reth;
+    const size_t first = (size_t)slots * (size_t)fan_in * 8;
+    sw->bytes = agg + arr + deg + reth + first;
+    sw->first_off = agg + arr + deg + reth;
     hipError_t e = hipMalloc(&sw->mem, sw->bytes);
-    if (e == hipSuccess) e = hipMemset(sw->mem, 0, sw->bytes);
+    if (e == hipSuccess) e = hipMemset(sw->mem, 0, sw->first_off);
+    if (e == hipSuccess) e = hipMemset((char *)sw->mem + sw->first_off, 0xFF, first);   /* no batch yet */
     if (e != hipSuccess) {
         inccl_hip_check(e, "switch: hipMalloc");
         if (sw->mem) hipFree(sw->mem);
@@ -59,6 +63,8 @@ struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device)
     sw->st.arrival = (uint32_t *)(p + agg);
     sw->st.degree = (int32_t *)(p + agg + arr);
     sw->st.reth = (uint32_t *)(p + agg + arr + deg);
+    sw->st.first = (uint64_t *)(p + sw->first_off);
+    sw->st.gen = 0;
     sw->st.slots = slots;
     sw->st.fan_in = fan_in;
     hipGetDevice(&sw->device);
@@ -83,7 +89,9 @@ int inccl_switch_destroy(struct inccl_switch *sw)
 int inccl_switch_reset(struct inccl_switch *sw, void *stream)
 {
     if (!sw) return inccl_set_error(INCCL_ERR_ARG, "switch is NULL");
-    INCCL_HIP(hipMemsetAsync(sw->mem, 0, sw->bytes, (hipStream_t)stream));
+    INCCL_HIP(hipMemsetAsync(sw->mem, 0, sw->first_off, (hipStream_t)stream));
+    INCCL_HIP(hipMemsetAsync((char *)sw->mem + sw->first_off, 0xFF, sw->bytes - sw->first_off, (hipStream_t)stream));
+    sw->st.gen = 0;
     return 0;
 }
 
@@ -97,6 +105,11 @@ int inccl_switch_ingress(struct inccl_switch *sw, const uint8_t *frames_dev, siz
                          const int32_t *ports_dev, int32_t *action_dev, uint32_t *psn_dev, void *stream)
 {
     if (!sw) return inccl_set_error(INCCL_ERR_ARG, "switch is NULL");
+    if (count && stride < INCCL_FRAME_MIN_STRIDE)
+        return inccl_set_error(INCCL_ERR_ARG, "inccl_switch_ingress: stride %zu below %d", stride, INCCL_FRAME_MIN_STRIDE);
+    /* a new batch: its first-arrival keys outrank every earlier batch's (switch
+     * state is per stream-ordered call sequence, like the reference's globals) */
+    if (count) sw->st.gen++;
     return kerr2(inccl_k_switch_ingress(&sw->st, frames_dev, stride, count, ports_dev, action_dev, psn_dev, stream),
                  "inccl_switch_ingress");
 }
@@ -107,7 +120,8 @@ int inccl_switch_egress(struct inccl_switch *sw, const uint8_t *frames_dev, size
                         int32_t *out_len_dev, void *stream)
 {
     if (!sw) return inccl_set_error(INCCL_ERR_ARG, "switch is NULL");
-    (void)stride;
+    if (count && stride < INCCL_FRAME_MIN_STRIDE)
+        return inccl_set_error(INCCL_ERR_ARG, "inccl_switch_egress: stride %zu below %d", stride, INCCL_FRAME_MIN_STRIDE);
     return kerr2(inccl_k_switch_egress(&sw->st, frames_dev, stride, count, ports_dev, action_dev, psn_dev,
                                        templates_dev, out_dev, out_stride, out_len_dev, stream),
                  "inccl_switch_egress");
@@ -115,5 +129,7 @@ int inccl_switch_egress(struct inccl_switch *sw, const uint8_t *frames_dev, size
 
 int inccl_icrc_frames(const uint8_t *frames_dev, size_t stride, size_t count, uint32_t *icrc_dev, void *stream)
 {
+    if (count && stride < INCCL_FRAME_MIN_STRIDE)
+        return inccl_set_error(INCCL_ERR_ARG, "inccl_icrc_frames: stride %zu below %d", stride, INCCL_FRAME_MIN_STRIDE);
     return kerr2(inccl_k_icrc(frames_dev, stride, count, icrc_dev, stream), "inccl_icrc_frames");
 }

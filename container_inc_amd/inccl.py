@@ -396,6 +396,7 @@ def _frames_arg(frames, name="frames"):
         raise ValueError(f"{name}: expected [count, stride] uint8")
     if frames.shape[1] % 4:
         raise ValueError(f"{name}: stride must be a multiple of 4")
+    # strides below the 62-B ACK frame reach the library, which refuses them
     return _dev_ptr(frames, torch.uint8, name), frames.shape[0], frames.shape[1]
 
 
@@ -431,13 +432,24 @@ class GpuSwitch:
                                           _stream_handle(stream)), "inccl_switch_ingress")
         return action, psn
 
-    def egress(self, frames, ports, action, psn, templates, out_stride: int = 1152, stream=None):
+    def egress(self, frames, ports, action, psn, templates, out_stride: int = 1152, stream=None, out=None,
+               out_len=None):
+        """Row i * fan_in + c is child c's frame for input frame i; out_len says
+        which rows were written (bytes, or 0).  Unwritten rows keep whatever the
+        buffer held: `out` / `out_len` may be passed in and reused."""
         torch = _torch()
         ptr, count, stride = _frames_arg(frames)
         if templates.dtype != torch.uint8 or templates.numel() != 28 * self.fan_in:
             raise ValueError("templates: fan_in x 28-byte inccl_frame_template records (uint8)")
-        out = torch.zeros((count * self.fan_in, out_stride), dtype=torch.uint8, device=frames.device)
-        out_len = torch.empty(count * self.fan_in, dtype=torch.int32, device=frames.device)
+        if out is None:
+            out = torch.empty((count * self.fan_in, out_stride), dtype=torch.uint8, device=frames.device)
+        elif out.dtype != torch.uint8 or out.dim() != 2 or out.shape[0] < count * self.fan_in:
+            raise ValueError("out: uint8 [count * fan_in, out_stride]")
+        out_stride = out.shape[1]
+        if out_len is None:
+            out_len = torch.empty(count * self.fan_in, dtype=torch.int32, device=frames.device)
+        _dev_ptr(out, torch.uint8, "out")
+        _dev_ptr(out_len, torch.int32, "out_len", count * self.fan_in)
         check(load().inccl_switch_egress(self.handle, ptr, stride, count, _dev_ptr(ports, torch.int32, "ports", count),
                                          _dev_ptr(action, torch.int32, "action", count),
                                          _dev_ptr(psn, torch.int32, "psn", count),

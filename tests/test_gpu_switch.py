@@ -98,6 +98,7 @@ def test_switch_batches(gpu, orc, fan_in):
     tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
     payload, reth, opcode = {}, {}, {}
     completed = set()
+    seen = set()
     for b in range(batches):
         psns = list(range(b * per_batch, (b + 1) * per_batch))
         frames, ports, keys = [], [], []
@@ -126,23 +127,21 @@ def test_switch_batches(gpu, orc, fan_in):
         torch.cuda.synchronize()
         action, psn_out = action.cpu().numpy(), psn_out.cpu().numpy()
         out, out_len = out.cpu().numpy(), out_len.cpu().numpy()
-        # which copy of a (psn, port) pair arrives first inside a batch is not
-        # defined: exactly one copy is added, the others are DROPPED; copies of a
-        # pair whose slot completed in an EARLIER batch are REPLAYed (nts.c:353-357)
-        groups = {}
+        # the batch in frame order is the reference's serial order (nts.c:353-372):
+        # the first copy of a pair counts, the PSN completes at its last port's
+        # counted copy, later copies REPLAY once it has completed, else DROP
+        done_psn = set(completed)
         for i, (p, port) in enumerate(order):
             assert psn_out[i] == p
-            groups.setdefault((p, port), []).append(int(action[i]))
-        n_completed = {}
-        for (p, port), acts in groups.items():
-            if p in completed:
-                assert acts == [inccl.SW_REPLAY] * len(acts), (p, port, acts)
-                continue
-            firsts = [a for a in acts if a in (inccl.SW_ABSORBED, inccl.SW_COMPLETED)]
-            assert len(firsts) == 1 and acts.count(inccl.SW_DROPPED) == len(acts) - 1, (p, port, acts)
-            if firsts[0] == inccl.SW_COMPLETED:
-                n_completed[p] = n_completed.get(p, 0) + 1
-        assert all(n_completed.get(p, 0) == 1 for p in psns), n_completed
+            if (p, port) in seen:
+                want = inccl.SW_REPLAY if p in done_psn else inccl.SW_DROPPED
+            else:
+                seen.add((p, port))
+                full = all((p, c) in seen for c in range(fan_in))
+                want = inccl.SW_COMPLETED if full else inccl.SW_ABSORBED
+                if full:
+                    done_psn.add(p)
+            assert action[i] == want, (i, p, port, int(action[i]), want)
         for i, (p, port) in enumerate(order):
             agg = orc.sum_q32([payload[(p, c)] for c in range(fan_in)])
             for c in range(fan_in):
@@ -246,4 +245,97 @@ def test_switch_large_batch_all_frames(gpu, orc, fan_in, P):
         want = _expected_frame(orc, tmpl, c, agg[p].view(np.int32), p, int(op_of[f]),
                                reth[src_row[(p, c)]].tobytes())
         assert bytes(oc[j, : len(want)]) == want, (j, f, c)
+    sw.destroy()
+
+
+@pytest.mark.parametrize("fan_in,seed", [(2, 1), (2, 2), (3, 3)])
+def test_switch_serial_order_vs_oracle_reference_ring(gpu, orc, fan_in, seed):
+    """The reference's own ring (16 slots, window 8 with slot psn+8 cleared at
+    completion, nts.c:21-25, :367) fed one frame sequence: the oracle processes
+    it serially (orc_switch_ingress), the GPU in batches of at most eight
+    consecutive PSNs.  Every copy of a frame carries a DIFFERENT payload, so the
+    actions, which copy is counted, and every emitted frame must all agree.
+    Retransmits land before, at and after their PSN's completion."""
+    import torch
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(700 + seed)
+    assert orc.SW_SLOTS == 16
+    sw = inccl.GpuSwitch(fan_in, 16)
+    ref = orc.Switch(fan_in)
+    tmpl = _templates(fan_in)
+    tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
+    orc_act = {orc.SW_ABSORBED: inccl.SW_ABSORBED, orc.SW_BROADCAST: inccl.SW_COMPLETED,
+               orc.SW_REPLAY: inccl.SW_REPLAY, orc.SW_DROPPED: inccl.SW_DROPPED}
+    counted_reth = {}
+    n_checked = {"COMPLETED": 0, "REPLAY": 0, "DROPPED": 0}
+    for b in range(12):
+        new = list(range(4 * b, 4 * b + 4))
+        recent = list(range(max(0, 4 * b - 4), 4 * b + 4))   # at most eight consecutive PSNs
+        seq = [(p, c) for p in new for c in range(fan_in)]
+        seq = [seq[i] for i in rng.permutation(len(seq))]
+        # retransmits spliced in at random positions: before and after completion
+        for _ in range(3 * fan_in):
+            p, c = int(rng.choice(recent)), int(rng.integers(0, fan_in))
+            seq.insert(int(rng.integers(0, len(seq) + 1)), (p, c))
+        frames, ports, rcs, eg = [], [], [], []
+        for (p, c) in seq:
+            op = [0x06, 0x07, 0x07, 0x08][p % 4]
+            pay = rng.integers(INT32_MIN, INT32_MAX, 256, dtype=np.int64, endpoint=True).astype(np.int32)
+            rb = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            wf = op == 0x06
+            frames.append(orc.build_data_frame(pay, psn=p, opcode=op, qp=0x11, with_reth=wf, reth=rb if wf else None,
+                                               src_ip=0x0A000001 + c))
+            ports.append(c)
+            rc, e = ref.ingress(c, p, pay.astype(">i4").view(np.uint32))   # serial, in frame order
+            rcs.append(orc_act[rc])
+            eg.append(e.copy())
+            if rc in (orc.SW_ABSORBED, orc.SW_BROADCAST):
+                counted_reth[(p, c)] = rb
+        fr = _rows(frames, gpu)
+        pt = torch.tensor(ports, dtype=torch.int32, device=gpu)
+        action, psn_out = sw.ingress(fr, pt)
+        out, out_len = sw.egress(fr, pt, action, psn_out, tmpl_dev)
+        torch.cuda.synchronize()
+        act = action.cpu().numpy().tolist()
+        assert act == rcs, (b, seq, act, rcs)
+        out, out_len = out.cpu().numpy(), out_len.cpu().numpy()
+        for i, (p, port) in enumerate(seq):
+            op = [0x06, 0x07, 0x07, 0x08][p % 4]
+            agg = eg[i].byteswap().view(np.int32)   # the oracle's egress words (util.c:403-405) in host order
+            for c in range(fan_in):
+                row = i * fan_in + c
+                emit = act[i] == inccl.SW_COMPLETED or (act[i] == inccl.SW_REPLAY and c == port)
+                if emit:
+                    want = _expected_frame(orc, tmpl, c, agg, p, op, counted_reth.get((p, c), bytes(16)))
+                    assert out_len[row] == len(want) and bytes(out[row, : len(want)]) == want, (b, i, c)
+                else:
+                    assert out_len[row] == 0, (b, i, c)
+            name = {inccl.SW_COMPLETED: "COMPLETED", inccl.SW_REPLAY: "REPLAY", inccl.SW_DROPPED: "DROPPED"}
+            if act[i] in name:
+                n_checked[name[act[i]]] += 1
+    assert all(v > 0 for v in n_checked.values()), n_checked   # every serial outcome occurred
+    sw.destroy()
+
+
+def test_switch_short_stride_rejected(gpu, orc):
+    """A frame's header may claim more bytes than its row holds: the row stride
+    bounds every read (a payload past the row is INVALID; an ICRC whose IP
+    length runs past the row is not computed), and strides below the 62-B ACK
+    frame are refused on the host."""
+    import torch
+    from container_inc_amd import inccl
+    sw = inccl.GpuSwitch(2, 16)
+    good = orc.build_data_frame(np.ones(256, np.int32), psn=3, opcode=0x07)   # 1082 B
+    rows = np.zeros((2, 1024), np.uint8)                                      # rows shorter than the frame
+    rows[0] = np.frombuffer(good[:1024], np.uint8)
+    rows[1] = np.frombuffer(good[:1024], np.uint8)
+    fr = torch.from_numpy(rows).to(gpu)
+    action, _ = sw.ingress(fr, torch.tensor([0, 1], dtype=torch.int32, device=gpu))
+    assert action.cpu().tolist() == [inccl.SW_INVALID, inccl.SW_INVALID]
+    crc = inccl.icrc_frames(fr).cpu().numpy()
+    assert (crc == 0).all()
+    with pytest.raises(inccl.IncclError):
+        inccl.icrc_frames(torch.zeros((4, 32), dtype=torch.uint8, device=gpu))
+    with pytest.raises(inccl.IncclError):
+        sw.ingress(torch.zeros((4, 32), dtype=torch.uint8, device=gpu), torch.zeros(4, dtype=torch.int32, device=gpu))
     sw.destroy()
