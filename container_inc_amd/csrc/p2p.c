@@ -33,23 +33,30 @@ typedef struct {
     hipIpcMemHandle_t part, res;
 } p2p_handles;
 
-void inccl_p2p_release(struct inccl_communicator *c)
+/* $INCCL_TRACE: every (re)growth logs, per rank, the FNV-1a hash of each
+ * exported handle and the base address each peer's buffer mapped to, so that
+ * a mapping that resolves to an earlier export (same base as before while the
+ * handle changed) is visible in the log */
+static uint64_t handle_hash(const hipIpcMemHandle_t *h)
 {
-    const int W = c->group->world_size, me = c->group->rank;
-    if (c->p2p_cap == 0 && !c->p2p_part) return;
-    hipDeviceSynchronize();
-    for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS; ++j) {
-        if (j == me) continue;
-        if (c->p2p_peer_part[j]) hipIpcCloseMemHandle(c->p2p_peer_part[j]);
-        if (c->p2p_peer_res[j]) hipIpcCloseMemHandle(c->p2p_peer_res[j]);
-        c->p2p_peer_part[j] = NULL;
-        c->p2p_peer_res[j] = NULL;
-    }
-    if (c->p2p_part) hipFree(c->p2p_part);
-    if (c->p2p_res) hipFree(c->p2p_res);
-    c->p2p_part = NULL;
-    c->p2p_res = NULL;
-    c->p2p_cap = 0;
+    const unsigned char *b = (const unsigned char *)h;
+    uint64_t x = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(*h); ++i) x = (x ^ b[i]) * 1099511628211ull;
+    return x;
+}
+
+static void p2p_trace(const struct inccl_communicator *c, const char *what, const p2p_handles *all, int W)
+{
+    if (!getenv("INCCL_TRACE")) return;
+    char line[2048];
+    int k = snprintf(line, sizeof(line), "[inccl p2p rank %d] %s cap %zu own part %p res %p", c->group->rank, what,
+                     c->p2p_cap, (void *)c->p2p_part, (void *)c->p2p_res);
+    for (int j = 0; j < W && k > 0 && (size_t)k < sizeof(line); ++j)
+        k += snprintf(line + k, sizeof(line) - (size_t)k, " | peer %d handle %016llx/%016llx -> part %p res %p", j,
+                      all ? (unsigned long long)handle_hash(&all[j].part) : 0ull,
+                      all ? (unsigned long long)handle_hash(&all[j].res) : 0ull, (void *)c->p2p_peer_part[j],
+                      (void *)c->p2p_peer_res[j]);
+    fprintf(stderr, "%s\n", line);   /* one write per line: ranks share the log */
 }
 
 /* collective: every rank calls it with the same `elems` */
@@ -74,6 +81,16 @@ static int p2p_ensure(struct inccl_communicator *c, size_t elems)
      * identity (a dmabuf fd number) while a peer's runtime may still resolve it
      * to the old import: a regrowth then, intermittently, left one rank reading
      * a peer's old buffer on every later call. */
+    /* $INCCL_P2P_FREE_FIRST=1 restores the first version's order (free the old
+     * buffers, then allocate and exchange the new ones) -- for the regrowth
+     * regression test only */
+    const char *ff = getenv("INCCL_P2P_FREE_FIRST");
+    if (ff && atoi(ff) != 0 && c->p2p_part) {
+        p2p_trace(c, "free-first: releasing", NULL, W);
+        rc = inccl_boot_barrier(g);
+        if (rc) return rc;
+        inccl_p2p_release(c);
+    }
     struct inccl_communicator old = *c;
     c->p2p_part = NULL;
     c->p2p_res = NULL;
@@ -117,6 +134,7 @@ static int p2p_ensure(struct inccl_communicator *c, size_t elems)
         c->p2p_peer_part[j] = (int32_t *)pp;
         c->p2p_peer_res[j] = (float *)pr;
     }
+    p2p_trace(c, "mapped", all, W);
     free(all);
     /* every peer has mapped the new buffers: the old ones can go */
     int rc_b = inccl_boot_barrier(g);
