@@ -192,10 +192,12 @@ int inccl_allreduce_f32_host(struct inccl_communicator *comm, const float *src_h
  * broadcast / replay) and util.c:331-442 (egress frame build, payload htonl,
  * RoCE ICRC), batched: a batch of ingress frames -> one ingress launch -> one
  * egress launch.  Frames live in device memory at a fixed `stride` (multiple of
- * 4 B).  Within one batch the arrival order is not defined: first arrivals of a
- * (psn, port) pair are added once, later copies are DROPPED (slot incomplete
- * before the batch) or REPLAYed (slot completed in an earlier batch).  A batch
- * must span fewer than slots/2 PSNs (the reference: window 8 of 16 slots). */
+ * 4 B, at least 64; every read stays inside a frame's row).  Frame order within
+ * a batch is the arrival order: the actions are exactly those of the reference
+ * processing the batch's frames one at a time (the first copy of a (psn, port)
+ * pair is added; a later copy is REPLAYed if the PSN completed before it, else
+ * DROPPED).  A batch must not hold two PSNs that are slots/2 or more apart (the
+ * reference: window 8 of 16 slots), so that no two share a slot or a recycle. */
 #define INCCL_SW_IGNORED 0    /* opcode the switch does not handle             */
 #define INCCL_SW_ABSORBED 1   /* first arrival, slot not complete (nts.c:359-363) */
 #define INCCL_SW_COMPLETED 2  /* first arrival completing the slot: broadcast (nts.c:365-372) */
