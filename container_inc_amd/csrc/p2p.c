@@ -59,6 +59,25 @@ static void p2p_trace(const struct inccl_communicator *c, const char *what, cons
     fprintf(stderr, "%s\n", line);   /* one write per line: ranks share the log */
 }
 
+void inccl_p2p_release(struct inccl_communicator *c)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    if (c->p2p_cap == 0 && !c->p2p_part) return;
+    hipDeviceSynchronize();
+    for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS; ++j) {
+        if (j == me) continue;
+        if (c->p2p_peer_part[j]) hipIpcCloseMemHandle(c->p2p_peer_part[j]);
+        if (c->p2p_peer_res[j]) hipIpcCloseMemHandle(c->p2p_peer_res[j]);
+        c->p2p_peer_part[j] = NULL;
+        c->p2p_peer_res[j] = NULL;
+    }
+    if (c->p2p_part) hipFree(c->p2p_part);
+    if (c->p2p_res) hipFree(c->p2p_res);
+    c->p2p_part = NULL;
+    c->p2p_res = NULL;
+    c->p2p_cap = 0;
+}
+
 /* collective: every rank calls it with the same `elems` */
 static int p2p_ensure(struct inccl_communicator *c, size_t elems)
 {

@@ -47,6 +47,15 @@ def test_library_exports_every_declared_symbol(lib):
         assert hasattr(lib, name)
 
 
+def test_library_has_no_unresolved_internal_symbols(lib):
+    """Every inccl_* function the library calls is defined in it (an undefined
+    one would only fail when the .so is loaded on the GPU box)."""
+    import container_inc_amd as cia
+    out = subprocess.check_output(["nm", "-D", "--undefined-only", cia.LIB_PATH], text=True)
+    undef = [ln.split()[-1] for ln in out.splitlines() if "inccl_" in ln]
+    assert not undef, undef
+
+
 def test_python_binding_covers_abi():
     from container_inc_amd._lib import SIGNATURES
     assert set(SIGNATURES) == declared_functions()
