@@ -693,10 +693,10 @@ def main():
         res["sweep"] = size_sweep(comm, dev, R, k, rank, world)
         comm.set_engine(chosen[0])
     if world == 1 and not a.no_extras:
+        res["host_e2e"] = host_e2e(comm, k)
         res["sizes"] = n1_sizes(dev, R, k)
         res["roofline_cold"] = cold_run(dev, R, k, n)
         res["numerics_vs_exact"] = numerics_vs_exact(dev, n)
-        res["host_e2e"] = host_e2e(comm, k)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(n, R, k, a.cpu_seconds)
         res["cpu_baseline_allcores"] = cpu_baseline_allcores(n, R, k, min(a.cpu_seconds, 5.0))

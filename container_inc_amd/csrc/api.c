@@ -313,8 +313,21 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     }
     INCCL_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     INCCL_HIP(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
-    INCCL_HIP(hipStreamCreateWithFlags(&c->copy_streams[0], hipStreamNonBlocking));
-    INCCL_HIP(hipStreamCreateWithFlags(&c->copy_streams[1], hipStreamNonBlocking));
+    /* The host paths' H2D and D2H streams are high-priority streams: those come
+     * from their own hardware-queue pool.  Created as normal streams after the
+     * process had already launched work (e.g. torch tensors made first), the
+     * H2D and D2H copies of config 3 ran one after the other (28 GB/s instead
+     * of 44-46 GB/s both ways at once; tools/host_pipe_probe.py).
+     * $INCCL_COPY_STREAMS=default keeps normal priority. */
+    const char *cse = getenv("INCCL_COPY_STREAMS");
+    int prio_lo = 0, prio_hi = 0;
+    INCCL_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    for (int i = 0; i < 2; ++i) {
+        if (cse && strcmp(cse, "default") == 0)
+            INCCL_HIP(hipStreamCreateWithFlags(&c->copy_streams[i], hipStreamNonBlocking));
+        else
+            INCCL_HIP(hipStreamCreateWithPriority(&c->copy_streams[i], hipStreamNonBlocking, prio_hi));
+    }
     for (int i = 0; i < 9; ++i) INCCL_HIP(hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming));
     INCCL_HIP(hipMalloc((void **)&c->d_words, 256));
     INCCL_HIP(hipMemset(c->d_words, 0, 256));
