@@ -26,10 +26,10 @@
 #define INCCL_ENGINE_AR 5
 #define INCCL_MAX_HOST_REGIONS 16
 #define INCCL_MESH_REGIONS 4
-/* Largest single allocation exported over HIP IPC.  hipIpcOpenMemHandle of a
- * 2.5 GiB allocation never returned under the HIP runtime torch bundles (ROCm
- * 7.0; measured: tools/mesh_size_probe.py, DESIGN.md "IPC buffer lifecycle"),
- * so every IPC buffer is split or refused below 2 GiB. */
+/* Largest single allocation exported over HIP IPC.  Importing a peer's 2.5 GiB
+ * allocation never returned in processes running torch's bundled HIP runtime
+ * (ROCm 7.0; DESIGN.md "2 GiB per IPC export"), so every IPC buffer is split
+ * or refused below 2 GiB. */
 #define INCCL_IPC_MAX_BYTES (((size_t)2 << 30) - ((size_t)2 << 20))
 
 struct inccl_local_hub;
