@@ -314,3 +314,59 @@ def test_reference_api_multiprocess(gpu, world, engine):
         assert err is None, f"rank {r}: {err}"
         assert ok.pop("engine") == "p2p", ok
         assert all(ok.values()), f"rank {r}: {ok}"
+
+
+def _host_path_main(rank, world, port, q, engine):
+    """BASELINE config 3 with more than one rank: every rank's fp32 gradient in
+    pinned host memory, buckets through the H2D / allreduce / D2H pipeline,
+    where each bucket's allreduce is a multi-process exchange."""
+    try:
+        os.environ["INCCL_ENGINE"] = engine
+        os.environ["INCCL_DEVICE"] = "0"
+        os.environ["INCCL_BOOT_TIMEOUT"] = "120"
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        from container_inc_amd import inccl
+        from oracle import oracle as O
+        grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port)
+        comm = inccl.inccl_communicator_create(grp, 0)
+        res = {}
+        for n, bucket in (((64 << 20) // 4 + 333, 16 << 20), (1_000_003, 1 << 20)):
+            xs = [np.random.default_rng(40 + r).standard_normal(n).astype(np.float32) for r in range(world)]
+            want = O.reduce_f32(xs, 24)
+            x = torch.from_numpy(xs[rank]).pin_memory()
+            y = torch.full((n,), float("nan")).pin_memory()
+            for rep in range(2):
+                comm.allreduce_f32_host(x, y, scale_exp=24, bucket_bytes=bucket)
+                res[f"n={n} rep={rep}"] = bool(np.array_equal(y.numpy().view(np.uint32), want.view(np.uint32)))
+                y.fill_(float("nan"))
+        comm.destroy()
+        grp.destroy()
+        q.put((rank, res, None))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "mesh")])
+def test_host_path_multiprocess(gpu, world, engine):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_host_path_main, args=(r, world, port, q, engine)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, ok, err = q.get(timeout=240)
+            res[r] = (ok, err)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        ok, err = res[r]
+        assert err is None, f"rank {r}: {err}"
+        assert all(ok.values()), f"rank {r}: {ok}"
