@@ -203,6 +203,35 @@ def agree(values, world: int):
     return v.tolist()
 
 
+def graph_replay_us(comm, xs, out, k: int, st, world: int, want, per: int = 20, reps: int = 10):
+    """Latency floor of a small bucket: `per` calls captured in one hipGraph
+    (torch.cuda.CUDAGraph around the C-ABI call), replayed `reps` times; µs per
+    call, max over ranks, or None if any rank could not capture.  The replayed
+    output must still equal the reference engine's."""
+    import torch
+    g = torch.cuda.CUDAGraph()
+    ok = 1
+    try:
+        with torch.cuda.graph(g, stream=st):
+            for _ in range(per):
+                comm.allreduce_f32(xs, out=out, scale_exp=k, stream=st.cuda_stream)
+    except Exception:  # noqa: BLE001 -- an engine with host synchronisation cannot be captured
+        ok = 0
+    if agree([0.0 if ok else 1.0], world)[0] != 0.0:   # every rank replays, or none does
+        return None, None
+    g.replay()
+    torch.cuda.synchronize()
+    agree([0.0], world)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    dt = agree([(time.perf_counter() - t0) / (reps * per)], world)[0]
+    same = agree([0.0 if want is None or torch.equal(out, want) else 1.0], world)[0] == 0.0
+    del g
+    return dt, same
+
+
 def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
     """BASELINE config 5 at N > 1 (and north_star's 1024 MiB point): per bucket
     size and engine, host wall time per call over back-to-back calls (max over
@@ -223,7 +252,12 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
         torch.cuda.synchronize()   # inputs made on torch's stream; the calls run on st
         refs = None
         iters = 50 if b <= (1 << 20) else (10 if b <= (256 << 20) else 4)
-        engines = ("rccl", "ar", "ll", "p2p") if b <= (1 << 20) else ("rccl", "ar", "a2a", "p2p", "mesh", "meshw")
+        # the reference engine is the first that passes on every rank: RCCL, or
+        # else the host-synchronised p2p exchange, before the in-kernel ll protocol
+        engines = ("rccl", "ar", "p2p", "ll") if b <= (1 << 20) else ("rccl", "ar", "a2a", "p2p", "mesh", "meshw")
+        only = os.environ.get("INCCL_BENCH_SWEEP_ENGINES")   # debugging aid: a subset, in this order
+        if only:
+            engines = tuple(e for e in only.split(",") if e in engines)
         for eng in engines:
             ok, dt, same, got = 1, float("inf"), False, None
             try:
@@ -251,6 +285,10 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
                    "value_GBps": round(world * R * b / v[0] / 1e9, 2) if good else None}
             if good:
                 row["xgmi_frac"] = xgmi_roofline(world, b, v[0])["frac"]
+                if b <= (1 << 20) and eng != "p2p":   # the small-message floor without host launch cost
+                    gdt, gsame = graph_replay_us(comm, inputs[0], out, k, st, world, refs[0] if refs else None)
+                    row["graph_us"] = round(gdt * 1e6, 2) if gdt is not None else None
+                    row["graph_bit_identical"] = gsame
             rows.append(row)
             del got
         del inputs, out, refs

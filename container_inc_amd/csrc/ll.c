@@ -149,11 +149,27 @@ int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R
     INCCL_HIP(hipStreamIsCapturing(st, &cap));
     const int capturing = cap != hipStreamCaptureStatusNone;
     if (!capturing && c->ll_last_stream && c->ll_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[7], 0));
+    /* $INCCL_LL_CHECK (debugging aid, eager calls only): wait before and after
+     * the call and check that the device call counter advanced by exactly one
+     * and the retire counter is back at 0 */
+    const int check = !capturing && getenv("INCCL_LL_CHECK") != NULL;
+    uint32_t before[2] = {0, 0}, after[2] = {0, 0};
+    if (check) {
+        INCCL_HIP(hipStreamSynchronize(st));
+        INCCL_HIP(hipMemcpy(before, l.ctr, sizeof(before), hipMemcpyDeviceToHost));
+    }
     rc = inccl_k_ll_oneshot(&l, st);
     if (rc) return inccl_set_error(INCCL_ERR_HIP, "ll kernel launch failed (%d)", rc);
     if (!capturing) {
         INCCL_HIP(hipEventRecord(c->ev[7], st));
         c->ll_last_stream = st;
+    }
+    if (check) {
+        INCCL_HIP(hipStreamSynchronize(st));
+        INCCL_HIP(hipMemcpy(after, l.ctr, sizeof(after), hipMemcpyDeviceToHost));
+        if (after[0] != before[0] + 1 || before[1] != 0 || after[1] != 0)
+            fprintf(stderr, "[inccl ll rank %d] n %zu grid %d: call counter %u -> %u, retired %u -> %u\n", me, n,
+                    inccl_k_ll_grid(n), before[0], after[0], before[1], after[1]);
     }
     return 0;
 }
