@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--engine", default="auto", choices=["auto", "rccl", "ar", "a2a", "p2p", "mesh", "meshw"],
                    help="N>1 exchange engine; auto = time every candidate during warmup, keep the fastest")
     p.add_argument("--no-sweep", action="store_true", help="N>1: skip the bucket-size sweep (BASELINE config 5)")
+    p.add_argument("--settle-seconds", type=float, default=0.1,
+                   help="untimed steps before the W warmup steps, until this much wall time has passed: the first "
+                        "~100 launches over freshly allocated buckets run up to 2x slower (launch_drift_probe.py)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true",
@@ -600,6 +603,17 @@ def main():
     def step():
         comm.allreduce_f32(srcs, out=out, scale_exp=k, chunks=chunks, stream=stream.cuda_stream)
 
+    # settle: untimed steps in groups of 10 until --settle-seconds have passed (the
+    # same count on every rank), so that the timed steps see steady state rather
+    # than the first passes over freshly allocated buckets
+    settle_steps, t_settle = 0, time.perf_counter()
+    while True:
+        for _ in range(10):
+            step()
+        settle_steps += 10
+        torch.cuda.synchronize()
+        if agree([1.0 if time.perf_counter() - t_settle >= a.settle_seconds else 0.0], world)[0] > 0.0:
+            break
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -692,6 +706,7 @@ def main():
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 4),
+        "settle_steps": settle_steps,
         "device_ms_per_step_rank0": round(dev_ms / a.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",

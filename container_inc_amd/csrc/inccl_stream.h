@@ -95,7 +95,16 @@ struct Geometry {
     static constexpr int U = Unroll<R>::U;
 };
 
-template <int IN, int OUT, int R, bool NT, int BLOCK = kBlock, int U = Unroll<R>::U, bool NTS = true>
+// Output store policy.  kStoreWT (sc1, write-through: the line leaves the L2)
+// measured best on MI355X (tools/tune/tune_cold.hip, R = 2 x 256 MiB): 7.40 TB/s
+// on repeated steps and 6.29-6.33 TB/s on cold data, against 6.96 / 6.10-6.13 for
+// nontemporal stores and 7.06 / 6.14 for plain ones.  Write-through leaves no
+// dirty output lines in L2: the inputs keep more of the caches, and the kernel
+// boundary has nothing to write back.
+constexpr int kStorePlain = 0, kStoreNT = 1, kStoreWT = 2;
+constexpr int kAuxSc1 = 16;   // buffer instruction cache policy bit sc1
+
+template <int IN, int OUT, int R, bool NT, int BLOCK = kBlock, int U = Unroll<R>::U, int SP = kStoreWT>
 __global__ __launch_bounds__(BLOCK) void k_stream_vec(SrcPtrs src, void* __restrict__ dst, int64_t n4, Scale sc)
 {
     const int k = resolve_k(sc);
@@ -108,6 +117,10 @@ __global__ __launch_bounds__(BLOCK) void k_stream_vec(SrcPtrs src, void* __restr
     for (int64_t base = (int64_t)blockIdx.x * tile_elems; base < n4; base += stride) {
         const int64_t i0 = base + threadIdx.x;
         if (base + tile_elems <= n4) {
+            // the tile's output through a buffer resource: the store's cache
+            // policy is then explicit (a plain pointer store cannot carry sc1)
+            const __amdgpu_buffer_rsrc_t orsrc =
+                __builtin_amdgcn_make_buffer_rsrc(out + base, 0, (int)(tile_elems * 16), 0x00020000);
             u32x4 v[R][U];
 #pragma unroll
             for (int u = 0; u < U; ++u)
@@ -131,8 +144,12 @@ __global__ __launch_bounds__(BLOCK) void k_stream_vec(SrcPtrs src, void* __restr
                 o.y = store_xform<OUT>(acc.y, inv);
                 o.z = store_xform<OUT>(acc.z, inv);
                 o.w = store_xform<OUT>(acc.w, inv);
-                if constexpr (NTS) __builtin_nontemporal_store(o, out + i0 + (int64_t)u * BLOCK);
-                else out[i0 + (int64_t)u * BLOCK] = o;
+                if constexpr (SP == kStoreWT)
+                    __builtin_amdgcn_raw_buffer_store_b128(o, orsrc, (int)((threadIdx.x + u * BLOCK) * 16), 0, kAuxSc1);
+                else if constexpr (SP == kStoreNT)
+                    __builtin_nontemporal_store(o, out + i0 + (int64_t)u * BLOCK);
+                else
+                    out[i0 + (int64_t)u * BLOCK] = o;
             }
         } else {
 #pragma unroll

@@ -64,6 +64,59 @@ __global__ __launch_bounds__(BLOCK) void k_xcd(SrcPtrs src, u32x4* __restrict__ 
     }
 }
 
+// the product kernel's tile (512 x 1) with the output stored through a buffer
+// resource and an explicit cache policy: AUX = 16 (sc1: write-through, the line
+// leaves L2) / 17 (sc0 sc1) / 2 (nt) / 0 (plain)
+template <int BLOCK, int AUX>
+__global__ __launch_bounds__(BLOCK) void k_store_policy(SrcPtrs src, u32x4* __restrict__ out, int64_t n4, Scale sc)
+{
+    const float scale = pow2f(sc.k), inv = pow2f(-sc.k);
+    const int64_t t = blockIdx.x;
+    const int64_t i = t * BLOCK + threadIdx.x;
+    const u32x4* a = reinterpret_cast<const u32x4*>(src.p[0]);
+    const u32x4* c = reinterpret_cast<const u32x4*>(src.p[1]);
+    const u32x4 x = __builtin_nontemporal_load(a + i);
+    const u32x4 y = __builtin_nontemporal_load(c + i);
+    u32x4 o;
+    o.x = __float_as_uint((float)(int32_t)(quant1(__uint_as_float(x.x), scale) + quant1(__uint_as_float(y.x), scale)) * inv);
+    o.y = __float_as_uint((float)(int32_t)(quant1(__uint_as_float(x.y), scale) + quant1(__uint_as_float(y.y), scale)) * inv);
+    o.z = __float_as_uint((float)(int32_t)(quant1(__uint_as_float(x.z), scale) + quant1(__uint_as_float(y.z), scale)) * inv);
+    o.w = __float_as_uint((float)(int32_t)(quant1(__uint_as_float(x.w), scale) + quant1(__uint_as_float(y.w), scale)) * inv);
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(out + t * BLOCK, 0, BLOCK * 16, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(o, r, (int)(threadIdx.x * 16), 0, AUX);
+}
+
+// loads and stores through buffer resources with explicit cache policies
+// (LAUX / SAUX: 0 plain, 2 nt, 16 sc1, 17 sc0 sc1), U float4 per lane per input
+template <int BLOCK, int U, int LAUX, int SAUX>
+__global__ __launch_bounds__(BLOCK) void k_policy(SrcPtrs src, u32x4* __restrict__ out, int64_t n4, Scale sc)
+{
+    const float scale = pow2f(sc.k), inv = pow2f(-sc.k);
+    const int64_t base = (int64_t)blockIdx.x * BLOCK * U;
+    const __amdgpu_buffer_rsrc_t ra =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(src.p[0]) , 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(src.p[1]), 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
+    u32x4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int off = (int)((base + u * BLOCK + threadIdx.x) * 16);
+        x[u] = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, LAUX);
+        y[u] = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, LAUX);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        u32x4 o;
+        o.x = __float_as_uint((float)(int32_t)(quant1(__uint_as_float(x[u].x), scale) + quant1(__uint_as_float(y[u].x), scale)) * inv);
+        o.y = __float_as_uint((float)(int32_t)(quant1(__uint_as_float(x[u].y), scale) + quant1(__uint_as_float(y[u].y), scale)) * inv);
+        o.z = __float_as_uint((float)(int32_t)(quant1(__uint_as_float(x[u].z), scale) + quant1(__uint_as_float(y[u].z), scale)) * inv);
+        o.w = __float_as_uint((float)(int32_t)(quant1(__uint_as_float(x[u].w), scale) + quant1(__uint_as_float(y[u].w), scale)) * inv);
+        __builtin_amdgcn_raw_buffer_store_b128(o, ro, (int)((base + u * BLOCK + threadIdx.x) * 16), 0, SAUX);
+    }
+}
+
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_add2(const u32x4* __restrict__ a, const u32x4* __restrict__ b,
                                                 u32x4* __restrict__ o, int64_t n4)
@@ -115,7 +168,7 @@ static void report(const char* name, int block, int u, int depth, int nt, int nt
     fflush(stdout);
 }
 
-template <int BLOCK, int U, bool NT, bool NTS>
+template <int BLOCK, int U, bool NT, int SP>
 static void product(int depth)
 {
     const int64_t tiles = n4 / ((int64_t)BLOCK * U);
@@ -125,10 +178,10 @@ static void product(int depth)
         p.p[0] = A[s];
         p.p[1] = B[s];
         Scale sc{25, nullptr, 2};
-        hipLaunchKernelGGL((k_stream_vec<F32, F32, 2, NT, BLOCK, U, NTS>), dim3((unsigned)grid), dim3(BLOCK), 0, 0, p,
+        hipLaunchKernelGGL((k_stream_vec<F32, F32, 2, NT, BLOCK, U, SP>), dim3((unsigned)grid), dim3(BLOCK), 0, 0, p,
                            O[s], n4, sc);
     });
-    report("fused", BLOCK, U, depth, NT, NTS, ms, 12.0 * n);
+    report("fused", BLOCK, U, depth, NT, SP, ms, 12.0 * n);
 }
 
 template <int BLOCK, int U, bool NT, bool NTS>
@@ -143,6 +196,38 @@ static void xcd()
                            (u32x4*)O[s], n4, sc);
     });
     report("fused_xcd_contiguous", BLOCK, U, 1, NT, NTS, ms, 12.0 * n);
+}
+
+template <int BLOCK, int AUX>
+static void store_policy()
+{
+    float ms = cold_ms([&](int s) {
+        SrcPtrs p = {};
+        p.p[0] = A[s];
+        p.p[1] = B[s];
+        Scale sc{25, nullptr, 2};
+        hipLaunchKernelGGL((k_store_policy<BLOCK, AUX>), dim3((unsigned)(n4 / BLOCK)), dim3(BLOCK), 0, 0, p,
+                           (u32x4*)O[s], n4, sc);
+    });
+    char name[64];
+    snprintf(name, sizeof(name), "fused_store_aux%d", AUX);
+    report(name, BLOCK, 1, 1, 1, AUX, ms, 12.0 * n);
+}
+
+template <int BLOCK, int U, int LAUX, int SAUX>
+static void policy2()
+{
+    float ms = cold_ms([&](int s) {
+        SrcPtrs p = {};
+        p.p[0] = A[s];
+        p.p[1] = B[s];
+        Scale sc{25, nullptr, 2};
+        hipLaunchKernelGGL((k_policy<BLOCK, U, LAUX, SAUX>), dim3((unsigned)(n4 / BLOCK / U)), dim3(BLOCK), 0, 0, p,
+                           (u32x4*)O[s], n4, sc);
+    });
+    char name[64];
+    snprintf(name, sizeof(name), "fused_load%d_store%d", LAUX, SAUX);
+    report(name, BLOCK, U, 1, LAUX, SAUX, ms, 12.0 * n);
 }
 
 template <int BLOCK>
@@ -176,17 +261,11 @@ int main()
     CHECK(hipEventCreate(&e1));
     for (int rep = 0; rep < 4; ++rep) {
         g_hot = rep & 1;
-        product<512, 1, true, true>(1);      // the product's geometry
-        product<512, 2, true, true>(1);
-        product<256, 2, true, true>(1);
-        product<1024, 1, true, true>(1);
-        product<1024, 2, true, true>(1);
-        xcd<512, 1, true, true>();
-        xcd<512, 2, true, true>();
-        xcd<256, 2, true, true>();
-        xcd<1024, 1, true, true>();
-        xcd<256, 4, true, true>();
-        xcd<512, 1, false, true>();
+        product<512, 1, true, kStoreWT>(1);   // the product (write-through stores)
+        product<512, 1, true, kStoreNT>(1);   // round 1's product (nontemporal stores)
+        product<512, 2, true, kStoreWT>(1);
+        product<1024, 1, true, kStoreWT>(1);
+        policy2<512, 1, 2, 16>();
         refs<512>();
     }
     return 0;

@@ -94,7 +94,7 @@ static void policy(const SrcPtrs& s, void* out, int64_t n4, int depth)
     const int64_t tiles = n4 / 512;
     const int64_t grid = tiles / depth;
     float ms = time_ms([&] {
-        hipLaunchKernelGGL((k_stream_vec<F32, F32, 2, NT, 512, 1, NTS>), dim3((unsigned)grid), dim3(512), 0, 0, s, out,
+        hipLaunchKernelGGL((k_stream_vec<F32, F32, 2, NT, 512, 1, NTS ? kStoreNT : kStorePlain>), dim3((unsigned)grid), dim3(512), 0, 0, s, out,
                            n4, sc);
     });
     printf("{\"kernel\": \"fused_policy\", \"R\": 2, \"nt_loads\": %d, \"nt_stores\": %d, \"tiles_per_block\": %d, "
