@@ -189,6 +189,10 @@ def run_verified(comm, eng: str, ch: int, inputs, out, k: int, stream, refs):
         comm.allreduce_f32(xs, out=out, scale_exp=k, chunks=ch, stream=stream.cuda_stream)
         torch.cuda.synchronize()
         got.append(out.clone())
+        # the clone runs on torch's stream, the next call on `stream`: without
+        # this wait the next call can overwrite lanes of `out` before the clone
+        # has read them (seen as "the previous call's values on some lanes")
+        torch.cuda.synchronize()
     if refs is None:
         same = bool(torch.equal(got[0], got[2]))
     else:

@@ -168,6 +168,7 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
         for (int j = 0; j < kMaxR; ++j)
             if (j < a.W) peer[j] = rsrc(a.peer_data[j] + slot, (uint32_t)(nq * 16));
     }
+    const __amdgpu_buffer_rsrc_t dst_rs = rsrc(a.dst, (uint32_t)(a.n * 4));
     for (int64_t q0 = (int64_t)blockIdx.x * kLLBlock + tid; q0 < nq; q0 += stride * kU) {
         u32x4 x[kU][kMaxR];
 #pragma unroll
@@ -200,7 +201,8 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
             o.z = __float_as_uint((float)(int32_t)acc.z * inv);
             o.w = __float_as_uint((float)(int32_t)acc.w * inv);
             if (vec_dst && 4 * q + 4 <= a.n) {
-                reinterpret_cast<u32x4*>(a.dst)[q] = o;
+                // write-through (sc1): nothing of dst stays dirty in this XCD's L2
+                __builtin_amdgcn_raw_buffer_store_b128(o, dst_rs, (int)(q * 16), 0, 16);
             } else {
                 const uint32_t v[4] = {o.x, o.y, o.z, o.w};
                 for (int e = 0; e < 4; ++e)

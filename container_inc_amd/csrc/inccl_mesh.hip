@@ -273,6 +273,7 @@ __device__ bool do_gather(const MeshArgs& a, int c, int j, uint32_t epoch)
                                        : a.peer_res[j] + (int64_t)c * a.chunk;
     const __amdgpu_buffer_rsrc_t src = rsrc(sbase, (uint32_t)(chunk_len(a, c) * 4));
     uint32_t* d = reinterpret_cast<uint32_t*>(a.dst) + lo;
+    const __amdgpu_buffer_rsrc_t drs = rsrc(d, (uint32_t)(nq * 16));   // write-through dst stores (vec_dst)
     for (int64_t q0 = threadIdx.x; q0 < nq; q0 += (int64_t)kMeshBlock * kMeshU) {
         u32x4 v[kMeshU];
 #pragma unroll
@@ -283,7 +284,7 @@ __device__ bool do_gather(const MeshArgs& a, int c, int j, uint32_t epoch)
             const int64_t q = q0 + (int64_t)u * kMeshBlock;
             if (q < nq) {
                 if (a.vec_dst) {
-                    __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(d) + q);
+                    __builtin_amdgcn_raw_buffer_store_b128(v[u], drs, (int)(q * 16), 0, 16);   // sc1
                 } else {
                     d[4 * q] = v[u].x;
                     d[4 * q + 1] = v[u].y;

@@ -6,8 +6,9 @@
 // addresses on every call.  So every load of peer memory is a system-scope
 // `buffer_load_dwordx4 ... sc0 sc1`: coherent, L1-bypassing, and 0-3 % slower
 // than a plain 16-B load (MI355X_MICROARCH.md, load flavours).  The producers'
-// plain stores reach memory at their kernel's end-of-kernel release, before
-// the host barrier that separates the phases.
+// stores are write-through (`sc1`, as the stream kernel's): they leave
+// the L2 at once and reach memory before the host barrier that separates the
+// phases, and nothing is left dirty for the kernel boundary to write back.
 //
 //   k_peer_reduce<R>:  out[i] = dequant( sum_{j<R} peer_j[i] )   int32 -> fp32
 //       the reference switch's aggregate (non_termination_switch.c:361-363)
@@ -25,6 +26,7 @@ namespace {
 using namespace inccl_dev;
 
 constexpr int kAuxSys = 1 | 16;   // buffer instruction cache policy: sc0 | sc1
+constexpr int kAuxWT = 16;        // sc1: write-through store
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes)
 {
@@ -67,7 +69,7 @@ __global__ __launch_bounds__(BLOCK) void k_peer_reduce(SrcPtrs src, float* __res
                 o.z = __float_as_uint((float)(int32_t)acc.z * inv);
                 o.w = __float_as_uint((float)(int32_t)acc.w * inv);
             }
-            __builtin_nontemporal_store(o, out + i);
+            __builtin_amdgcn_raw_buffer_store_b128(o, rsrc(out + base, tile_bytes), (int)(threadIdx.x * 16u), 0, kAuxWT);
         }
     }
 }
@@ -103,7 +105,8 @@ __global__ __launch_bounds__(kGatherBlock) void k_peer_gather(Segs s, uint32_t* 
             const int64_t i = base + threadIdx.x + (int64_t)u * kGatherBlock;
             if (i < n4) {
                 if (dvec) {
-                    __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(d) + i);
+                    __builtin_amdgcn_raw_buffer_store_b128(v[u], rsrc(reinterpret_cast<u32x4*>(d) + base, tile_bytes),
+                                                           (int)((threadIdx.x + u * kGatherBlock) * 16u), 0, kAuxWT);
                 } else {
                     d[4 * i] = v[u].x;
                     d[4 * i + 1] = v[u].y;

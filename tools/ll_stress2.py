@@ -3,7 +3,10 @@ on a side stream alternating two input sets, torch.cuda.synchronize(), a clone
 of dst on torch's stream -- then p2p calls on the same buffers, two ranks on
 one GPU; every clone AND a direct host read of dst checked against the
 oracle.  argv: iterations [rccl] (rccl: also attempt the RCCL engine, which
-fails on a shared GPU, before each ll round, as the sweep does)."""
+fails on a shared GPU, before each ll round, as the sweep does).
+STRESS_RACE=1: demonstrate the verification race of bench.run_verified before
+its fix -- a delayed clone of dst on torch's stream, not waited for, is
+overwritten by the next call on the side stream."""
 import multiprocessing as mp
 import os
 import socket
@@ -31,6 +34,7 @@ def _rank_main(rank, port, q, iters, rccl):
     grp = inccl.inccl_group_create(2, rank, "127.0.0.1", port=port)
     comm = inccl.inccl_communicator_create(grp, 0)
     k, n = 25, int(os.environ.get("STRESS_N", "16384"))
+    race = os.environ.get("STRESS_RACE") == "1"
     sets, wants = [], []
     for seed in (7000, 8000):
         every, mine = [], None
@@ -56,6 +60,24 @@ def _rank_main(rank, port, q, iters, rccl):
                 pass
         for eng in ("ll", "p2p"):
             comm.set_engine(eng)
+            if race:
+                # the round-2 bench bug, made deterministic: the clone on torch's
+                # stream is delayed and NOT waited for before the next call on st
+                clones = []
+                for which in (0, 1, 0):
+                    comm.allreduce_f32(sets[which], out=out, scale_exp=k, stream=st.cuda_stream)
+                    torch.cuda.synchronize()
+                    torch.cuda._sleep(20_000_000)
+                    clones.append(out.clone())
+                torch.cuda.synchronize()
+                for call, (which, c) in enumerate(zip((0, 1, 0), clones)):
+                    cl = c.cpu().numpy().view(np.uint32)
+                    wrong = np.flatnonzero(cl != wants[which])
+                    if wrong.size:
+                        other = int(np.count_nonzero(cl[wrong] == wants[1 - which][wrong]))
+                        lines.append(f"iter {it} {eng} call {call} (racing clone): {wrong.size} wrong, "
+                                     f"{other} = the next call's set")
+                continue
             for call, which in enumerate((0, 1, 0)):
                 comm.allreduce_f32(sets[which], out=out, scale_exp=k, stream=st.cuda_stream)
                 torch.cuda.synchronize()
