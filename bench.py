@@ -319,7 +319,13 @@ def kernel_time_ms(fn, stream, iters: int) -> float:
 
 def n1_sizes(dev, R: int, k: int, sizes_mib=(4, 64, 256, 1024)) -> list:
     """north_star's bucket sizes at N = 1: the fused kernel on R resident buckets
-    of each size, GB/s of buckets reduced and the kernel's HBM roofline fraction."""
+    of each size, GB/s of buckets reduced and the kernel's HBM roofline fraction.
+
+    `kernel_us` is per launch of `per` back-to-back launches captured in one
+    hipGraph and replayed (HIP events on the replay stream): the device rate.
+    `eager_us` is per call through the C ABI from Python, which at 4 MiB is
+    bound by the host (~7 us per ctypes call against ~3 us of kernel;
+    tools/tune/tune_small.hip, profiles/r02/tune_small.jsonl)."""
     import torch
 
     from container_inc_amd import inccl
@@ -333,9 +339,26 @@ def n1_sizes(dev, R: int, k: int, sizes_mib=(4, 64, 256, 1024)) -> list:
         out = torch.empty(n, device=dev)
         torch.cuda.synchronize()
         iters = max(50, min(400, (8 << 30) // (mib << 20)))
-        ms = kernel_time_ms(lambda: inccl.reduce_f32(xs, k, out=out, stream=st.cuda_stream), st, iters)
+        call = lambda: inccl.reduce_f32(xs, k, out=out, stream=st.cuda_stream)  # noqa: E731
+        eager = kernel_time_ms(call, st, iters)
+        per = max(10, min(100, iters // 4))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            for _ in range(per):
+                call()
+        reps = max(2, iters // per)
+        with torch.cuda.stream(st):   # replay() launches on the current stream
+            g.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(reps):
+                g.replay()
+            e1.record(st)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / (reps * per)
+        del g
         alg = (R + 1) * 4 * n
-        rows.append({"bucket_mib": mib, "kernel_us": round(ms * 1e3, 2),
+        rows.append({"bucket_mib": mib, "kernel_us": round(ms * 1e3, 2), "eager_us": round(eager * 1e3, 2),
                      "GBps_buckets": round(R * 4 * n / (ms * 1e-3) / 1e9, 1),
                      "hbm_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
                      "hbm_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
