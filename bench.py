@@ -23,6 +23,7 @@ Extra JSON fields:
   sizes             N = 1: north_star's 4/64/256/1024 MiB buckets, kernel GB/s + HBM fraction
   roofline_cold     N = 1: the fused kernel rotating through input sets far larger
                     than the 256 MiB Infinity Cache
+  r_variants        N = 1: config 2's R = 1 and R = 8 at 256 MiB, repeated and rotated
   numerics_vs_exact N = 1: error vs the exact (fp64) sum, R = 2 and 8, k = 25 and auto
   host_e2e          N = 1: BASELINE config 3, 1 GiB pinned host fp32 in 64 MiB buckets
   sweep             N > 1: 4 KiB .. 256 MiB and 1 GiB per engine, verified with
@@ -394,6 +395,42 @@ def cold_run(dev, R: int, k: int, n: int, sets: int = 4) -> dict:
     return {"sets": sets, "working_set_MiB": sets * alg >> 20, "kernel_us": round(ms * 1e3, 2),
             "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
             "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def r_variants(dev, k: int, n: int, rs=(1, 8)) -> list:
+    """BASELINE config 2's other local-bucket counts (R in {1, 2, 8}; R = 2 is the
+    headline): the fused kernel on R resident 256 MiB buckets, repeated launches
+    and, beside them, two rotated sets (2 x (R+1) x 256 MiB, beyond the Infinity
+    Cache)."""
+    import torch
+
+    from container_inc_amd import inccl
+    rows = []
+    st = torch.cuda.Stream(device=dev)
+    for R in rs:
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(3000 + R)
+        groups = [([torch.randn(n, generator=gen, device=dev) for _ in range(R)], torch.empty(n, device=dev))
+                  for _ in range(2)]
+        torch.cuda.synchronize()
+        hot = kernel_time_ms(lambda: inccl.reduce_f32(groups[0][0], k, out=groups[0][1], stream=st.cuda_stream),
+                             st, 40)
+        it = [0]
+
+        def rotated():
+            xs, out = groups[it[0] % 2]
+            it[0] += 1
+            inccl.reduce_f32(xs, k, out=out, stream=st.cuda_stream)
+
+        cold = kernel_time_ms(rotated, st, 40)
+        alg = (R + 1) * 4 * n
+        rows.append({"R": R, "bucket_mib": n * 4 >> 20, "kernel_us": round(hot * 1e3, 2),
+                     "hbm_frac": round(alg / (hot * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "rotated_kernel_us": round(cold * 1e3, 2),
+                     "rotated_hbm_frac": round(alg / (cold * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+        del groups
+        torch.cuda.empty_cache()
+    return rows
 
 
 def host_e2e(comm, k: int, gib: int = 1, bucket_mib: int = 64) -> dict:
@@ -776,6 +813,7 @@ def main():
         res["host_e2e"] = host_e2e(comm, k)
         res["sizes"] = n1_sizes(dev, R, k)
         res["roofline_cold"] = cold_run(dev, R, k, n)
+        res["r_variants"] = r_variants(dev, k, n)
         res["numerics_vs_exact"] = numerics_vs_exact(dev, n)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(n, R, k, a.cpu_seconds)
