@@ -26,6 +26,8 @@ Extra JSON fields:
   r_variants        N = 1: config 2's R = 1 and R = 8 at 256 MiB, repeated and rotated
   numerics_vs_exact N = 1: error vs the exact (fp64) sum, R = 2 and 8, k = 25 and auto
   host_e2e          N = 1: BASELINE config 3, 1 GiB pinned host fp32 in 64 MiB buckets
+  api_allreduce_write N = 1: the reference's entry point on a 256 MiB host int32
+                    message, registered and unregistered
   sweep             N > 1: 4 KiB .. 256 MiB and 1 GiB per engine, verified with
                     alternating input sets
 """
@@ -433,6 +435,43 @@ def r_variants(dev, k: int, n: int, rs=(1, 8)) -> list:
     return rows
 
 
+def api_allreduce_write(comm, mib: int = 256, calls: int = 7) -> dict:
+    """The reference's own entry point, inccl_allreduce_write (api.h:99, api.c:403-452),
+    on a `mib` MiB host int32 message at world 1: GB/s of one rank's message, with
+    src/dst registered (inccl_host_register, the ibv_reg_mr of api.c:170-176: direct
+    DMA) and unregistered (pinned staging).  Every call's dst is checked (at world 1
+    the sum is the message itself)."""
+    import numpy as np
+    n = mib << 18
+    rng = np.random.default_rng(9)
+    src = rng.integers(-(2 ** 31), 2 ** 31 - 1, n, dtype=np.int64, endpoint=True).astype(np.int32)
+    dst = np.empty_like(src)
+    res = {"message_mib": mib, "world": 1}
+    for mode in ("unregistered", "registered"):
+        if mode == "registered":
+            comm.host_register(src)
+            comm.host_register(dst)
+        for _ in range(2):   # first calls: staging / workspaces grow, DMA mappings warm up
+            comm.allreduce_write(src, n, dst)
+        ok = bool(np.array_equal(dst, src))
+        times = []
+        for _ in range(calls):
+            dst[:1] = 0
+            t0 = time.perf_counter()
+            comm.allreduce_write(src, n, dst)
+            times.append(time.perf_counter() - t0)
+            ok = ok and bool(dst[0] == src[0])
+        ok = ok and bool(np.array_equal(dst, src))
+        dt = sorted(times)[len(times) // 2]   # median: single calls vary on a fresh box (tools/api_write_probe.py)
+        res[mode] = {"ms": round(dt * 1e3, 3), "GBps": round(n * 4 / dt / 1e9, 2),
+                     "best_GBps": round(n * 4 / min(times) / 1e9, 2), "calls": calls, "correct": ok}
+        if mode == "registered":
+            comm.host_deregister(src)
+            comm.host_deregister(dst)
+    res["reference_cpu_GBps_per_core"] = 0.27   # SURVEY.md §6, the reference's compiled path incl. framing/ICRC
+    return res
+
+
 def host_e2e(comm, k: int, gib: int = 1, bucket_mib: int = 64) -> dict:
     """BASELINE config 3: a `gib` GiB fp32 gradient in pinned host memory through
     inccl_allreduce_f32_host (bucket_mib buckets, H2D / reduce / D2H on three
@@ -811,6 +850,7 @@ def main():
         comm.set_engine(chosen[0])
     if world == 1 and not a.no_extras:
         res["host_e2e"] = host_e2e(comm, k)
+        res["api_allreduce_write"] = api_allreduce_write(comm)
         res["sizes"] = n1_sizes(dev, R, k)
         res["roofline_cold"] = cold_run(dev, R, k, n)
         res["r_variants"] = r_variants(dev, k, n)
