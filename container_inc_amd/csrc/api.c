@@ -401,6 +401,7 @@ int inccl_communicator_destroy(struct inccl_communicator *comm)
     if (comm->d_stage) hipFree(comm->d_stage);
     if (comm->d_words) hipFree(comm->d_words);
     inccl_copy_pool_destroy(comm->pool);
+    inccl_d2h_worker_destroy(comm->d2h);
     if (comm->send_payload) hipHostFree(comm->send_payload);
     if (comm->receive_payload) hipHostFree(comm->receive_payload);
     for (int i = 0; i < 9; ++i)
@@ -799,35 +800,74 @@ static int host_registered(const struct inccl_communicator *c, const void *p, si
     return 0;
 }
 
-/* src and dst registered: no host copies, the DMA engines read and write the
- * caller's memory.  Chunk i's H2D overlaps chunk i-1's D2H (PCIe is full
- * duplex); two device buffers ping-pong. */
-static int allreduce_host_q32_registered(struct inccl_communicator *c, const int32_t *src, size_t n, int32_t *dst)
+/* Direct DMA between the caller's memory and two ping-ponging device chunks:
+ * chunk i's H2D overlaps chunk i-1's D2H (PCIe is full duplex).  Used when src
+ * and dst are registered, and -- unless $INCCL_HOST_STAGING=pool -- for
+ * unregistered (pageable) memory too: HIP's own pageable copies run at the
+ * pinned rate on MI355X boxes (tools/api_write_probe.py HOSTREF=1: 56 GB/s each
+ * way), far above the staged pipeline below.  A pageable copy returns only when
+ * done, so with pageable memory a helper thread issues the D2Hs (hostdma.c) and
+ * the two directions stay in flight together.  $INCCL_HOST_CHUNK_MIB sets the
+ * chunk (default 16 MiB). */
+static size_t host_chunk_elems(void)
 {
-    const size_t CH = ((size_t)16 << 20) / sizeof(int32_t);
+    static size_t ch = 0;
+    if (!ch) {
+        const char *e = getenv("INCCL_HOST_CHUNK_MIB");
+        long v = e ? atol(e) : 0;
+        if (v < 1 || v > 1024) v = 16;
+        ch = ((size_t)v << 20) / sizeof(int32_t);
+    }
+    return ch;
+}
+
+static int allreduce_host_q32_direct(struct inccl_communicator *c, const int32_t *src, size_t n, int32_t *dst,
+                                     int pageable)
+{
+    const size_t CH = host_chunk_elems();
     int rc = inccl_ensure_dev(&c->d_stage, &c->d_stage_bytes, 2 * CH * sizeof(int32_t));
     if (rc) return rc;
+    if (pageable && !c->d2h) c->d2h = inccl_d2h_worker_create(c->group->device);
+    struct inccl_d2h_worker *w = pageable ? c->d2h : NULL;   /* NULL: D2Hs issued here */
     int32_t *d[2] = {(int32_t *)c->d_stage, (int32_t *)c->d_stage + CH};
     hipStream_t h2d = c->copy_streams[0], d2h = c->copy_streams[1], ks = c->stream;
     hipEvent_t e_h2d[2] = {c->ev[0], c->ev[1]}, e_ar[2] = {c->ev[2], c->ev[3]}, e_d2h[2] = {c->ev[4], c->ev[5]};
     INCCL_HIP(hipStreamSynchronize(ks));
+    const unsigned long long base = w ? inccl_d2h_posted(w) : 0;
     const size_t nch = (n + CH - 1) / CH;
-    for (size_t i = 0; i < nch; ++i) {
+    for (size_t i = 0; i < nch && rc == 0; ++i) {
         const int s = (int)(i & 1);
         const size_t off = i * CH, cnt = (n - off) < CH ? (n - off) : CH;
-        if (i >= 2) INCCL_HIP(hipStreamWaitEvent(h2d, e_d2h[s], 0));    /* d[s] drained by chunk i-2 */
+        if (i >= 2) {   /* d[s] drained by chunk i-2 */
+            if (w) {
+                const hipError_t e = inccl_d2h_wait_issued(w, base + i - 1);
+                if (e != hipSuccess) {
+                    rc = inccl_hip_check(e, "D2H of a host chunk");
+                    break;
+                }
+            }
+            INCCL_HIP(hipStreamWaitEvent(h2d, e_d2h[s], 0));
+        }
         INCCL_HIP(hipMemcpyAsync(d[s], src + off, cnt * sizeof(int32_t), hipMemcpyHostToDevice, h2d));
         INCCL_HIP(hipEventRecord(e_h2d[s], h2d));
         INCCL_HIP(hipStreamWaitEvent(ks, e_h2d[s], 0));
         rc = inccl_tp_allreduce_q32(c, d[s], d[s], cnt, ks);            /* the switch's sum, nts.c:361-363 */
-        if (rc) return rc;
+        if (rc) break;
         INCCL_HIP(hipEventRecord(e_ar[s], ks));
-        INCCL_HIP(hipStreamWaitEvent(d2h, e_ar[s], 0));
-        INCCL_HIP(hipMemcpyAsync(dst + off, d[s], cnt * sizeof(int32_t), hipMemcpyDeviceToHost, d2h));
-        INCCL_HIP(hipEventRecord(e_d2h[s], d2h));
+        if (w) {
+            inccl_d2h_post(w, dst + off, d[s], cnt * sizeof(int32_t), e_ar[s], e_d2h[s], d2h);
+        } else {
+            INCCL_HIP(hipStreamWaitEvent(d2h, e_ar[s], 0));
+            INCCL_HIP(hipMemcpyAsync(dst + off, d[s], cnt * sizeof(int32_t), hipMemcpyDeviceToHost, d2h));
+            INCCL_HIP(hipEventRecord(e_d2h[s], d2h));
+        }
+    }
+    if (w) {   /* every posted job issued before the stream is drained, also after a failure */
+        const hipError_t e = inccl_d2h_wait_issued(w, inccl_d2h_posted(w));
+        if (e != hipSuccess && !rc) rc = inccl_hip_check(e, "D2H of a host chunk");
     }
     INCCL_HIP(hipStreamSynchronize(d2h));
-    return 0;
+    return rc;
 }
 
 /* Replaces api.c:403-452 / :330-401.  The reference encodes 1024-element
@@ -848,7 +888,13 @@ static int allreduce_host_q32(struct inccl_communicator *c, const int32_t *src, 
     if (!src || !dst) return inccl_set_error(INCCL_ERR_ARG, "NULL src/dst");
     INCCL_HIP(hipSetDevice(c->group->device));
     if (host_registered(c, src, n * sizeof(int32_t)) && host_registered(c, dst, n * sizeof(int32_t)))
-        return allreduce_host_q32_registered(c, src, n, dst);
+        return allreduce_host_q32_direct(c, src, n, dst, 0);
+    static int staging = -1;   /* $INCCL_HOST_STAGING=pool: the staged pipeline below */
+    if (staging < 0) {
+        const char *e = getenv("INCCL_HOST_STAGING");
+        staging = (e && strcmp(e, "pool") == 0) ? 1 : 0;
+    }
+    if (!staging) return allreduce_host_q32_direct(c, src, n, dst, 1);
     /* chunk: what the reference buffers hold, at least 1 MiB, at most 16 MiB */
     size_t chunk_bytes = c->payload_buf_size / 2;
     if (chunk_bytes < ((size_t)1 << 20)) chunk_bytes = (size_t)1 << 20;

@@ -35,6 +35,7 @@
 struct inccl_local_hub;
 struct inccl_shm_bar;
 struct inccl_copy_pool;
+struct inccl_d2h_worker;
 
 struct inccl_group {
     int rank;
@@ -107,6 +108,7 @@ struct inccl_communicator {
     struct { char *p; size_t len; } reg[INCCL_MAX_HOST_REGIONS];
     int nreg;
     struct inccl_copy_pool *pool;  /* host staging copies (copypool.c) */
+    struct inccl_d2h_worker *d2h;  /* issues pageable D2H copies beside the H2Ds (hostdma.c) */
     hipEvent_t ev[9];            /* [8]: p2p ordering across caller streams */
     hipStream_t p2p_last_stream;
 };
@@ -204,5 +206,13 @@ int inccl_mem_kind(const void *p);   /* hipPointerAttribute_t.allocationFlags */
 struct inccl_copy_pool *inccl_copy_pool_create(int n);
 void inccl_copy_pool_destroy(struct inccl_copy_pool *p);
 void inccl_copy(struct inccl_copy_pool *p, void *dst, const void *src, size_t bytes);
+
+/* hostdma.c */
+struct inccl_d2h_worker *inccl_d2h_worker_create(int device);
+void inccl_d2h_worker_destroy(struct inccl_d2h_worker *w);
+unsigned long long inccl_d2h_posted(struct inccl_d2h_worker *w);
+void inccl_d2h_post(struct inccl_d2h_worker *w, void *dst, const void *src, size_t bytes, hipEvent_t after,
+                    hipEvent_t done, hipStream_t st);
+hipError_t inccl_d2h_wait_issued(struct inccl_d2h_worker *w, unsigned long long count);
 
 #endif

@@ -57,7 +57,46 @@ def main():
     def emit(**kw):
         print(json.dumps(dict(pre=pre or "fresh", mib=mib, **kw)), flush=True)
 
-    for mode in ("unregistered", "registered", "registered", "unregistered"):
+    if os.environ.get("HOSTREF"):   # what the unregistered path is built from, alone
+        dbuf = torch.empty(n, dtype=torch.int32, device=dev)
+        ps, pd = torch.from_numpy(src), torch.from_numpy(dst)
+        for label, fn in (("np_copyto_1thread", lambda: np.copyto(dst, src)),
+                          ("hip_pageable_h2d", lambda: dbuf.copy_(ps)),
+                          ("hip_pageable_d2h", lambda: pd.copy_(dbuf))):
+            fn()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / 3
+            emit(what=label, ms=round(dt * 1e3, 3), GBps=round(n * 4 / dt / 1e9, 2))
+        del dbuf
+    if os.environ.get("SERIES"):   # per-call times over a long series: when does a slow phase end?
+        for phase in ("first_registration", "second_registration_new_buffers"):
+            s2 = src.copy() if phase.startswith("second") else src
+            d2 = np.empty_like(dst) if phase.startswith("second") else dst
+            comm.host_register(s2)
+            comm.host_register(d2)
+            t_start = time.perf_counter()
+            ms = []
+            for _ in range(int(os.environ["SERIES"])):
+                t0 = time.perf_counter()
+                comm.allreduce_write(s2, n, d2)
+                ms.append(round((time.perf_counter() - t0) * 1e3, 2))
+            emit(what="series_registered", phase=phase, ms_per_call=ms,
+                 elapsed_s=round(time.perf_counter() - t_start, 3), correct=bool(np.array_equal(s2, d2)))
+            comm.host_deregister(s2)
+            comm.host_deregister(d2)
+            # the same series unregistered (HIP pageable copies)
+            ms = []
+            for _ in range(int(os.environ["SERIES"])):
+                t0 = time.perf_counter()
+                comm.allreduce_write(s2, n, d2)
+                ms.append(round((time.perf_counter() - t0) * 1e3, 2))
+            emit(what="series_unregistered", phase=phase, ms_per_call=ms)
+    modes = os.environ.get("MODES", "unregistered,registered,registered,unregistered").split(",")
+    for mode in modes:
         if mode == "registered":
             comm.host_register(src)
             comm.host_register(dst)
@@ -66,7 +105,7 @@ def main():
         for _ in range(3):
             comm.allreduce_write(src, n, dst)
         dt = (time.perf_counter() - t0) / 3
-        emit(what="allreduce_write", mode=mode, ms=round(dt * 1e3, 3), GBps=round(n * 4 / dt / 1e9, 2),
+        emit(what="allreduce_write", mode=mode, copy_threads=os.environ.get("INCCL_COPY_THREADS", "4"), ms=round(dt * 1e3, 3), GBps=round(n * 4 / dt / 1e9, 2),
              correct=bool(np.array_equal(src, dst)))
         if mode == "registered":
             # the same DMA pattern through torch on pinned tensors: 16 MiB chunks, H2D on
