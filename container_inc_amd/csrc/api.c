@@ -793,6 +793,18 @@ int inccl_host_deregister(struct inccl_communicator *c, void *ptr)
     return inccl_set_error(INCCL_ERR_ARG, "host_deregister: %p is not a registered range", ptr);
 }
 
+/* page-locked host memory (hipHostMalloc'ed or hipHostRegister'ed by anyone) */
+static int host_pinned(const void *p)
+{
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof(a));
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();   /* pageable memory: not an error for the caller */
+        return 0;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 static int host_registered(const struct inccl_communicator *c, const void *p, size_t bytes)
 {
     for (int i = 0; i < c->nreg; ++i)
@@ -983,27 +995,49 @@ int inccl_allreduce_f32_host(struct inccl_communicator *c, const float *src_host
     float *out[2] = {(float *)c->d_stage + 2 * B, (float *)c->d_stage + 3 * B};
     hipStream_t h2d = c->copy_streams[0], d2h = c->copy_streams[1], ks = c->stream;
     hipEvent_t ev_h2d[2] = {c->ev[0], c->ev[1]}, ev_k[2] = {c->ev[2], c->ev[3]}, ev_d2h[2] = {c->ev[4], c->ev[5]};
+    /* pageable dst: its D2Hs come from the helper thread (hostdma.c), or each one
+     * would hold this thread until done and serialise the two directions */
+    if (!host_pinned(dst_host) && !c->d2h) c->d2h = inccl_d2h_worker_create(c->group->device);
+    struct inccl_d2h_worker *w = host_pinned(dst_host) ? NULL : c->d2h;
+    const unsigned long long base = w ? inccl_d2h_posted(w) : 0;
     /* start clean: streams idle w.r.t. earlier work on the compute stream */
     INCCL_HIP(hipStreamSynchronize(ks));
     size_t i = 0;
-    for (size_t off = 0; off < n; off += B, ++i) {
+    for (size_t off = 0; off < n && rc == 0; off += B, ++i) {
         const size_t cnt = (n - off) < B ? (n - off) : B;
         const int s = (int)(i & 1);
         if (i >= 2) INCCL_HIP(hipStreamWaitEvent(h2d, ev_k[s], 0));      /* in[s] consumed */
         INCCL_HIP(hipMemcpyAsync(in[s], src_host + off, cnt * sizeof(float), hipMemcpyHostToDevice, h2d));
         INCCL_HIP(hipEventRecord(ev_h2d[s], h2d));
         INCCL_HIP(hipStreamWaitEvent(ks, ev_h2d[s], 0));
-        if (i >= 2) INCCL_HIP(hipStreamWaitEvent(ks, ev_d2h[s], 0));     /* out[s] drained */
+        if (i >= 2) {   /* out[s] drained */
+            if (w) {   /* ev_d2h[s] holds chunk i-2's record only once the helper issued it */
+                const hipError_t e = inccl_d2h_wait_issued(w, base + i - 1);
+                if (e != hipSuccess) {
+                    rc = inccl_hip_check(e, "D2H of a host bucket");
+                    break;
+                }
+            }
+            INCCL_HIP(hipStreamWaitEvent(ks, ev_d2h[s], 0));
+        }
         const float *srcs[1] = {in[s]};
         rc = inccl_allreduce_f32(c, srcs, 1, out[s], cnt, scale_exp, ks);
-        if (rc) return rc;
+        if (rc) break;
         INCCL_HIP(hipEventRecord(ev_k[s], ks));
-        INCCL_HIP(hipStreamWaitEvent(d2h, ev_k[s], 0));
-        INCCL_HIP(hipMemcpyAsync(dst_host + off, out[s], cnt * sizeof(float), hipMemcpyDeviceToHost, d2h));
-        INCCL_HIP(hipEventRecord(ev_d2h[s], d2h));
+        if (w) {
+            inccl_d2h_post(w, dst_host + off, out[s], cnt * sizeof(float), ev_k[s], ev_d2h[s], d2h);
+        } else {
+            INCCL_HIP(hipStreamWaitEvent(d2h, ev_k[s], 0));
+            INCCL_HIP(hipMemcpyAsync(dst_host + off, out[s], cnt * sizeof(float), hipMemcpyDeviceToHost, d2h));
+            INCCL_HIP(hipEventRecord(ev_d2h[s], d2h));
+        }
+    }
+    if (w) {
+        const hipError_t e = inccl_d2h_wait_issued(w, inccl_d2h_posted(w));
+        if (e != hipSuccess && !rc) rc = inccl_hip_check(e, "D2H of a host bucket");
     }
     INCCL_HIP(hipStreamSynchronize(d2h));
     INCCL_HIP(hipStreamSynchronize(ks));
     INCCL_HIP(hipStreamSynchronize(h2d));
-    return 0;
+    return rc;
 }

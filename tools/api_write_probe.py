@@ -72,6 +72,17 @@ def main():
             dt = (time.perf_counter() - t0) / 3
             emit(what=label, ms=round(dt * 1e3, 3), GBps=round(n * 4 / dt / 1e9, 2))
         del dbuf
+    if os.environ.get("F32HOST"):   # config 3's entry point on pageable numpy buffers, 1 GiB, 64 MiB buckets
+        from oracle import oracle as O
+        xf = np.random.default_rng(3).standard_normal((1 << 30) // 4).astype(np.float32)
+        yf = np.empty_like(xf)
+        ms = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            comm.allreduce_f32_host(xf, yf, scale_exp=25, bucket_bytes=64 << 20)
+            ms.append(round((time.perf_counter() - t0) * 1e3, 2))
+        ok = bool(np.array_equal(yf.view(np.uint32), O.reduce_f32([xf], 25).view(np.uint32)))
+        emit(what="f32_host_pageable_1GiB", ms_per_call=ms, GBps_best=round((1 << 30) / min(ms) / 1e6, 2), correct=ok)
     if os.environ.get("SERIES"):   # per-call times over a long series: when does a slow phase end?
         for phase in ("first_registration", "second_registration_new_buffers"):
             s2 = src.copy() if phase.startswith("second") else src
@@ -95,7 +106,7 @@ def main():
                 comm.allreduce_write(s2, n, d2)
                 ms.append(round((time.perf_counter() - t0) * 1e3, 2))
             emit(what="series_unregistered", phase=phase, ms_per_call=ms)
-    modes = os.environ.get("MODES", "unregistered,registered,registered,unregistered").split(",")
+    modes = [m for m in os.environ.get("MODES", "unregistered,registered,registered,unregistered").split(",") if m]
     for mode in modes:
         if mode == "registered":
             comm.host_register(src)
