@@ -823,14 +823,10 @@ static int host_registered(const struct inccl_communicator *c, const void *p, si
  * chunk (default 16 MiB). */
 static size_t host_chunk_elems(void)
 {
-    static size_t ch = 0;
-    if (!ch) {
-        const char *e = getenv("INCCL_HOST_CHUNK_MIB");
-        long v = e ? atol(e) : 0;
-        if (v < 1 || v > 1024) v = 16;
-        ch = ((size_t)v << 20) / sizeof(int32_t);
-    }
-    return ch;
+    const char *e = getenv("INCCL_HOST_CHUNK_MIB");
+    long v = e ? atol(e) : 0;
+    if (v < 1 || v > 1024) v = 16;
+    return ((size_t)v << 20) / sizeof(int32_t);
 }
 
 static int allreduce_host_q32_direct(struct inccl_communicator *c, const int32_t *src, size_t n, int32_t *dst,
@@ -901,12 +897,8 @@ static int allreduce_host_q32(struct inccl_communicator *c, const int32_t *src, 
     INCCL_HIP(hipSetDevice(c->group->device));
     if (host_registered(c, src, n * sizeof(int32_t)) && host_registered(c, dst, n * sizeof(int32_t)))
         return allreduce_host_q32_direct(c, src, n, dst, 0);
-    static int staging = -1;   /* $INCCL_HOST_STAGING=pool: the staged pipeline below */
-    if (staging < 0) {
-        const char *e = getenv("INCCL_HOST_STAGING");
-        staging = (e && strcmp(e, "pool") == 0) ? 1 : 0;
-    }
-    if (!staging) return allreduce_host_q32_direct(c, src, n, dst, 1);
+    const char *staging = getenv("INCCL_HOST_STAGING");   /* "pool": the staged pipeline below */
+    if (!staging || strcmp(staging, "pool") != 0) return allreduce_host_q32_direct(c, src, n, dst, 1);
     /* chunk: what the reference buffers hold, at least 1 MiB, at most 16 MiB */
     size_t chunk_bytes = c->payload_buf_size / 2;
     if (chunk_bytes < ((size_t)1 << 20)) chunk_bytes = (size_t)1 << 20;

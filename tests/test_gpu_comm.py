@@ -154,6 +154,45 @@ def test_allreduce_write_registered(gpu, orc, world):
             assert np.all(dst[m:] == 5)
 
 
+@pytest.mark.parametrize("pipeline", ["direct-1MiB", "direct-default", "pool"])
+@pytest.mark.parametrize("world", [1, 2])
+def test_allreduce_write_unregistered_pipelines(gpu, orc, monkeypatch, pipeline, world):
+    """Plain (pageable) numpy src/dst -- host.c's malloc'ed buffers -- through both
+    host pipelines: direct pageable DMA with the D2Hs issued from the helper
+    thread (1 MiB chunks: 37 chunks, the helper's job ring wraps many times) and
+    the staged copy pool; three calls on the same arrays, dst prefilled with a
+    sentinel each time, tail beyond the last whole message untouched (api.c:406)."""
+    from container_inc_amd import inccl
+    if pipeline == "pool":
+        monkeypatch.setenv("INCCL_HOST_STAGING", "pool")
+    elif pipeline == "direct-1MiB":
+        monkeypatch.setenv("INCCL_HOST_CHUNK_MIB", "1")
+    n = 1024 * (256 * 37 + 5) + 300
+    m = n // 1024 * 1024
+    rng = np.random.default_rng(7 + world)
+    xs = [rng.integers(INT32_MIN, INT32_MAX, n, dtype=np.int64, endpoint=True).astype(np.int32) for _ in range(world)]
+    want = orc.sum_q32(xs)
+    hub = f"unreg-{pipeline}-{world}"
+
+    def rank(r):
+        grp = (inccl.inccl_group_create(1, 0, "127.0.0.1") if world == 1
+               else inccl.inccl_group_create_local(world, r, hub))
+        comm = inccl.inccl_communicator_create(grp, 1 << 20)
+        outs = []
+        for call in range(3):
+            dst = np.full(n, -3 - call, np.int32)
+            comm.allreduce_write(xs[r], n, dst)
+            outs.append((call, dst))
+        comm.destroy()
+        grp.destroy()
+        return outs
+
+    for outs in _run_ranks(world, rank):
+        for call, dst in outs:
+            np.testing.assert_array_equal(dst[:m], want[:m], err_msg=f"call {call}")
+            assert np.all(dst[m:] == -3 - call)
+
+
 @pytest.mark.parametrize("world,R,n,chunks,k", [
     (2, 2, 1 << 20, 1, 25),
     (2, 2, (1 << 20) + 77, 3, 25),
