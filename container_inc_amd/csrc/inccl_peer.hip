@@ -14,7 +14,10 @@
 //       the reference switch's aggregate (non_termination_switch.c:361-363)
 //       over the W ranks' shards, fused with the new dequantise stage
 //       (DEQ = false: the plain int32 sum, for the int32 allreduce)
-//   k_peer_gather:     dst[off_j + i] = src_j[i]  for every rank j (blockIdx.y)
+//   k_peer_gather:     dst[off_j + i] = src_j[i]  for every rank j; consecutive
+//       workgroups take consecutive ranks, so the resident workgroups read
+//       from every peer at once (segment-major dispatch would drain the peers
+//       one xGMI link at a time)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -78,6 +81,7 @@ struct Segs {
     const void* src[kMaxR];
     int64_t off[kMaxR];
     int64_t cnt[kMaxR];
+    int nseg;
 };
 
 constexpr int kGatherBlock = 256;
@@ -85,14 +89,15 @@ constexpr int kGatherU = 4;   // float4 per lane per tile
 
 __global__ __launch_bounds__(kGatherBlock) void k_peer_gather(Segs s, uint32_t* __restrict__ dst)
 {
-    const int j = blockIdx.y;
+    const int j = (int)(blockIdx.x % (unsigned)s.nseg);          // interleaved: every link busy at once
+    const int64_t xb = blockIdx.x / (unsigned)s.nseg, gxs = gridDim.x / (unsigned)s.nseg;
     const int64_t cnt = s.cnt[j];
     uint32_t* __restrict__ d = dst + s.off[j];
     const uint32_t* src = reinterpret_cast<const uint32_t*>(s.src[j]);
     const int64_t n4 = cnt >> 2;
     const int64_t tile = (int64_t)kGatherBlock * kGatherU;
     const bool dvec = (reinterpret_cast<uintptr_t>(d) & 15u) == 0;
-    for (int64_t base = (int64_t)blockIdx.x * tile; base < n4; base += (int64_t)gridDim.x * tile) {
+    for (int64_t base = xb * tile; base < n4; base += gxs * tile) {
         const int64_t left = n4 - base;
         const uint32_t tile_bytes = (uint32_t)((left < tile ? left : tile) * 16);
         const u32x4* tb = reinterpret_cast<const u32x4*>(src) + base;
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(kGatherBlock) void k_peer_gather(Segs s, uint32_t* 
             }
         }
     }
-    if (blockIdx.x == 0)   // ragged tail of the last shard
+    if (xb == 0)   // ragged tail of the last shard
         for (int64_t i = (n4 << 2) + threadIdx.x; i < cnt; i += kGatherBlock)
             d[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -193,6 +198,7 @@ extern "C" int inccl_k_peer_gather(const void* const* src, const int64_t* off, c
 {
     if (nseg < 1 || nseg > kMaxR || dst == nullptr) return INCCL_ERR_ARG;
     Segs s = {};
+    s.nseg = nseg;
     int64_t maxc = 0;
     for (int j = 0; j < nseg; ++j) {
         if ((src[j] == nullptr && cnt[j] > 0) || cnt[j] < 0 || !aligned16(src[j])) return INCCL_ERR_ARG;
@@ -205,7 +211,7 @@ extern "C" int inccl_k_peer_gather(const void* const* src, const int64_t* off, c
     const int64_t tile = (int64_t)kGatherBlock * kGatherU * 4;
     int64_t gx = (maxc + tile - 1) / tile;
     if (gx < 1) gx = 1;
-    hipLaunchKernelGGL(k_peer_gather, dim3((unsigned)gx, (unsigned)nseg), dim3(kGatherBlock), 0, (hipStream_t)stream, s,
+    hipLaunchKernelGGL(k_peer_gather, dim3((unsigned)(gx * nseg)), dim3(kGatherBlock), 0, (hipStream_t)stream, s,
                        reinterpret_cast<uint32_t*>(dst));
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
