@@ -89,6 +89,14 @@ template <int R>
 struct Unroll {
     static constexpr int U = 1;
 };
+// R = 2 with write-through stores (round 2, tools/tune/tune_cold.hip,
+// profiles/r02/tune_store_policy_wt.jsonl): 512 x 2 beats 512 x 1 both on
+// repeated steps (110.7 vs 111.5-111.8 us) and on cold data (124.5-124.9 vs
+// 125.1-127.2 us)
+template <>
+struct Unroll<2> {
+    static constexpr int U = 2;
+};
 template <int R>
 struct Geometry {
     static constexpr int BLOCK = (R == 2 || R == 3) ? 512 : 1024;
