@@ -821,6 +821,17 @@ static int host_registered(const struct inccl_communicator *c, const void *p, si
  * done, so with pageable memory a helper thread issues the D2Hs (hostdma.c) and
  * the two directions stay in flight together.  $INCCL_HOST_CHUNK_MIB sets the
  * chunk (default 16 MiB). */
+/* inside the host pipelines' chunk loops: a failed HIP call ends the loop (not
+ * the function), so that the D2H helper's posted jobs are drained before return */
+#define LOOP_HIP(call)                                 \
+    {                                                  \
+        const hipError_t e_ = (call);                  \
+        if (e_ != hipSuccess) {                        \
+            rc = inccl_hip_check(e_, #call);           \
+            break;                                     \
+        }                                              \
+    }
+
 static size_t host_chunk_elems(void)
 {
     const char *e = getenv("INCCL_HOST_CHUNK_MIB");
@@ -854,20 +865,20 @@ static int allreduce_host_q32_direct(struct inccl_communicator *c, const int32_t
                     break;
                 }
             }
-            INCCL_HIP(hipStreamWaitEvent(h2d, e_d2h[s], 0));
+            LOOP_HIP(hipStreamWaitEvent(h2d, e_d2h[s], 0));
         }
-        INCCL_HIP(hipMemcpyAsync(d[s], src + off, cnt * sizeof(int32_t), hipMemcpyHostToDevice, h2d));
-        INCCL_HIP(hipEventRecord(e_h2d[s], h2d));
-        INCCL_HIP(hipStreamWaitEvent(ks, e_h2d[s], 0));
+        LOOP_HIP(hipMemcpyAsync(d[s], src + off, cnt * sizeof(int32_t), hipMemcpyHostToDevice, h2d));
+        LOOP_HIP(hipEventRecord(e_h2d[s], h2d));
+        LOOP_HIP(hipStreamWaitEvent(ks, e_h2d[s], 0));
         rc = inccl_tp_allreduce_q32(c, d[s], d[s], cnt, ks);            /* the switch's sum, nts.c:361-363 */
         if (rc) break;
-        INCCL_HIP(hipEventRecord(e_ar[s], ks));
+        LOOP_HIP(hipEventRecord(e_ar[s], ks));
         if (w) {
             inccl_d2h_post(w, dst + off, d[s], cnt * sizeof(int32_t), e_ar[s], e_d2h[s], d2h);
         } else {
-            INCCL_HIP(hipStreamWaitEvent(d2h, e_ar[s], 0));
-            INCCL_HIP(hipMemcpyAsync(dst + off, d[s], cnt * sizeof(int32_t), hipMemcpyDeviceToHost, d2h));
-            INCCL_HIP(hipEventRecord(e_d2h[s], d2h));
+            LOOP_HIP(hipStreamWaitEvent(d2h, e_ar[s], 0));
+            LOOP_HIP(hipMemcpyAsync(dst + off, d[s], cnt * sizeof(int32_t), hipMemcpyDeviceToHost, d2h));
+            LOOP_HIP(hipEventRecord(e_d2h[s], d2h));
         }
     }
     if (w) {   /* every posted job issued before the stream is drained, also after a failure */
@@ -998,10 +1009,10 @@ int inccl_allreduce_f32_host(struct inccl_communicator *c, const float *src_host
     for (size_t off = 0; off < n && rc == 0; off += B, ++i) {
         const size_t cnt = (n - off) < B ? (n - off) : B;
         const int s = (int)(i & 1);
-        if (i >= 2) INCCL_HIP(hipStreamWaitEvent(h2d, ev_k[s], 0));      /* in[s] consumed */
-        INCCL_HIP(hipMemcpyAsync(in[s], src_host + off, cnt * sizeof(float), hipMemcpyHostToDevice, h2d));
-        INCCL_HIP(hipEventRecord(ev_h2d[s], h2d));
-        INCCL_HIP(hipStreamWaitEvent(ks, ev_h2d[s], 0));
+        if (i >= 2) LOOP_HIP(hipStreamWaitEvent(h2d, ev_k[s], 0));      /* in[s] consumed */
+        LOOP_HIP(hipMemcpyAsync(in[s], src_host + off, cnt * sizeof(float), hipMemcpyHostToDevice, h2d));
+        LOOP_HIP(hipEventRecord(ev_h2d[s], h2d));
+        LOOP_HIP(hipStreamWaitEvent(ks, ev_h2d[s], 0));
         if (i >= 2) {   /* out[s] drained */
             if (w) {   /* ev_d2h[s] holds chunk i-2's record only once the helper issued it */
                 const hipError_t e = inccl_d2h_wait_issued(w, base + i - 1);
@@ -1010,18 +1021,18 @@ int inccl_allreduce_f32_host(struct inccl_communicator *c, const float *src_host
                     break;
                 }
             }
-            INCCL_HIP(hipStreamWaitEvent(ks, ev_d2h[s], 0));
+            LOOP_HIP(hipStreamWaitEvent(ks, ev_d2h[s], 0));
         }
         const float *srcs[1] = {in[s]};
         rc = inccl_allreduce_f32(c, srcs, 1, out[s], cnt, scale_exp, ks);
         if (rc) break;
-        INCCL_HIP(hipEventRecord(ev_k[s], ks));
+        LOOP_HIP(hipEventRecord(ev_k[s], ks));
         if (w) {
             inccl_d2h_post(w, dst_host + off, out[s], cnt * sizeof(float), ev_k[s], ev_d2h[s], d2h);
         } else {
-            INCCL_HIP(hipStreamWaitEvent(d2h, ev_k[s], 0));
-            INCCL_HIP(hipMemcpyAsync(dst_host + off, out[s], cnt * sizeof(float), hipMemcpyDeviceToHost, d2h));
-            INCCL_HIP(hipEventRecord(ev_d2h[s], d2h));
+            LOOP_HIP(hipStreamWaitEvent(d2h, ev_k[s], 0));
+            LOOP_HIP(hipMemcpyAsync(dst_host + off, out[s], cnt * sizeof(float), hipMemcpyDeviceToHost, d2h));
+            LOOP_HIP(hipEventRecord(ev_d2h[s], d2h));
         }
     }
     if (w) {
