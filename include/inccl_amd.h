@@ -175,8 +175,10 @@ int inccl_allreduce_q32(struct inccl_communicator *comm, const int32_t *src_dev,
  * reference's ibv_reg_mr on its payload buffers (api.c:170-176).  It is pinned
  * (hipHostRegister) until inccl_host_deregister or communicator destroy, and
  * inccl_allreduce_write / _sendrecv whose src and dst both lie inside registered
- * ranges DMA them directly instead of staging them through the communicator's
- * pinned buffers (no host copies).  At most 16 ranges per communicator.
+ * ranges DMA them directly from pinned memory.  Unregistered memory is DMAed
+ * too, through HIP's pageable copies with the device-to-host copies issued from
+ * a helper thread ($INCCL_HOST_STAGING=pool: staging copies through the
+ * communicator's pinned buffers instead).  At most 16 ranges per communicator.
  * The memory must stay allocated while registered. */
 int inccl_host_register(struct inccl_communicator *comm, void *ptr, size_t bytes);
 int inccl_host_deregister(struct inccl_communicator *comm, void *ptr);

@@ -63,6 +63,33 @@ def test_host_example_binary(gpu, tmp_path):
         assert p.returncode == 0 and "result ok" in out, out + err
 
 
+def test_host_stress_binary(gpu, tmp_path):
+    """tests/c/host_stress.c through the C ABI alone: allreduce_write on pageable
+    and on registered memory and allreduce_f32_host on pageable memory, 5 pipeline
+    chunks plus a ragged tail, several calls -- world 1, two local ranks, and two
+    processes over the TCP rendezvous.  (tools/asan_host.sh runs the same program
+    under ASan + UBSan.)"""
+    exe = tmp_path / "host_stress"
+    subprocess.check_call(["gcc", "-O2", "-std=c11", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "c", "host_stress.c"), "-o", str(exe),
+                           "-L", os.path.join(ROOT, "container_inc_amd"), "-linccl_amd", "-lpthread",
+                           "-Wl,-rpath," + os.path.join(ROOT, "container_inc_amd")])
+    n = str((5 << 22) + 1000)
+    for world in (1, 2):
+        r = subprocess.run([str(exe), str(world), "local", "0", n, "2"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "result ok" in r.stdout, r.stdout + r.stderr
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, INCCL_MASTER_PORT=str(port), INCCL_DEVICE="0", INCCL_BOOT_TIMEOUT="120")
+    ps = [subprocess.Popen([str(exe), "2", "127.0.0.1", str(r), n, "2"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True, env=env) for r in range(2)]
+    outs = [p.communicate(timeout=300) for p in ps]
+    for p, (out, err) in zip(ps, outs):
+        assert p.returncode == 0 and "result ok" in out, out + err
+
+
 @pytest.mark.parametrize("variant", ["write", "sendrecv"])
 def test_allreduce_write_known_answer(gpu, variant):
     """host.c:20-25,41,47,51-55 with the reference's two ranks."""
@@ -87,7 +114,8 @@ def test_allreduce_write_known_answer(gpu, variant):
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_allreduce_write_random_ragged(gpu, orc, world):
     """Random int32 with wrap, len not a multiple of 1024: tail untouched (api.c:406),
-    small staging (comm size 16 KiB) so the pinned ping-pong path runs many chunks."""
+    with a small communicator (16 KiB; the reference sizes its registered buffers
+    from it, the direct DMA pipeline does not depend on it)."""
     from container_inc_amd import inccl
     n = 1024 * 37 + 500
     rng = np.random.default_rng(world)
@@ -112,8 +140,9 @@ def test_allreduce_write_random_ragged(gpu, orc, world):
 @pytest.mark.parametrize("world", [1, 2, 3])
 def test_allreduce_write_registered(gpu, orc, world):
     """Registered src/dst (the ibv_reg_mr analogue): direct DMA, several 16 MiB
-    chunks + a ragged tail, then the same arrays unregistered (staging path);
-    a partially registered call (dst only) also takes the staging path."""
+    chunks + a ragged tail, then the same arrays unregistered (pageable DMA with
+    the helper thread's D2Hs); a partially registered call (dst only) also takes
+    the pageable path."""
     from container_inc_amd import inccl
     n = 1024 * (4096 * 9 + 3) + 77          # 9 chunks of 16 MiB + 3 messages + a partial one
     m = n // 1024 * 1024
@@ -139,7 +168,7 @@ def test_allreduce_write_registered(gpu, orc, world):
         outs.append(dst.copy())
         comm.host_deregister(src)
         dst[:] = 5
-        comm.allreduce_write(src, n, dst)         # dst registered only -> staging
+        comm.allreduce_write(src, n, dst)         # dst registered only -> pageable path
         outs.append(dst.copy())
         comm.host_deregister(dst)
         with pytest.raises(RuntimeError):
