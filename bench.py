@@ -273,6 +273,12 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
             try:
                 comm.set_engine(eng)
                 got, same = run_verified(comm, eng, 1, inputs, out, k, st, refs)
+                # untimed calls first: an engine's buffers may just have been
+                # (re)allocated for this size, and the first passes over fresh
+                # memory run slow (launch_drift_probe.py)
+                for _ in range(max(3, iters // 2)):
+                    comm.allreduce_f32(inputs[0], out=out, scale_exp=k, stream=st.cuda_stream)
+                torch.cuda.synchronize()
                 dist.barrier()
                 t0 = time.perf_counter()
                 for _ in range(iters):

@@ -57,14 +57,20 @@ def main():
         comm.allreduce_f32(xs, out=out, scale_exp=25, stream=st.cuda_stream)
     torch.cuda.synchronize()
     comm.barrier()
+    per_call = []
     t0 = time.perf_counter()
     for _ in range(iters):
+        t1 = time.perf_counter()
         comm.allreduce_f32(xs, out=out, scale_exp=25, stream=st.cuda_stream)
+        if os.environ.get("PER_CALL"):   # host time of each call, synchronised
+            torch.cuda.synchronize()
+            per_call.append(round((time.perf_counter() - t1) * 1e3, 3))
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / iters
     comm.barrier()
     print(json.dumps({"rank": rank, "world": world, "engine": engine, "bucket_mib": mib, "R": 2,
-                      "ms_per_call": round(dt * 1e3, 4), "oracle_ok": ok}), flush=True)
+                      "ms_per_call": round(dt * 1e3, 4), "oracle_ok": ok,
+                      **({"per_call_ms": per_call} if per_call else {})}), flush=True)
     comm.destroy()
     grp.destroy()
 
