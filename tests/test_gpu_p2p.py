@@ -33,22 +33,29 @@ def _inputs(world, R, n, seed):
     return out
 
 
-def _rank_main(rank, world, port, cases, q, engine="p2p"):
+RCCL_ENGINES = ("rccl", "ar", "a2a")
+
+
+def _rank_main(rank, world, port, cases, q, engine="p2p", device=0):
     try:
-        os.environ["INCCL_ENGINE"] = engine
+        if engine not in RCCL_ENGINES:
+            os.environ["INCCL_ENGINE"] = engine
         if engine in ("p2p", "mesh", "meshw"):
             os.environ["INCCL_LL_MAX_BYTES"] = "0"   # the sharded exchange at every size
-        os.environ["INCCL_DEVICE"] = "0"
+        os.environ["INCCL_DEVICE"] = str(device)
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
         import sys
         sys.path.insert(0, ROOT)
         import torch
         from container_inc_amd import inccl
         from oracle import oracle as O
-        dev = torch.device("cuda:0")
-        grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port)
+        torch.cuda.set_device(device)
+        dev = torch.device("cuda", device)
+        grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=device)
         assert grp is not None, "group create failed"
         comm = inccl.inccl_communicator_create(grp, 0)
+        if engine in RCCL_ENGINES:
+            comm.set_engine(engine)   # needs a live multi-rank RCCL communicator (one GPU per rank)
         assert comm is not None and comm.engine == engine
         side = torch.cuda.Stream(device=dev)
         results = []
@@ -112,7 +119,8 @@ def _rank_main(rank, world, port, cases, q, engine="p2p"):
         # the IPC buffer kind: the ll / mesh kernels poll memory that peers write
         # over xGMI while they run, so it is fine-grained uncached; p2p's
         # buffers are only read after a kernel boundary and a barrier
-        results.append(comm.ipc_mem_kind(engine) == (0 if engine == "p2p" else 3))
+        if engine not in RCCL_ENGINES:
+            results.append(comm.ipc_mem_kind(engine) == (0 if engine == "p2p" else 3))
         comm.destroy()
         grp.destroy()
         q.put((rank, results, None))
@@ -147,6 +155,45 @@ def test_p2p_engine_multiprocess(gpu, world, engine):
     q = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_rank_main, args=(r, world, port, cases, q, engine)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, ok, err = q.get(timeout=240)
+            res[r] = (ok, err)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        ok, err = res[r]
+        assert err is None, f"rank {r}: {err}"
+        assert all(ok), f"rank {r}: {ok}"
+
+
+def _gpu_count():
+    import torch
+    return torch.cuda.device_count()   # does not initialise the GPU in this process
+
+
+@pytest.mark.parametrize("engine", ["rccl", "ar", "a2a", "p2p", "ll", "mesh", "meshw"])
+def test_engines_one_gpu_per_rank(gpu, engine):
+    """the multi-GPU paths with one process per GPU, as the
+    8-GPU bench runs them -- RCCL's reduce-scatter / all-gather, all-reduce and
+    grouped send/recv with more than one rank, and the IPC engines over real
+    xGMI -- every case bit-exact against the oracle.  World = every visible GPU
+    (at most 8); skipped on a one-GPU box, where RCCL refuses ranks sharing a
+    device and the tests above cover the IPC engines on one card."""
+    world = min(_gpu_count(), 8)
+    if world < 2:
+        pytest.skip("needs two or more GPUs (one process per GPU)")
+    cases = {"ll": LL_CASES, "mesh": MESH_CASES, "meshw": MESH_CASES}.get(engine, P2P_CASES)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, cases, q, engine, r)) for r in range(world)]
     for p in ps:
         p.start()
     res = {}
