@@ -298,19 +298,15 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     struct inccl_group *g = c->group;
     if (g->device < 0) return inccl_set_error(INCCL_ERR_STATE, "group has no device (bootstrap-only)");
     INCCL_HIP(hipSetDevice(g->device));
-    /* api.c:164 registers 2*size bytes per direction.  The staging here streams
-     * chunks of at most 16 MiB per ping-pong half (allreduce_host_q32), so the
-     * pinned buffers are capped at 32 MiB each (this also keeps 2*size from
+    /* api.c:164 registers 2*size bytes per direction.  Here those pinned
+     * buffers only serve the staged host pipeline ($INCCL_HOST_STAGING=pool),
+     * which allocates them on first use (ensure_staging); the default path DMAs
+     * the caller's memory directly.  The size still sets that pipeline's chunk,
+     * capped at 16 MiB per ping-pong half (this also keeps 2*size from
      * overflowing the 32-bit field for size >= 2 GiB). */
     const uint64_t want = 2ull * (uint64_t)size;
     c->payload_buf_size = (uint32_t)(want < (32ull << 20) ? want : (32ull << 20));
     c->window_size = WINDOW_SIZE;                /* api.c:226 */
-    if (c->payload_buf_size) {
-        INCCL_HIP(hipHostMalloc((void **)&c->send_payload, c->payload_buf_size, hipHostMallocDefault));
-        INCCL_HIP(hipHostMalloc((void **)&c->receive_payload, c->payload_buf_size, hipHostMallocDefault));
-        memset(c->send_payload, 0, c->payload_buf_size);      /* api.c:171-172 */
-        memset(c->receive_payload, 0, c->payload_buf_size);
-    }
     INCCL_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     INCCL_HIP(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
     /* The host paths' H2D and D2H streams are high-priority streams: those come
