@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     rank, world, port, engine = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
-    mib = int(sys.argv[5]) if len(sys.argv) > 5 else 256
+    mib = float(sys.argv[5]) if len(sys.argv) > 5 else 256.0   # fractions: 0.00390625 = 4 KiB
     iters = int(sys.argv[6]) if len(sys.argv) > 6 else 20
     os.environ.setdefault("INCCL_ENGINE", engine if engine in ("p2p", "mesh", "meshw") else "p2p")
     import numpy as np
@@ -30,7 +30,7 @@ def main():
     container_inc_amd.load()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(0)
-    n = mib << 18
+    n = max(64, int(mib * (1 << 18)))
     grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=0)
     if grp is None:
         raise SystemExit("group create failed")
