@@ -264,7 +264,8 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
         iters = 50 if b <= (1 << 20) else (10 if b <= (256 << 20) else 4)
         # the reference engine is the first that passes on every rank: RCCL, or
         # else the host-synchronised p2p exchange, before the in-kernel ll protocol
-        engines = ("rccl", "ar", "p2p", "ll") if b <= (1 << 20) else ("rccl", "ar", "a2a", "p2p", "mesh", "meshw")
+        engines = (("rccl", "ar", "p2p", "ll", "mesh", "meshw") if b <= (1 << 20)
+                   else ("rccl", "ar", "a2a", "p2p", "mesh", "meshw"))
         only = os.environ.get("INCCL_BENCH_SWEEP_ENGINES")   # debugging aid: a subset, in this order
         if only:
             engines = tuple(e for e in only.split(",") if e in engines)
