@@ -4,8 +4,8 @@
 // Peer buffers are mapped over HIP IPC.  Remote VRAM may be cached
 // non-coherently in this GPU's L2, and these kernels re-read the same peer
 // addresses on every call.  So every load of peer memory is a system-scope
-// `buffer_load_dwordx4 ... sc0 sc1`: coherent, L1-bypassing, and 0-3 % slower
-// than a plain 16-B load (MI355X_MICROARCH.md, load flavours).  The producers'
+// `buffer_load_dwordx4 ... sc0 sc1` (+ `nt` in the reduce): coherent and
+// L1-bypassing.  The producers'
 // stores are write-through (`sc1`, as the stream kernel's): they leave
 // the L2 at once and reach memory before the host barrier that separates the
 // phases, and nothing is left dirty for the kernel boundary to write back.
@@ -28,17 +28,26 @@ namespace {
 
 using namespace inccl_dev;
 
-constexpr int kAuxSys = 1 | 16;   // buffer instruction cache policy: sc0 | sc1
-constexpr int kAuxWT = 16;        // sc1: write-through store
+// Peer loads are system scope (sc0 sc1).  The pull-reduce's also carry the
+// nontemporal hint, which leaves the scope bits (and so coherence) unchanged:
+// 7.15 TB/s with it against 5.83 without on local HBM
+// (tools/tune/tune_peer.hip, profiles/r02/tune_peer.jsonl; W = 8: 6.31 vs 5.14),
+// 170 -> 115 us per call in the 2-rank one-GPU step.  The gather reads result
+// shards that were just written through to the Infinity Cache; there the hint
+// cost 147 -> 172 us, so its loads stay without it.
+constexpr int kAuxSys = 1 | 16;         // buffer instruction cache policy: sc0 | sc1
+constexpr int kAuxSysNT = 1 | 2 | 16;   // sc0 | nt | sc1
+constexpr int kAuxWT = 16;              // sc1: write-through store
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes)
 {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 
+template <int AUX = kAuxSys>
 __device__ __forceinline__ u32x4 ld_sys16(const void* tile_base, uint32_t tile_bytes, uint32_t off)
 {
-    return __builtin_amdgcn_raw_buffer_load_b128(rsrc(tile_base, tile_bytes), (int)off, 0, kAuxSys);
+    return __builtin_amdgcn_raw_buffer_load_b128(rsrc(tile_base, tile_bytes), (int)off, 0, AUX);
 }
 
 // DEQ = false: the int32 sum itself (the reference's int32 allreduce,
@@ -55,7 +64,7 @@ __global__ __launch_bounds__(BLOCK) void k_peer_reduce(SrcPtrs src, float* __res
         u32x4 v[R];
 #pragma unroll
         for (int r = 0; r < R; ++r)   // out-of-range lanes read 0 (buffer range check)
-            v[r] = ld_sys16(reinterpret_cast<const u32x4*>(src.p[r]) + base, tile_bytes, threadIdx.x * 16u);
+            v[r] = ld_sys16<kAuxSysNT>(reinterpret_cast<const u32x4*>(src.p[r]) + base, tile_bytes, threadIdx.x * 16u);
         if (i < n4) {
             u32x4 acc = v[0];
 #pragma unroll
