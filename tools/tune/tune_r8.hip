@@ -4,6 +4,7 @@
 // per lane, grid-stride depth, nontemporal vs plain loads; write-through stores
 // (the product's policy); a 9-stream memory-only reference.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I container_inc_amd/csrc tools/tune/tune_r8.hip -o tools/tune/tune_r8
+// (-DTUNE_R=1 -o tools/tune/tune_r1: the same sweep at R = 1)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -21,7 +22,10 @@ using namespace inccl_dev;
         }                                                                             \
     } while (0)
 
-constexpr int R = 8;
+#ifndef TUNE_R
+#define TUNE_R 8   // -DTUNE_R=1 for config 2's R = 1
+#endif
+constexpr int R = TUNE_R;
 
 __global__ void k_fill(float* p, int64_t n, uint32_t seed)
 {
