@@ -417,3 +417,82 @@ def test_host_path_multiprocess(gpu, world, engine):
         ok, err = res[r]
         assert err is None, f"rank {r}: {err}"
         assert all(ok.values()), f"rank {r}: {ok}"
+
+
+def _uneven_main(rank, world, port, q, engine, n, calls):
+    """Back-to-back calls on one stream with no host synchronisation, each rank
+    delaying its own kernels by a different random amount before every call
+    (a spinning kernel on the same stream), so the ranks arrive at each call's
+    flags unevenly; inputs rotate over three sets; every output is copied on
+    the stream right after its call and checked at the end."""
+    try:
+        os.environ["INCCL_ENGINE"] = engine
+        os.environ["INCCL_LL_MAX_BYTES"] = "0" if engine != "ll" else str(max(4 * n, 1 << 20))
+        os.environ["INCCL_DEVICE"] = "0"
+        os.environ["INCCL_BOOT_TIMEOUT"] = "120"
+        os.environ["INCCL_LL_TIMEOUT_MS"] = "5000"
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        from container_inc_amd import inccl
+        from oracle import oracle as O
+        dev = torch.device("cuda:0")
+        grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port)
+        assert grp is not None, "group create failed"
+        comm = inccl.inccl_communicator_create(grp, 0)
+        assert comm.engine == engine
+        sets = [_inputs(world, 2, n, 500 + 10 * s) for s in range(3)]
+        wants = [O.reduce_f32([x for per in xs for x in per], 24).view(np.uint32) for xs in sets]
+        srcs = [[torch.from_numpy(x).to(dev) for x in xs[rank]] for xs in sets]
+        out = torch.empty(n, device=dev)
+        hist = torch.empty((calls, n), device=dev)
+        st = torch.cuda.Stream(device=dev)
+        torch.cuda.synchronize()
+        comm.allreduce_f32(srcs[0], out=out, scale_exp=24, stream=st.cuda_stream)   # collective setup
+        torch.cuda.synchronize()
+        rng = np.random.default_rng(1234 + rank)
+        delays = rng.integers(0, 200_000, calls)   # GPU clock cycles: 0 to ~80 us
+        with torch.cuda.stream(st):
+            for i in range(calls):
+                if delays[i] > 20_000:
+                    torch.cuda._sleep(int(delays[i]))
+                comm.allreduce_f32(srcs[i % 3], out=out, scale_exp=24, stream=st.cuda_stream)
+                hist[i].copy_(out)
+        torch.cuda.synchronize()
+        got = hist.cpu().numpy().view(np.uint32)
+        bad = [i for i in range(calls) if not np.array_equal(got[i], wants[i % 3])]
+        comm.destroy()
+        grp.destroy()
+        q.put((rank, bad, None))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("engine,world,n", [("ll", 2, 65_536), ("ll", 3, 262_144), ("mesh", 3, 1 << 20),
+                                            ("meshw", 3, 1 << 20), ("mesh", 4, 300_001), ("p2p", 3, 1 << 20)])
+def test_engines_uneven_arrival(gpu, engine, world, n):
+    """The flag hand-offs under uneven load (MI355X_MICROARCH.md: "test every
+    hand-off under uneven load"): 48 back-to-back calls per rank, each rank's
+    kernels delayed by its own random 0-80 us before every call, three input
+    sets in rotation, every output bit-exact vs the oracle."""
+    calls = 48
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_uneven_main, args=(r, world, port, q, engine, n, calls)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, bad, err = q.get(timeout=240)
+            res[r] = (bad, err)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        bad, err = res[r]
+        assert err is None, f"rank {r}: {err}"
+        assert bad == [], f"rank {r}: wrong outputs at calls {bad}"
