@@ -43,6 +43,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+TUNE_CALLS = 10         # timed calls per engine candidate (after TUNE_CALLS / 2 untimed ones)
 
 
 def parse():
@@ -678,12 +679,15 @@ def main():
             try:
                 comm.set_engine(eng)
                 got, same = run_verified(comm, eng, ch, (srcs, srcs_b), out, k, stream, refs)
-                barrier()
-                t0 = time.perf_counter()
-                for _ in range(5):
+                for _ in range(TUNE_CALLS // 2):   # untimed: buffers just (re)allocated for this engine
                     comm.allreduce_f32(srcs, out=out, scale_exp=k, chunks=ch, stream=stream.cuda_stream)
                 torch.cuda.synchronize()
-                dt = time.perf_counter() - t0
+                barrier()
+                t0 = time.perf_counter()
+                for _ in range(TUNE_CALLS):
+                    comm.allreduce_f32(srcs, out=out, scale_exp=k, chunks=ch, stream=stream.cuda_stream)
+                torch.cuda.synchronize()
+                dt = (time.perf_counter() - t0) / TUNE_CALLS
             except Exception as e:  # noqa: BLE001
                 print(f"rank {rank}: engine {eng} chunks {ch} {env} failed: {e}", file=sys.stderr, flush=True)
                 ok = 0
@@ -695,10 +699,10 @@ def main():
                 refs = (got[0], got[1])
             if rank == 0:
                 print(f"tune {eng} chunks={ch} {env or ''}: ok={v[1] == 0.0} identical={v[2] == 0.0} "
-                      f"ms={v[0] * 200:.3f}", file=sys.stderr, flush=True)
+                      f"ms={v[0] * 1e3:.3f}", file=sys.stderr, flush=True)
             tuning.append({"engine": eng, "chunks": ch, "env": env or None, "ok": v[1] == 0.0,
                            "bit_identical": v[1] == 0.0 and v[2] == 0.0,
-                           "ms": round(v[0] * 200, 3) if v[1] == 0.0 else None})
+                           "ms": round(v[0] * 1e3, 3) if v[1] == 0.0 else None})
             if good and (best is None or v[0] < best[0]):
                 best = (v[0], eng, ch, env)
             del got
