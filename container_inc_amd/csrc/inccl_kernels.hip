@@ -20,10 +20,11 @@
 // Layout: each lane moves 16 B per access (global_load_dwordx4 = one 1 KiB
 // wave-instruction = exactly one reference packet payload of 256 lanes,
 // nts.c:55).  A workgroup of BLOCK lanes owns a tile of BLOCK*U float4 per
-// input and issues all R*U loads before touching them, then writes U
-// nontemporal float4 stores; BLOCK/U per R come from a measured sweep
-// (Geometry<R> in inccl_stream.h: U = 1, BLOCK = 512 or 1024).  One workgroup
-// per tile by default (a grid-stride loop covers a capped grid).
+// input and issues all R*U nontemporal loads before touching them, then writes
+// U write-through (sc1) float4 stores; BLOCK/U per R come from measured sweeps
+// (Geometry<R> in inccl_stream.h: 512 x 2 at R = 2, 512 x 1 at R = 3, 1024 x 1
+// otherwise).  One workgroup per tile by default (a grid-stride loop covers a
+// capped grid).
 //
 // The horizontal reductions (absmax for automatic scaling, the position
 // weighted checksum) use wave64 __shfl_xor trees, an LDS stage across the

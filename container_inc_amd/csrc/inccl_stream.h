@@ -80,11 +80,13 @@ __device__ __forceinline__ uint32_t store_xform(uint32_t acc, float inv)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Tile geometry per fan-in R, from the variant sweep on MI355X
-// (tools/tune/tune_stream.hip -> profiles/r01_tune_stream.jsonl, 2 x 256 MiB):
-// one float4 per lane per input (U = 1) beat deeper per-lane unrolling for
-// every R (e.g. R = 2: 6.96 TB/s at 512 x 1 vs 6.47 at 256 x 4); 512-lane
-// workgroups win at R = 2..3, 1024-lane ones at R = 1 and R >= 4.
+// Tile geometry per fan-in R, from the variant sweeps on MI355X.  Round 1
+// (nontemporal stores; tools/tune/tune_stream.hip -> profiles/r01_tune_stream.jsonl,
+// 2 x 256 MiB): one float4 per lane per input (U = 1) beat deeper per-lane
+// unrolling for every R (e.g. R = 2: 6.96 TB/s at 512 x 1 vs 6.47 at 256 x 4);
+// 512-lane workgroups win at R = 2..3, 1024-lane ones at R = 1 and R >= 4.
+// Round 2 re-ran them with write-through stores (below, and
+// profiles/r02/tune_stream_geometry_wt.jsonl, tune_r8.jsonl, tune_r1.jsonl).
 template <int R>
 struct Unroll {
     static constexpr int U = 1;
