@@ -327,6 +327,45 @@ def test_rccl_world1_paths(gpu, orc, force_rccl):
     grp.destroy()
 
 
+@pytest.mark.parametrize("engine,chunks", [("rccl", 1), ("rccl", 3), ("ar", 1), ("a2a", 1)])
+def test_rccl_world1_graph_capture(gpu, orc, force_rccl, engine, chunks):
+    """allreduce_f32 captured into a hipGraph (as a framework that graphs its
+    communication would) on the RCCL engines at world 1, including the chunked
+    pipeline's side stream: three captured calls, replayed with fresh inputs
+    each time, bit-exact vs the oracle."""
+    import torch
+    from container_inc_amd import inccl
+    grp = inccl.inccl_group_create(1, 0, "127.0.0.1")
+    comm = inccl.inccl_communicator_create(grp, 0)
+    comm.set_engine(engine)
+    n = (1 << 18) + 64
+    bufs = [torch.empty(n, device=gpu) for _ in range(2)]
+    outs = [torch.empty(n, device=gpu) for _ in range(3)]
+    st = torch.cuda.Stream(device=gpu)
+    comm.allreduce_f32(bufs, out=outs[0], scale_exp=24, chunks=chunks, stream=st.cuda_stream)   # workspaces sized eagerly
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=st):
+        for o in outs:
+            comm.allreduce_f32(bufs, out=o, scale_exp=24, chunks=chunks, stream=st.cuda_stream)
+    rng = np.random.default_rng(77)
+    for _ in range(3):
+        xs = [rng.standard_normal(n).astype(np.float32) for _ in range(2)]
+        for b, x in zip(bufs, xs):
+            b.copy_(torch.from_numpy(x))
+        for o in outs:
+            o.fill_(float("nan"))
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+        want = orc.reduce_f32(xs, 24).view(np.uint32)
+        for o in outs:
+            np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), want)
+    del graph
+    comm.destroy()
+    grp.destroy()
+
+
 def test_allreduce_f32_host_buckets(gpu, orc):
     """BASELINE config 3 shape (scaled down): host fp32 -> 3-stream pipeline -> host."""
     import torch
