@@ -58,9 +58,10 @@ def parse():
     p.add_argument("--engine", default="auto", choices=["auto", "rccl", "ar", "a2a", "p2p", "mesh", "meshw"],
                    help="N>1 exchange engine; auto = time every candidate during warmup, keep the fastest")
     p.add_argument("--no-sweep", action="store_true", help="N>1: skip the bucket-size sweep (BASELINE config 5)")
-    p.add_argument("--settle-seconds", type=float, default=0.1,
+    p.add_argument("--settle-seconds", type=float, default=1.0,
                    help="untimed steps before the W warmup steps, until this much wall time has passed: the first "
-                        "~100 launches over freshly allocated buckets run up to 2x slower (launch_drift_probe.py)")
+                        "launches over freshly allocated buckets run up to 2x slower, and the first process on a "
+                        "fresh box runs ~3%% slower for its first ~0.25 s of load (launch_drift_probe.py)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true",
