@@ -1,0 +1,100 @@
+"""PyTorch DDP communication hook over the INCCL engine -- the caller of this path.
+
+The reference's only caller is ``host.c:39-47``: it creates a group and a
+communicator, then calls ``inccl_allreduce_write`` on one int32 buffer.  In a
+training job the caller of a gradient-aggregation engine is the data-parallel
+wrapper, which hands over one flat fp32 gradient bucket at a time.  This module
+plugs the engine in there: ``DistributedDataParallel.register_comm_hook`` with
+:func:`allreduce_hook` sends every bucket through ``inccl_allreduce_f32``
+(quantise -> int32 sum across ranks -> dequantise; the int32 sum is the
+reference switch's aggregate, ``non_termination_switch.c:361-363``) and returns
+the bucket averaged over the ranks, as DDP's built-in allreduce hook does.
+
+Numerics: the scale defaults to ``SCALE_AUTO`` -- the bucket's absmax over every
+rank picks the largest exponent whose int32 sum cannot overflow
+(``orc_choose_scale``), so a bucket of any magnitude keeps ~30 significant bits
+of its largest element.  The averaged result is bit-identical to the oracle's
+``reduce_f32`` of the same buckets divided by the world size.
+
+Only fp32 CUDA buckets are accepted; anything else raises (no silent fallback
+to another collective).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+from . import inccl
+from ._lib import IncclError
+
+
+@dataclass
+class HookState:
+    """What :func:`allreduce_hook` needs: the communicator, the scale and
+    whether to average.  ``calls`` counts the buckets reduced (for tests and
+    logging)."""
+
+    comm: object
+    scale_exp: int = inccl.SCALE_AUTO
+    average: bool = True
+    calls: int = 0
+
+    @property
+    def world_size(self) -> int:
+        return self.comm.group.world_size
+
+
+def allreduce_hook(state: HookState, bucket):
+    """DDP comm hook: ``bucket.buffer()`` <- mean over ranks, through INCCL.
+
+    The collective is issued on the current stream (the stream DDP's backward
+    runs on), so the result is stream-ordered before DDP copies it back into
+    the parameters' ``.grad``; the returned future is already complete."""
+    import torch
+
+    buf = bucket.buffer()
+    if buf.dtype != torch.float32:
+        raise IncclError(f"inccl DDP hook: fp32 gradient buckets only, got {buf.dtype}")
+    # a CPU bucket reaches the communicator, which refuses it ("must live on the GPU")
+    stream = torch.cuda.current_stream(buf.device).cuda_stream if buf.is_cuda else None
+    state.comm.allreduce_f32([buf], out=buf, scale_exp=state.scale_exp, stream=stream)
+    w = state.world_size
+    if state.average and w > 1:
+        buf.div_(w)
+    state.calls += 1
+    fut = torch.futures.Future()
+    fut.set_result(buf)
+    return fut
+
+
+def communicator_from_env(port_offset: int = 17, device: int | None = None, engine: str | None = None):
+    """Create the INCCL group + communicator for this rank from the torchrun
+    environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT).  The
+    group's bootstrap listens on MASTER_PORT + ``port_offset`` so it does not
+    collide with torch.distributed's own store.  ``engine`` as in
+    ``Communicator.set_engine`` (default: the library's choice)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", "0"))
+    master = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ.get("MASTER_PORT", "29500")) + port_offset
+    grp = inccl.inccl_group_create(world, rank, master, port=port, device=device)
+    if grp is None:
+        from ._lib import load
+        raise IncclError("inccl_group_create failed: " + load().inccl_last_error().decode(errors="replace"))
+    comm = inccl.inccl_communicator_create(grp, 0)
+    if comm is None:
+        grp.destroy()
+        from ._lib import load
+        raise IncclError("inccl_communicator_create failed: " + load().inccl_last_error().decode(errors="replace"))
+    if engine:
+        comm.set_engine(engine)
+    return comm
+
+
+def register(ddp_model, comm, scale_exp: int = inccl.SCALE_AUTO, average: bool = True) -> HookState:
+    """Route every gradient bucket of ``ddp_model`` through ``comm``; returns the hook state."""
+    state = HookState(comm=comm, scale_exp=scale_exp, average=average)
+    ddp_model.register_comm_hook(state, allreduce_hook)
+    return state

@@ -1,0 +1,143 @@
+"""One rank of the DDP comm-hook tests (tests/test_ddp_hook.py, tests/test_gpu_ddp.py).
+
+A small MLP under DistributedDataParallel (gloo process group), a tiny bucket
+cap so the gradients travel in several buckets, and
+``container_inc_amd.ddp.allreduce_hook`` on every bucket.  Each rank reports:
+
+* ``buckets``: how many buckets the hook reduced per iteration;
+* ``bit_exact``: every hooked bucket equals the oracle's ``reduce_f32`` of all
+  ranks' buckets at ``choose_scale(absmax, W)``, divided by W (W = 2, 4: exact);
+* ``grad_err``: max |DDP grad - mean of the ranks' local grads| over the
+  quantisation bound of the bucket it travelled in (<= 1 expected).
+
+``mode`` "cpu": the communicator is :class:`GlooStandIn` (the engine's contract
+restated with the oracle over gloo), so the hook's plumbing is tested without a
+GPU.  ``mode`` "gpu": the real library on cuda:0 (every rank shares the card;
+engine p2p, because RCCL refuses two ranks on one GPU).
+"""
+import os
+import sys
+import types
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class GlooStandIn:
+    """CPU stand-in for ``inccl.Communicator.allreduce_f32`` (test infrastructure)."""
+
+    def __init__(self, world):
+        self.group = types.SimpleNamespace(world_size=world)
+
+    def allreduce_f32(self, srcs, out=None, scale_exp=25, chunks=1, stream=None):
+        import torch
+        import torch.distributed as dist
+        from container_inc_amd import inccl
+        from oracle import oracle as O
+        W = self.group.world_size
+        got = [torch.empty_like(srcs[0]) for _ in range(W)]
+        dist.all_gather(got, srcs[0].contiguous())
+        every = [g.numpy() for g in got]
+        k = O.choose_scale(O.absmax(every), W) if scale_exp == inccl.SCALE_AUTO else scale_exp
+        out.copy_(torch.from_numpy(O.reduce_f32(every, k)))
+        return out
+
+
+def run(rank, world, port, q, mode, iters=2):
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ["INCCL_BOOT_TIMEOUT"] = "120"
+        if mode == "gpu":
+            os.environ["INCCL_ENGINE"] = "p2p"
+        import torch
+        import torch.distributed as dist
+        from torch.nn.parallel import DistributedDataParallel as DDP
+
+        from container_inc_amd import ddp, inccl
+        from oracle import oracle as O
+
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        if mode == "gpu":
+            torch.cuda.set_device(0)
+            dev = torch.device("cuda", 0)
+            grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port + 1, device=0)
+            assert grp is not None, "group create failed"
+            comm = inccl.inccl_communicator_create(grp, 0)
+            assert comm is not None and comm.engine == "p2p", comm and comm.engine
+        else:
+            dev = torch.device("cpu")
+            comm = GlooStandIn(world)
+
+        torch.manual_seed(0)   # the same initial weights on every rank
+        model = torch.nn.Sequential(torch.nn.Linear(96, 512), torch.nn.Tanh(), torch.nn.Linear(512, 500),
+                                    torch.nn.Tanh(), torch.nn.Linear(500, 300), torch.nn.Tanh(),
+                                    torch.nn.Linear(300, 10)).to(dev)
+        import copy
+        local = copy.deepcopy(model)   # non-DDP twin: this rank's own gradients
+        net = DDP(model, device_ids=[0] if mode == "gpu" else None, bucket_cap_mb=0.25)
+        state = ddp.HookState(comm=comm)
+        seen = []
+
+        def hook(st, bucket):
+            before = bucket.buffer().detach().clone()
+            fut = ddp.allreduce_hook(st, bucket)
+            seen.append((before, bucket.buffer()))
+            return fut
+
+        net.register_comm_hook(state, hook)
+        opt = torch.optim.SGD(net.parameters(), lr=0.05)
+        opt_local = torch.optim.SGD(local.parameters(), lr=0.05)
+        report = {"buckets": [], "bit_exact": True, "grad_err": 0.0}
+        gen = torch.Generator().manual_seed(100 + rank)
+        for it in range(iters):
+            x = torch.randn(64, 96, generator=gen).to(dev)
+            y = torch.randn(64, 10, generator=gen).to(dev) * (10.0 ** it)   # later iterations: larger grads
+            seen.clear()
+            opt.zero_grad()
+            torch.nn.functional.mse_loss(net(x), y).backward()
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            report["buckets"].append(len(seen))
+            # every hooked bucket vs the oracle on all ranks' bucket inputs
+            for before, after in seen:
+                allb = [None] * world
+                dist.all_gather_object(allb, before.cpu().numpy().tobytes())
+                every = [np.frombuffer(b, np.float32) for b in allb]
+                k = O.choose_scale(O.absmax(every), world)
+                want = O.reduce_f32(every, k) / np.float32(world)
+                got = after.cpu().numpy()
+                if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+                    report["bit_exact"] = False
+            # DDP's averaged grads vs the mean of the ranks' local grads.  Bound per
+            # lane: W quantisation errors of 2^-(k+1) each, divided by W, at the
+            # smallest scale any bucket can have (k from the largest |grad| of all),
+            # plus the int32 -> fp32 rounding of the sum and the division (2^-23 rel)
+            opt_local.zero_grad()
+            torch.nn.functional.mse_loss(local(x), y).backward()
+            means, ddp_grads = [], []
+            for p, pl in zip(net.module.parameters(), local.parameters()):
+                g = pl.grad.detach().cpu().numpy().astype(np.float32)
+                allg = [None] * world
+                dist.all_gather_object(allg, g.tobytes())
+                stack = np.stack([np.frombuffer(b, np.float32).astype(np.float64) for b in allg])
+                means.append((stack.mean(axis=0), float(np.max(np.abs(stack)))))
+                ddp_grads.append(p.grad.detach().cpu().numpy().astype(np.float64).ravel())
+            k = O.choose_scale(np.float32(max(a for _, a in means)), world)
+            for (mean, _), got in zip(means, ddp_grads):
+                bound = 2.0 ** -(k + 1) + np.abs(mean) * 2.0 ** -23
+                report["grad_err"] = max(report["grad_err"], float(np.max(np.abs(got - mean) / bound)))
+            opt.step()
+            # the local twin follows the DDP model so the next iteration starts equal
+            with torch.no_grad():
+                for p, pl in zip(net.module.parameters(), local.parameters()):
+                    pl.copy_(p)
+        report["calls"] = state.calls
+        q.put((rank, report))
+        if mode == "gpu":
+            comm.destroy()
+            grp.destroy()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, {"error": repr(e), "tb": traceback.format_exc()}))

@@ -1,0 +1,22 @@
+"""DDP comm hook on the GPU (gpu): a small MLP under DistributedDataParallel
+with ``container_inc_amd.ddp.allreduce_hook`` on every gradient bucket, the
+real library underneath (p2p engine; every rank on cuda:0 of a one-GPU box).
+Every hooked bucket must equal the oracle's reduce_f32 of all ranks' buckets at
+the auto scale, divided by W, bit for bit; the parameters' ``.grad`` must sit
+within the quantisation bound of the ranks' mean gradient (tests/_ddp_rank.py)."""
+import pytest
+
+from test_ddp_hook import run_world
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ddp_hook_gpu(gpu, orc, world):
+    res = run_world(world, "gpu", 240)
+    for r, rep in res.items():
+        assert "error" not in rep, rep.get("tb")
+        assert rep["buckets"][-1] >= 2, rep
+        assert rep["calls"] == sum(rep["buckets"])
+        assert rep["bit_exact"], rep
+        assert rep["grad_err"] <= 1.0, rep

@@ -87,6 +87,19 @@ def _rank_main(rank, world, port, cases, q, engine="p2p", device=0):
             torch.cuda.synchronize()
             for o in outs:
                 results.append(bool(np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32))))
+        # in place, dst = srcs[0] (the DDP hook's call, container_inc_amd/ddp.py): a
+        # bucket inside the ll slot and one above it
+        for R, n, k, seed in ((1, 200_003, "auto", 41), (2, 1 << 20, 25, 42)):
+            xs = _inputs(world, R, n, seed)
+            every = [x for per in xs for x in per]
+            kk = O.choose_scale(O.absmax(every), world * R) if k == "auto" else k
+            want = O.reduce_f32(every, kk)
+            srcs = [torch.from_numpy(x).to(dev) for x in xs[rank]]
+            torch.cuda.synchronize()
+            comm.allreduce_f32(srcs, out=srcs[0], scale_exp=inccl.SCALE_AUTO if k == "auto" else k,
+                               stream=comm.stream)
+            torch.cuda.synchronize()
+            results.append(bool(np.array_equal(srcs[0].cpu().numpy().view(np.uint32), want.view(np.uint32))))
         if engine in ("ll", "mesh", "meshw"):
             # hipGraph: three calls captured once, replayed with fresh inputs (the
             # call counter lives on the device, so every replay is a new call)
