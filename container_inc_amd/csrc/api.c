@@ -129,6 +129,13 @@ int inccl_absmax_f32(const float *const *srcs_dev, int R, size_t n, uint32_t *am
     return kerr(inccl_k_absmax(srcs_dev, R, n, amax_bits_dev, zero_first, stream));
 }
 
+int inccl_absmax_bf16(const uint16_t *const *srcs_dev, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
+                      void *stream)
+{
+    if (!srcs_dev) return inccl_set_error(INCCL_ERR_ARG, "srcs is NULL");
+    return kerr(inccl_k_absmax_bf16(srcs_dev, R, n, amax_bits_dev, zero_first, stream));
+}
+
 int inccl_reduce_f32_auto(const float *const *srcs_dev, int R, float *dst_dev, size_t n, uint32_t *amax_word_dev,
                           void *stream)
 {
@@ -731,6 +738,79 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
     }
     /* `st` already waited on every side-stream chunk */
     return 0;
+}
+
+/* bfloat16 buckets: the fp32 path's arithmetic on the widened values.  The
+ * int32 partial sums travel as in the fp32 path (the switch's aggregate,
+ * nts.c:361-363); only the result's format differs, so the "rccl" engine's
+ * all-gather moves 2 bytes per element instead of 4. */
+int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev,
+                         size_t n, int scale_exp, void *stream)
+{
+    if (!c || !srcs_dev || R < 1 || R > INCCL_MAX_LOCAL_INPUTS || (!dst_dev && n))
+        return inccl_set_error(INCCL_ERR_ARG, "bad allreduce_bf16 args");
+    for (int r = 0; r < R; ++r)
+        if (!srcs_dev[r] && n) return inccl_set_error(INCCL_ERR_ARG, "srcs[%d] is NULL", r);
+    if (n == 0) return 0;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const int W = c->group->world_size, me = c->group->rank;
+    const void *const *srcs = (const void *const *)srcs_dev;
+    const uint32_t *amax = NULL;
+    if (scale_exp == INCCL_SCALE_AUTO) {
+        int rc = inccl_absmax_bf16(srcs_dev, R, n, c->d_words, 1, st);
+        if (rc) return rc;
+        if (W > 1) {
+            rc = inccl_tp_allreduce_max_u32(c, c->d_words, 1, st);
+            if (rc) return rc;
+        }
+        amax = c->d_words;
+    } else if (scale_exp < INCCL_SCALE_MIN || scale_exp > INCCL_SCALE_MAX) {
+        return inccl_set_error(INCCL_ERR_ARG, "scale_exp %d out of range", scale_exp);
+    }
+    const int k = amax ? 0 : scale_exp;
+    const int scale_R = R * W;
+    const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: RS/AG path even at world 1 */
+    if (W == 1 && !(fs && atoi(fs) != 0))   /* one fused HBM pass */
+        return kerr(inccl_k_stream(INCCL_KIND_BF16, INCCL_KIND_BF16, srcs, R, dst_dev, n, k, amax, scale_R, st));
+
+    if (c->engine == INCCL_ENGINE_RCCL || c->group->transport == INCCL_TRANSPORT_LOCAL) {
+        /* quant + local sum -> reduce-scatter (int32) -> dequantise own shard to
+         * bf16 -> all-gather (bf16), as allreduce_piece with a 2-byte result */
+        const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
+        int rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, (total + shard) * sizeof(int32_t));
+        if (rc) return rc;
+        const int in_place = (total == n);
+        if (!in_place) {
+            rc = inccl_ensure_dev(&c->d_f32, &c->d_f32_bytes, total * sizeof(uint16_t));
+            if (rc) return rc;
+        }
+        int32_t *qsend = (int32_t *)c->d_q32, *qrecv = qsend + total;
+        rc = kerr(inccl_k_stream(INCCL_KIND_BF16, INCCL_KIND_Q32, srcs, R, qsend, n, k, amax, scale_R, st));
+        if (rc) return rc;
+        if (total > n) INCCL_HIP(hipMemsetAsync(qsend + n, 0, (total - n) * sizeof(int32_t), st));
+        rc = inccl_tp_reduce_scatter_q32(c, qsend, qrecv, shard, st);
+        if (rc) return rc;
+        uint16_t *gather = in_place ? dst_dev : (uint16_t *)c->d_f32;
+        const size_t lo = (size_t)me * shard;
+        const void *s1[1] = {qrecv};
+        rc = kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_BF16, s1, 1, gather + lo, shard, k, amax, scale_R, st));
+        if (rc) return rc;
+        rc = inccl_tp_all_gather_bf16(c, gather + lo, gather, shard, st);
+        if (rc) return rc;
+        if (!in_place) INCCL_HIP(hipMemcpyAsync(dst_dev, gather, n * sizeof(uint16_t), hipMemcpyDeviceToDevice, st));
+        return 0;
+    }
+    /* every other engine: its int32 allreduce of the quantised partials
+     * (RCCL all-reduce for "ar" / "a2a", the p2p exchange for the IPC engines) */
+    int rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
+    if (rc) return rc;
+    int32_t *q = (int32_t *)c->d_q32;
+    rc = kerr(inccl_k_stream(INCCL_KIND_BF16, INCCL_KIND_Q32, srcs, R, q, n, k, amax, scale_R, st));
+    if (rc) return rc;
+    rc = inccl_tp_allreduce_q32(c, q, q, n, st);
+    if (rc) return rc;
+    const void *s1[1] = {q};
+    return kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_BF16, s1, 1, dst_dev, n, k, amax, scale_R, st));
 }
 
 /* ------------------------------------------------------------------ */

@@ -118,6 +118,8 @@ int inccl_tp_reduce_scatter_q32(struct inccl_communicator *c, const int32_t *sen
                                 hipStream_t st);
 int inccl_tp_all_gather_f32(struct inccl_communicator *c, const float *send, float *recv, size_t shard,
                             hipStream_t st);
+int inccl_tp_all_gather_bf16(struct inccl_communicator *c, const uint16_t *send, uint16_t *recv, size_t shard,
+                             hipStream_t st);
 int inccl_tp_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
                            hipStream_t st);
 int inccl_tp_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st);
@@ -130,6 +132,8 @@ int inccl_rccl_reduce_scatter_q32(struct inccl_communicator *c, const int32_t *s
                                   hipStream_t st);
 int inccl_rccl_all_gather_f32(struct inccl_communicator *c, const float *send, float *recv, size_t shard,
                               hipStream_t st);
+int inccl_rccl_all_gather_bf16(struct inccl_communicator *c, const uint16_t *send, uint16_t *recv, size_t shard,
+                               hipStream_t st);
 int inccl_rccl_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
                              hipStream_t st);
 int inccl_rccl_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, size_t n, hipStream_t st);

@@ -57,6 +57,117 @@ __global__ __launch_bounds__(kBlock) void k_stream_scalar(SrcPtrs src, void* __r
     }
 }
 
+// ---- bfloat16 buckets: 2-byte elements, 8 per 16-B lane access ------------
+// A bf16 value widens to fp32 exactly (its bits << 16), so quantisation is
+// quant1 of the widened value; the dequantised fp32 sum narrows with round to
+// nearest even.  The sums are finite (|(float)s * 2^-k| <= 2^95), so the
+// narrowing needs no NaN case.
+__device__ __forceinline__ uint32_t bf16_quant(uint32_t h, float scale) { return quant1(__uint_as_float(h << 16), scale); }
+
+__device__ __forceinline__ uint32_t bf16_rne(float f)
+{
+    const uint32_t b = __float_as_uint(f);
+    return (b + 0x7fffu + ((b >> 16) & 1u)) >> 16;
+}
+
+__device__ __forceinline__ uint32_t deq_bf16(uint32_t acc, float inv) { return bf16_rne((float)(int32_t)acc * inv); }
+
+// out = OUT(sum_r IN(src_r)) over 8-element groups; IN, OUT in {BF16, Q32},
+// not both Q32.  A workgroup owns BLOCK * U groups per tile; every load of the
+// tile is issued before the arithmetic; full tiles store write-through (sc1)
+// through a buffer resource as k_stream_vec does.
+template <int IN, int OUT, int R, int BLOCK, int U>
+__global__ __launch_bounds__(BLOCK) void k_stream16(SrcPtrs src, void* __restrict__ dst, int64_t n8, Scale sc)
+{
+    constexpr int VI = IN == BF16 ? 1 : 2;    // u32x4 per group per input
+    constexpr int VO = OUT == BF16 ? 1 : 2;   // u32x4 per group of output
+    const int k = resolve_k(sc);
+    const float scale = pow2f(k);
+    const float inv = pow2f(-k);
+    const int64_t tile = (int64_t)BLOCK * U;
+    u32x4* __restrict__ out = reinterpret_cast<u32x4*>(dst);
+
+    for (int64_t base = (int64_t)blockIdx.x * tile; base < n8; base += (int64_t)gridDim.x * tile) {
+        const bool full = base + tile <= n8;
+        u32x4 v[U][R][VI];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t g = base + threadIdx.x + (int64_t)u * BLOCK;
+            if (full || g < n8)
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int w = 0; w < VI; ++w)
+                        v[u][r][w] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src.p[r]) + g * VI + w);
+        }
+        __amdgpu_buffer_rsrc_t orsrc;
+        if (full) orsrc = __builtin_amdgcn_make_buffer_rsrc(out + base * VO, 0, (int)(tile * VO * 16), 0x00020000);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t g = base + threadIdx.x + (int64_t)u * BLOCK;
+            if (!full && g >= n8) continue;
+            uint32_t acc[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if constexpr (IN == BF16) {
+                    const u32x4 x = v[u][r][0];
+                    acc[0] += bf16_quant(x.x & 0xffffu, scale); acc[1] += bf16_quant(x.x >> 16, scale);
+                    acc[2] += bf16_quant(x.y & 0xffffu, scale); acc[3] += bf16_quant(x.y >> 16, scale);
+                    acc[4] += bf16_quant(x.z & 0xffffu, scale); acc[5] += bf16_quant(x.z >> 16, scale);
+                    acc[6] += bf16_quant(x.w & 0xffffu, scale); acc[7] += bf16_quant(x.w >> 16, scale);
+                } else {
+                    const u32x4 a = v[u][r][0], b = v[u][r][1];
+                    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+                    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+                }
+            }
+            u32x4 o[VO];
+            if constexpr (OUT == BF16) {
+                o[0].x = deq_bf16(acc[0], inv) | (deq_bf16(acc[1], inv) << 16);
+                o[0].y = deq_bf16(acc[2], inv) | (deq_bf16(acc[3], inv) << 16);
+                o[0].z = deq_bf16(acc[4], inv) | (deq_bf16(acc[5], inv) << 16);
+                o[0].w = deq_bf16(acc[6], inv) | (deq_bf16(acc[7], inv) << 16);
+            } else {
+                o[0] = u32x4{acc[0], acc[1], acc[2], acc[3]};
+                o[VO - 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
+            }
+#pragma unroll
+            for (int w = 0; w < VO; ++w) {
+                if (full)
+                    __builtin_amdgcn_raw_buffer_store_b128(o[w], orsrc,
+                                                           (int)(((threadIdx.x + u * BLOCK) * VO + w) * 16), 0, kAuxSc1);
+                else
+                    out[g * VO + w] = o[w];
+            }
+        }
+    }
+}
+
+// element-granular bf16 variant: the tail after the 8-element groups, or the
+// whole range when a pointer is not 16-B aligned
+template <int IN, int OUT, int R>
+__global__ __launch_bounds__(kBlock) void k_stream16_scalar(SrcPtrs src, void* __restrict__ dst, int64_t begin,
+                                                            int64_t n, Scale sc)
+{
+    const int k = resolve_k(sc);
+    const float scale = pow2f(k);
+    const float inv = pow2f(-k);
+    for (int64_t i = begin + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if constexpr (IN == BF16)
+                acc += bf16_quant(reinterpret_cast<const uint16_t*>(src.p[r])[i], scale);
+            else
+                acc += reinterpret_cast<const uint32_t*>(src.p[r])[i];
+        }
+        if constexpr (OUT == BF16)
+            reinterpret_cast<uint16_t*>(dst)[i] = (uint16_t)deq_bf16(acc, inv);
+        else
+            reinterpret_cast<uint32_t*>(dst)[i] = acc;
+    }
+}
+
 // ---- horizontal reductions: wave64 shuffle -> LDS -> one atomic per block ----
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 {
@@ -102,6 +213,46 @@ __global__ __launch_bounds__(kBlock) void k_absmax(SrcPtrs src, int64_t n, uint3
         const uint32_t* s = reinterpret_cast<const uint32_t*>(src.p[r]);
         for (int64_t i = (n4 << 2) + t0; i < n; i += stride) {
             const uint32_t a = abs_bits(s[i]);
+            m = m > a ? m : a;
+        }
+    }
+    m = wave_max_u32(m);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) part[wave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t b = part[0];
+#pragma unroll
+        for (int w = 1; w < kBlock / 64; ++w) b = b > part[w] ? b : part[w];
+        atomicMax(out, b);
+    }
+}
+
+// absmax over bf16 buckets, as the fp32 bits of the widened values
+__device__ __forceinline__ uint32_t abs_bits_bf16(uint32_t h) { return abs_bits(h << 16); }
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_absmax_bf16(SrcPtrs src, int64_t n, uint32_t* __restrict__ out)
+{
+    __shared__ uint32_t part[kBlock / 64];
+    uint32_t m = 0;
+    const int64_t n8 = n >> 3;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const u32x4* p = reinterpret_cast<const u32x4*>(src.p[r]);
+        for (int64_t i = t0; i < n8; i += stride) {
+            const u32x4 x = __builtin_nontemporal_load(p + i);
+            const uint32_t a = max(max(max(abs_bits_bf16(x.x & 0xffffu), abs_bits_bf16(x.x >> 16)),
+                                       max(abs_bits_bf16(x.y & 0xffffu), abs_bits_bf16(x.y >> 16))),
+                                   max(max(abs_bits_bf16(x.z & 0xffffu), abs_bits_bf16(x.z >> 16)),
+                                       max(abs_bits_bf16(x.w & 0xffffu), abs_bits_bf16(x.w >> 16))));
+            m = m > a ? m : a;
+        }
+        const uint16_t* s = reinterpret_cast<const uint16_t*>(src.p[r]);
+        for (int64_t i = (n8 << 3) + t0; i < n; i += stride) {
+            const uint32_t a = abs_bits_bf16(s[i]);
             m = m > a ? m : a;
         }
     }
@@ -222,9 +373,64 @@ int launch_stream(const void* const* srcs, int R, void* dst, int64_t n, const Sc
     }
 }
 
+// bf16 geometry: 512 lanes x 2 groups (16 KiB of bf16 input per workgroup and
+// input, as the fp32 R = 2 tile)
+constexpr int kB16Block = 512, kB16U = 2;
+
+template <int IN, int OUT, int R>
+int launch_stream16_R(const SrcPtrs& s, void* dst, int64_t n, const Scale& sc, hipStream_t st)
+{
+    bool vec = aligned16(dst);
+    for (int r = 0; r < R; ++r) vec = vec && aligned16(s.p[r]);
+    int64_t done = 0;
+    if (vec) {
+        const int64_t n8 = n >> 3;
+        if (n8 > 0) {
+            const int64_t tiles = (n8 + (int64_t)kB16Block * kB16U - 1) / ((int64_t)kB16Block * kB16U);
+            const int64_t cap = g_grid_cap > 0 ? g_grid_cap : (int64_t)0x7fffffff;
+            const int grid = (int)(tiles < cap ? tiles : cap);
+            hipLaunchKernelGGL((k_stream16<IN, OUT, R, kB16Block, kB16U>), dim3(grid), dim3(kB16Block), 0, st, s, dst,
+                               n8, sc);
+        }
+        done = n8 << 3;
+    }
+    if (done < n) {
+        const int64_t blocks = (n - done + kBlock - 1) / kBlock;
+        const int64_t cap = (int64_t)num_cus() * 8;
+        const int grid = (int)(blocks < cap ? blocks : cap);
+        hipLaunchKernelGGL((k_stream16_scalar<IN, OUT, R>), dim3(grid), dim3(kBlock), 0, st, s, dst, done, n, sc);
+    }
+    return (int)hipGetLastError();
+}
+
+template <int IN, int OUT>
+int launch_stream16(const void* const* srcs, int R, void* dst, int64_t n, const Scale& sc, hipStream_t st)
+{
+    if (R < 1 || R > kMaxR) return INCCL_ERR_ARG;
+    if (n <= 0) return 0;
+    SrcPtrs s = {};
+    for (int r = 0; r < R; ++r) {
+        if (srcs[r] == nullptr) return INCCL_ERR_ARG;
+        s.p[r] = srcs[r];
+    }
+    switch (R) {
+    case 1: return launch_stream16_R<IN, OUT, 1>(s, dst, n, sc, st);
+    case 2: return launch_stream16_R<IN, OUT, 2>(s, dst, n, sc, st);
+    case 3: return launch_stream16_R<IN, OUT, 3>(s, dst, n, sc, st);
+    case 4: return launch_stream16_R<IN, OUT, 4>(s, dst, n, sc, st);
+    case 5: return launch_stream16_R<IN, OUT, 5>(s, dst, n, sc, st);
+    case 6: return launch_stream16_R<IN, OUT, 6>(s, dst, n, sc, st);
+    case 7: return launch_stream16_R<IN, OUT, 7>(s, dst, n, sc, st);
+    default: return launch_stream16_R<IN, OUT, 8>(s, dst, n, sc, st);
+    }
+}
+
 int dispatch(int in_kind, int out_kind, const void* const* srcs, int R, void* dst, int64_t n, const Scale& sc,
              hipStream_t st)
 {
+    if (in_kind == BF16 && out_kind == BF16) return launch_stream16<BF16, BF16>(srcs, R, dst, n, sc, st);
+    if (in_kind == BF16 && out_kind == Q32) return launch_stream16<BF16, Q32>(srcs, R, dst, n, sc, st);
+    if (in_kind == Q32 && out_kind == BF16) return launch_stream16<Q32, BF16>(srcs, R, dst, n, sc, st);
 #define INCCL_CASE(I, O) \
     if (in_kind == I && out_kind == O) return launch_stream<I, O>(srcs, R, dst, n, sc, st);
     INCCL_CASE(F32, F32) INCCL_CASE(F32, Q32) INCCL_CASE(F32, Q32BE)
@@ -269,6 +475,33 @@ int inccl_k_absmax(const float* const* srcs, int R, size_t n, uint32_t* amax_bit
     switch (R) {
 #define INCCL_AM(RR) \
     case RR: hipLaunchKernelGGL((k_absmax<RR>), dim3(grid), dim3(kBlock), 0, st, s, (int64_t)n, amax_bits_dev); break;
+        INCCL_AM(1) INCCL_AM(2) INCCL_AM(3) INCCL_AM(4) INCCL_AM(5) INCCL_AM(6) INCCL_AM(7) INCCL_AM(8)
+#undef INCCL_AM
+    }
+    return (int)hipGetLastError();
+}
+
+int inccl_k_absmax_bf16(const uint16_t* const* srcs, int R, size_t n, uint32_t* amax_bits_dev, int zero_first,
+                        void* stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    if (R < 1 || R > kMaxR || amax_bits_dev == nullptr) return INCCL_ERR_ARG;
+    SrcPtrs s = {};
+    for (int r = 0; r < R; ++r) {
+        if (srcs[r] == nullptr || !aligned16(srcs[r])) return INCCL_ERR_ARG;
+        s.p[r] = srcs[r];
+    }
+    if (zero_first) {
+        hipError_t e = hipMemsetAsync(amax_bits_dev, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return (int)e;
+    }
+    if (n == 0) return 0;
+    const int64_t blocks = ((int64_t)(n >> 3) + kBlock - 1) / kBlock;
+    const int64_t cap = (int64_t)num_cus() * 8;
+    const int grid = (int)(blocks < 1 ? 1 : (blocks < cap ? blocks : cap));
+    switch (R) {
+#define INCCL_AM(RR) \
+    case RR: hipLaunchKernelGGL((k_absmax_bf16<RR>), dim3(grid), dim3(kBlock), 0, st, s, (int64_t)n, amax_bits_dev); break;
         INCCL_AM(1) INCCL_AM(2) INCCL_AM(3) INCCL_AM(4) INCCL_AM(5) INCCL_AM(6) INCCL_AM(7) INCCL_AM(8)
 #undef INCCL_AM
     }

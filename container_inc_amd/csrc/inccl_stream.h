@@ -15,7 +15,7 @@ namespace inccl_dev {
 constexpr int kBlock = 256;   // default workgroup size
 constexpr int kMaxR = INCCL_MAX_LOCAL_INPUTS;
 
-enum Kind { F32 = 0, Q32 = 1, Q32BE = 2 };
+enum Kind { F32 = 0, Q32 = 1, Q32BE = 2, BF16 = 3 };
 
 struct SrcPtrs {
     const void* p[kMaxR];

@@ -88,6 +88,12 @@ int inccl_rccl_all_gather_f32(struct inccl_communicator *c, const float *send, f
     return nccl_call(c, ncclAllGather(send, recv, shard, ncclFloat32, (ncclComm_t)c->nccl, st), "ncclAllGather");
 }
 
+int inccl_rccl_all_gather_bf16(struct inccl_communicator *c, const uint16_t *send, uint16_t *recv, size_t shard,
+                               hipStream_t st)
+{
+    return nccl_call(c, ncclAllGather(send, recv, shard, ncclBfloat16, (ncclComm_t)c->nccl, st), "ncclAllGather(bf16)");
+}
+
 int inccl_rccl_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
                              hipStream_t st)
 {
@@ -218,21 +224,28 @@ int inccl_local_reduce_scatter_q32(struct inccl_communicator *c, const int32_t *
     return rc ? inccl_set_error(INCCL_ERR_HIP, "local reduce-scatter kernel failed (%d)", rc) : rc2;
 }
 
-int inccl_local_all_gather_f32(struct inccl_communicator *c, const float *send, float *recv, size_t shard,
-                               hipStream_t st)
+/* shards of `esize`-byte elements */
+static int local_all_gather(struct inccl_communicator *c, const void *send, void *recv, size_t shard, size_t esize,
+                            hipStream_t st)
 {
     struct inccl_local_hub *h = c->group->hub;
     const int W = h->world_size;
     int rc = hub_publish(c, send, st);
     if (rc) return rc;
     for (int j = 0; j < W && rc == 0; ++j) {
-        float *d = recv + (size_t)j * shard;
+        char *d = (char *)recv + (size_t)j * shard * esize;
         if ((const void *)d == h->send[j]) continue;   /* in-place own shard */
-        hipError_t e = hipMemcpyAsync(d, h->send[j], shard * sizeof(float), hipMemcpyDeviceToDevice, st);
+        hipError_t e = hipMemcpyAsync(d, h->send[j], shard * esize, hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) rc = inccl_hip_check(e, "hipMemcpyAsync(all-gather)");
     }
     int rc2 = hub_release(c, st);
     return rc ? rc : rc2;
+}
+
+int inccl_local_all_gather_f32(struct inccl_communicator *c, const float *send, float *recv, size_t shard,
+                               hipStream_t st)
+{
+    return local_all_gather(c, send, recv, shard, sizeof(float), st);
 }
 
 int inccl_local_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
@@ -326,6 +339,19 @@ int inccl_tp_all_gather_f32(struct inccl_communicator *c, const float *send, flo
         return 0;
     }
     return inccl_rccl_all_gather_f32(c, send, recv, shard, st);
+}
+
+int inccl_tp_all_gather_bf16(struct inccl_communicator *c, const uint16_t *send, uint16_t *recv, size_t shard,
+                             hipStream_t st)
+{
+    if (is_local(c)) return local_all_gather(c, send, recv, shard, sizeof(uint16_t), st);
+    int rc = ensure_rccl(c);
+    if (rc) return rc;
+    if (!c->nccl) {
+        if (send != recv) INCCL_HIP(hipMemcpyAsync(recv, send, shard * 2, hipMemcpyDeviceToDevice, st));
+        return 0;
+    }
+    return inccl_rccl_all_gather_bf16(c, send, recv, shard, st);
 }
 
 int inccl_tp_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,

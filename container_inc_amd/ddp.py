@@ -16,8 +16,9 @@ rank picks the largest exponent whose int32 sum cannot overflow
 of its largest element.  The averaged result is bit-identical to the oracle's
 ``reduce_f32`` of the same buckets divided by the world size.
 
-Only fp32 CUDA buckets are accepted; anything else raises (no silent fallback
-to another collective).
+fp32 and bf16 CUDA buckets are accepted (bf16 through ``inccl_allreduce_bf16``:
+the same int32 sums, the result rounded to bf16, then divided by W in torch);
+anything else raises (no silent fallback to another collective).
 """
 from __future__ import annotations
 
@@ -53,11 +54,12 @@ def allreduce_hook(state: HookState, bucket):
     import torch
 
     buf = bucket.buffer()
-    if buf.dtype != torch.float32:
-        raise IncclError(f"inccl DDP hook: fp32 gradient buckets only, got {buf.dtype}")
+    if buf.dtype not in (torch.float32, torch.bfloat16):
+        raise IncclError(f"inccl DDP hook: fp32 or bf16 gradient buckets only, got {buf.dtype}")
     # a CPU bucket reaches the communicator, which refuses it ("must live on the GPU")
     stream = torch.cuda.current_stream(buf.device).cuda_stream if buf.is_cuda else None
-    state.comm.allreduce_f32([buf], out=buf, scale_exp=state.scale_exp, stream=stream)
+    reduce = state.comm.allreduce_f32 if buf.dtype == torch.float32 else state.comm.allreduce_bf16
+    reduce([buf], out=buf, scale_exp=state.scale_exp, stream=stream)
     w = state.world_size
     if state.average and w > 1:
         buf.div_(w)

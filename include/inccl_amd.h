@@ -49,6 +49,9 @@ extern "C" {
 #define INCCL_KIND_F32 0     /* fp32 gradient                                  */
 #define INCCL_KIND_Q32 1     /* int32, host byte order                         */
 #define INCCL_KIND_Q32BE 2   /* int32, big-endian wire word (api.c:301, util.c:404) */
+#define INCCL_KIND_BF16 3    /* bfloat16 gradient (2-byte elements): quantised as the fp32 it
+                                widens to exactly; dequantised as bf16_rne((float)s * 2^-k).
+                                Pairs: BF16->BF16, BF16->Q32, Q32->BF16 */
 
 const char *inccl_last_error(void);
 const char *inccl_version(void);
@@ -182,6 +185,19 @@ int inccl_allreduce_q32(struct inccl_communicator *comm, const int32_t *src_dev,
  * The memory must stay allocated while registered. */
 int inccl_host_register(struct inccl_communicator *comm, void *ptr, size_t bytes);
 int inccl_host_deregister(struct inccl_communicator *comm, void *ptr);
+
+/* bfloat16 buckets (uint16_t bit patterns), same arithmetic on the widened
+ * values: dst = bf16_rne( (float)( sum over ranks, sum over r<R  quant(srcs[r]) ) * 2^-k ).
+ * world == 1: one fused kernel, (R + 1) * 2 * n HBM bytes.  world > 1, engine
+ * "rccl": quant+local sum -> reduce-scatter (int32) -> dequantise own shard to
+ * bf16 -> all-gather (bf16, half the fp32 gather's bytes); every other engine:
+ * quant+local sum -> that engine's int32 allreduce -> dequantise.  dst may alias
+ * srcs[0]. */
+int inccl_allreduce_bf16(struct inccl_communicator *comm, const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev,
+                         size_t n, int scale_exp, void *stream);
+/* max |x| over R bf16 buckets into *amax_bits_dev (as fp32 bits; NaN ignored). */
+int inccl_absmax_bf16(const uint16_t *const *srcs_dev, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
+                      void *stream);
 
 /* Host-memory fp32 allreduce (BASELINE config 3): src/dst in host memory,
  * pipelined H2D / reduce / D2H over `bucket_bytes` buckets on three streams.

@@ -116,6 +116,64 @@ float orc_absmax_f32(const float *const *srcs, int R, size_t n)
     return m;
 }
 
+/* bfloat16: the top half of an fp32 word.  Widening is exact; narrowing rounds
+ * to nearest even (NaN kept quiet; the dequantised sums are always finite). */
+float orc_bf16_to_f32(uint16_t h)
+{
+    union { uint32_t u; float f; } c;
+    c.u = (uint32_t)h << 16;
+    return c.f;
+}
+
+uint16_t orc_f32_to_bf16(float f)
+{
+    union { uint32_t u; float f; } c;
+    c.f = f;
+    if (f != f) return (uint16_t)((c.u >> 16) | 0x40u);
+    const uint32_t lsb = (c.u >> 16) & 1u;
+    return (uint16_t)((c.u + 0x7fffu + lsb) >> 16);
+}
+
+void orc_reduce_bf16(const uint16_t *const *srcs, int R, uint16_t *dst, size_t n, int k)
+{
+    const float s = pow2f(-k);
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t acc = 0;
+        for (int r = 0; r < R; ++r) acc += (uint32_t)orc_quantise_one(orc_bf16_to_f32(srcs[r][i]), k);
+        dst[i] = orc_f32_to_bf16((float)(int32_t)acc * s);
+    }
+}
+
+void orc_quant_sum_bf16(const uint16_t *const *srcs, int R, int32_t *dst, size_t n, int k)
+{
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t acc = 0;
+        for (int r = 0; r < R; ++r) acc += (uint32_t)orc_quantise_one(orc_bf16_to_f32(srcs[r][i]), k);
+        dst[i] = (int32_t)acc;
+    }
+}
+
+void orc_sum_dequant_bf16(const int32_t *const *srcs, int R, uint16_t *dst, size_t n, int k)
+{
+    const float s = pow2f(-k);
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t acc = 0;
+        for (int r = 0; r < R; ++r) acc += (uint32_t)srcs[r][i];
+        dst[i] = orc_f32_to_bf16((float)(int32_t)acc * s);
+    }
+}
+
+float orc_absmax_bf16(const uint16_t *const *srcs, int R, size_t n)
+{
+    float m = 0.0f;
+    for (int r = 0; r < R; ++r)
+        for (size_t i = 0; i < n; ++i) {
+            float a = fabsf(orc_bf16_to_f32(srcs[r][i]));
+            if (a > m) m = a;
+        }
+    return m;
+}
+
 int orc_choose_scale(float absmax, int R)
 {
     if (!(absmax > 0.0f)) return ORC_SCALE_MAX;

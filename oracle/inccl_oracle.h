@@ -78,6 +78,14 @@ void orc_reduce_f32(const float *const *srcs, int R, float *dst, size_t n, int k
 void orc_quant_sum(const float *const *srcs, int R, int32_t *dst, size_t n, int k);
 /* max |x| over R buckets; NaN lanes ignored. */
 float orc_absmax_f32(const float *const *srcs, int R, size_t n);
+/* bfloat16 buckets (uint16_t bit patterns): quantise the exactly widened fp32
+ * value; dequantise to fp32 as above, then round to nearest even bf16 */
+float orc_bf16_to_f32(uint16_t h);
+uint16_t orc_f32_to_bf16(float f);
+void orc_reduce_bf16(const uint16_t *const *srcs, int R, uint16_t *dst, size_t n, int k);
+void orc_quant_sum_bf16(const uint16_t *const *srcs, int R, int32_t *dst, size_t n, int k);
+void orc_sum_dequant_bf16(const int32_t *const *srcs, int R, uint16_t *dst, size_t n, int k);
+float orc_absmax_bf16(const uint16_t *const *srcs, int R, size_t n);
 /* Largest k with R*absmax*2^k <= 2^30 (one bit of headroom), clamped to
  * [ORC_SCALE_MIN, ORC_SCALE_MAX]; absmax == 0 -> ORC_SCALE_MAX; Inf -> ORC_SCALE_MIN. */
 int   orc_choose_scale(float absmax, int R);

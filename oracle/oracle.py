@@ -51,6 +51,15 @@ def lib():
         L.orc_quant_sum.argtypes = [P, ctypes.c_int, P, sz, ctypes.c_int]
         L.orc_absmax_f32.argtypes = [P, ctypes.c_int, sz]
         L.orc_absmax_f32.restype = ctypes.c_float
+        L.orc_bf16_to_f32.argtypes = [ctypes.c_uint16]
+        L.orc_bf16_to_f32.restype = ctypes.c_float
+        L.orc_f32_to_bf16.argtypes = [ctypes.c_float]
+        L.orc_f32_to_bf16.restype = ctypes.c_uint16
+        L.orc_reduce_bf16.argtypes = [P, ctypes.c_int, P, sz, ctypes.c_int]
+        L.orc_quant_sum_bf16.argtypes = [P, ctypes.c_int, P, sz, ctypes.c_int]
+        L.orc_sum_dequant_bf16.argtypes = [P, ctypes.c_int, P, sz, ctypes.c_int]
+        L.orc_absmax_bf16.argtypes = [P, ctypes.c_int, sz]
+        L.orc_absmax_bf16.restype = ctypes.c_float
         L.orc_choose_scale.argtypes = [ctypes.c_float, ctypes.c_int]
         L.orc_choose_scale.restype = ctypes.c_int
         L.orc_checksum_q32.argtypes = [P, sz, ctypes.c_uint64]
@@ -134,6 +143,44 @@ def quant_sum(srcs, k: int) -> np.ndarray:
 def absmax(srcs) -> float:
     srcs = [np.ascontiguousarray(s, dtype=np.float32) for s in srcs]
     return float(lib().orc_absmax_f32(_ptr_array(srcs), len(srcs), srcs[0].size))
+
+
+# ---- bfloat16 buckets (uint16 bit patterns) ----
+def f32_to_bf16(x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32).ravel()
+    L = lib()
+    return np.array([L.orc_f32_to_bf16(float(v)) for v in x], np.uint16)
+
+
+def bf16_to_f32(h: np.ndarray) -> np.ndarray:
+    h = np.ascontiguousarray(h, dtype=np.uint16)
+    return (h.astype(np.uint32) << 16).view(np.float32)
+
+
+def reduce_bf16(srcs, k: int) -> np.ndarray:
+    srcs = [np.ascontiguousarray(s, dtype=np.uint16) for s in srcs]
+    out = np.empty(srcs[0].shape, np.uint16)
+    lib().orc_reduce_bf16(_ptr_array(srcs), len(srcs), _p(out), out.size, int(k))
+    return out
+
+
+def quant_sum_bf16(srcs, k: int) -> np.ndarray:
+    srcs = [np.ascontiguousarray(s, dtype=np.uint16) for s in srcs]
+    out = np.empty(srcs[0].shape, np.int32)
+    lib().orc_quant_sum_bf16(_ptr_array(srcs), len(srcs), _p(out), out.size, int(k))
+    return out
+
+
+def sum_dequant_bf16(srcs, k: int) -> np.ndarray:
+    srcs = [np.ascontiguousarray(s, dtype=np.int32) for s in srcs]
+    out = np.empty(srcs[0].shape, np.uint16)
+    lib().orc_sum_dequant_bf16(_ptr_array(srcs), len(srcs), _p(out), out.size, int(k))
+    return out
+
+
+def absmax_bf16(srcs) -> float:
+    srcs = [np.ascontiguousarray(s, dtype=np.uint16) for s in srcs]
+    return float(lib().orc_absmax_bf16(_ptr_array(srcs), len(srcs), srcs[0].size))
 
 
 def choose_scale(amax: float, R: int) -> int:

@@ -52,7 +52,7 @@ def test_ddp_hook_refuses_non_fp32():
 
     class Bucket:
         def buffer(self):
-            return torch.zeros(8, dtype=torch.float16)
+            return torch.zeros(8, dtype=torch.float16)   # neither fp32 nor bf16
 
     with pytest.raises(IncclError):
         ddp.allreduce_hook(ddp.HookState(comm=None), Bucket())
