@@ -28,6 +28,7 @@ Extra JSON fields:
   host_e2e          N = 1: BASELINE config 3, 1 GiB pinned host fp32 in 64 MiB buckets
   api_allreduce_write N = 1: the reference's entry point on a 256 MiB host int32
                     message, registered and unregistered
+  bf16              N = 1: R bf16 buckets of 256 MiB (k_stream16), repeated and rotated
   sweep             N > 1: 4 KiB .. 256 MiB and 1 GiB per engine, verified with
                     alternating input sets
 """
@@ -442,6 +443,39 @@ def r_variants(dev, k: int, n: int, rs=(1, 8)) -> list:
         del groups
         torch.cuda.empty_cache()
     return rows
+
+
+def bf16_buckets(dev, R: int, k: int, mib: int = 256) -> dict:
+    """bfloat16 gradient buckets (inccl_reduce_bf16 = k_stream16<BF16,BF16,R>): R
+    resident `mib` MiB bf16 buckets, repeated and rotated through two sets.
+    Algorithmic bytes (R + 1) * 2 * n.  Parity: tests/test_gpu_bf16.py."""
+    import torch
+
+    from container_inc_amd import inccl
+    n = mib * (1 << 20) // 2
+    st = torch.cuda.Stream(device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(4000)
+    groups = [([torch.randn(n, generator=gen, device=dev).to(torch.bfloat16) for _ in range(R)],
+               torch.empty(n, device=dev, dtype=torch.bfloat16)) for _ in range(2)]
+    torch.cuda.synchronize()
+    hot = kernel_time_ms(lambda: inccl.reduce_bf16(groups[0][0], k, out=groups[0][1], stream=st.cuda_stream), st, 40)
+    it = [0]
+
+    def rotated():
+        xs, out = groups[it[0] % 2]
+        it[0] += 1
+        inccl.reduce_bf16(xs, k, out=out, stream=st.cuda_stream)
+
+    cold = kernel_time_ms(rotated, st, 40)
+    alg = (R + 1) * 2 * n
+    del groups
+    torch.cuda.empty_cache()
+    return {"R": R, "bucket_mib": mib, "elems": n, "kernel_us": round(hot * 1e3, 2),
+            "GBps_buckets": round(R * 2 * n / (hot * 1e-3) / 1e9, 1),
+            "hbm_frac": round(alg / (hot * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "rotated_kernel_us": round(cold * 1e3, 2),
+            "rotated_hbm_frac": round(alg / (cold * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def api_allreduce_write(comm, mib: int = 256, calls: int = 7) -> dict:
@@ -876,6 +910,7 @@ def main():
         extra("roofline_cold", lambda: cold_run(dev, R, k, n))
         extra("r_variants", lambda: r_variants(dev, k, n))
         extra("numerics_vs_exact", lambda: numerics_vs_exact(dev, n))
+        extra("bf16", lambda: bf16_buckets(dev, R, k))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         extra("cpu_baseline", lambda: cpu_baseline(n, R, k, a.cpu_seconds))
         extra("cpu_baseline_allcores", lambda: cpu_baseline_allcores(n, R, k, min(a.cpu_seconds, 5.0)))
