@@ -56,3 +56,61 @@ def test_bf16_known_answers(orc):
     srcs = [np.array([a, mhalf, one], np.uint16), np.array([b, half, tiny], np.uint16)]
     got = orc.reduce_bf16(srcs, 10)
     np.testing.assert_array_equal(orc.bf16_to_f32(got), np.array([3.75, 0.0, 1.0], np.float32))
+
+
+def _gloo_bf16_rank(rank, world, port, n, R, k, q):
+    """inccl_allreduce_bf16's "rccl" decomposition over gloo: quant + local sum ->
+    reduce-scatter int32 (by exchange) -> dequantise own shard to bf16 ->
+    all-gather bf16, against reduce_bf16 of every rank's buckets."""
+    try:
+        _gloo_bf16_body(rank, world, port, n, R, k, q)
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def _gloo_bf16_body(rank, world, port, n, R, k, q):
+    import sys
+
+    from conftest import ROOT
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    from container_inc_amd.plan import shard_elems
+    from oracle import oracle as O
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    rng = np.random.default_rng(500 + rank)
+    hs = [_random_bf16(rng, n, 2.0) for _ in range(R)]
+    shard = shard_elems(n, world)
+    part = np.zeros(shard * world, np.int32)
+    part[:n] = O.quant_sum_bf16(hs, k)
+    got = [torch.zeros(shard * world, dtype=torch.int32) for _ in range(world)]
+    dist.all_gather(got, torch.from_numpy(part))
+    mine = O.sum_dequant_bf16([g[rank * shard:(rank + 1) * shard].numpy() for g in got], k)
+    # gloo has no 16-bit integer type: the bf16 bit patterns travel widened
+    shards = [torch.zeros(shard, dtype=torch.int32) for _ in range(world)]
+    dist.all_gather(shards, torch.from_numpy(mine.astype(np.int32)))
+    out = torch.cat(shards).numpy().astype(np.uint16)[:n]
+    allh = [None] * world
+    dist.all_gather_object(allh, [h.tobytes() for h in hs])
+    every = [np.frombuffer(b, np.uint16) for per in allh for b in per]
+    q.put((rank, bool(np.array_equal(out, O.reduce_bf16(every, k)))))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bf16_decomposition(orc):
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_bf16_rank, args=(r, 2, port, 10_007, 2, 24, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
