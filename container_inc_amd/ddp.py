@@ -56,10 +56,21 @@ def allreduce_hook(state: HookState, bucket):
     buf = bucket.buffer()
     if buf.dtype not in (torch.float32, torch.bfloat16):
         raise IncclError(f"inccl DDP hook: fp32 or bf16 gradient buckets only, got {buf.dtype}")
-    # a CPU bucket reaches the communicator, which refuses it ("must live on the GPU")
-    stream = torch.cuda.current_stream(buf.device).cuda_stream if buf.is_cuda else None
     reduce = state.comm.allreduce_f32 if buf.dtype == torch.float32 else state.comm.allreduce_bf16
-    reduce([buf], out=buf, scale_exp=state.scale_exp, stream=stream)
+    if not buf.is_cuda:   # reaches the communicator, which refuses it ("must live on the GPU")
+        reduce([buf], out=buf, scale_exp=state.scale_exp, stream=None)
+    else:
+        cur = torch.cuda.current_stream(buf.device)
+        if cur.cuda_stream:
+            reduce([buf], out=buf, scale_exp=state.scale_exp, stream=cur.cuda_stream)
+        else:
+            # backward on the legacy null stream: the C ABI reads a NULL stream as
+            # "the communicator's own stream", so order that stream explicitly
+            # after the gradient producers and before DDP's copy-back
+            side = torch.cuda.ExternalStream(state.comm.stream, device=buf.device)
+            side.wait_stream(cur)
+            reduce([buf], out=buf, scale_exp=state.scale_exp, stream=side.cuda_stream)
+            cur.wait_stream(side)
     w = state.world_size
     if state.average and w > 1:
         buf.div_(w)
