@@ -58,19 +58,34 @@ __global__ __launch_bounds__(kBlock) void k_stream_scalar(SrcPtrs src, void* __r
 }
 
 // ---- bfloat16 buckets: 2-byte elements, 8 per 16-B lane access ------------
-// A bf16 value widens to fp32 exactly (its bits << 16), so quantisation is
-// quant1 of the widened value; the dequantised fp32 sum narrows with round to
-// nearest even.  The sums are finite (|(float)s * 2^-k| <= 2^95), so the
-// narrowing needs no NaN case.
-__device__ __forceinline__ uint32_t bf16_quant(uint32_t h, float scale) { return quant1(__uint_as_float(h << 16), scale); }
+// A bf16 value widens to fp32 exactly (its bits << 16), so quantisation is the
+// fp32 rule on the widened value; the dequantised fp32 sum narrows with round to
+// nearest even.  Twice the elements per byte of the fp32 path, so the VALU work
+// per byte doubles: the fp32 path's compare/select form of quant1 (8 VALU ops
+// an element) would leave this kernel issue-bound, so here
+//  * quantise = v_mul, v_rndne, v_cvt_i32_f32: the conversion itself saturates
+//    to [INT32_MIN, INT32_MAX] and maps NaN to 0, which is exactly the spec
+//    (orc_quantise_one) -- 3 ops;
+//  * narrowing = gfx950's v_cvt_pk_bf16_f32 (round to nearest even), one op per
+//    pair.  The sums are finite (|(float)s * 2^-k| <= 2^95): no NaN or overflow case.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ uint32_t bf16_rne(float f)
+__device__ __forceinline__ uint32_t quant_sat(float y)
 {
-    const uint32_t b = __float_as_uint(f);
-    return (b + 0x7fffu + ((b >> 16) & 1u)) >> 16;
+    const float r = __builtin_rintf(y);
+    int32_t q;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(q) : "v"(r));
+    return (uint32_t)q;
 }
 
-__device__ __forceinline__ uint32_t deq_bf16(uint32_t acc, float inv) { return bf16_rne((float)(int32_t)acc * inv); }
+__device__ __forceinline__ uint32_t bf16_quant(uint32_t h, float scale) { return quant_sat(__uint_as_float(h << 16) * scale); }
+
+__device__ __forceinline__ uint32_t deq_bf16x2(uint32_t a, uint32_t b, float inv)
+{
+    const f32x2 f = {(float)(int32_t)a * inv, (float)(int32_t)b * inv};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2));
+}
 
 // out = OUT(sum_r IN(src_r)) over 8-element groups; IN, OUT in {BF16, Q32},
 // not both Q32.  A workgroup owns BLOCK * U groups per tile; every load of the
@@ -123,10 +138,10 @@ __global__ __launch_bounds__(BLOCK) void k_stream16(SrcPtrs src, void* __restric
             }
             u32x4 o[VO];
             if constexpr (OUT == BF16) {
-                o[0].x = deq_bf16(acc[0], inv) | (deq_bf16(acc[1], inv) << 16);
-                o[0].y = deq_bf16(acc[2], inv) | (deq_bf16(acc[3], inv) << 16);
-                o[0].z = deq_bf16(acc[4], inv) | (deq_bf16(acc[5], inv) << 16);
-                o[0].w = deq_bf16(acc[6], inv) | (deq_bf16(acc[7], inv) << 16);
+                o[0].x = deq_bf16x2(acc[0], acc[1], inv);
+                o[0].y = deq_bf16x2(acc[2], acc[3], inv);
+                o[0].z = deq_bf16x2(acc[4], acc[5], inv);
+                o[0].w = deq_bf16x2(acc[6], acc[7], inv);
             } else {
                 o[0] = u32x4{acc[0], acc[1], acc[2], acc[3]};
                 o[VO - 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
@@ -162,7 +177,7 @@ __global__ __launch_bounds__(kBlock) void k_stream16_scalar(SrcPtrs src, void* _
                 acc += reinterpret_cast<const uint32_t*>(src.p[r])[i];
         }
         if constexpr (OUT == BF16)
-            reinterpret_cast<uint16_t*>(dst)[i] = (uint16_t)deq_bf16(acc, inv);
+            reinterpret_cast<uint16_t*>(dst)[i] = (uint16_t)deq_bf16x2(acc, 0u, inv);
         else
             reinterpret_cast<uint32_t*>(dst)[i] = acc;
     }
