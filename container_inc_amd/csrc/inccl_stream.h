@@ -187,6 +187,107 @@ __global__ __launch_bounds__(BLOCK) void k_stream_vec(SrcPtrs src, void* __restr
     }
 }
 
+// ---- bfloat16 buckets: 2-byte elements, 8 per 16-B lane access ------------
+// A bf16 value widens to fp32 exactly (its bits << 16), so quantisation is the
+// fp32 rule on the widened value; the dequantised fp32 sum narrows with round to
+// nearest even.  Twice the elements per byte of the fp32 path, so the VALU work
+// per byte doubles: the fp32 path's compare/select form of quant1 (8 VALU ops
+// an element) would leave this kernel issue-bound, so here
+//  * quantise = v_mul, v_rndne, v_cvt_i32_f32: the conversion itself saturates
+//    to [INT32_MIN, INT32_MAX] and maps NaN to 0, which is exactly the spec
+//    (orc_quantise_one) -- 3 ops;
+//  * narrowing = gfx950's v_cvt_pk_bf16_f32 (round to nearest even), one op per
+//    pair.  The sums are finite (|(float)s * 2^-k| <= 2^95): no NaN or overflow case.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t quant_sat(float y)
+{
+    const float r = __builtin_rintf(y);
+    int32_t q;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(q) : "v"(r));
+    return (uint32_t)q;
+}
+
+__device__ __forceinline__ uint32_t bf16_quant(uint32_t h, float scale) { return quant_sat(__uint_as_float(h << 16) * scale); }
+
+__device__ __forceinline__ uint32_t deq_bf16x2(uint32_t a, uint32_t b, float inv)
+{
+    const f32x2 f = {(float)(int32_t)a * inv, (float)(int32_t)b * inv};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2));
+}
+
+// out = OUT(sum_r IN(src_r)) over 8-element groups; IN, OUT in {BF16, Q32},
+// not both Q32.  A workgroup owns BLOCK * U groups per tile; every load of the
+// tile is issued before the arithmetic; full tiles store write-through (sc1)
+// through a buffer resource as k_stream_vec does.
+template <int IN, int OUT, int R, int BLOCK, int U>
+__global__ __launch_bounds__(BLOCK) void k_stream16(SrcPtrs src, void* __restrict__ dst, int64_t n8, Scale sc)
+{
+    constexpr int VI = IN == BF16 ? 1 : 2;    // u32x4 per group per input
+    constexpr int VO = OUT == BF16 ? 1 : 2;   // u32x4 per group of output
+    const int k = resolve_k(sc);
+    const float scale = pow2f(k);
+    const float inv = pow2f(-k);
+    const int64_t tile = (int64_t)BLOCK * U;
+    u32x4* __restrict__ out = reinterpret_cast<u32x4*>(dst);
+
+    for (int64_t base = (int64_t)blockIdx.x * tile; base < n8; base += (int64_t)gridDim.x * tile) {
+        const bool full = base + tile <= n8;
+        u32x4 v[U][R][VI];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t g = base + threadIdx.x + (int64_t)u * BLOCK;
+            if (full || g < n8)
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int w = 0; w < VI; ++w)
+                        v[u][r][w] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src.p[r]) + g * VI + w);
+        }
+        __amdgpu_buffer_rsrc_t orsrc;
+        if (full) orsrc = __builtin_amdgcn_make_buffer_rsrc(out + base * VO, 0, (int)(tile * VO * 16), 0x00020000);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t g = base + threadIdx.x + (int64_t)u * BLOCK;
+            if (!full && g >= n8) continue;
+            uint32_t acc[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if constexpr (IN == BF16) {
+                    const u32x4 x = v[u][r][0];
+                    acc[0] += bf16_quant(x.x & 0xffffu, scale); acc[1] += bf16_quant(x.x >> 16, scale);
+                    acc[2] += bf16_quant(x.y & 0xffffu, scale); acc[3] += bf16_quant(x.y >> 16, scale);
+                    acc[4] += bf16_quant(x.z & 0xffffu, scale); acc[5] += bf16_quant(x.z >> 16, scale);
+                    acc[6] += bf16_quant(x.w & 0xffffu, scale); acc[7] += bf16_quant(x.w >> 16, scale);
+                } else {
+                    const u32x4 a = v[u][r][0], b = v[u][r][1];
+                    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+                    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+                }
+            }
+            u32x4 o[VO];
+            if constexpr (OUT == BF16) {
+                o[0].x = deq_bf16x2(acc[0], acc[1], inv);
+                o[0].y = deq_bf16x2(acc[2], acc[3], inv);
+                o[0].z = deq_bf16x2(acc[4], acc[5], inv);
+                o[0].w = deq_bf16x2(acc[6], acc[7], inv);
+            } else {
+                o[0] = u32x4{acc[0], acc[1], acc[2], acc[3]};
+                o[VO - 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
+            }
+#pragma unroll
+            for (int w = 0; w < VO; ++w) {
+                if (full)
+                    __builtin_amdgcn_raw_buffer_store_b128(o[w], orsrc,
+                                                           (int)(((threadIdx.x + u * BLOCK) * VO + w) * 16), 0, kAuxSc1);
+                else
+                    out[g * VO + w] = o[w];
+            }
+        }
+    }
+}
+
 }  // namespace inccl_dev
 
 #endif
