@@ -290,9 +290,17 @@ int launch_stream(const void* const* srcs, int R, void* dst, int64_t n, const Sc
     }
 }
 
-// bf16 geometry: 512 lanes x 2 groups (16 KiB of bf16 input per workgroup and
-// input, as the fp32 R = 2 tile)
-constexpr int kB16Block = 512, kB16U = 2;
+// bf16 geometry per R, from tools/tune/tune_bf16.hip on MI355X (256 MiB bf16
+// buckets, profiles/r02/tune_bf16.jsonl): R <= 2 -> 512 lanes x 1 group
+// (R = 2: 0.89-0.90 of HBM repeated, 0.80-0.81 rotated, against 0.88-0.89 /
+// 0.79 at 512 x 2); R >= 3 -> 256 x 2 (R = 8: 0.79 / 0.74; 512 x 1 drops to 0.72
+// rotated).  A memory-only kernel of the same access pattern reaches 0.86 / 0.78
+// at R = 2: the arithmetic is hidden.
+template <int R>
+struct B16Geometry {
+    static constexpr int BLOCK = R <= 2 ? 512 : 256;
+    static constexpr int U = R <= 2 ? 1 : 2;
+};
 
 template <int IN, int OUT, int R>
 int launch_stream16_R(const SrcPtrs& s, void* dst, int64_t n, const Scale& sc, hipStream_t st)
@@ -303,11 +311,11 @@ int launch_stream16_R(const SrcPtrs& s, void* dst, int64_t n, const Scale& sc, h
     if (vec) {
         const int64_t n8 = n >> 3;
         if (n8 > 0) {
-            const int64_t tiles = (n8 + (int64_t)kB16Block * kB16U - 1) / ((int64_t)kB16Block * kB16U);
+            constexpr int B = B16Geometry<R>::BLOCK, U = B16Geometry<R>::U;
+            const int64_t tiles = (n8 + (int64_t)B * U - 1) / ((int64_t)B * U);
             const int64_t cap = g_grid_cap > 0 ? g_grid_cap : (int64_t)0x7fffffff;
             const int grid = (int)(tiles < cap ? tiles : cap);
-            hipLaunchKernelGGL((k_stream16<IN, OUT, R, kB16Block, kB16U>), dim3(grid), dim3(kB16Block), 0, st, s, dst,
-                               n8, sc);
+            hipLaunchKernelGGL((k_stream16<IN, OUT, R, B, U>), dim3(grid), dim3(B), 0, st, s, dst, n8, sc);
         }
         done = n8 << 3;
     }
