@@ -15,7 +15,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--kernel", default="fused", choices=["fused", "quant_sum", "dequant", "sum_q32", "absmax", "quantise"])
+    p.add_argument("--kernel", default="fused", choices=["fused", "quant_sum", "dequant", "sum_q32", "absmax", "quantise", "bf16"])
     p.add_argument("--R", type=int, default=2)
     p.add_argument("--mib", type=int, default=256)
     p.add_argument("--iters", type=int, default=20)
@@ -35,6 +35,9 @@ def main():
     qs = [torch.randint(-2 ** 26, 2 ** 26, (n,), device=dev, dtype=torch.int32) for _ in range(R)]
     outf = torch.empty(n, device=dev)
     outq = torch.empty(n, device=dev, dtype=torch.int32)
+    n16 = a.mib * (1 << 20) // 2   # bf16 buckets of the same size in bytes
+    hs = [torch.randn(n16, generator=g, device=dev).to(torch.bfloat16) for _ in range(R)] if a.kernel == "bf16" else []
+    outh = torch.empty(n16, device=dev, dtype=torch.bfloat16) if a.kernel == "bf16" else None
     st = torch.cuda.Stream(device=dev)
 
     def run(kind):
@@ -51,10 +54,12 @@ def main():
             inccl.sum_q32(qs, out=outq, stream=s)
         elif kind == "absmax":
             inccl.absmax_word(xs, stream=s)
+        elif kind == "bf16":
+            inccl.reduce_bf16(hs, 25, out=outh, stream=s)
 
     def alg_bytes(kind):
         return {"fused": (R + 1) * 4 * n, "quant_sum": (R + 1) * 4 * n, "quantise": 8 * n, "dequant": 8 * n,
-                "sum_q32": (R + 1) * 4 * n, "absmax": R * 4 * n}[kind]
+                "sum_q32": (R + 1) * 4 * n, "absmax": R * 4 * n, "bf16": (R + 1) * 2 * n16}[kind]
 
     def timeit(kind, iters):
         for _ in range(3):

@@ -15,11 +15,13 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"fused": "k_stream_vec<F32,F32,R>", "quant_sum": "k_stream_vec<F32,Q32,R>"}
+# probe kind -> (traffic key's kernel name, substring of the mangled name, bytes per element)
+KERNELS = {"fused": ("k_stream_vec<F32,F32,R>", "k_stream_vec", 4), "quant_sum": ("k_stream_vec<F32,Q32,R>", "k_stream_vec", 4),
+           "bf16": ("k_stream16<BF16,BF16,R>", "k_stream16", 2)}
 
 
-def mean_counter(path):
-    rows = [r for r in csv.DictReader(open(path)) if "k_stream_vec" in r["Kernel_Name"]]
+def mean_counter(path, needle):
+    rows = [r for r in csv.DictReader(open(path)) if needle in r["Kernel_Name"]]
     vals = [float(r["Counter_Value"]) for r in rows]
     return sum(vals) / len(vals), len(vals)
 
@@ -39,21 +41,23 @@ def main():
         shutil.copy(os.path.join(src, "bench.json"), os.path.join(prof, f"{tag}_bench_n1.json"))
     if os.path.exists(os.path.join(src, "prof", "run_kernel_stats.csv")):
         shutil.copy(os.path.join(src, "prof", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_bench_n1_kernel_stats.csv"))
+    if os.path.exists(os.path.join(src, "prof_bf16", "run_kernel_stats.csv")):
+        shutil.copy(os.path.join(src, "prof_bf16", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_bf16_kernel_stats.csv"))
     if os.path.exists(os.path.join(src, "bench_profiled.json")):
         shutil.copy(os.path.join(src, "bench_profiled.json"), os.path.join(prof, f"{tag}_bench_n1_under_rocprof.json"))
     traffic_path = os.path.join(prof, "pmc_traffic.json")
     traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
-    n = a.mib * (1 << 20) // 4
-    for k, kname in KERNELS.items():
+    for k, (kname, needle, esize) in KERNELS.items():
+        n = a.mib * (1 << 20) // esize
         f_csv = os.path.join(src, f"pmc_{k}_FETCH_SIZE", "pmc_counter_collection.csv")
         w_csv = os.path.join(src, f"pmc_{k}_WRITE_SIZE", "pmc_counter_collection.csv")
         if not (os.path.exists(f_csv) and os.path.exists(w_csv)):
             continue
-        f, nf = mean_counter(f_csv)
-        w, nw = mean_counter(w_csv)
+        f, nf = mean_counter(f_csv, needle)
+        w, nw = mean_counter(w_csv, needle)
         shutil.copy(f_csv, os.path.join(prof, f"{tag}_pmc", f"{k}_fetch_size.csv"))
         shutil.copy(w_csv, os.path.join(prof, f"{tag}_pmc", f"{k}_write_size.csv"))
-        alg = (a.R + 1) * 4 * n
+        alg = (a.R + 1) * esize * n
         hbm = (2 * f + w) * 1024
         traffic[f"{kname} R={a.R} n={n}"] = {
             "hbm_bytes_per_launch": int(round(hbm)), "fetch_size_kib_raw": f, "write_size_kib": w,
