@@ -48,35 +48,39 @@ class HookState:
 def allreduce_hook(state: HookState, bucket):
     """DDP comm hook: ``bucket.buffer()`` <- mean over ranks, through INCCL.
 
-    The collective is issued on the current stream (the stream DDP's backward
-    runs on), so the result is stream-ordered before DDP copies it back into
-    the parameters' ``.grad``; the returned future is already complete."""
+    The collective runs on the communicator's own stream, after the work queued
+    so far on the current stream (the gradients of this bucket), so the backward
+    pass keeps computing the next buckets' gradients on its stream while this
+    one is exchanged -- the overlap DDP gets from its own collectives.  The
+    returned future is CUDA-aware: DDP's wait on it orders its copy-back into
+    ``.grad`` after the reduction."""
     import torch
 
     buf = bucket.buffer()
     if buf.dtype not in (torch.float32, torch.bfloat16):
         raise IncclError(f"inccl DDP hook: fp32 or bf16 gradient buckets only, got {buf.dtype}")
     reduce = state.comm.allreduce_f32 if buf.dtype == torch.float32 else state.comm.allreduce_bf16
+    w = state.world_size
     if not buf.is_cuda:   # reaches the communicator, which refuses it ("must live on the GPU")
         reduce([buf], out=buf, scale_exp=state.scale_exp, stream=None)
+        if state.average and w > 1:
+            buf.div_(w)
+        fut = torch.futures.Future()
     else:
-        cur = torch.cuda.current_stream(buf.device)
-        if cur.cuda_stream:
-            reduce([buf], out=buf, scale_exp=state.scale_exp, stream=cur.cuda_stream)
-        else:
-            # backward on the legacy null stream: the C ABI reads a NULL stream as
-            # "the communicator's own stream", so order that stream explicitly
-            # after the gradient producers and before DDP's copy-back
-            side = torch.cuda.ExternalStream(state.comm.stream, device=buf.device)
-            side.wait_stream(cur)
+        side = torch.cuda.ExternalStream(state.comm.stream, device=buf.device)
+        side.wait_stream(torch.cuda.current_stream(buf.device))
+        with torch.cuda.stream(side):
             reduce([buf], out=buf, scale_exp=state.scale_exp, stream=side.cuda_stream)
-            cur.wait_stream(side)
-    w = state.world_size
-    if state.average and w > 1:
-        buf.div_(w)
+            if state.average and w > 1:
+                buf.div_(w)
+            # the bucket is used on `side` now: the caching allocator must not
+            # hand its memory out before this stream's work is done
+            buf.record_stream(side)
+            fut = torch.futures.Future(devices=[buf.device])
+            fut.set_result(buf)   # records an event on `side`; wait() makes the waiter's stream wait on it
+    if not buf.is_cuda:
+        fut.set_result(buf)
     state.calls += 1
-    fut = torch.futures.Future()
-    fut.set_result(buf)
     return fut
 
 
