@@ -43,8 +43,33 @@ class GlooStandIn:
         out.copy_(torch.from_numpy(O.reduce_f32(every, k)))
         return out
 
+    def allreduce_bf16(self, srcs, out=None, scale_exp=25, stream=None):
+        import torch
+        import torch.distributed as dist
+        from container_inc_amd import inccl
+        from oracle import oracle as O
+        W = self.group.world_size
+        # gloo has no 16-bit types: the bit patterns travel widened to int32
+        mine = srcs[0].contiguous().view(torch.int16).to(torch.int32)
+        got = [torch.empty_like(mine) for _ in range(W)]
+        dist.all_gather(got, mine)
+        every = [g.numpy().astype(np.uint16) for g in got]
+        k = O.choose_scale(O.absmax_bf16(every), W) if scale_exp == inccl.SCALE_AUTO else scale_exp
+        out.copy_(torch.from_numpy(O.reduce_bf16(every, k).view(np.int16)).view(torch.bfloat16))
+        return out
 
-def run(rank, world, port, q, mode, iters=2):
+
+def _bits(t):
+    """bit patterns of an fp32 (uint32) or bf16 (uint16) tensor as numpy"""
+    import torch
+    if t.dtype == torch.bfloat16:
+        return t.detach().view(torch.int16).cpu().numpy().view(np.uint16)
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False):
+    """dtype "bf16": a bf16 model, so DDP's buckets are bf16 (inccl_allreduce_bf16);
+    as_view: gradient_as_bucket_view=True (the grads are views of the buckets)."""
     try:
         sys.path.insert(0, ROOT)
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
@@ -73,9 +98,12 @@ def run(rank, world, port, q, mode, iters=2):
         model = torch.nn.Sequential(torch.nn.Linear(96, 512), torch.nn.Tanh(), torch.nn.Linear(512, 500),
                                     torch.nn.Tanh(), torch.nn.Linear(500, 300), torch.nn.Tanh(),
                                     torch.nn.Linear(300, 10)).to(dev)
+        wdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        model = model.to(wdt)
         import copy
         local = copy.deepcopy(model)   # non-DDP twin: this rank's own gradients
-        net = DDP(model, device_ids=[0] if mode == "gpu" else None, bucket_cap_mb=0.25)
+        net = DDP(model, device_ids=[0] if mode == "gpu" else None, bucket_cap_mb=0.25,
+                  gradient_as_bucket_view=as_view)
         state = ddp.HookState(comm=comm)
         seen = []
 
@@ -91,8 +119,8 @@ def run(rank, world, port, q, mode, iters=2):
         report = {"buckets": [], "bit_exact": True, "grad_err": 0.0}
         gen = torch.Generator().manual_seed(100 + rank)
         for it in range(iters):
-            x = torch.randn(64, 96, generator=gen).to(dev)
-            y = torch.randn(64, 10, generator=gen).to(dev) * (10.0 ** it)   # later iterations: larger grads
+            x = torch.randn(64, 96, generator=gen).to(dev, wdt)
+            y = (torch.randn(64, 10, generator=gen) * (10.0 ** it)).to(dev, wdt)   # later iterations: larger grads
             seen.clear()
             opt.zero_grad()
             torch.nn.functional.mse_loss(net(x), y).backward()
@@ -102,30 +130,36 @@ def run(rank, world, port, q, mode, iters=2):
             # every hooked bucket vs the oracle on all ranks' bucket inputs
             for before, after in seen:
                 allb = [None] * world
-                dist.all_gather_object(allb, before.cpu().numpy().tobytes())
-                every = [np.frombuffer(b, np.float32) for b in allb]
-                k = O.choose_scale(O.absmax(every), world)
-                want = O.reduce_f32(every, k) / np.float32(world)
-                got = after.cpu().numpy()
-                if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+                dist.all_gather_object(allb, _bits(before).tobytes())
+                if dtype == "bf16":
+                    every = [np.frombuffer(b, np.uint16) for b in allb]
+                    k = O.choose_scale(O.absmax_bf16(every), world)
+                    s16 = torch.from_numpy(O.reduce_bf16(every, k).view(np.int16)).view(torch.bfloat16)
+                    want = _bits(s16 / world)   # the hook's div_ (exact for W = 2, 4)
+                else:
+                    every = [np.frombuffer(b, np.float32) for b in allb]
+                    k = O.choose_scale(O.absmax(every), world)
+                    want = (O.reduce_f32(every, k) / np.float32(world)).view(np.uint32)
+                if not np.array_equal(_bits(after), want):
                     report["bit_exact"] = False
             # DDP's averaged grads vs the mean of the ranks' local grads.  Bound per
             # lane: W quantisation errors of 2^-(k+1) each, divided by W, at the
             # smallest scale any bucket can have (k from the largest |grad| of all),
-            # plus the int32 -> fp32 rounding of the sum and the division (2^-23 rel)
+            # plus the rounding of the sum to the bucket's format (2^-23 relative for
+            # fp32, 2^-8 for bf16, doubled for slack)
             opt_local.zero_grad()
             torch.nn.functional.mse_loss(local(x), y).backward()
             means, ddp_grads = [], []
             for p, pl in zip(net.module.parameters(), local.parameters()):
-                g = pl.grad.detach().cpu().numpy().astype(np.float32)
+                g = pl.grad.detach().float().cpu().numpy()
                 allg = [None] * world
                 dist.all_gather_object(allg, g.tobytes())
                 stack = np.stack([np.frombuffer(b, np.float32).astype(np.float64) for b in allg])
                 means.append((stack.mean(axis=0), float(np.max(np.abs(stack)))))
-                ddp_grads.append(p.grad.detach().cpu().numpy().astype(np.float64).ravel())
+                ddp_grads.append(p.grad.detach().float().cpu().numpy().astype(np.float64).ravel())
             k = O.choose_scale(np.float32(max(a for _, a in means)), world)
             for (mean, _), got in zip(means, ddp_grads):
-                bound = 2.0 ** -(k + 1) + np.abs(mean) * 2.0 ** -23
+                bound = 2.0 ** -(k + 1) + np.abs(mean) * (2.0 ** -7 if dtype == "bf16" else 2.0 ** -23)
                 report["grad_err"] = max(report["grad_err"], float(np.max(np.abs(got - mean) / bound)))
             opt.step()
             # the local twin follows the DDP model so the next iteration starts equal

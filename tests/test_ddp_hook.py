@@ -17,12 +17,12 @@ def _free_port():
     return p
 
 
-def run_world(world, mode, timeout):
+def run_world(world, mode, timeout, dtype="f32", as_view=False):
     import _ddp_rank
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_ddp_rank.run, args=(r, world, port, q, mode)) for r in range(world)]
+    ps = [ctx.Process(target=_ddp_rank.run, args=(r, world, port, q, mode, 2, dtype, as_view)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=timeout) for _ in range(world))
@@ -31,9 +31,9 @@ def run_world(world, mode, timeout):
     return res
 
 
-@pytest.mark.parametrize("world", [2])
-def test_ddp_hook_plumbing_gloo(orc, world):
-    res = run_world(world, "cpu", 300)
+@pytest.mark.parametrize("world,dtype,as_view", [(2, "f32", False), (2, "bf16", False), (2, "f32", True)])
+def test_ddp_hook_plumbing_gloo(orc, world, dtype, as_view):
+    res = run_world(world, "cpu", 300, dtype, as_view)
     for r, rep in res.items():
         assert "error" not in rep, rep.get("tb")
         # DDP's first iteration sends everything in one bucket; after its bucket
