@@ -800,8 +800,12 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
         if (!in_place) INCCL_HIP(hipMemcpyAsync(dst_dev, gather, n * sizeof(uint16_t), hipMemcpyDeviceToDevice, st));
         return 0;
     }
-    /* every other engine: its int32 allreduce of the quantised partials
-     * (RCCL all-reduce for "ar" / "a2a", the p2p exchange for the IPC engines) */
+    /* the p2p engine: bf16 result shards gathered over xGMI (p2p.c) */
+    if (c->engine == INCCL_ENGINE_P2P && c->group->transport == INCCL_TRANSPORT_RCCL && ((uintptr_t)dst_dev & 3u) == 0)
+        return inccl_p2p_piece_bf16(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+    /* every other engine (and a p2p dst that is not 4-B aligned): its int32
+     * allreduce of the quantised partials (RCCL all-reduce for "ar" / "a2a",
+     * the p2p exchange for the IPC engines) */
     int rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
     if (rc) return rc;
     int32_t *q = (int32_t *)c->d_q32;

@@ -144,6 +144,8 @@ int inccl_rccl_alltoall_q32(struct inccl_communicator *c, const int32_t *send, i
 /* p2p engine */
 int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
                     const uint32_t *amax, int scale_R, hipStream_t st);
+int inccl_p2p_piece_bf16(struct inccl_communicator *c, const uint16_t *const *srcs, int R, uint16_t *dst, size_t n,
+                         int k, const uint32_t *amax, int scale_R, hipStream_t st);
 void inccl_p2p_release(struct inccl_communicator *c);
 /* int32 allreduce (wrapping sum) over the p2p engine's IPC buffers: the
  * reference API's inccl_allreduce_write on a multi-process group without RCCL */

@@ -90,6 +90,7 @@ struct Segs {
     const void* src[kMaxR];
     int64_t off[kMaxR];
     int64_t cnt[kMaxR];
+    int tail16[kMaxR];   // 2-byte gathers: one more element after cnt words (the low half of word cnt)
     int nseg;
 };
 
@@ -130,9 +131,13 @@ __global__ __launch_bounds__(kGatherBlock) void k_peer_gather(Segs s, uint32_t* 
             }
         }
     }
-    if (xb == 0)   // ragged tail of the last shard
+    if (xb == 0) {   // ragged tail of the last shard
         for (int64_t i = (n4 << 2) + threadIdx.x; i < cnt; i += kGatherBlock)
             d[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (s.tail16[j] && threadIdx.x == 0)   // an odd element count of 2-byte elements
+            reinterpret_cast<uint16_t*>(d + cnt)[0] =
+                (uint16_t)(__hip_atomic_load(src + cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 0xffffu);
+    }
 }
 
 template <int R, bool DEQ = true>
@@ -202,6 +207,8 @@ extern "C" int inccl_k_peer_sum_q32(const void* const* peers, int W, int32_t* ds
     return e == hipSuccess ? 0 : (int)e;
 }
 
+static int launch_gather(Segs& s, int64_t maxc, void* dst, void* stream);
+
 extern "C" int inccl_k_peer_gather(const void* const* src, const int64_t* off, const int64_t* cnt, int nseg, void* dst,
                                    void* stream)
 {
@@ -216,6 +223,34 @@ extern "C" int inccl_k_peer_gather(const void* const* src, const int64_t* off, c
         s.cnt[j] = cnt[j];
         maxc = cnt[j] > maxc ? cnt[j] : maxc;
     }
+    return launch_gather(s, maxc, dst, stream);
+}
+
+// 2-byte elements (bf16 result shards): whole 4-byte words, plus the odd last
+// element of a segment.  dst must be 4-byte aligned and every offset even.
+extern "C" int inccl_k_peer_gather16(const void* const* src, const int64_t* off, const int64_t* cnt, int nseg,
+                                     void* dst, void* stream)
+{
+    if (nseg < 1 || nseg > kMaxR || dst == nullptr || (reinterpret_cast<uintptr_t>(dst) & 3u) != 0)
+        return INCCL_ERR_ARG;
+    Segs s = {};
+    s.nseg = nseg;
+    int64_t maxc = 0;
+    for (int j = 0; j < nseg; ++j) {
+        if ((src[j] == nullptr && cnt[j] > 0) || cnt[j] < 0 || (off[j] & 1) || !aligned16(src[j])) return INCCL_ERR_ARG;
+        s.src[j] = src[j];
+        s.off[j] = off[j] >> 1;
+        s.cnt[j] = cnt[j] >> 1;
+        s.tail16[j] = (int)(cnt[j] & 1);
+        const int64_t c = s.cnt[j] + s.tail16[j];
+        maxc = c > maxc ? c : maxc;
+    }
+    return launch_gather(s, maxc, dst, stream);
+}
+
+static int launch_gather(Segs& s, int64_t maxc, void* dst, void* stream)
+{
+    const int nseg = s.nseg;
     if (maxc == 0) return 0;
     const int64_t tile = (int64_t)kGatherBlock * kGatherU * 4;
     int64_t gx = (maxc + tile - 1) / tile;

@@ -224,6 +224,54 @@ int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int 
     return 0;
 }
 
+/* bfloat16 buckets over the same buffers and barriers: quant + local sum of the
+ * bf16 buckets -> part; barrier; the int32 sum of shard `me` pulled from every
+ * peer, in place into my own part shard (peers read only their own shards of
+ * my part), dequantised to bf16 into res (as 2-byte elements at me * shard);
+ * barrier; every rank's bf16 result shard gathered -- 2 bytes per element over
+ * xGMI instead of the int32 allreduce's 4.  dst must be 4-byte aligned. */
+int inccl_p2p_piece_bf16(struct inccl_communicator *c, const uint16_t *const *srcs, int R, uint16_t *dst, size_t n,
+                         int k, const uint32_t *amax, int scale_R, hipStream_t st)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    if (W > INCCL_MAX_LOCAL_INPUTS) return inccl_set_error(INCCL_ERR_ARG, "p2p engine supports up to %d GPUs",
+                                                          INCCL_MAX_LOCAL_INPUTS);
+    const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
+    int rc = p2p_ensure(c, total);
+    if (rc) return rc;
+    if (c->p2p_last_stream && c->p2p_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[8], 0));
+    rc = inccl_k_stream(INCCL_KIND_BF16, INCCL_KIND_Q32, (const void *const *)srcs, R, c->p2p_part, n, k, amax,
+                        scale_R, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p bf16 quant+sum launch failed (%d)", rc);
+    if (total > n) INCCL_HIP(hipMemsetAsync(c->p2p_part + n, 0, (total - n) * sizeof(int32_t), st));
+    rc = sync_and_barrier(c, st);
+    if (rc) return rc;
+    int32_t *mine = c->p2p_part + (size_t)me * shard;
+    const void *peer[INCCL_MAX_LOCAL_INPUTS];
+    for (int j = 0; j < W; ++j) peer[j] = c->p2p_peer_part[j] + (size_t)me * shard;
+    rc = inccl_k_peer_sum_q32(peer, W, mine, shard, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p bf16 reduce-scatter launch failed (%d)", rc);
+    const void *s1[1] = {mine};
+    rc = inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_BF16, s1, 1, (uint16_t *)c->p2p_res + (size_t)me * shard, shard, k,
+                        amax, scale_R, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p bf16 dequantise launch failed (%d)", rc);
+    rc = sync_and_barrier(c, st);
+    if (rc) return rc;
+    const void *src[INCCL_MAX_LOCAL_INPUTS];
+    int64_t off[INCCL_MAX_LOCAL_INPUTS], cnt[INCCL_MAX_LOCAL_INPUTS];
+    for (int j = 0; j < W; ++j) {
+        const size_t lo = (size_t)j * shard;
+        src[j] = (const uint16_t *)c->p2p_peer_res[j] + lo;
+        off[j] = (int64_t)lo;
+        cnt[j] = lo >= n ? 0 : (int64_t)((n - lo) < shard ? (n - lo) : shard);
+    }
+    rc = inccl_k_peer_gather16(src, off, cnt, W, dst, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p bf16 gather launch failed (%d)", rc);
+    INCCL_HIP(hipEventRecord(c->ev[8], st));
+    c->p2p_last_stream = st;
+    return 0;
+}
+
 /* The int32 allreduce over the same buffers and barriers as inccl_p2p_piece,
  * with the sum left in int32 (the reference's switch add, nts.c:361-363, and
  * nothing else): copy in -> barrier -> pull + sum shard `me` from every peer ->

@@ -189,6 +189,11 @@ def _p2p_rank(rank, world, port, q):
             comm.allreduce_bf16(srcs, out=out, scale_exp=inccl.SCALE_AUTO if k == "auto" else k, stream=comm.stream)
             torch.cuda.synchronize()
             ok.append(bool(np.array_equal(_host(out), want)))
+            odd = torch.empty(n + 1, dtype=torch.bfloat16, device=dev)[1:]   # 2-B aligned: the int32-allreduce path
+            torch.cuda.synchronize()
+            comm.allreduce_bf16(srcs, out=odd, scale_exp=inccl.SCALE_AUTO if k == "auto" else k, stream=comm.stream)
+            torch.cuda.synchronize()
+            ok.append(bool(np.array_equal(_host(odd), want)))
             comm.allreduce_bf16(srcs, out=srcs[0], scale_exp=inccl.SCALE_AUTO if k == "auto" else k,
                                 stream=comm.stream)   # in place
             torch.cuda.synchronize()
@@ -200,8 +205,11 @@ def _p2p_rank(rank, world, port, q):
         q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_allreduce_bf16_p2p_multiprocess(gpu, world):
+    """The p2p engine's bf16 piece (bf16 result shards gathered, odd element
+    counts through the gather's 2-byte tail), a 2-byte-aligned dst (the int32
+    allreduce path) and in place."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
