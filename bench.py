@@ -28,7 +28,8 @@ Extra JSON fields:
   host_e2e          N = 1: BASELINE config 3, 1 GiB pinned host fp32 in 64 MiB buckets
   api_allreduce_write N = 1: the reference's entry point on a 256 MiB host int32
                     message, registered and unregistered
-  bf16              N = 1: R bf16 buckets of 256 MiB (k_stream16), repeated and rotated
+  bf16              N = 1: R bf16 buckets of 256 MiB (k_stream16), repeated and rotated;
+                    N > 1: inccl_allreduce_bf16 on the rccl and p2p engines, verified
   sweep             N > 1: 4 KiB .. 256 MiB and 1 GiB per engine, verified with
                     alternating input sets
 """
@@ -313,6 +314,67 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
             del got
         del inputs, out, refs
         torch.cuda.empty_cache()
+    return rows
+
+
+def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256) -> list:
+    """N > 1: R resident `mib` MiB bf16 buckets per rank through inccl_allreduce_bf16
+    on the engines with a bf16 result exchange (rccl: ncclAllGather of bf16; p2p:
+    bf16 result shards gathered), each verified bit-identical to the first engine
+    that passes on every rank over two alternating input sets; wall time per call,
+    max over ranks, and the xGMI link fraction of its (W-1)/W * n * (4 + 2) bytes."""
+    import torch
+    import torch.distributed as dist
+
+    from container_inc_amd import inccl
+    n = mib * (1 << 20) // 2
+    inputs = []
+    for seed in (9000, 9500):
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed + rank)
+        inputs.append([torch.randn(n, generator=gen, device=dev).to(torch.bfloat16) for _ in range(R)])
+    out = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    st = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize()
+    rows, refs = [], None
+    for eng in ("rccl", "p2p"):
+        ok, dt, same = 1, float("inf"), False
+        try:
+            comm.set_engine(eng)
+            got = []
+            for xs in (inputs[0], inputs[1], inputs[0]):
+                comm.allreduce_bf16(xs, out=out, scale_exp=25, stream=st.cuda_stream)
+                torch.cuda.synchronize()
+                got.append(out.clone())
+                torch.cuda.synchronize()
+            same = (torch.equal(got[0], got[2]) if refs is None
+                    else all(torch.equal(g, refs[i % 2]) for i, g in enumerate(got)))
+            for _ in range(5):
+                comm.allreduce_bf16(inputs[0], out=out, scale_exp=25, stream=st.cuda_stream)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(10):
+                comm.allreduce_bf16(inputs[0], out=out, scale_exp=25, stream=st.cuda_stream)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / 10
+        except Exception as e:  # noqa: BLE001
+            print(f"rank {rank}: bf16 engine {eng} failed: {e}", file=sys.stderr, flush=True)
+            ok, got = 0, None
+        v = agree([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0], world)
+        good, ident = v[1] == 0.0, v[2] == 0.0
+        if good and ident and refs is None:
+            refs = (got[0], got[1])
+        row = {"engine": eng, "bucket_mib": mib, "R": R, "ok": good, "bit_identical": good and ident,
+               "ms": round(v[0] * 1e3, 4) if good else None}
+        if good:
+            link = (world - 1) * n * 6 // world
+            row["GBps_buckets"] = round(world * R * 2 * n / v[0] / 1e9, 1)
+            row["xgmi_frac"] = round(link / v[0] / 1e9 / ((world - 1) * XGMI_LINK_GBS_BIDIR), 4)
+        rows.append(row)
+        del got
+    del inputs, out, refs
+    torch.cuda.empty_cache()
     return rows
 
 
@@ -893,6 +955,7 @@ def main():
         for key in chosen[2]:   # the sweep runs every engine with its defaults
             os.environ.pop(key, None)
         res["sweep"] = size_sweep(comm, dev, R, k, rank, world)
+        res["bf16"] = bf16_engines(comm, dev, R, rank, world)
         comm.set_engine(chosen[0])
     def extra(key, fn):
         """An N = 1 extra key (one process, no collectives): a failure is recorded
