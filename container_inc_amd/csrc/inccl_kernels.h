@@ -28,7 +28,10 @@ int inccl_k_peer_reduce(const void *const *peers, int W, float *dst, size_t n, i
                         const uint32_t *amax_bits_dev, int scale_R, void *stream);
 int inccl_k_peer_gather(const void *const *src, const int64_t *off, const int64_t *cnt, int nseg, void *dst,
                         void *stream);
-/* the same for 2-byte elements (counts and even offsets in elements; dst 4-B aligned) */
+/* the pull-reduce with bf16 results: dst[i] = bf16(dequant(sum_j peers[j][i])), n % 4 == 0, dst 8-B aligned */
+int inccl_k_peer_reduce_bf16(const void *const *peers, int W, uint16_t *dst, size_t n, int scale_exp,
+                             const uint32_t *amax_bits_dev, int scale_R, void *stream);
+/* the same gather for 2-byte elements (counts and even offsets in elements; dst 4-B aligned) */
 int inccl_k_peer_gather16(const void *const *src, const int64_t *off, const int64_t *cnt, int nseg, void *dst,
                           void *stream);
 /* dst[i] = sum_j peers[j][i] (int32, wrapping), n % 4 == 0, 16-B aligned */

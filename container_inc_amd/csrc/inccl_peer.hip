@@ -86,6 +86,39 @@ __global__ __launch_bounds__(BLOCK) void k_peer_reduce(SrcPtrs src, float* __res
     }
 }
 
+// The pull-reduce with a bf16 result (inccl_allreduce_bf16 on the p2p engine):
+// the same 16-B system-scope loads of 4 int32 partials per peer and lane, summed,
+// dequantised and narrowed (v_cvt_pk_bf16_f32) into 8 bytes per lane,
+// written through.
+template <int R, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_peer_reduce_bf16(SrcPtrs src, uint16_t* __restrict__ dst, int64_t n4, Scale sc)
+{
+    const float inv = pow2f(-resolve_k(sc));
+    for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n4; base += (int64_t)gridDim.x * BLOCK) {
+        const int64_t i = base + threadIdx.x;
+        const int64_t left = n4 - base;
+        const uint32_t tile_in = (uint32_t)((left < BLOCK ? left : BLOCK) * 16);
+        u32x4 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r)   // out-of-range lanes read 0 (buffer range check)
+            v[r] = ld_sys16<kAuxSysNT>(reinterpret_cast<const u32x4*>(src.p[r]) + base, tile_in, threadIdx.x * 16u);
+        if (i < n4) {
+            u32x4 acc = v[0];
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                acc.x += v[r].x;
+                acc.y += v[r].y;
+                acc.z += v[r].z;
+                acc.w += v[r].w;
+            }
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 o = {deq_bf16x2(acc.x, acc.y, inv), deq_bf16x2(acc.z, acc.w, inv)};
+            __builtin_amdgcn_raw_buffer_store_b64(o, rsrc(dst + base * 4, tile_in / 2), (int)(threadIdx.x * 8u), 0,
+                                                  kAuxWT);
+        }
+    }
+}
+
 struct Segs {
     const void* src[kMaxR];
     int64_t off[kMaxR];
@@ -177,6 +210,36 @@ extern "C" int inccl_k_peer_reduce(const void* const* peers, int W, float* dst, 
         case 7: e = launch_reduce_R<7>(s, dst, n4, sc, st); break;
         default: e = launch_reduce_R<8>(s, dst, n4, sc, st); break;
     }
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int inccl_k_peer_reduce_bf16(const void* const* peers, int W, uint16_t* dst, size_t n, int scale_exp,
+                                        const uint32_t* amax_bits_dev, int scale_R, void* stream)
+{
+    if (W < 1 || W > kMaxR || dst == nullptr || (n & 3) != 0 || (reinterpret_cast<uintptr_t>(dst) & 7u) != 0)
+        return INCCL_ERR_ARG;
+    if (n == 0) return 0;
+    SrcPtrs s = {};
+    for (int j = 0; j < W; ++j) {
+        if (peers[j] == nullptr || !aligned16(peers[j])) return INCCL_ERR_ARG;
+        s.p[j] = peers[j];
+    }
+    Scale sc{scale_exp, amax_bits_dev, scale_R > 0 ? scale_R : W};
+    const int64_t n4 = (int64_t)(n >> 2);
+    hipStream_t st = (hipStream_t)stream;
+    switch (W) {
+#define INCCL_PR16(WW)                                                                                                \
+    case WW: {                                                                                                         \
+        constexpr int B = Geometry<WW>::BLOCK;                                                                         \
+        hipLaunchKernelGGL((k_peer_reduce_bf16<WW, B>), dim3((unsigned)((n4 + B - 1) / B)), dim3(B), 0, st, s, dst, n4, \
+                           sc);                                                                                        \
+        break;                                                                                                         \
+    }
+        INCCL_PR16(1) INCCL_PR16(2) INCCL_PR16(3) INCCL_PR16(4) INCCL_PR16(5) INCCL_PR16(6) INCCL_PR16(7)
+        default: INCCL_PR16(8)
+#undef INCCL_PR16
+    }
+    const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
 

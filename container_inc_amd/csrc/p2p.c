@@ -225,11 +225,11 @@ int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int 
 }
 
 /* bfloat16 buckets over the same buffers and barriers: quant + local sum of the
- * bf16 buckets -> part; barrier; the int32 sum of shard `me` pulled from every
- * peer, in place into my own part shard (peers read only their own shards of
- * my part), dequantised to bf16 into res (as 2-byte elements at me * shard);
- * barrier; every rank's bf16 result shard gathered -- 2 bytes per element over
- * xGMI instead of the int32 allreduce's 4.  dst must be 4-byte aligned. */
+ * bf16 buckets -> part; barrier; shard `me` pulled from every peer, summed,
+ * dequantised and narrowed to bf16 in one kernel into res (2-byte elements at
+ * me * shard); barrier; every rank's bf16 result shard gathered -- 2 bytes per
+ * element over xGMI instead of the int32 allreduce's 4.  dst must be 4-byte
+ * aligned. */
 int inccl_p2p_piece_bf16(struct inccl_communicator *c, const uint16_t *const *srcs, int R, uint16_t *dst, size_t n,
                          int k, const uint32_t *amax, int scale_R, hipStream_t st)
 {
@@ -246,15 +246,10 @@ int inccl_p2p_piece_bf16(struct inccl_communicator *c, const uint16_t *const *sr
     if (total > n) INCCL_HIP(hipMemsetAsync(c->p2p_part + n, 0, (total - n) * sizeof(int32_t), st));
     rc = sync_and_barrier(c, st);
     if (rc) return rc;
-    int32_t *mine = c->p2p_part + (size_t)me * shard;
     const void *peer[INCCL_MAX_LOCAL_INPUTS];
     for (int j = 0; j < W; ++j) peer[j] = c->p2p_peer_part[j] + (size_t)me * shard;
-    rc = inccl_k_peer_sum_q32(peer, W, mine, shard, st);
+    rc = inccl_k_peer_reduce_bf16(peer, W, (uint16_t *)c->p2p_res + (size_t)me * shard, shard, k, amax, scale_R, st);
     if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p bf16 reduce-scatter launch failed (%d)", rc);
-    const void *s1[1] = {mine};
-    rc = inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_BF16, s1, 1, (uint16_t *)c->p2p_res + (size_t)me * shard, shard, k,
-                        amax, scale_R, st);
-    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p bf16 dequantise launch failed (%d)", rc);
     rc = sync_and_barrier(c, st);
     if (rc) return rc;
     const void *src[INCCL_MAX_LOCAL_INPUTS];
