@@ -510,6 +510,22 @@ int inccl_comm_ipc_mem_kind(struct inccl_communicator *comm, const char *engine)
     return inccl_mem_kind(p);
 }
 
+int inccl_comm_set_average(struct inccl_communicator *comm, int on)
+{
+    if (!comm) return inccl_set_error(INCCL_ERR_ARG, "NULL communicator");
+    const int W = comm->group->world_size;
+    if (!on) {
+        comm->out_shift = 0;
+        return 0;
+    }
+    if (W & (W - 1))
+        return inccl_set_error(INCCL_ERR_ARG, "set_average: world %d is not a power of two (the mean would round)", W);
+    int s = 0;
+    while ((1 << s) < W) ++s;
+    comm->out_shift = s;
+    return 0;
+}
+
 int inccl_comm_clear_error(struct inccl_communicator *comm)
 {
     if (!comm) return inccl_set_error(INCCL_ERR_ARG, "comm is NULL");
@@ -564,7 +580,8 @@ static int allreduce_piece_a2a(struct inccl_communicator *c, const float *const 
     const size_t lo = (size_t)me * shard;
     const int in_place = (total == n);
     float *gather = in_place ? dst : fws;
-    rc = kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_F32, parts, W, gather + lo, shard, k, amax, scale_R, st));
+    rc = kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_F32, parts, W, gather + lo, shard, k, amax, scale_R,
+                               c->out_shift, st));
     if (rc) return rc;
     rc = inccl_tp_all_gather_f32(c, gather + lo, gather, shard, st);
     if (rc) return rc;
@@ -591,7 +608,8 @@ static int allreduce_piece(struct inccl_communicator *c, const float *const *src
     const int in_place = (total == n);
     float *gather = in_place ? dst : fws;
     const void *s1[1] = {qrecv};
-    rc = kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, gather + lo, shard, k, amax, scale_R, st));
+    rc = kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, gather + lo, shard, k, amax, scale_R,
+                               c->out_shift, st));
     if (rc) return rc;
     rc = inccl_tp_all_gather_f32(c, gather + lo, gather, shard, st);
     if (rc) return rc;
@@ -642,8 +660,8 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
 
     const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: RS/AG path even at world 1 */
     if (W == 1 && !(fs && atoi(fs) != 0))   /* one fused HBM pass: quant + sum + dequant */
-        return kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, k,
-                                   amax, scale_R, st));
+        return kerr(inccl_k_stream_s(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, k,
+                                   amax, scale_R, c->out_shift, st));
 
     /* the IPC engines: the ll kernel for small buckets when the ll engine was
      * chosen explicitly (ll.c), else the one-kernel mesh exchange (mesh.c) or the
@@ -668,7 +686,8 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
         rc = inccl_tp_allreduce_q32(c, q, q, n, st);
         if (rc) return rc;
         const void *s1[1] = {q};
-        return kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, dst_dev, n, k, amax, scale_R, st));
+        return kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, dst_dev, n, k, amax, scale_R,
+                                     c->out_shift, st));
     }
     if (c->engine == INCCL_ENGINE_A2A && c->group->transport == INCCL_TRANSPORT_RCCL) {
         if (W > INCCL_MAX_LOCAL_INPUTS)
@@ -728,7 +747,8 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
         float *gather = in_place ? dst_dev + off : (float *)c->d_f32;
         const size_t lo = (size_t)c->group->rank * shard;
         const void *s1[1] = {qrecv};
-        rc = kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, gather + lo, shard, k, amax, scale_R, st));
+        rc = kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, gather + lo, shard, k, amax, scale_R,
+                                   c->out_shift, st));
         if (rc) return rc;
         rc = inccl_tp_all_gather_f32(c, gather + lo, gather, shard, st);
         if (rc) return rc;
@@ -771,7 +791,8 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
     const int scale_R = R * W;
     const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: RS/AG path even at world 1 */
     if (W == 1 && !(fs && atoi(fs) != 0))   /* one fused HBM pass */
-        return kerr(inccl_k_stream(INCCL_KIND_BF16, INCCL_KIND_BF16, srcs, R, dst_dev, n, k, amax, scale_R, st));
+        return kerr(inccl_k_stream_s(INCCL_KIND_BF16, INCCL_KIND_BF16, srcs, R, dst_dev, n, k, amax, scale_R,
+                                     c->out_shift, st));
 
     if (c->engine == INCCL_ENGINE_RCCL || c->group->transport == INCCL_TRANSPORT_LOCAL) {
         /* quant + local sum -> reduce-scatter (int32) -> dequantise own shard to
@@ -793,7 +814,8 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
         uint16_t *gather = in_place ? dst_dev : (uint16_t *)c->d_f32;
         const size_t lo = (size_t)me * shard;
         const void *s1[1] = {qrecv};
-        rc = kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_BF16, s1, 1, gather + lo, shard, k, amax, scale_R, st));
+        rc = kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_BF16, s1, 1, gather + lo, shard, k, amax, scale_R,
+                                   c->out_shift, st));
         if (rc) return rc;
         rc = inccl_tp_all_gather_bf16(c, gather + lo, gather, shard, st);
         if (rc) return rc;
@@ -814,7 +836,8 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
     rc = inccl_tp_allreduce_q32(c, q, q, n, st);
     if (rc) return rc;
     const void *s1[1] = {q};
-    return kerr(inccl_k_stream(INCCL_KIND_Q32, INCCL_KIND_BF16, s1, 1, dst_dev, n, k, amax, scale_R, st));
+    return kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_BF16, s1, 1, dst_dev, n, k, amax, scale_R,
+                                 c->out_shift, st));
 }
 
 /* ------------------------------------------------------------------ */

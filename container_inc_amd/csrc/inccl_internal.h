@@ -76,6 +76,7 @@ struct inccl_communicator {
     /* p2p engine: library-owned buffers shared with every peer through HIP IPC
      * handles; each GPU pulls its shard from all peers over xGMI */
     int engine;                  /* INCCL_ENGINE_* */
+    int out_shift;               /* log2(world) when results are averaged (inccl_comm_set_average), else 0 */
     size_t p2p_cap;              /* elements per buffer */
     int32_t *p2p_part;           /* this rank's quantised partial sums (W * shard) */
     float *p2p_res;              /* this rank's dequantised shard lives at rank * shard */

@@ -15,6 +15,9 @@ extern "C" {
 /* out[i] = OUT(sum_r IN(srcs[r][i])), kinds INCCL_KIND_*.  Returns 0 or a hipError_t / INCCL_ERR_ARG. */
 int inccl_k_stream(int in_kind, int out_kind, const void *const *srcs, int R, void *dst, size_t n, int scale_exp,
                    const uint32_t *amax_bits_dev, int scale_R, void *stream);
+/* the same with the dequantise scaled by 2^-out_shift (inccl_comm_set_average) */
+int inccl_k_stream_s(int in_kind, int out_kind, const void *const *srcs, int R, void *dst, size_t n, int scale_exp,
+                     const uint32_t *amax_bits_dev, int scale_R, int out_shift, void *stream);
 int inccl_k_absmax(const float *const *srcs, int R, size_t n, uint32_t *amax_bits_dev, int zero_first, void *stream);
 int inccl_k_absmax_bf16(const uint16_t *const *srcs, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
                         void *stream);
@@ -25,12 +28,12 @@ void inccl_k_set_tuning(int grid_cap, int nt_loads);
  * dst[i] = dequant(sum_j peers[j][i]), n % 4 == 0, 16-B aligned; and
  * dst[off[j] .. off[j]+cnt[j]) = src[j][0 .. cnt[j]) for j < nseg, one launch */
 int inccl_k_peer_reduce(const void *const *peers, int W, float *dst, size_t n, int scale_exp,
-                        const uint32_t *amax_bits_dev, int scale_R, void *stream);
+                        const uint32_t *amax_bits_dev, int scale_R, int out_shift, void *stream);
 int inccl_k_peer_gather(const void *const *src, const int64_t *off, const int64_t *cnt, int nseg, void *dst,
                         void *stream);
 /* the pull-reduce with bf16 results: dst[i] = bf16(dequant(sum_j peers[j][i])), n % 4 == 0, dst 8-B aligned */
 int inccl_k_peer_reduce_bf16(const void *const *peers, int W, uint16_t *dst, size_t n, int scale_exp,
-                             const uint32_t *amax_bits_dev, int scale_R, void *stream);
+                             const uint32_t *amax_bits_dev, int scale_R, int out_shift, void *stream);
 /* the same gather for 2-byte elements (counts and even offsets in elements; dst 4-B aligned) */
 int inccl_k_peer_gather16(const void *const *src, const int64_t *off, const int64_t *cnt, int nseg, void *dst,
                           void *stream);
@@ -56,6 +59,7 @@ struct inccl_ll_launch {
     int scale_exp;
     const uint32_t *amax_bits;
     int scale_R;
+    int out_shift;                                     /* dequantise with 2^-(k + out_shift) */
 };
 int inccl_k_ll_grid(size_t n);
 int inccl_k_ll_oneshot(const struct inccl_ll_launch *l, void *stream);
@@ -88,6 +92,7 @@ struct inccl_mesh_launch {
     int scale_exp;
     const uint32_t *amax_bits;
     int scale_R;
+    int out_shift;                                     /* dequantise with 2^-(k + out_shift) */
 };
 int inccl_k_mesh(const struct inccl_mesh_launch *l, void *stream);
 

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_scalar(SrcPtrs src, void* __r
 {
     const int k = resolve_k(sc);
     const float scale = pow2f(k);
-    const float inv = pow2f(-k);
+    const float inv = deq_scale(sc, k);
     uint32_t* __restrict__ out = reinterpret_cast<uint32_t*>(dst);
     for (int64_t i = begin + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
         uint32_t acc = 0;
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(kBlock) void k_stream16_scalar(SrcPtrs src, void* _
 {
     const int k = resolve_k(sc);
     const float scale = pow2f(k);
-    const float inv = pow2f(-k);
+    const float inv = deq_scale(sc, k);
     for (int64_t i = begin + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
         uint32_t acc = 0;
 #pragma unroll
@@ -371,13 +371,20 @@ bool scale_ok(int k) { return k >= INCCL_SCALE_MIN && k <= INCCL_SCALE_MAX; }
 
 extern "C" {
 
-int inccl_k_stream(int in_kind, int out_kind, const void* const* srcs, int R, void* dst, size_t n, int scale_exp,
-                   const uint32_t* amax_bits_dev, int scale_R, void* stream)
+int inccl_k_stream_s(int in_kind, int out_kind, const void* const* srcs, int R, void* dst, size_t n, int scale_exp,
+                     const uint32_t* amax_bits_dev, int scale_R, int out_shift, void* stream)
 {
     if (amax_bits_dev == nullptr && !scale_ok(scale_exp)) return INCCL_ERR_ARG;
     if (dst == nullptr && n > 0) return INCCL_ERR_ARG;
-    Scale sc{scale_exp, amax_bits_dev, scale_R > 0 ? scale_R : R};
+    if (out_shift < 0 || out_shift > 8) return INCCL_ERR_ARG;
+    Scale sc{scale_exp, amax_bits_dev, scale_R > 0 ? scale_R : R, out_shift};
     return dispatch(in_kind, out_kind, srcs, R, dst, (int64_t)n, sc, (hipStream_t)stream);
+}
+
+int inccl_k_stream(int in_kind, int out_kind, const void* const* srcs, int R, void* dst, size_t n, int scale_exp,
+                   const uint32_t* amax_bits_dev, int scale_R, void* stream)
+{
+    return inccl_k_stream_s(in_kind, out_kind, srcs, R, dst, n, scale_exp, amax_bits_dev, scale_R, 0, stream);
 }
 
 int inccl_k_absmax(const float* const* srcs, int R, size_t n, uint32_t* amax_bits_dev, int zero_first, void* stream)

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
 {
     const int k = resolve_k(a.sc);
     const float scale = pow2f(k);
-    const float inv = pow2f(-k);
+    const float inv = deq_scale(a.sc, k);
     const int64_t nq = (a.n + 3) >> 2;
     const int64_t stride = (int64_t)gridDim.x * kLLBlock;
     const int tid = threadIdx.x;
@@ -282,6 +282,7 @@ extern "C" int inccl_k_ll_oneshot(const struct inccl_ll_launch* l, void* stream)
     a.sc.k = l->scale_exp;
     a.sc.amax_bits = l->amax_bits;
     a.sc.scale_R = l->scale_R;
+    a.sc.out_shift = l->out_shift;
     int vs = 1;
     for (int r = 0; r < l->R; ++r) vs &= aligned16(l->src[r]) ? 1 : 0;
     const int vd = aligned16(l->dst) ? 1 : 0;

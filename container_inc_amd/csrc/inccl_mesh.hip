@@ -305,7 +305,7 @@ __global__ __launch_bounds__(kMeshBlock) void k_mesh(MeshArgs a)
     __shared__ int s_ticket;
     const int k = resolve_k(a.sc);
     const float scale = pow2f(k);
-    const float inv = pow2f(-k);
+    const float inv = deq_scale(a.sc, k);
     // this call's number, kept on the device so that graph replays advance it too
     const uint32_t epoch = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const int W = a.W;
@@ -384,6 +384,7 @@ extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
     a.sc.k = l->scale_exp;
     a.sc.amax_bits = l->amax_bits;
     a.sc.scale_R = l->scale_R;
+    a.sc.out_shift = l->out_shift;
     hipStream_t st = (hipStream_t)stream;
     const dim3 g((unsigned)l->grid), b(kMeshBlock);
     switch (l->R) {

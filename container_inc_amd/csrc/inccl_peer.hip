@@ -55,7 +55,7 @@ __device__ __forceinline__ u32x4 ld_sys16(const void* tile_base, uint32_t tile_b
 template <int R, int BLOCK, bool DEQ>
 __global__ __launch_bounds__(BLOCK) void k_peer_reduce(SrcPtrs src, float* __restrict__ dst, int64_t n4, Scale sc)
 {
-    const float inv = DEQ ? pow2f(-resolve_k(sc)) : 1.0f;
+    const float inv = DEQ ? deq_scale(sc, resolve_k(sc)) : 1.0f;
     u32x4* __restrict__ out = reinterpret_cast<u32x4*>(dst);
     for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n4; base += (int64_t)gridDim.x * BLOCK) {
         const int64_t i = base + threadIdx.x;
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(BLOCK) void k_peer_reduce(SrcPtrs src, float* __res
 template <int R, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_peer_reduce_bf16(SrcPtrs src, uint16_t* __restrict__ dst, int64_t n4, Scale sc)
 {
-    const float inv = pow2f(-resolve_k(sc));
+    const float inv = deq_scale(sc, resolve_k(sc));
     for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n4; base += (int64_t)gridDim.x * BLOCK) {
         const int64_t i = base + threadIdx.x;
         const int64_t left = n4 - base;
@@ -187,7 +187,7 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 }  // namespace
 
 extern "C" int inccl_k_peer_reduce(const void* const* peers, int W, float* dst, size_t n, int scale_exp,
-                                   const uint32_t* amax_bits_dev, int scale_R, void* stream)
+                                   const uint32_t* amax_bits_dev, int scale_R, int out_shift, void* stream)
 {
     if (W < 1 || W > kMaxR || dst == nullptr || (n & 3) != 0 || !aligned16(dst)) return INCCL_ERR_ARG;
     if (n == 0) return 0;
@@ -196,7 +196,7 @@ extern "C" int inccl_k_peer_reduce(const void* const* peers, int W, float* dst, 
         if (peers[j] == nullptr || !aligned16(peers[j])) return INCCL_ERR_ARG;
         s.p[j] = peers[j];
     }
-    Scale sc{scale_exp, amax_bits_dev, scale_R > 0 ? scale_R : W};
+    Scale sc{scale_exp, amax_bits_dev, scale_R > 0 ? scale_R : W, out_shift};
     const int64_t n4 = (int64_t)(n >> 2);
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
@@ -214,7 +214,7 @@ extern "C" int inccl_k_peer_reduce(const void* const* peers, int W, float* dst, 
 }
 
 extern "C" int inccl_k_peer_reduce_bf16(const void* const* peers, int W, uint16_t* dst, size_t n, int scale_exp,
-                                        const uint32_t* amax_bits_dev, int scale_R, void* stream)
+                                        const uint32_t* amax_bits_dev, int scale_R, int out_shift, void* stream)
 {
     if (W < 1 || W > kMaxR || dst == nullptr || (n & 3) != 0 || (reinterpret_cast<uintptr_t>(dst) & 7u) != 0)
         return INCCL_ERR_ARG;
@@ -224,7 +224,7 @@ extern "C" int inccl_k_peer_reduce_bf16(const void* const* peers, int W, uint16_
         if (peers[j] == nullptr || !aligned16(peers[j])) return INCCL_ERR_ARG;
         s.p[j] = peers[j];
     }
-    Scale sc{scale_exp, amax_bits_dev, scale_R > 0 ? scale_R : W};
+    Scale sc{scale_exp, amax_bits_dev, scale_R > 0 ? scale_R : W, out_shift};
     const int64_t n4 = (int64_t)(n >> 2);
     hipStream_t st = (hipStream_t)stream;
     switch (W) {

@@ -27,9 +27,14 @@ struct Scale {
     int k;
     const uint32_t* amax_bits;  // nullptr -> use k
     int scale_R;                // contributors for auto scale
+    int out_shift;              // dequantise with 2^-(k + out_shift): the sum / 2^out_shift
+                                // (inccl_comm_set_average); exact, so bit-equal to dividing after
 };
 
 __device__ __forceinline__ float pow2f(int k) { return __uint_as_float((uint32_t)(k + 127) << 23); }
+
+struct Scale;
+__device__ __forceinline__ float deq_scale(const Scale& s, int k);
 
 // Same arithmetic as orc_choose_scale (oracle/inccl_oracle.c).
 __device__ __forceinline__ int choose_scale(float amax, int R)
@@ -44,6 +49,8 @@ __device__ __forceinline__ int choose_scale(float amax, int R)
     k = k > INCCL_SCALE_MAX ? INCCL_SCALE_MAX : k;
     return k;
 }
+
+__device__ __forceinline__ float deq_scale(const Scale& s, int k) { return pow2f(-k - s.out_shift); }
 
 __device__ __forceinline__ int resolve_k(const Scale& s)
 {
@@ -119,7 +126,7 @@ __global__ __launch_bounds__(BLOCK) void k_stream_vec(SrcPtrs src, void* __restr
 {
     const int k = resolve_k(sc);
     const float scale = pow2f(k);
-    const float inv = pow2f(-k);
+    const float inv = deq_scale(sc, k);
     const int64_t tile_elems = (int64_t)BLOCK * U;
     const int64_t stride = (int64_t)gridDim.x * tile_elems;
     u32x4* __restrict__ out = reinterpret_cast<u32x4*>(dst);
@@ -228,7 +235,7 @@ __global__ __launch_bounds__(BLOCK) void k_stream16(SrcPtrs src, void* __restric
     constexpr int VO = OUT == BF16 ? 1 : 2;   // u32x4 per group of output
     const int k = resolve_k(sc);
     const float scale = pow2f(k);
-    const float inv = pow2f(-k);
+    const float inv = deq_scale(sc, k);
     const int64_t tile = (int64_t)BLOCK * U;
     u32x4* __restrict__ out = reinterpret_cast<u32x4*>(dst);
 

@@ -143,6 +143,7 @@ int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R
     l.scale_exp = k;
     l.amax_bits = amax;
     l.scale_R = scale_R;
+    l.out_shift = c->out_shift;
     /* the parity argument needs this rank's calls in order: chain across streams
      * (inside a graph capture the caller's single capture stream orders them) */
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;

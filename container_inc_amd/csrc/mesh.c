@@ -277,6 +277,7 @@ int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int
     l.scale_exp = k;
     l.amax_bits = amax;
     l.scale_R = scale_R;
+    l.out_shift = c->out_shift;
     /* the buffer-reuse argument needs this rank's calls in order: chain across
      * streams (inside a capture the caller's capture stream orders them) */
     if (!capturing && c->mesh_last_stream && c->mesh_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[6], 0));

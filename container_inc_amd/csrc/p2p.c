@@ -204,7 +204,7 @@ int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int 
     /* 3. pull shard `me` from every peer, sum, dequantise */
     const void *peer[INCCL_MAX_LOCAL_INPUTS];
     for (int j = 0; j < W; ++j) peer[j] = c->p2p_peer_part[j] + (size_t)me * shard;
-    rc = inccl_k_peer_reduce(peer, W, c->p2p_res + (size_t)me * shard, shard, k, amax, scale_R, st);
+    rc = inccl_k_peer_reduce(peer, W, c->p2p_res + (size_t)me * shard, shard, k, amax, scale_R, c->out_shift, st);
     if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p reduce-scatter launch failed (%d)", rc);
     rc = sync_and_barrier(c, st);
     if (rc) return rc;
@@ -248,7 +248,8 @@ int inccl_p2p_piece_bf16(struct inccl_communicator *c, const uint16_t *const *sr
     if (rc) return rc;
     const void *peer[INCCL_MAX_LOCAL_INPUTS];
     for (int j = 0; j < W; ++j) peer[j] = c->p2p_peer_part[j] + (size_t)me * shard;
-    rc = inccl_k_peer_reduce_bf16(peer, W, (uint16_t *)c->p2p_res + (size_t)me * shard, shard, k, amax, scale_R, st);
+    rc = inccl_k_peer_reduce_bf16(peer, W, (uint16_t *)c->p2p_res + (size_t)me * shard, shard, k, amax, scale_R,
+                                  c->out_shift, st);
     if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p bf16 reduce-scatter launch failed (%d)", rc);
     rc = sync_and_barrier(c, st);
     if (rc) return rc;

@@ -39,6 +39,21 @@ class HookState:
     scale_exp: int = inccl.SCALE_AUTO
     average: bool = True
     calls: int = 0
+    folded: bool | None = None   # the mean comes out of the dequantise stage (inccl_comm_set_average)
+
+    def fold_average(self) -> bool:
+        """Once: let the engine return the mean (power-of-two worlds: 2^-log2 W is
+        folded into the dequantise scale, bit-identical to dividing, one pass
+        fewer); otherwise the hook divides."""
+        if self.folded is None:
+            self.folded = False
+            if self.average and self.world_size > 1 and hasattr(self.comm, "set_average"):
+                try:
+                    self.comm.set_average(True)
+                    self.folded = True
+                except IncclError:
+                    pass
+        return self.folded
 
     @property
     def world_size(self) -> int:
@@ -61,9 +76,10 @@ def allreduce_hook(state: HookState, bucket):
         raise IncclError(f"inccl DDP hook: fp32 or bf16 gradient buckets only, got {buf.dtype}")
     reduce = state.comm.allreduce_f32 if buf.dtype == torch.float32 else state.comm.allreduce_bf16
     w = state.world_size
+    divide = state.average and w > 1 and not state.fold_average()
     if not buf.is_cuda:   # reaches the communicator, which refuses it ("must live on the GPU")
         reduce([buf], out=buf, scale_exp=state.scale_exp, stream=None)
-        if state.average and w > 1:
+        if divide:
             buf.div_(w)
         fut = torch.futures.Future()
     else:
@@ -71,7 +87,7 @@ def allreduce_hook(state: HookState, bucket):
         side.wait_stream(torch.cuda.current_stream(buf.device))
         with torch.cuda.stream(side):
             reduce([buf], out=buf, scale_exp=state.scale_exp, stream=side.cuda_stream)
-            if state.average and w > 1:
+            if divide:
                 buf.div_(w)
             # the bucket is used on `side` now: the caching allocator must not
             # hand its memory out before this stream's work is done

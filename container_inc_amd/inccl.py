@@ -266,6 +266,11 @@ class Communicator:
             check(rc, "inccl_comm_clear_error")
         return rc == 1
 
+    def set_average(self, on: bool = True) -> None:
+        """Results of allreduce_f32 / _bf16 become the mean over ranks (power-of-two
+        worlds; raises IncclError otherwise).  Bit-identical to sum / W."""
+        check(load().inccl_comm_set_average(self.handle, 1 if on else 0), "inccl_comm_set_average")
+
     # -- reference collectives on host int32 arrays (api.c:330-452) --
     def allreduce_write(self, src: np.ndarray, length: int, dst: np.ndarray) -> None:
         _host_int32_call(load().inccl_allreduce_write, self.handle, src, length, dst)

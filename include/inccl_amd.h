@@ -156,6 +156,12 @@ int inccl_comm_ipc_mem_kind(struct inccl_communicator *comm, const char *engine)
  * them from a clean state.  Check a call's outcome after synchronising its
  * stream: a timeout is reported by the NEXT call or by this function. */
 int inccl_comm_clear_error(struct inccl_communicator *comm);
+/* on != 0: every later inccl_allreduce_f32 / _bf16 (and _f32_host) of this rank
+ * returns the MEAN over the ranks instead of the sum -- the dequantise stage
+ * scales by 2^-(k + log2 W), which is exact, so the result is bit-identical to
+ * dividing the sum by W, without the extra pass over the bucket.  Only for a
+ * power-of-two world size (else INCCL_ERR_ARG).  Set it alike on every rank. */
+int inccl_comm_set_average(struct inccl_communicator *comm, int on);
 
 /* Device-resident fp32 allreduce of R local buckets per rank:
  *   dst = dequant( sum over ranks, sum over r<R  quant(srcs[r]) )

@@ -290,6 +290,48 @@ def test_allreduce_f32_local(gpu, orc, world, R, n, chunks, k):
         np.testing.assert_array_equal(res.view(np.uint32), want.view(np.uint32))
 
 
+@pytest.mark.parametrize("world,chunks", [(1, 1), (2, 1), (4, 3), (8, 1)])
+def test_allreduce_average_local(gpu, orc, world, chunks):
+    """inccl_comm_set_average: the mean, bit-identical to oracle sum / W, fp32 and bf16."""
+    import torch
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(600 + world)
+    n = (1 << 18) + 64 * 3
+    xs = [[(rng.standard_normal(n) * 2).astype(np.float32) for _ in range(2)] for _ in range(world)]
+    every = [x for per in xs for x in per]
+    k = orc.choose_scale(orc.absmax(every), world * 2)
+    want = orc.reduce_f32(every, k) / np.float32(world)
+    hs = [[torch.from_numpy(x).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16) for x in per]
+          for per in xs]
+    every16 = [h for per in hs for h in per]
+    k16 = orc.choose_scale(orc.absmax_bf16(every16), world * 2)
+    s16 = torch.from_numpy(orc.reduce_bf16(every16, k16).view(np.int16)).view(torch.bfloat16)
+    want16 = (s16 / world).view(torch.int16).numpy().view(np.uint16)
+    dev_in = [[torch.from_numpy(x).to(gpu) for x in per] for per in xs]
+    dev16 = [[torch.from_numpy(h.view(np.int16)).to(gpu).view(torch.bfloat16) for h in per] for per in hs]
+    torch.cuda.synchronize()
+    hub = f"avg-{world}-{chunks}"
+
+    def rank(r):
+        grp = inccl.inccl_group_create_local(world, r, hub)
+        comm = inccl.inccl_communicator_create(grp, 0)
+        comm.set_average(True)
+        out = torch.empty(n, dtype=torch.float32, device=gpu)
+        out16 = torch.empty(n, dtype=torch.bfloat16, device=gpu)
+        comm.allreduce_f32(dev_in[r], out=out, scale_exp=inccl.SCALE_AUTO, chunks=chunks, stream=comm.stream)
+        comm.allreduce_bf16(dev16[r], out=out16, scale_exp=inccl.SCALE_AUTO, stream=comm.stream)
+        torch.cuda.synchronize()
+        comm.barrier()
+        res = (out.cpu().numpy(), out16.view(torch.int16).cpu().numpy().view(np.uint16))
+        comm.destroy()
+        grp.destroy()
+        return res
+
+    for res, res16 in _run_ranks(world, rank):
+        np.testing.assert_array_equal(res.view(np.uint32), want.view(np.uint32))
+        np.testing.assert_array_equal(res16, want16)
+
+
 @pytest.fixture()
 def force_rccl(monkeypatch):
     monkeypatch.setenv("INCCL_FORCE_RCCL", "1")

@@ -100,6 +100,28 @@ def _rank_main(rank, world, port, cases, q, engine="p2p", device=0):
                                stream=comm.stream)
             torch.cuda.synchronize()
             results.append(bool(np.array_equal(srcs[0].cpu().numpy().view(np.uint32), want.view(np.uint32))))
+        # the mean instead of the sum (inccl_comm_set_average): bit-identical to the
+        # oracle's sum / W for a power-of-two world, refused otherwise
+        pow2 = world & (world - 1) == 0
+        try:
+            comm.set_average(True)
+            results.append(pow2)
+        except Exception:  # noqa: BLE001
+            results.append(not pow2)
+        if pow2:
+            for R, n, k, seed in ((2, 200_003, "auto", 51), (1, 1 << 20, 24, 52)):
+                xs = _inputs(world, R, n, seed)
+                every = [x for per in xs for x in per]
+                kk = O.choose_scale(O.absmax(every), world * R) if k == "auto" else k
+                want = O.reduce_f32(every, kk) / np.float32(world)
+                srcs = [torch.from_numpy(x).to(dev) for x in xs[rank]]
+                out = torch.empty(n, device=dev)
+                torch.cuda.synchronize()
+                comm.allreduce_f32(srcs, out=out, scale_exp=inccl.SCALE_AUTO if k == "auto" else k,
+                                   stream=comm.stream)
+                torch.cuda.synchronize()
+                results.append(bool(np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))))
+            comm.set_average(False)
         if engine in ("ll", "mesh", "meshw"):
             # hipGraph: three calls captured once, replayed with fresh inputs (the
             # call counter lives on the device, so every replay is a new call)
