@@ -112,11 +112,11 @@ __device__ __forceinline__ uint32_t abs_bits(uint32_t b)
 }
 
 template <int R>
-__global__ __launch_bounds__(kBlock) void k_absmax(SrcPtrs src, int64_t n, uint32_t* __restrict__ out)
+__global__ __launch_bounds__(kBlock) void k_absmax(SrcPtrs src, int64_t n, uint32_t* __restrict__ out, int vec)
 {
     __shared__ uint32_t part[kBlock / 64];
     uint32_t m = 0;
-    const int64_t n4 = n >> 2;
+    const int64_t n4 = vec ? n >> 2 : 0;   // a bucket not 16-B aligned: element loads only
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
 #pragma unroll
@@ -149,11 +149,11 @@ __global__ __launch_bounds__(kBlock) void k_absmax(SrcPtrs src, int64_t n, uint3
 __device__ __forceinline__ uint32_t abs_bits_bf16(uint32_t h) { return abs_bits(h << 16); }
 
 template <int R>
-__global__ __launch_bounds__(kBlock) void k_absmax_bf16(SrcPtrs src, int64_t n, uint32_t* __restrict__ out)
+__global__ __launch_bounds__(kBlock) void k_absmax_bf16(SrcPtrs src, int64_t n, uint32_t* __restrict__ out, int vec)
 {
     __shared__ uint32_t part[kBlock / 64];
     uint32_t m = 0;
-    const int64_t n8 = n >> 3;
+    const int64_t n8 = vec ? n >> 3 : 0;   // a bucket not 16-B aligned: element loads only
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
 #pragma unroll
@@ -392,9 +392,11 @@ int inccl_k_absmax(const float* const* srcs, int R, size_t n, uint32_t* amax_bit
     hipStream_t st = (hipStream_t)stream;
     if (R < 1 || R > kMaxR || amax_bits_dev == nullptr) return INCCL_ERR_ARG;
     SrcPtrs s = {};
+    int vec = 1;
     for (int r = 0; r < R; ++r) {
-        if (srcs[r] == nullptr || !aligned16(srcs[r])) return INCCL_ERR_ARG;
+        if (srcs[r] == nullptr) return INCCL_ERR_ARG;
         s.p[r] = srcs[r];
+        vec = vec && aligned16(srcs[r]);
     }
     if (zero_first) {
         hipError_t e = hipMemsetAsync(amax_bits_dev, 0, sizeof(uint32_t), st);
@@ -406,7 +408,7 @@ int inccl_k_absmax(const float* const* srcs, int R, size_t n, uint32_t* amax_bit
     const int grid = (int)(blocks < 1 ? 1 : (blocks < cap ? blocks : cap));
     switch (R) {
 #define INCCL_AM(RR) \
-    case RR: hipLaunchKernelGGL((k_absmax<RR>), dim3(grid), dim3(kBlock), 0, st, s, (int64_t)n, amax_bits_dev); break;
+    case RR: hipLaunchKernelGGL((k_absmax<RR>), dim3(grid), dim3(kBlock), 0, st, s, (int64_t)n, amax_bits_dev, vec); break;
         INCCL_AM(1) INCCL_AM(2) INCCL_AM(3) INCCL_AM(4) INCCL_AM(5) INCCL_AM(6) INCCL_AM(7) INCCL_AM(8)
 #undef INCCL_AM
     }
@@ -419,9 +421,11 @@ int inccl_k_absmax_bf16(const uint16_t* const* srcs, int R, size_t n, uint32_t* 
     hipStream_t st = (hipStream_t)stream;
     if (R < 1 || R > kMaxR || amax_bits_dev == nullptr) return INCCL_ERR_ARG;
     SrcPtrs s = {};
+    int vec = 1;
     for (int r = 0; r < R; ++r) {
-        if (srcs[r] == nullptr || !aligned16(srcs[r])) return INCCL_ERR_ARG;
+        if (srcs[r] == nullptr) return INCCL_ERR_ARG;
         s.p[r] = srcs[r];
+        vec = vec && aligned16(srcs[r]);
     }
     if (zero_first) {
         hipError_t e = hipMemsetAsync(amax_bits_dev, 0, sizeof(uint32_t), st);
@@ -433,7 +437,9 @@ int inccl_k_absmax_bf16(const uint16_t* const* srcs, int R, size_t n, uint32_t* 
     const int grid = (int)(blocks < 1 ? 1 : (blocks < cap ? blocks : cap));
     switch (R) {
 #define INCCL_AM(RR) \
-    case RR: hipLaunchKernelGGL((k_absmax_bf16<RR>), dim3(grid), dim3(kBlock), 0, st, s, (int64_t)n, amax_bits_dev); break;
+    case RR:                                                                                                    \
+        hipLaunchKernelGGL((k_absmax_bf16<RR>), dim3(grid), dim3(kBlock), 0, st, s, (int64_t)n, amax_bits_dev, vec); \
+        break;
         INCCL_AM(1) INCCL_AM(2) INCCL_AM(3) INCCL_AM(4) INCCL_AM(5) INCCL_AM(6) INCCL_AM(7) INCCL_AM(8)
 #undef INCCL_AM
     }

@@ -36,7 +36,8 @@ def _host(t):
 
 @pytest.mark.parametrize("R,n,k,shift", [(1, 8, 20, 0), (2, 1000, 22, 0), (2, 1 << 20, 25, 0),
                                          (3, (1 << 20) + 13, "auto", 0), (8, 3_000_001, "auto", 0),
-                                         (2, 100_003, 24, 1), (3, 40_000, 40, 0), (2, 4099, 40, 1)])
+                                         (2, 100_003, 24, 1), (3, 40_000, 40, 0), (2, 4099, 40, 1),
+                                         (3, 50_001, "auto", 3)])
 def test_reduce_bf16_kernel(gpu, orc, R, n, k, shift):
     """k = 40 saturates most lanes (|x| * 2^40 > 2^31) and wraps their sums."""
     import torch

@@ -131,14 +131,18 @@ def test_sum_dequant(gpu, orc, R):
     _bits_equal(out, orc.dequantise(orc.sum_q32(qs), 25))
 
 
-@pytest.mark.parametrize("R", [1, 2, 8])
-def test_absmax_and_auto_scale(gpu, orc, R):
+@pytest.mark.parametrize("R,shift", [(1, 0), (2, 0), (8, 0), (2, 1), (3, 3)])
+def test_absmax_and_auto_scale(gpu, orc, R, shift):
+    """shift > 0: buckets that start `shift` elements past a 16-B boundary (the
+    absmax then reads elements only, the reduce takes the element kernel)."""
+    import torch
     from container_inc_amd import inccl
     rng = np.random.default_rng(77 + R)
     n = 100_003
     xs = [(rng.standard_normal(n) * 3).astype(np.float32) for _ in range(R)]
     xs[0][17] = np.nan
-    ts = [_t(x, gpu) for x in xs]
+    xs[-1][n - 1] = -7.5   # the largest magnitude, in the ragged tail
+    ts = [torch.from_numpy(np.concatenate([np.zeros(shift, np.float32), x])).to(gpu)[shift:] for x in xs]
     amax = inccl.absmax(ts)
     assert amax == orc.absmax(xs)
     k = orc.choose_scale(amax, R)
