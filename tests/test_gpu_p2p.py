@@ -164,11 +164,11 @@ def _rank_main(rank, world, port, cases, q, engine="p2p", device=0):
 
 
 P2P_CASES = [(2, 1 << 20, 25, 11), (1, 100_003, 20, 12), (2, 65_536 * 3 + 5, "auto", 13), (2, 4 << 20, 24, 14),
-             (2, 300_001, 25, 15, 1)]
+             (2, 300_001, 25, 15, 1), (2, 65_536 * 3 + 5, "auto", 16, 1)]
 # the ll kernel: tiny, ragged, unaligned, one workgroup, the 256-workgroup cap, the
 # 1 MiB slot exactly, and one bucket above it (served by the p2p exchange)
 LL_CASES = [(2, 1, 25, 21), (1, 1000, 20, 22), (3, 4099, 25, 23, 1), (2, 65_536 * 3 + 5, "auto", 24),
-            (8, 262_144, 22, 25), (2, 262_143, 25, 26, 3), (2, 300_000, 25, 27)]
+            (8, 262_144, 22, 25), (2, 262_143, 25, 26, 3), (2, 300_000, 25, 27), (2, 4099, "auto", 28, 1)]
 
 
 # the mesh kernel: one chunk, many chunks (256 per shard), ragged ends inside and
