@@ -231,3 +231,45 @@ def test_allreduce_bf16_p2p_multiprocess(gpu, world):
         ok, err = res[r]
         assert err is None, f"rank {r}: {err}"
         assert all(ok), f"rank {r}: {ok}"
+
+
+@pytest.mark.parametrize("engine,average", [("rccl", False), ("ar", True)])
+def test_allreduce_bf16_graph_capture_world1(gpu, orc, monkeypatch, engine, average):
+    """inccl_allreduce_bf16 captured into a hipGraph on the RCCL engines (world 1,
+    sharded path forced): three captured calls replayed with fresh inputs,
+    bit-exact vs the oracle (set_average at world 1 is the identity)."""
+    import torch
+    from container_inc_amd import inccl
+    monkeypatch.setenv("INCCL_FORCE_RCCL", "1")
+    monkeypatch.setenv("INCCL_FORCE_SHARDED", "1")
+    monkeypatch.setenv("INCCL_MASTER_PORT", "0")
+    grp = inccl.inccl_group_create(1, 0, "127.0.0.1")
+    comm = inccl.inccl_communicator_create(grp, 0)
+    comm.set_engine(engine)
+    comm.set_average(average)
+    n = (1 << 18) + 64
+    bufs = [torch.empty(n, device=gpu, dtype=torch.bfloat16) for _ in range(2)]
+    outs = [torch.empty(n, device=gpu, dtype=torch.bfloat16) for _ in range(3)]
+    st = torch.cuda.Stream(device=gpu)
+    comm.allreduce_bf16(bufs, out=outs[0], scale_exp=24, stream=st.cuda_stream)   # workspaces sized eagerly
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=st):
+        for o in outs:
+            comm.allreduce_bf16(bufs, out=o, scale_exp=24, stream=st.cuda_stream)
+    rng = np.random.default_rng(78)
+    for _ in range(3):
+        hs = [_bf16(rng, n) for _ in range(2)]
+        for b, h in zip(bufs, hs):
+            b.copy_(_dev(h, gpu))
+        for o in outs:
+            o.fill_(float("nan"))
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+        want = orc.reduce_bf16(hs, 24)
+        for o in outs:
+            np.testing.assert_array_equal(_host(o), want)
+    del graph
+    comm.destroy()
+    grp.destroy()
