@@ -661,7 +661,7 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
     const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: RS/AG path even at world 1 */
     if (W == 1 && !(fs && atoi(fs) != 0))   /* one fused HBM pass: quant + sum + dequant */
         return kerr(inccl_k_stream_s(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, k,
-                                   amax, scale_R, c->out_shift, st));
+                                     amax, scale_R, c->out_shift, st));
 
     /* the IPC engines: the ll kernel for small buckets when the ll engine was
      * chosen explicitly (ll.c), else the one-kernel mesh exchange (mesh.c) or the
