@@ -39,6 +39,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -951,11 +952,44 @@ def main():
         algbw = n * 4 / (ms_per_step * 1e-3) / 1e9
         res["collective"] = {"algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2),
                              "bytes_per_rank": n * 4}
+    # The one JSON line, printed once: by the main thread at the end, or by the
+    # sweep guard below if the N > 1 sweep overruns its budget.
+    emit_lock, emitted = threading.Lock(), [False]
+
+    def emit():
+        with emit_lock:
+            if emitted[0]:
+                return False
+            emitted[0] = True
+        if rank == 0:
+            line = json.dumps(dict(res))   # a snapshot: the guard thread may emit while the main thread works
+            print(line, flush=True)
+            if a.json_out:
+                with open(a.json_out, "w") as f:
+                    f.write(line + "\n")
+        return True
+
     if world > 1 and not a.no_sweep:
         for key in chosen[2]:   # the sweep runs every engine with its defaults
             os.environ.pop(key, None)
+        # The sweep and the bf16 key run after the headline is measured.  They
+        # drive engines never before run across separate GPUs: should a collective
+        # hang there, the guard still emits the headline line (the sweep marked
+        # unfinished) and ends every rank, instead of losing the whole run.
+        budget = float(os.environ.get("INCCL_BENCH_SWEEP_BUDGET", "600"))
+
+        def overrun():
+            res["sweep_error"] = f"sweep / bf16 key unfinished after {budget:.0f} s; headline kept"
+            res.setdefault("sweep", None)
+            emit()
+            os._exit(0)
+
+        guard = threading.Timer(budget, overrun)
+        guard.daemon = True
+        guard.start()
         res["sweep"] = size_sweep(comm, dev, R, k, rank, world)
         res["bf16"] = bf16_engines(comm, dev, R, rank, world)
+        guard.cancel()
         comm.set_engine(chosen[0])
     def extra(key, fn):
         """An N = 1 extra key (one process, no collectives): a failure is recorded
@@ -978,12 +1012,7 @@ def main():
         extra("cpu_baseline", lambda: cpu_baseline(n, R, k, a.cpu_seconds))
         extra("cpu_baseline_allcores", lambda: cpu_baseline_allcores(n, R, k, min(a.cpu_seconds, 5.0)))
         extra("cpu_reference_pipeline", lambda: cpu_reference_pipeline(min(a.cpu_seconds, 5.0)))
-    if rank == 0:
-        line = json.dumps(res)
-        print(line, flush=True)
-        if a.json_out:
-            with open(a.json_out, "w") as f:
-                f.write(line + "\n")
+    emit()
     comm.destroy()
     grp.destroy()
     if world > 1:
