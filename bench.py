@@ -987,6 +987,8 @@ def main():
         guard = threading.Timer(budget, overrun)
         guard.daemon = True
         guard.start()
+        if os.environ.get("INCCL_BENCH_TEST_HANG") == "1" and rank == 0:   # test hook: a stuck rank 0
+            time.sleep(1e9)
         res["sweep"] = size_sweep(comm, dev, R, k, rank, world)
         res["bf16"] = bf16_engines(comm, dev, R, rank, world)
         guard.cancel()
