@@ -111,68 +111,62 @@ __device__ __forceinline__ uint32_t abs_bits(uint32_t b)
     return a > 0x7f800000u ? 0u : a;
 }
 
-template <int R>
-__global__ __launch_bounds__(kBlock) void k_absmax(SrcPtrs src, int64_t n, uint32_t* __restrict__ out, int vec)
-{
-    __shared__ uint32_t part[kBlock / 64];
-    uint32_t m = 0;
-    const int64_t n4 = vec ? n >> 2 : 0;   // a bucket not 16-B aligned: element loads only
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const u32x4* p = reinterpret_cast<const u32x4*>(src.p[r]);
-        for (int64_t i = t0; i < n4; i += stride) {
-            const u32x4 x = __builtin_nontemporal_load(p + i);
-            const uint32_t a = max(max(abs_bits(x.x), abs_bits(x.y)), max(abs_bits(x.z), abs_bits(x.w)));
-            m = m > a ? m : a;
-        }
-        const uint32_t* s = reinterpret_cast<const uint32_t*>(src.p[r]);
-        for (int64_t i = (n4 << 2) + t0; i < n; i += stride) {
-            const uint32_t a = abs_bits(s[i]);
-            m = m > a ? m : a;
-        }
-    }
-    m = wave_max_u32(m);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) part[wave] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t b = part[0];
-#pragma unroll
-        for (int w = 1; w < kBlock / 64; ++w) b = b > part[w] ? b : part[w];
-        atomicMax(out, b);
-    }
-}
-
 // absmax over bf16 buckets, as the fp32 bits of the widened values
 __device__ __forceinline__ uint32_t abs_bits_bf16(uint32_t h) { return abs_bits(h << 16); }
 
-template <int R>
-__global__ __launch_bounds__(kBlock) void k_absmax_bf16(SrcPtrs src, int64_t n, uint32_t* __restrict__ out, int vec)
+template <bool B16>
+__device__ __forceinline__ uint32_t amax_quad(u32x4 x)
 {
-    __shared__ uint32_t part[kBlock / 64];
+    if constexpr (B16)
+        return max(max(max(abs_bits_bf16(x.x & 0xffffu), abs_bits_bf16(x.x >> 16)),
+                       max(abs_bits_bf16(x.y & 0xffffu), abs_bits_bf16(x.y >> 16))),
+                   max(max(abs_bits_bf16(x.z & 0xffffu), abs_bits_bf16(x.z >> 16)),
+                       max(abs_bits_bf16(x.w & 0xffffu), abs_bits_bf16(x.w >> 16))));
+    else
+        return max(max(abs_bits(x.x), abs_bits(x.y)), max(abs_bits(x.z), abs_bits(x.w)));
+}
+
+// max |x| over R buckets of fp32 (B16 = false) or bf16 (B16 = true) elements.
+// Geometry from tools/tune/tune_absmax.hip (R = 2 x 256 MiB fp32,
+// profiles/r02/tune_absmax.jsonl): 512 lanes x 2 quads per input and step, all
+// 2R loads in flight before the first compare, grid capped at 2 workgroups per
+// CU -- 0.83-0.84 of HBM, against 0.73 for the round-1 form (256 x 1, 8 per CU).
+constexpr int kAmBlock = 512, kAmU = 2;
+
+template <int R, bool B16>
+__global__ __launch_bounds__(kAmBlock) void k_absmax(SrcPtrs src, int64_t n, uint32_t* __restrict__ out, int vec)
+{
+    constexpr int EPQ = B16 ? 8 : 4;   // elements per 16-B quad
+    __shared__ uint32_t part[kAmBlock / 64];
     uint32_t m = 0;
-    const int64_t n8 = vec ? n >> 3 : 0;   // a bucket not 16-B aligned: element loads only
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t nq = vec ? n / EPQ : 0;   // a bucket not 16-B aligned: element loads only
+    const int64_t tile = (int64_t)kAmBlock * kAmU;
+    for (int64_t base = (int64_t)blockIdx.x * tile; base < nq; base += (int64_t)gridDim.x * tile) {
+        u32x4 v[R][kAmU];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const u32x4* p = reinterpret_cast<const u32x4*>(src.p[r]);
-        for (int64_t i = t0; i < n8; i += stride) {
-            const u32x4 x = __builtin_nontemporal_load(p + i);
-            const uint32_t a = max(max(max(abs_bits_bf16(x.x & 0xffffu), abs_bits_bf16(x.x >> 16)),
-                                       max(abs_bits_bf16(x.y & 0xffffu), abs_bits_bf16(x.y >> 16))),
-                                   max(max(abs_bits_bf16(x.z & 0xffffu), abs_bits_bf16(x.z >> 16)),
-                                       max(abs_bits_bf16(x.w & 0xffffu), abs_bits_bf16(x.w >> 16))));
-            m = m > a ? m : a;
-        }
-        const uint16_t* s = reinterpret_cast<const uint16_t*>(src.p[r]);
-        for (int64_t i = (n8 << 3) + t0; i < n; i += stride) {
-            const uint32_t a = abs_bits_bf16(s[i]);
-            m = m > a ? m : a;
-        }
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < kAmU; ++u) {
+                const int64_t i = base + threadIdx.x + (int64_t)u * kAmBlock;
+                v[r][u] = i < nq ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src.p[r]) + i)
+                                 : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < kAmU; ++u) {
+                const uint32_t a = amax_quad<B16>(v[r][u]);
+                m = m > a ? m : a;
+            }
     }
+    const int64_t stride = (int64_t)gridDim.x * kAmBlock;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        for (int64_t i = nq * EPQ + (int64_t)blockIdx.x * kAmBlock + threadIdx.x; i < n; i += stride) {
+            const uint32_t a = B16 ? abs_bits_bf16(reinterpret_cast<const uint16_t*>(src.p[r])[i])
+                                   : abs_bits(reinterpret_cast<const uint32_t*>(src.p[r])[i]);
+            m = m > a ? m : a;
+        }
     m = wave_max_u32(m);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) part[wave] = m;
@@ -180,7 +174,7 @@ __global__ __launch_bounds__(kBlock) void k_absmax_bf16(SrcPtrs src, int64_t n, 
     if (threadIdx.x == 0) {
         uint32_t b = part[0];
 #pragma unroll
-        for (int w = 1; w < kBlock / 64; ++w) b = b > part[w] ? b : part[w];
+        for (int w = 1; w < kAmBlock / 64; ++w) b = b > part[w] ? b : part[w];
         atomicMax(out, b);
     }
 }
@@ -369,6 +363,40 @@ bool scale_ok(int k) { return k >= INCCL_SCALE_MIN && k <= INCCL_SCALE_MAX; }
 
 }  // namespace
 
+namespace {
+
+template <bool B16>
+int launch_absmax(const void* const* srcs, int R, size_t n, uint32_t* amax_bits_dev, int zero_first, hipStream_t st)
+{
+    if (R < 1 || R > kMaxR || amax_bits_dev == nullptr) return INCCL_ERR_ARG;
+    SrcPtrs s = {};
+    int vec = 1;
+    for (int r = 0; r < R; ++r) {
+        if (srcs[r] == nullptr) return INCCL_ERR_ARG;
+        s.p[r] = srcs[r];
+        vec = vec && aligned16(srcs[r]);
+    }
+    if (zero_first) {
+        hipError_t e = hipMemsetAsync(amax_bits_dev, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return (int)e;
+    }
+    if (n == 0) return 0;
+    const int64_t tiles = ((int64_t)(n / (B16 ? 8 : 4)) + (int64_t)kAmBlock * kAmU - 1) / ((int64_t)kAmBlock * kAmU);
+    const int64_t cap = (int64_t)num_cus() * 2;
+    const int grid = (int)(tiles < 1 ? 1 : (tiles < cap ? tiles : cap));
+    switch (R) {
+#define INCCL_AM(RR)                                                                                             \
+    case RR:                                                                                                     \
+        hipLaunchKernelGGL((k_absmax<RR, B16>), dim3(grid), dim3(kAmBlock), 0, st, s, (int64_t)n, amax_bits_dev, vec); \
+        break;
+        INCCL_AM(1) INCCL_AM(2) INCCL_AM(3) INCCL_AM(4) INCCL_AM(5) INCCL_AM(6) INCCL_AM(7) INCCL_AM(8)
+#undef INCCL_AM
+    }
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
 extern "C" {
 
 int inccl_k_stream_s(int in_kind, int out_kind, const void* const* srcs, int R, void* dst, size_t n, int scale_exp,
@@ -389,61 +417,15 @@ int inccl_k_stream(int in_kind, int out_kind, const void* const* srcs, int R, vo
 
 int inccl_k_absmax(const float* const* srcs, int R, size_t n, uint32_t* amax_bits_dev, int zero_first, void* stream)
 {
-    hipStream_t st = (hipStream_t)stream;
-    if (R < 1 || R > kMaxR || amax_bits_dev == nullptr) return INCCL_ERR_ARG;
-    SrcPtrs s = {};
-    int vec = 1;
-    for (int r = 0; r < R; ++r) {
-        if (srcs[r] == nullptr) return INCCL_ERR_ARG;
-        s.p[r] = srcs[r];
-        vec = vec && aligned16(srcs[r]);
-    }
-    if (zero_first) {
-        hipError_t e = hipMemsetAsync(amax_bits_dev, 0, sizeof(uint32_t), st);
-        if (e != hipSuccess) return (int)e;
-    }
-    if (n == 0) return 0;
-    const int64_t blocks = ((int64_t)(n >> 2) + kBlock - 1) / kBlock;
-    const int64_t cap = (int64_t)num_cus() * 8;
-    const int grid = (int)(blocks < 1 ? 1 : (blocks < cap ? blocks : cap));
-    switch (R) {
-#define INCCL_AM(RR) \
-    case RR: hipLaunchKernelGGL((k_absmax<RR>), dim3(grid), dim3(kBlock), 0, st, s, (int64_t)n, amax_bits_dev, vec); break;
-        INCCL_AM(1) INCCL_AM(2) INCCL_AM(3) INCCL_AM(4) INCCL_AM(5) INCCL_AM(6) INCCL_AM(7) INCCL_AM(8)
-#undef INCCL_AM
-    }
-    return (int)hipGetLastError();
+    return launch_absmax<false>(reinterpret_cast<const void* const*>(srcs), R, n, amax_bits_dev, zero_first,
+                                (hipStream_t)stream);
 }
 
 int inccl_k_absmax_bf16(const uint16_t* const* srcs, int R, size_t n, uint32_t* amax_bits_dev, int zero_first,
                         void* stream)
 {
-    hipStream_t st = (hipStream_t)stream;
-    if (R < 1 || R > kMaxR || amax_bits_dev == nullptr) return INCCL_ERR_ARG;
-    SrcPtrs s = {};
-    int vec = 1;
-    for (int r = 0; r < R; ++r) {
-        if (srcs[r] == nullptr) return INCCL_ERR_ARG;
-        s.p[r] = srcs[r];
-        vec = vec && aligned16(srcs[r]);
-    }
-    if (zero_first) {
-        hipError_t e = hipMemsetAsync(amax_bits_dev, 0, sizeof(uint32_t), st);
-        if (e != hipSuccess) return (int)e;
-    }
-    if (n == 0) return 0;
-    const int64_t blocks = ((int64_t)(n >> 3) + kBlock - 1) / kBlock;
-    const int64_t cap = (int64_t)num_cus() * 8;
-    const int grid = (int)(blocks < 1 ? 1 : (blocks < cap ? blocks : cap));
-    switch (R) {
-#define INCCL_AM(RR) \
-    case RR:                                                                                                    \
-        hipLaunchKernelGGL((k_absmax_bf16<RR>), dim3(grid), dim3(kBlock), 0, st, s, (int64_t)n, amax_bits_dev, vec); \
-        break;
-        INCCL_AM(1) INCCL_AM(2) INCCL_AM(3) INCCL_AM(4) INCCL_AM(5) INCCL_AM(6) INCCL_AM(7) INCCL_AM(8)
-#undef INCCL_AM
-    }
-    return (int)hipGetLastError();
+    return launch_absmax<true>(reinterpret_cast<const void* const*>(srcs), R, n, amax_bits_dev, zero_first,
+                               (hipStream_t)stream);
 }
 
 int inccl_k_checksum(const int32_t* q, size_t n, uint64_t index_base, uint32_t* out_dev, int zero_first, void* stream)
