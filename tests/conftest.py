@@ -6,7 +6,6 @@ libinccl_amd.so (loads + exports, no compute), the TCP bootstrap, and the
 multi-rank shard plan over ``gloo``.
 """
 import os
-import subprocess
 import sys
 
 import pytest

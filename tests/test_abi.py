@@ -1,7 +1,6 @@
 """The C-ABI boundary: libinccl_amd.so loads and exports exactly what
 include/api.h and include/inccl_amd.h declare; the headers compile as plain C
 with no HIP/RCCL/torch headers.  No compute calls (CPU only)."""
-import ctypes
 import os
 import re
 import subprocess

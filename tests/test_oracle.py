@@ -1,7 +1,6 @@
 """The CPU oracle (oracle/inccl_oracle.c) pinned against the reference's own
 known answers and the spec's known-answer vectors.  CPU only."""
 import json
-import math
 import os
 import struct
 
