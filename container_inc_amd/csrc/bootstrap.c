@@ -224,6 +224,7 @@ struct inccl_shm_bar {
     _Atomic uint32_t count;
     _Atomic uint32_t generation;
     uint32_t world;
+    _Atomic uint32_t words[64];   /* one word per rank for small host reductions */
 };
 
 int inccl_boot_shm_init(struct inccl_group *g)
@@ -291,6 +292,34 @@ int inccl_group_barrier(struct inccl_group *g)
             sched_yield();
         }
     }
+    return 0;
+}
+
+/* max of one word over the group: through the shared-memory segment when the
+ * group has one (two barriers, a few microseconds), else the TCP allgather */
+int inccl_group_allreduce_max_u32(struct inccl_group *g, uint32_t *v)
+{
+    if (g->world_size == 1) return 0;
+    struct inccl_shm_bar *b = g->shm_bar;
+    if (b) {
+        atomic_store(&b->words[g->rank], *v);
+        int rc = inccl_group_barrier(g);   /* every word written */
+        if (rc) return rc;
+        uint32_t m = 0;
+        for (int j = 0; j < g->world_size; ++j) {
+            const uint32_t w = atomic_load(&b->words[j]);
+            m = w > m ? w : m;
+        }
+        *v = m;
+        return inccl_group_barrier(g);     /* every word read before the next call rewrites it */
+    }
+    uint32_t all[64];
+    if (g->world_size > 64) return inccl_set_error(INCCL_ERR_ARG, "max-allreduce: world too large");
+    int rc = inccl_boot_allgather(g, v, all, sizeof(*v));
+    if (rc) return rc;
+    uint32_t m = 0;
+    for (int j = 0; j < g->world_size; ++j) m = all[j] > m ? all[j] : m;
+    *v = m;
     return 0;
 }
 

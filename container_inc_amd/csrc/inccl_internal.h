@@ -184,6 +184,7 @@ int inccl_boot_barrier(struct inccl_group *g);
 int inccl_boot_allgather(struct inccl_group *g, const void *mine, void *all, size_t bytes);
 int inccl_boot_shm_init(struct inccl_group *g);   /* collective; falls back silently */
 int inccl_group_barrier(struct inccl_group *g);   /* shm barrier if set up, else TCP */
+int inccl_group_allreduce_max_u32(struct inccl_group *g, uint32_t *v);   /* through shm if set up, else TCP */
 void inccl_boot_close(struct inccl_group *g);
 
 /* errors */

@@ -298,18 +298,16 @@ static int ensure_rccl(struct inccl_communicator *c)
     return inccl_rccl_comm_init(c);
 }
 
-/* 4-byte max over the group through the bootstrap sockets (p2p engine) */
+/* 4-byte max over the group on the host (the IPC engines): the node's shared
+ * memory segment once the engine has set it up, else the bootstrap sockets */
 static int host_allreduce_max_u32(struct inccl_communicator *c, uint32_t *buf, hipStream_t st)
 {
-    struct inccl_group *g = c->group;
-    uint32_t v = 0, all[64];
-    if (g->world_size > 64) return inccl_set_error(INCCL_ERR_ARG, "host max-allreduce: world too large");
+    uint32_t v = 0;
     INCCL_HIP(hipMemcpyAsync(&v, buf, sizeof(v), hipMemcpyDeviceToHost, st));
     INCCL_HIP(hipStreamSynchronize(st));
-    int rc = inccl_boot_allgather(g, &v, all, sizeof(v));
+    int rc = inccl_group_allreduce_max_u32(c->group, &v);
     if (rc) return rc;
-    uint32_t m = 0;
-    for (int j = 0; j < g->world_size; ++j) m = all[j] > m ? all[j] : m;
+    const uint32_t m = v;
     INCCL_HIP(hipMemcpyAsync(buf, &m, sizeof(m), hipMemcpyHostToDevice, st));
     INCCL_HIP(hipStreamSynchronize(st));
     return 0;
