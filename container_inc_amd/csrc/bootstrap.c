@@ -301,7 +301,8 @@ int inccl_group_allreduce_max_u32(struct inccl_group *g, uint32_t *v)
 {
     if (g->world_size == 1) return 0;
     struct inccl_shm_bar *b = g->shm_bar;
-    if (b) {
+    const char *tcp = getenv("INCCL_HOST_MAX_TCP");   /* measurement knob: the TCP allgather regardless */
+    if (b && !(tcp && atoi(tcp) != 0)) {
         atomic_store(&b->words[g->rank], *v);
         int rc = inccl_group_barrier(g);   /* every word written */
         if (rc) return rc;

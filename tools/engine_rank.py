@@ -22,6 +22,7 @@ def main():
     rank, world, port, engine = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     mib = float(sys.argv[5]) if len(sys.argv) > 5 else 256.0   # fractions: 0.00390625 = 4 KiB
     iters = int(sys.argv[6]) if len(sys.argv) > 6 else 20
+    k = 0x7FFFFFFF if os.environ.get("SCALE") == "auto" else 25   # SCALE=auto: inccl SCALE_AUTO
     os.environ.setdefault("INCCL_ENGINE", engine if engine in ("p2p", "mesh", "meshw") else "p2p")
     import numpy as np
     import torch
@@ -42,7 +43,7 @@ def main():
     out = torch.empty(n, device=dev)
     st = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize()
-    comm.allreduce_f32(xs, out=out, scale_exp=25, stream=st.cuda_stream)
+    comm.allreduce_f32(xs, out=out, scale_exp=k, stream=st.cuda_stream)
     torch.cuda.synchronize()
     ok = None
     if mib <= 64:   # oracle check of the first call (every rank's inputs regenerated here)
@@ -52,16 +53,17 @@ def main():
             g = torch.Generator(device=dev)
             g.manual_seed(1000 + r)
             every += [torch.randn(n, generator=g, device=dev).cpu().numpy() for _ in range(2)]
-        ok = bool(np.array_equal(out.cpu().numpy().view(np.uint32), O.reduce_f32(every, 25).view(np.uint32)))
+        kk = O.choose_scale(O.absmax(every), 2 * world) if k != 25 else 25
+        ok = bool(np.array_equal(out.cpu().numpy().view(np.uint32), O.reduce_f32(every, kk).view(np.uint32)))
     for _ in range(5):
-        comm.allreduce_f32(xs, out=out, scale_exp=25, stream=st.cuda_stream)
+        comm.allreduce_f32(xs, out=out, scale_exp=k, stream=st.cuda_stream)
     torch.cuda.synchronize()
     comm.barrier()
     per_call = []
     t0 = time.perf_counter()
     for _ in range(iters):
         t1 = time.perf_counter()
-        comm.allreduce_f32(xs, out=out, scale_exp=25, stream=st.cuda_stream)
+        comm.allreduce_f32(xs, out=out, scale_exp=k, stream=st.cuda_stream)
         if os.environ.get("PER_CALL"):   # host time of each call, synchronised
             torch.cuda.synchronize()
             per_call.append(round((time.perf_counter() - t1) * 1e3, 3))
@@ -69,6 +71,7 @@ def main():
     dt = (time.perf_counter() - t0) / iters
     comm.barrier()
     print(json.dumps({"rank": rank, "world": world, "engine": engine, "bucket_mib": mib, "R": 2,
+                      "scale": "auto" if k != 25 else 25, "host_max_tcp": os.environ.get("INCCL_HOST_MAX_TCP"),
                       "ms_per_call": round(dt * 1e3, 4), "oracle_ok": ok,
                       **({"per_call_ms": per_call} if per_call else {})}), flush=True)
     comm.destroy()
