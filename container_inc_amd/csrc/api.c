@@ -617,22 +617,45 @@ static int allreduce_piece(struct inccl_communicator *c, const float *const *src
     return 0;
 }
 
-static int resolve_scale(struct inccl_communicator *c, const float *const *srcs, int R, size_t n, int scale_exp,
-                         hipStream_t st, const uint32_t **amax_out)
+/* The scale of one allreduce.  A fixed exponent passes through.  INCCL_SCALE_AUTO
+ * takes the absmax of the local buckets (kind F32 or BF16) and its max over the
+ * group.  On the IPC engines that max is agreed on the host anyway (the node's
+ * shared memory), so the host also picks the exponent (inccl_choose_scale, the
+ * host twin of the kernels' choose_scale): *k_out, no device word, no copy
+ * back.  Otherwise the max stays on the device (*amax_out) for the kernels to
+ * resolve. */
+static int resolve_scale(struct inccl_communicator *c, int kind, const void *const *srcs, int R, size_t n,
+                         int scale_exp, hipStream_t st, const uint32_t **amax_out, int *k_out)
 {
     *amax_out = NULL;
+    *k_out = scale_exp;
     if (scale_exp != INCCL_SCALE_AUTO) {
         if (scale_exp < INCCL_SCALE_MIN || scale_exp > INCCL_SCALE_MAX)
             return inccl_set_error(INCCL_ERR_ARG, "scale_exp %d out of range", scale_exp);
         return 0;
     }
-    int rc = inccl_absmax_f32(srcs, R, n, c->d_words, 1, st);
+    int rc = kind == INCCL_KIND_BF16 ? inccl_absmax_bf16((const uint16_t *const *)srcs, R, n, c->d_words, 1, st)
+                                     : inccl_absmax_f32((const float *const *)srcs, R, n, c->d_words, 1, st);
     if (rc) return rc;
-    if (c->group->world_size > 1) {
+    const int W = c->group->world_size;
+    if (W > 1 && c->group->transport == INCCL_TRANSPORT_RCCL &&
+        (c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH)) {
+        uint32_t v = 0;
+        INCCL_HIP(hipMemcpyAsync(&v, c->d_words, sizeof(v), hipMemcpyDeviceToHost, st));
+        INCCL_HIP(hipStreamSynchronize(st));
+        rc = inccl_group_allreduce_max_u32(c->group, &v);
+        if (rc) return rc;
+        float amax;
+        memcpy(&amax, &v, sizeof(amax));
+        *k_out = inccl_choose_scale(amax, R * W);
+        return 0;
+    }
+    if (W > 1) {
         rc = inccl_tp_allreduce_max_u32(c, c->d_words, 1, st);
         if (rc) return rc;
     }
     *amax_out = c->d_words;
+    *k_out = 0;
     return 0;
 }
 
@@ -653,9 +676,9 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     const int W = c->group->world_size;
     const uint32_t *amax = NULL;
-    int rc = resolve_scale(c, srcs_dev, R, n, scale_exp, st, &amax);
+    int k = 0;
+    int rc = resolve_scale(c, INCCL_KIND_F32, (const void *const *)srcs_dev, R, n, scale_exp, st, &amax, &k);
     if (rc) return rc;
-    const int k = amax ? 0 : scale_exp;
     const int scale_R = R * W;
 
     const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: RS/AG path even at world 1 */
@@ -776,18 +799,11 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
     const int W = c->group->world_size, me = c->group->rank;
     const void *const *srcs = (const void *const *)srcs_dev;
     const uint32_t *amax = NULL;
-    if (scale_exp == INCCL_SCALE_AUTO) {
-        int rc = inccl_absmax_bf16(srcs_dev, R, n, c->d_words, 1, st);
+    int k = 0;
+    {
+        const int rc = resolve_scale(c, INCCL_KIND_BF16, srcs, R, n, scale_exp, st, &amax, &k);
         if (rc) return rc;
-        if (W > 1) {
-            rc = inccl_tp_allreduce_max_u32(c, c->d_words, 1, st);
-            if (rc) return rc;
-        }
-        amax = c->d_words;
-    } else if (scale_exp < INCCL_SCALE_MIN || scale_exp > INCCL_SCALE_MAX) {
-        return inccl_set_error(INCCL_ERR_ARG, "scale_exp %d out of range", scale_exp);
     }
-    const int k = amax ? 0 : scale_exp;
     const int scale_R = R * W;
     const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: RS/AG path even at world 1 */
     if (W == 1 && !(fs && atoi(fs) != 0))   /* one fused HBM pass */
