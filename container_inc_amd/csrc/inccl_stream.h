@@ -59,15 +59,20 @@ __device__ __forceinline__ int resolve_k(const Scale& s)
     return choose_scale(__uint_as_float(bits), s.scale_R);
 }
 
-// q = sat_i32(rne(x * 2^k)), NaN -> 0  (orc_quantise_one)
-__device__ __forceinline__ uint32_t quant1(float x, float scale)
+// sat_i32(rne(y)) with NaN -> 0: v_rndne_f32 then v_cvt_i32_f32, whose
+// conversion saturates to [INT32_MIN, INT32_MAX] and maps NaN to 0 -- exactly
+// the spec (orc_quantise_one), in 2 VALU ops where a compare/select form of the
+// same rule takes 7.  (The saturation and NaN cases are in the GPU parity tests.)
+__device__ __forceinline__ uint32_t quant_sat(float y)
 {
-    float y = x * scale;
-    y = (y != y) ? 0.0f : y;
-    y = __builtin_rintf(y);
-    int32_t q = (y >= 2147483648.0f) ? INT32_MAX : ((y <= -2147483648.0f) ? INT32_MIN : (int32_t)y);
+    const float r = __builtin_rintf(y);
+    int32_t q;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(q) : "v"(r));
     return (uint32_t)q;
 }
+
+// q = sat_i32(rne(x * 2^k)), NaN -> 0  (orc_quantise_one)
+__device__ __forceinline__ uint32_t quant1(float x, float scale) { return quant_sat(x * scale); }
 
 template <int IN>
 __device__ __forceinline__ uint32_t load_xform(uint32_t raw, float scale)
@@ -196,25 +201,15 @@ __global__ __launch_bounds__(BLOCK) void k_stream_vec(SrcPtrs src, void* __restr
 
 // ---- bfloat16 buckets: 2-byte elements, 8 per 16-B lane access ------------
 // A bf16 value widens to fp32 exactly (its bits << 16), so quantisation is the
-// fp32 rule on the widened value; the dequantised fp32 sum narrows with round to
-// nearest even.  Twice the elements per byte of the fp32 path, so the VALU work
-// per byte doubles: the fp32 path's compare/select form of quant1 (8 VALU ops
-// an element) would leave this kernel issue-bound, so here
-//  * quantise = v_mul, v_rndne, v_cvt_i32_f32: the conversion itself saturates
-//    to [INT32_MIN, INT32_MAX] and maps NaN to 0, which is exactly the spec
-//    (orc_quantise_one) -- 3 ops;
-//  * narrowing = gfx950's v_cvt_pk_bf16_f32 (round to nearest even), one op per
-//    pair.  The sums are finite (|(float)s * 2^-k| <= 2^95): no NaN or overflow case.
+// fp32 rule on the widened value (quant_sat above: v_mul, v_rndne, saturating
+// v_cvt_i32_f32); the dequantised fp32 sum narrows with round to nearest even
+// through gfx950's v_cvt_pk_bf16_f32, one op per pair.  Twice the elements per
+// byte of the fp32 path: with the earlier compare/select quantise (8 VALU ops an
+// element) this kernel was issue-bound at 0.76 of HBM.  The sums are finite
+// (|(float)s * 2^-k| <= 2^95): no NaN or overflow case in the narrowing.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ uint32_t quant_sat(float y)
-{
-    const float r = __builtin_rintf(y);
-    int32_t q;
-    asm("v_cvt_i32_f32 %0, %1" : "=v"(q) : "v"(r));
-    return (uint32_t)q;
-}
 
 __device__ __forceinline__ uint32_t bf16_quant(uint32_t h, float scale) { return quant_sat(__uint_as_float(h << 16) * scale); }
 
