@@ -838,6 +838,9 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
         if (!in_place) INCCL_HIP(hipMemcpyAsync(dst_dev, gather, n * sizeof(uint16_t), hipMemcpyDeviceToDevice, st));
         return 0;
     }
+    /* the mesh engines: the persistent kernel with bf16 sources and results (mesh.c) */
+    if (c->engine == INCCL_ENGINE_MESH && c->group->transport == INCCL_TRANSPORT_RCCL)
+        return inccl_mesh_piece_bf16(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
     /* the p2p engine: bf16 result shards gathered over xGMI (p2p.c) */
     if (c->engine == INCCL_ENGINE_P2P && c->group->transport == INCCL_TRANSPORT_RCCL && ((uintptr_t)dst_dev & 3u) == 0)
         return inccl_p2p_piece_bf16(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);

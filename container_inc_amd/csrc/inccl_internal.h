@@ -162,6 +162,8 @@ uint64_t inccl_wait_ticks(struct inccl_group *g);   /* bound of an in-kernel wai
 /* mesh engine (mesh.c) */
 int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
                      const uint32_t *amax, int scale_R, hipStream_t st);
+int inccl_mesh_piece_bf16(struct inccl_communicator *c, const uint16_t *const *srcs, int R, uint16_t *dst, size_t n,
+                          int k, const uint32_t *amax, int scale_R, hipStream_t st);
 void inccl_mesh_release(struct inccl_communicator *c);
 
 /* local transport */

@@ -83,6 +83,7 @@ struct inccl_mesh_launch {
     uint32_t *peer_resin[INCCL_MAX_LOCAL_INPUTS];      /* every rank's result inbox (push_res) */
     const uint32_t *own_resin;
     int push_res;                                      /* 1: reduce pushes results, gather copies locally */
+    int b16;                                           /* 1: src / dst hold bf16 (uint16_t) elements */
     uint32_t *peer_sig[INCCL_MAX_LOCAL_INPUTS];        /* every rank's signal array */
     const uint32_t *own_sig;
     uint32_t *ctr;                                     /* own words: calls, retired, ticket, abort */

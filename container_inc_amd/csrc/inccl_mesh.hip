@@ -87,7 +87,7 @@ struct MeshArgs {
     uint32_t* ctr;                       // [0] calls done, [1] retired, [2] ticket, [3] abort
     uint32_t* err;                       // host-mapped error word
     uint64_t timeout_ticks;
-    int nchunks, W, me, lag, vec_src, vec_dst, push_res;
+    int nchunks, W, me, lag, vec_src, vec_dst, push_res, b16;
     Scale sc;
 };
 
@@ -138,8 +138,12 @@ __device__ __forceinline__ int64_t chunk_len(const MeshArgs& a, int c)
     return rest < a.chunk ? rest : a.chunk;
 }
 
-// push(c, j): partial sums of chunk c of shard j -> rank j's inbox, slot me
-template <int R>
+// push(c, j): partial sums of chunk c of shard j -> rank j's inbox, slot me.
+// B16: the sources are bf16 (8 bytes per quad of elements); the partials are
+// int32 either way.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <int R, bool B16>
 __device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float scale)
 {
     const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;   // global element index
@@ -149,7 +153,28 @@ __device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float s
     const bool full = a.vec_src && lo + 4 * nq <= a.n;
     for (int64_t q0 = threadIdx.x; q0 < nq; q0 += (int64_t)kMeshBlock * kMeshU) {
         u32x4 acc[kMeshU];
-        if (full) {
+        if (full && B16) {
+            u32x2 x[kMeshU][R];
+#pragma unroll
+            for (int u = 0; u < kMeshU; ++u) {
+                const int64_t q = q0 + (int64_t)u * kMeshBlock;
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    x[u][r] = q < nq ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(a.src.p[r]) + (lo >> 2) + q)
+                                     : u32x2{0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < kMeshU; ++u) {
+                acc[u] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    acc[u].x += bf16_quant(x[u][r].x & 0xffffu, scale);
+                    acc[u].y += bf16_quant(x[u][r].x >> 16, scale);
+                    acc[u].z += bf16_quant(x[u][r].y & 0xffffu, scale);
+                    acc[u].w += bf16_quant(x[u][r].y >> 16, scale);
+                }
+            }
+        } else if (full) {
             u32x4 x[kMeshU][R];
 #pragma unroll
             for (int u = 0; u < kMeshU; ++u) {
@@ -181,7 +206,9 @@ __device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float s
                         const int64_t i = lo + 4 * q + e;
                         if (i < a.n)
 #pragma unroll
-                            for (int r = 0; r < R; ++r) s[e] += quant1(reinterpret_cast<const float*>(a.src.p[r])[i], scale);
+                            for (int r = 0; r < R; ++r)
+                                s[e] += B16 ? bf16_quant(reinterpret_cast<const uint16_t*>(a.src.p[r])[i], scale)
+                                            : quant1(reinterpret_cast<const float*>(a.src.p[r])[i], scale);
                     }
                 acc[u] = u32x4{s[0], s[1], s[2], s[3]};
             }
@@ -197,7 +224,9 @@ __device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float s
     if (threadIdx.x == 0) st_sys(a.peer_sig[j] + arrive_idx(a.me, c), epoch);
 }
 
-// reduce(c): my shard's chunk c = dequant(sum over the W inbox slots)
+// reduce(c): my shard's chunk c = dequant(sum over the W inbox slots); B16: the
+// result chunk is bf16 (8 bytes per quad), at element offsets in 2-byte units
+template <bool B16>
 __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
 {
     bool ok = true;
@@ -209,12 +238,16 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
 #pragma unroll
     for (int j = 0; j < kMaxR; ++j)
         in[j] = rsrc(a.own_inbox + (int64_t)(j < a.W ? j : 0) * a.inbox_stride + (int64_t)c * a.chunk, bytes);
-    const __amdgpu_buffer_rsrc_t res = rsrc(a.own_res + (int64_t)c * a.chunk, bytes);
+    constexpr int ES = B16 ? 2 : 4;   // result element bytes
+    const uint32_t obytes = (uint32_t)(nq * 4 * ES);
+    const __amdgpu_buffer_rsrc_t res = rsrc(reinterpret_cast<const char*>(a.own_res) + (int64_t)c * a.chunk * ES, obytes);
     __amdgpu_buffer_rsrc_t outs[kMaxR];   // push_res: my slot of every rank's result inbox
     if (a.push_res) {
 #pragma unroll
         for (int j = 0; j < kMaxR; ++j)
-            outs[j] = rsrc(a.peer_resin[j < a.W ? j : 0] + (int64_t)a.me * a.inbox_stride + (int64_t)c * a.chunk, bytes);
+            outs[j] = rsrc(reinterpret_cast<const char*>(a.peer_resin[j < a.W ? j : 0]) +
+                               ((int64_t)a.me * a.inbox_stride + (int64_t)c * a.chunk) * ES,
+                           obytes);
     }
     for (int64_t q0 = threadIdx.x; q0 < nq; q0 += (int64_t)kMeshBlock * 2) {
         u32x4 x[2][kMaxR];
@@ -236,17 +269,28 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
                 acc.z += x[u][j].z;
                 acc.w += x[u][j].w;
             }
-            u32x4 o;
-            o.x = __float_as_uint((float)(int32_t)acc.x * inv);
-            o.y = __float_as_uint((float)(int32_t)acc.y * inv);
-            o.z = __float_as_uint((float)(int32_t)acc.z * inv);
-            o.w = __float_as_uint((float)(int32_t)acc.w * inv);
-            if (a.push_res) {
+            if constexpr (B16) {
+                const u32x2 o = {deq_bf16x2(acc.x, acc.y, inv), deq_bf16x2(acc.z, acc.w, inv)};
+                if (a.push_res) {
 #pragma unroll
-                for (int j = 0; j < kMaxR; ++j)
-                    if (j < a.W) st_sys16(outs[j], (uint32_t)(q * 16), o);
+                    for (int j = 0; j < kMaxR; ++j)
+                        if (j < a.W) __builtin_amdgcn_raw_buffer_store_b64(o, outs[j], (int)(q * 8), 0, kAuxSys);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b64(o, res, (int)(q * 8), 0, kAuxSys);
+                }
             } else {
-                st_sys16(res, (uint32_t)(q * 16), o);
+                u32x4 o;
+                o.x = __float_as_uint((float)(int32_t)acc.x * inv);
+                o.y = __float_as_uint((float)(int32_t)acc.y * inv);
+                o.z = __float_as_uint((float)(int32_t)acc.z * inv);
+                o.w = __float_as_uint((float)(int32_t)acc.w * inv);
+                if (a.push_res) {
+#pragma unroll
+                    for (int j = 0; j < kMaxR; ++j)
+                        if (j < a.W) st_sys16(outs[j], (uint32_t)(q * 16), o);
+                } else {
+                    st_sys16(res, (uint32_t)(q * 16), o);
+                }
             }
         }
     }
@@ -299,7 +343,52 @@ __device__ bool do_gather(const MeshArgs& a, int c, int j, uint32_t epoch)
     return true;
 }
 
-template <int R>
+// gather(c, j) of a bf16 result: 8 elements per 16-B access, a ragged end of
+// the bucket element by element
+__device__ bool do_gather16(const MeshArgs& a, int c, int j, uint32_t epoch)
+{
+    bool ok = true;
+    if (threadIdx.x == 0) ok = wait_flag(a, a.own_sig + ready_idx(j, c), epoch);
+    if (!__syncthreads_and(ok)) return false;
+    const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;
+    if (lo >= a.n) return true;
+    int64_t cnt = chunk_len(a, c);
+    if (lo + cnt > a.n) cnt = a.n - lo;
+    const int64_t n8 = cnt >> 3;
+    const uint16_t* sbase = a.push_res
+                                ? reinterpret_cast<const uint16_t*>(a.own_resin) + (int64_t)j * a.inbox_stride + (int64_t)c * a.chunk
+                                : reinterpret_cast<const uint16_t*>(a.peer_res[j]) + (int64_t)c * a.chunk;
+    const __amdgpu_buffer_rsrc_t src = rsrc(sbase, (uint32_t)(chunk_len(a, c) * 2));
+    uint16_t* d = reinterpret_cast<uint16_t*>(a.dst) + lo;
+    const __amdgpu_buffer_rsrc_t drs = rsrc(d, (uint32_t)(n8 * 16));
+    for (int64_t q0 = threadIdx.x; q0 < n8; q0 += (int64_t)kMeshBlock * kMeshU) {
+        u32x4 v[kMeshU];
+#pragma unroll
+        for (int u = 0; u < kMeshU; ++u)
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(src, (int)((q0 + u * kMeshBlock) * 16), 0, kAuxSys);
+#pragma unroll
+        for (int u = 0; u < kMeshU; ++u) {
+            const int64_t q = q0 + (int64_t)u * kMeshBlock;
+            if (q < n8) {
+                if (a.vec_dst) {
+                    __builtin_amdgcn_raw_buffer_store_b128(v[u], drs, (int)(q * 16), 0, 16);   // sc1
+                } else {
+                    const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        d[8 * q + 2 * e] = (uint16_t)(w[e] & 0xffffu);
+                        d[8 * q + 2 * e + 1] = (uint16_t)(w[e] >> 16);
+                    }
+                }
+            }
+        }
+    }
+    for (int64_t i = 8 * n8 + threadIdx.x; i < cnt; i += kMeshBlock)   // ragged end of the bucket
+        d[i] = (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(src, (int)(i * 2), 0, kAuxSys);
+    return true;
+}
+
+template <int R, bool B16>
 __global__ __launch_bounds__(kMeshBlock) void k_mesh(MeshArgs a)
 {
     __shared__ int s_ticket;
@@ -320,13 +409,14 @@ __global__ __launch_bounds__(kMeshBlock) void k_mesh(MeshArgs a)
         if (t >= total) break;
         const int s = t / per_slot, pos = t - s * per_slot;
         if (pos < W) {
-            if (s < a.nchunks) do_push<R>(a, s, (a.me + 1 + pos) % W, epoch, scale);
+            if (s < a.nchunks) do_push<R, B16>(a, s, (a.me + 1 + pos) % W, epoch, scale);
         } else if (pos == W) {
             const int c = s - a.lag;
-            if (c >= 0 && c < a.nchunks && !do_reduce(a, c, epoch, inv)) break;
+            if (c >= 0 && c < a.nchunks && !do_reduce<B16>(a, c, epoch, inv)) break;
         } else {
             const int c = s - 2 * a.lag;
-            if (c >= 0 && c < a.nchunks && !do_gather(a, c, (a.me + pos - W) % W, epoch)) break;
+            const int jj = (a.me + pos - W) % W;
+            if (c >= 0 && c < a.nchunks && !(B16 ? do_gather16(a, c, jj, epoch) : do_gather(a, c, jj, epoch))) break;
         }
     }
     // retire: the last workgroup resets the ticket and advances the call counter
@@ -366,6 +456,7 @@ extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
     }
     a.own_resin = l->own_resin;
     a.push_res = l->push_res ? 1 : 0;
+    a.b16 = l->b16 ? 1 : 0;
     if (a.push_res && (l->own_resin == nullptr || l->peer_resin[0] == nullptr)) return INCCL_ERR_ARG;
     a.own_inbox = l->own_inbox;
     a.own_res = l->own_res;
@@ -387,16 +478,19 @@ extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
     a.sc.out_shift = l->out_shift;
     hipStream_t st = (hipStream_t)stream;
     const dim3 g((unsigned)l->grid), b(kMeshBlock);
+#define INCCL_MESH_CASE(RR)                                                  \
+    case RR:                                                                 \
+        if (l->b16)                                                          \
+            hipLaunchKernelGGL((k_mesh<RR, true>), g, b, 0, st, a);          \
+        else                                                                 \
+            hipLaunchKernelGGL((k_mesh<RR, false>), g, b, 0, st, a);         \
+        break;
     switch (l->R) {
-        case 1: hipLaunchKernelGGL(k_mesh<1>, g, b, 0, st, a); break;
-        case 2: hipLaunchKernelGGL(k_mesh<2>, g, b, 0, st, a); break;
-        case 3: hipLaunchKernelGGL(k_mesh<3>, g, b, 0, st, a); break;
-        case 4: hipLaunchKernelGGL(k_mesh<4>, g, b, 0, st, a); break;
-        case 5: hipLaunchKernelGGL(k_mesh<5>, g, b, 0, st, a); break;
-        case 6: hipLaunchKernelGGL(k_mesh<6>, g, b, 0, st, a); break;
-        case 7: hipLaunchKernelGGL(k_mesh<7>, g, b, 0, st, a); break;
-        default: hipLaunchKernelGGL(k_mesh<8>, g, b, 0, st, a); break;
+        INCCL_MESH_CASE(1) INCCL_MESH_CASE(2) INCCL_MESH_CASE(3) INCCL_MESH_CASE(4) INCCL_MESH_CASE(5)
+        INCCL_MESH_CASE(6) INCCL_MESH_CASE(7)
+        default: INCCL_MESH_CASE(8)
     }
+#undef INCCL_MESH_CASE
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }

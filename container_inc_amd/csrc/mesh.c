@@ -219,8 +219,8 @@ static size_t mesh_chunk(size_t shard)
     return ch;
 }
 
-int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
-                     const uint32_t *amax, int scale_R, hipStream_t st)
+static int mesh_piece(struct inccl_communicator *c, int b16, const void *const *srcs, int R, void *dst, size_t n,
+                      int k, const uint32_t *amax, int scale_R, hipStream_t st)
 {
     const int W = c->group->world_size, me = c->group->rank;
     const size_t shard = inccl_shard_elems(n, W);
@@ -248,9 +248,10 @@ int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int
     if (lag > nchunks) lag = nchunks;
     struct inccl_mesh_launch l;
     memset(&l, 0, sizeof(l));
-    for (int r = 0; r < R; ++r) l.src[r] = srcs[r];
+    for (int r = 0; r < R; ++r) l.src[r] = (const float *)srcs[r];
     l.R = R;
-    l.dst = dst;
+    l.dst = (float *)dst;
+    l.b16 = b16;
     l.n = n;
     l.shard = shard;
     l.chunk = chunk;
@@ -289,4 +290,18 @@ int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int
         c->mesh_last_stream = st;
     }
     return 0;
+}
+
+int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
+                     const uint32_t *amax, int scale_R, hipStream_t st)
+{
+    return mesh_piece(c, 0, (const void *const *)srcs, R, dst, n, k, amax, scale_R, st);
+}
+
+/* bf16 buckets: the same kernel with bf16 sources, int32 partials and a bf16
+ * result, so the xGMI bytes are 4 + 2 per element instead of 4 + 4 */
+int inccl_mesh_piece_bf16(struct inccl_communicator *c, const uint16_t *const *srcs, int R, uint16_t *dst, size_t n,
+                          int k, const uint32_t *amax, int scale_R, hipStream_t st)
+{
+    return mesh_piece(c, 1, (const void *const *)srcs, R, dst, n, k, amax, scale_R, st);
 }

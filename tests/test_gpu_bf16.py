@@ -162,9 +162,9 @@ def _free_port():
     return p
 
 
-def _p2p_rank(rank, world, port, q):
+def _p2p_rank(rank, world, port, q, engine="p2p"):
     try:
-        os.environ["INCCL_ENGINE"] = "p2p"
+        os.environ["INCCL_ENGINE"] = engine
         os.environ["INCCL_DEVICE"] = "0"
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
         import sys
@@ -206,15 +206,17 @@ def _p2p_rank(rank, world, port, q):
         q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_allreduce_bf16_p2p_multiprocess(gpu, world):
-    """The p2p engine's bf16 piece (bf16 result shards gathered, odd element
-    counts through the gather's 2-byte tail), a 2-byte-aligned dst (the int32
-    allreduce path) and in place."""
+@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (8, "p2p"), (2, "mesh"), (3, "mesh"), (4, "meshw"),
+                                          (8, "mesh")])
+def test_allreduce_bf16_p2p_multiprocess(gpu, world, engine):
+    """The IPC engines' bf16 paths: p2p (bf16 result shards gathered, odd element
+    counts through the gather's 2-byte tail; a 2-byte-aligned dst takes the int32
+    allreduce) and mesh / meshw (the persistent kernel with bf16 sources and
+    results, any dst alignment), each also in place."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_p2p_rank, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_p2p_rank, args=(r, world, port, q, engine)) for r in range(world)]
     for p in ps:
         p.start()
     res = {}
