@@ -29,7 +29,7 @@ Extra JSON fields:
   api_allreduce_write N = 1: the reference's entry point on a 256 MiB host int32
                     message, registered and unregistered
   bf16              N = 1: R bf16 buckets of 256 MiB (k_stream16), repeated and rotated;
-                    N > 1: inccl_allreduce_bf16 on the rccl and p2p engines, verified
+                    N > 1: inccl_allreduce_bf16 on the rccl, p2p, mesh and meshw engines, verified
   sweep             N > 1: 4 KiB .. 256 MiB and 1 GiB per engine, verified with
                     alternating input sets
 """
@@ -321,7 +321,8 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
 def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256) -> list:
     """N > 1: R resident `mib` MiB bf16 buckets per rank through inccl_allreduce_bf16
     on the engines with a bf16 result exchange (rccl: ncclAllGather of bf16; p2p:
-    bf16 result shards gathered), each verified bit-identical to the first engine
+    bf16 result shards gathered; mesh / meshw: bf16 result chunks), each verified
+    bit-identical to the first engine
     that passes on every rank over two alternating input sets; wall time per call,
     max over ranks, and the xGMI link fraction of its (W-1)/W * n * (4 + 2) bytes."""
     import torch
@@ -338,7 +339,7 @@ def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256) -> li
     st = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize()
     rows, refs = [], None
-    for eng in ("rccl", "p2p"):
+    for eng in ("rccl", "p2p", "mesh", "meshw"):
         ok, dt, same = 1, float("inf"), False
         try:
             comm.set_engine(eng)
