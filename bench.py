@@ -322,9 +322,9 @@ def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256) -> li
     """N > 1: R resident `mib` MiB bf16 buckets per rank through inccl_allreduce_bf16
     on the engines with a bf16 result exchange (rccl: ncclAllGather of bf16; p2p:
     bf16 result shards gathered; mesh / meshw: bf16 result chunks), each verified
-    bit-identical to the first engine
-    that passes on every rank over two alternating input sets; wall time per call,
-    max over ranks, and the xGMI link fraction of its (W-1)/W * n * (4 + 2) bytes."""
+    bit-identical to the first engine that passes on every rank over two
+    alternating input sets; wall time per call, max over ranks, and the xGMI link
+    fraction of its (W-1)/W * n * (4 + 2) bytes."""
     import torch
     import torch.distributed as dist
 
