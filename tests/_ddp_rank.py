@@ -67,14 +67,14 @@ def _bits(t):
     return t.detach().cpu().numpy().view(np.uint32)
 
 
-def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False):
+def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine="p2p"):
     """dtype "bf16": a bf16 model, so DDP's buckets are bf16 (inccl_allreduce_bf16);
     as_view: gradient_as_bucket_view=True (the grads are views of the buckets)."""
     try:
         sys.path.insert(0, ROOT)
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
         if mode == "gpu":
-            os.environ["INCCL_ENGINE"] = "p2p"
+            os.environ["INCCL_ENGINE"] = engine
         import torch
         import torch.distributed as dist
         from torch.nn.parallel import DistributedDataParallel as DDP
@@ -89,7 +89,7 @@ def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False):
             grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port + 1, device=0)
             assert grp is not None, "group create failed"
             comm = inccl.inccl_communicator_create(grp, 0)
-            assert comm is not None and comm.engine == "p2p", comm and comm.engine
+            assert comm is not None and comm.engine == engine, comm and comm.engine
         else:
             dev = torch.device("cpu")
             comm = GlooStandIn(world)

@@ -17,12 +17,12 @@ def _free_port():
     return p
 
 
-def run_world(world, mode, timeout, dtype="f32", as_view=False):
+def run_world(world, mode, timeout, dtype="f32", as_view=False, engine="p2p"):
     import _ddp_rank
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_ddp_rank.run, args=(r, world, port, q, mode, 2, dtype, as_view)) for r in range(world)]
+    ps = [ctx.Process(target=_ddp_rank.run, args=(r, world, port, q, mode, 2, dtype, as_view, engine)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=timeout) for _ in range(world))

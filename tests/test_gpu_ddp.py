@@ -11,10 +11,11 @@ from test_ddp_hook import run_world
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("world,dtype,as_view", [(2, "f32", False), (4, "f32", False), (2, "bf16", False),
-                                                 (4, "bf16", True)])
-def test_ddp_hook_gpu(gpu, orc, world, dtype, as_view):
-    res = run_world(world, "gpu", 240, dtype, as_view)
+@pytest.mark.parametrize("world,dtype,as_view,engine", [(2, "f32", False, "p2p"), (4, "f32", False, "p2p"),
+                                                        (2, "bf16", False, "p2p"), (4, "bf16", True, "p2p"),
+                                                        (2, "f32", False, "mesh"), (4, "bf16", False, "meshw")])
+def test_ddp_hook_gpu(gpu, orc, world, dtype, as_view, engine):
+    res = run_world(world, "gpu", 240, dtype, as_view, engine)
     for r, rep in res.items():
         assert "error" not in rep, rep.get("tb")
         assert rep["buckets"][-1] >= 2, rep
