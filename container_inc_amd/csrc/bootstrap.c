@@ -224,7 +224,7 @@ struct inccl_shm_bar {
     _Atomic uint32_t count;
     _Atomic uint32_t generation;
     uint32_t world;
-    _Atomic uint32_t words[64];   /* one word per rank for small host reductions */
+    _Atomic uint32_t words[2][64];   /* one word per rank for small host reductions, two banks */
 };
 
 int inccl_boot_shm_init(struct inccl_group *g)
@@ -296,23 +296,28 @@ int inccl_group_barrier(struct inccl_group *g)
 }
 
 /* max of one word over the group: through the shared-memory segment when the
- * group has one (two barriers, a few microseconds), else the TCP allgather */
+ * group has one (one barrier, a few microseconds), else the TCP allgather.
+ * Calls alternate between two banks of words, so no second barrier is needed:
+ * a rank writes bank b again only in the call after next, which it reaches
+ * after the next call's barrier -- i.e. after every rank has finished reading
+ * bank b in this call. */
 int inccl_group_allreduce_max_u32(struct inccl_group *g, uint32_t *v)
 {
     if (g->world_size == 1) return 0;
     struct inccl_shm_bar *b = g->shm_bar;
     const char *tcp = getenv("INCCL_HOST_MAX_TCP");   /* measurement knob: the TCP allgather regardless */
     if (b && !(tcp && atoi(tcp) != 0)) {
-        atomic_store(&b->words[g->rank], *v);
-        int rc = inccl_group_barrier(g);   /* every word written */
+        _Atomic uint32_t *words = b->words[g->max_seq++ & 1u];
+        atomic_store(&words[g->rank], *v);
+        int rc = inccl_group_barrier(g);   /* every word of this bank written */
         if (rc) return rc;
         uint32_t m = 0;
         for (int j = 0; j < g->world_size; ++j) {
-            const uint32_t w = atomic_load(&b->words[j]);
+            const uint32_t w = atomic_load(&words[j]);
             m = w > m ? w : m;
         }
         *v = m;
-        return inccl_group_barrier(g);     /* every word read before the next call rewrites it */
+        return 0;
     }
     uint32_t all[64];
     if (g->world_size > 64) return inccl_set_error(INCCL_ERR_ARG, "max-allreduce: world too large");

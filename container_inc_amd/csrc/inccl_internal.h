@@ -49,6 +49,7 @@ struct inccl_group {
     int master_fd;
     int *peer_fds;
     struct inccl_shm_bar *shm_bar;   /* same-node fast barrier (NULL: TCP barrier) */
+    uint32_t max_seq;                /* host max-allreduces through shm so far (picks the word bank) */
     /* local transport */
     struct inccl_local_hub *hub;
     int comm_seq;   /* communicators created so far (names the hub slot) */
