@@ -44,7 +44,8 @@ class HookState:
     def fold_average(self) -> bool:
         """Once: let the engine return the mean (power-of-two worlds: 2^-log2 W is
         folded into the dequantise scale, bit-identical to dividing, one pass
-        fewer); otherwise the hook divides."""
+        fewer); otherwise the hook divides.  This switches the communicator
+        itself to averaging: give the hook a communicator of its own."""
         if self.folded is None:
             self.folded = False
             if self.average and self.world_size > 1 and hasattr(self.comm, "set_average"):
