@@ -838,10 +838,6 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
         if (!in_place) INCCL_HIP(hipMemcpyAsync(dst_dev, gather, n * sizeof(uint16_t), hipMemcpyDeviceToDevice, st));
         return 0;
     }
-    /* the ll engine (small buckets): one kernel with bf16 sources and result (ll.c) */
-    if (c->engine == INCCL_ENGINE_LL && c->group->transport == INCCL_TRANSPORT_RCCL &&
-        n <= c->ll_max_bytes / sizeof(float))
-        return inccl_ll_piece_bf16(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
     /* the mesh engines: the persistent kernel with bf16 sources and results (mesh.c) */
     if (c->engine == INCCL_ENGINE_MESH && c->group->transport == INCCL_TRANSPORT_RCCL)
         return inccl_mesh_piece_bf16(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);

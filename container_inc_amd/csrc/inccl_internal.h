@@ -157,8 +157,6 @@ int inccl_p2p_allreduce_q32(struct inccl_communicator *c, const int32_t *send, i
 /* ll engine (ll.c): n <= c->ll_max_bytes / 4 */
 int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
                    const uint32_t *amax, int scale_R, hipStream_t st);
-int inccl_ll_piece_bf16(struct inccl_communicator *c, const uint16_t *const *srcs, int R, uint16_t *dst, size_t n,
-                        int k, const uint32_t *amax, int scale_R, hipStream_t st);
 void inccl_ll_release(struct inccl_communicator *c);
 uint64_t inccl_wait_ticks(struct inccl_group *g);   /* bound of an in-kernel wait */
 

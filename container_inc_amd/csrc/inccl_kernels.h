@@ -60,7 +60,6 @@ struct inccl_ll_launch {
     const uint32_t *amax_bits;
     int scale_R;
     int out_shift;                                     /* dequantise with 2^-(k + out_shift) */
-    int b16;                                           /* 1: src / dst hold bf16 (uint16_t) elements */
 };
 int inccl_k_ll_grid(size_t n);
 int inccl_k_ll_oneshot(const struct inccl_ll_launch *l, void *stream);

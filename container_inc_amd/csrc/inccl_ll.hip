@@ -86,11 +86,7 @@ __device__ __forceinline__ void st_sys16(__amdgpu_buffer_rsrc_t r, uint32_t byte
 //             on the flag store and an acquire (buffer_inv) after the wait.
 // WT = true:  data written through and read around the caches (sc0 sc1), so the
 //             flag store only has to follow the data stores' completion.
-// B16: bf16 sources and result (8 bytes per quad of elements); the int32
-// partials in the data slots are the same as for fp32
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-template <int R, bool WT, bool B16>
+template <int R, bool WT>
 __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, int vec_dst)
 {
     const int k = resolve_k(a.sc);
@@ -108,16 +104,7 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
     const __amdgpu_buffer_rsrc_t own_rs = rsrc(a.own_data + slot, (uint32_t)(nq * 16));
     for (int64_t q = (int64_t)blockIdx.x * kLLBlock + tid; q < nq; q += stride) {
         u32x4 acc = {0u, 0u, 0u, 0u};
-        if (B16 && vec_src && 4 * q + 4 <= a.n) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const u32x2 x = reinterpret_cast<const u32x2*>(a.src.p[r])[q];
-                acc.x += bf16_quant(x.x & 0xffffu, scale);
-                acc.y += bf16_quant(x.x >> 16, scale);
-                acc.z += bf16_quant(x.y & 0xffffu, scale);
-                acc.w += bf16_quant(x.y >> 16, scale);
-            }
-        } else if (!B16 && vec_src && 4 * q + 4 <= a.n) {
+        if (vec_src && 4 * q + 4 <= a.n) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const u32x4 x = reinterpret_cast<const u32x4*>(a.src.p[r])[q];
@@ -133,9 +120,7 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
                 const int64_t i = 4 * q + e;
                 if (i < a.n)
 #pragma unroll
-                    for (int r = 0; r < R; ++r)
-                        s[e] += B16 ? bf16_quant(reinterpret_cast<const uint16_t*>(a.src.p[r])[i], scale)
-                                    : quant1(reinterpret_cast<const float*>(a.src.p[r])[i], scale);
+                    for (int r = 0; r < R; ++r) s[e] += quant1(reinterpret_cast<const float*>(a.src.p[r])[i], scale);
             }
             acc.x = s[0];
             acc.y = s[1];
@@ -183,7 +168,7 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
         for (int j = 0; j < kMaxR; ++j)
             if (j < a.W) peer[j] = rsrc(a.peer_data[j] + slot, (uint32_t)(nq * 16));
     }
-    const __amdgpu_buffer_rsrc_t dst_rs = rsrc(a.dst, (uint32_t)(a.n * (B16 ? 2 : 4)));
+    const __amdgpu_buffer_rsrc_t dst_rs = rsrc(a.dst, (uint32_t)(a.n * 4));
     for (int64_t q0 = (int64_t)blockIdx.x * kLLBlock + tid; q0 < nq; q0 += stride * kU) {
         u32x4 x[kU][kMaxR];
 #pragma unroll
@@ -210,17 +195,6 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
                     acc.z += x[u][j].z;
                     acc.w += x[u][j].w;
                 }
-            if constexpr (B16) {
-                const u32x2 o = {deq_bf16x2(acc.x, acc.y, inv), deq_bf16x2(acc.z, acc.w, inv)};
-                if (vec_dst && 4 * q + 4 <= a.n) {
-                    __builtin_amdgcn_raw_buffer_store_b64(o, dst_rs, (int)(q * 8), 0, 16);   // sc1
-                } else {
-                    const uint32_t v[4] = {o.x & 0xffffu, o.x >> 16, o.y & 0xffffu, o.y >> 16};
-                    for (int e = 0; e < 4; ++e)
-                        if (4 * q + e < a.n) reinterpret_cast<uint16_t*>(a.dst)[4 * q + e] = (uint16_t)v[e];
-                }
-                continue;
-            }
             u32x4 o;
             o.x = __float_as_uint((float)(int32_t)acc.x * inv);
             o.y = __float_as_uint((float)(int32_t)acc.y * inv);
@@ -249,7 +223,7 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
     }
 }
 
-template <int R, bool B16>
+template <int R>
 hipError_t launch_R(const LLArgs& a, int grid, int vs, int vd, hipStream_t st)
 {
     static int wt = -1;   // $INCCL_LL_PROTOCOL: "wt" (default) or "fence"; same on every rank
@@ -257,8 +231,8 @@ hipError_t launch_R(const LLArgs& a, int grid, int vs, int vd, hipStream_t st)
         const char* e = getenv("INCCL_LL_PROTOCOL");
         wt = (e && e[0] == 'f') ? 0 : 1;
     }
-    if (wt) hipLaunchKernelGGL((k_ll_oneshot<R, true, B16>), dim3(grid), dim3(kLLBlock), 0, st, a, vs, vd);
-    else hipLaunchKernelGGL((k_ll_oneshot<R, false, B16>), dim3(grid), dim3(kLLBlock), 0, st, a, vs, vd);
+    if (wt) hipLaunchKernelGGL((k_ll_oneshot<R, true>), dim3(grid), dim3(kLLBlock), 0, st, a, vs, vd);
+    else hipLaunchKernelGGL((k_ll_oneshot<R, false>), dim3(grid), dim3(kLLBlock), 0, st, a, vs, vd);
     return hipGetLastError();
 }
 
@@ -315,13 +289,15 @@ extern "C" int inccl_k_ll_oneshot(const struct inccl_ll_launch* l, void* stream)
     const int grid = inccl_k_ll_grid(l->n);
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
-#define INCCL_LL_CASE(RR) \
-    case RR: e = l->b16 ? launch_R<RR, true>(a, grid, vs, vd, st) : launch_R<RR, false>(a, grid, vs, vd, st); break;
     switch (l->R) {
-        INCCL_LL_CASE(1) INCCL_LL_CASE(2) INCCL_LL_CASE(3) INCCL_LL_CASE(4) INCCL_LL_CASE(5) INCCL_LL_CASE(6)
-        INCCL_LL_CASE(7)
-        default: INCCL_LL_CASE(8)
+        case 1: e = launch_R<1>(a, grid, vs, vd, st); break;
+        case 2: e = launch_R<2>(a, grid, vs, vd, st); break;
+        case 3: e = launch_R<3>(a, grid, vs, vd, st); break;
+        case 4: e = launch_R<4>(a, grid, vs, vd, st); break;
+        case 5: e = launch_R<5>(a, grid, vs, vd, st); break;
+        case 6: e = launch_R<6>(a, grid, vs, vd, st); break;
+        case 7: e = launch_R<7>(a, grid, vs, vd, st); break;
+        default: e = launch_R<8>(a, grid, vs, vd, st); break;
     }
-#undef INCCL_LL_CASE
     return e == hipSuccess ? 0 : (int)e;
 }

@@ -107,8 +107,8 @@ uint64_t inccl_wait_ticks(struct inccl_group *g)
     return (uint64_t)(ms * (double)khz);
 }
 
-static int ll_piece(struct inccl_communicator *c, int b16, const void *const *srcs, int R, void *dst, size_t n, int k,
-                    const uint32_t *amax, int scale_R, hipStream_t st)
+int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
+                   const uint32_t *amax, int scale_R, hipStream_t st)
 {
     const int W = c->group->world_size, me = c->group->rank;
     if (!c->ll_buf) {   /* the collective setup cannot run inside a graph capture */
@@ -124,10 +124,9 @@ static int ll_piece(struct inccl_communicator *c, int b16, const void *const *sr
         return inccl_set_error(INCCL_ERR_STATE, "ll: an earlier call timed out waiting for a peer (results invalid)");
     struct inccl_ll_launch l;
     memset(&l, 0, sizeof(l));
-    for (int r = 0; r < R; ++r) l.src[r] = (const float *)srcs[r];
+    for (int r = 0; r < R; ++r) l.src[r] = srcs[r];
     l.R = R;
-    l.dst = (float *)dst;
-    l.b16 = b16;
+    l.dst = dst;
     l.n = n;
     l.own_data = (uint32_t *)(c->ll_buf + LL_SIG_BYTES);
     l.slot_elems = c->ll_cap;
@@ -174,18 +173,4 @@ static int ll_piece(struct inccl_communicator *c, int b16, const void *const *sr
                     inccl_k_ll_grid(n), before[0], after[0], before[1], after[1]);
     }
     return 0;
-}
-
-int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
-                   const uint32_t *amax, int scale_R, hipStream_t st)
-{
-    return ll_piece(c, 0, (const void *const *)srcs, R, dst, n, k, amax, scale_R, st);
-}
-
-/* bf16 buckets: the same kernel with bf16 sources and result (the slots hold
- * the int32 partials, so the same element capacity) */
-int inccl_ll_piece_bf16(struct inccl_communicator *c, const uint16_t *const *srcs, int R, uint16_t *dst, size_t n,
-                        int k, const uint32_t *amax, int scale_R, hipStream_t st)
-{
-    return ll_piece(c, 1, (const void *const *)srcs, R, dst, n, k, amax, scale_R, st);
 }

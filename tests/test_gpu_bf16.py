@@ -176,7 +176,7 @@ def _p2p_rank(rank, world, port, q, engine="p2p"):
         grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=0)
         comm = inccl.inccl_communicator_create(grp, 0)
         ok = []
-        for R, n, k, seed in ((2, 1 << 20, 25, 1), (1, 300_001, "auto", 2), (2, 4099, 23, 3), (3, 65_537, "auto", 4)):
+        for R, n, k, seed in ((2, 1 << 20, 25, 1), (1, 300_001, "auto", 2), (2, 4099, 23, 3)):
             hs = []
             for r in range(world):
                 rng = np.random.default_rng(seed * 100 + r)
@@ -207,13 +207,12 @@ def _p2p_rank(rank, world, port, q, engine="p2p"):
 
 
 @pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (8, "p2p"), (2, "mesh"), (3, "mesh"), (4, "meshw"),
-                                          (8, "mesh"), (2, "ll"), (3, "ll"), (8, "ll")])
+                                          (8, "mesh")])
 def test_allreduce_bf16_p2p_multiprocess(gpu, world, engine):
     """The IPC engines' bf16 paths: p2p (bf16 result shards gathered, odd element
     counts through the gather's 2-byte tail; a 2-byte-aligned dst takes the int32
-    allreduce), mesh / meshw (the persistent kernel with bf16 sources and
-    results, any dst alignment) and ll (one kernel for buckets within its slot,
-    the p2p int32 allreduce above it), each also in place."""
+    allreduce) and mesh / meshw (the persistent kernel with bf16 sources and
+    results, any dst alignment), each also in place."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
