@@ -19,7 +19,27 @@
 #ifndef INCCL_AMD_API_H
 #define INCCL_AMD_API_H
 
+/* The system headers the reference api.h:1-18 hands to its callers (host.c
+ * uses printf, atoi, clock_t, clock() and CLOCKS_PER_SEC through them, never
+ * including them itself), minus <infiniband/verbs.h>, plus <time.h>, which
+ * the reference gets transitively from verbs.h. */
+#include <netinet/in.h>
+#include <arpa/inet.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
 #include <stdint.h>
+#include <inttypes.h>
+#include <endian.h>
+#include <byteswap.h>
+#include <stdbool.h>
+#include <getopt.h>
+#include <sys/time.h>
+#include <sys/types.h>
+#include <sys/socket.h>
+#include <netdb.h>
+#include <time.h>
 
 #ifdef __cplusplus
 extern "C" {

@@ -63,6 +63,28 @@ def test_host_example_binary(gpu, tmp_path):
         assert p.returncode == 0 and "result ok" in out, out + err
 
 
+def test_reference_host_binary(gpu):
+    """The reference's own program, repository/src/host.c compiled unchanged
+    against include/ and linked with libinccl_amd.so (oracle/Makefile `ref`,
+    built in the container where the reference lives), run exactly as the
+    reference runs it: `host <world> <master_ip> <rank>`, one process per rank.
+    Its own assert (host.c:51-55, dst[i] == 3*i) is the check; it prints
+    "result ok" only if every lane passed."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "host_ref")
+    if not os.path.isfile(exe):
+        pytest.skip("oracle/_ref/host_ref not built (needs the reference tree at build time)")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, INCCL_MASTER_PORT=str(port), INCCL_DEVICE="0", INCCL_BOOT_TIMEOUT="120")
+    ps = [subprocess.Popen([exe, "2", "127.0.0.1", str(r)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True, env=env) for r in range(2)]
+    outs = [p.communicate(timeout=240) for p in ps]
+    for p, (out, err) in zip(ps, outs):
+        assert p.returncode == 0 and "result ok" in out, out + err
+
+
 def test_host_stress_binary(gpu, tmp_path):
     """tests/c/host_stress.c through the C ABI alone: allreduce_write on pageable
     and on registered memory and allreduce_f32_host on pageable memory, 5 pipeline
