@@ -47,6 +47,115 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TUNE_CALLS = 10         # timed calls per engine candidate (after TUNE_CALLS / 2 untimed ones)
+T_START = time.monotonic()
+# what the process is doing now; the watchdog names it when it fires
+STAGE = {"stage": "start"}
+
+
+def self_launch(a) -> int:
+    """--gpus N > 1 with no WORLD_SIZE in the environment: start the N rank
+    processes ourselves (torch.distributed.run as a child, one rank per GPU,
+    rendezvous on 127.0.0.1) and return their exit code.  Runs before this
+    process touches the GPU; rank 0's JSON line reaches stdout directly."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench: launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+class Watchdog:
+    """Bounds the whole run from process start.  A collective that never
+    returns cannot be interrupted, so when the budget is spent this thread
+    emits what has been measured (rank 0), names the stage it was stuck in,
+    and ends the process with exit code 3: a hang never reads as success.
+    The budget default (480 s) sits well below the driver's 600 s limit."""
+
+    def __init__(self, budget_s: float, rank: int):
+        self.rank = rank
+        self.on_fire = None   # set once the headline exists: emits it with the error
+        self.t = threading.Timer(max(1.0, budget_s - (time.monotonic() - T_START)), self.fire)
+        self.t.daemon = True
+        self.budget_s = budget_s
+        self.t.start()
+
+    def fire(self):
+        msg = f"watchdog: run exceeded {self.budget_s:.0f} s from process start, stuck in: {STAGE['stage']}"
+        print(f"rank {self.rank}: {msg}", file=sys.stderr, flush=True)
+        if self.on_fire is not None:
+            self.on_fire(msg)
+        elif self.rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "error": msg}), flush=True)
+        os._exit(3)
+
+    def cancel(self):
+        self.t.cancel()
+
+
+METRIC = "GB/s device-resident fp32 bucket quantise+reduce, 256 MiB, 1/2/4/8 GPUs"
+
+
+def oracle_lanes(n: int, world: int, chunks: int, target: int) -> "list[int]":
+    """A deterministic lane sample of an n-element bucket: `target` evenly
+    strided lanes plus both sides of every shard and chunk boundary any engine
+    uses (the rank shards of chunk_plan, the plain n*g/W split, the mesh chunks'
+    256 KiB grid) and both ends."""
+    from container_inc_amd.plan import chunk_plan
+    stride = max(1, n // max(1, target))
+    lanes = set(range(0, n, stride))
+    cuts = {0, n}
+    for off, cnt, shard in chunk_plan(n, world, chunks):
+        for g in range(world + 1):
+            cuts.add(min(n, off + g * shard))
+        cuts.add(off + cnt)
+    for g in range(world + 1):
+        cuts.add(n * g // world)
+    for c in range(0, n, 1 << 16):   # 256 KiB of fp32: the mesh engines' chunk grid
+        cuts.add(c)
+    for c in cuts:
+        for d in (-1, 0):
+            if 0 <= c + d < n:
+                lanes.add(c + d)
+    return sorted(lanes)
+
+
+def oracle_check(srcs, out, lanes, k: int, rank: int, world: int, bf16: bool = False) -> dict:
+    """The C oracle as the checker of an N-rank result (outside any timed
+    region): every rank's R inputs and its output at `lanes` are gathered to
+    rank 0 over gloo; rank 0 runs orc_reduce_f32 (orc_reduce_bf16) on all W*R
+    inputs -- the reference's sum over every child, non_termination_switch.c:361-372,
+    behind the quantiser -- and compares every rank's output bit for bit."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    idx = torch.as_tensor(lanes, dtype=torch.int64, device=out.device)
+    rows = [s.index_select(0, idx) for s in srcs] + [out.index_select(0, idx)]
+    mine = torch.stack(rows).cpu()
+    mine = mine.view(torch.int16) if bf16 else mine.view(torch.int32)
+    if world > 1:
+        bucket = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
+        dist.gather(mine, gather_list=bucket, dst=0)
+    else:
+        bucket = [mine]
+    res = {"lanes": len(lanes), "ranks": world, "mismatches": None,
+           "checker": "oracle/inccl_oracle.c " + ("orc_reduce_bf16" if bf16 else "orc_reduce_f32")}
+    if rank == 0:
+        from oracle import oracle as O
+        R = len(srcs)
+        arr = [b.numpy() for b in bucket]
+        if bf16:
+            want = O.reduce_bf16([a[j].view(np.uint16) for a in arr for j in range(R)], k).view(np.uint16)
+            got = [a[R].view(np.uint16) for a in arr]
+        else:
+            want = O.reduce_f32([a[j].view(np.float32) for a in arr for j in range(R)], k).view(np.uint32)
+            got = [a[R].view(np.uint32) for a in arr]
+        res["mismatches"] = int(sum(np.count_nonzero(g != want) for g in got))
+    return res
 
 
 def parse():
@@ -140,28 +249,53 @@ def cpu_baseline_allcores(n_elems: int, R: int, k: int, seconds: float) -> dict:
 
 
 def cpu_reference_pipeline(seconds: float) -> dict:
-    """The reference's own per-element CPU path restated end to end, int32:
-    encode (api.c:300-302) -> root switch add per 1 KiB packet (nts.c:361-363) ->
-    egress frame build + ICRC per child (util.c:331-442) -> decode (api.c:428-430),
-    two ranks in one thread (oracle orc_allreduce_write_loopback with framing)."""
+    """BASELINE config 1 as SURVEY.md §8(d) states it: the reference's own
+    per-element CPU path restated end to end -- encode (api.c:300-302) -> root
+    switch add per 1 KiB packet (nts.c:361-363) -> egress frame build + ICRC per
+    child (util.c:331-442) -> decode (api.c:428-430) -- on one 4 MiB bucket per
+    rank, in one thread (oracle orc_allreduce_write_loopback with framing), at
+    2 ranks (the reference's FAN_IN, nts.c:23) and at 8 ranks (FAN_IN
+    generalised to one switch with 8 children).  Each rank count runs on int32
+    buckets (the reference's data) and on fp32 buckets through the quantiser
+    (orc_quantise_f32 before the encode, orc_dequantise_q32 after the decode,
+    k = 25).  Every run's result is checked against the plain sum."""
     import numpy as np
 
     from oracle import oracle as O
     m = 1 << 20   # 4 MiB bucket per rank (BASELINE config 1)
-    rng = np.random.default_rng(1)
-    xs = [rng.integers(-2 ** 31, 2 ** 31 - 1, m, dtype=np.int64).astype(np.int32) for _ in range(2)]
-    t0 = time.perf_counter()
-    iters = 0
-    while True:
-        rc, _, _ = O.allreduce_write_loopback(xs, with_icrc=True)
-        assert rc == m // 1024
-        iters += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(iters * m * 4 / dt / 1e9, 4), "unit": "GB/s of one rank's int32 bucket", "cores": 1,
-            "kind": "port", "sample": f"{iters} x loopback inccl_allreduce_write of 2 ranks x 4 MiB int32 with "
-                                      f"switch aggregation and ICRC framing, {dt:.1f} s"}
+    k = 25
+    rows = []
+    per = seconds / 4
+    for W in (2, 8):
+        rng = np.random.default_rng(1)
+        xi = [rng.integers(-2 ** 31, 2 ** 31 - 1, m, dtype=np.int64).astype(np.int32) for _ in range(W)]
+        xf = [rng.standard_normal(m).astype(np.float32) for _ in range(W)]
+        want_i = O.sum_q32(xi)
+        want_f = O.reduce_f32(xf, k)
+        for kind in ("int32", "fp32"):
+            t0 = time.perf_counter()
+            iters, ok = 0, True
+            while True:
+                if kind == "int32":
+                    rc, dsts, _ = O.allreduce_write_loopback(xi, with_icrc=True)
+                    ok = ok and all(np.array_equal(d, want_i) for d in dsts)
+                else:
+                    rc, dsts, _ = O.allreduce_write_loopback([O.quantise(x, k) for x in xf], with_icrc=True)
+                    outs = [O.dequantise(d, k) for d in dsts]
+                    ok = ok and all(np.array_equal(o.view(np.uint32), want_f.view(np.uint32)) for o in outs)
+                assert rc == m // 1024
+                iters += 1
+                if time.perf_counter() - t0 >= per:
+                    break
+            dt = time.perf_counter() - t0
+            rows.append({"ranks": W, "data": kind, "iters": iters, "ms_per_allreduce": round(dt / iters * 1e3, 2),
+                         "GBps_one_rank_bucket": round(iters * m * 4 / dt / 1e9, 4),
+                         "GBps_all_ranks": round(iters * W * m * 4 / dt / 1e9, 4), "correct": bool(ok)})
+    head = rows[0]
+    return {"value": head["GBps_one_rank_bucket"], "unit": "GB/s of one rank's int32 bucket", "cores": 1,
+            "kind": "port", "configs": rows,
+            "sample": f"loopback inccl_allreduce_write of 4 MiB per rank with switch aggregation and ICRC framing, "
+                      f"2 and 8 ranks, int32 and quantised fp32; `value` = 2 ranks int32, {head['iters']} calls"}
 
 
 # 4 KiB (one reference message, api.h:39) .. 256 MiB in x4 steps (BASELINE config 5),
@@ -247,16 +381,23 @@ def graph_replay_us(comm, xs, out, k: int, st, world: int, want, per: int = 20, 
     return dt, same
 
 
-def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
+def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: float, rows: list) -> list:
     """BASELINE config 5 at N > 1 (and north_star's 1024 MiB point): per bucket
     size and engine, host wall time per call over back-to-back calls (max over
-    ranks), GB/s, the xGMI link fraction, and whether the results of two
-    alternating input sets are bit-identical to the first engine's."""
+    ranks), GB/s, the xGMI link fraction, whether the results of two
+    alternating input sets are bit-identical to the first engine's, and a
+    sampled oracle check of each engine's result (`parity_vs_oracle`).
+    Rows are appended to `rows` as they finish (the watchdog reports a partial
+    sweep).  A size is started only while every rank is within
+    `soft_budget_s` of process start; the rest are skipped and listed."""
     import torch
     import torch.distributed as dist
-    rows = []
     for b in SWEEP_BYTES:
+        if agree([time.monotonic() - T_START], world)[0] > soft_budget_s:
+            rows.append({"bucket_bytes": b, "skipped": f"run past {soft_budget_s:.0f} s from process start"})
+            continue
         n = b // 4
+        lanes = oracle_lanes(n, world, 1, 4096)
         inputs = []
         for seed in (7000, 8000):
             gen = torch.Generator(device=dev)
@@ -275,6 +416,7 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
         if only:
             engines = tuple(e for e in only.split(",") if e in engines)
         for eng in engines:
+            STAGE["stage"] = f"sweep {b} B engine {eng}"
             ok, dt, same, got = 1, float("inf"), False, None
             try:
                 comm.set_engine(eng)
@@ -306,6 +448,7 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int) -> list:
                    "algbw_GBps": round(b / v[0] / 1e9, 2) if good else None,
                    "value_GBps": round(world * R * b / v[0] / 1e9, 2) if good else None}
             if good:
+                row["parity_vs_oracle"] = oracle_check(inputs[0], got[0], lanes, k, rank, world)
                 row["xgmi_frac"] = xgmi_roofline(world, b, v[0])["frac"]
                 if b <= (1 << 20) and eng != "p2p":   # the small-message floor without host launch cost
                     gdt, gsame = graph_replay_us(comm, inputs[0], out, k, st, world, refs[0] if refs else None)
@@ -339,7 +482,9 @@ def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256) -> li
     st = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize()
     rows, refs = [], None
+    lanes = oracle_lanes(n, world, 1, 1 << 16)
     for eng in ("rccl", "p2p", "mesh", "meshw"):
+        STAGE["stage"] = f"bf16 {mib} MiB engine {eng}"
         ok, dt, same = 1, float("inf"), False
         try:
             comm.set_engine(eng)
@@ -370,6 +515,7 @@ def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256) -> li
         row = {"engine": eng, "bucket_mib": mib, "R": R, "ok": good, "bit_identical": good and ident,
                "ms": round(v[0] * 1e3, 4) if good else None}
         if good:
+            row["parity_vs_oracle"] = oracle_check(inputs[0], got[0], lanes, 25, rank, world, bf16=True)
             link = (world - 1) * n * 6 // world
             row["GBps_buckets"] = round(world * R * 2 * n / v[0] / 1e9, 1)
             row["xgmi_frac"] = round(link / v[0] / 1e9 / ((world - 1) * XGMI_LINK_GBS_BIDIR), 4)
@@ -595,11 +741,18 @@ def host_e2e(comm, k: int, gib: int = 1, bucket_mib: int = 64) -> dict:
         comm.allreduce_f32_host(x, y, scale_exp=k, bucket_bytes=bucket_mib << 20)
     dt = (time.perf_counter() - t0) / reps
     # this box's PCIe ceiling on the same pinned buffers: H2D alone, D2H alone,
-    # and both at once on two streams (what the pipeline overlaps)
+    # and both at once on two streams (what the pipeline overlaps).  The streams
+    # have the greatest priority, as the pipeline's copy streams do (api.c
+    # comm_init): normal-priority ones can serialise the two directions, which
+    # would make this "ceiling" lower than the pipeline itself.
     dev = torch.device("cuda", torch.cuda.current_device())
     m = (bucket_mib << 20) // 4
     d_in, d_out = torch.empty(m, device=dev), torch.empty(m, device=dev)
-    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    try:
+        prio = torch.cuda.Stream.priority_range()[1]
+    except Exception:  # noqa: BLE001
+        prio = -1
+    s1, s2 = torch.cuda.Stream(device=dev, priority=prio), torch.cuda.Stream(device=dev, priority=prio)
 
     def copies(h2d: bool, d2h: bool) -> float:
         torch.cuda.synchronize()
@@ -620,7 +773,8 @@ def host_e2e(comm, k: int, gib: int = 1, bucket_mib: int = 64) -> dict:
     return {"gradient_GiB": gib, "bucket_MiB": bucket_mib, "streams": 3, "ms": round(dt * 1e3, 2),
             "GBps": round((gib << 30) / dt / 1e9, 2),
             "pcie_GBps_both_directions": round(2 * (gib << 30) / dt / 1e9, 2),
-            "copy_only_GBps": {"h2d": round(h2d, 2), "d2h": round(d2h, 2), "h2d_and_d2h_concurrent": round(both, 2)},
+            "copy_only_GBps": {"h2d": round(h2d, 2), "d2h": round(d2h, 2), "h2d_and_d2h_concurrent": round(both, 2),
+                               "stream_priority": prio},
             "frac_of_concurrent_copy": round((gib << 30) / dt / 1e9 / both, 4),
             "what": "pinned host fp32 -> H2D -> fused quantise+sum+dequantise -> D2H, wall clock"}
 
@@ -693,21 +847,28 @@ def load_traffic(workload: str):
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # nothing has touched the GPU yet: the ranks are separate fresh processes
+        sys.exit(self_launch(a))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        sys.exit(f"bench: WORLD_SIZE={world} but --gpus={a.gpus}: launch with --nproc-per-node equal to --gpus, "
+                 "or omit WORLD_SIZE and let bench.py start the ranks")
+    watchdog = Watchdog(float(os.environ.get("INCCL_BENCH_BUDGET", "480")), rank)
+
     import torch
     import torch.distributed as dist
 
     import container_inc_amd
     from container_inc_amd import inccl
+    from container_inc_amd._lib import runtime_libs
     from container_inc_amd.plan import chunk_plan
 
     if os.environ.get("INCCL_BENCH_WATCHDOG"):   # debugging aid: dump every thread's stack when stuck
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["INCCL_BENCH_WATCHDOG"]), repeat=True)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        print(f"warning: WORLD_SIZE={world} but --gpus={a.gpus}; using WORLD_SIZE", file=sys.stderr)
     # rehearsal hook: every rank on device 0 (a one-GPU box running N>1 over the
     # p2p engine; RCCL refuses two ranks on one GPU)
     if os.environ.get("INCCL_BENCH_SAME_DEVICE") == "1":
@@ -772,7 +933,9 @@ def main():
             if a.engine in ("auto", eng):
                 cands += [(eng, 1, {}), (eng, 1, {"INCCL_MESH_LAG": "32"})]
         best = None
+        tune_lanes = oracle_lanes(n, world, max(ch for _, ch, _ in cands), 1 << 16)
         for eng, ch, env in cands:
+            STAGE["stage"] = f"engine tuning: {eng} chunks={ch} {env or ''}"
             ok, dt, same, got = 1, float("inf"), False, None
             os.environ.update(env)
             try:
@@ -794,13 +957,21 @@ def main():
                 os.environ.pop(key, None)
             v = agree([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0], world)
             good = v[1] == 0.0 and v[2] == 0.0
+            par = None
+            if v[1] == 0.0:
+                # the candidate's result on input set A against the oracle: an
+                # engine that is only self-consistent never becomes the reference
+                par = oracle_check(srcs, got[0], tune_lanes, k, rank, world)
+                good = good and agree([float(par["mismatches"] or 0) if rank == 0 else 0.0], world)[0] == 0.0
             if good and refs is None:
                 refs = (got[0], got[1])
             if rank == 0:
                 print(f"tune {eng} chunks={ch} {env or ''}: ok={v[1] == 0.0} identical={v[2] == 0.0} "
-                      f"ms={v[0] * 1e3:.3f}", file=sys.stderr, flush=True)
+                      f"oracle_mismatches={par and par['mismatches']} ms={v[0] * 1e3:.3f}", file=sys.stderr,
+                      flush=True)
             tuning.append({"engine": eng, "chunks": ch, "env": env or None, "ok": v[1] == 0.0,
-                           "bit_identical": v[1] == 0.0 and v[2] == 0.0,
+                           "bit_identical": v[1] == 0.0 and v[2] == 0.0, "verified": good,
+                           "oracle_mismatches": par["mismatches"] if par else None,
                            "ms": round(v[0] * 1e3, 3) if v[1] == 0.0 else None})
             if good and (best is None or v[0] < best[0]):
                 best = (v[0], eng, ch, env)
@@ -819,6 +990,7 @@ def main():
     # settle: untimed steps in groups of 10 until --settle-seconds have passed (the
     # same count on every rank), so that the timed steps see steady state rather
     # than the first passes over freshly allocated buckets
+    STAGE["stage"] = f"settle/warmup/timed steps of engine {comm.engine if world > 1 else 'fused'}"
     settle_steps, t_settle = 0, time.perf_counter()
     while True:
         for _ in range(10):
@@ -863,7 +1035,16 @@ def main():
         verified = agree([float(bad)], world)[0] == 0.0
         del refs, srcs_b
 
+    # the timed path's result against the oracle on a lane sample: 2^20 strided
+    # lanes plus both sides of every shard / chunk boundary, every rank's inputs
+    # gathered to rank 0 (one more step first: `out` then holds srcs' result)
+    STAGE["stage"] = "oracle parity check of the timed engine"
+    step()
+    torch.cuda.synchronize()
+    parity = oracle_check(srcs, out, oracle_lanes(n, world, chunks, 1 << 20), k, rank, world)
+
     # dominant kernel alone: fused (N=1) or quant + local sum (N>1), HIP events on its stream
+    STAGE["stage"] = "dominant-kernel timing"
     kstream = torch.cuda.Stream(device=dev)
     qbuf = torch.empty(n, device=dev, dtype=torch.int32) if world > 1 else None
 
@@ -909,6 +1090,15 @@ def main():
         "alg_bytes_per_launch": alg_bytes,
         "kernel_ms": round(k_ms, 5),
     }
+    if world == 1:
+        # the same kernel rotating through 4 input/output sets (3 GiB, far past
+        # the 256 MiB Infinity Cache): `frac` re-reads the same buffers every
+        # launch, `frac_cold` cannot find them on die
+        STAGE["stage"] = "cold (rotated-set) kernel timing"
+        cold = cold_run(dev, R, k, n)
+        hbm_roofline["frac_cold"] = cold["frac"]
+        hbm_roofline["achieved_cold"] = cold["achieved"]
+        hbm_roofline["kernel_ms_cold"] = round(cold["kernel_us"] * 1e-3, 5)
 
     value = world * R * n * 4 / (ms_per_step * 1e-3) / 1e9
     res = {
@@ -944,7 +1134,12 @@ def main():
         # dominant HBM kernel's figure moves to `roofline_hbm_kernel`.
         "roofline": hbm_roofline if world == 1 else xgmi_roofline(world, n * 4, ms_per_step * 1e-3),
         "cpu_baseline": None,
+        "parity_vs_oracle": parity,
+        # the HIP / HSA / RCCL copies this rank is bound to (DESIGN.md "Runtimes")
+        "runtime": runtime_libs(),
     }
+    if world == 1:
+        res["roofline_cold"] = cold
     if world > 1:
         res["roofline_hbm_kernel"] = hbm_roofline
         res["verified_vs_reference_engine"] = verified
@@ -954,7 +1149,8 @@ def main():
         res["collective"] = {"algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2),
                              "bytes_per_rank": n * 4}
     # The one JSON line, printed once: by the main thread at the end, or by the
-    # sweep guard below if the N > 1 sweep overruns its budget.
+    # watchdog (with the stage it was stuck in, exit code 3) if the run overruns
+    # its budget -- from here on that line carries the measured headline.
     emit_lock, emitted = threading.Lock(), [False]
 
     def emit():
@@ -962,41 +1158,42 @@ def main():
             if emitted[0]:
                 return False
             emitted[0] = True
+        res["elapsed_s"] = round(time.monotonic() - T_START, 1)
         if rank == 0:
-            line = json.dumps(dict(res))   # a snapshot: the guard thread may emit while the main thread works
+            line = json.dumps(dict(res))   # a snapshot: the watchdog may emit while the main thread works
             print(line, flush=True)
             if a.json_out:
                 with open(a.json_out, "w") as f:
                     f.write(line + "\n")
         return True
 
+    def on_overrun(msg):
+        res["error"] = msg + "; headline measured and kept, later keys partial"
+        emit()
+
+    watchdog.on_fire = on_overrun
     if world > 1 and not a.no_sweep:
         for key in chosen[2]:   # the sweep runs every engine with its defaults
             os.environ.pop(key, None)
         # The sweep and the bf16 key run after the headline is measured.  They
-        # drive engines never before run across separate GPUs: should a collective
-        # hang there, the guard still emits the headline line (the sweep marked
-        # unfinished) and ends every rank, instead of losing the whole run.
-        budget = float(os.environ.get("INCCL_BENCH_SWEEP_BUDGET", "600"))
-
-        def overrun():
-            res["sweep_error"] = f"sweep / bf16 key unfinished after {budget:.0f} s; headline kept"
-            res.setdefault("sweep", None)
-            emit()
-            os._exit(0)
-
-        guard = threading.Timer(budget, overrun)
-        guard.daemon = True
-        guard.start()
+        # drive engines never before run across separate GPUs; a size is only
+        # started while the run is inside the soft budget, and a collective that
+        # hangs is ended by the watchdog (headline line + partial sweep, rc 3).
+        soft = float(os.environ.get("INCCL_BENCH_SWEEP_SOFT", "300"))
+        res["sweep"] = []
         if os.environ.get("INCCL_BENCH_TEST_HANG") == "1" and rank == 0:   # test hook: a stuck rank 0
+            STAGE["stage"] = "INCCL_BENCH_TEST_HANG sleep on rank 0"
             time.sleep(1e9)
-        res["sweep"] = size_sweep(comm, dev, R, k, rank, world)
-        res["bf16"] = bf16_engines(comm, dev, R, rank, world)
-        guard.cancel()
+        size_sweep(comm, dev, R, k, rank, world, soft, res["sweep"])
+        if agree([time.monotonic() - T_START], world)[0] <= soft:
+            res["bf16"] = bf16_engines(comm, dev, R, rank, world)
+        else:
+            res["bf16"] = {"skipped": f"run past {soft:.0f} s from process start"}
         comm.set_engine(chosen[0])
     def extra(key, fn):
         """An N = 1 extra key (one process, no collectives): a failure is recorded
         in the key instead of costing the headline line."""
+        STAGE["stage"] = f"extra key {key}"
         try:
             res[key] = fn()
         except Exception as e:  # noqa: BLE001
@@ -1007,7 +1204,6 @@ def main():
         extra("host_e2e", lambda: host_e2e(comm, k))
         extra("api_allreduce_write", lambda: api_allreduce_write(comm))
         extra("sizes", lambda: n1_sizes(dev, R, k))
-        extra("roofline_cold", lambda: cold_run(dev, R, k, n))
         extra("r_variants", lambda: r_variants(dev, k, n))
         extra("numerics_vs_exact", lambda: numerics_vs_exact(dev, n))
         extra("bf16", lambda: bf16_buckets(dev, R, k))
@@ -1016,6 +1212,8 @@ def main():
         extra("cpu_baseline_allcores", lambda: cpu_baseline_allcores(n, R, k, min(a.cpu_seconds, 5.0)))
         extra("cpu_reference_pipeline", lambda: cpu_reference_pipeline(min(a.cpu_seconds, 5.0)))
     emit()
+    watchdog.cancel()
+    STAGE["stage"] = "teardown"
     comm.destroy()
     grp.destroy()
     if world > 1:

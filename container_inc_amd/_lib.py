@@ -106,6 +106,40 @@ def load() -> ctypes.CDLL:
     return lib
 
 
+RUNTIME_LIBS = ("libamdhip64", "libhsa-runtime64", "librccl", "libinccl_amd")
+
+
+def runtime_libs() -> dict:
+    """Which HIP, HSA and RCCL runtimes this process has mapped, from
+    /proc/self/maps, and the HIP runtime's version (hipRuntimeGetVersion of the
+    copy the process bound to).  libinccl_amd.so is built against /opt/rocm's
+    headers but, loaded after torch, binds to torch's bundled runtimes (same
+    sonames); a C program binds to /opt/rocm's.  This records which."""
+    found = {}
+    try:
+        with open("/proc/self/maps") as f:
+            for ln in f:
+                parts = ln.split()
+                if len(parts) < 6:
+                    continue
+                path = parts[5]
+                base = os.path.basename(path)
+                for key in RUNTIME_LIBS:
+                    if base.startswith(key + ".so") and key not in found:
+                        found[key] = os.path.realpath(path)
+    except OSError:
+        pass
+    if "libamdhip64" in found:
+        try:
+            hip = ctypes.CDLL(found["libamdhip64"])
+            v = ctypes.c_int(0)
+            if hip.hipRuntimeGetVersion(ctypes.byref(v)) == 0:
+                found["hip_runtime_version"] = v.value
+        except OSError:
+            pass
+    return found
+
+
 def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = load().inccl_last_error().decode(errors="replace")

@@ -17,6 +17,26 @@ if ROOT not in sys.path:
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+def pytest_sessionstart(session):
+    """Which HIP / HSA / RCCL copies this test process is bound to (DESIGN.md
+    "Runtimes"), at the top of every test log (-q included)."""
+    tr = session.config.pluginmanager.get_plugin("terminalreporter")
+    if tr is not None:
+        tr.write_line(_runtime_line())
+
+
+def _runtime_line():
+    try:
+        import torch  # noqa: F401 -- loaded first, as the package does
+        import container_inc_amd as cia
+        if os.path.exists(cia.LIB_PATH):
+            cia.load()
+        from container_inc_amd._lib import runtime_libs
+        return f"runtime: {runtime_libs()}"
+    except Exception as e:  # noqa: BLE001
+        return f"runtime: unknown ({e!r})"
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X GPU (HIP kernels / RCCL)")
 

@@ -31,3 +31,60 @@ def test_sweep_sizes():
     assert sizes[0] == 4 << 10                      # one reference message (api.h:39)
     assert (256 << 20) in sizes and (1 << 30) in sizes
     assert all(y == 4 * x for x, y in zip(sizes[:-2], sizes[1:-1]))   # x4 steps up to 256 MiB
+
+
+def test_oracle_lanes_cover_boundaries():
+    b = _bench()
+    from container_inc_amd.plan import chunk_plan
+    for n, W, ch in ((1 << 20, 8, 1), ((1 << 20) + 37, 3, 4), (1000, 2, 1), (64, 8, 1)):
+        lanes = b.oracle_lanes(n, W, ch, 4096)
+        assert lanes == sorted(set(lanes)) and lanes[0] == 0 and lanes[-1] == n - 1
+        s = set(lanes)
+        for off, cnt, shard in chunk_plan(n, W, ch):
+            for g in range(W):
+                c = off + g * shard
+                if 0 < c < n:
+                    assert c in s and c - 1 in s
+        for g in range(1, W):
+            assert n * g // W in s
+
+
+def test_oracle_check_world1_detects_mismatch(orc):
+    """The bench's sampled oracle check at world 1, on CPU tensors: the
+    oracle's own result passes, one flipped lane at a sampled index fails."""
+    import numpy as np
+    import torch
+    b = _bench()
+    rng = np.random.default_rng(5)
+    xs = [rng.standard_normal(5000).astype(np.float32) for _ in range(3)]
+    want = orc.reduce_f32(xs, 25)
+    srcs = [torch.from_numpy(x) for x in xs]
+    out = torch.from_numpy(want.copy())
+    lanes = b.oracle_lanes(5000, 1, 1, 100)
+    r = b.oracle_check(srcs, out, lanes, 25, 0, 1)
+    assert r["mismatches"] == 0 and r["lanes"] == len(lanes)
+    out[lanes[7]] += 1.0
+    assert b.oracle_check(srcs, out, lanes, 25, 0, 1)["mismatches"] == 1
+
+
+def test_world_size_mismatch_is_an_error():
+    import os
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE=2 but --gpus=1" in p.stderr
+
+
+def test_watchdog_emits_line_and_exits_nonzero():
+    """A run past its budget prints one JSON line naming the stuck stage and
+    exits 3 (a hang never reads as success)."""
+    import json
+    import os
+    import subprocess
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; bench.STAGE['stage'] = 'sweep 4096 B engine x'; "
+            "w = bench.Watchdog(1.0, 0); time.sleep(30)" % ROOT)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 3, p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["value"] is None and "sweep 4096 B engine x" in line["error"]

@@ -116,3 +116,52 @@ def test_gloo_world2_decomposition(orc, n, chunks):
     for p in ps:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def _oracle_check_rank(rank, world, port, q):
+    import os
+    import sys
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from oracle import oracle as O
+    n, R, k = 3000, 2, 25
+    xs = [np.random.default_rng(100 * r + j).standard_normal(n).astype(np.float32)
+          for r in range(world) for j in range(R)]
+    want = O.reduce_f32(xs, k)
+    mine = [torch.from_numpy(xs[rank * R + j]) for j in range(R)]
+    out = torch.from_numpy(want.copy())
+    lanes = bench.oracle_lanes(n, world, 1, 200)
+    good = bench.oracle_check(mine, out, lanes, k, rank, world)
+    if rank == 1:
+        out[lanes[3]] = -out[lanes[3]] + 1.0
+    bad = bench.oracle_check(mine, out, lanes, k, rank, world)
+    q.put((rank, good["mismatches"], bad["mismatches"]))
+    dist.destroy_process_group()
+
+
+def test_bench_oracle_check_gloo_world2():
+    """bench.py's N>1 parity check: every rank's inputs and output at the
+    sampled lanes are gathered to rank 0 over gloo and checked against the
+    oracle's sum over all W*R buckets; a wrong lane on rank 1 is counted."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_oracle_check_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((r, (g, b)) for r, g, b in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0] == (0, 1)          # rank 0 reports: clean, then exactly one bad lane
+    assert res[1] == (None, None)    # other ranks only contribute
