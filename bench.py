@@ -136,7 +136,8 @@ def oracle_check(srcs, out, lanes, k: int, rank: int, world: int, bf16: bool = F
     idx = torch.as_tensor(lanes, dtype=torch.int64, device=out.device)
     rows = [s.index_select(0, idx) for s in srcs] + [out.index_select(0, idx)]
     mine = torch.stack(rows).cpu()
-    mine = mine.view(torch.int16) if bf16 else mine.view(torch.int32)
+    # gloo gathers no 16-bit integers: bf16 bit patterns travel widened to int32
+    mine = mine.view(torch.int16).to(torch.int32) if bf16 else mine.view(torch.int32)
     if world > 1:
         bucket = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
         dist.gather(mine, gather_list=bucket, dst=0)
@@ -149,8 +150,8 @@ def oracle_check(srcs, out, lanes, k: int, rank: int, world: int, bf16: bool = F
         R = len(srcs)
         arr = [b.numpy() for b in bucket]
         if bf16:
-            want = O.reduce_bf16([a[j].view(np.uint16) for a in arr for j in range(R)], k).view(np.uint16)
-            got = [a[R].view(np.uint16) for a in arr]
+            want = O.reduce_bf16([a[j].astype(np.uint16) for a in arr for j in range(R)], k).view(np.uint16)
+            got = [a[R].astype(np.uint16) for a in arr]
         else:
             want = O.reduce_f32([a[j].view(np.float32) for a in arr for j in range(R)], k).view(np.uint32)
             got = [a[R].view(np.uint32) for a in arr]
@@ -1184,9 +1185,19 @@ def main():
         if os.environ.get("INCCL_BENCH_TEST_HANG") == "1" and rank == 0:   # test hook: a stuck rank 0
             STAGE["stage"] = "INCCL_BENCH_TEST_HANG sleep on rank 0"
             time.sleep(1e9)
-        size_sweep(comm, dev, R, k, rank, world, soft, res["sweep"])
+        # an exception here (the same on every rank: the keys' collectives are
+        # symmetric) is recorded in the line instead of costing the headline
+        try:
+            size_sweep(comm, dev, R, k, rank, world, soft, res["sweep"])
+        except Exception as e:  # noqa: BLE001
+            print(f"rank {rank}: sweep failed: {e!r}", file=sys.stderr, flush=True)
+            res["sweep_error"] = repr(e)
         if agree([time.monotonic() - T_START], world)[0] <= soft:
-            res["bf16"] = bf16_engines(comm, dev, R, rank, world)
+            try:
+                res["bf16"] = bf16_engines(comm, dev, R, rank, world)
+            except Exception as e:  # noqa: BLE001
+                print(f"rank {rank}: bf16 key failed: {e!r}", file=sys.stderr, flush=True)
+                res["bf16"] = {"error": repr(e)}
         else:
             res["bf16"] = {"skipped": f"run past {soft:.0f} s from process start"}
         comm.set_engine(chosen[0])

@@ -88,3 +88,18 @@ def test_watchdog_emits_line_and_exits_nonzero():
     assert p.returncode == 3, p.stderr
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["value"] is None and "sweep 4096 B engine x" in line["error"]
+
+
+def test_oracle_check_bf16_world1(orc):
+    import numpy as np
+    import torch
+    b = _bench()
+    rng = np.random.default_rng(6)
+    xs = [orc.f32_to_bf16(rng.standard_normal(700).astype(np.float32)) for _ in range(2)]
+    want = orc.reduce_bf16(xs, 25)
+    srcs = [torch.from_numpy(x.view(np.int16)).view(torch.bfloat16) for x in xs]
+    out = torch.from_numpy(want.view(np.int16).copy()).view(torch.bfloat16)
+    lanes = b.oracle_lanes(700, 1, 1, 50)
+    assert b.oracle_check(srcs, out, lanes, 25, 0, 1, bf16=True)["mismatches"] == 0
+    out.view(torch.int16)[lanes[2]] ^= 1
+    assert b.oracle_check(srcs, out, lanes, 25, 0, 1, bf16=True)["mismatches"] == 1

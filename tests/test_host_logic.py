@@ -141,7 +141,13 @@ def _oracle_check_rank(rank, world, port, q):
     if rank == 1:
         out[lanes[3]] = -out[lanes[3]] + 1.0
     bad = bench.oracle_check(mine, out, lanes, k, rank, world)
-    q.put((rank, good["mismatches"], bad["mismatches"]))
+    # bf16 buckets: 16-bit patterns, which gloo only gathers widened
+    hb = [O.f32_to_bf16(x[:300]) for x in xs]
+    wb = O.reduce_bf16(hb, k)
+    mb = [torch.from_numpy(hb[rank * R + j].view(np.int16)).view(torch.bfloat16) for j in range(R)]
+    ob = torch.from_numpy(wb.view(np.int16).copy()).view(torch.bfloat16)
+    gb = bench.oracle_check(mb, ob, bench.oracle_lanes(300, world, 1, 50), k, rank, world, bf16=True)
+    q.put((rank, good["mismatches"], bad["mismatches"], gb["mismatches"]))
     dist.destroy_process_group()
 
 
@@ -160,8 +166,8 @@ def test_bench_oracle_check_gloo_world2():
     ps = [ctx.Process(target=_oracle_check_rank, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict((r, (g, b)) for r, g, b in (q.get(timeout=120) for _ in ps))
+    res = dict((r, (g, b, h)) for r, g, b, h in (q.get(timeout=120) for _ in ps))
     for p in ps:
         p.join(timeout=60)
-    assert res[0] == (0, 1)          # rank 0 reports: clean, then exactly one bad lane
-    assert res[1] == (None, None)    # other ranks only contribute
+    assert res[0] == (0, 1, 0)             # rank 0 reports: clean, one bad lane, clean bf16
+    assert res[1] == (None, None, None)    # other ranks only contribute
