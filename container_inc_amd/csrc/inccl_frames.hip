@@ -391,15 +391,43 @@ __device__ void build_header_image(uint8_t* fr, const InccFrameTemplate& h, bool
     bth[4] = (uint8_t)(q >> 24); bth[5] = (uint8_t)(q >> 16); bth[6] = (uint8_t)(q >> 8); bth[7] = (uint8_t)q;
 }
 
+// Egress ICRC by linearity.  The raw CRC (init 0, no final XOR) of a message
+// of fixed length is linear over GF(2) in its bytes, so an egress frame's ICRC
+// message -- [4 x 0xFF][masked IP .. BTH (.. RETH)][1024-B payload], L =
+// doff + 1014 bytes -- splits into parts computed at different rates:
+//   P   the payload (shared by every child of an input frame): 64 lanes x 16 B,
+//       each lane's segment CRC (32 nibble lookups) shifted past the segments
+//       after it (Z_{16 (63 - lane)}, 8 lookups), XOR over the wave -- once per
+//       input frame, from registers;
+//   H_c the header with opcode, PSN and RETH zeroed: constant per (child,
+//       RETH flag), computed once per block at start-up;
+//   V   opcode + PSN (5 bytes, shared by the children) and each child's RETH
+//       (16 bytes): one table lookup pair per byte from tables that hold each
+//       byte position's contribution already shifted to the message end.
+// ICRC = ~(P ^ V_op,psn ^ H_c ^ V_reth,c): the per-child CRC work is one RETH
+// reduction (RETH frames only), not a pass over the 1 KiB frame.
+constexpr int kVarBytes = 21;   // opcode, 4 PSN bytes, 16 RETH bytes
+__device__ uint32_t g_lane16[8][16][kWave];            // [nibble][value][lane] = Z_{16 (63 - lane)}(value << 4 nibble)
+__device__ uint32_t g_var[2][kVarBytes][2][16];       // [reth][byte][nibble][value]: contribution at the message end
+__device__ uint32_t g_z1024[8][16];                   // Z_1024(value << 4 nibble)
+
+struct EgressLds {
+    uint32_t seg[kSeg][2][16];      // g_seg: rows 1..16 are a 16-byte segment's Z_{15-j}
+    uint32_t lane16[8][16][kWave];
+    uint32_t var[2][kVarBytes][2][16];
+    uint32_t z1024[8][16];
+    uint32_t hcrc[2 * 31];          // H_c for (child, RETH flag)
+};
+
 // What one egress wave needs from global memory for input frame f: loaded one
 // frame ahead of its use (k_egress), so these dependent loads overlap the
-// previous frame's build + CRC instead of stalling the wave.
+// previous frame's build instead of stalling the wave.
 struct EgressIn {
     int act, port;
     uint32_t psn, slot;
     uint32_t op;        // bytes 40-43 of the input frame across lanes (opcode: lane 2)
     uint32_t reth;      // lane 4c+i: word i of child c's RETH (c < 16)
-    int32_t agg[4];     // word j * 64 + lane of the slot's aggregate
+    int32_t agg[4];     // words 4 lane .. 4 lane + 3 of the slot's aggregate: this lane's 16 payload bytes
 };
 
 // Branch-free, so that no wait is needed until egress_emit uses the values: the
@@ -420,78 +448,161 @@ __device__ __forceinline__ EgressIn egress_fetch(const InccSwitchState& s, const
     e.op = in_frames[f * in_stride + 40 + (lane & 3)];
     e.slot = e.psn & (s.slots - 1);
     e.reth = lane < 4 * fan ? s.reth[(size_t)e.slot * fan * 4 + lane] : 0u;
-    const int32_t* agg = s.agg + (size_t)e.slot * kLanes;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) e.agg[j] = agg[j * kWave + lane];
+    typedef int32_t i4 __attribute__((ext_vector_type(4)));
+    const i4 v = reinterpret_cast<const i4*>(s.agg + (size_t)e.slot * kLanes)[lane];   // one dwordx4 per lane
+    e.agg[0] = v.x; e.agg[1] = v.y; e.agg[2] = v.z; e.agg[3] = v.w;
     return e;
+}
+
+__device__ __forceinline__ uint32_t wave_xor(uint32_t c)
+{
+    // the DPP XOR-reduction of icrc_wave: lane 63 ends with the whole wave's XOR
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x141, 0xF, 0xF, false);
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x140, 0xF, 0xF, false);
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x142, 0xA, 0xF, false);
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x143, 0xC, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)c, 63);
+}
+
+// A 16-byte segment's raw CRC (bytes in memory order in a[0..3], little-endian
+// words) shifted by Z_{16 (63 - sh_lane)}.
+__device__ __forceinline__ uint32_t seg16_crc(const EgressLds& t, const uint32_t (&a)[4], int sh_lane)
+{
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c ^= t.seg[4 * k + (i >> 1) + 1][i & 1][(a[k] >> (4 * i)) & 15u];
+    }
+    uint32_t r = 0;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) r ^= t.lane16[n][(c >> (4 * n)) & 15u][sh_lane];
+    return r;
+}
+
+__device__ __forceinline__ uint32_t var_crc(const EgressLds& t, int wf, int k, uint32_t b)
+{
+    return t.var[wf][k][0][b & 15u] ^ t.var[wf][k][1][(b >> 4) & 15u];
+}
+
+// H_c for every (child, RETH flag) of the block's templates: quad q of wave w
+// takes pair i = 16 w + q.  The header part of the message (doff - 10 bytes:
+// 44, or 60 with RETH) is right-aligned in a 64-byte window (leading zeros do
+// not change a raw CRC); lane s of the quad takes window bytes 16 s .. 16 s + 15.
+__device__ void header_crcs(EgressLds& t, const uint8_t (*himg)[kHdrImg], int fan, int w, int lane)
+{
+    const int i = w * 16 + (lane >> 2), s = lane & 3;
+    uint32_t c = 0;
+    if (i < 2 * fan) {
+        const int wf = i & 1;
+        const int hdr = wf ? 60 : 44;
+        uint32_t a[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int p = 16 * s + 4 * k + b - (64 - hdr);   // header byte; frame byte p + 10
+                uint32_t byte = 0;
+                if (p >= 0) {
+                    const int fo = p + 10;
+                    bool ff = fo < 14;
+#pragma unroll
+                    for (int m = 4; m < kNumMasked; ++m) ff = ff || fo == masked_pos(m);
+                    byte = ff ? 0xFFu : himg[i][fo];
+                }
+                v |= byte << (8 * b);
+            }
+            a[k] = v;
+        }
+        c = seg16_crc(t, a, 60 + s);
+    }
+    c ^= (uint32_t)__shfl_xor((int)c, 1, kWave);
+    c ^= (uint32_t)__shfl_xor((int)c, 2, kWave);
+    uint32_t r = 0;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) r ^= t.z1024[n][(c >> (4 * n)) & 15u];   // past the 1024-byte payload
+    if (i < 2 * fan && s == 0) t.hcrc[i] = r;
 }
 
 // Every output frame of input frame f (rows f * fan_in + c): all fan_in children
 // on COMPLETED (the broadcast, nts.c:368-371), the sender's child on REPLAY
 // (nts.c:353-356).  The payload (htonl of the aggregate, util.c:403-405 /
 // :419-421) is written into the LDS frame once and shared by the children; each
-// child rewrites only the header bytes before its ICRC and copy-out.
+// child rewrites only its header words and ICRC, all lanes at once.
 __device__ void egress_emit(const InccSwitchState& s, const EgressIn& e, const uint8_t (*himg)[kHdrImg],
                             uint8_t* __restrict__ out, int64_t out_stride, bool out16, int32_t* __restrict__ out_len,
-                            const CrcLds& t, uint8_t* frbuf, int64_t f, int lane)
+                            const EgressLds& t, uint8_t* frbuf, int64_t f, int lane)
 {
     const int fan = s.fan_in;
     const bool all = e.act == INCCL_SW_COMPLETED;
     const bool one = e.act == INCCL_SW_REPLAY && e.port >= 0 && e.port < fan;
-    const uint32_t op = (uint32_t)__shfl((int)e.op, 2, kWave);
-    const bool wf = is_write_first((uint8_t)op);
-    const int total = 14 + 20 + 8 + 12 + (wf ? 16 : 0) + kLanes * 4 + 4;   // util.c:341-345
+    const uint32_t op = (uint32_t)__shfl((int)e.op, 2, kWave) & 0xFFu;
+    const int wf = is_write_first((uint8_t)op) ? 1 : 0;
+    const int doff = 54 + 16 * wf;
+    const int total = doff + kLanes * 4 + 4;   // util.c:341-345
     if (lane < fan) out_len[f * fan + lane] = (all || (one && lane == e.port)) ? total : 0;
     if (!all && !one) return;
     uint8_t* fr = frbuf;
-    const int doff = 54 + (wf ? 16 : 0);
-    // offsets 54 / 70 are 2-byte aligned: 16-bit LDS stores
-    uint16_t* d16 = reinterpret_cast<uint16_t*>(fr + doff);
+    // this lane's 16 payload bytes (big-endian words, util.c:403-405), memory order
+    uint32_t a[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int i = j * kWave + lane;
-        const uint32_t be = __builtin_bswap32((uint32_t)e.agg[j]);
-        d16[2 * i] = (uint16_t)be;
-        d16[2 * i + 1] = (uint16_t)(be >> 16);
+    for (int k = 0; k < 4; ++k) a[k] = __builtin_bswap32((uint32_t)e.agg[k]);
+    // payload into the LDS frame at doff + 16 lane (doff = 2 mod 4): a 16-bit
+    // store, three aligned dwords, a 16-bit store
+    {
+        uint8_t* p = fr + doff + 16 * lane;
+        *reinterpret_cast<uint16_t*>(p) = (uint16_t)a[0];
+        *reinterpret_cast<uint32_t*>(p + 2) = __builtin_amdgcn_alignbyte(a[1], a[0], 2);
+        *reinterpret_cast<uint32_t*>(p + 6) = __builtin_amdgcn_alignbyte(a[2], a[1], 2);
+        *reinterpret_cast<uint32_t*>(p + 10) = __builtin_amdgcn_alignbyte(a[3], a[2], 2);
+        *reinterpret_cast<uint16_t*>(p + 14) = (uint16_t)(a[3] >> 16);
     }
+    // P ^ V_op,psn: the payload's contribution (this lane's segment) and, on
+    // lanes 0-4, the opcode and the four PSN bytes (util.c:378, :386)
+    const uint32_t pw = e.psn | 0x80000000u;
+    uint32_t pv = seg16_crc(t, a, lane);
+    if (lane < 5) {
+        const uint32_t b = lane == 0 ? op : (pw >> (8 * (4 - lane))) & 0xFFu;
+        pv ^= var_crc(t, wf, lane, b);
+    }
+    const uint32_t pc = wave_xor(pv);
     const int c0 = all ? 0 : e.port, c1 = all ? fan : e.port + 1;
     for (int c = c0; c < c1; ++c) {
-        // header bytes 0-49 from the image (50-53 are the PSN, below; the image's
-        // bytes past 53 would overlap the shared payload)
-        if (lane < 13)
-            reinterpret_cast<uint32_t*>(fr)[lane] = reinterpret_cast<const uint32_t*>(himg[c * 2 + (wf ? 1 : 0)])[lane];
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {                                             // util.c:378, :386
-            const uint32_t p = e.psn | 0x80000000u;
-            fr[42] = (uint8_t)op;
-            fr[50] = (uint8_t)(p >> 24); fr[51] = (uint8_t)(p >> 16); fr[52] = (uint8_t)(p >> 8); fr[53] = (uint8_t)p;
+        // child c's RETH words (reth_keeper[slot][c], nts.c:442): lane 4c+i of
+        // e.reth for c < 16, else from memory
+        uint32_t r = 0, rk = 0;
+        if (wf) {
+            const int src = (4 * c + (lane & 3)) & (kWave - 1);
+            r = (uint32_t)__shfl((int)e.reth, src, kWave);
+            if (c >= kWave / 4) r = s.reth[((size_t)e.slot * fan + c) * 4 + (lane & 3)];
+            // lane k < 16: RETH byte k = byte k & 3 of word k >> 2
+            rk = (uint32_t)__shfl((int)r, lane >> 2, kWave);
         }
-        if (wf) {                                                    // util.c:409-417, reth_keeper[slot][c]
-            uint32_t r = (uint32_t)__shfl((int)e.reth, (4 * c + (lane & 3)) & (kWave - 1), kWave);
-            if (c >= kWave / 4 && lane < 4) r = s.reth[((size_t)e.slot * fan + c) * 4 + lane];
-            if (lane < 4) {
-                uint16_t* r16 = reinterpret_cast<uint16_t*>(fr + 54);
-                r16[2 * lane] = (uint16_t)r;
-                r16[2 * lane + 1] = (uint16_t)(r >> 16);
-            }
+        uint32_t vr = 0;
+        if (wf) vr = wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
+        const uint32_t crc = ~(pc ^ t.hcrc[2 * c + wf] ^ vr);   // util.c:424-426
+        // header words 0-12 (bytes 0-51) from the image, opcode and PSN patched in
+        if (lane < 13) {
+            uint32_t hw = reinterpret_cast<const uint32_t*>(himg[2 * c + wf])[lane];
+            if (lane == 10) hw = (hw & 0xFF00FFFFu) | (op << 16);                            // byte 42
+            if (lane == 12) hw = (hw & 0x0000FFFFu) | ((pw >> 24) << 16) | (((pw >> 16) & 0xFFu) << 24);   // 50-51
+            reinterpret_cast<uint32_t*>(fr)[lane] = hw;
+        } else if (lane == 13) {                                                               // 52-53
+            *reinterpret_cast<uint16_t*>(fr + 52) = (uint16_t)(((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8));
         }
-        __builtin_amdgcn_wave_barrier();
-        uint8_t saved = 0;
-        if (lane < kNumMasked) {
-            saved = fr[masked_pos(lane)];
-            fr[masked_pos(lane)] = 0xFF;
+        if (wf) {                                                   // util.c:409-417: bytes 54-69
+            const int k = lane - 14;                                // lanes 14..18
+            const uint32_t rlo = (uint32_t)__shfl((int)r, (k - 1) & 3, kWave);
+            const uint32_t rhi = (uint32_t)__shfl((int)r, k & 3, kWave);
+            if (k == 0) *reinterpret_cast<uint16_t*>(fr + 54) = (uint16_t)rhi;
+            else if (k >= 1 && k <= 3) *reinterpret_cast<uint32_t*>(fr + 52 + 4 * k) = __builtin_amdgcn_alignbyte(rhi, rlo, 2);
+            else if (k == 4) *reinterpret_cast<uint16_t*>(fr + 68) = (uint16_t)(rlo >> 16);
         }
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t crc = icrc_wave(fr, t, lane);                // util.c:424-426
-        __builtin_amdgcn_wave_barrier();
-        if (lane < kNumMasked) fr[masked_pos(lane)] = saved;
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {                                             // stored host order (LE)
-            fr[total - 4] = (uint8_t)crc;
-            fr[total - 3] = (uint8_t)(crc >> 8);
-            fr[total - 2] = (uint8_t)(crc >> 16);
-            fr[total - 1] = (uint8_t)(crc >> 24);
-        }
+        if (lane == 0) *reinterpret_cast<uint16_t*>(fr + total - 4) = (uint16_t)crc;           // stored host order (LE)
+        if (lane == 1) *reinterpret_cast<uint16_t*>(fr + total - 2) = (uint16_t)(crc >> 16);
         __builtin_amdgcn_wave_barrier();
         uint8_t* o = out + (f * fan + c) * out_stride;
         // fixed trip counts (total <= 1098 B): the compiler can then count this
@@ -528,14 +639,19 @@ __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState 
                                                                uint8_t* __restrict__ out, int64_t out_stride,
                                                                int32_t* __restrict__ out_len)
 {
-    __shared__ CrcLds t;
+    __shared__ EgressLds t;
     __shared__ __attribute__((aligned(16))) uint8_t buf[kEgressWaves][kFrameMax];
     __shared__ __attribute__((aligned(16))) uint8_t himg[2 * 31][kHdrImg];
-    load_tables(t);
+    for (int i = threadIdx.x; i < kSeg * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg[0][0][0])[i];
+    for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) (&t.lane16[0][0][0])[i] = (&g_lane16[0][0][0])[i];
+    for (int i = threadIdx.x; i < 2 * kVarBytes * 2 * 16; i += blockDim.x) (&t.var[0][0][0][0])[i] = (&g_var[0][0][0][0])[i];
+    for (int i = threadIdx.x; i < 8 * 16; i += blockDim.x) (&t.z1024[0][0])[i] = (&g_z1024[0][0])[i];
     const int fan = s.fan_in;
     for (int i = threadIdx.x; i < 2 * fan; i += blockDim.x) build_header_image(himg[i], tmpl[i >> 1], (i & 1) != 0);
     __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    header_crcs(t, himg, fan, w, lane);
+    __syncthreads();
     const bool out16 = ((out_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
     // Round r covers frames [r * step, (r + 1) * step); in round r this wave
     // takes frame r * step + (wave + r) mod step.  Rotating the offset by one per
@@ -593,6 +709,9 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_recycle(InccSwitchSta
 uint32_t host_tab[256];
 uint32_t host_seg[kSeg][2][16];
 uint32_t host_lane_shift[8][16][kWave];
+uint32_t host_lane16[8][16][kWave];
+uint32_t host_var[2][kVarBytes][2][16];
+uint32_t host_z1024[8][16];
 bool g_tables_ready[64];
 std::mutex g_tables_mu;
 
@@ -626,8 +745,31 @@ int ensure_tables()
                 x = zeros_append(x, kSeg);
             }
         }
+    // egress by linearity (k_egress): Z_{16 (63 - lane)}, each variable header
+    // byte's contribution shifted to the message end, and Z_1024
+    for (int n = 0; n < 8; ++n)
+        for (uint32_t v = 0; v < 16; ++v) {
+            uint32_t x = v << (4 * n);
+            host_z1024[n][v] = zeros_append(x, 1024);
+            for (int lane = kWave - 1; lane >= 0; --lane) {
+                host_lane16[n][v][lane] = x;
+                x = zeros_append(x, 16);
+            }
+        }
+    for (int wf = 0; wf < 2; ++wf) {
+        const int hdr = wf ? 60 : 44;   // ICRC message bytes before the payload (frame 10 .. doff - 1)
+        for (int k = 0; k < kVarBytes; ++k) {
+            const int p = k == 0 ? 32 : 39 + k;   // message position: opcode (frame 42), PSN (50-53), RETH (54-69)
+            for (int h = 0; h < 2; ++h)
+                for (uint32_t v = 0; v < 16; ++v)
+                    host_var[wf][k][h][v] = p < hdr ? zeros_append(host_tab[v << (4 * h)], hdr - 1 - p + 1024) : 0u;
+        }
+    }
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg), host_seg, sizeof(host_seg));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane_shift), host_lane_shift, sizeof(host_lane_shift));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane16), host_lane16, sizeof(host_lane16));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_var), host_var, sizeof(host_var));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_z1024), host_z1024, sizeof(host_z1024));
     if (e != hipSuccess) return (int)e;
     if (dev >= 0 && dev < 64) g_tables_ready[dev] = true;
     return 0;

@@ -27,10 +27,22 @@
 #define INCCL_MAX_HOST_REGIONS 16
 #define INCCL_MESH_REGIONS 4
 /* Largest single allocation exported over HIP IPC.  Importing a peer's 2.5 GiB
- * allocation never returned in processes running torch's bundled HIP runtime
- * (ROCm 7.0; DESIGN.md "2 GiB per IPC export"), so every IPC buffer is split
- * or refused below 2 GiB. */
-#define INCCL_IPC_MAX_BYTES (((size_t)2 << 30) - ((size_t)2 << 20))
+ * mesh buffer never returned in round 2's two-rank bench (DESIGN.md "2 GiB per
+ * IPC export"); a two-process C probe imports 2.6 GB one-way and both ways at
+ * once, coarse and uncached, on torch's HIP 7.0 and on /opt/rocm's 7.2 alike
+ * (profiles/r03/ipc_runtime_probe.log), so the runtime is not the cause.
+ * Every IPC buffer stays split or refused below 2 GiB by default;
+ * $INCCL_IPC_MAX_BYTES (same on every rank) raises the bound for the probe
+ * that tests the engines beyond it (tools/ipc_big_engine_probe.py). */
+#define INCCL_IPC_MAX_BYTES_DEFAULT (((size_t)2 << 30) - ((size_t)2 << 20))
+#include <stdlib.h>
+static inline size_t inccl_ipc_max_bytes(void)
+{
+    const char *e = getenv("INCCL_IPC_MAX_BYTES");
+    const unsigned long long v = e ? strtoull(e, NULL, 0) : 0;
+    return v ? (size_t)v : INCCL_IPC_MAX_BYTES_DEFAULT;
+}
+#define INCCL_IPC_MAX_BYTES (inccl_ipc_max_bytes())
 
 struct inccl_local_hub;
 struct inccl_shm_bar;
