@@ -300,13 +300,14 @@ int inccl_group_barrier(struct inccl_group *g)
  * Calls alternate between two banks of words, so no second barrier is needed:
  * a rank writes bank b again only in the call after next, which it reaches
  * after the next call's barrier -- i.e. after every rank has finished reading
- * bank b in this call. */
+ * bank b in this call.  The bank sequence is per group: calls on one group
+ * must not run concurrently (communicators that share a group from different
+ * threads serialise their auto-scale calls themselves). */
 int inccl_group_allreduce_max_u32(struct inccl_group *g, uint32_t *v)
 {
     if (g->world_size == 1) return 0;
     struct inccl_shm_bar *b = g->shm_bar;
-    const char *tcp = getenv("INCCL_HOST_MAX_TCP");   /* measurement knob: the TCP allgather regardless */
-    if (b && !(tcp && atoi(tcp) != 0)) {
+    if (b) {
         _Atomic uint32_t *words = b->words[g->max_seq++ & 1u];
         atomic_store(&words[g->rank], *v);
         int rc = inccl_group_barrier(g);   /* every word of this bank written */

@@ -17,8 +17,10 @@ of its largest element.  The averaged result is bit-identical to the oracle's
 ``reduce_f32`` of the same buckets divided by the world size.
 
 fp32 and bf16 CUDA buckets are accepted (bf16 through ``inccl_allreduce_bf16``:
-the same int32 sums, the result rounded to bf16, then divided by W in torch);
-anything else raises (no silent fallback to another collective).
+the same int32 sums, the result rounded to bf16).  For a power-of-two world the
+mean comes out of the dequantise stage itself (``inccl_comm_set_average``: scale
+2^-(k + log2 W)), for fp32 and bf16 alike; otherwise the hook divides by W in
+torch.  Anything else raises (no silent fallback to another collective).
 """
 from __future__ import annotations
 

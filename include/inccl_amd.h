@@ -194,11 +194,17 @@ int inccl_host_deregister(struct inccl_communicator *comm, void *ptr);
 
 /* bfloat16 buckets (uint16_t bit patterns), same arithmetic on the widened
  * values: dst = bf16_rne( (float)( sum over ranks, sum over r<R  quant(srcs[r]) ) * 2^-k ).
- * world == 1: one fused kernel, (R + 1) * 2 * n HBM bytes.  world > 1, engine
- * "rccl": quant+local sum -> reduce-scatter (int32) -> dequantise own shard to
- * bf16 -> all-gather (bf16, half the fp32 gather's bytes); every other engine:
- * quant+local sum -> that engine's int32 allreduce -> dequantise.  dst may alias
- * srcs[0]. */
+ * world == 1: one fused kernel, (R + 1) * 2 * n HBM bytes.  world > 1:
+ *   "rccl" and the in-process transport: quant+local sum -> reduce-scatter
+ *     (int32) -> dequantise own shard to bf16 -> all-gather (bf16, half the fp32
+ *     gather's bytes);
+ *   "mesh" / "meshw": the persistent kernel with bf16 sources and bf16 result
+ *     chunks;
+ *   "p2p" (4-byte aligned dst): int32 shards pulled and reduced, bf16 result
+ *     shards gathered;
+ *   "ar", "a2a", "ll": quant+local sum -> that engine's int32 allreduce ->
+ *     dequantise.
+ * dst may alias srcs[0]. */
 int inccl_allreduce_bf16(struct inccl_communicator *comm, const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev,
                          size_t n, int scale_exp, void *stream);
 /* max |x| over R bf16 buckets into *amax_bits_dev (as fp32 bits; NaN ignored). */
