@@ -4,6 +4,13 @@ quantised + reduced (+ dequantised), 256 MiB per bucket, 1/2/4/8 GPUs.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`python bench.py --gpus N` (N > 1, no WORLD_SIZE) starts its N ranks itself
+through torch.distributed.run before touching the GPU; WORLD_SIZE != --gpus is
+an error.  Whatever happens, rank 0's one JSON line gets printed: a watchdog
+timed from process start (INCCL_BENCH_BUDGET, 480 s) prints it with the stuck
+stage and exits 3, and a helper process prints it if rank 0 dies after the
+headline (LineKeeper); both carry an "error" key and leave a non-zero status.
+
 Workload (one "step"): every rank holds R = 2 resident 256 MiB fp32 buckets
 (the reference's FAN_IN = 2 children per switch, non_termination_switch.c:23)
 and produces their allreduce over all ranks into a third buffer:
@@ -20,6 +27,11 @@ Extra JSON fields:
                     N > 1: the step's xGMI link roofline; the quant+sum kernel's
                     HBM figure is roofline_hbm_kernel
   cpu_baseline      the C oracle on a bounded sample, rank 0 at N = 1 only
+  parity_vs_oracle  the timed engine's result at 2^20 strided lanes plus every
+                    shard / chunk boundary, every rank's inputs gathered to rank 0
+                    and checked bit for bit by the C oracle (also per engine
+                    candidate, sweep row and bf16 row, on smaller samples)
+  runtime           the HIP / HSA / RCCL libraries this rank mapped
   sizes             N = 1: north_star's 4/64/256/1024 MiB buckets, kernel GB/s + HBM fraction
   roofline_cold     N = 1: the fused kernel rotating through input sets far larger
                     than the 256 MiB Infinity Cache
@@ -48,8 +60,83 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TUNE_CALLS = 10         # timed calls per engine candidate (after TUNE_CALLS / 2 untimed ones)
 T_START = time.monotonic()
-# what the process is doing now; the watchdog names it when it fires
+# what the process is doing now; the watchdog and the line keeper name it
 STAGE = {"stage": "start"}
+KEEPER = [None]   # rank 0's LineKeeper
+RESULT = [None]   # the result dict once the headline is measured
+
+
+def set_stage(stage: str) -> None:
+    STAGE["stage"] = stage
+    if KEEPER[0] is not None:
+        KEEPER[0].update()
+
+
+class LineKeeper:
+    """Rank 0's guarantee that the run prints its JSON line even if rank 0
+    dies (a GPU fault, a signal) after the headline is measured.
+
+    A helper process, started before this process touches the GPU and in a
+    session of its own (so a launcher's kill of the rank's process group does
+    not reach it), blocks on a pipe from rank 0.  Rank 0 keeps a state file
+    current: the result so far, the stage it is in, and whether the line has
+    been printed.  When the pipe closes -- rank 0 exited for any reason -- the
+    helper prints nothing if the line was printed, else the result so far
+    with an "error" naming the stage rank 0 died in (or a null-valued line
+    if the headline never existed).  The exit status stays the launcher's:
+    non-zero for a rank that died."""
+
+    def __init__(self):
+        import subprocess
+        import tempfile
+        fd, self.path = tempfile.mkstemp(prefix="inccl_bench_line_", suffix=".json")
+        os.close(fd)
+        self.printed = False
+        self.update()
+        self.proc = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--line-keeper", self.path],
+                                     stdin=subprocess.PIPE, start_new_session=True)
+
+    def update(self, printed: bool = False) -> None:
+        self.printed = self.printed or printed
+        state = {"res": RESULT[0], "stage": STAGE["stage"], "printed": self.printed,
+                 "elapsed_s": round(time.monotonic() - T_START, 1)}
+        tmp = self.path + ".tmp"
+        try:
+            with open(tmp, "w") as f:
+                json.dump(state, f)
+            os.replace(tmp, self.path)
+        except (OSError, TypeError, ValueError) as e:   # never costs the run
+            print(f"bench: line keeper state not written: {e!r}", file=sys.stderr, flush=True)
+
+
+def line_keeper_main(path: str) -> None:
+    """The helper side of LineKeeper: wait for rank 0 to exit, then print its
+    line if it did not."""
+    try:
+        sys.stdin.buffer.read()   # EOF when rank 0's end of the pipe closes
+    except OSError:
+        pass
+    try:
+        with open(path) as f:
+            state = json.load(f)
+    except (OSError, ValueError):
+        state = {"res": None, "stage": "unknown (no state file)", "printed": False}
+    if not state.get("printed"):
+        msg = f"rank 0 exited without printing its line, during: {state.get('stage')}"
+        res = state.get("res")
+        if res is None:
+            res = {"metric": METRIC, "value": None, "unit": "GB/s"}
+            msg += " (before the headline was measured)"
+        else:
+            msg += "; headline measured and kept, later keys partial"
+        res["error"] = msg
+        res.setdefault("elapsed_s", state.get("elapsed_s"))
+        print(json.dumps(res), flush=True)
+    for q in (path, path + ".tmp"):
+        try:
+            os.remove(q)
+        except OSError:
+            pass
 
 
 def self_launch(a) -> int:
@@ -91,6 +178,8 @@ class Watchdog:
             self.on_fire(msg)
         elif self.rank == 0:
             print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "error": msg}), flush=True)
+            if KEEPER[0] is not None:
+                KEEPER[0].update(printed=True)
         os._exit(3)
 
     def cancel(self):
@@ -417,7 +506,7 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: 
         if only:
             engines = tuple(e for e in only.split(",") if e in engines)
         for eng in engines:
-            STAGE["stage"] = f"sweep {b} B engine {eng}"
+            set_stage(f"sweep {b} B engine {eng}")
             ok, dt, same, got = 1, float("inf"), False, None
             try:
                 comm.set_engine(eng)
@@ -485,7 +574,7 @@ def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256) -> li
     rows, refs = [], None
     lanes = oracle_lanes(n, world, 1, 1 << 16)
     for eng in ("rccl", "p2p", "mesh", "meshw"):
-        STAGE["stage"] = f"bf16 {mib} MiB engine {eng}"
+        set_stage(f"bf16 {mib} MiB engine {eng}")
         ok, dt, same = 1, float("inf"), False
         try:
             comm.set_engine(eng)
@@ -858,6 +947,8 @@ def main():
         sys.exit(f"bench: WORLD_SIZE={world} but --gpus={a.gpus}: launch with --nproc-per-node equal to --gpus, "
                  "or omit WORLD_SIZE and let bench.py start the ranks")
     watchdog = Watchdog(float(os.environ.get("INCCL_BENCH_BUDGET", "480")), rank)
+    if rank == 0:
+        KEEPER[0] = LineKeeper()   # before anything touches the GPU
 
     import torch
     import torch.distributed as dist
@@ -936,7 +1027,7 @@ def main():
         best = None
         tune_lanes = oracle_lanes(n, world, max(ch for _, ch, _ in cands), 1 << 16)
         for eng, ch, env in cands:
-            STAGE["stage"] = f"engine tuning: {eng} chunks={ch} {env or ''}"
+            set_stage(f"engine tuning: {eng} chunks={ch} {env or ''}")
             ok, dt, same, got = 1, float("inf"), False, None
             os.environ.update(env)
             try:
@@ -991,7 +1082,7 @@ def main():
     # settle: untimed steps in groups of 10 until --settle-seconds have passed (the
     # same count on every rank), so that the timed steps see steady state rather
     # than the first passes over freshly allocated buckets
-    STAGE["stage"] = f"settle/warmup/timed steps of engine {comm.engine if world > 1 else 'fused'}"
+    set_stage(f"settle/warmup/timed steps of engine {comm.engine if world > 1 else 'fused'}")
     settle_steps, t_settle = 0, time.perf_counter()
     while True:
         for _ in range(10):
@@ -1039,13 +1130,13 @@ def main():
     # the timed path's result against the oracle on a lane sample: 2^20 strided
     # lanes plus both sides of every shard / chunk boundary, every rank's inputs
     # gathered to rank 0 (one more step first: `out` then holds srcs' result)
-    STAGE["stage"] = "oracle parity check of the timed engine"
+    set_stage("oracle parity check of the timed engine")
     step()
     torch.cuda.synchronize()
     parity = oracle_check(srcs, out, oracle_lanes(n, world, chunks, 1 << 20), k, rank, world)
 
     # dominant kernel alone: fused (N=1) or quant + local sum (N>1), HIP events on its stream
-    STAGE["stage"] = "dominant-kernel timing"
+    set_stage("dominant-kernel timing")
     kstream = torch.cuda.Stream(device=dev)
     qbuf = torch.empty(n, device=dev, dtype=torch.int32) if world > 1 else None
 
@@ -1095,7 +1186,7 @@ def main():
         # the same kernel rotating through 4 input/output sets (3 GiB, far past
         # the 256 MiB Infinity Cache): `frac` re-reads the same buffers every
         # launch, `frac_cold` cannot find them on die
-        STAGE["stage"] = "cold (rotated-set) kernel timing"
+        set_stage("cold (rotated-set) kernel timing")
         cold = cold_run(dev, R, k, n)
         hbm_roofline["frac_cold"] = cold["frac"]
         hbm_roofline["achieved_cold"] = cold["achieved"]
@@ -1163,6 +1254,8 @@ def main():
         if rank == 0:
             line = json.dumps(dict(res))   # a snapshot: the watchdog may emit while the main thread works
             print(line, flush=True)
+            if KEEPER[0] is not None:
+                KEEPER[0].update(printed=True)
             if a.json_out:
                 with open(a.json_out, "w") as f:
                     f.write(line + "\n")
@@ -1173,6 +1266,11 @@ def main():
         emit()
 
     watchdog.on_fire = on_overrun
+    RESULT[0] = res
+    set_stage("headline measured")
+    if os.environ.get("INCCL_BENCH_TEST_DIE") == "1" and rank == 0:   # test hook: rank 0 dies after the headline
+        import signal
+        os.kill(os.getpid(), signal.SIGKILL)
     if world > 1 and not a.no_sweep:
         for key in chosen[2]:   # the sweep runs every engine with its defaults
             os.environ.pop(key, None)
@@ -1183,7 +1281,7 @@ def main():
         soft = float(os.environ.get("INCCL_BENCH_SWEEP_SOFT", "300"))
         res["sweep"] = []
         if os.environ.get("INCCL_BENCH_TEST_HANG") == "1" and rank == 0:   # test hook: a stuck rank 0
-            STAGE["stage"] = "INCCL_BENCH_TEST_HANG sleep on rank 0"
+            set_stage("INCCL_BENCH_TEST_HANG sleep on rank 0")
             time.sleep(1e9)
         # an exception here (the same on every rank: the keys' collectives are
         # symmetric) is recorded in the line instead of costing the headline
@@ -1204,7 +1302,7 @@ def main():
     def extra(key, fn):
         """An N = 1 extra key (one process, no collectives): a failure is recorded
         in the key instead of costing the headline line."""
-        STAGE["stage"] = f"extra key {key}"
+        set_stage(f"extra key {key}")
         try:
             res[key] = fn()
         except Exception as e:  # noqa: BLE001
@@ -1224,7 +1322,7 @@ def main():
         extra("cpu_reference_pipeline", lambda: cpu_reference_pipeline(min(a.cpu_seconds, 5.0)))
     emit()
     watchdog.cancel()
-    STAGE["stage"] = "teardown"
+    set_stage("teardown")
     comm.destroy()
     grp.destroy()
     if world > 1:
@@ -1232,4 +1330,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 3 and sys.argv[1] == "--line-keeper":
+        line_keeper_main(sys.argv[2])
+    else:
+        main()

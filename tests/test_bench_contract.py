@@ -103,3 +103,34 @@ def test_oracle_check_bf16_world1(orc):
     assert b.oracle_check(srcs, out, lanes, 25, 0, 1, bf16=True)["mismatches"] == 0
     out.view(torch.int16)[lanes[2]] ^= 1
     assert b.oracle_check(srcs, out, lanes, 25, 0, 1, bf16=True)["mismatches"] == 1
+
+
+def _keeper_run(body: str):
+    import os
+    import subprocess
+    code = ("import sys, os, signal; sys.path.insert(0, %r); import bench; bench.KEEPER[0] = bench.LineKeeper(); "
+            % ROOT) + body
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                          env=dict(os.environ))
+
+
+def test_line_keeper_prints_when_rank0_dies():
+    """Rank 0 killed (SIGKILL: no handler runs) after the headline: the keeper
+    prints the measured line with the stage it died in."""
+    import json
+    p = _keeper_run("bench.RESULT[0] = {'metric': bench.METRIC, 'value': 12.5, 'sweep': [{'bucket_bytes': 4096}]}; "
+                    "bench.set_stage('sweep 16384 B engine mesh'); os.kill(os.getpid(), signal.SIGKILL)")
+    assert p.returncode == -9
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["value"] == 12.5 and line["sweep"] == [{"bucket_bytes": 4096}]
+    assert "sweep 16384 B engine mesh" in line["error"] and "headline measured" in line["error"]
+
+
+def test_line_keeper_before_headline_and_silent_after_print():
+    import json
+    p = _keeper_run("bench.set_stage('engine tuning: mesh'); os._exit(7)")
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 7 and line["value"] is None and "engine tuning: mesh" in line["error"]
+    p = _keeper_run("bench.RESULT[0] = {'metric': bench.METRIC, 'value': 1.0}; print('{\"the\": \"line\"}', flush=True); "
+                    "bench.KEEPER[0].update(printed=True)")
+    assert p.returncode == 0 and p.stdout.strip().splitlines() == ['{"the": "line"}']
