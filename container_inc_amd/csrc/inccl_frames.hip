@@ -270,6 +270,15 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
     psn_out[f] = psn;
 }
 
+// A payload word of frame `fr` (payload at byte 54, or 70 after a RETH: 2-byte
+// aligned only), network order -> host order (nts.c:361-363's ntohl).
+__device__ __forceinline__ uint32_t payload_word(const uint8_t* fr, int i)
+{
+    const bool wf = is_write_first(fr[42]);
+    const uint16_t* d16 = reinterpret_cast<const uint16_t*>(fr + 54 + (wf ? 16 : 0));
+    return __builtin_bswap32((uint32_t)d16[2 * i] | ((uint32_t)d16[2 * i + 1] << 16));
+}
+
 __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwitchState s,
                                                                          const uint8_t* __restrict__ frames,
                                                                          int64_t stride, int64_t count,
@@ -291,12 +300,16 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwi
     // 0 = before the batch, ~0 = not by the end of the batch
     uint32_t at = 0;
     uint32_t mine = 0xFFFFFFFFu;                                // frame index of my pair's first copy
+    bool counted = false;                                       // port p's counted arrival is in this batch
     if (lane < s.fan_in) {
         const uint64_t e = s.first[(size_t)slot * s.fan_in + lane];
         const bool in_batch = (uint32_t)(e >> 32) == tag;
         at = (pre & (1u << lane)) ? 0u : (in_batch ? (uint32_t)e + 1u : 0xFFFFFFFFu);
         mine = in_batch ? (uint32_t)e : 0xFFFFFFFFu;
+        counted = in_batch && !(pre & (1u << lane));
     }
+    const uint64_t counted_ports = __ballot(counted);
+    const uint32_t first_of = mine;                             // lane p: frame of port p's counted arrival
     mine = (uint32_t)__shfl((int)mine, port, kWave);
     uint32_t done_at = at;                                      // max over ports: the completing arrival
 #pragma unroll
@@ -307,23 +320,32 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwi
     done_at = (uint32_t)__shfl((int)done_at, 0, kWave);
     int act;
     if (!(pre & bit) && mine == (uint32_t)f) {                  // the counted arrival: nts.c:359-363
-        const bool wf = is_write_first(fr[42]);
-        const uint8_t* data = fr + 54 + (wf ? 16 : 0);
-        // the payload starts at byte 54 (70 with RETH): 2-byte aligned only
-        const uint16_t* d16 = reinterpret_cast<const uint16_t*>(data);
-        if (wf && lane < 4) {                                    // reth_keeper, nts.c:442
+        if (is_write_first(fr[42]) && lane < 4) {                // reth_keeper, nts.c:442
             const uint16_t* r = reinterpret_cast<const uint16_t*>(fr + 54);
             s.reth[((size_t)slot * s.fan_in + port) * 4 + lane] =
                 (uint32_t)r[2 * lane] | ((uint32_t)r[2 * lane + 1] << 16);
         }
-        int32_t* agg = s.agg + (size_t)slot * kLanes;
-        // word i = j*64 + lane: each wave-instruction adds 256 contiguous
-        // bytes (the full-rate atomic shape, MI355X_MICROARCH.md atomics)
+        // The slot's counted arrivals of this batch are summed by ONE wave --
+        // the one of the lowest counted port -- into the slot's partial from
+        // earlier batches, with plain loads and stores: the same wrap-around
+        // sum as one atomic add per arrival (nts.c:361-363 / :443-445, integer
+        // addition commutes), without the atomics.  The other counted arrivals
+        // of the slot only classify themselves.
+        if (port == __builtin_ctzll(counted_ports)) {
+            int32_t* agg = s.agg + (size_t)slot * kLanes;
+            uint32_t acc[4];
+            // word i = j*64 + lane: each wave-instruction covers 256 contiguous bytes
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {                            // nts.c:361-363 / :443-445
-            const int i = j * kWave + lane;
-            const uint32_t raw = (uint32_t)d16[2 * i] | ((uint32_t)d16[2 * i + 1] << 16);
-            atomicAdd(&agg[i], (int32_t)__builtin_bswap32(raw));
+            for (int j = 0; j < 4; ++j) acc[j] = (uint32_t)agg[j * kWave + lane];
+            for (uint64_t m = counted_ports; m; m &= m - 1) {
+                const int q = __builtin_ctzll(m);
+                const uint32_t fq = (uint32_t)__shfl((int)first_of, q, kWave);
+                const uint8_t* frq = frames + (int64_t)fq * stride;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] += payload_word(frq, j * kWave + lane);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) agg[j * kWave + lane] = (int32_t)acc[j];
         }
         act = (done_at == (uint32_t)f + 1u) ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
     } else {                                                     // retransmit: nts.c:353-357
@@ -529,12 +551,20 @@ __device__ void header_crcs(EgressLds& t, const uint8_t (*himg)[kHdrImg], int fa
 
 // Every output frame of input frame f (rows f * fan_in + c): all fan_in children
 // on COMPLETED (the broadcast, nts.c:368-371), the sender's child on REPLAY
-// (nts.c:353-356).  The payload (htonl of the aggregate, util.c:403-405 /
-// :419-421) is written into the LDS frame once and shared by the children; each
-// child rewrites only its header words and ICRC, all lanes at once.
+// (nts.c:353-356).
+//
+// The payload (htonl of the aggregate, util.c:403-405 / :419-421) goes from
+// registers straight to the output rows.  Lane l holds payload bytes
+// [16 l, 16 l + 16), i.e. frame bytes doff + 16 l ..; doff (54, or 70 with a
+// RETH) is 6 mod 16, so 16-byte output chunk doff/16 + 1 + l is lane l's bytes
+// 10..15 followed by lane l+1's bytes 0..9: one funnel shift with the next
+// lane's words, built once per input frame and stored once per child.  The
+// chunks before it (the header, with the payload's first 10 bytes) are staged
+// in a 80-byte LDS buffer per wave; lane 63 stores the last chunk: payload
+// bytes 1018-1023 and the ICRC.  No per-child pass over the payload touches LDS.
 __device__ void egress_emit(const InccSwitchState& s, const EgressIn& e, const uint8_t (*himg)[kHdrImg],
                             uint8_t* __restrict__ out, int64_t out_stride, bool out16, int32_t* __restrict__ out_len,
-                            const EgressLds& t, uint8_t* frbuf, int64_t f, int lane)
+                            const EgressLds& t, uint8_t* hbuf, int64_t f, int lane)
 {
     const int fan = s.fan_in;
     const bool all = e.act == INCCL_SW_COMPLETED;
@@ -542,23 +572,29 @@ __device__ void egress_emit(const InccSwitchState& s, const EgressIn& e, const u
     const uint32_t op = (uint32_t)__shfl((int)e.op, 2, kWave) & 0xFFu;
     const int wf = is_write_first((uint8_t)op) ? 1 : 0;
     const int doff = 54 + 16 * wf;
+    const int hchunks = doff / 16 + 1;         // 4 (or 5) chunks: header + payload bytes 0-9
     const int total = doff + kLanes * 4 + 4;   // util.c:341-345
     if (lane < fan) out_len[f * fan + lane] = (all || (one && lane == e.port)) ? total : 0;
     if (!all && !one) return;
-    uint8_t* fr = frbuf;
     // this lane's 16 payload bytes (big-endian words, util.c:403-405), memory order
     uint32_t a[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) a[k] = __builtin_bswap32((uint32_t)e.agg[k]);
-    // payload into the LDS frame at doff + 16 lane (doff = 2 mod 4): a 16-bit
-    // store, three aligned dwords, a 16-bit store
+    uint32_t nx[3];                            // lane l+1's first 12 bytes
+#pragma unroll
+    for (int k = 0; k < 3; ++k) nx[k] = (uint32_t)__shfl_down((int)a[k], 1, kWave);
+    // output chunk hchunks + lane (lanes 0-62): bytes 10-15 of mine, 0-9 of the next lane's
+    const uint32_t pc0 = __builtin_amdgcn_alignbyte(a[3], a[2], 2);
+    const uint32_t pc1 = __builtin_amdgcn_alignbyte(nx[0], a[3], 2);
+    const uint32_t pc2 = __builtin_amdgcn_alignbyte(nx[1], nx[0], 2);
+    const uint32_t pc3 = __builtin_amdgcn_alignbyte(nx[2], nx[1], 2);
+    // the payload's first 10 bytes into the header buffer (doff = 2 mod 4), once
     {
-        uint8_t* p = fr + doff + 16 * lane;
-        *reinterpret_cast<uint16_t*>(p) = (uint16_t)a[0];
-        *reinterpret_cast<uint32_t*>(p + 2) = __builtin_amdgcn_alignbyte(a[1], a[0], 2);
-        *reinterpret_cast<uint32_t*>(p + 6) = __builtin_amdgcn_alignbyte(a[2], a[1], 2);
-        *reinterpret_cast<uint32_t*>(p + 10) = __builtin_amdgcn_alignbyte(a[3], a[2], 2);
-        *reinterpret_cast<uint16_t*>(p + 14) = (uint16_t)(a[3] >> 16);
+        const uint32_t a0 = (uint32_t)__shfl((int)a[0], 0, kWave), a1 = (uint32_t)__shfl((int)a[1], 0, kWave);
+        const uint32_t a2 = (uint32_t)__shfl((int)a[2], 0, kWave);
+        if (lane == 0) *reinterpret_cast<uint16_t*>(hbuf + doff) = (uint16_t)a0;
+        if (lane == 1) *reinterpret_cast<uint32_t*>(hbuf + doff + 2) = __builtin_amdgcn_alignbyte(a1, a0, 2);
+        if (lane == 2) *reinterpret_cast<uint32_t*>(hbuf + doff + 6) = __builtin_amdgcn_alignbyte(a2, a1, 2);
     }
     // P ^ V_op,psn: the payload's contribution (this lane's segment) and, on
     // lanes 0-4, the opcode and the four PSN bytes (util.c:378, :386)
@@ -589,38 +625,39 @@ __device__ void egress_emit(const InccSwitchState& s, const EgressIn& e, const u
             uint32_t hw = reinterpret_cast<const uint32_t*>(himg[2 * c + wf])[lane];
             if (lane == 10) hw = (hw & 0xFF00FFFFu) | (op << 16);                            // byte 42
             if (lane == 12) hw = (hw & 0x0000FFFFu) | ((pw >> 24) << 16) | (((pw >> 16) & 0xFFu) << 24);   // 50-51
-            reinterpret_cast<uint32_t*>(fr)[lane] = hw;
+            reinterpret_cast<uint32_t*>(hbuf)[lane] = hw;
         } else if (lane == 13) {                                                               // 52-53
-            *reinterpret_cast<uint16_t*>(fr + 52) = (uint16_t)(((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8));
+            *reinterpret_cast<uint16_t*>(hbuf + 52) = (uint16_t)(((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8));
         }
         if (wf) {                                                   // util.c:409-417: bytes 54-69
             const int k = lane - 14;                                // lanes 14..18
             const uint32_t rlo = (uint32_t)__shfl((int)r, (k - 1) & 3, kWave);
             const uint32_t rhi = (uint32_t)__shfl((int)r, k & 3, kWave);
-            if (k == 0) *reinterpret_cast<uint16_t*>(fr + 54) = (uint16_t)rhi;
-            else if (k >= 1 && k <= 3) *reinterpret_cast<uint32_t*>(fr + 52 + 4 * k) = __builtin_amdgcn_alignbyte(rhi, rlo, 2);
-            else if (k == 4) *reinterpret_cast<uint16_t*>(fr + 68) = (uint16_t)(rlo >> 16);
+            if (k == 0) *reinterpret_cast<uint16_t*>(hbuf + 54) = (uint16_t)rhi;
+            else if (k >= 1 && k <= 3) *reinterpret_cast<uint32_t*>(hbuf + 52 + 4 * k) = __builtin_amdgcn_alignbyte(rhi, rlo, 2);
+            else if (k == 4) *reinterpret_cast<uint16_t*>(hbuf + 68) = (uint16_t)(rlo >> 16);
         }
-        if (lane == 0) *reinterpret_cast<uint16_t*>(fr + total - 4) = (uint16_t)crc;           // stored host order (LE)
-        if (lane == 1) *reinterpret_cast<uint16_t*>(fr + total - 2) = (uint16_t)(crc >> 16);
         __builtin_amdgcn_wave_barrier();
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
         uint8_t* o = out + (f * fan + c) * out_stride;
-        // fixed trip counts (total <= 1098 B): the compiler can then count this
-        // wave's outstanding stores, and the next frame's prefetched loads are
-        // not held behind them by a conservative vmcnt(0)
-        if (out16) {
-            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-            for (int k = 0; k < (kFrameMax / 16 + kWave - 1) / kWave; ++k) {
-                const int i = lane + k * kWave;
-                if (i < (total + 15) / 16) reinterpret_cast<u4*>(o)[i] = reinterpret_cast<const u4*>(fr)[i];
+        // header chunks (lanes 0 .. hchunks-1) from LDS
+        if (lane < hchunks) {
+            const u4 h = reinterpret_cast<const u4*>(hbuf)[lane];
+            if (out16) reinterpret_cast<u4*>(o)[lane] = h;
+            else {
+                uint32_t* o32 = reinterpret_cast<uint32_t*>(o) + 4 * lane;
+                o32[0] = h.x; o32[1] = h.y; o32[2] = h.z; o32[3] = h.w;
             }
-        } else {
-#pragma unroll
-            for (int k = 0; k < (kFrameMax / 4 + kWave - 1) / kWave; ++k) {
-                const int i = lane + k * kWave;
-                if (i < (total + 3) / 4) reinterpret_cast<uint32_t*>(o)[i] = reinterpret_cast<const uint32_t*>(fr)[i];
-            }
+        }
+        // payload chunks (lanes 0-62) and the last chunk (lane 63: payload bytes
+        // 1018-1023, the ICRC stored host order (LE), two bytes of zero padding)
+        const u4 v = lane < kWave - 1 ? u4{pc0, pc1, pc2, pc3}
+                                      : u4{pc0, (a[3] >> 16) | ((crc & 0xFFFFu) << 16), crc >> 16, 0u};
+        if (out16) reinterpret_cast<u4*>(o)[hchunks + lane] = v;
+        else {
+            uint32_t* o32 = reinterpret_cast<uint32_t*>(o) + 4 * (hchunks + lane);
+            o32[0] = v.x; o32[1] = v.y; o32[2] = v.z;
+            if (lane < kWave - 1) o32[3] = v.w;   // lane 63: stop at the frame's 4-byte-rounded end
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -640,7 +677,7 @@ __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState 
                                                                int32_t* __restrict__ out_len)
 {
     __shared__ EgressLds t;
-    __shared__ __attribute__((aligned(16))) uint8_t buf[kEgressWaves][kFrameMax];
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kEgressWaves][80];   // per wave: header chunks
     __shared__ __attribute__((aligned(16))) uint8_t himg[2 * 31][kHdrImg];
     for (int i = threadIdx.x; i < kSeg * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg[0][0][0])[i];
     for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) (&t.lane16[0][0][0])[i] = (&g_lane16[0][0][0])[i];
@@ -789,9 +826,10 @@ int num_cus()
     return cus;
 }
 
-// persistent blocks per CU (43-48 KiB of LDS each, so up to three fit).  The
-// ICRC kernel is fastest at three (65.9 vs 78.4 us per 131 072 frames at two),
-// egress at two (189 us at three: its stores and prefetches contend).
+// persistent blocks per CU (43-46 KiB of LDS each, so up to three fit).  The
+// ICRC kernel is fastest at three (65.9 vs 78.4 us per 131 072 frames at two).
+// Egress was fastest at two while it staged every output frame in LDS (189 us
+// at three); with the payload stored from registers it takes three.
 // INCCL_ICRC_BLOCKS_PER_CU / INCCL_EGRESS_BLOCKS_PER_CU override for sweeps.
 int blocks_per_cu(const char* env, int dflt)
 {
@@ -858,7 +896,7 @@ int inccl_k_switch_egress(const InccSwitchState* s, const uint8_t* in_frames, si
     hipStream_t st = (hipStream_t)stream;
     // persistent grid: the CRC tables are loaded once per block
     const int64_t need = ((int64_t)count + kEgressWaves - 1) / kEgressWaves;
-    const int64_t cap = (int64_t)num_cus() * blocks_per_cu("INCCL_EGRESS_BLOCKS_PER_CU", 2);
+    const int64_t cap = (int64_t)num_cus() * blocks_per_cu("INCCL_EGRESS_BLOCKS_PER_CU", 3);
     const int eg = (int)(need < cap ? (need < 1 ? 1 : need) : cap);
     hipLaunchKernelGGL(k_egress, dim3(eg), dim3(kWave * kEgressWaves), 0, st, *s,
                        in_frames, (int64_t)in_stride, (int64_t)count, ports, action, psns, tmpl, out,
