@@ -232,9 +232,13 @@ __device__ __forceinline__ bool is_write_first(uint8_t op) { return op == 0x06 |
 constexpr int kActPending = 100;   // claim -> apply: a data frame still to classify
 constexpr int kClaimBlock = 256;
 
-__device__ __forceinline__ uint64_t first_key(uint32_t gen, int64_t f)
+// (~gen << 32) | (frame << 1) | wf: the minimum over a (slot, port)'s keys is the
+// newest batch's earliest copy (the frame index dominates bit 0), and bit 0 tells
+// apply where that copy's payload starts (byte 54, or 70 after a RETH) without
+// another dependent load.  Frame indices stay below 2^31.
+__device__ __forceinline__ uint64_t first_key(uint32_t gen, int64_t f, bool wf)
 {
-    return ((uint64_t)(~gen) << 32) | (uint64_t)(uint32_t)f;
+    return ((uint64_t)(~gen) << 32) | ((uint64_t)(uint32_t)f << 1) | (wf ? 1u : 0u);
 }
 
 __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s, const uint8_t* __restrict__ frames,
@@ -262,7 +266,7 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
             const uint32_t slot = psn & (s.slots - 1);
             atomicAdd(&s.degree[slot], 1);                       // nts.c:351 / :431
             atomicMin(reinterpret_cast<unsigned long long*>(&s.first[(size_t)slot * s.fan_in + port]),
-                      (unsigned long long)first_key(s.gen, f));
+                      (unsigned long long)first_key(s.gen, f, wf));
             act = kActPending;
         }
     }
@@ -270,12 +274,19 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
     psn_out[f] = psn;
 }
 
-// A payload word of frame `fr` (payload at byte 54, or 70 after a RETH: 2-byte
-// aligned only), network order -> host order (nts.c:361-363's ntohl).
-__device__ __forceinline__ uint32_t payload_word(const uint8_t* fr, int i)
+// Apply, several frames per wave.  A one-frame wave is a chain of dependent
+// round trips (its metadata -> its slot's bitmap and first copies -> the
+// payloads -> the stores), and with 131 072 short waves that latency, not HBM,
+// set the pass's time (102 us).  A wave now takes kApplyFrames consecutive
+// frames and runs each stage for all of them before the next, so every round
+// trip carries kApplyFrames frames' loads.
+constexpr int kApplyFrames = 4;
+
+// payload word i (i = j*64 + lane) of the frame at `fr`, its payload at byte
+// 54 + 16*wf (2-byte aligned), network order -> host order (nts.c:361-363)
+__device__ __forceinline__ uint32_t payload_word(const uint8_t* fr, uint32_t wf, int i)
 {
-    const bool wf = is_write_first(fr[42]);
-    const uint16_t* d16 = reinterpret_cast<const uint16_t*>(fr + 54 + (wf ? 16 : 0));
+    const uint16_t* d16 = reinterpret_cast<const uint16_t*>(fr + 54 + 16 * wf);
     return __builtin_bswap32((uint32_t)d16[2 * i] | ((uint32_t)d16[2 * i + 1] << 16));
 }
 
@@ -287,73 +298,146 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwi
                                                                          const uint32_t* __restrict__ psns)
 {
     const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    const int64_t f = (int64_t)blockIdx.x * kWavesPerBlock + w;
-    if (f >= count || action[f] != kActPending) return;
-    const uint8_t* fr = frames + f * stride;
-    const int port = ports[f];
-    const uint32_t psn = psns[f];
-    const uint32_t slot = psn & (s.slots - 1);
-    const uint32_t bit = 1u << port, result_bit = 1u << s.fan_in;
-    const uint32_t pre = s.arrival[slot];                       // the slot before this batch
-    const uint32_t tag = ~s.gen;
-    // lane p < fan_in: when port p's counted arrival happens, as 1 + frame index;
-    // 0 = before the batch, ~0 = not by the end of the batch
-    uint32_t at = 0;
-    uint32_t mine = 0xFFFFFFFFu;                                // frame index of my pair's first copy
-    bool counted = false;                                       // port p's counted arrival is in this batch
-    if (lane < s.fan_in) {
-        const uint64_t e = s.first[(size_t)slot * s.fan_in + lane];
-        const bool in_batch = (uint32_t)(e >> 32) == tag;
-        at = (pre & (1u << lane)) ? 0u : (in_batch ? (uint32_t)e + 1u : 0xFFFFFFFFu);
-        mine = in_batch ? (uint32_t)e : 0xFFFFFFFFu;
-        counted = in_batch && !(pre & (1u << lane));
-    }
-    const uint64_t counted_ports = __ballot(counted);
-    const uint32_t first_of = mine;                             // lane p: frame of port p's counted arrival
-    mine = (uint32_t)__shfl((int)mine, port, kWave);
-    uint32_t done_at = at;                                      // max over ports: the completing arrival
+    const int64_t f0 = ((int64_t)blockIdx.x * kWavesPerBlock + w) * kApplyFrames;
+    if (f0 >= count) return;
+    const int fan = s.fan_in;
+    const uint32_t tag = ~s.gen, result_bit = 1u << fan;
+    // stage A: each frame's action, port and PSN
+    int act[kApplyFrames], port[kApplyFrames];
+    uint32_t psn[kApplyFrames];
 #pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) {
-        const uint32_t v = (uint32_t)__shfl_xor((int)done_at, o, kWave);
-        done_at = v > done_at ? v : done_at;
+    for (int k = 0; k < kApplyFrames; ++k) {
+        const bool in = f0 + k < count;
+        act[k] = in ? action[f0 + k] : 0;
+        port[k] = in ? ports[f0 + k] : 0;
+        psn[k] = in ? psns[f0 + k] : 0;
     }
-    done_at = (uint32_t)__shfl((int)done_at, 0, kWave);
-    int act;
-    if (!(pre & bit) && mine == (uint32_t)f) {                  // the counted arrival: nts.c:359-363
-        if (is_write_first(fr[42]) && lane < 4) {                // reth_keeper, nts.c:442
-            const uint16_t* r = reinterpret_cast<const uint16_t*>(fr + 54);
-            s.reth[((size_t)slot * s.fan_in + port) * 4 + lane] =
-                (uint32_t)r[2 * lane] | ((uint32_t)r[2 * lane + 1] << 16);
+    // stage B: the slot as it was before the batch, and lane p < fan_in: the
+    // first-copy key of port p
+    uint32_t pre[kApplyFrames];
+    uint64_t key[kApplyFrames];
+#pragma unroll
+    for (int k = 0; k < kApplyFrames; ++k) {
+        const bool live = act[k] == kActPending;
+        const uint32_t slot = psn[k] & (s.slots - 1);
+        pre[k] = live ? s.arrival[slot] : 0u;
+        key[k] = live && lane < fan ? s.first[(size_t)slot * fan + lane] : 0ull;
+    }
+    // stage C: classify (nts.c:353-372) and find the slot leaders
+    int out_act[kApplyFrames];
+    bool lead[kApplyFrames];
+    uint64_t counted_ports[kApplyFrames];
+    uint32_t first_of[kApplyFrames], done_at[kApplyFrames];
+#pragma unroll
+    for (int k = 0; k < kApplyFrames; ++k) {
+        const int64_t f = f0 + k;
+        const bool live = act[k] == kActPending;
+        const uint32_t bit = 1u << port[k];
+        // lane p < fan_in: when port p's counted arrival happens, as 1 + frame
+        // index; 0 = before the batch, ~0 = not by the end of the batch
+        uint32_t at = 0, mine = 0xFFFFFFFFu, fo = 0xFFFFFFFFu;
+        bool counted = false;
+        if (lane < fan) {
+            const uint64_t e = key[k];
+            const bool in_batch = (uint32_t)(e >> 32) == tag;
+            const uint32_t ef = ((uint32_t)e) >> 1;
+            at = (pre[k] & (1u << lane)) ? 0u : (in_batch ? ef + 1u : 0xFFFFFFFFu);
+            mine = in_batch ? ef : 0xFFFFFFFFu;
+            fo = (uint32_t)e;                                   // frame << 1 | wf
+            counted = in_batch && !(pre[k] & (1u << lane));
+        }
+        counted_ports[k] = __ballot(counted);
+        first_of[k] = fo;
+        mine = (uint32_t)__shfl((int)mine, port[k] & (kWave - 1), kWave);
+        uint32_t d = at;                                        // max over ports: the completing arrival
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) {
+            const uint32_t v = (uint32_t)__shfl_xor((int)d, o, kWave);
+            d = v > d ? v : d;
+        }
+        done_at[k] = d = (uint32_t)__shfl((int)d, 0, kWave);
+        const bool arrival = live && !(pre[k] & bit) && mine == (uint32_t)f;   // the counted arrival: nts.c:359-363
+        if (arrival) {
+            out_act[k] = (d == (uint32_t)f + 1u) ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
+        } else {                                                 // retransmit: nts.c:353-357
+            const bool done_before = (pre[k] & result_bit) != 0;
+            const bool done_earlier = d != 0u && d != 0xFFFFFFFFu && d - 1u < (uint32_t)f;
+            out_act[k] = (done_before || done_earlier) ? INCCL_SW_REPLAY : INCCL_SW_DROPPED;
         }
         // The slot's counted arrivals of this batch are summed by ONE wave --
-        // the one of the lowest counted port -- into the slot's partial from
-        // earlier batches, with plain loads and stores: the same wrap-around
-        // sum as one atomic add per arrival (nts.c:361-363 / :443-445, integer
-        // addition commutes), without the atomics.  The other counted arrivals
-        // of the slot only classify themselves.
-        if (port == __builtin_ctzll(counted_ports)) {
-            int32_t* agg = s.agg + (size_t)slot * kLanes;
-            uint32_t acc[4];
-            // word i = j*64 + lane: each wave-instruction covers 256 contiguous bytes
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[j] = (uint32_t)agg[j * kWave + lane];
-            for (uint64_t m = counted_ports; m; m &= m - 1) {
-                const int q = __builtin_ctzll(m);
-                const uint32_t fq = (uint32_t)__shfl((int)first_of, q, kWave);
-                const uint8_t* frq = frames + (int64_t)fq * stride;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] += payload_word(frq, j * kWave + lane);
+        // the one holding the lowest counted port's frame -- into the slot's
+        // partial from earlier batches, with plain loads and stores: the same
+        // wrap-around sum as one atomic add per arrival (nts.c:361-363 /
+        // :443-445; integer addition commutes), without the atomics.
+        lead[k] = arrival && port[k] == __builtin_ctzll(counted_ports[k]);
+        if (arrival && lane < 4) {                               // reth_keeper, nts.c:442
+            const uint32_t wf = (uint32_t)__shfl((int)fo, port[k] & (kWave - 1), kWave) & 1u;
+            if (wf) {
+                const uint16_t* r = reinterpret_cast<const uint16_t*>(frames + f * stride + 54);
+                s.reth[((size_t)(psn[k] & (s.slots - 1)) * fan + port[k]) * 4 + lane] =
+                    (uint32_t)r[2 * lane] | ((uint32_t)r[2 * lane + 1] << 16);
             }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) agg[j * kWave + lane] = (int32_t)acc[j];
         }
-        act = (done_at == (uint32_t)f + 1u) ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
-    } else {                                                     // retransmit: nts.c:353-357
-        const bool done_before = (pre & result_bit) != 0;
-        const bool done_earlier = done_at != 0u && done_at != 0xFFFFFFFFu && done_at - 1u < (uint32_t)f;
-        act = (done_before || done_earlier) ? INCCL_SW_REPLAY : INCCL_SW_DROPPED;
     }
-    if (lane == 0) action[f] = act;
+    // stage D: the leaders' sums.  Every leader's slot partial and its two lowest
+    // counted ports' payloads are loaded before any is added (fan-in 2 needs no
+    // more); further ports, if any, follow.  Word i = j*64 + lane: each wave
+    // instruction covers 256 contiguous bytes.
+    uint32_t acc[kApplyFrames][4], p0[kApplyFrames][4], p1[kApplyFrames][4];
+#pragma unroll
+    for (int k = 0; k < kApplyFrames; ++k) {
+        if (!lead[k]) continue;
+        const int32_t* agg = s.agg + (size_t)(psn[k] & (s.slots - 1)) * kLanes;
+        uint64_t m = counted_ports[k];
+        const int q0 = __builtin_ctzll(m);
+        m &= m - 1;
+        const uint32_t e0 = (uint32_t)__shfl((int)first_of[k], q0, kWave);
+        const uint8_t* fr0 = frames + (int64_t)(e0 >> 1) * stride;
+        const int q1 = m ? __builtin_ctzll(m) : q0;
+        const uint32_t e1 = (uint32_t)__shfl((int)first_of[k], q1, kWave);
+        const uint8_t* fr1 = frames + (int64_t)(e1 >> 1) * stride;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            acc[k][j] = (uint32_t)agg[j * kWave + lane];
+            p0[k][j] = payload_word(fr0, e0 & 1u, j * kWave + lane);
+            p1[k][j] = m ? payload_word(fr1, e1 & 1u, j * kWave + lane) : 0u;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kApplyFrames; ++k) {
+        if (!lead[k]) continue;
+        const uint32_t slot = psn[k] & (s.slots - 1);
+        int32_t* agg = s.agg + (size_t)slot * kLanes;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[k][j] += p0[k][j] + p1[k][j];
+        uint64_t m = counted_ports[k];
+        m &= m - 1;
+        m &= m - 1;
+        for (; m; m &= m - 1) {                                  // ports beyond the first two
+            const uint32_t e = (uint32_t)__shfl((int)first_of[k], __builtin_ctzll(m), kWave);
+            const uint8_t* frq = frames + (int64_t)(e >> 1) * stride;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[k][j] += payload_word(frq, e & 1u, j * kWave + lane);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) agg[j * kWave + lane] = (int32_t)acc[k][j];
+        // clear_state_data(psn + WINDOW) when the PSN completes in this batch
+        // (nts.c:235-242, :367): slot psn + slots/2, which no frame of the batch
+        // touches (a batch's PSNs are less than slots/2 apart)
+        if (done_at[k] != 0xFFFFFFFFu) {
+            const uint32_t rs = (psn[k] + (s.slots >> 1)) & (s.slots - 1);
+            typedef int32_t i4 __attribute__((ext_vector_type(4)));
+            reinterpret_cast<i4*>(s.agg + (size_t)rs * kLanes)[lane] = i4{0, 0, 0, 0};
+            for (int i = lane; i < fan * 4; i += kWave) s.reth[(size_t)rs * fan * 4 + i] = 0;
+            if (lane == 0) {
+                s.arrival[rs] = 0;
+                s.degree[rs] = 0;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kApplyFrames; ++k)
+        if (lane == 0 && act[k] == kActPending && f0 + k < count) action[f0 + k] = out_act[k];
 }
 
 __global__ __launch_bounds__(kClaimBlock) void k_ingress_commit(InccSwitchState s, int64_t count,
@@ -722,24 +806,6 @@ __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState 
     }
 }
 
-// clear_state_data(psn + WINDOW) for every slot completed in the batch (nts.c:235-242, :367)
-__global__ __launch_bounds__(kWave* kWavesPerBlock) void k_recycle(InccSwitchState s, int64_t count,
-                                                                  const int32_t* __restrict__ action,
-                                                                  const uint32_t* __restrict__ psns)
-{
-    const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    const int64_t f = (int64_t)blockIdx.x * kWavesPerBlock + w;
-    if (f >= count || action[f] != INCCL_SW_COMPLETED) return;
-    const uint32_t slot = (psns[f] + (s.slots >> 1)) & (s.slots - 1);
-    typedef int32_t i4 __attribute__((ext_vector_type(4)));
-    reinterpret_cast<i4*>(s.agg + (size_t)slot * kLanes)[lane] = i4{0, 0, 0, 0};   // 64 lanes x 16 B = one slot
-    for (int i = lane; i < s.fan_in * 4; i += kWave) s.reth[(size_t)slot * s.fan_in * 4 + i] = 0;
-    if (lane == 0) {
-        s.arrival[slot] = 0;
-        s.degree[slot] = 0;
-    }
-}
-
 // ---------------------------------------------------------------------------
 // host: CRC tables (util.c:141-159) and the zero-append operators per tree level
 // ---------------------------------------------------------------------------
@@ -870,13 +936,14 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
 {
     if (count == 0) return 0;
     if (!s || !frames || !ports || !action || !psn_out || (stride & 3) || stride < INCCL_FRAME_MIN_STRIDE ||
-        ((uintptr_t)frames & 3) || count >= 0xFFFFFFFFull)
+        ((uintptr_t)frames & 3) || count >= 0x7FFFFFFFull)
         return INCCL_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     const dim3 lanes((unsigned)(((int64_t)count + kClaimBlock - 1) / kClaimBlock));
     hipLaunchKernelGGL(k_ingress_claim, lanes, dim3(kClaimBlock), 0, st, *s, frames, (int64_t)stride, (int64_t)count,
                        ports, action, psn_out);
-    hipLaunchKernelGGL(k_ingress_apply, dim3(grid_for((int64_t)count)), dim3(kWave * kWavesPerBlock), 0, st, *s,
+    hipLaunchKernelGGL(k_ingress_apply, dim3(grid_for(((int64_t)count + kApplyFrames - 1) / kApplyFrames)),
+                       dim3(kWave * kWavesPerBlock), 0, st, *s,
                        frames, (int64_t)stride, (int64_t)count, ports, action, psn_out);
     hipLaunchKernelGGL(k_ingress_commit, lanes, dim3(kClaimBlock), 0, st, *s, (int64_t)count, ports, action, psn_out);
     return (int)hipGetLastError();
@@ -901,8 +968,6 @@ int inccl_k_switch_egress(const InccSwitchState* s, const uint8_t* in_frames, si
     hipLaunchKernelGGL(k_egress, dim3(eg), dim3(kWave * kEgressWaves), 0, st, *s,
                        in_frames, (int64_t)in_stride, (int64_t)count, ports, action, psns, tmpl, out,
                        (int64_t)out_stride, out_len);
-    hipLaunchKernelGGL(k_recycle, dim3(grid_for((int64_t)count)), dim3(kWave * kWavesPerBlock), 0, st, *s,
-                       (int64_t)count, action, psns);
     return (int)hipGetLastError();
 }
 

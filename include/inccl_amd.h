@@ -251,13 +251,15 @@ int inccl_switch_destroy(struct inccl_switch *sw);
 int inccl_switch_reset(struct inccl_switch *sw, void *stream);
 /* device pointer of the 256-lane aggregator slot of `psn` */
 const int32_t *inccl_switch_slot(struct inccl_switch *sw, uint32_t psn);
-/* ports_dev[i] = ingress port of frame i.  Writes action_dev[i] (INCCL_SW_*) and psn_dev[i]. */
+/* ports_dev[i] = ingress port of frame i.  Writes action_dev[i] (INCCL_SW_*) and psn_dev[i], and
+ * recycles slot psn + slots/2 of every psn the batch completes (clear_state_data(psn + WINDOW),
+ * nts.c:367, which the reference runs at completion, in its ingress pipeline). */
 int inccl_switch_ingress(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
                          const int32_t *ports_dev, int32_t *action_dev, uint32_t *psn_dev, void *stream);
 /* For every COMPLETED frame i: fan_in egress frames to children c at
  * out_dev[(i*fan_in + c) * out_stride]; for every REPLAY frame: one frame to
- * its port.  out_len_dev[i*fan_in + c] = frame bytes or 0.  Then recycles
- * slot psn + slots/2 of every completed psn (nts.c:367).  templates_dev holds
+ * its port.  out_len_dev[i*fan_in + c] = frame bytes or 0 (bytes past a frame, up to its 16-byte
+ * rounded length, are written as zero or left as they were).  templates_dev holds
  * fan_in inccl_frame_template records (device memory). */
 int inccl_switch_egress(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
                         const int32_t *ports_dev, const int32_t *action_dev, const uint32_t *psn_dev,

@@ -102,7 +102,7 @@ def main():
     torch.cuda.synchronize()
     assert (a.cpu().numpy() == inccl.SW_COMPLETED).sum() == P
     payload_bytes = fan_in * P * 1024
-    print(json.dumps({"what": "GPU switch dataplane batch (ingress claim/apply/commit + egress + recycle; no reset)", "fan_in": fan_in,
+    print(json.dumps({"what": "GPU switch dataplane batch (ingress claim/apply+recycle/commit + egress; no reset)", "fan_in": fan_in,
                       "psns": P, "ingress_frames": fan_in * P, "egress_frames": fan_in * P, "ms": round(ms, 4),
                       "payload_GBs": round(payload_bytes / (ms * 1e-3) / 1e9, 2),
                       "frames_per_s": round(2 * fan_in * P / (ms * 1e-3), 1)}), flush=True)
