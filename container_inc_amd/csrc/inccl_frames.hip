@@ -370,8 +370,10 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwi
         // wrap-around sum as one atomic add per arrival (nts.c:361-363 /
         // :443-445; integer addition commutes), without the atomics.
         lead[k] = arrival && port[k] == __builtin_ctzll(counted_ports[k]);
+        // (the shuffle runs on every lane: a bpermute from a lane that is
+        // inactive in a divergent branch does not return that lane's value)
+        const uint32_t wf = (uint32_t)__shfl((int)fo, port[k] & (kWave - 1), kWave) & 1u;
         if (arrival && lane < 4) {                               // reth_keeper, nts.c:442
-            const uint32_t wf = (uint32_t)__shfl((int)fo, port[k] & (kWave - 1), kWave) & 1u;
             if (wf) {
                 const uint16_t* r = reinterpret_cast<const uint16_t*>(frames + f * stride + 54);
                 s.reth[((size_t)(psn[k] & (s.slots - 1)) * fan + port[k]) * 4 + lane] =
