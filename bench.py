@@ -815,21 +815,26 @@ def api_allreduce_write(comm, mib: int = 256, calls: int = 7) -> dict:
     return res
 
 
-def host_e2e(comm, k: int, gib: int = 1, bucket_mib: int = 64) -> dict:
+def host_e2e(comm, k: int, gib: int = 1, bucket_mib: int = 64, world: int = 1) -> dict:
     """BASELINE config 3: a `gib` GiB fp32 gradient in pinned host memory through
     inccl_allreduce_f32_host (bucket_mib buckets, H2D / reduce / D2H on three
-    streams).  PCIe-inclusive; reported beside `value`, never as it."""
+    streams).  PCIe-inclusive; reported beside `value`, never as it.  At N > 1
+    every rank runs it (the reduce is the engine's allreduce across ranks); the
+    time is the max over ranks."""
     import torch
+    import torch.distributed as dist
     n = (gib << 30) // 4
     gen = torch.Generator().manual_seed(3)
     x = torch.randn(n, generator=gen, dtype=torch.float32).pin_memory()
     y = torch.empty(n, dtype=torch.float32).pin_memory()
     comm.allreduce_f32_host(x, y, scale_exp=k, bucket_bytes=bucket_mib << 20)   # warm
     reps = 4
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
         comm.allreduce_f32_host(x, y, scale_exp=k, bucket_bytes=bucket_mib << 20)
-    dt = (time.perf_counter() - t0) / reps
+    dt = agree([(time.perf_counter() - t0) / reps], world)[0]
     # this box's PCIe ceiling on the same pinned buffers: H2D alone, D2H alone,
     # and both at once on two streams (what the pipeline overlaps).  The streams
     # have the greatest priority, as the pipeline's copy streams do (api.c
@@ -866,7 +871,9 @@ def host_e2e(comm, k: int, gib: int = 1, bucket_mib: int = 64) -> dict:
             "copy_only_GBps": {"h2d": round(h2d, 2), "d2h": round(d2h, 2), "h2d_and_d2h_concurrent": round(both, 2),
                                "stream_priority": prio},
             "frac_of_concurrent_copy": round((gib << 30) / dt / 1e9 / both, 4),
-            "what": "pinned host fp32 -> H2D -> fused quantise+sum+dequantise -> D2H, wall clock"}
+            "what": "pinned host fp32 -> H2D -> fused quantise+sum+dequantise -> D2H, wall clock" if world == 1 else
+                    f"pinned host fp32 on each of {world} ranks -> H2D -> the engine's allreduce -> D2H, wall clock, "
+                    "max over ranks"}
 
 
 def numerics_vs_exact(dev, n: int) -> list:
@@ -1299,6 +1306,15 @@ def main():
         else:
             res["bf16"] = {"skipped": f"run past {soft:.0f} s from process start"}
         comm.set_engine(chosen[0])
+        # north_star: the path starts and ends in host memory -- the end-to-end
+        # rate with pinned H2D / D2H, at this N too
+        if agree([time.monotonic() - T_START], world)[0] <= soft:
+            set_stage("host_e2e at N > 1")
+            try:
+                res["host_e2e"] = host_e2e(comm, k, world=world)
+            except Exception as e:  # noqa: BLE001
+                print(f"rank {rank}: host_e2e failed: {e!r}", file=sys.stderr, flush=True)
+                res["host_e2e"] = {"error": repr(e)}
     def extra(key, fn):
         """An N = 1 extra key (one process, no collectives): a failure is recorded
         in the key instead of costing the headline line."""

@@ -282,12 +282,40 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
 // trip carries kApplyFrames frames' loads.
 constexpr int kApplyFrames = 4;
 
-// payload word i (i = j*64 + lane) of the frame at `fr`, its payload at byte
-// 54 + 16*wf (2-byte aligned), network order -> host order (nts.c:361-363)
+// payload word i of the frame at `fr`, its payload at byte 54 + 16*wf (2-byte
+// aligned), network order -> host order (nts.c:361-363)
 __device__ __forceinline__ uint32_t payload_word(const uint8_t* fr, uint32_t wf, int i)
 {
     const uint16_t* d16 = reinterpret_cast<const uint16_t*>(fr + 54 + 16 * wf);
     return __builtin_bswap32((uint32_t)d16[2 * i] | ((uint32_t)d16[2 * i + 1] << 16));
+}
+
+// Payload words 4 lane .. 4 lane + 3, host order.  With 16-byte aligned rows
+// (`wide`): the payload starts at 54 or 70, both 6 mod 16, so lane l loads the
+// aligned 16-byte chunk holding payload bytes 16 l - 6 .. 16 l + 9 in ONE
+// dwordx4 load and takes bytes 16 l + 10 .. 16 l + 15 from lane l+1's chunk
+// (lane 63 reads those six bytes, still inside the frame, as two dwords).  The
+// 2-byte-load fallback takes eight loads per lane.  Call in uniform control flow.
+__device__ __forceinline__ void payload16(const uint8_t* fr, uint32_t wf, int lane, bool wide, uint32_t (&w)[4])
+{
+    if (wide) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const u4* c = reinterpret_cast<const u4*>(fr) + (3 + wf);
+        const u4 a = c[lane];
+        uint32_t n0 = (uint32_t)__shfl_down((int)a.x, 1, kWave), n1 = (uint32_t)__shfl_down((int)a.y, 1, kWave);
+        if (lane == kWave - 1) {
+            const uint32_t* t = reinterpret_cast<const uint32_t*>(c + kWave);
+            n0 = t[0];
+            n1 = t[1];
+        }
+        w[0] = __builtin_bswap32(__builtin_amdgcn_alignbyte(a.z, a.y, 2));
+        w[1] = __builtin_bswap32(__builtin_amdgcn_alignbyte(a.w, a.z, 2));
+        w[2] = __builtin_bswap32(__builtin_amdgcn_alignbyte(n0, a.w, 2));
+        w[3] = __builtin_bswap32(__builtin_amdgcn_alignbyte(n1, n0, 2));
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = payload_word(fr, wf, 4 * lane + j);
+    }
 }
 
 __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwitchState s,
@@ -295,7 +323,7 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwi
                                                                          int64_t stride, int64_t count,
                                                                          const int32_t* __restrict__ ports,
                                                                          int32_t* __restrict__ action,
-                                                                         const uint32_t* __restrict__ psns)
+                                                                         const uint32_t* __restrict__ psns, bool wide)
 {
     const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
     const int64_t f0 = ((int64_t)blockIdx.x * kWavesPerBlock + w) * kApplyFrames;
@@ -383,33 +411,31 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwi
     }
     // stage D: the leaders' sums.  Every leader's slot partial and its two lowest
     // counted ports' payloads are loaded before any is added (fan-in 2 needs no
-    // more); further ports, if any, follow.  Word i = j*64 + lane: each wave
-    // instruction covers 256 contiguous bytes.
+    // more); further ports, if any, follow.  Lane l owns words 4 l .. 4 l + 3:
+    // one dwordx4 per lane moves the slot's 1 KiB.
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     uint32_t acc[kApplyFrames][4], p0[kApplyFrames][4], p1[kApplyFrames][4];
 #pragma unroll
     for (int k = 0; k < kApplyFrames; ++k) {
         if (!lead[k]) continue;
-        const int32_t* agg = s.agg + (size_t)(psn[k] & (s.slots - 1)) * kLanes;
+        const u4 g = reinterpret_cast<const u4*>(s.agg + (size_t)(psn[k] & (s.slots - 1)) * kLanes)[lane];
+        acc[k][0] = g.x; acc[k][1] = g.y; acc[k][2] = g.z; acc[k][3] = g.w;
         uint64_t m = counted_ports[k];
-        const int q0 = __builtin_ctzll(m);
+        const uint32_t e0 = (uint32_t)__shfl((int)first_of[k], __builtin_ctzll(m), kWave);
         m &= m - 1;
-        const uint32_t e0 = (uint32_t)__shfl((int)first_of[k], q0, kWave);
-        const uint8_t* fr0 = frames + (int64_t)(e0 >> 1) * stride;
-        const int q1 = m ? __builtin_ctzll(m) : q0;
-        const uint32_t e1 = (uint32_t)__shfl((int)first_of[k], q1, kWave);
-        const uint8_t* fr1 = frames + (int64_t)(e1 >> 1) * stride;
+        payload16(frames + (int64_t)(e0 >> 1) * stride, e0 & 1u, lane, wide, p0[k]);
+        if (m) {
+            const uint32_t e1 = (uint32_t)__shfl((int)first_of[k], __builtin_ctzll(m), kWave);
+            payload16(frames + (int64_t)(e1 >> 1) * stride, e1 & 1u, lane, wide, p1[k]);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            acc[k][j] = (uint32_t)agg[j * kWave + lane];
-            p0[k][j] = payload_word(fr0, e0 & 1u, j * kWave + lane);
-            p1[k][j] = m ? payload_word(fr1, e1 & 1u, j * kWave + lane) : 0u;
+            for (int j = 0; j < 4; ++j) p1[k][j] = 0u;
         }
     }
 #pragma unroll
     for (int k = 0; k < kApplyFrames; ++k) {
         if (!lead[k]) continue;
         const uint32_t slot = psn[k] & (s.slots - 1);
-        int32_t* agg = s.agg + (size_t)slot * kLanes;
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[k][j] += p0[k][j] + p1[k][j];
         uint64_t m = counted_ports[k];
@@ -417,12 +443,12 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwi
         m &= m - 1;
         for (; m; m &= m - 1) {                                  // ports beyond the first two
             const uint32_t e = (uint32_t)__shfl((int)first_of[k], __builtin_ctzll(m), kWave);
-            const uint8_t* frq = frames + (int64_t)(e >> 1) * stride;
+            uint32_t pq[4];
+            payload16(frames + (int64_t)(e >> 1) * stride, e & 1u, lane, wide, pq);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[k][j] += payload_word(frq, e & 1u, j * kWave + lane);
+            for (int j = 0; j < 4; ++j) acc[k][j] += pq[j];
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) agg[j * kWave + lane] = (int32_t)acc[k][j];
+        reinterpret_cast<u4*>(s.agg + (size_t)slot * kLanes)[lane] = u4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
         // clear_state_data(psn + WINDOW) when the PSN completes in this batch
         // (nts.c:235-242, :367): slot psn + slots/2, which no frame of the batch
         // touches (a batch's PSNs are less than slots/2 apart)
@@ -944,9 +970,11 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
     const dim3 lanes((unsigned)(((int64_t)count + kClaimBlock - 1) / kClaimBlock));
     hipLaunchKernelGGL(k_ingress_claim, lanes, dim3(kClaimBlock), 0, st, *s, frames, (int64_t)stride, (int64_t)count,
                        ports, action, psn_out);
+    // 16-byte aligned rows: apply loads each payload with one dwordx4 per lane
+    const bool wide = ((uintptr_t)frames & 15) == 0 && (stride & 15) == 0;
     hipLaunchKernelGGL(k_ingress_apply, dim3(grid_for(((int64_t)count + kApplyFrames - 1) / kApplyFrames)),
                        dim3(kWave * kWavesPerBlock), 0, st, *s,
-                       frames, (int64_t)stride, (int64_t)count, ports, action, psn_out);
+                       frames, (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
     hipLaunchKernelGGL(k_ingress_commit, lanes, dim3(kClaimBlock), 0, st, *s, (int64_t)count, ports, action, psn_out);
     return (int)hipGetLastError();
 }

@@ -15,9 +15,9 @@ STRIDE = 1152
 INT32_MIN, INT32_MAX = -(2 ** 31), 2 ** 31 - 1
 
 
-def _rows(frames, dev):
+def _rows(frames, dev, stride=STRIDE):
     import torch
-    a = np.zeros((len(frames), STRIDE), np.uint8)
+    a = np.zeros((len(frames), stride), np.uint8)
     for i, f in enumerate(frames):
         a[i, : len(f)] = np.frombuffer(f, np.uint8)
     return torch.from_numpy(a).to(dev)
@@ -86,9 +86,11 @@ def _expected_frame(orc, t, c, agg, psn, op, reth):
                                 src_mac=bytes(t[c]["src_mac"]), dst_mac=bytes(t[c]["dst_mac"]))
 
 
-# 20 children: RETH words of children 16+ are loaded directly, not shuffled from the prefetch
-@pytest.mark.parametrize("fan_in", [2, 3, 8, 20])
-def test_switch_batches(gpu, orc, fan_in):
+# 20 children: RETH words of children 16+ are loaded directly, not shuffled from the prefetch.
+# Stride 1100 (4-byte but not 16-byte aligned rows): ingress's 2-byte payload
+# loads and egress's dword stores instead of the 16-byte paths.
+@pytest.mark.parametrize("fan_in,stride", [(2, STRIDE), (3, STRIDE), (8, STRIDE), (20, STRIDE), (2, 1100), (8, 1100)])
+def test_switch_batches(gpu, orc, fan_in, stride):
     import torch
     from container_inc_amd import inccl
     rng = np.random.default_rng(100 + fan_in)
@@ -120,10 +122,10 @@ def test_switch_batches(gpu, orc, fan_in):
             frames.append(orc.build_data_frame(payload[(p, port)], psn=p, opcode=opcode[p], qp=0x11, with_reth=wf,
                                                reth=reth[(p, port)] if wf else None, src_ip=0x0A000001 + port))
             ports.append(port)
-        fr = _rows(frames, gpu)
+        fr = _rows(frames, gpu, stride)
         pt = torch.tensor(ports, dtype=torch.int32, device=gpu)
         action, psn_out = sw.ingress(fr, pt)
-        out, out_len = sw.egress(fr, pt, action, psn_out, tmpl_dev)
+        out, out_len = sw.egress(fr, pt, action, psn_out, tmpl_dev, out_stride=stride)
         torch.cuda.synchronize()
         action, psn_out = action.cpu().numpy(), psn_out.cpu().numpy()
         out, out_len = out.cpu().numpy(), out_len.cpu().numpy()
@@ -291,10 +293,10 @@ def test_switch_serial_order_vs_oracle_reference_ring(gpu, orc, fan_in, seed):
             eg.append(e.copy())
             if rc in (orc.SW_ABSORBED, orc.SW_BROADCAST):
                 counted_reth[(p, c)] = rb
-        fr = _rows(frames, gpu)
+        fr = _rows(frames, gpu, stride)
         pt = torch.tensor(ports, dtype=torch.int32, device=gpu)
         action, psn_out = sw.ingress(fr, pt)
-        out, out_len = sw.egress(fr, pt, action, psn_out, tmpl_dev)
+        out, out_len = sw.egress(fr, pt, action, psn_out, tmpl_dev, out_stride=stride)
         torch.cuda.synchronize()
         act = action.cpu().numpy().tolist()
         assert act == rcs, (b, seq, act, rcs)
