@@ -258,6 +258,7 @@ def test_switch_serial_order_vs_oracle_reference_ring(gpu, orc, fan_in, seed):
     consecutive PSNs.  Every copy of a frame carries a DIFFERENT payload, so the
     actions, which copy is counted, and every emitted frame must all agree.
     Retransmits land before, at and after their PSN's completion."""
+    stride = 1100 if seed == 2 else STRIDE   # seed 2: rows 4- but not 16-byte aligned
     import torch
     from container_inc_amd import inccl
     rng = np.random.default_rng(700 + seed)
