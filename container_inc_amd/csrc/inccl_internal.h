@@ -30,7 +30,8 @@
  * mesh buffer never returned in round 2's two-rank bench (DESIGN.md "2 GiB per
  * IPC export"); a two-process C probe imports 2.6 GB one-way and both ways at
  * once, coarse and uncached, on torch's HIP 7.0 and on /opt/rocm's 7.2 alike
- * (profiles/r03/ipc_runtime_probe.log), so the runtime is not the cause.
+ * (profiles/r03/ipc_probe/), so the runtime is not the cause; two Python-hosted
+ * processes hang at that size, with or without torch.
  * Every IPC buffer stays split or refused below 2 GiB by default;
  * $INCCL_IPC_MAX_BYTES (same on every rank) raises the bound for the probe
  * that tests the engines beyond it (tools/ipc_big_engine_probe.py). */
