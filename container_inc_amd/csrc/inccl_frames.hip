@@ -279,8 +279,8 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
 // payloads -> the stores), and with 131 072 short waves that latency, not HBM,
 // set the pass's time (102 us).  A wave now takes kApplyFrames consecutive
 // frames and runs each stage for all of them before the next, so every round
-// trip carries kApplyFrames frames' loads.
-constexpr int kApplyFrames = 4;
+// trip carries kApplyFrames frames' loads.  (Template parameter: 4 by default,
+// $INCCL_APPLY_FRAMES = 2 or 8 for sweeps.)
 
 // payload word i of the frame at `fr`, its payload at byte 54 + 16*wf (2-byte
 // aligned), network order -> host order (nts.c:361-363)
@@ -318,6 +318,7 @@ __device__ __forceinline__ void payload16(const uint8_t* fr, uint32_t wf, int la
     }
 }
 
+template <int kApplyFrames>
 __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwitchState s,
                                                                          const uint8_t* __restrict__ frames,
                                                                          int64_t stride, int64_t count,
@@ -972,9 +973,21 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
                        ports, action, psn_out);
     // 16-byte aligned rows: apply loads each payload with one dwordx4 per lane
     const bool wide = ((uintptr_t)frames & 15) == 0 && (stride & 15) == 0;
-    hipLaunchKernelGGL(k_ingress_apply, dim3(grid_for(((int64_t)count + kApplyFrames - 1) / kApplyFrames)),
-                       dim3(kWave * kWavesPerBlock), 0, st, *s,
-                       frames, (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
+    static const int apply_frames = [] {
+        const char* e = getenv("INCCL_APPLY_FRAMES");
+        const int v = e ? atoi(e) : 4;
+        return (v == 2 || v == 8) ? v : 4;
+    }();
+    const int64_t waves = ((int64_t)count + apply_frames - 1) / apply_frames;
+    if (apply_frames == 2)
+        hipLaunchKernelGGL(k_ingress_apply<2>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
+                           (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
+    else if (apply_frames == 8)
+        hipLaunchKernelGGL(k_ingress_apply<8>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
+                           (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
+    else
+        hipLaunchKernelGGL(k_ingress_apply<4>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
+                           (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
     hipLaunchKernelGGL(k_ingress_commit, lanes, dim3(kClaimBlock), 0, st, *s, (int64_t)count, ports, action, psn_out);
     return (int)hipGetLastError();
 }
