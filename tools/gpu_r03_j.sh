@@ -21,6 +21,9 @@ ln -s "$TL/libamdhip64.so" "$A/libamdhip64.so.7"                        # HIP 7.
 ln -s /opt/rocm/lib/libhsa-runtime64.so.1 "$A/libhsa-runtime64.so"     # ... over HSA 7.2
 ln -s /opt/rocm/lib/libamdhip64.so.7 "$B/libamdhip64.so.7"              # HIP 7.2 ...
 ln -s "$TL/libhsa-runtime64.so" "$B/libhsa-runtime64.so.1"             # ... over HSA 7.0
+for dep in libelf.so libdrm.so libdrm_amdgpu.so libnuma.so librocprofiler-register.so; do
+  ln -s "$TL/$dep" "$B/$dep"                                          # torch HSA's own deps ($ORIGIN = B)
+done
 for combo in A B; do
   d=$A; [ $combo = B ] && d=$B
   LD_LIBRARY_PATH=$d timeout -k 10 60 tools/probes/ipc_size_probe 0 2600 sib > $O/c_sib_2600_mix$combo.log 2>&1
