@@ -49,6 +49,8 @@ SIGNATURES = {
     "inccl_group_rank": (_I, [_P]),
     "inccl_group_size": (_I, [_P]),
     "inccl_group_device": (_I, [_P]),
+    "inccl_ipc_max_bytes": (_SZ, []),
+    "inccl_group_ipc_max_bytes": (_SZ, [_P]),
     "inccl_group_transport": (_S, [_P]),
     "inccl_comm_stream": (_P, [_P]),
     "inccl_comm_barrier": (_I, [_P]),

@@ -231,6 +231,7 @@ static struct inccl_group *group_alloc(int world_size, int rank, int device)
     g->world_size = world_size;
     g->device = dev;
     g->master_fd = -1;
+    g->ipc_max_bytes = inccl_ipc_local_max_bytes();   /* agreed over the ranks after the bootstrap */
     return g;
 }
 
@@ -264,6 +265,17 @@ struct inccl_group *inccl_group_create_ex(int world_size, int rank, const char *
     if (rc == 0 && rank == 0 && g->peer_fds == NULL) {
         g->peer_fds = (int *)calloc((size_t)world_size, sizeof(int));
         for (int i = 0; g->peer_fds && i < world_size; ++i) g->peer_fds[i] = -1;
+    }
+    if (rc == 0 && world_size > 1) {
+        /* the smallest IPC bound over the ranks (MiB), so that every rank
+         * refuses an oversized IPC buffer alike: max of the complements */
+        const size_t mib = g->ipc_max_bytes >> 20;
+        uint32_t w = 0xFFFFFFFFu - (uint32_t)(mib < 0xFFFFFFFEu ? mib : 0xFFFFFFFEu);
+        rc = inccl_group_allreduce_max_u32(g, &w);
+        if (rc == 0) {
+            const size_t agreed = (size_t)(0xFFFFFFFFu - w) << 20;
+            if (agreed < g->ipc_max_bytes) g->ipc_max_bytes = agreed;
+        }
     }
     if (rc != 0) {
         fprintf(stderr, "inccl_group_create: %s\n", inccl_last_error());

@@ -279,8 +279,10 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
 // payloads -> the stores), and with 131 072 short waves that latency, not HBM,
 // set the pass's time (102 us).  A wave now takes kApplyFrames consecutive
 // frames and runs each stage for all of them before the next, so every round
-// trip carries kApplyFrames frames' loads.  (Template parameter: 4 by default,
-// $INCCL_APPLY_FRAMES = 2 or 8 for sweeps.)
+// trip carries kApplyFrames frames' loads.  Template parameter: 2 by default
+// (82 us per 131 072-frame batch, against 97 at 4 and 113 at 8, where the
+// extra registers cost more occupancy than the shared round trips save;
+// profiles/r03/apply_frames_sweep.txt); $INCCL_APPLY_FRAMES = 1, 4 or 8 for sweeps.
 
 // payload word i of the frame at `fr`, its payload at byte 54 + 16*wf (2-byte
 // aligned), network order -> host order (nts.c:361-363)
@@ -975,18 +977,24 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
     const bool wide = ((uintptr_t)frames & 15) == 0 && (stride & 15) == 0;
     static const int apply_frames = [] {
         const char* e = getenv("INCCL_APPLY_FRAMES");
-        const int v = e ? atoi(e) : 4;
-        return (v == 2 || v == 8) ? v : 4;
+        const int v = e ? atoi(e) : 2;
+        return (v == 1 || v == 4 || v == 8) ? v : 2;
     }();
     const int64_t waves = ((int64_t)count + apply_frames - 1) / apply_frames;
-    if (apply_frames == 2)
+    if (apply_frames == 1)
+        hipLaunchKernelGGL(k_ingress_apply<1>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
+                           (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
+    else if (apply_frames == 4)
+        hipLaunchKernelGGL(k_ingress_apply<4>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
+                           (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
+    else if (apply_frames == 2)
         hipLaunchKernelGGL(k_ingress_apply<2>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
                            (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
     else if (apply_frames == 8)
         hipLaunchKernelGGL(k_ingress_apply<8>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
                            (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
     else
-        hipLaunchKernelGGL(k_ingress_apply<4>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
+        hipLaunchKernelGGL(k_ingress_apply<2>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
                            (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
     hipLaunchKernelGGL(k_ingress_commit, lanes, dim3(kClaimBlock), 0, st, *s, (int64_t)count, ports, action, psn_out);
     return (int)hipGetLastError();

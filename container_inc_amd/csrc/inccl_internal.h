@@ -26,24 +26,16 @@
 #define INCCL_ENGINE_AR 5
 #define INCCL_MAX_HOST_REGIONS 16
 #define INCCL_MESH_REGIONS 4
-/* Largest single allocation exported over HIP IPC.  Importing a peer's 2.5 GiB
- * mesh buffer never returned in round 2's two-rank bench (DESIGN.md "2 GiB per
- * IPC export"); a two-process C probe imports 2.6 GB one-way and both ways at
- * once, coarse and uncached, on torch's HIP 7.0 and on /opt/rocm's 7.2 alike
- * (profiles/r03/ipc_probe/), so the runtime is not the cause; two Python-hosted
- * processes hang at that size, with or without torch.
- * Every IPC buffer stays split or refused below 2 GiB by default;
- * $INCCL_IPC_MAX_BYTES (same on every rank) raises the bound for the probe
- * that tests the engines beyond it (tools/ipc_big_engine_probe.py). */
+/* Largest single allocation exported over HIP IPC (runtime.c).  Importing a
+ * peer's allocation above 2 GiB hangs under PyTorch's bundled HSA runtime
+ * (ROCr 7.0.2) and works under /opt/rocm's 7.2 (DESIGN.md "2 GiB per IPC
+ * export"); the bound follows the HSA runtime the process mapped, and a group
+ * agrees on the smallest over its ranks ($INCCL_IPC_MAX_BYTES overrides). */
 #define INCCL_IPC_MAX_BYTES_DEFAULT (((size_t)2 << 30) - ((size_t)2 << 20))
-#include <stdlib.h>
-static inline size_t inccl_ipc_max_bytes(void)
-{
-    const char *e = getenv("INCCL_IPC_MAX_BYTES");
-    const unsigned long long v = e ? strtoull(e, NULL, 0) : 0;
-    return v ? (size_t)v : INCCL_IPC_MAX_BYTES_DEFAULT;
-}
-#define INCCL_IPC_MAX_BYTES (inccl_ipc_max_bytes())
+#define INCCL_IPC_MAX_BYTES_UNBOUNDED ((size_t)1 << 40)
+const char *inccl_hsa_runtime_path(void);
+unsigned inccl_hsa_build_of(const char *path);
+size_t inccl_ipc_local_max_bytes(void);
 
 struct inccl_local_hub;
 struct inccl_shm_bar;
@@ -62,6 +54,7 @@ struct inccl_group {
     int master_fd;
     int *peer_fds;
     struct inccl_shm_bar *shm_bar;   /* same-node fast barrier (NULL: TCP barrier) */
+    size_t ipc_max_bytes;            /* largest IPC export, agreed over the ranks (runtime.c) */
     uint32_t max_seq;                /* host max-allreduces through shm so far (picks the word bank) */
     /* local transport */
     struct inccl_local_hub *hub;

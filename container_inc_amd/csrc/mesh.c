@@ -10,7 +10,7 @@
  * overlap, and the host never waits.
  *
  * Per rank, four device allocations shared over HIP IPC (separate, so that no
- * single export reaches 2 GiB; see INCCL_IPC_MAX_BYTES):
+ * single export needs to exceed the group's IPC bound; see runtime.c):
  *   sig    [0, 64 KiB) signal array: arrive[8][1024] and ready[8][1024] words;
  *          [64 KiB, +16) call counter, retired workgroups, ticket, abort word
  *   inbox  W * cap int32: slot j holds rank j's partial of my shard
@@ -89,9 +89,10 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
         return inccl_set_error(INCCL_ERR_ARG, "mesh engine supports up to %d GPUs", INCCL_MAX_LOCAL_INPUTS);
     const size_t cap = (shard + ((size_t)1 << 19) - 1) & ~(((size_t)1 << 19) - 1);   /* 2 MiB granules */
     /* every rank computes the same sizes, so every rank refuses alike */
-    if (mesh_region_bytes(1, W, cap) > INCCL_IPC_MAX_BYTES)
-        return inccl_set_error(INCCL_ERR_ARG, "mesh: a %zu-element shard needs a %zu-byte inbox; IPC buffers stay below "
-                               "2 GiB (hipIpcOpenMemHandle of larger ones hangs)", shard, mesh_region_bytes(1, W, cap));
+    if (mesh_region_bytes(1, W, cap) > g->ipc_max_bytes)
+        return inccl_set_error(INCCL_ERR_ARG, "mesh: a %zu-element shard needs a %zu-byte inbox; this group's IPC "
+                               "buffers stay below %zu bytes (under PyTorch's bundled HSA runtime, importing a larger "
+                               "one hangs; runtime.c)", shard, mesh_region_bytes(1, W, cap), g->ipc_max_bytes);
     /* make before break (as p2p_ensure): the old buffers stay alive, and mapped
      * by the peers, until every rank has mapped the new ones */
     struct inccl_communicator old = *c;

@@ -84,9 +84,10 @@ static int p2p_ensure(struct inccl_communicator *c, size_t elems)
     struct inccl_group *g = c->group;
     const int W = g->world_size, me = g->rank;
     if (c->p2p_cap >= elems && c->p2p_part) return 0;
-    if (elems * sizeof(int32_t) > INCCL_IPC_MAX_BYTES)   /* same sizes on every rank: all refuse alike */
-        return inccl_set_error(INCCL_ERR_ARG, "p2p: a %zu-element bucket needs %zu-byte IPC buffers; they stay below "
-                               "2 GiB (hipIpcOpenMemHandle of larger ones hangs)", elems, elems * sizeof(int32_t));
+    if (elems * sizeof(int32_t) > g->ipc_max_bytes)   /* same sizes and bound on every rank: all refuse alike */
+        return inccl_set_error(INCCL_ERR_ARG, "p2p: a %zu-element bucket needs %zu-byte IPC buffers; this group's stay "
+                               "below %zu bytes (under PyTorch's bundled HSA runtime, importing a larger one hangs; "
+                               "runtime.c)", elems, elems * sizeof(int32_t), g->ipc_max_bytes);
     /* this rank's queued reads of the peers' buffers (the previous call's gather)
      * drain before anyone may drop them */
     INCCL_HIP(hipDeviceSynchronize());

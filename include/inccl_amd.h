@@ -113,6 +113,16 @@ int inccl_group_size(const struct inccl_group *group);
 int inccl_group_device(const struct inccl_group *group);
 /* "rccl" or "local" */
 const char *inccl_group_transport(const struct inccl_group *group);
+/* Largest single buffer the IPC engines (p2p, mesh) may share with peers, in
+ * bytes.  It follows the HSA runtime the process runs on: PyTorch's bundled
+ * ROCr (ROCm 7.0.2) hangs importing a peer allocation above 2 GiB, so 2 GiB -
+ * 2 MiB there; no bound under a ROCr of ROCm 7.2 or later (/opt/rocm);
+ * $INCCL_IPC_MAX_BYTES overrides.  inccl_ipc_max_bytes: this process;
+ * inccl_group_ipc_max_bytes: the smallest over the group's ranks, agreed at
+ * creation -- a bucket whose IPC buffer would exceed it is refused on every
+ * rank alike. */
+size_t inccl_ipc_max_bytes(void);
+size_t inccl_group_ipc_max_bytes(const struct inccl_group *group);
 /* The communicator's own HIP stream (void* hipStream_t). */
 void *inccl_comm_stream(struct inccl_communicator *comm);
 int inccl_comm_barrier(struct inccl_communicator *comm);

@@ -96,6 +96,30 @@ def test_reference_host_c_builds_unchanged(tmp_path):
     assert used == {"inccl_group_create", "inccl_communicator_create", "inccl_allreduce_write"}, used
 
 
+def test_ipc_bound_follows_the_hsa_runtime(lib, tmp_path):
+    """The IPC engines' largest shared buffer follows the HSA runtime the
+    process mapped (csrc/runtime.c): 2 GiB - 2 MiB under PyTorch's bundled ROCr
+    (this Python process), no bound under /opt/rocm's ROCm 7.2 ROCr (a C
+    program linked with the library); $INCCL_IPC_MAX_BYTES overrides."""
+    from container_inc_amd._lib import runtime_libs
+    hsa = runtime_libs().get("libhsa-runtime64", "")
+    if os.path.basename(hsa) == "libhsa-runtime64.so":   # torch's file: no ROCm build in its name
+        assert lib.inccl_ipc_max_bytes() == (2 << 30) - (2 << 20)
+    src = tmp_path / "ipcmax.c"
+    src.write_text('#include <stdio.h>\n#include "inccl_amd.h"\nint main(void){printf("%zu\\n", inccl_ipc_max_bytes());}\n')
+    exe = tmp_path / "ipcmax"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe), "-L",
+                           os.path.join(ROOT, "container_inc_amd"), "-linccl_amd",
+                           "-Wl,-rpath," + os.path.join(ROOT, "container_inc_amd")])
+    env = {k: v for k, v in os.environ.items() if k != "INCCL_IPC_MAX_BYTES"}
+    rocm_hsa = os.path.realpath("/opt/rocm/lib/libhsa-runtime64.so.1")
+    if re.search(r"libhsa-runtime64\.so\.1\.\d+\.(\d+)$", rocm_hsa) and \
+            int(re.search(r"\.(\d+)$", rocm_hsa).group(1)) >= 70200:
+        assert int(subprocess.check_output([str(exe)], env=env, text=True)) == 1 << 40
+    env["INCCL_IPC_MAX_BYTES"] = "12345"
+    assert int(subprocess.check_output([str(exe)], env=env, text=True)) == 12345
+
+
 def test_version_and_host_helpers(lib):
     assert lib.inccl_version().startswith(b"inccl-amd")
     from container_inc_amd import inccl

@@ -85,6 +85,34 @@ def test_reference_host_binary(gpu):
         assert p.returncode == 0 and "result ok" in out, out + err
 
 
+@pytest.mark.parametrize("engine", ["p2p", "mesh"])
+def test_ipc_engine_over_2gib_c_hosted(gpu, tmp_path, engine):
+    """The IPC engines on a 2.25 GiB bucket (p2p: 2.25 GiB IPC buffers; mesh:
+    a 2.25 GiB inbox) in C processes, which map /opt/rocm's HSA runtime where
+    importing such buffers works (csrc/runtime.c lifts the 2 GiB bound there;
+    under PyTorch's bundled ROCr the import hangs).  Two processes
+    on GPU 0, rank 0 the TCP master, two calls, every lane exact."""
+    exe = tmp_path / "big_ipc"
+    subprocess.check_call(["gcc", "-O2", "-std=gnu11", "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(ROOT, "include"),
+                           "-I", "/opt/rocm/include", os.path.join(ROOT, "tests", "c", "big_ipc.c"), "-o", str(exe),
+                           "-L", os.path.join(ROOT, "container_inc_amd"), "-linccl_amd", "-L", "/opt/rocm/lib",
+                           "-lamdhip64", "-Wl,-rpath," + os.path.join(ROOT, "container_inc_amd"),
+                           "-Wl,-rpath,/opt/rocm/lib"])
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items() if k != "INCCL_IPC_MAX_BYTES"}
+    env.update(INCCL_MASTER_PORT=str(port), INCCL_DEVICE="0", INCCL_BOOT_TIMEOUT="120", INCCL_ENGINE=engine)
+    n = str(9 << 26)   # 603 979 776 elements: 2.25 GiB of int32 partials
+    ps = [subprocess.Popen([str(exe), "2", str(r), n, engine], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True, env=env) for r in range(2)]
+    outs = [p.communicate(timeout=200) for p in ps]
+    for p, (out, err) in zip(ps, outs):
+        assert p.returncode == 0 and "result ok" in out, out + err
+        assert "group bound 1099511627776" in out, out
+
+
 def test_host_stress_binary(gpu, tmp_path):
     """tests/c/host_stress.c through the C ABI alone: allreduce_write on pageable
     and on registered memory and allreduce_f32_host on pageable memory, 5 pipeline
