@@ -44,16 +44,24 @@ constexpr int kEgressWaves = 8;       // 512-lane blocks, two per CU, persistent
 constexpr int kLanes = 256;           // int32 lanes per packet (nts.c:55)
 
 __device__ uint32_t g_seg[kSeg][2][16];       // [byte j][nibble][value] = Z_{16-j}(T[value << 4 nibble]), T = util.c:141-150
+__device__ uint32_t g_segb[kSeg][256];        // [byte j][value] = Z_{16-j}(T[value])
 __device__ uint32_t g_lane_shift[8][16][kWave];   // [nibble][value][lane] = Z_{17 (63 - lane)}(value << 4 nibble)
 
+// kByte = false: a lane's segment CRC as 34 independent nibble lookups in a
+// 2.2 KiB table (no bank conflicts, two VALU ops of index math per lookup).
+// kByte = true: 17 byte lookups in a 17 KiB table (half the index math; the
+// lanes' random entries conflict in the banks).  $INCCL_ICRC_BYTE_TABLES picks.
+template <bool kByte>
 struct CrcLds {
-    uint32_t seg[kSeg][2][16];      // a lane's segment CRC as 34 independent nibble lookups (2.2 KiB)
+    uint32_t seg[kByte ? kSeg * 256 : kSeg * 2 * 16];
     uint32_t lane_sh[8][16][kWave]; // per-lane zero-append operator, nibble-sliced
 };
 
-__device__ __forceinline__ void load_tables(CrcLds& t)
+template <bool kByte>
+__device__ __forceinline__ void load_tables(CrcLds<kByte>& t)
 {
-    for (int i = threadIdx.x; i < kSeg * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg[0][0][0])[i];
+    const uint32_t* seg = kByte ? &g_segb[0][0] : &g_seg[0][0][0];
+    for (int i = threadIdx.x; i < (kByte ? kSeg * 256 : kSeg * 2 * 16); i += blockDim.x) t.seg[i] = seg[i];
     uint32_t* dst = &t.lane_sh[0][0][0];
     const uint32_t* src = &g_lane_shift[0][0][0];
     for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) dst[i] = src[i];
@@ -73,7 +81,8 @@ __device__ __forceinline__ int masked_pos(int i)
 
 // ICRC of the frame staged at `fr` (LDS, at least 1152 B, 4-B aligned), whose
 // masked bytes are already 0xFF; result valid in every lane.
-__device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds& t, int lane)
+template <bool kByte>
+__device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds<kByte>& t, int lane)
 {
     const int ip_total = ((int)fr[16] << 8) | fr[17];   // message = 4 (init) + ip_total - 4 (no ICRC) bytes
     const int lead = kWin - ip_total;                   // zero bytes before the message
@@ -101,12 +110,21 @@ __device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds& t, int lane)
         // bytes: XOR over byte j of Z_{16-j}(T[b_j]), each split into two nibble
         // lookups.  No lookup depends on another, and the 16 entries one
         // ds_read_b32 can touch sit in 16 distinct banks (no conflicts).
+        if (kByte) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < 4; ++k) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) c ^= t.seg[4 * k + (i >> 1)][i & 1][(a[k] >> (4 * i)) & 15u];
+                for (int b = 0; b < 4; ++b) c ^= t.seg[(4 * k + b) * 256 + ((a[k] >> (8 * b)) & 0xFFu)];
+            }
+            c ^= t.seg[16 * 256 + (a[4] & 0xFFu)];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) c ^= t.seg[((4 * k + (i >> 1)) * 2 + (i & 1)) * 16 + ((a[k] >> (4 * i)) & 15u)];
+            }
+            c ^= t.seg[(16 * 2) * 16 + (a[4] & 15u)] ^ t.seg[(16 * 2 + 1) * 16 + ((a[4] >> 4) & 15u)];
         }
-        c ^= t.seg[16][0][a[4] & 15u] ^ t.seg[16][1][(a[4] >> 4) & 15u];
         // shift to the window's end: Z_{17 (63 - lane)}(c)
         uint32_t r = 0;
 #pragma unroll
@@ -150,10 +168,11 @@ __device__ __forceinline__ bool icrc_len_ok(int ipt, int64_t stride)
 // Persistent: each wave walks its frames with the next frame's words (5 dwords
 // a lane, coalesced) and the one after's header in flight while the current
 // frame's CRC runs from LDS.
+template <bool kByte>
 __global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __restrict__ frames, int64_t stride,
                                                                 int64_t count, uint32_t* __restrict__ out)
 {
-    __shared__ CrcLds t;
+    __shared__ CrcLds<kByte> t;
     __shared__ __attribute__((aligned(16))) uint8_t buf[kIcrcWaves][kFrameMax];
     load_tables(t);
     __syncthreads();
@@ -190,7 +209,7 @@ __global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __res
             fetch(fn, ipn, cur);
             hdrN = fn + step < count ? icrc_hdr_load(frames + (fn + step) * stride, lane) : 0u;
         }
-        const uint32_t crc = icrc_len_ok(ip, stride) ? icrc_wave(buf[w], t, lane) : 0u;
+        const uint32_t crc = icrc_len_ok(ip, stride) ? icrc_wave<kByte>(buf[w], t, lane) : 0u;
         if (lane == 0) out[f] = crc;
         __builtin_amdgcn_wave_barrier();
         f = fn;
@@ -842,6 +861,7 @@ __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState 
 // ---------------------------------------------------------------------------
 uint32_t host_tab[256];
 uint32_t host_seg[kSeg][2][16];
+uint32_t host_segb[kSeg][256];
 uint32_t host_lane_shift[8][16][kWave];
 uint32_t host_lane16[8][16][kWave];
 uint32_t host_var[2][kVarBytes][2][16];
@@ -870,6 +890,8 @@ int ensure_tables()
     for (int j = 0; j < kSeg; ++j)
         for (int h = 0; h < 2; ++h)
             for (uint32_t v = 0; v < 16; ++v) host_seg[j][h][v] = zeros_append(host_tab[v << (4 * h)], kSeg - 1 - j);
+    for (int j = 0; j < kSeg; ++j)
+        for (uint32_t v = 0; v < 256; ++v) host_segb[j][v] = zeros_append(host_tab[v], kSeg - 1 - j);
     // Z_n is linear: Z_{n+17}(x) = Z_17(Z_n(x)), so lanes are filled from 63 down
     for (int n = 0; n < 8; ++n)
         for (uint32_t v = 0; v < 16; ++v) {
@@ -901,6 +923,7 @@ int ensure_tables()
     }
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg), host_seg, sizeof(host_seg));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane_shift), host_lane_shift, sizeof(host_lane_shift));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_segb), host_segb, sizeof(host_segb));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane16), host_lane16, sizeof(host_lane16));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_var), host_var, sizeof(host_var));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_z1024), host_z1024, sizeof(host_z1024));
@@ -955,10 +978,19 @@ int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* o
     int rc = ensure_tables();
     if (rc) return rc;
     const int64_t blocks = ((int64_t)count + kIcrcWaves - 1) / kIcrcWaves;
-    const int64_t cap = (int64_t)num_cus() * blocks_per_cu("INCCL_ICRC_BLOCKS_PER_CU", 3);   // persistent: tables loaded once per block
+    static const bool byte_tables = [] {
+        const char* e = getenv("INCCL_ICRC_BYTE_TABLES");
+        return e && atoi(e) != 0;
+    }();
+    // persistent: tables loaded once per block (the byte tables' 59 KiB fit twice per CU)
+    const int64_t cap = (int64_t)num_cus() * blocks_per_cu("INCCL_ICRC_BLOCKS_PER_CU", byte_tables ? 2 : 3);
     const int grid = (int)(blocks < cap ? blocks : cap);
-    hipLaunchKernelGGL(k_icrc, dim3(grid), dim3(kWave * kIcrcWaves), 0, (hipStream_t)stream, frames,
-                       (int64_t)stride, (int64_t)count, out);
+    if (byte_tables)
+        hipLaunchKernelGGL(k_icrc<true>, dim3(grid), dim3(kWave * kIcrcWaves), 0, (hipStream_t)stream, frames,
+                           (int64_t)stride, (int64_t)count, out);
+    else
+        hipLaunchKernelGGL(k_icrc<false>, dim3(grid), dim3(kWave * kIcrcWaves), 0, (hipStream_t)stream, frames,
+                           (int64_t)stride, (int64_t)count, out);
     return (int)hipGetLastError();
 }
 
