@@ -50,7 +50,10 @@ __device__ uint32_t g_lane_shift[8][16][kWave];   // [nibble][value][lane] = Z_{
 // kByte = false: a lane's segment CRC as 34 independent nibble lookups in a
 // 2.2 KiB table (no bank conflicts, two VALU ops of index math per lookup).
 // kByte = true: 17 byte lookups in a 17 KiB table (half the index math; the
-// lanes' random entries conflict in the banks).  $INCCL_ICRC_BYTE_TABLES picks.
+// lanes' random entries conflict in the banks, and 59 KiB of LDS per block
+// leaves two blocks per CU).  Measured 64.5 vs 62.7 us per 131 072 frames, so
+// the nibble form stays the product; $INCCL_ICRC_BYTE_TABLES=1 selects the
+// byte form (profiles/r03/icrc_byte_vs_nibble.txt).
 template <bool kByte>
 struct CrcLds {
     uint32_t seg[kByte ? kSeg * 256 : kSeg * 2 * 16];
