@@ -70,29 +70,6 @@ __device__ __forceinline__ void load_tables(CrcLds<kByte>& t)
     for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) dst[i] = src[i];
 }
 
-// XOR of the 8 nibble-table lookups of one dword `a` holding segment bytes
-// j0 .. j0+3 (memory order), from a table laid out [byte j][nibble h][16]
-// (entry (j, h, v) at byte ((j*2 + h)*16 + v)*4).  The scaled indices of all
-// four low nibbles come from one shift and one mask ((a << 2) & 0x3C3C3C3C),
-// likewise the high nibbles, so each lookup costs one byte extract instead of
-// a shift and a mask.
-__device__ __forceinline__ uint32_t seg_dword(const uint32_t* tab, uint32_t a, int j0)
-{
-    uint32_t lo = (a << 2) & 0x3C3C3C3Cu;
-    uint32_t hi = (a >> 2) & 0x3C3C3C3Cu;
-    // opaque to the optimiser (no instruction): it would otherwise fold each
-    // byte extract back into its own shift-and-mask of `a`
-    asm volatile("" : "+v"(lo), "+v"(hi));
-    const char* base = reinterpret_cast<const char*>(tab);
-    uint32_t x[8];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        x[2 * b] = *reinterpret_cast<const uint32_t*>(base + ((j0 + b) * 2) * 64 + ((lo >> (8 * b)) & 0xFFu));
-        x[2 * b + 1] = *reinterpret_cast<const uint32_t*>(base + ((j0 + b) * 2 + 1) * 64 + ((hi >> (8 * b)) & 0xFFu));
-    }
-    return (x[0] ^ x[1] ^ x[2]) ^ (x[3] ^ x[4] ^ x[5]) ^ (x[6] ^ x[7]);
-}
-
 // frame bytes that read as 0xFF while the ICRC runs: 10-13 carry the CRC init
 // (the 4 x 0xFF prefix), the rest are the ICRC masks of util.c:266-270 (tos,
 // ttl, IP checksum, UDP checksum, BTH resv8a)
@@ -144,8 +121,11 @@ __device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds<kByte>& t, int lan
             }
             c ^= t.seg[16 * 256 + (a[4] & 0xFFu)];
         } else {
-            c = seg_dword(t.seg, a[0], 0) ^ seg_dword(t.seg, a[1], 4) ^ seg_dword(t.seg, a[2], 8) ^
-                seg_dword(t.seg, a[3], 12);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) c ^= t.seg[((4 * k + (i >> 1)) * 2 + (i & 1)) * 16 + ((a[k] >> (4 * i)) & 15u)];
+            }
             c ^= t.seg[(16 * 2) * 16 + (a[4] & 15u)] ^ t.seg[(16 * 2 + 1) * 16 + ((a[4] >> 4) & 15u)];
         }
         // shift to the window's end: Z_{17 (63 - lane)}(c)
@@ -649,8 +629,12 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t c)
 // words) shifted by Z_{16 (63 - sh_lane)}.
 __device__ __forceinline__ uint32_t seg16_crc(const EgressLds& t, const uint32_t (&a)[4], int sh_lane)
 {
-    const uint32_t* seg = &t.seg[0][0][0];
-    uint32_t c = seg_dword(seg, a[0], 1) ^ seg_dword(seg, a[1], 5) ^ seg_dword(seg, a[2], 9) ^ seg_dword(seg, a[3], 13);
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c ^= t.seg[4 * k + (i >> 1) + 1][i & 1][(a[k] >> (4 * i)) & 15u];
+    }
     uint32_t r = 0;
 #pragma unroll
     for (int n = 0; n < 8; ++n) r ^= t.lane16[n][(c >> (4 * n)) & 15u][sh_lane];
