@@ -443,8 +443,16 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwi
 #pragma unroll
     for (int k = 0; k < kApplyFrames; ++k) {
         if (!lead[k]) continue;
-        const u4 g = reinterpret_cast<const u4*>(s.agg + (size_t)(psn[k] & (s.slots - 1)) * kLanes)[lane];
-        acc[k][0] = g.x; acc[k][1] = g.y; acc[k][2] = g.z; acc[k][3] = g.w;
+        // a slot whose arrival bitmap was empty before the batch holds zeros
+        // (reset, or recycled since its last use: nts.c:235-242), so its partial
+        // is not read -- in the common case, every port of a PSN in one batch,
+        // that saves a quarter of the pass's bytes
+        if (pre[k] != 0u) {
+            const u4 g = reinterpret_cast<const u4*>(s.agg + (size_t)(psn[k] & (s.slots - 1)) * kLanes)[lane];
+            acc[k][0] = g.x; acc[k][1] = g.y; acc[k][2] = g.z; acc[k][3] = g.w;
+        } else {
+            acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0u;
+        }
         uint64_t m = counted_ports[k];
         const uint32_t e0 = (uint32_t)__shfl((int)first_of[k], __builtin_ctzll(m), kWave);
         m &= m - 1;
