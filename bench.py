@@ -18,7 +18,13 @@ and produces their allreduce over all ranks into a third buffer:
   N > 1   the exchange engine that is fastest during warmup among rccl
           (quant + local sum -> RCCL reduce-scatter int32 -> dequant shard ->
           RCCL all-gather), ar, a2a, p2p, mesh and meshw, all bit-identical
-          (config 4; DESIGN.md "Multi-GPU"); then the config 5 size sweep
+          (config 4; DESIGN.md "Multi-GPU"); then the config 5 size sweep.
+          Two phases: the RCCL engines are tuned and a full headline is
+          measured with the fastest BEFORE the library's IPC engines (never
+          run across separate GPUs) are tried; an IPC engine that tunes faster
+          is measured the same way, and the faster measured headline is the
+          line (`headline_candidates` lists both).  An IPC engine that faults or
+          hangs leaves the RCCL headline to the line keeper / watchdog.
 value = bucket bytes reduced per second over the whole job = N * R * 256 MiB / t.
 
 Extra JSON fields:
@@ -1007,13 +1013,22 @@ def main():
 
     # N>1: pick the exchange engine / chunking during warmup (untimed).  Every
     # candidate runs alternating input sets A, B, A and must reproduce the
-    # reference engine's results bit for bit (integer sums are exact); any
-    # failure or mismatch on any rank drops that candidate on all ranks.  The
-    # first candidate that passes on every rank (rccl when RCCL is up) is the
-    # reference.
-    chosen = ("rccl", 1, {})
+    # reference engine's results bit for bit (integer sums are exact) and the
+    # oracle on a lane sample; any failure or mismatch on any rank drops that
+    # candidate on all ranks.  The first candidate that passes on every rank is
+    # the reference.
+    #
+    # Two phases, so that an engine never run across separate GPUs cannot cost
+    # the line: phase 1 tunes the RCCL collectives (rccl, ar, a2a) and measures
+    # a complete, verified headline with the fastest; only then does phase 2
+    # tune this library's IPC engines (p2p, mesh, meshw).  A phase-2 engine that
+    # faults or hangs leaves the phase-1 headline to the line keeper / watchdog.
+    # If a phase-2 engine tunes faster, it is measured the same way and the
+    # faster of the two measured headlines is the line (both are reported).
     tuning = []
-    refs = None
+    refs = [None]
+    phases = [[]]
+    srcs_b = None
     if world > 1:
         gen_b = torch.Generator(device=dev)
         gen_b.manual_seed(5000 + rank)
@@ -1031,15 +1046,22 @@ def main():
         for eng in ("mesh", "meshw"):
             if a.engine in ("auto", eng):
                 cands += [(eng, 1, {}), (eng, 1, {"INCCL_MESH_LAG": "32"})]
-        best = None
+        # rehearsal hook: which engines count as phase 1 (one-GPU rehearsals have no RCCL)
+        safe = set((os.environ.get("INCCL_BENCH_SAFE_ENGINES") or "rccl,ar,a2a").split(","))
+        phases = [[c for c in cands if c[0] in safe], [c for c in cands if c[0] not in safe]]
         tune_lanes = oracle_lanes(n, world, max(ch for _, ch, _ in cands), 1 << 16)
-        for eng, ch, env in cands:
-            set_stage(f"engine tuning: {eng} chunks={ch} {env or ''}")
+
+    def tune(cand_list, phase: int):
+        """Warmup-time candidates of one phase: verified, then timed over
+        TUNE_CALLS calls; returns (ms, engine, chunks, env) of the fastest."""
+        best = None
+        for eng, ch, env in cand_list:
+            set_stage(f"engine tuning (phase {phase}): {eng} chunks={ch} {env or ''}")
             ok, dt, same, got = 1, float("inf"), False, None
             os.environ.update(env)
             try:
                 comm.set_engine(eng)
-                got, same = run_verified(comm, eng, ch, (srcs, srcs_b), out, k, stream, refs)
+                got, same = run_verified(comm, eng, ch, (srcs, srcs_b), out, k, stream, refs[0])
                 for _ in range(TUNE_CALLS // 2):   # untimed: buffers just (re)allocated for this engine
                     comm.allreduce_f32(srcs, out=out, scale_exp=k, chunks=ch, stream=stream.cuda_stream)
                 torch.cuda.synchronize()
@@ -1062,194 +1084,210 @@ def main():
                 # engine that is only self-consistent never becomes the reference
                 par = oracle_check(srcs, got[0], tune_lanes, k, rank, world)
                 good = good and agree([float(par["mismatches"] or 0) if rank == 0 else 0.0], world)[0] == 0.0
-            if good and refs is None:
-                refs = (got[0], got[1])
+            if good and refs[0] is None:
+                refs[0] = (got[0], got[1])
             if rank == 0:
                 print(f"tune {eng} chunks={ch} {env or ''}: ok={v[1] == 0.0} identical={v[2] == 0.0} "
                       f"oracle_mismatches={par and par['mismatches']} ms={v[0] * 1e3:.3f}", file=sys.stderr,
                       flush=True)
-            tuning.append({"engine": eng, "chunks": ch, "env": env or None, "ok": v[1] == 0.0,
+            tuning.append({"engine": eng, "chunks": ch, "env": env or None, "phase": phase, "ok": v[1] == 0.0,
                            "bit_identical": v[1] == 0.0 and v[2] == 0.0, "verified": good,
                            "oracle_mismatches": par["mismatches"] if par else None,
                            "ms": round(v[0] * 1e3, 3) if v[1] == 0.0 else None})
             if good and (best is None or v[0] < best[0]):
                 best = (v[0], eng, ch, env)
             del got
-        if best is None:
-            raise SystemExit("no exchange engine produced verified results on every rank")
-        chosen = (best[1], best[2], best[3])
-        comm.set_engine(chosen[0])
-        os.environ.update(chosen[2])
-        del srcs_b
-    chunks = chosen[1]
+        return best
 
-    def step():
-        comm.allreduce_f32(srcs, out=out, scale_exp=k, chunks=chunks, stream=stream.cuda_stream)
+    def measure(eng: str, ch: int, env: dict) -> dict:
+        """The headline measurement of one engine: settle, W warmup steps, K
+        timed steps between barriers (max over ranks), the timed output and four
+        alternating calls against the reference engine, and the oracle check."""
+        if world > 1:
+            comm.set_engine(eng)
+        os.environ.update(env)
 
-    # settle: untimed steps in groups of 10 until --settle-seconds have passed (the
-    # same count on every rank), so that the timed steps see steady state rather
-    # than the first passes over freshly allocated buckets
-    set_stage(f"settle/warmup/timed steps of engine {comm.engine if world > 1 else 'fused'}")
-    settle_steps, t_settle = 0, time.perf_counter()
-    while True:
-        for _ in range(10):
-            step()
-        settle_steps += 10
-        torch.cuda.synchronize()
-        if agree([1.0 if time.perf_counter() - t_settle >= a.settle_seconds else 0.0], world)[0] > 0.0:
-            break
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
+        def step():
+            comm.allreduce_f32(srcs, out=out, scale_exp=k, chunks=ch, stream=stream.cuda_stream)
 
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(a.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    barrier()
-    wall = time.perf_counter() - t0
-    dev_ms = ev0.elapsed_time(ev1)
-    wall = agree([wall], world)[0]
-    ms_per_step = wall * 1e3 / a.steps
-    # the timed steps' output against the reference engine's (N>1)
-    verified = None
-    if refs is not None:
-        # the last timed step's output, then four more steps alternating the two
-        # input sets, each against the reference engine's results
-        bad = 0 if torch.equal(out, refs[0]) else 1
-        gen_b = torch.Generator(device=dev)
-        gen_b.manual_seed(5000 + rank)
-        srcs_b = [torch.randn(n, generator=gen_b, device=dev, dtype=torch.float32) for _ in range(R)]
-        torch.cuda.synchronize()
-        for i in range(4):
-            comm.allreduce_f32(srcs_b if i % 2 == 0 else srcs, out=out, scale_exp=k, chunks=chunks,
-                               stream=stream.cuda_stream)
+        # settle: untimed steps in groups of 10 until --settle-seconds have passed
+        # (the same count on every rank), so that the timed steps see steady state
+        # rather than the first passes over freshly allocated buckets
+        set_stage(f"settle/warmup/timed steps of engine {eng if world > 1 else 'fused'}")
+        settle_steps, t_settle = 0, time.perf_counter()
+        while True:
+            for _ in range(10):
+                step()
+            settle_steps += 10
             torch.cuda.synchronize()
-            bad += 0 if torch.equal(out, refs[(i + 1) % 2]) else 1
-        verified = agree([float(bad)], world)[0] == 0.0
-        del refs, srcs_b
+            if agree([1.0 if time.perf_counter() - t_settle >= a.settle_seconds else 0.0], world)[0] > 0.0:
+                break
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
 
-    # the timed path's result against the oracle on a lane sample: 2^20 strided
-    # lanes plus both sides of every shard / chunk boundary, every rank's inputs
-    # gathered to rank 0 (one more step first: `out` then holds srcs' result)
-    set_stage("oracle parity check of the timed engine")
-    step()
-    torch.cuda.synchronize()
-    parity = oracle_check(srcs, out, oracle_lanes(n, world, chunks, 1 << 20), k, rank, world)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for _ in range(a.steps):
+            step()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        barrier()
+        wall = time.perf_counter() - t0
+        dev_ms = ev0.elapsed_time(ev1)
+        wall = agree([wall], world)[0]
+        # the timed steps' output against the reference engine's (N>1): the last
+        # timed step's output, then four more steps alternating the two input
+        # sets, each against the reference engine's results
+        verified = None
+        if refs[0] is not None:
+            set_stage(f"verification of the timed engine {eng}")
+            bad = 0 if torch.equal(out, refs[0][0]) else 1
+            for i in range(4):
+                comm.allreduce_f32(srcs_b if i % 2 == 0 else srcs, out=out, scale_exp=k, chunks=ch,
+                                   stream=stream.cuda_stream)
+                torch.cuda.synchronize()
+                bad += 0 if torch.equal(out, refs[0][(i + 1) % 2]) else 1
+            verified = agree([float(bad)], world)[0] == 0.0
+        # the timed path's result against the oracle on a lane sample: 2^20
+        # strided lanes plus both sides of every shard / chunk boundary, every
+        # rank's inputs gathered to rank 0 (one more step first: `out` then holds
+        # srcs' result)
+        set_stage(f"oracle parity check of the timed engine {eng if world > 1 else 'fused'}")
+        step()
+        torch.cuda.synchronize()
+        parity = oracle_check(srcs, out, oracle_lanes(n, world, ch, 1 << 20), k, rank, world)
+        for key in env:
+            os.environ.pop(key, None)
+        return {"engine": eng if world > 1 else "fused", "chunks": ch, "env": env, "ms_per_step": wall * 1e3 / a.steps,
+                "settle_steps": settle_steps, "dev_ms": dev_ms, "verified": verified, "parity": parity}
 
-    # dominant kernel alone: fused (N=1) or quant + local sum (N>1), HIP events on its stream
-    set_stage("dominant-kernel timing")
-    kstream = torch.cuda.Stream(device=dev)
-    qbuf = torch.empty(n, device=dev, dtype=torch.int32) if world > 1 else None
+    # dominant kernel alone: fused (N=1) or quant + local sum (N>1), HIP events
+    # on its stream; timed once, right after the first headline measurement
+    kinfo = {}
 
-    def kernel():
+    def dominant_kernel():
+        set_stage("dominant-kernel timing")
+        kstream = torch.cuda.Stream(device=dev)
+        qbuf = torch.empty(n, device=dev, dtype=torch.int32) if world > 1 else None
+
+        def kernel():
+            if world == 1:
+                inccl.reduce_f32(srcs, k, out=out, stream=kstream.cuda_stream)
+            else:
+                inccl.quant_sum(srcs, k, out=qbuf, stream=kstream.cuda_stream)
+
+        k_ms = kernel_time_ms(kernel, kstream, max(a.steps, 20))
+        del qbuf
+        alg_bytes = (R + 1) * 4 * n
+        achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+        kname = "k_stream_vec<F32,F32,R>" if world == 1 else "k_stream_vec<F32,Q32,R>"
+        traffic, traffic_round = load_traffic(kname + f" R={R} n={n}")
+        hbm = {
+            "kernel": kname,
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": ("profiles/pmc_traffic.json: separate rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and "
+                               f"WRITE_SIZE passes over this kernel and size, recorded in round {traffic_round} "
+                               "(not re-measured in this run)")
+            if traffic is not None else None,
+            "alg_bytes_per_launch": alg_bytes,
+            "kernel_ms": round(k_ms, 5),
+        }
         if world == 1:
-            inccl.reduce_f32(srcs, k, out=out, stream=kstream.cuda_stream)
-        else:
-            inccl.quant_sum(srcs, k, out=qbuf, stream=kstream.cuda_stream)
+            # the same kernel rotating through 4 input/output sets (3 GiB, far past
+            # the 256 MiB Infinity Cache): `frac` re-reads the same buffers every
+            # launch, `frac_cold` cannot find them on die
+            set_stage("cold (rotated-set) kernel timing")
+            cold = cold_run(dev, R, k, n)
+            hbm["frac_cold"] = cold["frac"]
+            hbm["achieved_cold"] = cold["achieved"]
+            hbm["kernel_ms_cold"] = round(cold["kernel_us"] * 1e-3, 5)
+            kinfo["cold"] = cold
+        kinfo["hbm"] = hbm
 
-    k_ms = kernel_time_ms(kernel, kstream, max(a.steps, 20))
-    alg_bytes = (R + 1) * 4 * n
-    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
     per_rank = f"R={R} resident {a.bucket_mib} MiB fp32 buckets per rank: "
-    workload = (f"fused quantise+sum+dequantise of R={R} resident {a.bucket_mib} MiB fp32 buckets, 1 GPU"
-                if world == 1 else per_rank + {
-                    "rccl": f"quant+local sum -> RCCL reduce-scatter int32 -> dequant shard -> RCCL all-gather fp32, "
-                            f"{chunks} pipelined chunks",
-                    "ar": "quant+local sum -> RCCL all-reduce int32 in place -> dequant",
-                    "a2a": "quant+local sum -> RCCL all-to-all of int32 shards -> fused sum+dequant (HIP) -> RCCL "
-                           "all-gather fp32",
-                    "p2p": "quant+local sum -> p2p pull of every peer's shard over xGMI with fused sum+dequant -> p2p "
-                           "gather of every result shard",
-                    "mesh": "one persistent HIP kernel: per-chunk quant+local sum pushed into the owner's inbox over "
-                            "xGMI -> owner's sum+dequant on arrival flags -> pull of every result chunk",
-                    "meshw": "one persistent HIP kernel: per-chunk quant+local sum pushed into the owner's inbox over "
-                             "xGMI -> owner's sum+dequant on arrival flags, result chunk pushed into every rank's "
-                             "inbox (all xGMI transfers are writes) -> local copy into dst",
-                }.get(comm.engine, comm.engine))
-    kname = "k_stream_vec<F32,F32,R>" if world == 1 else "k_stream_vec<F32,Q32,R>"
-    traffic, traffic_round = load_traffic(kname + f" R={R} n={n}")
-    hbm_roofline = {
-        "kernel": kname,
-        "bound": "hbm",
-        "achieved": round(achieved, 1),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": traffic,
-        "traffic_source": ("profiles/pmc_traffic.json: separate rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and "
-                           f"WRITE_SIZE passes over this kernel and size, recorded in round {traffic_round} "
-                           "(not re-measured in this run)")
-        if traffic is not None else None,
-        "alg_bytes_per_launch": alg_bytes,
-        "kernel_ms": round(k_ms, 5),
-    }
-    if world == 1:
-        # the same kernel rotating through 4 input/output sets (3 GiB, far past
-        # the 256 MiB Infinity Cache): `frac` re-reads the same buffers every
-        # launch, `frac_cold` cannot find them on die
-        set_stage("cold (rotated-set) kernel timing")
-        cold = cold_run(dev, R, k, n)
-        hbm_roofline["frac_cold"] = cold["frac"]
-        hbm_roofline["achieved_cold"] = cold["achieved"]
-        hbm_roofline["kernel_ms_cold"] = round(cold["kernel_us"] * 1e-3, 5)
 
-    value = world * R * n * 4 / (ms_per_step * 1e-3) / 1e9
-    res = {
-        "metric": "GB/s device-resident fp32 bucket quantise+reduce, 256 MiB, 1/2/4/8 GPUs",
-        "value": round(value, 2),
-        "unit": "GB/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(ms_per_step, 4),
-        "settle_steps": settle_steps,
-        "device_ms_per_step_rank0": round(dev_ms / a.steps, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "int32",
-        "data": "synthetic N(0,1) fp32 buckets, torch.Generator seed 1000+rank",
-        "config": {
-            "workload": workload,
-            "bucket_mib": a.bucket_mib,
-            "local_buckets": R,
-            "scale_exp": k,
-            "numerics": f"fp32 in/out; quantised to int32 fixed point 2^-{k}; int32 wrap-around sum (exact)",
-            "parallelism": f"dp{world}",
-            "chunks": chunks,
-            "engine": comm.engine if world > 1 else "fused",
-            "engine_env": (chosen[2] or None) if world > 1 else None,
-            "engine_tuning": tuning or None,
-            "shard_elems": chunk_plan(n, world, chunks)[0][2] if world > 1 else n,
-        },
-        # N = 1: the fused kernel's HBM roofline.  N > 1: the step is bound by the
-        # xGMI links, so `roofline` is the link fraction of the whole step and the
-        # dominant HBM kernel's figure moves to `roofline_hbm_kernel`.
-        "roofline": hbm_roofline if world == 1 else xgmi_roofline(world, n * 4, ms_per_step * 1e-3),
-        "cpu_baseline": None,
-        "parity_vs_oracle": parity,
-        # the HIP / HSA / RCCL copies this rank is bound to (DESIGN.md "Runtimes")
-        "runtime": runtime_libs(),
-    }
-    if world == 1:
-        res["roofline_cold"] = cold
-    if world > 1:
-        res["roofline_hbm_kernel"] = hbm_roofline
-        res["verified_vs_reference_engine"] = verified
-        # nccl-tests convention (BASELINE config 4): algbw = one rank's bucket bytes
-        # / step time; busbw = algbw * 2(W-1)/W, the per-GPU link traffic of RS + AG
-        algbw = n * 4 / (ms_per_step * 1e-3) / 1e9
-        res["collective"] = {"algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2),
-                             "bytes_per_rank": n * 4}
+    def build_res(m: dict) -> dict:
+        """The JSON line of one headline measurement."""
+        ms_per_step, chunks = m["ms_per_step"], m["chunks"]
+        workload = (f"fused quantise+sum+dequantise of R={R} resident {a.bucket_mib} MiB fp32 buckets, 1 GPU"
+                    if world == 1 else per_rank + {
+                        "rccl": f"quant+local sum -> RCCL reduce-scatter int32 -> dequant shard -> RCCL all-gather "
+                                f"fp32, {chunks} pipelined chunks",
+                        "ar": "quant+local sum -> RCCL all-reduce int32 in place -> dequant",
+                        "a2a": "quant+local sum -> RCCL all-to-all of int32 shards -> fused sum+dequant (HIP) -> RCCL "
+                               "all-gather fp32",
+                        "p2p": "quant+local sum -> p2p pull of every peer's shard over xGMI with fused sum+dequant -> "
+                               "p2p gather of every result shard",
+                        "mesh": "one persistent HIP kernel: per-chunk quant+local sum pushed into the owner's inbox "
+                                "over xGMI -> owner's sum+dequant on arrival flags -> pull of every result chunk",
+                        "meshw": "one persistent HIP kernel: per-chunk quant+local sum pushed into the owner's inbox "
+                                 "over xGMI -> owner's sum+dequant on arrival flags, result chunk pushed into every "
+                                 "rank's inbox (all xGMI transfers are writes) -> local copy into dst",
+                    }.get(m["engine"], m["engine"]))
+        value = world * R * n * 4 / (ms_per_step * 1e-3) / 1e9
+        res = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "settle_steps": m["settle_steps"],
+            "device_ms_per_step_rank0": round(m["dev_ms"] / a.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic N(0,1) fp32 buckets, torch.Generator seed 1000+rank",
+            "config": {
+                "workload": workload,
+                "bucket_mib": a.bucket_mib,
+                "local_buckets": R,
+                "scale_exp": k,
+                "numerics": f"fp32 in/out; quantised to int32 fixed point 2^-{k}; int32 wrap-around sum (exact)",
+                "parallelism": f"dp{world}",
+                "chunks": chunks,
+                "engine": m["engine"],
+                "engine_env": (m["env"] or None) if world > 1 else None,
+                "engine_tuning": tuning or None,
+                "shard_elems": chunk_plan(n, world, chunks)[0][2] if world > 1 else n,
+            },
+            # N = 1: the fused kernel's HBM roofline.  N > 1: the step is bound by
+            # the xGMI links, so `roofline` is the link fraction of the whole step
+            # and the dominant HBM kernel's figure moves to `roofline_hbm_kernel`.
+            "roofline": kinfo["hbm"] if world == 1 else xgmi_roofline(world, n * 4, ms_per_step * 1e-3),
+            "cpu_baseline": None,
+            "parity_vs_oracle": m["parity"],
+            # the HIP / HSA / RCCL copies this rank is bound to (DESIGN.md "Runtimes")
+            "runtime": runtime_libs(),
+        }
+        if world == 1:
+            res["roofline_cold"] = kinfo["cold"]
+        if world > 1:
+            res["roofline_hbm_kernel"] = kinfo["hbm"]
+            res["verified_vs_reference_engine"] = m["verified"]
+            # nccl-tests convention (BASELINE config 4): algbw = one rank's bucket
+            # bytes / step time; busbw = algbw * 2(W-1)/W, the per-GPU link traffic
+            # of RS + AG
+            algbw = n * 4 / (ms_per_step * 1e-3) / 1e9
+            res["collective"] = {"algbw_GBps": round(algbw, 2),
+                                 "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2), "bytes_per_rank": n * 4}
+        return res
+
     # The one JSON line, printed once: by the main thread at the end, or by the
     # watchdog (with the stage it was stuck in, exit code 3) if the run overruns
-    # its budget -- from here on that line carries the measured headline.
+    # its budget, or by the line keeper if rank 0 dies -- from the first headline
+    # measurement on, that line carries a measured headline (RESULT[0]).
     emit_lock, emitted = threading.Lock(), [False]
 
     def emit():
@@ -1257,6 +1295,7 @@ def main():
             if emitted[0]:
                 return False
             emitted[0] = True
+        res = RESULT[0]
         res["elapsed_s"] = round(time.monotonic() - T_START, 1)
         if rank == 0:
             line = json.dumps(dict(res))   # a snapshot: the watchdog may emit while the main thread works
@@ -1269,12 +1308,56 @@ def main():
         return True
 
     def on_overrun(msg):
-        res["error"] = msg + "; headline measured and kept, later keys partial"
+        RESULT[0]["error"] = msg + "; headline measured and kept, later keys partial"
         emit()
 
-    watchdog.on_fire = on_overrun
-    RESULT[0] = res
-    set_stage("headline measured")
+    def publish(res: dict, stage: str) -> None:
+        """From now on every way the run can end prints `res`."""
+        RESULT[0] = res
+        watchdog.on_fire = on_overrun
+        set_stage(stage)
+
+    measured = []   # (measurement, line) per headline measurement, in order
+    if world == 1:
+        m = measure("fused", 1, {})
+        dominant_kernel()
+        measured.append((m, build_res(m)))
+        publish(measured[-1][1], "headline measured")
+    else:
+        best1 = tune(phases[0], 1)
+        if best1 is not None:
+            m = measure(best1[1], best1[2], best1[3])
+            dominant_kernel()
+            measured.append((m, build_res(m)))
+            publish(measured[-1][1], f"headline measured on {m['engine']}; phase 2 (IPC engines) next")
+        if os.environ.get("INCCL_BENCH_TEST_DIE") == "phase2" and rank == 0:   # test hook: rank 0 dies in phase 2
+            import signal
+            os.kill(os.getpid(), signal.SIGKILL)
+        best2 = tune(phases[1], 2)
+        if best2 is not None and (best1 is None or best2[0] < best1[0]):
+            m = measure(best2[1], best2[2], best2[3])
+            if not kinfo:
+                dominant_kernel()
+            line = build_res(m)
+            # a phase-2 headline replaces phase 1's only if it was verified like it
+            ok = m["verified"] is not False and (m["parity"]["mismatches"] or 0) == 0
+            if agree([0.0 if ok else 1.0], world)[0] == 0.0:
+                measured.append((m, line))
+        if not measured:
+            raise SystemExit("no exchange engine produced verified results on every rank")
+        # the faster measured headline is the line; every measured one is listed
+        best = min(measured, key=lambda x: x[0]["ms_per_step"])
+        best[1]["config"]["engine_tuning"] = tuning or None
+        best[1]["headline_candidates"] = [
+            {"engine": mm["engine"], "chunks": mm["chunks"], "env": mm["env"] or None,
+             "ms_per_step": round(mm["ms_per_step"], 4), "value": ln["value"],
+             "verified_vs_reference_engine": mm["verified"], "oracle_mismatches": mm["parity"]["mismatches"]}
+            for mm, ln in measured]
+        publish(best[1], "headline measured")
+        comm.set_engine(best[0]["engine"])
+        os.environ.update(best[0]["env"])
+    res = RESULT[0]
+    chosen = ("fused", 1, {}) if world == 1 else (best[0]["engine"], best[0]["chunks"], dict(best[0]["env"]))
     if os.environ.get("INCCL_BENCH_TEST_DIE") == "1" and rank == 0:   # test hook: rank 0 dies after the headline
         import signal
         os.kill(os.getpid(), signal.SIGKILL)
