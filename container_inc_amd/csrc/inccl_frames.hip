@@ -694,6 +694,22 @@ __device__ void header_crcs(EgressLds& t, const uint8_t (*himg)[kHdrImg], int fa
     if (i < 2 * fan && s == 0) t.hcrc[i] = r;
 }
 
+// The CRC tables, the 2 * fan_in header images and their constant ICRC terms
+// into the block's LDS (ends with a block barrier).  Blocks of 8 waves: quad
+// q of wave w computes header term 16 w + q (2 * 31 at most).
+__device__ void egress_setup(EgressLds& t, uint8_t (*himg)[kHdrImg], const InccFrameTemplate* __restrict__ tmpl, int fan,
+                             int w, int lane)
+{
+    for (int i = threadIdx.x; i < kSeg * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg[0][0][0])[i];
+    for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) (&t.lane16[0][0][0])[i] = (&g_lane16[0][0][0])[i];
+    for (int i = threadIdx.x; i < 2 * kVarBytes * 2 * 16; i += blockDim.x) (&t.var[0][0][0][0])[i] = (&g_var[0][0][0][0])[i];
+    for (int i = threadIdx.x; i < 8 * 16; i += blockDim.x) (&t.z1024[0][0])[i] = (&g_z1024[0][0])[i];
+    for (int i = threadIdx.x; i < 2 * fan; i += blockDim.x) build_header_image(himg[i], tmpl[i >> 1], (i & 1) != 0);
+    __syncthreads();
+    header_crcs(t, himg, fan, w, lane);
+    __syncthreads();
+}
+
 // Every output frame of input frame f (rows f * fan_in + c): all fan_in children
 // on COMPLETED (the broadcast, nts.c:368-371), the sender's child on REPLAY
 // (nts.c:353-356).
@@ -824,16 +840,8 @@ __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState 
     __shared__ EgressLds t;
     __shared__ __attribute__((aligned(16))) uint8_t buf[kEgressWaves][80];   // per wave: header chunks
     __shared__ __attribute__((aligned(16))) uint8_t himg[2 * 31][kHdrImg];
-    for (int i = threadIdx.x; i < kSeg * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg[0][0][0])[i];
-    for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) (&t.lane16[0][0][0])[i] = (&g_lane16[0][0][0])[i];
-    for (int i = threadIdx.x; i < 2 * kVarBytes * 2 * 16; i += blockDim.x) (&t.var[0][0][0][0])[i] = (&g_var[0][0][0][0])[i];
-    for (int i = threadIdx.x; i < 8 * 16; i += blockDim.x) (&t.z1024[0][0])[i] = (&g_z1024[0][0])[i];
-    const int fan = s.fan_in;
-    for (int i = threadIdx.x; i < 2 * fan; i += blockDim.x) build_header_image(himg[i], tmpl[i >> 1], (i & 1) != 0);
-    __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
-    header_crcs(t, himg, fan, w, lane);
-    __syncthreads();
+    egress_setup(t, himg, tmpl, s.fan_in, w, lane);
     const bool out16 = ((out_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
     // Round r covers frames [r * step, (r + 1) * step); in round r this wave
     // takes frame r * step + (wave + r) mod step.  Rotating the offset by one per
@@ -862,6 +870,163 @@ __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState 
         fn = next();
         if (fn < count) a = egress_fetch(s, in_frames, in_stride, ports, action, psns, fn, lane);
         egress_emit(s, b, himg, out, out_stride, out16, out_len, t, buf[w], f, lane);
+        f = fn;
+        if (f >= count) break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Egress with a fixed fan-in (2, 3, 4 or 8): the same frames as k_egress, with
+// every frame issuing the same global-memory instructions.
+//
+// gfx9 counts loads and stores on one counter (vmcnt), retired in issue order.
+// The compiler waits for a loaded value with "vmcnt <= number of memory
+// instructions issued after it" -- and where paths that issue different numbers
+// of stores join (an absorbed frame returns early, a REPLAY emits one child, a
+// COMPLETED fan_in), it can only wait conservatively.  k_egress's ISA shows
+// vmcnt(0) at the top of every frame: it waits for the previous frame's stores
+// AND for the next frame's prefetch, which then hides nothing.  Here the
+// children loop is unrolled, the loads are unconditional (the last frame is
+// re-read past the end), all CRC work sits in branches without memory
+// instructions, and every store is predicated on the lane (exec mask), not
+// branched around.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int opaque(int v)
+{
+    // a value the compiler cannot prove wave-uniform: a predicate on it compiles
+    // to an exec mask, not to a branch around the store
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+template <int kFan, bool kOut16>
+__device__ __forceinline__ void egress_emit_fixed(const EgressIn& e, const uint8_t (*himg)[kHdrImg],
+                                                  uint8_t* __restrict__ out, int64_t out_stride,
+                                                  int32_t* __restrict__ out_len, const EgressLds& t, uint8_t* hbuf,
+                                                  int64_t f, int lane)
+{
+    const bool all = e.act == INCCL_SW_COMPLETED;
+    const bool one = e.act == INCCL_SW_REPLAY && e.port >= 0 && e.port < kFan;
+    const uint32_t op = (uint32_t)__shfl((int)e.op, 2, kWave) & 0xFFu;
+    const int wf = is_write_first((uint8_t)op) ? 1 : 0;
+    const int doff = 54 + 16 * wf;
+    const int hchunks = doff / 16 + 1;
+    const int total = doff + kLanes * 4 + 4;   // util.c:341-345
+    if (lane < kFan) out_len[f * kFan + lane] = (all || (one && lane == e.port)) ? total : 0;
+    uint32_t a[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = __builtin_bswap32((uint32_t)e.agg[k]);
+    uint32_t nx[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) nx[k] = (uint32_t)__shfl_down((int)a[k], 1, kWave);
+    const uint32_t pc0 = __builtin_amdgcn_alignbyte(a[3], a[2], 2);
+    const uint32_t pc1 = __builtin_amdgcn_alignbyte(nx[0], a[3], 2);
+    const uint32_t pc2 = __builtin_amdgcn_alignbyte(nx[1], nx[0], 2);
+    const uint32_t pc3 = __builtin_amdgcn_alignbyte(nx[2], nx[1], 2);
+    const uint32_t pw = e.psn | 0x80000000u;
+    uint32_t pc = 0;
+    if (all || one) {
+        const uint32_t a0 = (uint32_t)__shfl((int)a[0], 0, kWave), a1 = (uint32_t)__shfl((int)a[1], 0, kWave);
+        const uint32_t a2 = (uint32_t)__shfl((int)a[2], 0, kWave);
+        if (lane == 0) *reinterpret_cast<uint16_t*>(hbuf + doff) = (uint16_t)a0;
+        if (lane == 1) *reinterpret_cast<uint32_t*>(hbuf + doff + 2) = __builtin_amdgcn_alignbyte(a1, a0, 2);
+        if (lane == 2) *reinterpret_cast<uint32_t*>(hbuf + doff + 6) = __builtin_amdgcn_alignbyte(a2, a1, 2);
+        uint32_t pv = seg16_crc(t, a, lane);
+        if (lane < 5) {
+            const uint32_t b = lane == 0 ? op : (pw >> (8 * (4 - lane))) & 0xFFu;
+            pv ^= var_crc(t, wf, lane, b);
+        }
+        pc = wave_xor(pv);
+    }
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int c = 0; c < kFan; ++c) {
+        const bool act_c = all || (one && c == e.port);
+        uint32_t crc = 0;
+        if (act_c) {
+            uint32_t r = 0, rk = 0;
+            if (wf) {
+                r = (uint32_t)__shfl((int)e.reth, 4 * c + (lane & 3), kWave);
+                rk = (uint32_t)__shfl((int)r, lane >> 2, kWave);
+            }
+            uint32_t vr = 0;
+            if (wf) vr = wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
+            crc = ~(pc ^ t.hcrc[2 * c + wf] ^ vr);   // util.c:424-426
+            if (lane < 13) {
+                uint32_t hw = reinterpret_cast<const uint32_t*>(himg[2 * c + wf])[lane];
+                if (lane == 10) hw = (hw & 0xFF00FFFFu) | (op << 16);
+                if (lane == 12) hw = (hw & 0x0000FFFFu) | ((pw >> 24) << 16) | (((pw >> 16) & 0xFFu) << 24);
+                reinterpret_cast<uint32_t*>(hbuf)[lane] = hw;
+            } else if (lane == 13) {
+                *reinterpret_cast<uint16_t*>(hbuf + 52) = (uint16_t)(((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8));
+            }
+            if (wf) {                                                   // util.c:409-417: bytes 54-69
+                const int k = lane - 14;
+                const uint32_t rlo = (uint32_t)__shfl((int)r, (k - 1) & 3, kWave);
+                const uint32_t rhi = (uint32_t)__shfl((int)r, k & 3, kWave);
+                if (k == 0) *reinterpret_cast<uint16_t*>(hbuf + 54) = (uint16_t)rhi;
+                else if (k >= 1 && k <= 3) *reinterpret_cast<uint32_t*>(hbuf + 52 + 4 * k) = __builtin_amdgcn_alignbyte(rhi, rlo, 2);
+                else if (k == 4) *reinterpret_cast<uint16_t*>(hbuf + 68) = (uint16_t)(rlo >> 16);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint8_t* o = out + (f * kFan + c) * out_stride;
+        const int lim_h = opaque(act_c ? hchunks : 0), lim_p = opaque(act_c ? kWave : 0);
+        const u4 h = reinterpret_cast<const u4*>(hbuf)[lane < 5 ? lane : 0];   // 5 chunks at most
+        const u4 v = lane < kWave - 1 ? u4{pc0, pc1, pc2, pc3}
+                                      : u4{pc0, (a[3] >> 16) | ((crc & 0xFFFFu) << 16), crc >> 16, 0u};
+        if (kOut16) {
+            if (lane < lim_h) reinterpret_cast<u4*>(o)[lane] = h;
+            if (lane < lim_p) reinterpret_cast<u4*>(o)[hchunks + lane] = v;
+        } else {
+            uint32_t* oh = reinterpret_cast<uint32_t*>(o) + 4 * lane;
+            if (lane < lim_h) { oh[0] = h.x; oh[1] = h.y; oh[2] = h.z; oh[3] = h.w; }
+            uint32_t* op32 = reinterpret_cast<uint32_t*>(o) + 4 * (hchunks + lane);
+            if (lane < lim_p) { op32[0] = v.x; op32[1] = v.y; op32[2] = v.z; }
+            if (lane < (lim_p < kWave - 1 ? lim_p : kWave - 1)) op32[3] = v.w;   // lane 63 stops at the frame's end
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+template <int kFan, bool kOut16>
+__global__ __launch_bounds__(kWave* kEgressWaves) void k_egress_fixed(InccSwitchState s,
+                                                                      const uint8_t* __restrict__ in_frames,
+                                                                      int64_t in_stride, int64_t count,
+                                                                      const int32_t* __restrict__ ports,
+                                                                      const int32_t* __restrict__ action,
+                                                                      const uint32_t* __restrict__ psns,
+                                                                      const InccFrameTemplate* __restrict__ tmpl,
+                                                                      uint8_t* __restrict__ out, int64_t out_stride,
+                                                                      int32_t* __restrict__ out_len)
+{
+    __shared__ EgressLds t;
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kEgressWaves][80];
+    __shared__ __attribute__((aligned(16))) uint8_t himg[2 * 31][kHdrImg];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    egress_setup(t, himg, tmpl, kFan, w, lane);
+    // the rotation of k_egress; frames past the end re-read the last one (a fixed
+    // instruction stream) and are never emitted
+    const int64_t step = (int64_t)gridDim.x * kEgressWaves;
+    int64_t rot = (int64_t)blockIdx.x * kEgressWaves + w, base = 0;
+    int64_t f = rot;
+    if (f >= count) return;
+    auto next = [&]() {
+        base += step;
+        rot = rot + 1 == step ? 0 : rot + 1;
+        return base + rot;
+    };
+    auto clamp = [&](int64_t x) { return x < count ? x : count - 1; };
+    EgressIn a = egress_fetch(s, in_frames, in_stride, ports, action, psns, f, lane), b;
+    for (;;) {
+        int64_t fn = next();
+        b = egress_fetch(s, in_frames, in_stride, ports, action, psns, clamp(fn), lane);
+        egress_emit_fixed<kFan, kOut16>(a, himg, out, out_stride, out_len, t, buf[w], f, lane);
+        f = fn;
+        if (f >= count) break;
+        fn = next();
+        a = egress_fetch(s, in_frames, in_stride, ports, action, psns, clamp(fn), lane);
+        egress_emit_fixed<kFan, kOut16>(b, himg, out, out_stride, out_len, t, buf[w], f, lane);
         f = fn;
         if (f >= count) break;
     }
@@ -1059,9 +1224,35 @@ int inccl_k_switch_egress(const InccSwitchState* s, const uint8_t* in_frames, si
     const int64_t need = ((int64_t)count + kEgressWaves - 1) / kEgressWaves;
     const int64_t cap = (int64_t)num_cus() * blocks_per_cu("INCCL_EGRESS_BLOCKS_PER_CU", 3);
     const int eg = (int)(need < cap ? (need < 1 ? 1 : need) : cap);
-    hipLaunchKernelGGL(k_egress, dim3(eg), dim3(kWave * kEgressWaves), 0, st, *s,
-                       in_frames, (int64_t)in_stride, (int64_t)count, ports, action, psns, tmpl, out,
-                       (int64_t)out_stride, out_len);
+    // fan-in 2, 3, 4, 8: the straight-line kernel (k_egress_fixed); others, or
+    // $INCCL_EGRESS_GENERIC=1 (A/B), the generic one
+    static const bool generic = [] {
+        const char* e = getenv("INCCL_EGRESS_GENERIC");
+        return e && atoi(e) != 0;
+    }();
+    const bool o16 = ((out_stride & 15) == 0) && (((uintptr_t)out & 15) == 0);
+    const dim3 g(eg), b(kWave * kEgressWaves);
+    const int64_t is = (int64_t)in_stride, os = (int64_t)out_stride, n = (int64_t)count;
+#define INCCL_EGRESS_FIXED(F)                                                                                   \
+    case F:                                                                                                     \
+        if (o16)                                                                                                \
+            hipLaunchKernelGGL((k_egress_fixed<F, true>), g, b, 0, st, *s, in_frames, is, n, ports, action, psns, \
+                               tmpl, out, os, out_len);                                                         \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_egress_fixed<F, false>), g, b, 0, st, *s, in_frames, is, n, ports, action,      \
+                               psns, tmpl, out, os, out_len);                                                   \
+        return (int)hipGetLastError();
+    if (!generic) {
+        switch (s->fan_in) {
+            INCCL_EGRESS_FIXED(2)
+            INCCL_EGRESS_FIXED(3)
+            INCCL_EGRESS_FIXED(4)
+            INCCL_EGRESS_FIXED(8)
+        default: break;
+        }
+    }
+#undef INCCL_EGRESS_FIXED
+    hipLaunchKernelGGL(k_egress, g, b, 0, st, *s, in_frames, is, n, ports, action, psns, tmpl, out, os, out_len);
     return (int)hipGetLastError();
 }
 
