@@ -89,7 +89,9 @@ def _expected_frame(orc, t, c, agg, psn, op, reth):
 # 20 children: RETH words of children 16+ are loaded directly, not shuffled from the prefetch.
 # Stride 1100 (4-byte but not 16-byte aligned rows): ingress's 2-byte payload
 # loads and egress's dword stores instead of the 16-byte paths.
-@pytest.mark.parametrize("fan_in,stride", [(2, STRIDE), (3, STRIDE), (8, STRIDE), (20, STRIDE), (2, 1100), (8, 1100)])
+# Fan-in 2, 3, 4 and 8 take the straight-line egress (k_egress_fixed), others the generic one.
+@pytest.mark.parametrize("fan_in,stride", [(2, STRIDE), (3, STRIDE), (4, STRIDE), (8, STRIDE), (20, STRIDE), (2, 1100),
+                                           (4, 1100), (8, 1100), (5, 1100)])
 def test_switch_batches(gpu, orc, fan_in, stride):
     import torch
     from container_inc_amd import inccl
@@ -178,7 +180,7 @@ def test_switch_rejects_bad_frames(gpu, orc):
 # the per-round rotation of each wave's frame offset wrapping.  Every emitted
 # row is checked (length, payload = htonl of the wrap-around sum, ICRC), and a
 # sample of rows including the batch's last ones byte-exact against the oracle.
-@pytest.mark.parametrize("fan_in,P", [(2, 40000), (3, 21111)])
+@pytest.mark.parametrize("fan_in,P", [(2, 40000), (3, 21111), (4, 9999)])
 def test_switch_large_batch_all_frames(gpu, orc, fan_in, P):
     import torch
     from container_inc_amd import inccl
