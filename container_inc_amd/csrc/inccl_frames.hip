@@ -343,7 +343,7 @@ __device__ __forceinline__ void payload16(const uint8_t* fr, uint32_t wf, int la
 }
 
 template <int kApplyFrames>
-__global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwitchState s,
+__global__ __launch_bounds__(kWave * 16) void k_ingress_apply(InccSwitchState s,
                                                                          const uint8_t* __restrict__ frames,
                                                                          int64_t stride, int64_t count,
                                                                          const int32_t* __restrict__ ports,
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void k_ingress_apply(InccSwi
                                                                          const uint32_t* __restrict__ psns, bool wide)
 {
     const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    const int64_t f0 = ((int64_t)blockIdx.x * kWavesPerBlock + w) * kApplyFrames;
+    const int64_t f0 = ((int64_t)blockIdx.x * (blockDim.x / kWave) + w) * kApplyFrames;
     if (f0 >= count) return;
     const int fan = s.fan_in;
     const uint32_t tag = ~s.gen, result_bit = 1u << fan;
@@ -1175,9 +1175,20 @@ int blocks_per_cu(const char* env, int dflt)
     return (v >= 1 && v <= 3) ? v : dflt;
 }
 
+// waves per apply workgroup: 4 by default, $INCCL_APPLY_WPB = 1, 2, 8 or 16 for sweeps
+int apply_wpb()
+{
+    static const int v = [] {
+        const char* e = getenv("INCCL_APPLY_WPB");
+        const int x = e ? atoi(e) : kWavesPerBlock;
+        return (x == 1 || x == 2 || x == 4 || x == 8 || x == 16) ? x : kWavesPerBlock;
+    }();
+    return v;
+}
+
 inline int grid_for(int64_t waves)
 {
-    const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int64_t blocks = (waves + apply_wpb() - 1) / apply_wpb();
     return (int)(blocks < 1 ? 1 : blocks);
 }
 
@@ -1231,19 +1242,19 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
     }();
     const int64_t waves = ((int64_t)count + apply_frames - 1) / apply_frames;
     if (apply_frames == 1)
-        hipLaunchKernelGGL(k_ingress_apply<1>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
+        hipLaunchKernelGGL(k_ingress_apply<1>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
                            (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
     else if (apply_frames == 4)
-        hipLaunchKernelGGL(k_ingress_apply<4>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
+        hipLaunchKernelGGL(k_ingress_apply<4>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
                            (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
     else if (apply_frames == 2)
-        hipLaunchKernelGGL(k_ingress_apply<2>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
+        hipLaunchKernelGGL(k_ingress_apply<2>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
                            (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
     else if (apply_frames == 8)
-        hipLaunchKernelGGL(k_ingress_apply<8>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
+        hipLaunchKernelGGL(k_ingress_apply<8>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
                            (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
     else
-        hipLaunchKernelGGL(k_ingress_apply<2>, dim3(grid_for(waves)), dim3(kWave * kWavesPerBlock), 0, st, *s, frames,
+        hipLaunchKernelGGL(k_ingress_apply<2>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
                            (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
     hipLaunchKernelGGL(k_ingress_commit, lanes, dim3(kClaimBlock), 0, st, *s, (int64_t)count, ports, action, psn_out);
     return (int)hipGetLastError();
