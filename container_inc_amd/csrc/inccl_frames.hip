@@ -39,7 +39,6 @@ constexpr int kWin = 1088;            // 64 lanes x 17 bytes
 constexpr int kSeg = 17;
 constexpr int kFrameMax = 1152;       // staged frame bytes (>= 1098)
 constexpr int kWavesPerBlock = 4;
-constexpr int kIcrcWaves = 8;        // 512-lane blocks, three per CU (43 KiB of LDS each)
 constexpr int kEgressWaves = 8;       // 512-lane blocks, two per CU, persistent grid
 constexpr int kLanes = 256;           // int32 lanes per packet (nts.c:55)
 
@@ -82,6 +81,23 @@ __device__ __forceinline__ int masked_pos(int i)
     return i < 8 ? (int)((lo >> (8 * i)) & 0xFF) : (int)((hi >> (8 * (i - 8))) & 0xFF);
 }
 
+// a value whose bits the compiler may not reason about: keeps a nibble plane's
+// byte extracts as byte extracts (one SDWA select each) instead of folding them
+// back into a shift + mask of the original word
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t v)
+{
+    asm("" : "+v"(v));
+    return v;
+}
+
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // ICRC of the frame staged at `fr` (LDS, at least 1152 B, 4-B aligned), whose
 // masked bytes are already 0xFF; result valid in every lane.
 template <bool kByte>
@@ -121,18 +137,30 @@ __device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds<kByte>& t, int lan
             }
             c ^= t.seg[16 * 256 + (a[4] & 0xFFu)];
         } else {
+            // nibble planes: byte b of lo / hi is the low / high nibble of byte b,
+            // so each lookup's index is one SDWA byte select; XOR three at a time
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
+                const uint32_t lo = opaque_u32(a[k] & 0x0F0F0F0Fu), hi = opaque_u32((a[k] >> 4) & 0x0F0F0F0Fu);
+                uint32_t v[8];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) c ^= t.seg[((4 * k + (i >> 1)) * 2 + (i & 1)) * 16 + ((a[k] >> (4 * i)) & 15u)];
+                for (int b = 0; b < 4; ++b) {
+                    v[2 * b] = t.seg[((4 * k + b) * 2) * 16 + (uint8_t)(lo >> (8 * b))];
+                    v[2 * b + 1] = t.seg[((4 * k + b) * 2 + 1) * 16 + (uint8_t)(hi >> (8 * b))];
+                }
+                c = xor3(xor3(xor3(c, v[0], v[1]), v[2], v[3]), xor3(v[4], v[5], v[6]), v[7]);
             }
-            c ^= t.seg[(16 * 2) * 16 + (a[4] & 15u)] ^ t.seg[(16 * 2 + 1) * 16 + ((a[4] >> 4) & 15u)];
+            c = xor3(c, t.seg[(16 * 2) * 16 + (a[4] & 15u)], t.seg[(16 * 2 + 1) * 16 + ((a[4] >> 4) & 15u)]);
         }
         // shift to the window's end: Z_{17 (63 - lane)}(c)
-        uint32_t r = 0;
+        const uint32_t clo = opaque_u32(c & 0x0F0F0F0Fu), chi = opaque_u32((c >> 4) & 0x0F0F0F0Fu);
+        uint32_t v[8];
 #pragma unroll
-        for (int n = 0; n < 8; ++n) r ^= t.lane_sh[n][(c >> (4 * n)) & 15u][lane];
-        c = r;
+        for (int b = 0; b < 4; ++b) {
+            v[2 * b] = t.lane_sh[2 * b][(uint8_t)(clo >> (8 * b))][lane];
+            v[2 * b + 1] = t.lane_sh[2 * b + 1][(uint8_t)(chi >> (8 * b))][lane];
+        }
+        c = xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
     }
     // XOR-reduce the 64 lane contributions with DPP (one VALU op per step, no
     // LDS): quads, half-rows, rows, then the row broadcasts; lane 63 ends with
@@ -171,7 +199,7 @@ __device__ __forceinline__ bool icrc_len_ok(int ipt, int64_t stride)
 // Persistent: each wave walks its frames with the next frame's words (5 dwords
 // a lane, coalesced) and the one after's header in flight while the current
 // frame's CRC runs from LDS.
-template <bool kByte>
+template <bool kByte, int kIcrcWaves>
 __global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __restrict__ frames, int64_t stride,
                                                                 int64_t count, uint32_t* __restrict__ out)
 {
@@ -1205,20 +1233,31 @@ int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* o
     if ((stride & 3) || stride < INCCL_FRAME_MIN_STRIDE || ((uintptr_t)frames & 3)) return INCCL_ERR_ARG;
     int rc = ensure_tables();
     if (rc) return rc;
-    const int64_t blocks = ((int64_t)count + kIcrcWaves - 1) / kIcrcWaves;
     static const bool byte_tables = [] {
         const char* e = getenv("INCCL_ICRC_BYTE_TABLES");
         return e && atoi(e) != 0;
     }();
-    // persistent: tables loaded once per block (the byte tables' 59 KiB fit twice per CU)
-    const int64_t cap = (int64_t)num_cus() * blocks_per_cu("INCCL_ICRC_BLOCKS_PER_CU", byte_tables ? 2 : 3);
+    // 16-wave blocks share one copy of the tables: two per CU hold 32 waves (the
+    // most a CU runs), where 8-wave blocks fit three (24 waves) in the LDS;
+    // $INCCL_ICRC_WAVES=8 selects the 8-wave form (A/B)
+    static const int waves = [] {
+        const char* e = getenv("INCCL_ICRC_WAVES");
+        return e && atoi(e) == 8 ? 8 : 16;
+    }();
+    const int64_t blocks = ((int64_t)count + waves - 1) / waves;
+    // persistent: tables loaded once per block
+    const int64_t cap =
+        (int64_t)num_cus() * blocks_per_cu("INCCL_ICRC_BLOCKS_PER_CU", waves == 16 ? 2 : (byte_tables ? 2 : 3));
     const int grid = (int)(blocks < cap ? blocks : cap);
+    hipStream_t st = (hipStream_t)stream;
     if (byte_tables)
-        hipLaunchKernelGGL(k_icrc<true>, dim3(grid), dim3(kWave * kIcrcWaves), 0, (hipStream_t)stream, frames,
-                           (int64_t)stride, (int64_t)count, out);
+        hipLaunchKernelGGL((k_icrc<true, 8>), dim3(grid), dim3(kWave * 8), 0, st, frames, (int64_t)stride, (int64_t)count, out);
+    else if (waves == 16)
+        hipLaunchKernelGGL((k_icrc<false, 16>), dim3(grid), dim3(kWave * 16), 0, st, frames, (int64_t)stride, (int64_t)count,
+                           out);
     else
-        hipLaunchKernelGGL(k_icrc<false>, dim3(grid), dim3(kWave * kIcrcWaves), 0, (hipStream_t)stream, frames,
-                           (int64_t)stride, (int64_t)count, out);
+        hipLaunchKernelGGL((k_icrc<false, 8>), dim3(grid), dim3(kWave * 8), 0, st, frames, (int64_t)stride, (int64_t)count,
+                           out);
     return (int)hipGetLastError();
 }
 
