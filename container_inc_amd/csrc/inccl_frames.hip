@@ -512,11 +512,14 @@ __global__ __launch_bounds__(kWave * 16) void k_ingress_apply(InccSwitchState s,
         reinterpret_cast<u4*>(s.agg + (size_t)slot * kLanes)[lane] = u4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
         // clear_state_data(psn + WINDOW) when the PSN completes in this batch
         // (nts.c:235-242, :367): slot psn + slots/2, which no frame of the batch
-        // touches (a batch's PSNs are less than slots/2 apart)
+        // touches (a batch's PSNs are less than slots/2 apart).  Its bitmap, degree
+        // and RETH keeper are cleared; its 1 KiB of aggregator words are not: a
+        // slot whose bitmap is empty is summed from zero without reading them
+        // (above), and nothing else reads a slot before its next counted arrival
+        // rewrites them (egress reads completed slots only) -- 67 MB fewer stores
+        // per 131 072-frame batch
         if (done_at[k] != 0xFFFFFFFFu) {
             const uint32_t rs = (psn[k] + (s.slots >> 1)) & (s.slots - 1);
-            typedef int32_t i4 __attribute__((ext_vector_type(4)));
-            reinterpret_cast<i4*>(s.agg + (size_t)rs * kLanes)[lane] = i4{0, 0, 0, 0};
             for (int i = lane; i < fan * 4; i += kWave) s.reth[(size_t)rs * fan * 4 + i] = 0;
             if (lane == 0) {
                 s.arrival[rs] = 0;

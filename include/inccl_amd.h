@@ -259,7 +259,10 @@ struct inccl_switch;
 struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device);
 int inccl_switch_destroy(struct inccl_switch *sw);
 int inccl_switch_reset(struct inccl_switch *sw, void *stream);
-/* device pointer of the 256-lane aggregator slot of `psn` */
+/* device pointer of the 256-lane aggregator slot of `psn`: the wrap-around sum of the arrivals counted
+ * since the slot was last recycled, while its arrival bitmap is non-zero.  A recycle (nts.c:235-242)
+ * clears the slot's bitmap, degree and RETH keeper; its words are stale until the next counted
+ * arrival rewrites them (the next sum starts from zero without reading them). */
 const int32_t *inccl_switch_slot(struct inccl_switch *sw, uint32_t psn);
 /* ports_dev[i] = ingress port of frame i.  Writes action_dev[i] (INCCL_SW_*) and psn_dev[i], and
  * recycles slot psn + slots/2 of every psn the batch completes (clear_state_data(psn + WINDOW),
