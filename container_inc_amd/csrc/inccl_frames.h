@@ -20,9 +20,11 @@ typedef struct InccSwitchState {
     uint32_t *reth;      /* [slots][fan_in][4]  nts.c:57 */
     uint64_t *first;     /* [slots][fan_in]     batch-tagged index of the first copy in a batch:
                           * (~gen << 32) | frame, atomicMin -> the earliest frame of the newest batch */
+    uint32_t *gen;       /* device word: batches ingested so far.  A batch's claim and apply use *gen + 1 as
+                          * its generation and its commit stores it, so that a captured batch (hipGraph)
+                          * tags every replay anew */
     uint32_t slots;      /* power of two */
     int fan_in;
-    uint32_t gen;        /* batch generation (host counter, advanced per ingress call) */
 } InccSwitchState;
 
 #define INCCL_FRAME_MIN_STRIDE 64   /* a row must hold the 62-B ACK frame (headers through the BTH) */

@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
             const uint32_t slot = psn & (s.slots - 1);
             atomicAdd(&s.degree[slot], 1);                       // nts.c:351 / :431
             atomicMin(reinterpret_cast<unsigned long long*>(&s.first[(size_t)slot * s.fan_in + port]),
-                      (unsigned long long)first_key(s.gen, f, wf));
+                      (unsigned long long)first_key(*s.gen + 1u, f, wf));
             act = kActPending;
         }
     }
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(kWave * 16) void k_ingress_apply(InccSwitchState s,
     const int64_t f0 = ((int64_t)blockIdx.x * (blockDim.x / kWave) + w) * kApplyFrames;
     if (f0 >= count) return;
     const int fan = s.fan_in;
-    const uint32_t tag = ~s.gen, result_bit = 1u << fan;
+    const uint32_t tag = ~(*s.gen + 1u), result_bit = 1u << fan;   // this batch's generation (k_ingress_commit)
     // stage A: each frame's action, port and PSN
     int act[kApplyFrames], port[kApplyFrames];
     uint32_t psn[kApplyFrames];
@@ -538,6 +538,9 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_commit(InccSwitchState 
                                                                 const uint32_t* __restrict__ psns)
 {
     const int64_t f = (int64_t)blockIdx.x * kClaimBlock + threadIdx.x;
+    // the batch is done with its generation (claim and apply ran before this
+    // launch): the next batch's is one higher
+    if (f == 0) *s.gen = *s.gen + 1u;
     if (f >= count) return;
     const int act = action[f];
     if (act != INCCL_SW_ABSORBED && act != INCCL_SW_COMPLETED) return;

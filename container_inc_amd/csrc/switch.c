@@ -3,9 +3,10 @@
  * The reference's root switch keeps its aggregation state in globals
  * (non_termination_switch.c:55-60) and processes one frame at a time on one
  * CPU thread (nts.c:508-530).  Here the state lives in HBM and frames are
- * processed in batches: one ingress launch (parse + idempotent add, nts.c:303-483),
- * one egress launch (frame build + ICRC, util.c:331-442) and one recycle launch
- * (clear_state_data(psn + window), nts.c:235-242, :367).  A batch must span
+ * processed in batches: ingress launches (parse + idempotent add + the recycle,
+ * clear_state_data(psn + window), nts.c:303-483, :235-242, :367) and one egress
+ * launch (frame build + ICRC, util.c:331-442).  No host state changes per batch,
+ * so a batch's launches can be captured in a hipGraph and replayed.  A batch must span
  * fewer than slots/2 PSNs -- the reference's window of 8 packets over 16 slots
  * (nts.c:21-22) has the same ratio. */
 #define _GNU_SOURCE
@@ -47,8 +48,9 @@ struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device)
     const size_t deg = (size_t)slots * sizeof(int32_t);
     const size_t reth = (size_t)slots * (size_t)fan_in * 16;
     const size_t first = (size_t)slots * (size_t)fan_in * 8;
-    sw->bytes = agg + arr + deg + reth + first;
-    sw->first_off = agg + arr + deg + reth;
+    const size_t gen = 8;   /* the batch-generation word (zeroed with the state) */
+    sw->bytes = agg + arr + deg + reth + gen + first;
+    sw->first_off = agg + arr + deg + reth + gen;
     hipError_t e = hipMalloc(&sw->mem, sw->bytes);
     if (e == hipSuccess) e = hipMemset(sw->mem, 0, sw->first_off);
     if (e == hipSuccess) e = hipMemset((char *)sw->mem + sw->first_off, 0xFF, first);   /* no batch yet */
@@ -63,8 +65,8 @@ struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device)
     sw->st.arrival = (uint32_t *)(p + agg);
     sw->st.degree = (int32_t *)(p + agg + arr);
     sw->st.reth = (uint32_t *)(p + agg + arr + deg);
+    sw->st.gen = (uint32_t *)(p + agg + arr + deg + reth);
     sw->st.first = (uint64_t *)(p + sw->first_off);
-    sw->st.gen = 0;
     sw->st.slots = slots;
     sw->st.fan_in = fan_in;
     hipGetDevice(&sw->device);
@@ -91,7 +93,6 @@ int inccl_switch_reset(struct inccl_switch *sw, void *stream)
     if (!sw) return inccl_set_error(INCCL_ERR_ARG, "switch is NULL");
     INCCL_HIP(hipMemsetAsync(sw->mem, 0, sw->first_off, (hipStream_t)stream));
     INCCL_HIP(hipMemsetAsync((char *)sw->mem + sw->first_off, 0xFF, sw->bytes - sw->first_off, (hipStream_t)stream));
-    sw->st.gen = 0;
     return 0;
 }
 
@@ -107,9 +108,10 @@ int inccl_switch_ingress(struct inccl_switch *sw, const uint8_t *frames_dev, siz
     if (!sw) return inccl_set_error(INCCL_ERR_ARG, "switch is NULL");
     if (count && stride < INCCL_FRAME_MIN_STRIDE)
         return inccl_set_error(INCCL_ERR_ARG, "inccl_switch_ingress: stride %zu below %d", stride, INCCL_FRAME_MIN_STRIDE);
-    /* a new batch: its first-arrival keys outrank every earlier batch's (switch
-     * state is per stream-ordered call sequence, like the reference's globals) */
-    if (count) sw->st.gen++;
+    /* a new batch: its first-arrival keys outrank every earlier batch's (the
+     * generation is a device word the batch's commit advances, so a captured
+     * batch stays correct on replay; switch state is per stream-ordered call
+     * sequence, like the reference's globals) */
     return kerr2(inccl_k_switch_ingress(&sw->st, frames_dev, stride, count, ports_dev, action_dev, psn_dev, stream),
                  "inccl_switch_ingress");
 }

@@ -344,3 +344,95 @@ def test_switch_short_stride_rejected(gpu, orc):
     with pytest.raises(inccl.IncclError):
         sw.ingress(torch.zeros((4, 32), dtype=torch.uint8, device=gpu), torch.zeros(4, dtype=torch.int32, device=gpu))
     sw.destroy()
+
+
+def test_switch_batch_graph_replay(gpu, orc):
+    """One batch's launches (ingress: claim / apply / commit, then egress)
+    captured once in a hipGraph and replayed over new frame contents: the
+    batch generation is a device word the commit advances, so every replay is
+    a new batch (first-copy keys of the previous replay never count).  Batches
+    alternate between the two halves of the PSN ring (each recycles the other's
+    slots, nts.c:367); every replay's actions, payload sums and ICRCs are
+    checked, then eager calls continue on the same state."""
+    import torch
+    from container_inc_amd import inccl
+    fan_in, P = 2, 3000
+    rng = np.random.default_rng(900)
+    slots = 2 * (1 << int(np.ceil(np.log2(P))))
+    half = slots // 2
+    base = {op: np.frombuffer(orc.build_data_frame(np.zeros(256, np.int32), psn=0, opcode=op, qp=0x11,
+                                                   with_reth=(op == 0x06), reth=bytes(16) if op == 0x06 else None),
+                              np.uint8) for op in (0x06, 0x07, 0x08)}
+    n = fan_in * P
+    port = np.tile(np.arange(fan_in, dtype=np.int32), P)
+
+    def batch(b):
+        psn = np.repeat(np.arange(P, dtype=np.uint32), fan_in) + (half if b % 2 else 0)
+        op_of = np.array([0x06, 0x07, 0x07, 0x08], np.uint8)[psn % 4]
+        pay = rng.integers(INT32_MIN, INT32_MAX, (n, 256), dtype=np.int64, endpoint=True).astype(np.int32)
+        frames = np.zeros((n, STRIDE), np.uint8)
+        for op in (0x06, 0x07, 0x08):
+            idx = np.nonzero(op_of == op)[0]
+            frames[idx, : len(base[op])] = base[op]
+            off = 70 if op == 0x06 else 54
+            frames[idx, off:off + 1024] = pay[idx].astype(">i4").view(np.uint8).reshape(len(idx), 1024)
+            frames[idx, 50:54] = (psn[idx] | 0x80000000).astype(">u4").view(np.uint8).reshape(len(idx), 4)
+        return psn, op_of, pay, frames
+
+    def check(psn, op_of, pay, action, psn_out, out, out_len):
+        act = action.cpu().numpy()
+        assert np.array_equal(psn_out.cpu().numpy(), psn)
+        done = act == inccl.SW_COMPLETED
+        assert done.sum() == P and (act[~done] == inccl.SW_ABSORBED).all()
+        agg = (pay[0::2].view(np.uint32).astype(np.uint64) + pay[1::2].view(np.uint32)).astype(np.uint32)
+        ln = out_len.cpu().numpy().reshape(n, fan_in)
+        assert (ln[~done] == 0).all()
+        rows = (np.nonzero(done)[0][:, None] * fan_in + np.arange(fan_in)[None, :]).reshape(-1)
+        oc = out[torch.from_numpy(rows).to(gpu)].cpu().numpy()
+        wf = op_of[rows // fan_in] == 0x06
+        for d in (54, 70):
+            sel = np.where(wf, 70, 54) == d
+            got = oc[sel, d:d + 1024].copy().view(">u4").astype(np.uint32)
+            assert np.array_equal(got, agg[(psn[rows // fan_in][sel] % half).astype(np.int64)])
+        crc = inccl.icrc_frames(torch.from_numpy(oc).to(gpu)).cpu().numpy().view(np.uint32)
+        lens = np.where(wf, 1098, 1082)
+        stored = np.array([int.from_bytes(oc[i, lens[i] - 4:lens[i]].tobytes(), "little") for i in range(len(rows))],
+                          np.uint32)
+        assert np.array_equal(crc, stored)
+
+    sw = inccl.GpuSwitch(fan_in, slots)
+    tmpl_dev = torch.from_numpy(_templates(fan_in).view(np.uint8).copy()).to(gpu)
+    fr = torch.zeros((n, STRIDE), dtype=torch.uint8, device=gpu)
+    pt = torch.from_numpy(port).to(gpu)
+    out = torch.zeros((n * fan_in, STRIDE), dtype=torch.uint8, device=gpu)
+    out_len = torch.zeros(n * fan_in, dtype=torch.int32, device=gpu)
+    st = torch.cuda.Stream(device=gpu)
+    # one eager batch first (b = 0), then the captured one replayed for b = 1..4
+    psn, op_of, pay, frames = batch(0)
+    fr.copy_(torch.from_numpy(frames))
+    torch.cuda.synchronize()
+    a, q = sw.ingress(fr, pt, stream=st)
+    sw.egress(fr, pt, a, q, tmpl_dev, stream=st, out=out, out_len=out_len)
+    torch.cuda.synchronize()
+    check(psn, op_of, pay, a, q, out, out_len)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        ga, gq = sw.ingress(fr, pt, stream=st)
+        sw.egress(fr, pt, ga, gq, tmpl_dev, stream=st, out=out, out_len=out_len)
+    for b in range(1, 5):
+        psn, op_of, pay, frames = batch(b)
+        fr.copy_(torch.from_numpy(frames))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        check(psn, op_of, pay, ga, gq, out, out_len)
+    # eager again on the same state (b = 5)
+    psn, op_of, pay, frames = batch(5)
+    fr.copy_(torch.from_numpy(frames))
+    torch.cuda.synchronize()
+    a, q = sw.ingress(fr, pt, stream=st)
+    sw.egress(fr, pt, a, q, tmpl_dev, stream=st, out=out, out_len=out_len)
+    torch.cuda.synchronize()
+    check(psn, op_of, pay, a, q, out, out_len)
+    del g
+    sw.destroy()

@@ -106,6 +106,29 @@ def main():
                       "psns": P, "ingress_frames": fan_in * P, "egress_frames": fan_in * P, "ms": round(ms, 4),
                       "payload_GBs": round(payload_bytes / (ms * 1e-3) / 1e9, 2),
                       "frames_per_s": round(2 * fan_in * P / (ms * 1e-3), 1)}), flush=True)
+    # the same batches captured in a hipGraph (two batches, one per half of the
+    # ring) and replayed: no launch gaps between the batch's kernels
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        run()
+        run()
+    g.replay()
+    torch.cuda.synchronize()
+    reps = 5
+    with torch.cuda.stream(st):
+        e0.record(st)
+        for _ in range(reps):
+            g.replay()
+        e1.record(st)
+    torch.cuda.synchronize()
+    ms_g = e0.elapsed_time(e1) / (2 * reps)
+    a, o, ln = run()   # eager again after the replays: still one completion per PSN
+    torch.cuda.synchronize()
+    assert (a.cpu().numpy() == inccl.SW_COMPLETED).sum() == P
+    del g
+    print(json.dumps({"what": "GPU switch dataplane batch, hipGraph-replayed (claim / apply / commit / egress)",
+                      "fan_in": fan_in, "psns": P, "ms": round(ms_g, 4),
+                      "payload_GBs": round(payload_bytes / (ms_g * 1e-3) / 1e9, 2)}), flush=True)
     icrc_out = torch.empty(fan_in * P, dtype=torch.int32, device=dev)
     with torch.cuda.stream(st):
         inccl.icrc_frames(fr, stream=st)
