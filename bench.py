@@ -1334,15 +1334,26 @@ def main():
             import signal
             os.kill(os.getpid(), signal.SIGKILL)
         best2 = tune(phases[1], 2)
+        phase2_error = None
         if best2 is not None and (best1 is None or best2[0] < best1[0]):
-            m = measure(best2[1], best2[2], best2[3])
-            if not kinfo:
-                dominant_kernel()
-            line = build_res(m)
-            # a phase-2 headline replaces phase 1's only if it was verified like it
-            ok = m["verified"] is not False and (m["parity"]["mismatches"] or 0) == 0
-            if agree([0.0 if ok else 1.0], world)[0] == 0.0:
-                measured.append((m, line))
+            try:
+                m = measure(best2[1], best2[2], best2[3])
+            except Exception as e:  # noqa: BLE001 -- an engine error is the same on every rank
+                if not measured:
+                    raise
+                phase2_error = f"{best2[1]}: {e!r}"
+                print(f"rank {rank}: phase-2 headline on {phase2_error} failed; phase 1's stands", file=sys.stderr,
+                      flush=True)
+                for key in best2[3]:
+                    os.environ.pop(key, None)
+            else:
+                if not kinfo:
+                    dominant_kernel()
+                line = build_res(m)
+                # a phase-2 headline replaces phase 1's only if it was verified like it
+                ok = m["verified"] is not False and (m["parity"]["mismatches"] or 0) == 0
+                if agree([0.0 if ok else 1.0], world)[0] == 0.0:
+                    measured.append((m, line))
         if not measured:
             raise SystemExit("no exchange engine produced verified results on every rank")
         # the faster measured headline is the line; every measured one is listed
@@ -1353,6 +1364,8 @@ def main():
              "ms_per_step": round(mm["ms_per_step"], 4), "value": ln["value"],
              "verified_vs_reference_engine": mm["verified"], "oracle_mismatches": mm["parity"]["mismatches"]}
             for mm, ln in measured]
+        if phase2_error:
+            best[1]["phase2_error"] = phase2_error
         publish(best[1], "headline measured")
         comm.set_engine(best[0]["engine"])
         os.environ.update(best[0]["env"])
