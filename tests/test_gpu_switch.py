@@ -90,8 +90,8 @@ def _expected_frame(orc, t, c, agg, psn, op, reth):
 # Stride 1100 (4-byte but not 16-byte aligned rows): ingress's 2-byte payload
 # loads and egress's dword stores instead of the 16-byte paths.
 # Fan-in 2, 3, 4 and 8 take the straight-line egress (k_egress_fixed), others the generic one.
-@pytest.mark.parametrize("fan_in,stride", [(2, STRIDE), (3, STRIDE), (4, STRIDE), (8, STRIDE), (20, STRIDE), (2, 1100),
-                                           (4, 1100), (8, 1100), (5, 1100)])
+@pytest.mark.parametrize("fan_in,stride", [(1, STRIDE), (2, STRIDE), (3, STRIDE), (4, STRIDE), (8, STRIDE), (20, STRIDE),
+                                           (31, STRIDE), (2, 1100), (4, 1100), (8, 1100), (5, 1100)])
 def test_switch_batches(gpu, orc, fan_in, stride):
     import torch
     from container_inc_amd import inccl
