@@ -557,7 +557,7 @@ __device__ __forceinline__ void put16(uint8_t* p, uint32_t v)
 // Header image of child c's egress frames (util.c:348-388) with opcode and PSN
 // left zero: identical for every frame of that child and RETH flag, so each
 // block builds the 2*fan_in images once into LDS and frames copy them word-wise.
-constexpr int kHdrImg = 72;   // 70 header bytes (with RETH slot) rounded to dwords
+constexpr int kHdrImg = 80;   // 70 header bytes (with RETH slot), rows 16-byte aligned (read as 16-byte chunks)
 
 __device__ void build_header_image(uint8_t* fr, const InccFrameTemplate& h, bool wf)
 {
@@ -964,8 +964,8 @@ __device__ __forceinline__ EgressIn egress_fetch_fixed(const InccSwitchState& s,
 template <int kFan, bool kOut16>
 __device__ __forceinline__ void egress_emit_fixed(const EgressIn& e, const uint8_t (*himg)[kHdrImg],
                                                   uint8_t* __restrict__ out, int64_t out_stride,
-                                                  int32_t* __restrict__ out_len, const EgressLds& t, uint8_t* hbuf,
-                                                  int64_t f, int lane)
+                                                  int32_t* __restrict__ out_len, const EgressLds& t, int64_t f,
+                                                  int lane)
 {
     const bool all = e.act == INCCL_SW_COMPLETED;
     const bool one = e.act == INCCL_SW_REPLAY && e.port >= 0 && e.port < kFan;
@@ -990,13 +990,13 @@ __device__ __forceinline__ void egress_emit_fixed(const EgressIn& e, const uint8
     const uint32_t pc2 = __builtin_amdgcn_alignbyte(nx[1], nx[0], 2);
     const uint32_t pc3 = __builtin_amdgcn_alignbyte(nx[2], nx[1], 2);
     const uint32_t pw = e.psn | 0x80000000u;
+    // the payload's first 10 bytes (words 0-2 of lane 0, memory order): they
+    // end the header chunks
+    const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)a[0], 0);
+    const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)a[1], 0);
+    const uint32_t a2 = (uint32_t)__builtin_amdgcn_readlane((int)a[2], 0);
     uint32_t pc = 0;
     if (all || one) {
-        const uint32_t a0 = (uint32_t)__shfl((int)a[0], 0, kWave), a1 = (uint32_t)__shfl((int)a[1], 0, kWave);
-        const uint32_t a2 = (uint32_t)__shfl((int)a[2], 0, kWave);
-        if (lane == 0) *reinterpret_cast<uint16_t*>(hbuf + doff) = (uint16_t)a0;
-        if (lane == 1) *reinterpret_cast<uint32_t*>(hbuf + doff + 2) = __builtin_amdgcn_alignbyte(a1, a0, 2);
-        if (lane == 2) *reinterpret_cast<uint32_t*>(hbuf + doff + 6) = __builtin_amdgcn_alignbyte(a2, a1, 2);
         uint32_t pv = seg16_crc(t, a, lane);
         if (lane < 5) {
             const uint32_t b = lane == 0 ? op : (pw >> (8 * (4 - lane))) & 0xFFu;
@@ -1004,45 +1004,50 @@ __device__ __forceinline__ void egress_emit_fixed(const EgressIn& e, const uint8
         }
         pc = wave_xor(pv);
     }
+    const uint32_t psn_hi = (pw >> 24) | (((pw >> 16) & 0xFFu) << 8);    // frame bytes 50, 51 (util.c:386)
+    const uint32_t psn_lo = ((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8);   // bytes 52, 53
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int c = 0; c < kFan; ++c) {
         const bool act_c = all || (one && c == e.port);
         uint32_t crc = 0;
+        // child c's RETH words (reth_keeper[slot][c], nts.c:442), wave-uniform
+        const uint32_t R0 = (uint32_t)__builtin_amdgcn_readlane((int)e.reth, 4 * c);
+        const uint32_t R1 = (uint32_t)__builtin_amdgcn_readlane((int)e.reth, 4 * c + 1);
+        const uint32_t R2 = (uint32_t)__builtin_amdgcn_readlane((int)e.reth, 4 * c + 2);
+        const uint32_t R3 = (uint32_t)__builtin_amdgcn_readlane((int)e.reth, 4 * c + 3);
         if (act_c) {
-            uint32_t r = 0, rk = 0;
-            if (wf) {
-                r = (uint32_t)__shfl((int)e.reth, 4 * c + (lane & 3), kWave);
-                rk = (uint32_t)__shfl((int)r, lane >> 2, kWave);
-            }
             uint32_t vr = 0;
-            if (wf) vr = wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
+            if (wf) {
+                // lane k < 16: RETH byte k = byte k & 3 of word k >> 2
+                const uint32_t rk = (lane & 8) ? ((lane & 4) ? R3 : R2) : ((lane & 4) ? R1 : R0);
+                vr = wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
+            }
             crc = ~(pc ^ t.hcrc[2 * c + wf] ^ vr);   // util.c:424-426
-            if (lane < 13) {
-                uint32_t hw = reinterpret_cast<const uint32_t*>(himg[2 * c + wf])[lane];
-                if (lane == 10) hw = (hw & 0xFF00FFFFu) | (op << 16);
-                if (lane == 12) hw = (hw & 0x0000FFFFu) | ((pw >> 24) << 16) | (((pw >> 16) & 0xFFu) << 24);
-                reinterpret_cast<uint32_t*>(hbuf)[lane] = hw;
-            } else if (lane == 13) {
-                *reinterpret_cast<uint16_t*>(hbuf + 52) = (uint16_t)(((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8));
-            }
-            if (wf) {                                                   // util.c:409-417: bytes 54-69
-                const int k = lane - 14;
-                const uint32_t rlo = (uint32_t)__shfl((int)r, (k - 1) & 3, kWave);
-                const uint32_t rhi = (uint32_t)__shfl((int)r, k & 3, kWave);
-                if (k == 0) *reinterpret_cast<uint16_t*>(hbuf + 54) = (uint16_t)rhi;
-                else if (k >= 1 && k <= 3) *reinterpret_cast<uint32_t*>(hbuf + 52 + 4 * k) = __builtin_amdgcn_alignbyte(rhi, rlo, 2);
-                else if (k == 4) *reinterpret_cast<uint16_t*>(hbuf + 68) = (uint16_t)(rlo >> 16);
-            }
         }
-        __builtin_amdgcn_wave_barrier();
-        // stores through a buffer resource over the row: a lane that must not
-        // store gets an offset past the row, and the hardware drops the store
-        // (no exec mask, no branch)
+        // header chunk `lane` (< hchunks) built in registers: the template image's
+        // 16 bytes (util.c:348-388) with the opcode (byte 42), the PSN (50-53), the
+        // RETH (54-69, util.c:409-417) and the payload's first 10 bytes patched in
+        const u4 img = reinterpret_cast<const u4*>(himg[2 * c + wf])[lane < 5 ? lane : 0];
+        uint32_t h0 = img.x, h1 = img.y, h2 = img.z, h3 = img.w;
+        if (lane == 2) h2 = (h2 & 0xFF00FFFFu) | (op << 16);
+        if (lane == 3) {
+            const uint32_t b0 = wf ? R0 : a0, b1 = wf ? R1 : a1, b2 = wf ? R2 : a2;   // bytes 54-63
+            h0 = (h0 & 0xFFFFu) | (psn_hi << 16);
+            h1 = psn_lo | (b0 << 16);
+            h2 = __builtin_amdgcn_alignbyte(b1, b0, 2);
+            h3 = __builtin_amdgcn_alignbyte(b2, b1, 2);
+        }
+        if (lane == 4) {                                                // RETH frames only: bytes 64-79
+            h0 = __builtin_amdgcn_alignbyte(R3, R2, 2);
+            h1 = (R3 >> 16) | (a0 << 16);
+            h2 = __builtin_amdgcn_alignbyte(a1, a0, 2);
+            h3 = __builtin_amdgcn_alignbyte(a2, a1, 2);
+        }
+        const u4 h = {h0, h1, h2, h3};
         const __amdgpu_buffer_rsrc_t orow =
             __builtin_amdgcn_make_buffer_rsrc(out + (f * kFan + c) * out_stride, 0, (int)out_stride, 0x00020000);
         const bool sh = act_c && lane < hchunks;
-        const u4 h = reinterpret_cast<const u4*>(hbuf)[lane < 5 ? lane : 0];   // 5 chunks at most
         const u4 v = lane < kWave - 1 ? u4{pc0, pc1, pc2, pc3}
                                       : u4{pc0, (a[3] >> 16) | ((crc & 0xFFFFu) << 16), crc >> 16, 0u};
         const int ho = sh ? 16 * lane : kOobOffset, po = act_c ? 16 * (hchunks + lane) : kOobOffset;
@@ -1060,7 +1065,6 @@ __device__ __forceinline__ void egress_emit_fixed(const EgressIn& e, const uint8
             // lane 63 stops at the frame's 4-byte-rounded end
             __builtin_amdgcn_raw_buffer_store_b32(v.w, orow, lane < kWave - 1 ? po + 12 : kOobOffset, 0, 0);
         }
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -1076,7 +1080,6 @@ __device__ __forceinline__ void egress_fixed_body(InccSwitchState s,
                                                                       int32_t* __restrict__ out_len)
 {
     __shared__ EgressLds t;
-    __shared__ __attribute__((aligned(16))) uint8_t buf[kEgW][80];
     __shared__ __attribute__((aligned(16))) uint8_t himg[2 * 31][kHdrImg];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     egress_setup(t, himg, tmpl, kFan, w, lane);
@@ -1107,12 +1110,12 @@ __device__ __forceinline__ void egress_fixed_body(InccSwitchState s,
     for (;;) {
         int64_t fn = next();
         b = egress_fetch_fixed<kFan>(s, in_frames, in_stride, ports, action, psns, clamp(fn), lane);
-        egress_emit_fixed<kFan, kOut16>(a, himg, out, out_stride, out_len, t, buf[w], f, lane);
+        egress_emit_fixed<kFan, kOut16>(a, himg, out, out_stride, out_len, t, f, lane);
         f = fn;
         if (f >= count) break;
         fn = next();
         a = egress_fetch_fixed<kFan>(s, in_frames, in_stride, ports, action, psns, clamp(fn), lane);
-        egress_emit_fixed<kFan, kOut16>(b, himg, out, out_stride, out_len, t, buf[w], f, lane);
+        egress_emit_fixed<kFan, kOut16>(b, himg, out, out_stride, out_len, t, f, lane);
         f = fn;
         if (f >= count) break;
     }

@@ -11,7 +11,7 @@ rc=$?; echo "switch tests rc=$rc"; tail -1 $O/pytest_switch.log; [ $rc -eq 0 ] |
 for v in fixed generic fixed generic; do
   if [ $v = generic ]; then export INCCL_EGRESS_GENERIC=1; else unset INCCL_EGRESS_GENERIC; fi
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_$v -o run --output-format csv -- python3 tools/switch_bench.py > $O/bench_$v.log 2>&1 || { tail -20 $O/bench_$v.log; exit 6; }
-  echo "== $v: $(grep '"what": "GPU switch' $O/bench_$v.log | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["ms"])') ms per batch"
+  echo "== $v: $(grep -m1 '"what": "GPU switch' $O/bench_$v.log | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["ms"])') ms per batch"
   python3 - $O/prof_$v/run_kernel_stats.csv <<'PY'
 import csv, sys
 for r in csv.DictReader(open(sys.argv[1])):
