@@ -249,11 +249,6 @@ __global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __res
     }
 }
 
-__device__ __forceinline__ uint32_t be32(const uint8_t* p)
-{
-    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
-}
-
 __device__ __forceinline__ bool is_data_opcode(uint8_t op)
 {
     return op == 0x00 || op == 0x01 || op == 0x02 || op == 0x04 || op == 0x07 || op == 0x08;   // nts.c:314-319
@@ -299,11 +294,14 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
 {
     const int64_t f = (int64_t)blockIdx.x * kClaimBlock + threadIdx.x;
     if (f >= count) return;
-    const uint8_t* fr = frames + f * stride;
+    // rows are 4-byte aligned and at least 64 bytes: the header fields from four
+    // dword loads (bytes 36-43 and 48-55 of the row) instead of byte loads
+    const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + f * stride);
+    const uint32_t w9 = fw[9], w10 = fw[10], w12 = fw[12], w13 = fw[13];
     const int port = ports[f];
-    const uint8_t op = fr[42];
-    const uint32_t psn = be32(fr + 50) & 0x00FFFFFFu;          // nts.c:311
-    const int udp_len = ((int)fr[38] << 8) | fr[39];
+    const uint8_t op = (uint8_t)(w10 >> 16);                                    // byte 42
+    const uint32_t psn = ((w12 >> 24) << 16) | ((w13 & 0xFFu) << 8) | ((w13 >> 8) & 0xFFu);   // bytes 51-53, nts.c:311
+    const int udp_len = (int)(((w9 >> 16) & 0xFFu) << 8 | (w9 >> 24));          // bytes 38-39
     int act = INCCL_SW_IGNORED;
     if (port < 0 || port >= s.fan_in) act = INCCL_SW_INVALID;
     else if (op == 0x11) act = INCCL_SW_ACK;                    // nts.c:336-342, :403-406 (reflect)
