@@ -953,8 +953,13 @@ __device__ __forceinline__ EgressIn egress_fetch_fixed(const InccSwitchState& s,
     const __amdgpu_buffer_rsrc_t rr =
         __builtin_amdgcn_make_buffer_rsrc(s.reth + (size_t)e.slot * kFan * 4, 0, 16 * kFan, 0x00020000);
     e.reth = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rr, lane < 4 * kFan ? 4 * lane : kOobOffset, 0, 0);
+    // the slot's aggregate only for a frame that emits (COMPLETED / REPLAY): an
+    // absorbed frame's load goes past the buffer (no memory traffic)
     typedef int32_t i4 __attribute__((ext_vector_type(4)));
-    const i4 v = reinterpret_cast<const i4*>(s.agg + (size_t)e.slot * kLanes)[lane];
+    const bool emits = e.act == INCCL_SW_COMPLETED || e.act == INCCL_SW_REPLAY;
+    const i4 v = (i4)__builtin_amdgcn_raw_buffer_load_b128(
+        __builtin_amdgcn_make_buffer_rsrc(s.agg + (size_t)e.slot * kLanes, 0, 1024, 0x00020000),
+        emits ? 16 * lane : kOobOffset, 0, 0);
     e.agg[0] = v.x; e.agg[1] = v.y; e.agg[2] = v.z; e.agg[3] = v.w;
     return e;
 }
