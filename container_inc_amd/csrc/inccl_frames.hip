@@ -607,16 +607,23 @@ __device__ void build_header_image(uint8_t* fr, const InccFrameTemplate& h, bool
 // reduction (RETH frames only), not a pass over the 1 KiB frame.
 constexpr int kVarBytes = 21;   // opcode, 4 PSN bytes, 16 RETH bytes
 __device__ uint32_t g_lane16[8][16][kWave];            // [nibble][value][lane] = Z_{16 (63 - lane)}(value << 4 nibble)
-__device__ uint32_t g_var[2][kVarBytes][2][16];       // [reth][byte][nibble][value]: contribution at the message end
+__device__ uint32_t g_var[5 + kVarBytes][2][16];     // [var_row(reth, byte)][nibble][value]: contribution at the message end
 __device__ uint32_t g_z1024[8][16];                   // Z_1024(value << 4 nibble)
 
-struct EgressLds {
+// variable-byte rows: a RETH-less frame's 5 (opcode, PSN) at rows 0-4, a RETH
+// frame's 21 (opcode, PSN, RETH) at rows 5-25
+constexpr int kVarRows = 5 + kVarBytes;
+__device__ __forceinline__ constexpr int var_row(int wf, int k) { return wf ? 5 + k : k; }
+
+template <int kImgs>
+struct EgressLdsT {
     uint32_t seg[kSeg][2][16];      // g_seg: rows 1..16 are a 16-byte segment's Z_{15-j}
     uint32_t lane16[8][16][kWave];
-    uint32_t var[2][kVarBytes][2][16];
+    uint32_t var[kVarRows][2][16];
     uint32_t z1024[8][16];
-    uint32_t hcrc[2 * 31];          // H_c for (child, RETH flag)
+    uint32_t hcrc[kImgs];           // H_c for (child, RETH flag)
 };
+using EgressLds = EgressLdsT<2 * 31>;
 
 // What one egress wave needs from global memory for input frame f: loaded one
 // frame ahead of its use (k_egress), so these dependent loads overlap the
@@ -667,7 +674,8 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t c)
 
 // A 16-byte segment's raw CRC (bytes in memory order in a[0..3], little-endian
 // words) shifted by Z_{16 (63 - sh_lane)}.
-__device__ __forceinline__ uint32_t seg16_crc(const EgressLds& t, const uint32_t (&a)[4], int sh_lane)
+template <class L>
+__device__ __forceinline__ uint32_t seg16_crc(const L& t, const uint32_t (&a)[4], int sh_lane)
 {
     // nibble planes, one SDWA byte select per lookup, XORs three at a time (icrc_wave)
     uint32_t c = 0;
@@ -692,16 +700,18 @@ __device__ __forceinline__ uint32_t seg16_crc(const EgressLds& t, const uint32_t
     return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
 }
 
-__device__ __forceinline__ uint32_t var_crc(const EgressLds& t, int wf, int k, uint32_t b)
+template <class L>
+__device__ __forceinline__ uint32_t var_crc(const L& t, int wf, int k, uint32_t b)
 {
-    return t.var[wf][k][0][b & 15u] ^ t.var[wf][k][1][(b >> 4) & 15u];
+    return t.var[var_row(wf, k)][0][b & 15u] ^ t.var[var_row(wf, k)][1][(b >> 4) & 15u];
 }
 
 // H_c for every (child, RETH flag) of the block's templates: quad q of wave w
 // takes pair i = 16 w + q.  The header part of the message (doff - 10 bytes:
 // 44, or 60 with RETH) is right-aligned in a 64-byte window (leading zeros do
 // not change a raw CRC); lane s of the quad takes window bytes 16 s .. 16 s + 15.
-__device__ void header_crcs(EgressLds& t, const uint8_t (*himg)[kHdrImg], int fan, int w, int lane)
+template <class L>
+__device__ void header_crcs(L& t, const uint8_t (*himg)[kHdrImg], int fan, int w, int lane)
 {
     const int i = w * 16 + (lane >> 2), s = lane & 3;
     uint32_t c = 0;
@@ -740,12 +750,13 @@ __device__ void header_crcs(EgressLds& t, const uint8_t (*himg)[kHdrImg], int fa
 // The CRC tables, the 2 * fan_in header images and their constant ICRC terms
 // into the block's LDS (ends with a block barrier).  Blocks of 8 waves: quad
 // q of wave w computes header term 16 w + q (2 * 31 at most).
-__device__ void egress_setup(EgressLds& t, uint8_t (*himg)[kHdrImg], const InccFrameTemplate* __restrict__ tmpl, int fan,
-                             int w, int lane)
+template <class L>
+__device__ void egress_setup(L& t, uint8_t (*himg)[kHdrImg], const InccFrameTemplate* __restrict__ tmpl, int fan, int w,
+                             int lane)
 {
     for (int i = threadIdx.x; i < kSeg * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg[0][0][0])[i];
     for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) (&t.lane16[0][0][0])[i] = (&g_lane16[0][0][0])[i];
-    for (int i = threadIdx.x; i < 2 * kVarBytes * 2 * 16; i += blockDim.x) (&t.var[0][0][0][0])[i] = (&g_var[0][0][0][0])[i];
+    for (int i = threadIdx.x; i < kVarRows * 2 * 16; i += blockDim.x) (&t.var[0][0][0])[i] = (&g_var[0][0][0])[i];
     for (int i = threadIdx.x; i < 8 * 16; i += blockDim.x) (&t.z1024[0][0])[i] = (&g_z1024[0][0])[i];
     for (int i = threadIdx.x; i < 2 * fan; i += blockDim.x) build_header_image(himg[i], tmpl[i >> 1], (i & 1) != 0);
     __syncthreads();
@@ -964,11 +975,10 @@ __device__ __forceinline__ EgressIn egress_fetch_fixed(const InccSwitchState& s,
     return e;
 }
 
-template <int kFan, bool kOut16>
+template <int kFan, bool kOut16, class L>
 __device__ __forceinline__ void egress_emit_fixed(const EgressIn& e, const uint8_t (*himg)[kHdrImg],
                                                   uint8_t* __restrict__ out, int64_t out_stride,
-                                                  int32_t* __restrict__ out_len, const EgressLds& t, int64_t f,
-                                                  int lane)
+                                                  int32_t* __restrict__ out_len, const L& t, int64_t f, int lane)
 {
     const bool all = e.act == INCCL_SW_COMPLETED;
     const bool one = e.act == INCCL_SW_REPLAY && e.port >= 0 && e.port < kFan;
@@ -1082,8 +1092,8 @@ __device__ __forceinline__ void egress_fixed_body(InccSwitchState s,
                                                                       uint8_t* __restrict__ out, int64_t out_stride,
                                                                       int32_t* __restrict__ out_len)
 {
-    __shared__ EgressLds t;
-    __shared__ __attribute__((aligned(16))) uint8_t himg[2 * 31][kHdrImg];
+    __shared__ EgressLdsT<2 * kFan> t;   // header terms and images for this fan-in only
+    __shared__ __attribute__((aligned(16))) uint8_t himg[2 * kFan][kHdrImg];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     egress_setup(t, himg, tmpl, kFan, w, lane);
     // the rotation of k_egress; frames past the end re-read the last one (a fixed
@@ -1129,8 +1139,8 @@ __device__ __forceinline__ void egress_fixed_body(InccSwitchState s,
         const int32_t *__restrict__ ports, const int32_t *__restrict__ action, const uint32_t *__restrict__ psns,    \
         const InccFrameTemplate *__restrict__ tmpl, uint8_t *__restrict__ out, int64_t out_stride,                   \
         int32_t *__restrict__ out_len
-// 8-wave blocks, three per CU (the LDS bound: 24 waves; 14-wave blocks, two per CU
-// = 28 waves, measured 82 vs 73.3-73.8 us)
+// 8-wave blocks, three per CU = 24 waves: the measured optimum (profiles/r03/egress_waves/: 8 / 16 / 24 / 28
+// waves per CU = 95.5 / 74.8 / 71.0 / 82-83 us)
 template <int kFan, bool kOut16>
 __global__ __launch_bounds__(kWave * 8) void k_egress_fixed(INCCL_EGRESS_FIXED_ARGS)
 {
@@ -1147,7 +1157,7 @@ uint32_t host_seg[kSeg][2][16];
 uint32_t host_segb[kSeg][256];
 uint32_t host_lane_shift[8][16][kWave];
 uint32_t host_lane16[8][16][kWave];
-uint32_t host_var[2][kVarBytes][2][16];
+uint32_t host_var[5 + kVarBytes][2][16];
 uint32_t host_z1024[8][16];
 bool g_tables_ready[64];
 std::mutex g_tables_mu;
@@ -1201,7 +1211,7 @@ int ensure_tables()
             const int p = k == 0 ? 32 : 39 + k;   // message position: opcode (frame 42), PSN (50-53), RETH (54-69)
             for (int h = 0; h < 2; ++h)
                 for (uint32_t v = 0; v < 16; ++v)
-                    host_var[wf][k][h][v] = p < hdr ? zeros_append(host_tab[v << (4 * h)], hdr - 1 - p + 1024) : 0u;
+                    if (wf || k < 5) host_var[wf ? 5 + k : k][h][v] = p < hdr ? zeros_append(host_tab[v << (4 * h)], hdr - 1 - p + 1024) : 0u;
         }
     }
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg), host_seg, sizeof(host_seg));
