@@ -249,6 +249,138 @@ __global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __res
     }
 }
 
+// ---------------------------------------------------------------------------
+// ICRC, two frames per wave (the default; $INCCL_ICRC_PAIR=0: k_icrc): lanes 0-31 take frame 2p,
+// lanes 32-63 frame 2p+1, each lane 34 bytes of the 1088-byte window (32 x 34).
+// Per frame: 34 x 2 nibble lookups over 32 lanes (38 lookup instructions per
+// frame, against 42), a 16 KiB lane-shift table (Z_{34 (31 - lane')}), and one
+// 5-step DPP reduction for both frames.  Same right-aligned window, masks and
+// results as icrc_wave.
+// ---------------------------------------------------------------------------
+constexpr int kSeg2 = 34;
+__device__ uint32_t g_seg34[kSeg2][2][16];          // [byte j][nibble][value] = Z_{33-j}(T[value << 4 nibble])
+__device__ uint32_t g_lane_shift32[8][16][32];      // [nibble][value][lane'] = Z_{34 (31 - lane')}(value << 4 nibble)
+
+struct CrcLdsPair {
+    uint32_t seg[kSeg2][2][16];
+    uint32_t lane_sh[8][16][32];
+};
+
+// ICRC of the frame of this lane's half (staged at `fr`, masked bytes 0xFF);
+// returns the raw (pre-reduction) contribution of this lane
+__device__ __forceinline__ uint32_t icrc_half_lane(const uint8_t* fr, const CrcLdsPair& t, int l)
+{
+    const int ip_total = ((int)fr[16] << 8) | fr[17];
+    const int lead = kWin - ip_total;
+    const int o = 10 + l * kSeg2 - lead;                 // frame offset of this lane's first byte
+    uint32_t c = 0;
+    if (o + kSeg2 > 10) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(fr);
+        const int d0 = o >> 2;
+        uint32_t dw[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) dw[k] = d0 + k >= 0 ? w[d0 + k] : 0u;
+        const uint32_t sh = (uint32_t)o & 3u;
+        uint32_t a[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a[k] = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
+        const int nz = 10 - o;
+        if (nz > 0) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const int z = nz - 4 * k;
+                a[k] = z >= 4 ? 0u : (z > 0 ? a[k] & (0xFFFFFFFFu << (8 * z)) : a[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t lo = opaque_u32(a[k] & 0x0F0F0F0Fu), hi = opaque_u32((a[k] >> 4) & 0x0F0F0F0Fu);
+            uint32_t v[8];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                v[2 * b] = t.seg[4 * k + b][0][(uint8_t)(lo >> (8 * b))];
+                v[2 * b + 1] = t.seg[4 * k + b][1][(uint8_t)(hi >> (8 * b))];
+            }
+            c = xor3(xor3(xor3(c, v[0], v[1]), v[2], v[3]), xor3(v[4], v[5], v[6]), v[7]);
+        }
+        // bytes 32 and 33 of the segment
+        c = xor3(c, t.seg[32][0][a[8] & 15u], t.seg[32][1][(a[8] >> 4) & 15u]);
+        c = xor3(c, t.seg[33][0][(a[8] >> 8) & 15u], t.seg[33][1][(a[8] >> 12) & 15u]);
+        const uint32_t clo = opaque_u32(c & 0x0F0F0F0Fu), chi = opaque_u32((c >> 4) & 0x0F0F0F0Fu);
+        uint32_t v[8];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            v[2 * b] = t.lane_sh[2 * b][(uint8_t)(clo >> (8 * b))][l];
+            v[2 * b + 1] = t.lane_sh[2 * b + 1][(uint8_t)(chi >> (8 * b))][l];
+        }
+        c = xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
+    }
+    return c;
+}
+
+template <int kW>
+__global__ __launch_bounds__(kWave* kW) void k_icrc_pair(const uint8_t* __restrict__ frames, int64_t stride,
+                                                         int64_t count, uint32_t* __restrict__ out)
+{
+    __shared__ CrcLdsPair t;
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kW][2][kFrameMax];
+    for (int i = threadIdx.x; i < kSeg2 * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg34[0][0][0])[i];
+    for (int i = threadIdx.x; i < 8 * 16 * 32; i += blockDim.x) (&t.lane_sh[0][0][0])[i] = (&g_lane_shift32[0][0][0])[i];
+    __syncthreads();
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    const int half = lane >> 5, l = lane & 31;
+    constexpr int kWords = kFrameMax / 4 / 32;   // 9 dwords per lane and frame
+    const int64_t pairs = (count + 1) >> 1, step = (int64_t)gridDim.x * kW;
+    int64_t p = (int64_t)blockIdx.x * kW + w;
+    if (p >= pairs) return;
+    uint8_t* mine = buf[w][half];
+    uint32_t* lds = reinterpret_cast<uint32_t*>(mine);
+    auto fetch = [&](int64_t pp, uint32_t (&v)[kWords]) {
+        const int64_t f = 2 * pp + half;
+        const bool in = f < count;
+        const uint8_t* g8 = frames + (in ? f : 0) * stride;
+        const uint32_t* g = reinterpret_cast<const uint32_t*>(g8);
+        // the half's IP length (its lanes all read the same dword) bounds the words read
+        const uint32_t hw = g[4];
+        const int ipt = (int)(((hw & 0xFFu) << 8) | ((hw >> 8) & 0xFFu));
+        const int words = in && icrc_len_ok(ipt, stride) ? (14 + ipt + 3) >> 2 : 0;
+#pragma unroll
+        for (int k = 0; k < kWords; ++k) {
+            const int i = l + k * 32;
+            v[k] = i < words ? g[i] : 0u;
+        }
+    };
+    uint32_t cur[kWords];
+    fetch(p, cur);
+    for (;;) {
+#pragma unroll
+        for (int k = 0; k < kWords; ++k) lds[l + k * 32] = cur[k];
+        __builtin_amdgcn_wave_barrier();
+        if (l < kNumMasked) mine[masked_pos(l)] = 0xFF;
+        __builtin_amdgcn_wave_barrier();
+        const int64_t pn = p + step;
+        if (pn < pairs) fetch(pn, cur);
+        const int ipt = ((int)mine[16] << 8) | mine[17];
+        const int64_t f = 2 * p + half;
+        uint32_t c = icrc_half_lane(mine, t, l);
+        if (!icrc_len_ok(ipt, stride)) c = 0u;
+        // XOR-reduce each 32-lane half: quads, half-rows, rows, then row 0 into
+        // row 1 and row 2 into row 3 (lanes 31 and 63 end with the two frames)
+        c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);
+        c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);
+        c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x141, 0xF, 0xF, false);
+        c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x140, 0xF, 0xF, false);
+        c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x142, 0xA, 0xF, false);
+        const uint32_t ca = ~(uint32_t)__builtin_amdgcn_readlane((int)c, 31);
+        const uint32_t cb = ~(uint32_t)__builtin_amdgcn_readlane((int)c, 63);
+        if (lane == 0) out[2 * p] = icrc_len_ok(((int)buf[w][0][16] << 8) | buf[w][0][17], stride) ? ca : 0u;
+        if (lane == 32 && f < count) out[f] = icrc_len_ok(ipt, stride) ? cb : 0u;
+        __builtin_amdgcn_wave_barrier();
+        p = pn;
+        if (p >= pairs) break;
+    }
+}
+
 __device__ __forceinline__ bool is_data_opcode(uint8_t op)
 {
     return op == 0x00 || op == 0x01 || op == 0x02 || op == 0x04 || op == 0x07 || op == 0x08;   // nts.c:314-319
@@ -1157,6 +1289,8 @@ uint32_t host_seg[kSeg][2][16];
 uint32_t host_segb[kSeg][256];
 uint32_t host_lane_shift[8][16][kWave];
 uint32_t host_lane16[8][16][kWave];
+uint32_t host_seg34[kSeg2][2][16];
+uint32_t host_lane_shift32[8][16][32];
 uint32_t host_var[5 + kVarBytes][2][16];
 uint32_t host_z1024[8][16];
 bool g_tables_ready[64];
@@ -1194,6 +1328,18 @@ int ensure_tables()
                 x = zeros_append(x, kSeg);
             }
         }
+    // the paired ICRC (k_icrc_pair): 34-byte segments, Z_{34 (31 - lane')}
+    for (int j = 0; j < kSeg2; ++j)
+        for (int h = 0; h < 2; ++h)
+            for (uint32_t v = 0; v < 16; ++v) host_seg34[j][h][v] = zeros_append(host_tab[v << (4 * h)], kSeg2 - 1 - j);
+    for (int n = 0; n < 8; ++n)
+        for (uint32_t v = 0; v < 16; ++v) {
+            uint32_t x = v << (4 * n);
+            for (int l = 31; l >= 0; --l) {
+                host_lane_shift32[n][v][l] = x;
+                x = zeros_append(x, kSeg2);
+            }
+        }
     // egress by linearity (k_egress): Z_{16 (63 - lane)}, each variable header
     // byte's contribution shifted to the message end, and Z_1024
     for (int n = 0; n < 8; ++n)
@@ -1220,6 +1366,8 @@ int ensure_tables()
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane16), host_lane16, sizeof(host_lane16));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_var), host_var, sizeof(host_var));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_z1024), host_z1024, sizeof(host_z1024));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg34), host_seg34, sizeof(host_seg34));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane_shift32), host_lane_shift32, sizeof(host_lane_shift32));
     if (e != hipSuccess) return (int)e;
     if (dev >= 0 && dev < 64) g_tables_ready[dev] = true;
     return 0;
@@ -1298,6 +1446,20 @@ int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* o
         (int64_t)num_cus() * blocks_per_cu("INCCL_ICRC_BLOCKS_PER_CU", waves == 16 ? 2 : (byte_tables ? 2 : 3));
     const int grid = (int)(blocks < cap ? blocks : cap);
     hipStream_t st = (hipStream_t)stream;
+    // two frames per wave (k_icrc_pair, 49.0 vs 52.8-54.9 us per 131 072 frames);
+    // $INCCL_ICRC_PAIR=0 selects one frame per wave (A/B)
+    static const bool pair = [] {
+        const char* e = getenv("INCCL_ICRC_PAIR");
+        return !(e && atoi(e) == 0);
+    }();
+    if (pair && !byte_tables) {
+        // 8-wave blocks: 2 x 1152 B of staging per wave + 20.6 KiB of tables = 39 KiB
+        const int64_t pairs = ((int64_t)count + 1) / 2, need = (pairs + 7) / 8;
+        const int64_t pcap = (int64_t)num_cus() * 4;   // four per CU: 32 waves
+        hipLaunchKernelGGL((k_icrc_pair<8>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0, st, frames,
+                           (int64_t)stride, (int64_t)count, out);
+        return (int)hipGetLastError();
+    }
     if (byte_tables)
         hipLaunchKernelGGL((k_icrc<true, 8>), dim3(grid), dim3(kWave * 8), 0, st, frames, (int64_t)stride, (int64_t)count, out);
     else if (waves == 16)
