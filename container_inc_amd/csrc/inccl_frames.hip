@@ -500,7 +500,7 @@ __device__ __forceinline__ void payload16(const uint8_t* fr, uint32_t wf, int la
     }
 }
 
-template <int kApplyFrames>
+template <int kApplyFrames, bool kNtAgg = true>
 __global__ __launch_bounds__(kWave * 16) void k_ingress_apply(InccSwitchState s,
                                                                          const uint8_t* __restrict__ frames,
                                                                          int64_t stride, int64_t count,
@@ -639,7 +639,14 @@ __global__ __launch_bounds__(kWave * 16) void k_ingress_apply(InccSwitchState s,
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[k][j] += pq[j];
         }
-        reinterpret_cast<u4*>(s.agg + (size_t)slot * kLanes)[lane] = u4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
+        {
+            const u4 o = u4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
+            u4* dst = reinterpret_cast<u4*>(s.agg + (size_t)slot * kLanes) + lane;
+            if constexpr (kNtAgg)   // non-temporal: 1.3 us off egress (profiles/r03/store_policy/)
+                __builtin_nontemporal_store(o, dst);
+            else
+                *dst = o;
+        }
         // clear_state_data(psn + WINDOW) when the PSN completes in this batch
         // (nts.c:235-242, :367): slot psn + slots/2, which no frame of the batch
         // touches (a batch's PSNs are less than slots/2 apart).  Its bitmap, degree
@@ -1077,6 +1084,7 @@ __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState 
 // instructions, and every store is predicated on the lane (exec mask), not
 // branched around.
 // ---------------------------------------------------------------------------
+constexpr int kAuxNt = 2;   // buffer instruction cache policy: nt (streaming, not re-read)
 constexpr int kOobOffset = 0x7FFFFFF0;   // past any row: a buffer store there is dropped
 
 // egress_fetch with the RETH words through a buffer resource (lanes past
@@ -1107,7 +1115,7 @@ __device__ __forceinline__ EgressIn egress_fetch_fixed(const InccSwitchState& s,
     return e;
 }
 
-template <int kFan, bool kOut16, class L>
+template <int kFan, bool kOut16, int kAux, class L>
 __device__ __forceinline__ void egress_emit_fixed(const EgressIn& e, const uint8_t (*himg)[kHdrImg],
                                                   uint8_t* __restrict__ out, int64_t out_stride,
                                                   int32_t* __restrict__ out_len, const L& t, int64_t f, int lane)
@@ -1197,23 +1205,23 @@ __device__ __forceinline__ void egress_emit_fixed(const EgressIn& e, const uint8
                                       : u4{pc0, (a[3] >> 16) | ((crc & 0xFFFFu) << 16), crc >> 16, 0u};
         const int ho = sh ? 16 * lane : kOobOffset, po = act_c ? 16 * (hchunks + lane) : kOobOffset;
         if (kOut16) {
-            __builtin_amdgcn_raw_buffer_store_b128(h, orow, ho, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(v, orow, po, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(h, orow, ho, 0, kAux);
+            __builtin_amdgcn_raw_buffer_store_b128(v, orow, po, 0, kAux);
         } else {
-            __builtin_amdgcn_raw_buffer_store_b32(h.x, orow, ho, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(h.y, orow, ho + 4, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(h.z, orow, ho + 8, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(h.w, orow, ho + 12, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(v.x, orow, po, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(v.y, orow, po + 4, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(v.z, orow, po + 8, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(h.x, orow, ho, 0, kAux);
+            __builtin_amdgcn_raw_buffer_store_b32(h.y, orow, ho + 4, 0, kAux);
+            __builtin_amdgcn_raw_buffer_store_b32(h.z, orow, ho + 8, 0, kAux);
+            __builtin_amdgcn_raw_buffer_store_b32(h.w, orow, ho + 12, 0, kAux);
+            __builtin_amdgcn_raw_buffer_store_b32(v.x, orow, po, 0, kAux);
+            __builtin_amdgcn_raw_buffer_store_b32(v.y, orow, po + 4, 0, kAux);
+            __builtin_amdgcn_raw_buffer_store_b32(v.z, orow, po + 8, 0, kAux);
             // lane 63 stops at the frame's 4-byte-rounded end
-            __builtin_amdgcn_raw_buffer_store_b32(v.w, orow, lane < kWave - 1 ? po + 12 : kOobOffset, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(v.w, orow, lane < kWave - 1 ? po + 12 : kOobOffset, 0, kAux);
         }
     }
 }
 
-template <int kFan, bool kOut16, int kEgW>
+template <int kFan, bool kOut16, int kEgW, int kAux>
 __device__ __forceinline__ void egress_fixed_body(InccSwitchState s,
                                                                       const uint8_t* __restrict__ in_frames,
                                                                       int64_t in_stride, int64_t count,
@@ -1255,12 +1263,12 @@ __device__ __forceinline__ void egress_fixed_body(InccSwitchState s,
     for (;;) {
         int64_t fn = next();
         b = egress_fetch_fixed<kFan>(s, in_frames, in_stride, ports, action, psns, clamp(fn), lane);
-        egress_emit_fixed<kFan, kOut16>(a, himg, out, out_stride, out_len, t, f, lane);
+        egress_emit_fixed<kFan, kOut16, kAux>(a, himg, out, out_stride, out_len, t, f, lane);
         f = fn;
         if (f >= count) break;
         fn = next();
         a = egress_fetch_fixed<kFan>(s, in_frames, in_stride, ports, action, psns, clamp(fn), lane);
-        egress_emit_fixed<kFan, kOut16>(b, himg, out, out_stride, out_len, t, f, lane);
+        egress_emit_fixed<kFan, kOut16, kAux>(b, himg, out, out_stride, out_len, t, f, lane);
         f = fn;
         if (f >= count) break;
     }
@@ -1273,10 +1281,10 @@ __device__ __forceinline__ void egress_fixed_body(InccSwitchState s,
         int32_t *__restrict__ out_len
 // 8-wave blocks, three per CU = 24 waves: the measured optimum (profiles/r03/egress_waves/: 8 / 16 / 24 / 28
 // waves per CU = 95.5 / 74.8 / 71.0 / 82-83 us)
-template <int kFan, bool kOut16>
+template <int kFan, bool kOut16, int kAux = 0>
 __global__ __launch_bounds__(kWave * 8) void k_egress_fixed(INCCL_EGRESS_FIXED_ARGS)
 {
-    egress_fixed_body<kFan, kOut16, 8>(s, in_frames, in_stride, count, ports, action, psns, tmpl, out, out_stride,
+    egress_fixed_body<kFan, kOut16, 8, kAux>(s, in_frames, in_stride, count, ports, action, psns, tmpl, out, out_stride,
                                        out_len);
 }
 #undef INCCL_EGRESS_FIXED_ARGS
@@ -1489,6 +1497,11 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
         const int v = e ? atoi(e) : 2;
         return (v == 1 || v == 4 || v == 8) ? v : 2;
     }();
+    // $INCCL_APPLY_NT=0: plain aggregate stores (A/B of the non-temporal default)
+    static const bool apply_nt = [] {
+        const char* e = getenv("INCCL_APPLY_NT");
+        return !(e && atoi(e) == 0);
+    }();
     const int64_t waves = ((int64_t)count + apply_frames - 1) / apply_frames;
     if (apply_frames == 1)
         hipLaunchKernelGGL(k_ingress_apply<1>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
@@ -1496,6 +1509,9 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
     else if (apply_frames == 4)
         hipLaunchKernelGGL(k_ingress_apply<4>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
                            (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
+    else if (apply_frames == 2 && !apply_nt)
+        hipLaunchKernelGGL((k_ingress_apply<2, false>), dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s,
+                           frames, (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
     else if (apply_frames == 2)
         hipLaunchKernelGGL(k_ingress_apply<2>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
                            (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
@@ -1532,13 +1548,27 @@ int inccl_k_switch_egress(const InccSwitchState* s, const uint8_t* in_frames, si
         return e && atoi(e) != 0;
     }();
     const bool o16 = ((out_stride & 15) == 0) && (((uintptr_t)out & 15) == 0);
+    // non-temporal output stores (the frames are not re-read here): egress 65.3 vs
+    // 71.0 us (sc1 70.2-70.4, sc1|nt 67.6-68.0), and the next batch's apply 55.5 vs
+    // 65.2 us, no longer behind 144 MB of dirty lines (profiles/r03/store_policy/);
+    // $INCCL_EGRESS_NT=0 for A/B
+    static const bool nt = [] {
+        const char* e = getenv("INCCL_EGRESS_NT");
+        return !(e && atoi(e) == 0);
+    }();
     const dim3 g(eg), b(kWave * kEgressWaves);
     const int64_t is = (int64_t)in_stride, os = (int64_t)out_stride, n = (int64_t)count;
 #define INCCL_EGRESS_FIXED(F)                                                                                   \
     case F:                                                                                                     \
-        if (o16)                                                                                                \
+        if (o16 && nt)                                                                                          \
+            hipLaunchKernelGGL((k_egress_fixed<F, true, kAuxNt>), g, b, 0, st, *s, in_frames, is, n, ports,     \
+                               action, psns, tmpl, out, os, out_len);                                           \
+        else if (o16)                                                                                           \
             hipLaunchKernelGGL((k_egress_fixed<F, true>), g, b, 0, st, *s, in_frames, is, n, ports, action,    \
                                psns, tmpl, out, os, out_len);                                                   \
+        else if (nt)                                                                                            \
+            hipLaunchKernelGGL((k_egress_fixed<F, false, kAuxNt>), g, b, 0, st, *s, in_frames, is, n, ports,    \
+                               action, psns, tmpl, out, os, out_len);                                           \
         else                                                                                                    \
             hipLaunchKernelGGL((k_egress_fixed<F, false>), g, b, 0, st, *s, in_frames, is, n, ports, action,   \
                                psns, tmpl, out, os, out_len);                                                   \
