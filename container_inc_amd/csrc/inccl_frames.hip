@@ -41,6 +41,8 @@ constexpr int kFrameMax = 1152;       // staged frame bytes (>= 1098)
 constexpr int kWavesPerBlock = 4;
 constexpr int kEgressWaves = 8;       // 512-lane blocks, two per CU, persistent grid
 constexpr int kLanes = 256;           // int32 lanes per packet (nts.c:55)
+constexpr int kAuxNt = 2;   // buffer instruction cache policy: nt (streaming, not re-read)
+constexpr int kOobOffset = 0x7FFFFFF0;   // past any row: a buffer store there is dropped
 
 __device__ uint32_t g_seg[kSeg][2][16];       // [byte j][nibble][value] = Z_{16-j}(T[value << 4 nibble]), T = util.c:141-150
 __device__ uint32_t g_segb[kSeg][256];        // [byte j][value] = Z_{16-j}(T[value])
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __res
 }
 
 // ---------------------------------------------------------------------------
-// ICRC, two frames per wave (the default; $INCCL_ICRC_PAIR=0: k_icrc): lanes 0-31 take frame 2p,
+// ICRC, two frames per wave ($INCCL_ICRC_DIRECT=0; $INCCL_ICRC_PAIR=0: k_icrc): lanes 0-31 take frame 2p,
 // lanes 32-63 frame 2p+1, each lane 34 bytes of the 1088-byte window (32 x 34).
 // Per frame: 34 x 2 nibble lookups over 32 lanes (38 lookup instructions per
 // frame, against 42), a 16 KiB lane-shift table (Z_{34 (31 - lane')}), and one
@@ -268,18 +270,12 @@ struct CrcLdsPair {
 
 // ICRC of the frame of this lane's half (staged at `fr`, masked bytes 0xFF);
 // returns the raw (pre-reduction) contribution of this lane
-__device__ __forceinline__ uint32_t icrc_half_lane(const uint8_t* fr, const CrcLdsPair& t, int l)
+// The segment's contribution from its frame dwords dw[k] = frame dword (o >> 2) + k
+// (o = the segment's first frame byte; masked bytes already 0xFF)
+__device__ __forceinline__ uint32_t icrc_half_regs(const uint32_t (&dw)[10], int o, const CrcLdsPair& t, int l)
 {
-    const int ip_total = ((int)fr[16] << 8) | fr[17];
-    const int lead = kWin - ip_total;
-    const int o = 10 + l * kSeg2 - lead;                 // frame offset of this lane's first byte
     uint32_t c = 0;
     if (o + kSeg2 > 10) {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(fr);
-        const int d0 = o >> 2;
-        uint32_t dw[10];
-#pragma unroll
-        for (int k = 0; k < 10; ++k) dw[k] = d0 + k >= 0 ? w[d0 + k] : 0u;
         const uint32_t sh = (uint32_t)o & 3u;
         uint32_t a[9];
 #pragma unroll
@@ -316,6 +312,19 @@ __device__ __forceinline__ uint32_t icrc_half_lane(const uint8_t* fr, const CrcL
         c = xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
     }
     return c;
+}
+
+__device__ __forceinline__ uint32_t icrc_half_lane(const uint8_t* fr, const CrcLdsPair& t, int l)
+{
+    const int ip_total = ((int)fr[16] << 8) | fr[17];
+    const int lead = kWin - ip_total;
+    const int o = 10 + l * kSeg2 - lead;                 // frame offset of this lane's first byte
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(fr);
+    const int d0 = o >> 2;
+    uint32_t dw[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) dw[k] = d0 + k >= 0 && o + kSeg2 > 10 ? w[d0 + k] : 0u;
+    return icrc_half_regs(dw, o, t, l);
 }
 
 template <int kW>
@@ -378,6 +387,139 @@ __global__ __launch_bounds__(kWave* kW) void k_icrc_pair(const uint8_t* __restri
         __builtin_amdgcn_wave_barrier();
         p = pn;
         if (p >= pairs) break;
+    }
+}
+
+// masked_pos() as a bitmap of frame byte positions (10-13, 15, 22, 24, 25, 40, 41, 46)
+constexpr uint64_t kIcrcMaskBits = (1ull << 10) | (1ull << 11) | (1ull << 12) | (1ull << 13) | (1ull << 15) |
+                                   (1ull << 22) | (1ull << 24) | (1ull << 25) | (1ull << 40) | (1ull << 41) |
+                                   (1ull << 46);
+
+// OR the mask bytes into dw[k] = frame dword d0 + k, straight-line: the bitmap
+// shifted to byte 4 d0, and each nibble spread to four byte masks (bit i -> byte i)
+__device__ __forceinline__ void icrc_mask_regs(uint32_t (&dw)[10], int d0)
+{
+    const int s4 = 4 * d0;   // -28 .. 44 where any mask byte is in reach
+    const uint64_t x = d0 >= 12 ? 0ull : (s4 >= 0 ? kIcrcMaskBits >> s4 : kIcrcMaskBits << (-s4));
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        const uint32_t b = __builtin_amdgcn_ubfe(k < 8 ? lo : hi, 4 * (k & 7), 4);
+        const uint32_t m = (b * 0x00204081u) & 0x01010101u;
+        dw[k] |= (m << 8) - m;
+    }
+}
+
+// ICRC, two frames per wave without LDS staging (the default): each lane loads its own 34-byte
+// segment straight from the frame (two dwordx4 + two dword buffer loads at the
+// segment's dword offset), the mask bytes are ORed in registers, and LDS holds
+// only the tables.  Every memory instruction runs on every pass (a frame past
+// the end, or malformed, gets a zero-size buffer: its loads return 0 and its
+// store is dropped), so the waits stay one pass deep.  39 VGPRs and 20.7 KiB of
+// LDS (k_icrc_pair: 50 and 39 KiB).  Same window, masks and
+// results as k_icrc_pair.  Out-of-range segment words: a load partly before
+// the frame covers only bytes below 10 (zeroed or masked), and the segment's
+// last byte o + 33 <= 14 + ip_total - 5 keeps both dwordx4 inside the frame.
+template <int kW, int kPP>
+__global__ __launch_bounds__(kWave* kW) void k_icrc_direct(const uint8_t* __restrict__ frames, int64_t stride,
+                                                           int64_t count, uint32_t* __restrict__ out)
+{
+    __shared__ CrcLdsPair t;
+    for (int i = threadIdx.x; i < kSeg2 * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg34[0][0][0])[i];
+    for (int i = threadIdx.x; i < 8 * 16 * 32; i += blockDim.x) (&t.lane_sh[0][0][0])[i] = (&g_lane_shift32[0][0][0])[i];
+    __syncthreads();
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    const int half = lane >> 5, l = lane & 31;
+    // a wave takes kPP consecutive pairs per pass (group q = pairs kPP q .. kPP q + kPP - 1),
+    // all fetched one pass ahead: kPP pairs of loads in flight while a group's CRCs run
+    const int64_t pairs = (count + 1) >> 1, groups = (pairs + kPP - 1) / kPP, step = (int64_t)gridDim.x * kW;
+    int64_t q = (int64_t)blockIdx.x * kW + w;
+    if (q >= groups) return;
+    // one buffer per pair (wave-uniform): its two rows, one for a last odd frame, none past the end
+    auto pair_rsrc = [&](int64_t pp) {
+        const int64_t rows = count - 2 * pp;
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(frames) + (rows > 0 ? 2 * pp : 0) * stride, 0,
+                                                 rows >= 2 ? (int)(2 * stride) : rows == 1 ? (int)stride : 0, 0x00020000);
+    };
+    const int row_off = half * (int)stride;
+    // bytes 16-19 of this half's frame (the IP total length), 0 past the end
+    auto hdr = [&](int64_t pp) -> uint32_t {
+        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(pair_rsrc(pp), stride >= 20 ? row_off + 16 : kOobOffset, 0, 0);
+    };
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    auto fetch = [&](int64_t pp, uint32_t h, uint32_t (&dw)[10], int& o, bool& ok) {
+        const int64_t f = 2 * pp + half;
+        const int ipt = (int)(((h & 0xFFu) << 8) | ((h >> 8) & 0xFFu));
+        ok = f < count && icrc_len_ok(ipt, stride);
+        o = 10 + l * kSeg2 - (kWin - ipt);
+        // the segment's dwords, inside this frame's row: a dword before the row (a
+        // lane whose segment starts before byte 10) or past the frame's last dword
+        // reads 0; the two dwordx4 never reach past the frame (header comment)
+        const int d = o >> 2, words = (14 + ipt + 3) >> 2;
+        const __amdgpu_buffer_rsrc_t rs = pair_rsrc(pp);
+        // (each offset a VGPR the compiler cannot see through: a select it could
+        // split into two loads on two paths would bring back the joined waits)
+        auto at = [&](int k) {
+            return (int)opaque_u32((uint32_t)(ok && d + k >= 0 && d + k < words ? row_off + 4 * (d + k) : kOobOffset));
+        };
+        const u4 a = __builtin_amdgcn_raw_buffer_load_b128(
+            rs, (int)opaque_u32((uint32_t)(ok && d >= 0 ? row_off + 4 * d : kOobOffset)), 0, 0);
+        const u4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, at(4), 0, 0);
+        dw[8] = __builtin_amdgcn_raw_buffer_load_b32(rs, at(8), 0, 0);
+        dw[9] = __builtin_amdgcn_raw_buffer_load_b32(rs, at(9), 0, 0);
+        dw[0] = a.x; dw[1] = a.y; dw[2] = a.z; dw[3] = a.w;
+        dw[4] = b.x; dw[5] = b.y; dw[6] = b.z; dw[7] = b.w;
+    };
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(4 * count), 0x00020000);
+    uint32_t cur[kPP][10], hn[kPP];
+    int o[kPP];
+    bool ok[kPP];
+#pragma unroll
+    for (int j = 0; j < kPP; ++j) fetch(kPP * q + j, hdr(kPP * q + j), cur[j], o[j], ok[j]);
+#pragma unroll
+    for (int j = 0; j < kPP; ++j) hn[j] = hdr(kPP * (q + step) + j);
+    // dropped stores: the loop is entered with its back edge's memory history
+#pragma unroll
+    for (int j = 0; j < kPP; ++j) __builtin_amdgcn_raw_buffer_store_b32(0u, ors, kOobOffset, 0, 0);
+    for (;;) {
+        const int64_t qn = q + step;
+        uint32_t nxt[kPP][10];
+        int on[kPP];
+        bool okn[kPP];
+#pragma unroll
+        for (int j = 0; j < kPP; ++j) fetch(kPP * qn + j, hn[j], nxt[j], on[j], okn[j]);
+#pragma unroll
+        for (int j = 0; j < kPP; ++j) hn[j] = hdr(kPP * (qn + step) + j);
+        uint32_t c[kPP];
+#pragma unroll
+        for (int j = 0; j < kPP; ++j) {
+            icrc_mask_regs(cur[j], o[j] >> 2);
+            c[j] = ok[j] ? icrc_half_regs(cur[j], o[j], t, l) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kPP; ++j) {
+            uint32_t x = c[j];
+            x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
+            x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);
+            x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);
+            x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);
+            x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+            const uint32_t ca = ~(uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+            const uint32_t cb = ~(uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+            // lane 0 writes frame 2 pp, lane 32 frame 2 pp + 1 (past the end: dropped)
+            const int64_t pp = kPP * q + j;
+            __builtin_amdgcn_raw_buffer_store_b32(ok[j] ? (half ? cb : ca) : 0u, ors,
+                                                  l == 0 && pp < pairs ? (int)(4 * (2 * pp + half)) : kOobOffset, 0, 0);
+        }
+        q = qn;
+        if (q >= groups) break;
+#pragma unroll
+        for (int j = 0; j < kPP; ++j) {
+#pragma unroll
+            for (int k = 0; k < 10; ++k) cur[j][k] = nxt[j][k];
+            o[j] = on[j];
+            ok[j] = okn[j];
+        }
     }
 }
 
@@ -1084,8 +1226,6 @@ __global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState 
 // instructions, and every store is predicated on the lane (exec mask), not
 // branched around.
 // ---------------------------------------------------------------------------
-constexpr int kAuxNt = 2;   // buffer instruction cache policy: nt (streaming, not re-read)
-constexpr int kOobOffset = 0x7FFFFFF0;   // past any row: a buffer store there is dropped
 
 // egress_fetch with the RETH words through a buffer resource (lanes past
 // 4 fan_in read out of range and get 0): no predicated load
@@ -1404,7 +1544,7 @@ int blocks_per_cu(const char* env, int dflt)
 {
     const char* e = getenv(env);
     const int v = e ? atoi(e) : 0;
-    return (v >= 1 && v <= 3) ? v : dflt;
+    return (v >= 1 && v <= 8) ? v : dflt;
 }
 
 // waves per apply workgroup: 4 by default, $INCCL_APPLY_WPB = 1, 2, 8 or 16 for sweeps
@@ -1460,6 +1600,30 @@ int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* o
         const char* e = getenv("INCCL_ICRC_PAIR");
         return !(e && atoi(e) == 0);
     }();
+    // two frames per wave without LDS staging (k_icrc_direct), the default: 47.9-49.8 vs
+    // 49.2-54.4 us for k_icrc_pair over this round's runs (profiles/r03/icrc_direct/);
+    // $INCCL_ICRC_DIRECT=0 selects k_icrc_pair, $INCCL_ICRC_PAIRS_PER_PASS=2 two pairs a
+    // pass (50.9-51.4 us: more bytes in flight do not help)
+    static const bool direct = [] {
+        const char* e = getenv("INCCL_ICRC_DIRECT");
+        return !(e && atoi(e) == 0);
+    }();
+    if (pair && direct && !byte_tables && count < (1ull << 29) && stride < (1ull << 29)) {   // 32-bit offsets
+        const int64_t pairs = ((int64_t)count + 1) / 2, need = (pairs + 7) / 8;
+        const int64_t pcap = (int64_t)num_cus() * blocks_per_cu("INCCL_ICRC_BLOCKS_PER_CU", 4);
+        static const int pp = [] {
+            const char* e = getenv("INCCL_ICRC_PAIRS_PER_PASS");
+            return e && atoi(e) == 2 ? 2 : 1;
+        }();
+        const int64_t groups = (pairs + pp - 1) / pp, gneed = (groups + 7) / 8;
+        if (pp == 1)
+            hipLaunchKernelGGL((k_icrc_direct<8, 1>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0, st,
+                               frames, (int64_t)stride, (int64_t)count, out);
+        else
+            hipLaunchKernelGGL((k_icrc_direct<8, 2>), dim3((unsigned)(gneed < pcap ? gneed : pcap)), dim3(kWave * 8), 0,
+                               st, frames, (int64_t)stride, (int64_t)count, out);
+        return (int)hipGetLastError();
+    }
     if (pair && !byte_tables) {
         // 8-wave blocks: 2 x 1152 B of staging per wave + 20.6 KiB of tables = 39 KiB
         const int64_t pairs = ((int64_t)count + 1) / 2, need = (pairs + 7) / 8;

@@ -64,6 +64,25 @@ def test_icrc_any_length(gpu, orc):
         assert int(c) == orc.icrc(f), ipt
 
 
+@pytest.mark.parametrize("stride,count", [(1100, 7), (1100, 1), (1104, 9), (1152, 5), (1240, 3)])
+def test_icrc_row_strides_odd_counts(gpu, orc, stride, count):
+    """Rows that are 4- but not 16-byte aligned, rows that end 2 bytes after a
+    1098-byte frame (stride 1100), and odd frame counts (the two-frames-per-wave
+    kernels' lone last frame).  Every ICRC against the oracle."""
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(stride + count)
+    lens = [1084, 1068] + [int(x) for x in rng.integers(28, 1085, max(count - 2, 0))]
+    frames = []
+    for ipt in lens[:count]:
+        f = bytearray(rng.integers(0, 256, 14 + ipt, dtype=np.uint8).tobytes())
+        f[16], f[17] = ipt >> 8, ipt & 0xFF
+        frames.append(bytes(f))
+    got = inccl.icrc_frames(_rows(frames, gpu, stride)).cpu().numpy().view(np.uint32)
+    assert len(got) == count
+    for f, c in zip(frames, got):
+        assert int(c) == orc.icrc(f), len(f)
+
+
 def _templates(fan_in):
     from container_inc_amd.inccl import FRAME_TEMPLATE_DTYPE
     t = np.zeros(fan_in, FRAME_TEMPLATE_DTYPE)
