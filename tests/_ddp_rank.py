@@ -67,9 +67,10 @@ def _bits(t):
     return t.detach().cpu().numpy().view(np.uint32)
 
 
-def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine="p2p"):
+def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine="p2p", boot_port=None):
     """dtype "bf16": a bf16 model, so DDP's buckets are bf16 (inccl_allreduce_bf16);
-    as_view: gradient_as_bucket_view=True (the grads are views of the buckets)."""
+    as_view: gradient_as_bucket_view=True (the grads are views of the buckets);
+    boot_port: the library bootstrap's port, chosen free by the parent (gloo uses `port`)."""
     try:
         sys.path.insert(0, ROOT)
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
@@ -86,7 +87,7 @@ def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine=
         if mode == "gpu":
             torch.cuda.set_device(0)
             dev = torch.device("cuda", 0)
-            grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port + 1, device=0)
+            grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=boot_port, device=0)
             assert grp is not None, "group create failed"
             comm = inccl.inccl_communicator_create(grp, 0)
             assert comm is not None and comm.engine == engine, comm and comm.engine

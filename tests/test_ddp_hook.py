@@ -9,20 +9,28 @@ import socket
 import pytest
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _free_ports(n):
+    """n distinct free ports, all held until every one is chosen.  (The GPU
+    variant once derived the bootstrap's port as gloo's + 1, unchecked: gloo's
+    own peer sockets sit in the same ephemeral range, and one took it.)"""
+    socks = []
+    for _ in range(n):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+    ports = [s.getsockname()[1] for s in socks]
+    for s in socks:
+        s.close()
+    return ports
 
 
 def run_world(world, mode, timeout, dtype="f32", as_view=False, engine="p2p"):
     import _ddp_rank
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    ps = [ctx.Process(target=_ddp_rank.run, args=(r, world, port, q, mode, 2, dtype, as_view, engine)) for r in range(world)]
+    port, boot_port = _free_ports(2)
+    ps = [ctx.Process(target=_ddp_rank.run, args=(r, world, port, q, mode, 2, dtype, as_view, engine, boot_port))
+          for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=timeout) for _ in range(world))
