@@ -266,6 +266,7 @@ __device__ uint32_t g_lane_shift32[8][16][32];      // [nibble][value][lane'] = 
 struct CrcLdsPair {
     uint32_t seg[kSeg2][2][16];
     uint32_t lane_sh[8][16][32];
+    uint32_t spread[16];   // k_icrc_direct<.., kMaskLds>: nibble -> byte mask (bit i -> byte i)
 };
 
 // ICRC of the frame of this lane's half (staged at `fr`, masked bytes 0xFF);
@@ -410,6 +411,17 @@ __device__ __forceinline__ void icrc_mask_regs(uint32_t (&dw)[10], int d0)
     }
 }
 
+// icrc_mask_regs with the nibble -> byte-mask spread from a 16-entry LDS table
+// (3 VALU + 1 LDS read per dword instead of 6 VALU; $INCCL_ICRC_MASK_LDS=1)
+__device__ __forceinline__ void icrc_mask_regs_lds(uint32_t (&dw)[10], int d0, const CrcLdsPair& t)
+{
+    const int s4 = 4 * d0;
+    const uint64_t x = d0 >= 12 ? 0ull : (s4 >= 0 ? kIcrcMaskBits >> s4 : kIcrcMaskBits << (-s4));
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) dw[k] |= t.spread[__builtin_amdgcn_ubfe(k < 8 ? lo : hi, 4 * (k & 7), 4)];
+}
+
 // ICRC, two frames per wave without LDS staging (the default): each lane loads its own 34-byte
 // segment straight from the frame (two dwordx4 + two dword buffer loads at the
 // segment's dword offset), the mask bytes are ORed in registers, and LDS holds
@@ -420,13 +432,17 @@ __device__ __forceinline__ void icrc_mask_regs(uint32_t (&dw)[10], int d0)
 // results as k_icrc_pair.  Out-of-range segment words: a load partly before
 // the frame covers only bytes below 10 (zeroed or masked), and the segment's
 // last byte o + 33 <= 14 + ip_total - 5 keeps both dwordx4 inside the frame.
-template <int kW, int kPP>
+template <int kW, int kPP, bool kMaskLds = false>
 __global__ __launch_bounds__(kWave* kW) void k_icrc_direct(const uint8_t* __restrict__ frames, int64_t stride,
                                                            int64_t count, uint32_t* __restrict__ out)
 {
     __shared__ CrcLdsPair t;
     for (int i = threadIdx.x; i < kSeg2 * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg34[0][0][0])[i];
     for (int i = threadIdx.x; i < 8 * 16 * 32; i += blockDim.x) (&t.lane_sh[0][0][0])[i] = (&g_lane_shift32[0][0][0])[i];
+    if (threadIdx.x < 16) {
+        const uint32_t m = (threadIdx.x * 0x00204081u) & 0x01010101u;
+        t.spread[threadIdx.x] = (m << 8) - m;
+    }
     __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     const int half = lane >> 5, l = lane & 31;
@@ -493,7 +509,10 @@ __global__ __launch_bounds__(kWave* kW) void k_icrc_direct(const uint8_t* __rest
         uint32_t c[kPP];
 #pragma unroll
         for (int j = 0; j < kPP; ++j) {
-            icrc_mask_regs(cur[j], o[j] >> 2);
+            if (kMaskLds)
+                icrc_mask_regs_lds(cur[j], o[j] >> 2, t);
+            else
+                icrc_mask_regs(cur[j], o[j] >> 2);
             c[j] = ok[j] ? icrc_half_regs(cur[j], o[j], t, l) : 0u;
         }
 #pragma unroll
@@ -1616,7 +1635,14 @@ int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* o
             return e && atoi(e) == 2 ? 2 : 1;
         }();
         const int64_t groups = (pairs + pp - 1) / pp, gneed = (groups + 7) / 8;
-        if (pp == 1)
+        static const bool mask_lds = [] {
+            const char* e = getenv("INCCL_ICRC_MASK_LDS");
+            return e && atoi(e) != 0;
+        }();
+        if (pp == 1 && mask_lds)
+            hipLaunchKernelGGL((k_icrc_direct<8, 1, true>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0,
+                               st, frames, (int64_t)stride, (int64_t)count, out);
+        else if (pp == 1)
             hipLaunchKernelGGL((k_icrc_direct<8, 1>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0, st,
                                frames, (int64_t)stride, (int64_t)count, out);
         else
