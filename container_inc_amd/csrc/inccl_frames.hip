@@ -411,8 +411,9 @@ __device__ __forceinline__ void icrc_mask_regs(uint32_t (&dw)[10], int d0)
     }
 }
 
-// icrc_mask_regs with the nibble -> byte-mask spread from a 16-entry LDS table
-// (3 VALU + 1 LDS read per dword instead of 6 VALU; $INCCL_ICRC_MASK_LDS=1)
+// icrc_mask_regs with the nibble -> byte-mask spread from a 16-entry LDS table,
+// the default (323 instead of 343 VALU per pair, 10 more LDS reads;
+// $INCCL_ICRC_MASK_LDS=0 selects the VALU spread)
 __device__ __forceinline__ void icrc_mask_regs_lds(uint32_t (&dw)[10], int d0, const CrcLdsPair& t)
 {
     const int s4 = 4 * d0;
@@ -1635,9 +1636,11 @@ int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* o
             return e && atoi(e) == 2 ? 2 : 1;
         }();
         const int64_t groups = (pairs + pp - 1) / pp, gneed = (groups + 7) / 8;
+        // mask bytes spread through a 16-entry LDS table: 46.0-48.2 vs 47.0-50.8 us in
+        // paired runs (profiles/r03/icrc_mask_lds/); $INCCL_ICRC_MASK_LDS=0 for A/B
         static const bool mask_lds = [] {
             const char* e = getenv("INCCL_ICRC_MASK_LDS");
-            return e && atoi(e) != 0;
+            return !(e && atoi(e) == 0);
         }();
         if (pp == 1 && mask_lds)
             hipLaunchKernelGGL((k_icrc_direct<8, 1, true>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0,
