@@ -266,23 +266,27 @@ __device__ uint32_t g_lane_shift32[8][16][32];      // [nibble][value][lane'] = 
 struct CrcLdsPair {
     uint32_t seg[kSeg2][2][16];
     uint32_t lane_sh[8][16][32];
-    uint32_t spread[16];   // k_icrc_direct<.., kMaskLds>: nibble -> byte mask (bit i -> byte i)
+    uint32_t spread[16];   // k_icrc_direct<.., 1>: nibble -> byte mask (bit i -> byte i)
+    uint32_t andor[32][2];   // k_icrc_direct<.., 2>: [nibble | 16 (frame dword <= 2)] -> (AND, OR)
 };
 
 // ICRC of the frame of this lane's half (staged at `fr`, masked bytes 0xFF);
 // returns the raw (pre-reduction) contribution of this lane
 // The segment's contribution from its frame dwords dw[k] = frame dword (o >> 2) + k
 // (o = the segment's first frame byte; masked bytes already 0xFF)
+// kZeroed: dw already holds 0 for every frame byte below 10 (icrc_mask_regs_zero),
+// so neither the zeroing nor the skip of an all-zero segment is needed
+template <bool kZeroed = false>
 __device__ __forceinline__ uint32_t icrc_half_regs(const uint32_t (&dw)[10], int o, const CrcLdsPair& t, int l)
 {
     uint32_t c = 0;
-    if (o + kSeg2 > 10) {
+    if (kZeroed || o + kSeg2 > 10) {
         const uint32_t sh = (uint32_t)o & 3u;
         uint32_t a[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) a[k] = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
         const int nz = 10 - o;
-        if (nz > 0) {
+        if (!kZeroed && nz > 0) {
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
                 const int z = nz - 4 * k;
@@ -400,8 +404,10 @@ constexpr uint64_t kIcrcMaskBits = (1ull << 10) | (1ull << 11) | (1ull << 12) | 
 // shifted to byte 4 d0, and each nibble spread to four byte masks (bit i -> byte i)
 __device__ __forceinline__ void icrc_mask_regs(uint32_t (&dw)[10], int d0)
 {
-    const int s4 = 4 * d0;   // -28 .. 44 where any mask byte is in reach
-    const uint64_t x = d0 >= 12 ? 0ull : (s4 >= 0 ? kIcrcMaskBits >> s4 : kIcrcMaskBits << (-s4));
+    // -28 .. 44 where any mask byte is in reach; a shift of 64 or more (a segment far
+    // before the frame) is clamped to no bits, not left to the hardware's 6-bit shift
+    const int s4 = 4 * d0;
+    const uint64_t x = (d0 >= 12 || d0 <= -16) ? 0ull : (s4 >= 0 ? kIcrcMaskBits >> s4 : kIcrcMaskBits << (-s4));
     const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
@@ -411,16 +417,33 @@ __device__ __forceinline__ void icrc_mask_regs(uint32_t (&dw)[10], int d0)
     }
 }
 
-// icrc_mask_regs with the nibble -> byte-mask spread from a 16-entry LDS table,
-// the default (323 instead of 343 VALU per pair, 10 more LDS reads;
-// $INCCL_ICRC_MASK_LDS=0 selects the VALU spread)
+// icrc_mask_regs with the nibble -> byte-mask spread from a 16-entry LDS table
+// (323 instead of 343 VALU per pair, 10 more LDS reads; $INCCL_ICRC_MASK_LDS=1)
 __device__ __forceinline__ void icrc_mask_regs_lds(uint32_t (&dw)[10], int d0, const CrcLdsPair& t)
 {
     const int s4 = 4 * d0;
-    const uint64_t x = d0 >= 12 ? 0ull : (s4 >= 0 ? kIcrcMaskBits >> s4 : kIcrcMaskBits << (-s4));
+    const uint64_t x = (d0 >= 12 || d0 <= -16) ? 0ull : (s4 >= 0 ? kIcrcMaskBits >> s4 : kIcrcMaskBits << (-s4));
     const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
 #pragma unroll
     for (int k = 0; k < 10; ++k) dw[k] |= t.spread[__builtin_amdgcn_ubfe(k < 8 ? lo : hi, 4 * (k & 7), 4)];
+}
+
+// icrc_mask_regs_lds that also clears frame bytes 0-9 (dwords 0-2; bytes 10-11 of
+// dword 2 are then set by its OR mask): dw = (dw & AND) | OR from a 32-entry table
+// indexed by the dword's mask nibble and a "dword <= 2" bit, so that the CRC needs
+// no per-byte zeroing of the leading bytes: 295 VALU per pair (the default)
+__device__ __forceinline__ void icrc_mask_regs_zero(uint32_t (&dw)[10], int d0, const CrcLdsPair& t)
+{
+    const int s4 = 4 * d0;
+    const uint64_t x = (d0 >= 12 || d0 <= -16) ? 0ull : (s4 >= 0 ? kIcrcMaskBits >> s4 : kIcrcMaskBits << (-s4));
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const int cnt = min(max(3 - d0, 0), 10);           // dwords k with d0 + k <= 2
+    const uint32_t zbits = (1u << cnt) - 1u;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        const uint32_t i = __builtin_amdgcn_ubfe(k < 8 ? lo : hi, 4 * (k & 7), 4) | (((zbits >> k) & 1u) << 4);
+        dw[k] = (dw[k] & t.andor[i][0]) | t.andor[i][1];
+    }
 }
 
 // ICRC, two frames per wave without LDS staging (the default): each lane loads its own 34-byte
@@ -433,16 +456,18 @@ __device__ __forceinline__ void icrc_mask_regs_lds(uint32_t (&dw)[10], int d0, c
 // results as k_icrc_pair.  Out-of-range segment words: a load partly before
 // the frame covers only bytes below 10 (zeroed or masked), and the segment's
 // last byte o + 33 <= 14 + ip_total - 5 keeps both dwordx4 inside the frame.
-template <int kW, int kPP, bool kMaskLds = false>
+template <int kW, int kPP, int kMaskLds = 0>
 __global__ __launch_bounds__(kWave* kW) void k_icrc_direct(const uint8_t* __restrict__ frames, int64_t stride,
                                                            int64_t count, uint32_t* __restrict__ out)
 {
     __shared__ CrcLdsPair t;
     for (int i = threadIdx.x; i < kSeg2 * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg34[0][0][0])[i];
     for (int i = threadIdx.x; i < 8 * 16 * 32; i += blockDim.x) (&t.lane_sh[0][0][0])[i] = (&g_lane_shift32[0][0][0])[i];
-    if (threadIdx.x < 16) {
-        const uint32_t m = (threadIdx.x * 0x00204081u) & 0x01010101u;
-        t.spread[threadIdx.x] = (m << 8) - m;
+    if (threadIdx.x < 32) {
+        const uint32_t m = ((threadIdx.x & 15u) * 0x00204081u) & 0x01010101u;
+        if (threadIdx.x < 16) t.spread[threadIdx.x] = (m << 8) - m;
+        t.andor[threadIdx.x][0] = threadIdx.x & 16u ? 0u : 0xFFFFFFFFu;
+        t.andor[threadIdx.x][1] = (m << 8) - m;
     }
     __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
@@ -510,11 +535,13 @@ __global__ __launch_bounds__(kWave* kW) void k_icrc_direct(const uint8_t* __rest
         uint32_t c[kPP];
 #pragma unroll
         for (int j = 0; j < kPP; ++j) {
-            if (kMaskLds)
+            if (kMaskLds == 2)
+                icrc_mask_regs_zero(cur[j], o[j] >> 2, t);
+            else if (kMaskLds == 1)
                 icrc_mask_regs_lds(cur[j], o[j] >> 2, t);
             else
                 icrc_mask_regs(cur[j], o[j] >> 2);
-            c[j] = ok[j] ? icrc_half_regs(cur[j], o[j], t, l) : 0u;
+            c[j] = ok[j] ? icrc_half_regs<kMaskLds == 2>(cur[j], o[j], t, l) : 0u;
         }
 #pragma unroll
         for (int j = 0; j < kPP; ++j) {
@@ -1636,14 +1663,20 @@ int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* o
             return e && atoi(e) == 2 ? 2 : 1;
         }();
         const int64_t groups = (pairs + pp - 1) / pp, gneed = (groups + 7) / 8;
-        // mask bytes spread through a 16-entry LDS table: 46.0-48.2 vs 47.0-50.8 us in
-        // paired runs (profiles/r03/icrc_mask_lds/); $INCCL_ICRC_MASK_LDS=0 for A/B
-        static const bool mask_lds = [] {
+        // mask bytes and the zeroed leading bytes from one 32-entry (AND, OR) LDS table
+        // (2, the default): 43.6-47.0 vs 48.0-49.2 us for the 16-entry mask table with
+        // per-byte zeroing (1), itself 46.0-48.2 vs 47.0-50.8 us for the VALU spread (0),
+        // in paired runs (profiles/r03/icrc_mask_lds/, icrc_mask_zero/); $INCCL_ICRC_MASK_LDS
+        // selects 0 or 1 for A/B
+        static const int mask_lds = [] {
             const char* e = getenv("INCCL_ICRC_MASK_LDS");
-            return !(e && atoi(e) == 0);
+            return e ? atoi(e) : 2;
         }();
-        if (pp == 1 && mask_lds)
-            hipLaunchKernelGGL((k_icrc_direct<8, 1, true>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0,
+        if (pp == 1 && mask_lds == 2)
+            hipLaunchKernelGGL((k_icrc_direct<8, 1, 2>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0,
+                               st, frames, (int64_t)stride, (int64_t)count, out);
+        else if (pp == 1 && mask_lds == 1)
+            hipLaunchKernelGGL((k_icrc_direct<8, 1, 1>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0,
                                st, frames, (int64_t)stride, (int64_t)count, out);
         else if (pp == 1)
             hipLaunchKernelGGL((k_icrc_direct<8, 1>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0, st,

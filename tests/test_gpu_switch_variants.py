@@ -20,6 +20,7 @@ VARIANTS = {
     "icrc_one_frame_per_wave": {"INCCL_ICRC_DIRECT": "0", "INCCL_ICRC_PAIR": "0"},
     "icrc_two_pairs_per_pass": {"INCCL_ICRC_PAIRS_PER_PASS": "2"},
     "icrc_mask_valu": {"INCCL_ICRC_MASK_LDS": "0"},
+    "icrc_mask_table_byte_zeroing": {"INCCL_ICRC_MASK_LDS": "1"},
     "egress_generic": {"INCCL_EGRESS_GENERIC": "1"},
     "apply_4_frames_8_waves": {"INCCL_APPLY_FRAMES": "4", "INCCL_APPLY_WPB": "8"},
 }
