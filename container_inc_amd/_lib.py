@@ -51,6 +51,9 @@ SIGNATURES = {
     "inccl_group_device": (_I, [_P]),
     "inccl_ipc_max_bytes": (_SZ, []),
     "inccl_group_ipc_max_bytes": (_SZ, [_P]),
+    "inccl_hsa_runtime_release": (_U32, []),
+    "inccl_hsa_runtime_build": (_S, []),
+    "inccl_rccl_version": (_I, [_P, _P]),
     "inccl_group_transport": (_S, [_P]),
     "inccl_comm_stream": (_P, [_P]),
     "inccl_comm_barrier": (_I, [_P]),
@@ -139,6 +142,17 @@ def runtime_libs() -> dict:
                 found["hip_runtime_version"] = v.value
         except OSError:
             pass
+    if "libinccl_amd" in found:
+        # RCCL: the NCCL_VERSION_CODE the library was compiled against and the
+        # ncclGetVersion of the librccl it bound to; the HSA runtime's own ROCm
+        # release (its build string), which sets the IPC bound (csrc/runtime.c)
+        lib = load()
+        c, ld = ctypes.c_int(0), ctypes.c_int(0)
+        if lib.inccl_rccl_version(ctypes.byref(c), ctypes.byref(ld)) == 0:
+            found["rccl_compiled"], found["rccl_loaded"] = c.value, ld.value
+        found["hsa_release"] = int(lib.inccl_hsa_runtime_release())
+        found["hsa_build"] = lib.inccl_hsa_runtime_build().decode(errors="replace")
+        found["ipc_max_bytes"] = int(lib.inccl_ipc_max_bytes())
     return found
 
 

@@ -33,8 +33,7 @@
  * agrees on the smallest over its ranks ($INCCL_IPC_MAX_BYTES overrides). */
 #define INCCL_IPC_MAX_BYTES_DEFAULT (((size_t)2 << 30) - ((size_t)2 << 20))
 #define INCCL_IPC_MAX_BYTES_UNBOUNDED ((size_t)1 << 40)
-const char *inccl_hsa_runtime_path(void);
-unsigned inccl_hsa_build_of(const char *path);
+unsigned inccl_hsa_release_of(const char *build);   /* "..-rocm-rel-7.2-.." -> 702, 0 without the tag */
 size_t inccl_ipc_local_max_bytes(void);
 
 struct inccl_local_hub;

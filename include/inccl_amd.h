@@ -116,13 +116,23 @@ const char *inccl_group_transport(const struct inccl_group *group);
 /* Largest single buffer the IPC engines (p2p, mesh) may share with peers, in
  * bytes.  It follows the HSA runtime the process runs on: PyTorch's bundled
  * ROCr (ROCm 7.0.2) hangs importing a peer allocation above 2 GiB, so 2 GiB -
- * 2 MiB there; no bound under a ROCr of ROCm 7.2 or later (/opt/rocm);
- * $INCCL_IPC_MAX_BYTES overrides.  inccl_ipc_max_bytes: this process;
+ * 2 MiB there; no bound under a ROCr that reports ROCm 7.2 or later
+ * (/opt/rocm; inccl_hsa_runtime_release); $INCCL_IPC_MAX_BYTES overrides
+ * (whole MiB, at least 1 MiB).  inccl_ipc_max_bytes: this process;
  * inccl_group_ipc_max_bytes: the smallest over the group's ranks, agreed at
  * creation -- a bucket whose IPC buffer would exceed it is refused on every
  * rank alike. */
 size_t inccl_ipc_max_bytes(void);
 size_t inccl_group_ipc_max_bytes(const struct inccl_group *group);
+/* The ROCm release of the HSA runtime this process mapped, as that runtime
+ * reports it (HSA_AMD_SYSTEM_INFO_BUILD_VERSION "..-rocm-rel-7.2-.." -> 702),
+ * and the build string itself; 0 / "" when it cannot be asked (no GPU). */
+unsigned inccl_hsa_runtime_release(void);
+const char *inccl_hsa_runtime_build(void);
+/* RCCL: *compiled = the NCCL_VERSION_CODE of the headers this library was
+ * built against (/opt/rocm), *loaded = ncclGetVersion() of the librccl the
+ * process bound to (torch's in a Python process).  0 or an error code. */
+int inccl_rccl_version(int *compiled, int *loaded);
 /* The communicator's own HIP stream (void* hipStream_t). */
 void *inccl_comm_stream(struct inccl_communicator *comm);
 int inccl_comm_barrier(struct inccl_communicator *comm);

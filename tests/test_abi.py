@@ -97,27 +97,53 @@ def test_reference_host_c_builds_unchanged(tmp_path):
 
 
 def test_ipc_bound_follows_the_hsa_runtime(lib, tmp_path):
-    """The IPC engines' largest shared buffer follows the HSA runtime the
-    process mapped (csrc/runtime.c): 2 GiB - 2 MiB under PyTorch's bundled ROCr
-    (this Python process), no bound under /opt/rocm's ROCm 7.2 ROCr (a C
-    program linked with the library); $INCCL_IPC_MAX_BYTES overrides."""
-    from container_inc_amd._lib import runtime_libs
-    hsa = runtime_libs().get("libhsa-runtime64", "")
-    if os.path.basename(hsa) == "libhsa-runtime64.so":   # torch's file: no ROCm build in its name
-        assert lib.inccl_ipc_max_bytes() == (2 << 30) - (2 << 20)
+    """The IPC engines' largest shared buffer follows the ROCm release the mapped
+    HSA runtime reports about itself (csrc/runtime.c): its build string is
+    parsed for "rocm-rel-X.Y", 7.2 or later lifts the 2 GiB - 2 MiB bound.  On
+    this GPU-less host the runtime cannot be asked, so the bound stays, in this
+    Python process and in a C program alike; $INCCL_IPC_MAX_BYTES overrides in
+    whole MiB, and a value below 1 MiB is ignored.  The parser runs on the two
+    build strings the MI355X box's runtimes report (tests/c/hsa_release.c);
+    tests/test_gpu_comm.py checks the query there."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: tests/test_gpu_comm.py::test_ipc_bound_on_the_gpu covers it")
+    bound = (2 << 30) - (2 << 20)
+    assert lib.inccl_hsa_runtime_release() == 0 and lib.inccl_hsa_runtime_build() == b""
+    assert lib.inccl_ipc_max_bytes() == bound
     src = tmp_path / "ipcmax.c"
-    src.write_text('#include <stdio.h>\n#include "inccl_amd.h"\nint main(void){printf("%zu\\n", inccl_ipc_max_bytes());}\n')
+    src.write_text('#include <stdio.h>\n#include "inccl_amd.h"\n'
+                   'int main(void){printf("%zu %u\\n", inccl_ipc_max_bytes(), inccl_hsa_runtime_release());}\n')
     exe = tmp_path / "ipcmax"
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe), "-L",
                            os.path.join(ROOT, "container_inc_amd"), "-linccl_amd",
                            "-Wl,-rpath," + os.path.join(ROOT, "container_inc_amd")])
     env = {k: v for k, v in os.environ.items() if k != "INCCL_IPC_MAX_BYTES"}
-    rocm_hsa = os.path.realpath("/opt/rocm/lib/libhsa-runtime64.so.1")
-    if re.search(r"libhsa-runtime64\.so\.1\.\d+\.(\d+)$", rocm_hsa) and \
-            int(re.search(r"\.(\d+)$", rocm_hsa).group(1)) >= 70200:
-        assert int(subprocess.check_output([str(exe)], env=env, text=True)) == 1 << 40
-    env["INCCL_IPC_MAX_BYTES"] = "12345"
-    assert int(subprocess.check_output([str(exe)], env=env, text=True)) == 12345
+    assert subprocess.check_output([str(exe)], env=env, text=True).split() == [str(bound), "0"]
+    for val, want in (("12345", bound), (str((5 << 20) + 123), 5 << 20), (str(16 << 30), 16 << 30)):
+        env["INCCL_IPC_MAX_BYTES"] = val
+        r = subprocess.run([str(exe)], env=env, capture_output=True, text=True, check=True)
+        assert int(r.stdout.split()[0]) == want, (val, r.stdout)
+        assert ("below 1 MiB" in r.stderr) == (want == bound)
+    parser = tmp_path / "hsa_release"
+    subprocess.check_call(["gcc", "-std=gnu11", "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include", "-I",
+                           os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "container_inc_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "c", "hsa_release.c"), "-o", str(parser), "-L",
+                           "/opt/rocm/lib", "-lamdhip64", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
+    out = subprocess.check_output([str(parser)], text=True)
+    assert "parser ok" in out and f"release 0 build  bound {bound}" in out, out
+
+
+def test_rccl_version_reported(lib):
+    """The RCCL the library was compiled against (/opt/rocm's headers) and the
+    one the process bound to (torch's librccl in Python) are both reported."""
+    import ctypes
+    c, ld = ctypes.c_int(0), ctypes.c_int(0)
+    assert lib.inccl_rccl_version(ctypes.byref(c), ctypes.byref(ld)) == 0
+    assert c.value >= 22700 and ld.value >= 22000, (c.value, ld.value)
+    from container_inc_amd._lib import runtime_libs
+    rt = runtime_libs()
+    assert rt["rccl_compiled"] == c.value and rt["rccl_loaded"] == ld.value
 
 
 def test_version_and_host_helpers(lib):

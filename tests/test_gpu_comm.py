@@ -85,6 +85,39 @@ def test_reference_host_binary(gpu):
         assert p.returncode == 0 and "result ok" in out, out + err
 
 
+def _c_release(tmp_path):
+    """(release, bound) that a C program linked against /opt/rocm's runtime
+    reports: the HSA runtime's own build string, csrc/runtime.c."""
+    src = tmp_path / "release.c"
+    src.write_text('#include <stdio.h>\n#include "inccl_amd.h"\nint main(void){printf("%u %zu %s\\n", '
+                   'inccl_hsa_runtime_release(), inccl_ipc_max_bytes(), inccl_hsa_runtime_build());}\n')
+    exe = tmp_path / "release"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe), "-L",
+                           os.path.join(ROOT, "container_inc_amd"), "-linccl_amd",
+                           "-Wl,-rpath," + os.path.join(ROOT, "container_inc_amd")])
+    env = {k: v for k, v in os.environ.items() if k != "INCCL_IPC_MAX_BYTES"}
+    out = subprocess.check_output([str(exe)], env=env, text=True).split()
+    return int(out[0]), int(out[1]), " ".join(out[2:])
+
+
+def test_ipc_bound_on_the_gpu(gpu, lib, tmp_path):
+    """The IPC bound follows the ROCm release each process's HSA runtime
+    reports (hsa_system_get_info BUILD_VERSION), not a file name: this Python
+    process runs on PyTorch's bundled ROCr (release 7.0 here: bound 2 GiB -
+    2 MiB), a C program on /opt/rocm's (7.2 on this image: no bound)."""
+    import re
+    build = lib.inccl_hsa_runtime_build().decode()
+    rel = lib.inccl_hsa_runtime_release()
+    assert re.search(r"rocm-rel-\d+\.\d+", build), build
+    want = (1 << 40) if rel >= 702 else (2 << 30) - (2 << 20)
+    if "INCCL_IPC_MAX_BYTES" not in os.environ:
+        assert lib.inccl_ipc_max_bytes() == want
+    crel, cbound, cbuild = _c_release(tmp_path)
+    assert re.search(r"rocm-rel-\d+\.\d+", cbuild), cbuild
+    assert cbound == ((1 << 40) if crel >= 702 else (2 << 30) - (2 << 20)), (crel, cbound, cbuild)
+    print(f"python process: release {rel} ({build}); C process: release {crel} ({cbuild}), bound {cbound}")
+
+
 @pytest.mark.parametrize("engine", ["p2p", "mesh"])
 def test_ipc_engine_over_2gib_c_hosted(gpu, tmp_path, engine):
     """The IPC engines on a 2.25 GiB bucket (p2p: 2.25 GiB IPC buffers; mesh:
@@ -92,6 +125,9 @@ def test_ipc_engine_over_2gib_c_hosted(gpu, tmp_path, engine):
     importing such buffers works (csrc/runtime.c lifts the 2 GiB bound there;
     under PyTorch's bundled ROCr the import hangs).  Two processes
     on GPU 0, rank 0 the TCP master, two calls, every lane exact."""
+    crel, cbound, cbuild = _c_release(tmp_path)
+    if cbound < (9 << 28):
+        pytest.skip(f"/opt/rocm's HSA runtime reports release {crel} ({cbuild}): the 2 GiB IPC bound stays")
     exe = tmp_path / "big_ipc"
     subprocess.check_call(["gcc", "-O2", "-std=gnu11", "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(ROOT, "include"),
                            "-I", "/opt/rocm/include", os.path.join(ROOT, "tests", "c", "big_ipc.c"), "-o", str(exe),
