@@ -76,6 +76,7 @@ SIGNATURES = {
     "inccl_switch_slot": (_P, [_P, _U32]),
     "inccl_switch_ingress": (_I, [_P, _P, _SZ, _SZ, _P, _P, _P, _P]),
     "inccl_switch_egress": (_I, [_P, _P, _SZ, _SZ, _P, _P, _P, _P, _P, _SZ, _P, _P]),
+    "inccl_switch_batch": (_I, [_P, _P, _SZ, _SZ, _P, _P, _P, _P, _P, _SZ, _P, _P]),
     "inccl_icrc_frames": (_I, [_P, _SZ, _SZ, _P, _P]),
 }
 

@@ -15,14 +15,16 @@ extern "C" {
 /* device-side state of one root switch (pointers into one allocation) */
 typedef struct InccSwitchState {
     int32_t *agg;        /* [slots][256]        non_termination_switch.c:55 */
-    uint32_t *arrival;   /* [slots]             nts.c:59 */
+    uint64_t *arrival;   /* [slots][2]          nts.c:59: {bitmap, tag = the batch that wrote it}, double-buffered
+                          * by batch parity so a batch reads the bitmap as it was before it (k_ingress_apply) */
     int32_t *degree;     /* [slots]             nts.c:60 */
     uint32_t *reth;      /* [slots][fan_in][4]  nts.c:57 */
     uint64_t *first;     /* [slots][fan_in]     batch-tagged index of the first copy in a batch:
                           * (~gen << 32) | frame, atomicMin -> the earliest frame of the newest batch */
-    uint32_t *gen;       /* device word: batches ingested so far.  A batch's claim and apply use *gen + 1 as
-                          * its generation and its commit stores it, so that a captured batch (hipGraph)
-                          * tags every replay anew */
+    uint32_t *gen;       /* gen[0]: batches ingested so far.  A batch's claim tags it first-copy keys with
+                          * g = gen[0] + 1 and stores g in gen[1]; its apply reads gen[1] and stores g in
+                          * gen[0], so that a captured batch (hipGraph) tags every replay anew */
+    uint32_t *hdr;       /* batch call: [62][80 B] header images, then [62] ICRC header terms (claim writes them) */
     uint32_t slots;      /* power of two */
     int fan_in;
 } InccSwitchState;
@@ -35,6 +37,9 @@ int inccl_k_frames_init(void);
 int inccl_k_icrc(const uint8_t *frames, size_t stride, size_t count, uint32_t *out, void *stream);
 int inccl_k_switch_ingress(const InccSwitchState *s, const uint8_t *frames, size_t stride, size_t count,
                            const int32_t *ports, int32_t *action, uint32_t *psn_out, void *stream);
+int inccl_k_switch_batch(const InccSwitchState *s, const uint8_t *frames, size_t stride, size_t count,
+                         const int32_t *ports, int32_t *action, uint32_t *psn_out, const InccFrameTemplate *tmpl,
+                         uint8_t *out, size_t out_stride, int32_t *out_len, void *stream);
 int inccl_k_switch_egress(const InccSwitchState *s, const uint8_t *in_frames, size_t in_stride, size_t count,
                           const int32_t *ports, const int32_t *action, const uint32_t *psns,
                           const InccFrameTemplate *tmpl, uint8_t *out, size_t out_stride, int32_t *out_len,

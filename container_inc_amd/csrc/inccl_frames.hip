@@ -5,23 +5,30 @@
 // repository/src/util.c:331-442 (build_eth_packet), :250-286 (compute_icrc),
 // :141-195 (crc32), :106-127 (ipv4_checksum).
 //
-// One wave64 per frame.  A frame is staged in LDS; the ICRC input (4 x 0xFF --
-// the CRC init folded into the message -- then the masked IP .. payload bytes)
-// is the frame from byte 10 on, with bytes 10-13 and the masked fields set to
-// 0xFF in LDS while the CRC runs.  It is right-aligned in a 1088-byte window
-// (64 lanes x 17 B), so leading zeros do not change the raw CRC.  CRC-32 is
-// linear over GF(2): the window's raw CRC is the XOR over lanes of
-// Z_{17 (63 - lane)}(crc(segment)), Z_n = "append n zero bytes".  Each lane
-// (1) reads its 17 bytes as 6 dwords + byte-aligns them, (2) computes the
-// segment's CRC as 34 independent nibble lookups (byte j's contribution is
-// Z_{16-j}(T[b_j]); a 2.2 KiB table whose 16 entries per lookup sit in 16
-// distinct banks, so no dependency chain and no bank conflicts), (3) applies
-// its own fixed Z as 8 nibble lookups in a lane-major table (bank = lane), and
-// (4) the wave XOR-reduces.  34 KiB of tables per block.
+// A batch of frames (frame index = arrival order) goes through
+//   k_ingress_claim   a lane per frame: parse + validate, degree, and the
+//                     first copy of every (slot, port) by a batch-tagged atomicMin
+//   k_ingress_apply   persistent, a wave per two consecutive frames: classify
+//                     in the reference's serial order (nts.c:353-372), sum each
+//                     slot's counted arrivals into its aggregate (:361-363), the
+//                     arrival bitmap, the RETH keeper (:442), the recycle
+//                     (:235-242, :367) -- and in the batch call
+//                     (inccl_switch_batch) the broadcast frames of every PSN that
+//                     completes (:447-453, util.c:331-442) straight from the
+//                     aggregate in registers
+//   k_egress_fixed<F> / k_egress   (inccl_switch_egress) every output frame of a
+//                     batch from the state ingress left: COMPLETED broadcasts and
+//                     REPLAY resends (:353-356)
+//   k_replay          (inccl_switch_batch) the REPLAY resends, after apply
+// The ICRC is linear over GF(2), so every CRC here is a XOR of table lookups
+// (nibble planes, one SDWA byte select per lookup, three-way XORs) reduced over
+// the wave with DPP -- no serial byte loop.
 //
 // State on the GPU (slots = PSN ring size, power of two; the reference uses 16):
 //   agg[slots][256] int32        aggregator        (nts.c:55)
-//   arrival[slots] uint32        port bitmap + bit fan_in = "result known" (nts.c:59, :366)
+//   arrival[slots][2] uint64     port bitmap + bit fan_in = "result known" (nts.c:59, :366),
+//                                tagged with the batch that wrote it, double-buffered by
+//                                batch parity (k_ingress_apply)
 //   degree[slots] int32          arrivals incl. retransmits (nts.c:60, :351)
 //   reth[slots][fan_in][16 B]    RETH of each child's WRITE_FIRST (nts.c:57, :442)
 #include <hip/hip_runtime.h>
@@ -35,41 +42,18 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kWin = 1088;            // 64 lanes x 17 bytes
-constexpr int kSeg = 17;
-constexpr int kFrameMax = 1152;       // staged frame bytes (>= 1098)
-constexpr int kWavesPerBlock = 4;
-constexpr int kEgressWaves = 8;       // 512-lane blocks, two per CU, persistent grid
+constexpr int kWin = 1088;            // ICRC window: the longest message (1098-B frame from byte 10)
+constexpr int kFrameMax = 1152;
+constexpr int kSeg = 17;              // egress segment table rows (row j: Z_{16-j})
+constexpr int kEgressWaves = 8;       // 512-lane blocks, three per CU, persistent grid
 constexpr int kLanes = 256;           // int32 lanes per packet (nts.c:55)
 constexpr int kAuxNt = 2;   // buffer instruction cache policy: nt (streaming, not re-read)
-constexpr int kOobOffset = 0x7FFFFFF0;   // past any row: a buffer store there is dropped
+constexpr int kOobOffset = 0x7FFFFFF0;   // past any row: a buffer store there is dropped, a load returns 0
+
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u2 __attribute__((ext_vector_type(2)));
 
 __device__ uint32_t g_seg[kSeg][2][16];       // [byte j][nibble][value] = Z_{16-j}(T[value << 4 nibble]), T = util.c:141-150
-__device__ uint32_t g_segb[kSeg][256];        // [byte j][value] = Z_{16-j}(T[value])
-__device__ uint32_t g_lane_shift[8][16][kWave];   // [nibble][value][lane] = Z_{17 (63 - lane)}(value << 4 nibble)
-
-// kByte = false: a lane's segment CRC as 34 independent nibble lookups in a
-// 2.2 KiB table (no bank conflicts, two VALU ops of index math per lookup).
-// kByte = true: 17 byte lookups in a 17 KiB table (half the index math; the
-// lanes' random entries conflict in the banks, and 59 KiB of LDS per block
-// leaves two blocks per CU).  Measured 64.5 vs 62.7 us per 131 072 frames, so
-// the nibble form stays the product; $INCCL_ICRC_BYTE_TABLES=1 selects the
-// byte form (profiles/r03/icrc_byte_vs_nibble.txt).
-template <bool kByte>
-struct CrcLds {
-    uint32_t seg[kByte ? kSeg * 256 : kSeg * 2 * 16];
-    uint32_t lane_sh[8][16][kWave]; // per-lane zero-append operator, nibble-sliced
-};
-
-template <bool kByte>
-__device__ __forceinline__ void load_tables(CrcLds<kByte>& t)
-{
-    const uint32_t* seg = kByte ? &g_segb[0][0] : &g_seg[0][0][0];
-    for (int i = threadIdx.x; i < (kByte ? kSeg * 256 : kSeg * 2 * 16); i += blockDim.x) t.seg[i] = seg[i];
-    uint32_t* dst = &t.lane_sh[0][0][0];
-    const uint32_t* src = &g_lane_shift[0][0][0];
-    for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) dst[i] = src[i];
-}
 
 // frame bytes that read as 0xFF while the ICRC runs: 10-13 carry the CRC init
 // (the 4 x 0xFF prefix), the rest are the ICRC masks of util.c:266-270 (tos,
@@ -100,96 +84,6 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
     return r;
 }
 
-// ICRC of the frame staged at `fr` (LDS, at least 1152 B, 4-B aligned), whose
-// masked bytes are already 0xFF; result valid in every lane.
-template <bool kByte>
-__device__ uint32_t icrc_wave(const uint8_t* fr, const CrcLds<kByte>& t, int lane)
-{
-    const int ip_total = ((int)fr[16] << 8) | fr[17];   // message = 4 (init) + ip_total - 4 (no ICRC) bytes
-    const int lead = kWin - ip_total;                   // zero bytes before the message
-    const int o = 10 + lane * kSeg - lead;              // frame offset of this lane's first byte
-    uint32_t c = 0;
-    if (o + kSeg > 10) {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(fr);
-        const int d0 = o >> 2;   // floor division (o may be negative)
-        uint32_t dw[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) dw[k] = d0 + k >= 0 ? w[d0 + k] : 0u;
-        const uint32_t sh = (uint32_t)o & 3u;
-        uint32_t a[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) a[k] = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
-        const int nz = 10 - o;   // leading bytes of this lane before the message: zero
-        if (nz > 0) {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                const int z = nz - 4 * k;
-                a[k] = z >= 4 ? 0u : (z > 0 ? a[k] & (0xFFFFFFFFu << (8 * z)) : a[k]);
-            }
-        }
-        // the segment's CRC register (util.c:190-192 run from 0) is linear in its
-        // bytes: XOR over byte j of Z_{16-j}(T[b_j]), each split into two nibble
-        // lookups.  No lookup depends on another, and the 16 entries one
-        // ds_read_b32 can touch sit in 16 distinct banks (no conflicts).
-        if (kByte) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-#pragma unroll
-                for (int b = 0; b < 4; ++b) c ^= t.seg[(4 * k + b) * 256 + ((a[k] >> (8 * b)) & 0xFFu)];
-            }
-            c ^= t.seg[16 * 256 + (a[4] & 0xFFu)];
-        } else {
-            // nibble planes: byte b of lo / hi is the low / high nibble of byte b,
-            // so each lookup's index is one SDWA byte select; XOR three at a time
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t lo = opaque_u32(a[k] & 0x0F0F0F0Fu), hi = opaque_u32((a[k] >> 4) & 0x0F0F0F0Fu);
-                uint32_t v[8];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    v[2 * b] = t.seg[((4 * k + b) * 2) * 16 + (uint8_t)(lo >> (8 * b))];
-                    v[2 * b + 1] = t.seg[((4 * k + b) * 2 + 1) * 16 + (uint8_t)(hi >> (8 * b))];
-                }
-                c = xor3(xor3(xor3(c, v[0], v[1]), v[2], v[3]), xor3(v[4], v[5], v[6]), v[7]);
-            }
-            c = xor3(c, t.seg[(16 * 2) * 16 + (a[4] & 15u)], t.seg[(16 * 2 + 1) * 16 + ((a[4] >> 4) & 15u)]);
-        }
-        // shift to the window's end: Z_{17 (63 - lane)}(c)
-        const uint32_t clo = opaque_u32(c & 0x0F0F0F0Fu), chi = opaque_u32((c >> 4) & 0x0F0F0F0Fu);
-        uint32_t v[8];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            v[2 * b] = t.lane_sh[2 * b][(uint8_t)(clo >> (8 * b))][lane];
-            v[2 * b + 1] = t.lane_sh[2 * b + 1][(uint8_t)(chi >> (8 * b))][lane];
-        }
-        c = xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
-    }
-    // XOR-reduce the 64 lane contributions with DPP (one VALU op per step, no
-    // LDS): quads, half-rows, rows, then the row broadcasts; lane 63 ends with
-    // the whole window
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x141, 0xF, 0xF, false);   // row_half_mirror
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x140, 0xF, 0xF, false);   // row_mirror
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x142, 0xA, 0xF, false);   // row_bcast15 -> rows 1, 3
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x143, 0xC, 0xF, false);   // row_bcast31 -> rows 2, 3
-    return ~(uint32_t)__builtin_amdgcn_readlane((int)c, 63);
-}
-
-// Header word of a frame (bytes 16-19), loaded lane-varying so that it stays a
-// vector load: a uniform one would go through the scalar cache, and the LDS
-// waits of the running CRC (lgkmcnt) would then wait for it too.
-__device__ __forceinline__ uint32_t icrc_hdr_load(const uint8_t* g, int lane)
-{
-    return reinterpret_cast<const uint32_t*>(g)[4 + (lane & 1)];
-}
-
-__device__ __forceinline__ int icrc_ip_total(uint32_t hdr_lane)
-{
-    const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)hdr_lane, 0);
-    return (int)(((h & 0xFFu) << 8) | ((h >> 8) & 0xFFu));
-}
-
 // an ICRC is computed only for an IP length the window holds and whose frame
 // lies inside its row: a header claiming more bytes than the row has reads as
 // malformed (ICRC 0), never as the next row's bytes
@@ -198,241 +92,44 @@ __device__ __forceinline__ bool icrc_len_ok(int ipt, int64_t stride)
     return ipt >= 28 && ipt <= kWin && 14 + ipt <= kFrameMax && 14 + ipt <= stride;
 }
 
-// Persistent: each wave walks its frames with the next frame's words (5 dwords
-// a lane, coalesced) and the one after's header in flight while the current
-// frame's CRC runs from LDS.
-template <bool kByte, int kIcrcWaves>
-__global__ __launch_bounds__(kWave* kIcrcWaves) void k_icrc(const uint8_t* __restrict__ frames, int64_t stride,
-                                                                int64_t count, uint32_t* __restrict__ out)
-{
-    __shared__ CrcLds<kByte> t;
-    __shared__ __attribute__((aligned(16))) uint8_t buf[kIcrcWaves][kFrameMax];
-    load_tables(t);
-    __syncthreads();
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
-    constexpr int kWords = (kFrameMax / 4 + kWave - 1) / kWave;   // 5
-    const int64_t step = (int64_t)gridDim.x * kIcrcWaves;
-    int64_t f = (int64_t)blockIdx.x * kIcrcWaves + w;
-    if (f >= count) return;
-    uint32_t* lds = reinterpret_cast<uint32_t*>(buf[w]);
-    auto fetch = [&](int64_t fr, int ipt, uint32_t (&v)[kWords]) {
-        const uint32_t* g = reinterpret_cast<const uint32_t*>(frames + fr * stride);
-        const int words = icrc_len_ok(ipt, stride) ? (14 + ipt + 3) >> 2 : 0;
-#pragma unroll
-        for (int k = 0; k < kWords; ++k) {
-            const int i = lane + k * kWave;
-            v[k] = i < words ? g[i] : 0u;
-        }
-    };
-    int ip = icrc_ip_total(icrc_hdr_load(frames + f * stride, lane));
-    uint32_t cur[kWords];
-    fetch(f, ip, cur);
-    uint32_t hdrN = f + step < count ? icrc_hdr_load(frames + (f + step) * stride, lane) : 0u;
-    for (;;) {
-#pragma unroll
-        for (int k = 0; k < kWords; ++k)
-            if (lane + k * kWave < kFrameMax / 4) lds[lane + k * kWave] = cur[k];
-        __builtin_amdgcn_wave_barrier();
-        if (lane < kNumMasked) buf[w][masked_pos(lane)] = 0xFF;
-        __builtin_amdgcn_wave_barrier();
-        const int64_t fn = f + step;
-        int ipn = 0;
-        if (fn < count) {
-            ipn = icrc_ip_total(hdrN);
-            fetch(fn, ipn, cur);
-            hdrN = fn + step < count ? icrc_hdr_load(frames + (fn + step) * stride, lane) : 0u;
-        }
-        const uint32_t crc = icrc_len_ok(ip, stride) ? icrc_wave<kByte>(buf[w], t, lane) : 0u;
-        if (lane == 0) out[f] = crc;
-        __builtin_amdgcn_wave_barrier();
-        f = fn;
-        ip = ipn;
-        if (f >= count) break;
-    }
-}
-
 // ---------------------------------------------------------------------------
-// ICRC, two frames per wave ($INCCL_ICRC_DIRECT=0; $INCCL_ICRC_PAIR=0: k_icrc): lanes 0-31 take frame 2p,
-// lanes 32-63 frame 2p+1, each lane 34 bytes of the 1088-byte window (32 x 34).
-// Per frame: 34 x 2 nibble lookups over 32 lanes (38 lookup instructions per
-// frame, against 42), a 16 KiB lane-shift table (Z_{34 (31 - lane')}), and one
-// 5-step DPP reduction for both frames.  Same right-aligned window, masks and
-// results as icrc_wave.
+// Standalone ICRC (inccl_icrc_frames; util.c:250-286 for any frame), two frames
+// per wave: lanes 0-31 take frame 2p, lanes 32-63 frame 2p+1, each lane a
+// 34-byte segment of the frame's ICRC message right-aligned in a 1088-byte
+// window (32 x 34; leading zeros do not change a raw CRC).  Each lane loads its
+// segment straight from the frame (two dwordx4 + two dword buffer loads at the
+// segment's dword offset), sets the mask bytes and clears the bytes before the
+// message with one (AND, OR) LDS table lookup per dword, computes the segment's
+// CRC as 68 independent nibble lookups, shifts it to the window's end
+// (Z_{34 (31 - lane')}, 8 lookups in a lane-major table) and the 32-lane halves
+// XOR-reduce with DPP.  Every memory instruction runs on every pass (a frame
+// past the end, or malformed, gets a zero-size buffer: its loads return 0 and
+// its store is dropped), so the waits stay one pass deep.  The variants this
+// was chosen over (LDS-staged frames, one frame per wave, byte tables, two pairs
+// per pass, the VALU mask) live in tools/tune/tune_icrc.hip.
 // ---------------------------------------------------------------------------
 constexpr int kSeg2 = 34;
 __device__ uint32_t g_seg34[kSeg2][2][16];          // [byte j][nibble][value] = Z_{33-j}(T[value << 4 nibble])
 __device__ uint32_t g_lane_shift32[8][16][32];      // [nibble][value][lane'] = Z_{34 (31 - lane')}(value << 4 nibble)
 
-struct CrcLdsPair {
+struct IcrcLds {
     uint32_t seg[kSeg2][2][16];
     uint32_t lane_sh[8][16][32];
-    uint32_t spread[16];   // k_icrc_direct<.., 1>: nibble -> byte mask (bit i -> byte i)
-    uint32_t andor[32][2];   // k_icrc_direct<.., 2>: [nibble | 16 (frame dword <= 2)] -> (AND, OR)
+    uint32_t andor[32][2];   // [nibble | 16 (frame dword <= 2)] -> (AND, OR)
 };
 
-// ICRC of the frame of this lane's half (staged at `fr`, masked bytes 0xFF);
-// returns the raw (pre-reduction) contribution of this lane
-// The segment's contribution from its frame dwords dw[k] = frame dword (o >> 2) + k
-// (o = the segment's first frame byte; masked bytes already 0xFF)
-// kZeroed: dw already holds 0 for every frame byte below 10 (icrc_mask_regs_zero),
-// so neither the zeroing nor the skip of an all-zero segment is needed
-template <bool kZeroed = false>
-__device__ __forceinline__ uint32_t icrc_half_regs(const uint32_t (&dw)[10], int o, const CrcLdsPair& t, int l)
-{
-    uint32_t c = 0;
-    if (kZeroed || o + kSeg2 > 10) {
-        const uint32_t sh = (uint32_t)o & 3u;
-        uint32_t a[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) a[k] = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
-        const int nz = 10 - o;
-        if (!kZeroed && nz > 0) {
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                const int z = nz - 4 * k;
-                a[k] = z >= 4 ? 0u : (z > 0 ? a[k] & (0xFFFFFFFFu << (8 * z)) : a[k]);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t lo = opaque_u32(a[k] & 0x0F0F0F0Fu), hi = opaque_u32((a[k] >> 4) & 0x0F0F0F0Fu);
-            uint32_t v[8];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                v[2 * b] = t.seg[4 * k + b][0][(uint8_t)(lo >> (8 * b))];
-                v[2 * b + 1] = t.seg[4 * k + b][1][(uint8_t)(hi >> (8 * b))];
-            }
-            c = xor3(xor3(xor3(c, v[0], v[1]), v[2], v[3]), xor3(v[4], v[5], v[6]), v[7]);
-        }
-        // bytes 32 and 33 of the segment
-        c = xor3(c, t.seg[32][0][a[8] & 15u], t.seg[32][1][(a[8] >> 4) & 15u]);
-        c = xor3(c, t.seg[33][0][(a[8] >> 8) & 15u], t.seg[33][1][(a[8] >> 12) & 15u]);
-        const uint32_t clo = opaque_u32(c & 0x0F0F0F0Fu), chi = opaque_u32((c >> 4) & 0x0F0F0F0Fu);
-        uint32_t v[8];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            v[2 * b] = t.lane_sh[2 * b][(uint8_t)(clo >> (8 * b))][l];
-            v[2 * b + 1] = t.lane_sh[2 * b + 1][(uint8_t)(chi >> (8 * b))][l];
-        }
-        c = xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
-    }
-    return c;
-}
-
-__device__ __forceinline__ uint32_t icrc_half_lane(const uint8_t* fr, const CrcLdsPair& t, int l)
-{
-    const int ip_total = ((int)fr[16] << 8) | fr[17];
-    const int lead = kWin - ip_total;
-    const int o = 10 + l * kSeg2 - lead;                 // frame offset of this lane's first byte
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(fr);
-    const int d0 = o >> 2;
-    uint32_t dw[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) dw[k] = d0 + k >= 0 && o + kSeg2 > 10 ? w[d0 + k] : 0u;
-    return icrc_half_regs(dw, o, t, l);
-}
-
-template <int kW>
-__global__ __launch_bounds__(kWave* kW) void k_icrc_pair(const uint8_t* __restrict__ frames, int64_t stride,
-                                                         int64_t count, uint32_t* __restrict__ out)
-{
-    __shared__ CrcLdsPair t;
-    __shared__ __attribute__((aligned(16))) uint8_t buf[kW][2][kFrameMax];
-    for (int i = threadIdx.x; i < kSeg2 * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg34[0][0][0])[i];
-    for (int i = threadIdx.x; i < 8 * 16 * 32; i += blockDim.x) (&t.lane_sh[0][0][0])[i] = (&g_lane_shift32[0][0][0])[i];
-    __syncthreads();
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
-    const int half = lane >> 5, l = lane & 31;
-    constexpr int kWords = kFrameMax / 4 / 32;   // 9 dwords per lane and frame
-    const int64_t pairs = (count + 1) >> 1, step = (int64_t)gridDim.x * kW;
-    int64_t p = (int64_t)blockIdx.x * kW + w;
-    if (p >= pairs) return;
-    uint8_t* mine = buf[w][half];
-    uint32_t* lds = reinterpret_cast<uint32_t*>(mine);
-    auto fetch = [&](int64_t pp, uint32_t (&v)[kWords]) {
-        const int64_t f = 2 * pp + half;
-        const bool in = f < count;
-        const uint8_t* g8 = frames + (in ? f : 0) * stride;
-        const uint32_t* g = reinterpret_cast<const uint32_t*>(g8);
-        // the half's IP length (its lanes all read the same dword) bounds the words read
-        const uint32_t hw = g[4];
-        const int ipt = (int)(((hw & 0xFFu) << 8) | ((hw >> 8) & 0xFFu));
-        const int words = in && icrc_len_ok(ipt, stride) ? (14 + ipt + 3) >> 2 : 0;
-#pragma unroll
-        for (int k = 0; k < kWords; ++k) {
-            const int i = l + k * 32;
-            v[k] = i < words ? g[i] : 0u;
-        }
-    };
-    uint32_t cur[kWords];
-    fetch(p, cur);
-    for (;;) {
-#pragma unroll
-        for (int k = 0; k < kWords; ++k) lds[l + k * 32] = cur[k];
-        __builtin_amdgcn_wave_barrier();
-        if (l < kNumMasked) mine[masked_pos(l)] = 0xFF;
-        __builtin_amdgcn_wave_barrier();
-        const int64_t pn = p + step;
-        if (pn < pairs) fetch(pn, cur);
-        const int ipt = ((int)mine[16] << 8) | mine[17];
-        const int64_t f = 2 * p + half;
-        uint32_t c = icrc_half_lane(mine, t, l);
-        if (!icrc_len_ok(ipt, stride)) c = 0u;
-        // XOR-reduce each 32-lane half: quads, half-rows, rows, then row 0 into
-        // row 1 and row 2 into row 3 (lanes 31 and 63 end with the two frames)
-        c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);
-        c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);
-        c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x141, 0xF, 0xF, false);
-        c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x140, 0xF, 0xF, false);
-        c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x142, 0xA, 0xF, false);
-        const uint32_t ca = ~(uint32_t)__builtin_amdgcn_readlane((int)c, 31);
-        const uint32_t cb = ~(uint32_t)__builtin_amdgcn_readlane((int)c, 63);
-        if (lane == 0) out[2 * p] = icrc_len_ok(((int)buf[w][0][16] << 8) | buf[w][0][17], stride) ? ca : 0u;
-        if (lane == 32 && f < count) out[f] = icrc_len_ok(ipt, stride) ? cb : 0u;
-        __builtin_amdgcn_wave_barrier();
-        p = pn;
-        if (p >= pairs) break;
-    }
-}
-
-// masked_pos() as a bitmap of frame byte positions (10-13, 15, 22, 24, 25, 40, 41, 46)
+// the masked byte positions (10-13, 15, 22, 24, 25, 40, 41, 46) as a bitmap
 constexpr uint64_t kIcrcMaskBits = (1ull << 10) | (1ull << 11) | (1ull << 12) | (1ull << 13) | (1ull << 15) |
                                    (1ull << 22) | (1ull << 24) | (1ull << 25) | (1ull << 40) | (1ull << 41) |
                                    (1ull << 46);
 
-// OR the mask bytes into dw[k] = frame dword d0 + k, straight-line: the bitmap
-// shifted to byte 4 d0, and each nibble spread to four byte masks (bit i -> byte i)
-__device__ __forceinline__ void icrc_mask_regs(uint32_t (&dw)[10], int d0)
-{
-    // -28 .. 44 where any mask byte is in reach; a shift of 64 or more (a segment far
-    // before the frame) is clamped to no bits, not left to the hardware's 6-bit shift
-    const int s4 = 4 * d0;
-    const uint64_t x = (d0 >= 12 || d0 <= -16) ? 0ull : (s4 >= 0 ? kIcrcMaskBits >> s4 : kIcrcMaskBits << (-s4));
-    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        const uint32_t b = __builtin_amdgcn_ubfe(k < 8 ? lo : hi, 4 * (k & 7), 4);
-        const uint32_t m = (b * 0x00204081u) & 0x01010101u;
-        dw[k] |= (m << 8) - m;
-    }
-}
-
-// icrc_mask_regs with the nibble -> byte-mask spread from a 16-entry LDS table
-// (323 instead of 343 VALU per pair, 10 more LDS reads; $INCCL_ICRC_MASK_LDS=1)
-__device__ __forceinline__ void icrc_mask_regs_lds(uint32_t (&dw)[10], int d0, const CrcLdsPair& t)
-{
-    const int s4 = 4 * d0;
-    const uint64_t x = (d0 >= 12 || d0 <= -16) ? 0ull : (s4 >= 0 ? kIcrcMaskBits >> s4 : kIcrcMaskBits << (-s4));
-    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-#pragma unroll
-    for (int k = 0; k < 10; ++k) dw[k] |= t.spread[__builtin_amdgcn_ubfe(k < 8 ? lo : hi, 4 * (k & 7), 4)];
-}
-
-// icrc_mask_regs_lds that also clears frame bytes 0-9 (dwords 0-2; bytes 10-11 of
-// dword 2 are then set by its OR mask): dw = (dw & AND) | OR from a 32-entry table
-// indexed by the dword's mask nibble and a "dword <= 2" bit, so that the CRC needs
-// no per-byte zeroing of the leading bytes: 295 VALU per pair (the default)
-__device__ __forceinline__ void icrc_mask_regs_zero(uint32_t (&dw)[10], int d0, const CrcLdsPair& t)
+// dw[k] = frame dword d0 + k -> (dw & AND) | OR from the 32-entry table,
+// indexed by the dword's mask nibble and a "dword <= 2" bit: the mask bytes set
+// to 0xFF and frame bytes 0-9 cleared (bytes 10-11 of dword 2 are then set by
+// its OR), so the CRC needs no per-byte zeroing of the leading bytes.  The
+// bitmap shift is clamped: a segment far before a short frame would shift it by
+// 64 or more, which the hardware takes modulo 64.
+__device__ __forceinline__ void icrc_mask_regs(uint32_t (&dw)[10], int d0, const IcrcLds& t)
 {
     const int s4 = 4 * d0;
     const uint64_t x = (d0 >= 12 || d0 <= -16) ? 0ull : (s4 >= 0 ? kIcrcMaskBits >> s4 : kIcrcMaskBits << (-s4));
@@ -446,37 +143,60 @@ __device__ __forceinline__ void icrc_mask_regs_zero(uint32_t (&dw)[10], int d0, 
     }
 }
 
-// ICRC, two frames per wave without LDS staging (the default): each lane loads its own 34-byte
-// segment straight from the frame (two dwordx4 + two dword buffer loads at the
-// segment's dword offset), the mask bytes are ORed in registers, and LDS holds
-// only the tables.  Every memory instruction runs on every pass (a frame past
-// the end, or malformed, gets a zero-size buffer: its loads return 0 and its
-// store is dropped), so the waits stay one pass deep.  39 VGPRs and 20.7 KiB of
-// LDS (k_icrc_pair: 50 and 39 KiB).  Same window, masks and
-// results as k_icrc_pair.  Out-of-range segment words: a load partly before
-// the frame covers only bytes below 10 (zeroed or masked), and the segment's
-// last byte o + 33 <= 14 + ip_total - 5 keeps both dwordx4 inside the frame.
-template <int kW, int kPP, int kMaskLds = 0>
-__global__ __launch_bounds__(kWave* kW) void k_icrc_direct(const uint8_t* __restrict__ frames, int64_t stride,
-                                                           int64_t count, uint32_t* __restrict__ out)
+// The raw CRC contribution of this lane's 34-byte segment (frame byte o on;
+// dw[k] = frame dword (o >> 2) + k, masked), shifted to the window's end.
+__device__ __forceinline__ uint32_t icrc_segment(const uint32_t (&dw)[10], int o, const IcrcLds& t, int l)
 {
-    __shared__ CrcLdsPair t;
+    const uint32_t sh = (uint32_t)o & 3u;
+    uint32_t a[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a[k] = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t lo = opaque_u32(a[k] & 0x0F0F0F0Fu), hi = opaque_u32((a[k] >> 4) & 0x0F0F0F0Fu);
+        uint32_t v[8];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            v[2 * b] = t.seg[4 * k + b][0][(uint8_t)(lo >> (8 * b))];
+            v[2 * b + 1] = t.seg[4 * k + b][1][(uint8_t)(hi >> (8 * b))];
+        }
+        c = xor3(xor3(xor3(c, v[0], v[1]), v[2], v[3]), xor3(v[4], v[5], v[6]), v[7]);
+    }
+    // bytes 32 and 33 of the segment
+    c = xor3(c, t.seg[32][0][a[8] & 15u], t.seg[32][1][(a[8] >> 4) & 15u]);
+    c = xor3(c, t.seg[33][0][(a[8] >> 8) & 15u], t.seg[33][1][(a[8] >> 12) & 15u]);
+    const uint32_t clo = opaque_u32(c & 0x0F0F0F0Fu), chi = opaque_u32((c >> 4) & 0x0F0F0F0Fu);
+    uint32_t v[8];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        v[2 * b] = t.lane_sh[2 * b][(uint8_t)(clo >> (8 * b))][l];
+        v[2 * b + 1] = t.lane_sh[2 * b + 1][(uint8_t)(chi >> (8 * b))][l];
+    }
+    return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
+}
+
+// Out-of-range segment words: a load partly before the frame covers only bytes
+// below 10 (cleared or masked), and the segment's last byte o + 33 <= 14 +
+// ip_total - 5 keeps both dwordx4 inside the frame.
+template <int kW>
+__global__ __launch_bounds__(kWave* kW) void k_icrc(const uint8_t* __restrict__ frames, int64_t stride, int64_t count,
+                                                     uint32_t* __restrict__ out)
+{
+    __shared__ IcrcLds t;
     for (int i = threadIdx.x; i < kSeg2 * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg34[0][0][0])[i];
     for (int i = threadIdx.x; i < 8 * 16 * 32; i += blockDim.x) (&t.lane_sh[0][0][0])[i] = (&g_lane_shift32[0][0][0])[i];
     if (threadIdx.x < 32) {
-        const uint32_t m = ((threadIdx.x & 15u) * 0x00204081u) & 0x01010101u;
-        if (threadIdx.x < 16) t.spread[threadIdx.x] = (m << 8) - m;
+        const uint32_t m = ((threadIdx.x & 15u) * 0x00204081u) & 0x01010101u;   // nibble bit i -> byte i
         t.andor[threadIdx.x][0] = threadIdx.x & 16u ? 0u : 0xFFFFFFFFu;
         t.andor[threadIdx.x][1] = (m << 8) - m;
     }
     __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     const int half = lane >> 5, l = lane & 31;
-    // a wave takes kPP consecutive pairs per pass (group q = pairs kPP q .. kPP q + kPP - 1),
-    // all fetched one pass ahead: kPP pairs of loads in flight while a group's CRCs run
-    const int64_t pairs = (count + 1) >> 1, groups = (pairs + kPP - 1) / kPP, step = (int64_t)gridDim.x * kW;
+    const int64_t pairs = (count + 1) >> 1, step = (int64_t)gridDim.x * kW;
     int64_t q = (int64_t)blockIdx.x * kW + w;
-    if (q >= groups) return;
+    if (q >= pairs) return;
     // one buffer per pair (wave-uniform): its two rows, one for a last odd frame, none past the end
     auto pair_rsrc = [&](int64_t pp) {
         const int64_t rows = count - 2 * pp;
@@ -488,7 +208,6 @@ __global__ __launch_bounds__(kWave* kW) void k_icrc_direct(const uint8_t* __rest
     auto hdr = [&](int64_t pp) -> uint32_t {
         return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(pair_rsrc(pp), stride >= 20 ? row_off + 16 : kOobOffset, 0, 0);
     };
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     auto fetch = [&](int64_t pp, uint32_t h, uint32_t (&dw)[10], int& o, bool& ok) {
         const int64_t f = 2 * pp + half;
         const int ipt = (int)(((h & 0xFFu) << 8) | ((h >> 8) & 0xFFu));
@@ -496,7 +215,7 @@ __global__ __launch_bounds__(kWave* kW) void k_icrc_direct(const uint8_t* __rest
         o = 10 + l * kSeg2 - (kWin - ipt);
         // the segment's dwords, inside this frame's row: a dword before the row (a
         // lane whose segment starts before byte 10) or past the frame's last dword
-        // reads 0; the two dwordx4 never reach past the frame (header comment)
+        // reads 0; the two dwordx4 never reach past the frame (above)
         const int d = o >> 2, words = (14 + ipt + 3) >> 2;
         const __amdgpu_buffer_rsrc_t rs = pair_rsrc(pp);
         // (each offset a VGPR the compiler cannot see through: a select it could
@@ -513,60 +232,40 @@ __global__ __launch_bounds__(kWave* kW) void k_icrc_direct(const uint8_t* __rest
         dw[4] = b.x; dw[5] = b.y; dw[6] = b.z; dw[7] = b.w;
     };
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(4 * count), 0x00020000);
-    uint32_t cur[kPP][10], hn[kPP];
-    int o[kPP];
-    bool ok[kPP];
-#pragma unroll
-    for (int j = 0; j < kPP; ++j) fetch(kPP * q + j, hdr(kPP * q + j), cur[j], o[j], ok[j]);
-#pragma unroll
-    for (int j = 0; j < kPP; ++j) hn[j] = hdr(kPP * (q + step) + j);
-    // dropped stores: the loop is entered with its back edge's memory history
-#pragma unroll
-    for (int j = 0; j < kPP; ++j) __builtin_amdgcn_raw_buffer_store_b32(0u, ors, kOobOffset, 0, 0);
+    uint32_t cur[10];
+    int o;
+    bool ok;
+    fetch(q, hdr(q), cur, o, ok);
+    uint32_t hn = hdr(q + step);
+    // a dropped store: the loop is entered with its back edge's memory history
+    __builtin_amdgcn_raw_buffer_store_b32(0u, ors, kOobOffset, 0, 0);
     for (;;) {
         const int64_t qn = q + step;
-        uint32_t nxt[kPP][10];
-        int on[kPP];
-        bool okn[kPP];
-#pragma unroll
-        for (int j = 0; j < kPP; ++j) fetch(kPP * qn + j, hn[j], nxt[j], on[j], okn[j]);
-#pragma unroll
-        for (int j = 0; j < kPP; ++j) hn[j] = hdr(kPP * (qn + step) + j);
-        uint32_t c[kPP];
-#pragma unroll
-        for (int j = 0; j < kPP; ++j) {
-            if (kMaskLds == 2)
-                icrc_mask_regs_zero(cur[j], o[j] >> 2, t);
-            else if (kMaskLds == 1)
-                icrc_mask_regs_lds(cur[j], o[j] >> 2, t);
-            else
-                icrc_mask_regs(cur[j], o[j] >> 2);
-            c[j] = ok[j] ? icrc_half_regs<kMaskLds == 2>(cur[j], o[j], t, l) : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < kPP; ++j) {
-            uint32_t x = c[j];
-            x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
-            x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);
-            x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);
-            x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);
-            x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
-            const uint32_t ca = ~(uint32_t)__builtin_amdgcn_readlane((int)x, 31);
-            const uint32_t cb = ~(uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-            // lane 0 writes frame 2 pp, lane 32 frame 2 pp + 1 (past the end: dropped)
-            const int64_t pp = kPP * q + j;
-            __builtin_amdgcn_raw_buffer_store_b32(ok[j] ? (half ? cb : ca) : 0u, ors,
-                                                  l == 0 && pp < pairs ? (int)(4 * (2 * pp + half)) : kOobOffset, 0, 0);
-        }
+        uint32_t nxt[10];
+        int on;
+        bool okn;
+        fetch(qn, hn, nxt, on, okn);
+        hn = hdr(qn + step);
+        icrc_mask_regs(cur, o >> 2, t);
+        uint32_t x = ok ? icrc_segment(cur, o, t, l) : 0u;
+        // XOR-reduce each 32-lane half: quads, half-rows, rows, then row 0 into
+        // row 1 and row 2 into row 3 (lanes 31 and 63 end with the two frames)
+        x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
+        x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);
+        x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);
+        x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);
+        x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+        const uint32_t ca = ~(uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+        const uint32_t cb = ~(uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+        // lane 0 writes frame 2 q, lane 32 frame 2 q + 1 (past the end: dropped)
+        __builtin_amdgcn_raw_buffer_store_b32(ok ? (half ? cb : ca) : 0u, ors,
+                                              l == 0 && q < pairs ? (int)(4 * (2 * q + half)) : kOobOffset, 0, 0);
         q = qn;
-        if (q >= groups) break;
+        if (q >= pairs) break;
 #pragma unroll
-        for (int j = 0; j < kPP; ++j) {
-#pragma unroll
-            for (int k = 0; k < 10; ++k) cur[j][k] = nxt[j][k];
-            o[j] = on[j];
-            ok[j] = okn[j];
-        }
+        for (int k = 0; k < 10; ++k) cur[k] = nxt[k];
+        o = on;
+        ok = okn;
     }
 }
 
@@ -576,83 +275,6 @@ __device__ __forceinline__ bool is_data_opcode(uint8_t op)
 }
 __device__ __forceinline__ bool is_write_first(uint8_t op) { return op == 0x06 || op == 0x0A; }   // nts.c:327-328
 
-// Ingress (nts.c:303-483, root branch) in three passes that reproduce the
-// reference's one-frame-at-a-time order: frame index within the batch = arrival
-// order.  What a serial switch decides for frame f depends on which copies of
-// its (psn, port) and of its PSN's other ports came BEFORE f, so:
-//   claim   (a lane per frame) parse + validate; per (slot, port) an atomicMin
-//           of a batch-tagged frame index finds the first copy in the batch
-//   apply   (a wave per frame) the first copy of a pair whose port bit was not
-//           set before the batch is the arrival that counts: it adds its payload
-//           (nts.c:359-363) and keeps its RETH (:442).  The PSN completes at the
-//           LAST of its ports' counted arrivals (the max over ports of the first
-//           index; ports already in before the batch count as earlier than
-//           every frame): that frame is COMPLETED (:365-372), the others
-//           ABSORBED.  Every other copy is a retransmit (:353): REPLAY if the
-//           slot completed before the batch or at an earlier frame of it
-//           (:354-356), else DROPPED.
-//   commit  (a lane per frame) the arrival bitmap: port bits of the counted
-//           arrivals, and the result bit (:366) of the completing ones.
-// The arrival bitmap is read (apply) and written (commit) in different
-// launches, so every frame sees the state from before the batch.
-constexpr int kActPending = 100;   // claim -> apply: a data frame still to classify
-constexpr int kClaimBlock = 256;
-
-// (~gen << 32) | (frame << 1) | wf: the minimum over a (slot, port)'s keys is the
-// newest batch's earliest copy (the frame index dominates bit 0), and bit 0 tells
-// apply where that copy's payload starts (byte 54, or 70 after a RETH) without
-// another dependent load.  Frame indices stay below 2^31.
-__device__ __forceinline__ uint64_t first_key(uint32_t gen, int64_t f, bool wf)
-{
-    return ((uint64_t)(~gen) << 32) | ((uint64_t)(uint32_t)f << 1) | (wf ? 1u : 0u);
-}
-
-__global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s, const uint8_t* __restrict__ frames,
-                                                               int64_t stride, int64_t count,
-                                                               const int32_t* __restrict__ ports,
-                                                               int32_t* __restrict__ action,
-                                                               uint32_t* __restrict__ psn_out)
-{
-    const int64_t f = (int64_t)blockIdx.x * kClaimBlock + threadIdx.x;
-    if (f >= count) return;
-    // rows are 4-byte aligned and at least 64 bytes: the header fields from four
-    // dword loads (bytes 36-43 and 48-55 of the row) instead of byte loads
-    const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + f * stride);
-    const uint32_t w9 = fw[9], w10 = fw[10], w12 = fw[12], w13 = fw[13];
-    const int port = ports[f];
-    const uint8_t op = (uint8_t)(w10 >> 16);                                    // byte 42
-    const uint32_t psn = ((w12 >> 24) << 16) | ((w13 & 0xFFu) << 8) | ((w13 >> 8) & 0xFFu);   // bytes 51-53, nts.c:311
-    const int udp_len = (int)(((w9 >> 16) & 0xFFu) << 8 | (w9 >> 24));          // bytes 38-39
-    int act = INCCL_SW_IGNORED;
-    if (port < 0 || port >= s.fan_in) act = INCCL_SW_INVALID;
-    else if (op == 0x11) act = INCCL_SW_ACK;                    // nts.c:336-342, :403-406 (reflect)
-    else if (is_data_opcode(op) || is_write_first(op)) {
-        const bool wf = is_write_first(op);
-        const int data_len = udp_len - 12 - 8 - 4 - (wf ? 16 : 0);   // nts.c:349, :429
-        // nts.c:350 asserts the length; the payload must also lie inside the row
-        if (data_len != kLanes * 4 || 54 + (wf ? 16 : 0) + kLanes * 4 > stride) act = INCCL_SW_INVALID;
-        else {
-            const uint32_t slot = psn & (s.slots - 1);
-            atomicAdd(&s.degree[slot], 1);                       // nts.c:351 / :431
-            atomicMin(reinterpret_cast<unsigned long long*>(&s.first[(size_t)slot * s.fan_in + port]),
-                      (unsigned long long)first_key(*s.gen + 1u, f, wf));
-            act = kActPending;
-        }
-    }
-    action[f] = act;
-    psn_out[f] = psn;
-}
-
-// Apply, several frames per wave.  A one-frame wave is a chain of dependent
-// round trips (its metadata -> its slot's bitmap and first copies -> the
-// payloads -> the stores), and with 131 072 short waves that latency, not HBM,
-// set the pass's time (102 us).  A wave now takes kApplyFrames consecutive
-// frames and runs each stage for all of them before the next, so every round
-// trip carries kApplyFrames frames' loads.  Template parameter: 2 by default
-// (82 us per 131 072-frame batch, against 97 at 4 and 113 at 8, where the
-// extra registers cost more occupancy than the shared round trips save;
-// profiles/r03/apply_frames_sweep.txt); $INCCL_APPLY_FRAMES = 1, 4 or 8 for sweeps.
-
 // payload word i of the frame at `fr`, its payload at byte 54 + 16*wf (2-byte
 // aligned), network order -> host order (nts.c:361-363)
 __device__ __forceinline__ uint32_t payload_word(const uint8_t* fr, uint32_t wf, int i)
@@ -661,16 +283,25 @@ __device__ __forceinline__ uint32_t payload_word(const uint8_t* fr, uint32_t wf,
     return __builtin_bswap32((uint32_t)d16[2 * i] | ((uint32_t)d16[2 * i + 1] << 16));
 }
 
-// Payload words 4 lane .. 4 lane + 3, host order.  With 16-byte aligned rows
-// (`wide`): the payload starts at 54 or 70, both 6 mod 16, so lane l loads the
-// aligned 16-byte chunk holding payload bytes 16 l - 6 .. 16 l + 9 in ONE
-// dwordx4 load and takes bytes 16 l + 10 .. 16 l + 15 from lane l+1's chunk
-// (lane 63 reads those six bytes, still inside the frame, as two dwords).  The
-// 2-byte-load fallback takes eight loads per lane.  Call in uniform control flow.
+// Payload words 4 lane .. 4 lane + 3, host order, from the 16-byte chunks that
+// hold them: the payload starts at byte 54 or 70, both 6 mod 16, so lane l's
+// words are bytes 6-15 of chunk `lo` and bytes 0-5 of chunk `hi` (the next one).
+__device__ __forceinline__ void payload_from_chunks(u4 lo, uint32_t hi0, uint32_t hi1, uint32_t (&w)[4])
+{
+    w[0] = __builtin_bswap32(__builtin_amdgcn_alignbyte(lo.z, lo.y, 2));
+    w[1] = __builtin_bswap32(__builtin_amdgcn_alignbyte(lo.w, lo.z, 2));
+    w[2] = __builtin_bswap32(__builtin_amdgcn_alignbyte(hi0, lo.w, 2));
+    w[3] = __builtin_bswap32(__builtin_amdgcn_alignbyte(hi1, hi0, 2));
+}
+
+// Payload words 4 lane .. 4 lane + 3, host order, loaded.  With 16-byte aligned
+// rows (`wide`) lane l loads the aligned chunk holding payload bytes 16 l - 6 ..
+// 16 l + 9 in ONE dwordx4 and takes bytes 16 l + 10 .. 16 l + 15 from lane l+1's
+// chunk (lane 63 reads those six bytes, still inside the frame, as two dwords).
+// The 2-byte-load fallback takes eight loads per lane.  Call in uniform control flow.
 __device__ __forceinline__ void payload16(const uint8_t* fr, uint32_t wf, int lane, bool wide, uint32_t (&w)[4])
 {
     if (wide) {
-        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
         const u4* c = reinterpret_cast<const u4*>(fr) + (3 + wf);
         const u4 a = c[lane];
         uint32_t n0 = (uint32_t)__shfl_down((int)a.x, 1, kWave), n1 = (uint32_t)__shfl_down((int)a.y, 1, kWave);
@@ -679,199 +310,21 @@ __device__ __forceinline__ void payload16(const uint8_t* fr, uint32_t wf, int la
             n0 = t[0];
             n1 = t[1];
         }
-        w[0] = __builtin_bswap32(__builtin_amdgcn_alignbyte(a.z, a.y, 2));
-        w[1] = __builtin_bswap32(__builtin_amdgcn_alignbyte(a.w, a.z, 2));
-        w[2] = __builtin_bswap32(__builtin_amdgcn_alignbyte(n0, a.w, 2));
-        w[3] = __builtin_bswap32(__builtin_amdgcn_alignbyte(n1, n0, 2));
+        payload_from_chunks(a, n0, n1, w);
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) w[j] = payload_word(fr, wf, 4 * lane + j);
     }
 }
 
-template <int kApplyFrames, bool kNtAgg = true>
-__global__ __launch_bounds__(kWave * 16) void k_ingress_apply(InccSwitchState s,
-                                                                         const uint8_t* __restrict__ frames,
-                                                                         int64_t stride, int64_t count,
-                                                                         const int32_t* __restrict__ ports,
-                                                                         int32_t* __restrict__ action,
-                                                                         const uint32_t* __restrict__ psns, bool wide)
+// The 16 RETH bytes of the frame at `fr` (bytes 54-69, util.c:409-417) as four
+// little-endian words, wave-uniform (2-byte loads: the RETH is 2-byte aligned).
+__device__ __forceinline__ void reth_words(const uint8_t* fr, int lane, uint32_t (&r)[4])
 {
-    const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    const int64_t f0 = ((int64_t)blockIdx.x * (blockDim.x / kWave) + w) * kApplyFrames;
-    if (f0 >= count) return;
-    const int fan = s.fan_in;
-    const uint32_t tag = ~(*s.gen + 1u), result_bit = 1u << fan;   // this batch's generation (k_ingress_commit)
-    // stage A: each frame's action, port and PSN
-    int act[kApplyFrames], port[kApplyFrames];
-    uint32_t psn[kApplyFrames];
+    const uint16_t* h = reinterpret_cast<const uint16_t*>(fr + 54);
+    const uint32_t v = lane < 4 ? ((uint32_t)h[2 * lane] | ((uint32_t)h[2 * lane + 1] << 16)) : 0u;
 #pragma unroll
-    for (int k = 0; k < kApplyFrames; ++k) {
-        const bool in = f0 + k < count;
-        act[k] = in ? action[f0 + k] : 0;
-        port[k] = in ? ports[f0 + k] : 0;
-        psn[k] = in ? psns[f0 + k] : 0;
-    }
-    // stage B: the slot as it was before the batch, and lane p < fan_in: the
-    // first-copy key of port p
-    uint32_t pre[kApplyFrames];
-    uint64_t key[kApplyFrames];
-#pragma unroll
-    for (int k = 0; k < kApplyFrames; ++k) {
-        const bool live = act[k] == kActPending;
-        const uint32_t slot = psn[k] & (s.slots - 1);
-        pre[k] = live ? s.arrival[slot] : 0u;
-        key[k] = live && lane < fan ? s.first[(size_t)slot * fan + lane] : 0ull;
-    }
-    // stage C: classify (nts.c:353-372) and find the slot leaders
-    int out_act[kApplyFrames];
-    bool lead[kApplyFrames];
-    uint64_t counted_ports[kApplyFrames];
-    uint32_t first_of[kApplyFrames], done_at[kApplyFrames];
-#pragma unroll
-    for (int k = 0; k < kApplyFrames; ++k) {
-        const int64_t f = f0 + k;
-        const bool live = act[k] == kActPending;
-        const uint32_t bit = 1u << port[k];
-        // lane p < fan_in: when port p's counted arrival happens, as 1 + frame
-        // index; 0 = before the batch, ~0 = not by the end of the batch
-        uint32_t at = 0, mine = 0xFFFFFFFFu, fo = 0xFFFFFFFFu;
-        bool counted = false;
-        if (lane < fan) {
-            const uint64_t e = key[k];
-            const bool in_batch = (uint32_t)(e >> 32) == tag;
-            const uint32_t ef = ((uint32_t)e) >> 1;
-            at = (pre[k] & (1u << lane)) ? 0u : (in_batch ? ef + 1u : 0xFFFFFFFFu);
-            mine = in_batch ? ef : 0xFFFFFFFFu;
-            fo = (uint32_t)e;                                   // frame << 1 | wf
-            counted = in_batch && !(pre[k] & (1u << lane));
-        }
-        counted_ports[k] = __ballot(counted);
-        first_of[k] = fo;
-        mine = (uint32_t)__shfl((int)mine, port[k] & (kWave - 1), kWave);
-        uint32_t d = at;                                        // max over ports: the completing arrival
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) {
-            const uint32_t v = (uint32_t)__shfl_xor((int)d, o, kWave);
-            d = v > d ? v : d;
-        }
-        done_at[k] = d = (uint32_t)__shfl((int)d, 0, kWave);
-        const bool arrival = live && !(pre[k] & bit) && mine == (uint32_t)f;   // the counted arrival: nts.c:359-363
-        if (arrival) {
-            out_act[k] = (d == (uint32_t)f + 1u) ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
-        } else {                                                 // retransmit: nts.c:353-357
-            const bool done_before = (pre[k] & result_bit) != 0;
-            const bool done_earlier = d != 0u && d != 0xFFFFFFFFu && d - 1u < (uint32_t)f;
-            out_act[k] = (done_before || done_earlier) ? INCCL_SW_REPLAY : INCCL_SW_DROPPED;
-        }
-        // The slot's counted arrivals of this batch are summed by ONE wave --
-        // the one holding the lowest counted port's frame -- into the slot's
-        // partial from earlier batches, with plain loads and stores: the same
-        // wrap-around sum as one atomic add per arrival (nts.c:361-363 /
-        // :443-445; integer addition commutes), without the atomics.
-        lead[k] = arrival && port[k] == __builtin_ctzll(counted_ports[k]);
-        // (the shuffle runs on every lane: a bpermute from a lane that is
-        // inactive in a divergent branch does not return that lane's value)
-        const uint32_t wf = (uint32_t)__shfl((int)fo, port[k] & (kWave - 1), kWave) & 1u;
-        if (arrival && lane < 4) {                               // reth_keeper, nts.c:442
-            if (wf) {
-                const uint16_t* r = reinterpret_cast<const uint16_t*>(frames + f * stride + 54);
-                s.reth[((size_t)(psn[k] & (s.slots - 1)) * fan + port[k]) * 4 + lane] =
-                    (uint32_t)r[2 * lane] | ((uint32_t)r[2 * lane + 1] << 16);
-            }
-        }
-    }
-    // stage D: the leaders' sums.  Every leader's slot partial and its two lowest
-    // counted ports' payloads are loaded before any is added (fan-in 2 needs no
-    // more); further ports, if any, follow.  Lane l owns words 4 l .. 4 l + 3:
-    // one dwordx4 per lane moves the slot's 1 KiB.
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    uint32_t acc[kApplyFrames][4], p0[kApplyFrames][4], p1[kApplyFrames][4];
-#pragma unroll
-    for (int k = 0; k < kApplyFrames; ++k) {
-        if (!lead[k]) continue;
-        // a slot whose arrival bitmap was empty before the batch holds zeros
-        // (reset, or recycled since its last use: nts.c:235-242), so its partial
-        // is not read -- in the common case, every port of a PSN in one batch,
-        // that saves a quarter of the pass's bytes
-        if (pre[k] != 0u) {
-            const u4 g = reinterpret_cast<const u4*>(s.agg + (size_t)(psn[k] & (s.slots - 1)) * kLanes)[lane];
-            acc[k][0] = g.x; acc[k][1] = g.y; acc[k][2] = g.z; acc[k][3] = g.w;
-        } else {
-            acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0u;
-        }
-        uint64_t m = counted_ports[k];
-        const uint32_t e0 = (uint32_t)__shfl((int)first_of[k], __builtin_ctzll(m), kWave);
-        m &= m - 1;
-        payload16(frames + (int64_t)(e0 >> 1) * stride, e0 & 1u, lane, wide, p0[k]);
-        if (m) {
-            const uint32_t e1 = (uint32_t)__shfl((int)first_of[k], __builtin_ctzll(m), kWave);
-            payload16(frames + (int64_t)(e1 >> 1) * stride, e1 & 1u, lane, wide, p1[k]);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) p1[k][j] = 0u;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < kApplyFrames; ++k) {
-        if (!lead[k]) continue;
-        const uint32_t slot = psn[k] & (s.slots - 1);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[k][j] += p0[k][j] + p1[k][j];
-        uint64_t m = counted_ports[k];
-        m &= m - 1;
-        m &= m - 1;
-        for (; m; m &= m - 1) {                                  // ports beyond the first two
-            const uint32_t e = (uint32_t)__shfl((int)first_of[k], __builtin_ctzll(m), kWave);
-            uint32_t pq[4];
-            payload16(frames + (int64_t)(e >> 1) * stride, e & 1u, lane, wide, pq);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[k][j] += pq[j];
-        }
-        {
-            const u4 o = u4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
-            u4* dst = reinterpret_cast<u4*>(s.agg + (size_t)slot * kLanes) + lane;
-            if constexpr (kNtAgg)   // non-temporal: 1.3 us off egress (profiles/r03/store_policy/)
-                __builtin_nontemporal_store(o, dst);
-            else
-                *dst = o;
-        }
-        // clear_state_data(psn + WINDOW) when the PSN completes in this batch
-        // (nts.c:235-242, :367): slot psn + slots/2, which no frame of the batch
-        // touches (a batch's PSNs are less than slots/2 apart).  Its bitmap, degree
-        // and RETH keeper are cleared; its 1 KiB of aggregator words are not: a
-        // slot whose bitmap is empty is summed from zero without reading them
-        // (above), and nothing else reads a slot before its next counted arrival
-        // rewrites them (egress reads completed slots only) -- 67 MB fewer stores
-        // per 131 072-frame batch
-        if (done_at[k] != 0xFFFFFFFFu) {
-            const uint32_t rs = (psn[k] + (s.slots >> 1)) & (s.slots - 1);
-            for (int i = lane; i < fan * 4; i += kWave) s.reth[(size_t)rs * fan * 4 + i] = 0;
-            if (lane == 0) {
-                s.arrival[rs] = 0;
-                s.degree[rs] = 0;
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < kApplyFrames; ++k)
-        if (lane == 0 && act[k] == kActPending && f0 + k < count) action[f0 + k] = out_act[k];
-}
-
-__global__ __launch_bounds__(kClaimBlock) void k_ingress_commit(InccSwitchState s, int64_t count,
-                                                                const int32_t* __restrict__ ports,
-                                                                const int32_t* __restrict__ action,
-                                                                const uint32_t* __restrict__ psns)
-{
-    const int64_t f = (int64_t)blockIdx.x * kClaimBlock + threadIdx.x;
-    // the batch is done with its generation (claim and apply ran before this
-    // launch): the next batch's is one higher
-    if (f == 0) *s.gen = *s.gen + 1u;
-    if (f >= count) return;
-    const int act = action[f];
-    if (act != INCCL_SW_ABSORBED && act != INCCL_SW_COMPLETED) return;
-    const uint32_t slot = psns[f] & (s.slots - 1);
-    atomicOr(&s.arrival[slot], (1u << ports[f]) | (act == INCCL_SW_COMPLETED ? 1u << s.fan_in : 0u));   // nts.c:359, :366
+    for (int i = 0; i < 4; ++i) r[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, i);
 }
 
 __device__ __forceinline__ void put16(uint8_t* p, uint32_t v)
@@ -1476,18 +929,682 @@ __global__ __launch_bounds__(kWave * 8) void k_egress_fixed(INCCL_EGRESS_FIXED_A
 }
 #undef INCCL_EGRESS_FIXED_ARGS
 
+
 // ---------------------------------------------------------------------------
-// host: CRC tables (util.c:141-159) and the zero-append operators per tree level
+// Ingress (nts.c:303-483, root branch) reproduces the reference's one-frame-at-
+// a-time order: frame index within the batch = arrival order.  What a serial
+// switch decides for frame f depends on which copies of its (psn, port) and of
+// its PSN's other ports came BEFORE f, so:
+//   claim   (a lane per frame) parse + validate; per (slot, port) an atomicMin
+//           of a batch-tagged frame index finds the first copy in the batch
+//   apply   the first copy of a pair whose port bit was not set before the
+//           batch is the arrival that counts: it adds its payload (nts.c:359-
+//           363) and keeps its RETH (:442).  The PSN completes at the LAST of
+//           its ports' counted arrivals (the max over ports of the first index;
+//           ports already in before the batch count as earlier than every
+//           frame): that frame is COMPLETED (:365-372), the others ABSORBED.
+//           Every other copy is a retransmit (:353): REPLAY if the slot completed
+//           before the batch or at an earlier frame of it (:354-356), else
+//           DROPPED.
+// Batch generation: claim tags its first-copy keys with g = gen[0] + 1 and
+// publishes g in gen[1]; apply reads g from gen[1] and stores it to gen[0] for
+// the next batch.  Each word is written while no kernel of the batch reads it,
+// and nothing changes on the host per batch, so a captured batch (hipGraph)
+// tags every replay anew.
+// ---------------------------------------------------------------------------
+constexpr int kActPending = 0x100;   // claim -> apply: a data frame still to classify, | its opcode
+constexpr int kClaimBlock = 256;
+
+// (~gen << 32) | (frame << 1) | wf: the minimum over a (slot, port)'s keys is the
+// newest batch's earliest copy (the frame index dominates bit 0), and bit 0 tells
+// apply where that copy's payload starts (byte 54, or 70 after a RETH) without
+// another dependent load.  Frame indices stay below 2^31.
+__device__ __forceinline__ uint64_t first_key(uint32_t gen, int64_t f, bool wf)
+{
+    return ((uint64_t)(~gen) << 32) | ((uint64_t)(uint32_t)f << 1) | (wf ? 1u : 0u);
+}
+
+// The batch call's per-child header terms, once per batch (claim's first wave):
+// lane i < 2 fan_in builds child i/2's header image with RETH flag i&1
+// (util.c:348-388; opcode, PSN and RETH left zero) and its ICRC term H =
+// Z_1024(raw CRC of frame bytes 10 .. doff-1 with the CRC init and the masks as
+// 0xFF) (util.c:250-286), into s.hdr: 2 * 31 images of 80 bytes, then the terms.
+__device__ uint32_t g_tab[256];   // util.c:141-150
+
+__device__ void header_terms(const InccSwitchState& s, const InccFrameTemplate* __restrict__ tmpl, int lane,
+                             uint8_t (*img)[kHdrImg], uint32_t* tab)
+{
+    for (int i = lane; i < 256; i += kWave) tab[i] = g_tab[i];
+    const int fan = s.fan_in;
+    if (lane < 2 * fan) build_header_image(img[lane], tmpl[lane >> 1], (lane & 1) != 0);
+    __builtin_amdgcn_wave_barrier();
+    if (lane >= 2 * fan) return;
+    const int wf = lane & 1, hdr = wf ? 60 : 44;
+    uint32_t c = 0;
+    for (int p = 0; p < hdr; ++p) {
+        const int fo = p + 10;
+        bool ff = fo < 14;
+#pragma unroll
+        for (int m = 4; m < kNumMasked; ++m) ff = ff || fo == masked_pos(m);
+        const uint32_t b = ff ? 0xFFu : img[lane][fo];
+        c = (c >> 8) ^ tab[(c ^ b) & 0xFFu];
+    }
+    uint32_t r = 0;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) r ^= g_z1024[n][(c >> (4 * n)) & 15u];   // past the 1024-byte payload
+    uint32_t* out = s.hdr + lane * (kHdrImg / 4);
+    const uint32_t* im = reinterpret_cast<const uint32_t*>(img[lane]);
+#pragma unroll
+    for (int i = 0; i < kHdrImg / 4; ++i) out[i] = im[i];
+    s.hdr[2 * 31 * (kHdrImg / 4) + lane] = r;
+}
+
+__global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s, const uint8_t* __restrict__ frames,
+                                                               int64_t stride, int64_t count,
+                                                               const int32_t* __restrict__ ports,
+                                                               int32_t* __restrict__ action,
+                                                               uint32_t* __restrict__ psn_out,
+                                                               const InccFrameTemplate* __restrict__ tmpl)
+{
+    const uint32_t g = *s.gen + 1u;   // this batch's generation
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) s.gen[1] = g;
+        if (tmpl && threadIdx.x < kWave) {
+            __shared__ __attribute__((aligned(16))) uint8_t img[2 * 31][kHdrImg];
+            __shared__ uint32_t tab[256];
+            header_terms(s, tmpl, threadIdx.x, img, tab);
+        }
+    }
+    const int64_t f = (int64_t)blockIdx.x * kClaimBlock + threadIdx.x;
+    if (f >= count) return;
+    // rows are 4-byte aligned and at least 64 bytes: the header fields from four
+    // dword loads (bytes 36-43 and 48-55 of the row) instead of byte loads
+    const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + f * stride);
+    const uint32_t w9 = fw[9], w10 = fw[10], w12 = fw[12], w13 = fw[13];
+    const int port = ports[f];
+    const uint8_t op = (uint8_t)(w10 >> 16);                                    // byte 42
+    const uint32_t psn = ((w12 >> 24) << 16) | ((w13 & 0xFFu) << 8) | ((w13 >> 8) & 0xFFu);   // bytes 51-53, nts.c:311
+    const int udp_len = (int)(((w9 >> 16) & 0xFFu) << 8 | (w9 >> 24));          // bytes 38-39
+    int act = INCCL_SW_IGNORED;
+    if (port < 0 || port >= s.fan_in) act = INCCL_SW_INVALID;
+    else if (op == 0x11) act = INCCL_SW_ACK;                    // nts.c:336-342, :403-406 (reflect)
+    else if (is_data_opcode(op) || is_write_first(op)) {
+        const bool wf = is_write_first(op);
+        const int data_len = udp_len - 12 - 8 - 4 - (wf ? 16 : 0);   // nts.c:349, :429
+        // nts.c:350 asserts the length; the payload must also lie inside the row
+        if (data_len != kLanes * 4 || 54 + (wf ? 16 : 0) + kLanes * 4 > stride) act = INCCL_SW_INVALID;
+        else {
+            const uint32_t slot = psn & (s.slots - 1);
+            atomicAdd(&s.degree[slot], 1);                       // nts.c:351 / :431
+            atomicMin(reinterpret_cast<unsigned long long*>(&s.first[(size_t)slot * s.fan_in + port]),
+                      (unsigned long long)first_key(g, f, wf));
+            act = kActPending | op;
+        }
+    }
+    action[f] = act;
+    psn_out[f] = psn;
+}
+
+// ---------------------------------------------------------------------------
+// Apply (after claim): one wave per two consecutive frames.
+//
+// A wave's work on its pair is three dependent memory round trips at most, and
+// in the common case -- every port of a PSN arriving as consecutive frames,
+// the reference's hosts posting one message each (api.c:293-327) -- two:
+//   1. the claim results (action | opcode, port, PSN) and, on 16-byte aligned
+//      rows, both rows' payload chunks, loaded before anything is known about
+//      the frames (lane l the 16-byte chunk 3 + l of each row, lanes 0 and 1
+//      also chunks 67 and 68: the payload starts 6 bytes into chunk 3 or 4,
+//      whichever the opcode says, so both placements are covered);
+//   2. the slot state, lane-parallel: lanes 32 k + p hold frame k's port p
+//      (first-copy key), lanes 32 k and 32 k + 1 its two tagged arrival words;
+//      in the batch call also the RETH keeper;
+//   3. only when needed: the slot's partial from earlier batches (its bitmap
+//      was not empty), the payload of a counted copy another wave holds.
+// The slot's counted arrivals of this batch are summed by ONE wave -- the one
+// holding the lowest counted port's first copy -- into the slot's partial with
+// plain loads and stores: the same wrap-around sum as one atomic add per
+// arrival (nts.c:361-363 / :443-445; integer addition commutes).  That wave
+// also writes the slot's new arrival bitmap, recycles slot psn + slots/2 when
+// the PSN completes (nts.c:235-242, :367: bitmap, degree and RETH keeper; the
+// 1 KiB of aggregator words are left, since a slot whose bitmap is empty is
+// summed from zero without reading them and nothing else reads a slot before
+// its next counted arrival rewrites them), and in the batch call builds the
+// completed PSN's fan_in broadcast frames (nts.c:447-453, util.c:331-442) from
+// the aggregate in its registers.  Waves are short and not persistent: a wave
+// leaves once its stores are issued and the next starts, which hides the
+// latency a persistent loop would wait out before every next round trip (on
+// gfx9 loads and stores retire in order on one counter).
+//
+// Arrival bitmap: every frame classifies against the bitmap as it was before
+// the batch, while the summing wave writes the new one in the same launch.  A
+// slot holds two 64-bit words {bits, tag = the batch that wrote them}; batch g
+// writes word g & 1 only, and reads the newer of the words whose tag is not g.
+// Whether a reader sees a word before or after batch g's store, it gets the
+// pre-batch bitmap (64-bit accesses are single-copy atomic).  The recycle
+// writes both words (no frame of the batch reads that slot).
+// ---------------------------------------------------------------------------
+constexpr int kApplyWaves = 8;
+
+struct ApplyArgs {
+    InccSwitchState s;
+    const uint8_t* frames;
+    int64_t stride, count;
+    const int32_t* ports;
+    int32_t* action;
+    const uint32_t* psns;
+    uint8_t* out;                    // batch call: the output rows and lengths
+    int64_t out_stride;
+    int32_t* out_len;
+    int wide;                        // 16-byte aligned rows
+};
+
+// the arrival bitmap as it was before batch g: the newer of the two tagged
+// words that batch g did not write (nts.c:59)
+__device__ __forceinline__ uint32_t arrival_before(uint64_t w0, uint64_t w1, uint32_t g)
+{
+    const uint32_t t0 = (uint32_t)(w0 >> 32), t1 = (uint32_t)(w1 >> 32);
+    const uint32_t d0 = t0 == g ? 0xFFFFFFFFu : g - t0, d1 = t1 == g ? 0xFFFFFFFFu : g - t1;
+    return d0 <= d1 ? (uint32_t)w0 : (uint32_t)w1;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
+{
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
+}
+
+// A buffer resource over [base, base + bytes) whose fields are wave-uniform by
+// construction: a resource the compiler cannot prove uniform is used through a
+// readfirstlane "waterfall" loop around every load and store.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int64_t bytes)
+{
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+    const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+
+// The batch call's egress tables in LDS.  The payload's ICRC contribution is
+// P = XOR over lanes of Z_{16 (63 - lane)}(crc of lane's 16 bytes); the shift
+// is taken in two steps, Z_{16 (7 - lane % 8)} then, once the 8 lanes of a
+// group are XORed, Z_{128 (7 - lane / 8)}: 8 KiB of tables where one step
+// would need 32 KiB, so that a short-lived block loads them cheaply.
+__device__ uint32_t g_ls[8][16][8];   // [nibble][value][lane % 8] = Z_{16 (7 - lane % 8)}(value << 4 nibble)
+__device__ uint32_t g_gs[8][16][8];   // [nibble][value][lane / 8] = Z_{128 (7 - lane / 8)}(value << 4 nibble)
+
+struct EmitLds {
+    uint32_t seg[16][2][16];          // segment byte j: Z_{15-j}(T[value << 4 nibble]) (g_seg rows 1-16)
+    uint32_t ls[8][16][8];
+    uint32_t gs[8][16][8];
+    uint32_t var[kVarRows][2][16];
+    uint32_t hcrc[2 * 31];
+    __attribute__((aligned(16))) uint8_t img[2 * 31][kHdrImg];
+};
+constexpr int kEmitFixedU4 = (sizeof(uint32_t) * (16 * 2 * 16 + 2 * 8 * 16 * 8 + kVarRows * 2 * 16)) / 16;
+
+template <bool kEmit>
+struct ApplyShared {};
+template <>
+struct ApplyShared<true> {
+    EmitLds t;
+};
+
+// t.ls / t.gs applied to c: 8 nibble lookups at column col
+__device__ __forceinline__ uint32_t shift8(const uint32_t (*tab)[16][8], uint32_t c, int col)
+{
+    const uint32_t lo = opaque_u32(c & 0x0F0F0F0Fu), hi = opaque_u32((c >> 4) & 0x0F0F0F0Fu);
+    uint32_t v[8];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        v[2 * b] = tab[2 * b][(uint8_t)(lo >> (8 * b))][col];
+        v[2 * b + 1] = tab[2 * b + 1][(uint8_t)(hi >> (8 * b))][col];
+    }
+    return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
+}
+
+// P for the aggregate whose bytes (big-endian, memory order) lane l holds in a[]
+__device__ __forceinline__ uint32_t payload_crc(const EmitLds& t, const uint32_t (&a)[4], int lane)
+{
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t lo = opaque_u32(a[k] & 0x0F0F0F0Fu), hi = opaque_u32((a[k] >> 4) & 0x0F0F0F0Fu);
+        uint32_t v[8];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            v[2 * b] = t.seg[4 * k + b][0][(uint8_t)(lo >> (8 * b))];
+            v[2 * b + 1] = t.seg[4 * k + b][1][(uint8_t)(hi >> (8 * b))];
+        }
+        c = xor3(xor3(xor3(c, v[0], v[1]), v[2], v[3]), xor3(v[4], v[5], v[6]), v[7]);
+    }
+    c = shift8(t.ls, c, lane & 7);
+    // XOR the group of 8: quads, then the half-row mirror
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    c = shift8(t.gs, c, lane >> 3);
+    // XOR the 8 groups: the row mirror pairs them, the row broadcasts end in lane 63
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x140, 0xF, 0xF, false);   // row_mirror
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x142, 0xA, 0xF, false);   // row_bcast15 -> rows 1, 3
+    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x143, 0xC, 0xF, false);   // row_bcast31 -> rows 2, 3
+    return (uint32_t)__builtin_amdgcn_readlane((int)c, 63);
+}
+
+// Child c's frame of one aggregate into `row`: the header chunks (lanes below
+// hchunks) from the template image with the opcode (byte 42), the PSN (50-53),
+// the RETH R (54-69, util.c:409-417) and the payload's first 10 bytes (a0..a2
+// of lane 0) patched in; the payload chunks (pcs: output chunk hchunks + l)
+// from registers; the ICRC by linearity, ~(P ^ V_op,psn ^ H_c ^ V_reth) with
+// pc = P ^ V_op,psn (util.c:424-426).  Every lane stores: what it must not
+// write goes past the row (dropped).
+template <bool kOut16>
+__device__ __forceinline__ void emit_child(const EmitLds& t, int c, int wf, uint32_t op, uint32_t pw, uint32_t pc,
+                                           const uint32_t (&pcs)[4], uint32_t a0, uint32_t a1, uint32_t a2,
+                                           uint32_t a3, const uint32_t (&R)[4], uint8_t* row, int64_t out_stride,
+                                           int lane)
+{
+    const int doff = 54 + 16 * wf;
+    const int hchunks = doff / 16 + 1;
+    uint32_t vr = 0;
+    if (wf) {
+        // lane k < 16: RETH byte k = byte k & 3 of word k >> 2
+        const uint32_t rk = (lane & 8) ? ((lane & 4) ? R[3] : R[2]) : ((lane & 4) ? R[1] : R[0]);
+        vr = wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
+    }
+    const uint32_t crc = ~(pc ^ t.hcrc[2 * c + wf] ^ vr);
+    const uint32_t psn_hi = (pw >> 24) | (((pw >> 16) & 0xFFu) << 8);    // frame bytes 50, 51 (util.c:386)
+    const uint32_t psn_lo = ((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8);   // bytes 52, 53
+    const u4 img = reinterpret_cast<const u4*>(t.img[2 * c + wf])[lane < 5 ? lane : 0];
+    uint32_t h0 = img.x, h1 = img.y, h2 = img.z, h3 = img.w;
+    if (lane == 2) h2 = (h2 & 0xFF00FFFFu) | (op << 16);
+    if (lane == 3) {
+        const uint32_t b0 = wf ? R[0] : a0, b1 = wf ? R[1] : a1, b2 = wf ? R[2] : a2;   // bytes 54-63
+        h0 = (h0 & 0xFFFFu) | (psn_hi << 16);
+        h1 = psn_lo | (b0 << 16);
+        h2 = __builtin_amdgcn_alignbyte(b1, b0, 2);
+        h3 = __builtin_amdgcn_alignbyte(b2, b1, 2);
+    }
+    if (lane == 4) {                                                    // RETH frames only: bytes 64-79
+        h0 = __builtin_amdgcn_alignbyte(R[3], R[2], 2);
+        h1 = (R[3] >> 16) | (a0 << 16);
+        h2 = __builtin_amdgcn_alignbyte(a1, a0, 2);
+        h3 = __builtin_amdgcn_alignbyte(a2, a1, 2);
+    }
+    const u4 h = {h0, h1, h2, h3};
+    const __amdgpu_buffer_rsrc_t orow = uniform_rsrc(row, out_stride);
+    // the last chunk (lane 63): payload bytes 1018-1023, the ICRC stored host
+    // order (LE), two bytes of zero padding
+    const u4 v = lane < kWave - 1 ? u4{pcs[0], pcs[1], pcs[2], pcs[3]}
+                                  : u4{pcs[0], (a3 >> 16) | ((crc & 0xFFFFu) << 16), crc >> 16, 0u};
+    const int ho = lane < hchunks ? 16 * lane : kOobOffset, po = 16 * (hchunks + lane);
+    if (kOut16) {
+        __builtin_amdgcn_raw_buffer_store_b128(h, orow, ho, 0, kAuxNt);
+        __builtin_amdgcn_raw_buffer_store_b128(v, orow, po, 0, kAuxNt);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(h.x, orow, ho, 0, kAuxNt);
+        __builtin_amdgcn_raw_buffer_store_b32(h.y, orow, ho + 4, 0, kAuxNt);
+        __builtin_amdgcn_raw_buffer_store_b32(h.z, orow, ho + 8, 0, kAuxNt);
+        __builtin_amdgcn_raw_buffer_store_b32(h.w, orow, ho + 12, 0, kAuxNt);
+        __builtin_amdgcn_raw_buffer_store_b32(v.x, orow, po, 0, kAuxNt);
+        __builtin_amdgcn_raw_buffer_store_b32(v.y, orow, po + 4, 0, kAuxNt);
+        __builtin_amdgcn_raw_buffer_store_b32(v.z, orow, po + 8, 0, kAuxNt);
+        // lane 63 stops at the frame's 4-byte-rounded end
+        __builtin_amdgcn_raw_buffer_store_b32(v.w, orow, lane < kWave - 1 ? po + 12 : kOobOffset, 0, kAuxNt);
+    }
+}
+
+template <bool kEmit, bool kOut16>
+__global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_apply(ApplyArgs A)
+{
+    const InccSwitchState& s = A.s;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    const int fan = s.fan_in;
+    const int64_t count = A.count, stride = A.stride;
+    const int64_t pidx = (int64_t)blockIdx.x * kApplyWaves + w;   // this wave's pair
+    const bool have = 2 * pidx < count;   // (a wave without a pair still joins its block's table load)
+    const int64_t f0 = have ? 2 * pidx : 0;
+    const bool in1 = have && f0 + 1 < count;
+    const int64_t f1 = in1 ? f0 + 1 : f0;
+    // round trip 1: the payload chunks of both rows, and the claim results
+    u4 x[2] = {}, e[2] = {};
+    if (A.wide) {
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(A.frames + f0 * stride, have ? (in1 ? 2 : 1) * stride : 0);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int rb = k * (int)stride;
+            x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, rb + 48 + 16 * lane, 0, 0);
+            e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane < 2 ? rb + 1072 + 16 * lane : kOobOffset, 0, 0);
+        }
+    }
+    const uint32_t g = s.gen[1];   // this batch's generation (claim's)
+    int act[2], port[2];
+    uint32_t psn[2];
+    act[0] = A.action[f0];
+    act[1] = A.action[f1];
+    port[0] = A.ports[f0];
+    port[1] = A.ports[f1];
+    psn[0] = A.psns[f0];
+    psn[1] = A.psns[f1];
+    if (!have) act[0] = INCCL_SW_IGNORED;
+    if (!in1) act[1] = INCCL_SW_IGNORED;
+    // the batch call's tables, while round trip 1 is in flight
+    __shared__ ApplyShared<kEmit> sh;
+    if constexpr (kEmit) {
+        // the four fixed tables are one contiguous run of u4 in EmitLds, read
+        // from their own arrays; two u4 per thread (clamped indices: a thread
+        // past the end rewrites the last entry)
+        constexpr int kThreads = kWave * kApplyWaves;
+        auto src = [&](int i) -> u4 {
+            constexpr int n0 = 16 * 2 * 16 / 4, n1 = n0 + 8 * 16 * 8 / 4, n2 = n1 + 8 * 16 * 8 / 4;
+            return i < n0 ? reinterpret_cast<const u4*>(&g_seg[1][0][0])[i]
+                 : i < n1 ? reinterpret_cast<const u4*>(&g_ls[0][0][0])[i - n0]
+                 : i < n2 ? reinterpret_cast<const u4*>(&g_gs[0][0][0])[i - n1]
+                          : reinterpret_cast<const u4*>(&g_var[0][0][0])[i - n2];
+        };
+        const int i0 = (int)threadIdx.x < kEmitFixedU4 ? (int)threadIdx.x : kEmitFixedU4 - 1;
+        const int i1 = (int)threadIdx.x + kThreads < kEmitFixedU4 ? (int)threadIdx.x + kThreads : kEmitFixedU4 - 1;
+        const u4 v0 = src(i0), v1 = src(i1);
+        // this fan-in's header images and terms (claim's first wave wrote them)
+        const int nh = 2 * fan * (kHdrImg / 4), nt = nh + 2 * fan;
+        int j[3];
+        uint32_t hv[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            j[r] = (int)threadIdx.x + r * kThreads < nt ? (int)threadIdx.x + r * kThreads : nt - 1;
+            hv[r] = j[r] < nh ? s.hdr[j[r]] : s.hdr[2 * 31 * (kHdrImg / 4) + (j[r] - nh)];
+        }
+        u4* tf = reinterpret_cast<u4*>(&sh.t.seg[0][0][0]);
+        tf[i0] = v0;
+        tf[i1] = v1;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            if (j[r] < nh) reinterpret_cast<uint32_t*>(&sh.t.img[0][0])[j[r]] = hv[r];
+            else sh.t.hcrc[j[r] - nh] = hv[r];
+        }
+        __syncthreads();
+    }
+    const uint32_t tag = ~g, result_bit = 1u << fan, smask = s.slots - 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) s.gen[0] = g;   // the next batch's claim adds one
+    bool live[2];
+    uint32_t op[2], wf[2], slot[2];
+    uint32_t P[2][4], R[2][4];   // each frame's payload words (this lane's four) and RETH words (uniform)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        live[k] = (act[k] & ~0xFF) == kActPending;
+        op[k] = (uint32_t)act[k] & 0xFFu;
+        wf[k] = is_write_first((uint8_t)op[k]) ? 1u : 0u;
+        slot[k] = psn[k] & smask;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) P[k][j] = R[k][j] = 0u;
+        if (!live[k]) continue;
+        if (A.wide) {
+            // chunk 4 + lane (lane 63: chunk 67) and 5 + lane (lane 62: 67, lane 63: 68)
+            uint32_t y0 = (uint32_t)__shfl_down((int)x[k].x, 1, kWave), y1 = (uint32_t)__shfl_down((int)x[k].y, 1, kWave);
+            const uint32_t c67x = (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 0);
+            const uint32_t c67y = (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 0);
+            if (lane == kWave - 1) {
+                y0 = c67x;
+                y1 = c67y;
+            }
+            if (wf[k]) {
+                uint32_t y2 = (uint32_t)__shfl_down((int)x[k].z, 1, kWave), y3 = (uint32_t)__shfl_down((int)x[k].w, 1, kWave);
+                uint32_t z0 = (uint32_t)__shfl_down((int)y0, 1, kWave), z1 = (uint32_t)__shfl_down((int)y1, 1, kWave);
+                if (lane == kWave - 1) {
+                    y2 = (uint32_t)__builtin_amdgcn_readlane((int)e[k].z, 0);
+                    y3 = (uint32_t)__builtin_amdgcn_readlane((int)e[k].w, 0);
+                    z0 = (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 1);
+                    z1 = (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 1);
+                }
+                payload_from_chunks(u4{y0, y1, y2, y3}, z0, z1, P[k]);
+                // the RETH, bytes 54-69: bytes 6-15 of chunk 3 (lane 0), 0-5 of chunk 4 (lane 1)
+                const uint32_t c3y = (uint32_t)__builtin_amdgcn_readlane((int)x[k].y, 0);
+                const uint32_t c3z = (uint32_t)__builtin_amdgcn_readlane((int)x[k].z, 0);
+                const uint32_t c3w = (uint32_t)__builtin_amdgcn_readlane((int)x[k].w, 0);
+                const uint32_t c4x = (uint32_t)__builtin_amdgcn_readlane((int)x[k].x, 1);
+                const uint32_t c4y = (uint32_t)__builtin_amdgcn_readlane((int)x[k].y, 1);
+                R[k][0] = __builtin_amdgcn_alignbyte(c3z, c3y, 2);
+                R[k][1] = __builtin_amdgcn_alignbyte(c3w, c3z, 2);
+                R[k][2] = __builtin_amdgcn_alignbyte(c4x, c3w, 2);
+                R[k][3] = __builtin_amdgcn_alignbyte(c4y, c4x, 2);
+            } else {
+                payload_from_chunks(x[k], y0, y1, P[k]);
+            }
+        } else {
+            const uint8_t* fr = A.frames + (f0 + k) * stride;
+            payload16(fr, wf[k], lane, false, P[k]);
+            if (wf[k]) reth_words(fr, lane, R[k]);
+        }
+    }
+    // round trip 2, lane-parallel over the two frames: half h = lane / 32 is
+    // frame h; lane 32 h + p < 32 h + fan_in loads port p's first-copy key,
+    // lanes 32 h and 32 h + 1 the two tagged arrival words
+    const int hf = lane >> 5, pl = lane & 31;
+    const bool live_h = hf ? live[1] : live[0];
+    const uint32_t slot_h = hf ? slot[1] : slot[0];
+    const uint64_t key = live_h && pl < fan ? s.first[(size_t)slot_h * fan + pl] : 0ull;
+    const uint64_t av = live_h && pl < 2 ? s.arrival[2 * (size_t)slot_h + pl] : 0ull;
+    uint32_t keep[2] = {0u, 0u};   // the batch call: the RETH keeper of each frame's slot
+    if (kEmit) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (live[k]) keep[k] = s.reth[(size_t)slot[k] * fan * 4 + (lane < 4 * fan ? lane : 0)];
+    }
+    uint32_t pre[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) pre[k] = live[k] ? arrival_before(readlane64(av, 32 * k), readlane64(av, 32 * k + 1), g) : 0u;
+    // classify (nts.c:353-372): lane 32 h + p < fan_in says when frame h's port
+    // p counts, as 1 + frame index; 0 = before the batch, ~0 = not in this batch
+    const uint32_t pre_h = hf ? pre[1] : pre[0];
+    uint32_t at = 0, mine = 0xFFFFFFFFu, fo = 0xFFFFFFFFu;
+    bool counted = false;
+    if (live_h && pl < fan) {
+        const bool in_batch = (uint32_t)(key >> 32) == tag;
+        const uint32_t ef = ((uint32_t)key) >> 1;
+        at = (pre_h & (1u << pl)) ? 0u : (in_batch ? ef + 1u : 0xFFFFFFFFu);
+        mine = in_batch ? ef : 0xFFFFFFFFu;
+        fo = (uint32_t)key;                                 // frame << 1 | wf
+        counted = in_batch && !(pre_h & (1u << pl));
+    }
+    const uint64_t bal = __ballot(counted);
+    uint32_t d = at;                                        // max over each half: the completing arrival
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) {
+        const uint32_t v = (uint32_t)__shfl_xor((int)d, o, kWave);
+        d = v > d ? v : d;
+    }
+    int out_act[2];
+    bool lead[2], counted_me[2];
+    uint32_t cports[2], done_at[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        out_act[k] = act[k];
+        cports[k] = (uint32_t)(bal >> (32 * k));
+        done_at[k] = (uint32_t)__builtin_amdgcn_readlane((int)d, 32 * k);
+        lead[k] = counted_me[k] = false;
+        if (!live[k]) continue;
+        const uint32_t f = (uint32_t)(f0 + k);
+        const uint32_t mk = (uint32_t)__builtin_amdgcn_readlane((int)mine, 32 * k + port[k]);
+        const uint32_t dk = done_at[k];
+        const bool arrival = !(pre[k] & (1u << port[k])) && mk == f;   // the counted arrival: nts.c:359-363
+        counted_me[k] = arrival;
+        if (arrival) {
+            out_act[k] = (dk == f + 1u) ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
+        } else {                                                 // retransmit: nts.c:353-357
+            const bool done_before = (pre[k] & result_bit) != 0;
+            const bool done_earlier = dk != 0u && dk != 0xFFFFFFFFu && dk - 1u < f;
+            out_act[k] = (done_before || done_earlier) ? INCCL_SW_REPLAY : INCCL_SW_DROPPED;
+        }
+        lead[k] = arrival && port[k] == __builtin_ctz(cports[k]);
+    }
+    // the leaders: sum, store, bitmap, recycle, broadcast
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (!lead[k]) continue;
+        u4 acc = {0u, 0u, 0u, 0u};
+        // a slot whose bitmap was empty before the batch holds zeros (reset,
+        // or recycled since its last use), so its partial is not read
+        if (pre[k] != 0u) acc = reinterpret_cast<const u4*>(s.agg + (size_t)slot[k] * kLanes)[lane];
+        for (uint32_t m = cports[k]; m; m &= m - 1) {
+            const uint32_t ek = (uint32_t)__builtin_amdgcn_readlane((int)fo, 32 * k + __builtin_ctz(m));
+            const int64_t fe = (int64_t)(ek >> 1);
+            uint32_t q[4];
+            if (fe == f0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) q[j] = P[0][j];
+            } else if (in1 && fe == f1) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) q[j] = P[1][j];
+            } else {
+                payload16(A.frames + fe * stride, ek & 1u, lane, A.wide != 0, q);
+            }
+            acc.x += q[0];
+            acc.y += q[1];
+            acc.z += q[2];
+            acc.w += q[3];
+        }
+        __builtin_nontemporal_store(acc, reinterpret_cast<u4*>(s.agg + (size_t)slot[k] * kLanes) + lane);
+        const bool complete = done_at[k] != 0xFFFFFFFFu;
+        if (lane == 0)
+            s.arrival[2 * (size_t)slot[k] + (g & 1u)] =
+                ((uint64_t)g << 32) | (pre[k] | cports[k] | (complete ? result_bit : 0u));   // nts.c:359, :366
+        if (!complete) continue;
+        {   // clear_state_data(psn + WINDOW), nts.c:235-242, :367
+            const uint32_t rs = (psn[k] + (s.slots >> 1)) & smask;
+            for (int i = lane; i < fan * 4; i += kWave) s.reth[(size_t)rs * fan * 4 + i] = 0u;
+            if (lane < 2) s.arrival[2 * (size_t)rs + lane] = (uint64_t)g << 32;
+            if (lane == 0) s.degree[rs] = 0;
+        }
+        if constexpr (kEmit) {
+            const EmitLds& t = sh.t;
+            // the broadcast of the completing frame fd (nts.c:447-453): its
+            // opcode, this PSN, each child's RETH as the keeper now holds it
+            const int64_t fd = (int64_t)done_at[k] - 1;
+            uint32_t opd;
+            if (fd == f0) opd = op[0];
+            else if (in1 && fd == f1) opd = op[1];
+            else {
+                const uint32_t w10 = reinterpret_cast<const uint32_t*>(A.frames + fd * stride)[10 + (lane & 1)];
+                opd = ((uint32_t)__builtin_amdgcn_readlane((int)w10, 0) >> 16) & 0xFFu;
+            }
+            const int wfd = is_write_first((uint8_t)opd) ? 1 : 0;
+            uint32_t a[4];   // this lane's 16 payload bytes, big-endian (util.c:403-405), memory order
+            a[0] = __builtin_bswap32(acc.x);
+            a[1] = __builtin_bswap32(acc.y);
+            a[2] = __builtin_bswap32(acc.z);
+            a[3] = __builtin_bswap32(acc.w);
+            uint32_t nx[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) nx[j] = (uint32_t)__shfl_down((int)a[j], 1, kWave);
+            const uint32_t pcs[4] = {__builtin_amdgcn_alignbyte(a[3], a[2], 2), __builtin_amdgcn_alignbyte(nx[0], a[3], 2),
+                                     __builtin_amdgcn_alignbyte(nx[1], nx[0], 2), __builtin_amdgcn_alignbyte(nx[2], nx[1], 2)};
+            const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)a[0], 0);
+            const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)a[1], 0);
+            const uint32_t a2 = (uint32_t)__builtin_amdgcn_readlane((int)a[2], 0);
+            const uint32_t pw = psn[k] | 0x80000000u;
+            // P, and the opcode and PSN bytes (util.c:378, :386) on lanes 0-4
+            const uint32_t vb = lane < 5 ? var_crc(t, wfd, lane, lane == 0 ? opd : (pw >> (8 * (4 - lane))) & 0xFFu) : 0u;
+            const uint32_t pc = payload_crc(t, a, lane) ^ (uint32_t)__builtin_amdgcn_readlane((int)vb, 0) ^
+                                (uint32_t)__builtin_amdgcn_readlane((int)vb, 1) ^ (uint32_t)__builtin_amdgcn_readlane((int)vb, 2) ^
+                                (uint32_t)__builtin_amdgcn_readlane((int)vb, 3) ^ (uint32_t)__builtin_amdgcn_readlane((int)vb, 4);
+            for (int c = 0; c < fan; ++c) {
+                uint32_t Rc[4] = {0u, 0u, 0u, 0u};
+                if (wfd) {
+                    const uint32_t ec = (uint32_t)__builtin_amdgcn_readlane((int)fo, 32 * k + c);
+                    if (((cports[k] >> c) & 1u) && (ec & 1u)) {   // counted in this batch from a WRITE_FIRST copy
+                        const int64_t fe = (int64_t)(ec >> 1);
+                        if (fe == f0) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) Rc[j] = R[0][j];
+                        } else if (in1 && fe == f1) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) Rc[j] = R[1][j];
+                        } else {
+                            reth_words(A.frames + fe * stride, lane, Rc);
+                        }
+                    } else if (c < kWave / 4) {                 // the keeper, as loaded
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) Rc[j] = (uint32_t)__builtin_amdgcn_readlane((int)keep[k], 4 * c + j);
+                    } else {
+                        const uint32_t v = s.reth[((size_t)slot[k] * fan + c) * 4 + (lane & 3)];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) Rc[j] = (uint32_t)__builtin_amdgcn_readlane((int)v, j);
+                    }
+                }
+                emit_child<kOut16>(t, c, wfd, opd, pw, pc, pcs, a0, a1, a2, a[3], Rc, A.out + (fd * fan + c) * A.out_stride,
+                                   A.out_stride, lane);
+            }
+        }
+    }
+    // every frame: its action, its RETH into the keeper if it is a counted
+    // WRITE_FIRST (nts.c:442), and (batch call) its rows' lengths
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (k == 0 ? !have : !in1) continue;
+        const int64_t f = f0 + k;
+        if (live[k] && lane == 0) A.action[f] = out_act[k];
+        if (counted_me[k] && wf[k] && lane < 4)
+            s.reth[((size_t)slot[k] * fan + port[k]) * 4 + lane] =
+                lane == 0 ? R[k][0] : lane == 1 ? R[k][1] : lane == 2 ? R[k][2] : R[k][3];
+        if (kEmit && lane < fan) {
+            const int fin = out_act[k];
+            const int total = 54 + 16 * (int)wf[k] + kLanes * 4 + 4;   // util.c:341-345
+            A.out_len[f * fan + lane] =
+                (live[k] && (fin == INCCL_SW_COMPLETED || (fin == INCCL_SW_REPLAY && lane == port[k]))) ? total : 0;
+        }
+    }
+}
+
+// The batch call's REPLAY resends (nts.c:353-356 / :435-438), after apply: a
+// slot that completed earlier in the same batch has its aggregate only now.
+// Each block scans its share of the actions; a block with no REPLAY leaves
+// before loading any table (the common case: no retransmits).
+__global__ __launch_bounds__(kWave* kEgressWaves) void k_replay(InccSwitchState s, const uint8_t* __restrict__ in_frames,
+                                                                int64_t in_stride, int64_t count,
+                                                                const int32_t* __restrict__ ports,
+                                                                const int32_t* __restrict__ action,
+                                                                const uint32_t* __restrict__ psns,
+                                                                const InccFrameTemplate* __restrict__ tmpl,
+                                                                uint8_t* __restrict__ out, int64_t out_stride,
+                                                                int32_t* __restrict__ out_len)
+{
+    __shared__ EgressLds t;
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kEgressWaves][80];
+    __shared__ __attribute__((aligned(16))) uint8_t himg[2 * 31][kHdrImg];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    const int64_t per = ((count + gridDim.x - 1) / gridDim.x + kWave - 1) / kWave * kWave;
+    const int64_t b0 = (int64_t)blockIdx.x * per, b1 = b0 + per < count ? b0 + per : count;
+    int any = 0;
+    for (int64_t f = b0 + threadIdx.x; f < b1; f += blockDim.x) any |= action[f] == INCCL_SW_REPLAY;
+    if (!__syncthreads_or(any)) return;
+    egress_setup(t, himg, tmpl, s.fan_in, w, lane);
+    const bool out16 = ((out_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+    for (int64_t base = b0 + (int64_t)w * kWave; base < b1; base += (int64_t)kEgressWaves * kWave) {
+        const int64_t f = base + lane;
+        uint64_t m = __ballot(f < b1 && action[f] == INCCL_SW_REPLAY);
+        while (m) {
+            const int64_t fr = base + __builtin_ctzll(m);
+            m &= m - 1;
+            const EgressIn e = egress_fetch(s, in_frames, in_stride, ports, action, psns, fr, lane);
+            egress_emit(s, e, himg, out, out_stride, out16, out_len, t, buf[w], fr, lane);
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// host: CRC tables (util.c:141-159) and the zero-append operators
 // ---------------------------------------------------------------------------
 uint32_t host_tab[256];
 uint32_t host_seg[kSeg][2][16];
-uint32_t host_segb[kSeg][256];
-uint32_t host_lane_shift[8][16][kWave];
 uint32_t host_lane16[8][16][kWave];
 uint32_t host_seg34[kSeg2][2][16];
 uint32_t host_lane_shift32[8][16][32];
 uint32_t host_var[5 + kVarBytes][2][16];
 uint32_t host_z1024[8][16];
+uint32_t host_ls[8][16][8];
+uint32_t host_gs[8][16][8];
 bool g_tables_ready[64];
 std::mutex g_tables_mu;
 
@@ -1512,18 +1629,8 @@ int ensure_tables()
     for (int j = 0; j < kSeg; ++j)
         for (int h = 0; h < 2; ++h)
             for (uint32_t v = 0; v < 16; ++v) host_seg[j][h][v] = zeros_append(host_tab[v << (4 * h)], kSeg - 1 - j);
-    for (int j = 0; j < kSeg; ++j)
-        for (uint32_t v = 0; v < 256; ++v) host_segb[j][v] = zeros_append(host_tab[v], kSeg - 1 - j);
-    // Z_n is linear: Z_{n+17}(x) = Z_17(Z_n(x)), so lanes are filled from 63 down
-    for (int n = 0; n < 8; ++n)
-        for (uint32_t v = 0; v < 16; ++v) {
-            uint32_t x = v << (4 * n);
-            for (int lane = kWave - 1; lane >= 0; --lane) {
-                host_lane_shift[n][v][lane] = x;
-                x = zeros_append(x, kSeg);
-            }
-        }
-    // the paired ICRC (k_icrc_pair): 34-byte segments, Z_{34 (31 - lane')}
+    // the standalone ICRC (k_icrc): 34-byte segments, Z_{34 (31 - lane')}; Z_n is
+    // linear, Z_{n+34}(x) = Z_34(Z_n(x)), so lanes are filled from 31 down
     for (int j = 0; j < kSeg2; ++j)
         for (int h = 0; h < 2; ++h)
             for (uint32_t v = 0; v < 16; ++v) host_seg34[j][h][v] = zeros_append(host_tab[v << (4 * h)], kSeg2 - 1 - j);
@@ -1535,8 +1642,8 @@ int ensure_tables()
                 x = zeros_append(x, kSeg2);
             }
         }
-    // egress by linearity (k_egress): Z_{16 (63 - lane)}, each variable header
-    // byte's contribution shifted to the message end, and Z_1024
+    // egress by linearity: Z_{16 (63 - lane)}, each variable header byte's
+    // contribution shifted to the message end, and Z_1024
     for (int n = 0; n < 8; ++n)
         for (uint32_t v = 0; v < 16; ++v) {
             uint32_t x = v << (4 * n);
@@ -1544,6 +1651,17 @@ int ensure_tables()
             for (int lane = kWave - 1; lane >= 0; --lane) {
                 host_lane16[n][v][lane] = x;
                 x = zeros_append(x, 16);
+            }
+        }
+    // the batch call's two-step payload shift: Z_{16 (7 - s)} and Z_{128 (7 - s)}
+    for (int n = 0; n < 8; ++n)
+        for (uint32_t v = 0; v < 16; ++v) {
+            uint32_t x = v << (4 * n), y = x;
+            for (int c = 7; c >= 0; --c) {
+                host_ls[n][v][c] = x;
+                host_gs[n][v][c] = y;
+                x = zeros_append(x, 16);
+                y = zeros_append(y, 128);
             }
         }
     for (int wf = 0; wf < 2; ++wf) {
@@ -1556,13 +1674,14 @@ int ensure_tables()
         }
     }
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg), host_seg, sizeof(host_seg));
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane_shift), host_lane_shift, sizeof(host_lane_shift));
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_segb), host_segb, sizeof(host_segb));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane16), host_lane16, sizeof(host_lane16));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_var), host_var, sizeof(host_var));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_z1024), host_z1024, sizeof(host_z1024));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg34), host_seg34, sizeof(host_seg34));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane_shift32), host_lane_shift32, sizeof(host_lane_shift32));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_ls), host_ls, sizeof(host_ls));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_gs), host_gs, sizeof(host_gs));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_tab), host_tab, sizeof(host_tab));
     if (e != hipSuccess) return (int)e;
     if (dev >= 0 && dev < 64) g_tables_ready[dev] = true;
     return 0;
@@ -1582,33 +1701,47 @@ int num_cus()
     return cus;
 }
 
-// persistent blocks per CU (43-46 KiB of LDS each, so up to three fit).  The
-// ICRC kernel is fastest at three (65.9 vs 78.4 us per 131 072 frames at two).
-// Egress was fastest at two while it staged every output frame in LDS (189 us
-// at three); with the payload stored from registers it takes three.
-// INCCL_ICRC_BLOCKS_PER_CU / INCCL_EGRESS_BLOCKS_PER_CU override for sweeps.
-int blocks_per_cu(const char* env, int dflt)
+// one wave per pair of frames, short-lived blocks
+template <bool kEmit, bool kOut16>
+int launch_apply(const ApplyArgs& a, hipStream_t st)
 {
-    const char* e = getenv(env);
-    const int v = e ? atoi(e) : 0;
-    return (v >= 1 && v <= 8) ? v : dflt;
+    const int64_t pairs = (a.count + 1) / 2, blocks = (pairs + kApplyWaves - 1) / kApplyWaves;
+    hipLaunchKernelGGL((k_ingress_apply<kEmit, kOut16>), dim3((unsigned)(blocks < 1 ? 1 : blocks)),
+                       dim3(kWave * kApplyWaves), 0, st, a);
+    return (int)hipGetLastError();
 }
 
-// waves per apply workgroup: 4 by default, $INCCL_APPLY_WPB = 1, 2, 8 or 16 for sweeps
-int apply_wpb()
+int check_batch_args(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count, const int32_t* ports,
+                     const int32_t* action, const uint32_t* psn_out)
 {
-    static const int v = [] {
-        const char* e = getenv("INCCL_APPLY_WPB");
-        const int x = e ? atoi(e) : kWavesPerBlock;
-        return (x == 1 || x == 2 || x == 4 || x == 8 || x == 16) ? x : kWavesPerBlock;
-    }();
-    return v;
+    if (!s || !frames || !ports || !action || !psn_out || (stride & 3) || stride < INCCL_FRAME_MIN_STRIDE ||
+        ((uintptr_t)frames & 3) || count >= 0x7FFFFFFFull || stride > (1u << 20))
+        return INCCL_ERR_ARG;
+    return 0;
 }
 
-inline int grid_for(int64_t waves)
+ApplyArgs apply_args(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count,
+                     const int32_t* ports, int32_t* action, const uint32_t* psn_out)
 {
-    const int64_t blocks = (waves + apply_wpb() - 1) / apply_wpb();
-    return (int)(blocks < 1 ? 1 : blocks);
+    ApplyArgs a{};
+    a.s = *s;
+    a.frames = frames;
+    a.stride = (int64_t)stride;
+    a.count = (int64_t)count;
+    a.ports = ports;
+    a.action = action;
+    a.psns = psn_out;
+    // 16-byte aligned rows: payloads as one dwordx4 per lane, loaded speculatively
+    a.wide = ((uintptr_t)frames & 15) == 0 && (stride & 15) == 0;
+    return a;
+}
+
+void launch_claim(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count, const int32_t* ports,
+                  int32_t* action, uint32_t* psn_out, const InccFrameTemplate* tmpl, hipStream_t st)
+{
+    const dim3 lanes((unsigned)(((int64_t)count + kClaimBlock - 1) / kClaimBlock));
+    hipLaunchKernelGGL(k_ingress_claim, lanes, dim3(kClaimBlock), 0, st, *s, frames, (int64_t)stride, (int64_t)count,
+                       ports, action, psn_out, tmpl);
 }
 
 }  // namespace
@@ -1621,87 +1754,20 @@ int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* o
 {
     if ((frames == nullptr || out == nullptr) && count) return INCCL_ERR_ARG;
     if (count == 0) return 0;
-    if ((stride & 3) || stride < INCCL_FRAME_MIN_STRIDE || ((uintptr_t)frames & 3)) return INCCL_ERR_ARG;
+    if ((stride & 3) || stride < INCCL_FRAME_MIN_STRIDE || stride > (1u << 20) || ((uintptr_t)frames & 3))
+        return INCCL_ERR_ARG;
     int rc = ensure_tables();
     if (rc) return rc;
-    static const bool byte_tables = [] {
-        const char* e = getenv("INCCL_ICRC_BYTE_TABLES");
-        return e && atoi(e) != 0;
-    }();
-    // 16-wave blocks share one copy of the tables: two per CU hold 32 waves (the
-    // most a CU runs), where 8-wave blocks fit three (24 waves) in the LDS;
-    // $INCCL_ICRC_WAVES=8 selects the 8-wave form (A/B)
-    static const int waves = [] {
-        const char* e = getenv("INCCL_ICRC_WAVES");
-        return e && atoi(e) == 8 ? 8 : 16;
-    }();
-    const int64_t blocks = ((int64_t)count + waves - 1) / waves;
-    // persistent: tables loaded once per block
-    const int64_t cap =
-        (int64_t)num_cus() * blocks_per_cu("INCCL_ICRC_BLOCKS_PER_CU", waves == 16 ? 2 : (byte_tables ? 2 : 3));
-    const int grid = (int)(blocks < cap ? blocks : cap);
     hipStream_t st = (hipStream_t)stream;
-    // two frames per wave (k_icrc_pair, 49.0 vs 52.8-54.9 us per 131 072 frames);
-    // $INCCL_ICRC_PAIR=0 selects one frame per wave (A/B)
-    static const bool pair = [] {
-        const char* e = getenv("INCCL_ICRC_PAIR");
-        return !(e && atoi(e) == 0);
-    }();
-    // two frames per wave without LDS staging (k_icrc_direct), the default: 47.9-49.8 vs
-    // 49.2-54.4 us for k_icrc_pair over this round's runs (profiles/r03/icrc_direct/);
-    // $INCCL_ICRC_DIRECT=0 selects k_icrc_pair, $INCCL_ICRC_PAIRS_PER_PASS=2 two pairs a
-    // pass (50.9-51.4 us: more bytes in flight do not help)
-    static const bool direct = [] {
-        const char* e = getenv("INCCL_ICRC_DIRECT");
-        return !(e && atoi(e) == 0);
-    }();
-    if (pair && direct && !byte_tables && count < (1ull << 29) && stride < (1ull << 29)) {   // 32-bit offsets
-        const int64_t pairs = ((int64_t)count + 1) / 2, need = (pairs + 7) / 8;
-        const int64_t pcap = (int64_t)num_cus() * blocks_per_cu("INCCL_ICRC_BLOCKS_PER_CU", 4);
-        static const int pp = [] {
-            const char* e = getenv("INCCL_ICRC_PAIRS_PER_PASS");
-            return e && atoi(e) == 2 ? 2 : 1;
-        }();
-        const int64_t groups = (pairs + pp - 1) / pp, gneed = (groups + 7) / 8;
-        // mask bytes and the zeroed leading bytes from one 32-entry (AND, OR) LDS table
-        // (2, the default): 43.6-47.0 vs 48.0-49.2 us for the 16-entry mask table with
-        // per-byte zeroing (1), itself 46.0-48.2 vs 47.0-50.8 us for the VALU spread (0),
-        // in paired runs (profiles/r03/icrc_mask_lds/, icrc_mask_zero/); $INCCL_ICRC_MASK_LDS
-        // selects 0 or 1 for A/B
-        static const int mask_lds = [] {
-            const char* e = getenv("INCCL_ICRC_MASK_LDS");
-            return e ? atoi(e) : 2;
-        }();
-        if (pp == 1 && mask_lds == 2)
-            hipLaunchKernelGGL((k_icrc_direct<8, 1, 2>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0,
-                               st, frames, (int64_t)stride, (int64_t)count, out);
-        else if (pp == 1 && mask_lds == 1)
-            hipLaunchKernelGGL((k_icrc_direct<8, 1, 1>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0,
-                               st, frames, (int64_t)stride, (int64_t)count, out);
-        else if (pp == 1)
-            hipLaunchKernelGGL((k_icrc_direct<8, 1>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0, st,
-                               frames, (int64_t)stride, (int64_t)count, out);
-        else
-            hipLaunchKernelGGL((k_icrc_direct<8, 2>), dim3((unsigned)(gneed < pcap ? gneed : pcap)), dim3(kWave * 8), 0,
-                               st, frames, (int64_t)stride, (int64_t)count, out);
-        return (int)hipGetLastError();
+    // 8-wave blocks, four per CU (20.7 KiB of tables each); the output buffer's
+    // byte size is a 32-bit field, so very large counts go in pieces
+    const int64_t piece = (int64_t)1 << 28, cap = (int64_t)num_cus() * 4;
+    for (int64_t f = 0; f < (int64_t)count; f += piece) {
+        const int64_t n = (int64_t)count - f < piece ? (int64_t)count - f : piece;
+        const int64_t need = ((n + 1) / 2 + 7) / 8;
+        hipLaunchKernelGGL(k_icrc<8>, dim3((unsigned)(need < cap ? need : cap)), dim3(kWave * 8), 0, st,
+                           frames + f * (int64_t)stride, (int64_t)stride, n, out + f);
     }
-    if (pair && !byte_tables) {
-        // 8-wave blocks: 2 x 1152 B of staging per wave + 20.6 KiB of tables = 39 KiB
-        const int64_t pairs = ((int64_t)count + 1) / 2, need = (pairs + 7) / 8;
-        const int64_t pcap = (int64_t)num_cus() * 4;   // four per CU: 32 waves
-        hipLaunchKernelGGL((k_icrc_pair<8>), dim3((unsigned)(need < pcap ? need : pcap)), dim3(kWave * 8), 0, st, frames,
-                           (int64_t)stride, (int64_t)count, out);
-        return (int)hipGetLastError();
-    }
-    if (byte_tables)
-        hipLaunchKernelGGL((k_icrc<true, 8>), dim3(grid), dim3(kWave * 8), 0, st, frames, (int64_t)stride, (int64_t)count, out);
-    else if (waves == 16)
-        hipLaunchKernelGGL((k_icrc<false, 16>), dim3(grid), dim3(kWave * 16), 0, st, frames, (int64_t)stride, (int64_t)count,
-                           out);
-    else
-        hipLaunchKernelGGL((k_icrc<false, 8>), dim3(grid), dim3(kWave * 8), 0, st, frames, (int64_t)stride, (int64_t)count,
-                           out);
     return (int)hipGetLastError();
 }
 
@@ -1709,45 +1775,36 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
                            const int32_t* ports, int32_t* action, uint32_t* psn_out, void* stream)
 {
     if (count == 0) return 0;
-    if (!s || !frames || !ports || !action || !psn_out || (stride & 3) || stride < INCCL_FRAME_MIN_STRIDE ||
-        ((uintptr_t)frames & 3) || count >= 0x7FFFFFFFull)
-        return INCCL_ERR_ARG;
+    if (check_batch_args(s, frames, stride, count, ports, action, psn_out)) return INCCL_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
-    const dim3 lanes((unsigned)(((int64_t)count + kClaimBlock - 1) / kClaimBlock));
-    hipLaunchKernelGGL(k_ingress_claim, lanes, dim3(kClaimBlock), 0, st, *s, frames, (int64_t)stride, (int64_t)count,
-                       ports, action, psn_out);
-    // 16-byte aligned rows: apply loads each payload with one dwordx4 per lane
-    const bool wide = ((uintptr_t)frames & 15) == 0 && (stride & 15) == 0;
-    static const int apply_frames = [] {
-        const char* e = getenv("INCCL_APPLY_FRAMES");
-        const int v = e ? atoi(e) : 2;
-        return (v == 1 || v == 4 || v == 8) ? v : 2;
-    }();
-    // $INCCL_APPLY_NT=0: plain aggregate stores (A/B of the non-temporal default)
-    static const bool apply_nt = [] {
-        const char* e = getenv("INCCL_APPLY_NT");
-        return !(e && atoi(e) == 0);
-    }();
-    const int64_t waves = ((int64_t)count + apply_frames - 1) / apply_frames;
-    if (apply_frames == 1)
-        hipLaunchKernelGGL(k_ingress_apply<1>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
-                           (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
-    else if (apply_frames == 4)
-        hipLaunchKernelGGL(k_ingress_apply<4>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
-                           (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
-    else if (apply_frames == 2 && !apply_nt)
-        hipLaunchKernelGGL((k_ingress_apply<2, false>), dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s,
-                           frames, (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
-    else if (apply_frames == 2)
-        hipLaunchKernelGGL(k_ingress_apply<2>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
-                           (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
-    else if (apply_frames == 8)
-        hipLaunchKernelGGL(k_ingress_apply<8>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
-                           (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
-    else
-        hipLaunchKernelGGL(k_ingress_apply<2>, dim3(grid_for(waves)), dim3(kWave * apply_wpb()), 0, st, *s, frames,
-                           (int64_t)stride, (int64_t)count, ports, action, psn_out, wide);
-    hipLaunchKernelGGL(k_ingress_commit, lanes, dim3(kClaimBlock), 0, st, *s, (int64_t)count, ports, action, psn_out);
+    launch_claim(s, frames, stride, count, ports, action, psn_out, nullptr, st);
+    return launch_apply<false, true>(apply_args(s, frames, stride, count, ports, action, psn_out), st);
+}
+
+int inccl_k_switch_batch(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count,
+                         const int32_t* ports, int32_t* action, uint32_t* psn_out, const InccFrameTemplate* tmpl,
+                         uint8_t* out, size_t out_stride, int32_t* out_len, void* stream)
+{
+    if (count == 0) return 0;
+    if (check_batch_args(s, frames, stride, count, ports, action, psn_out) || !tmpl || !out || !out_len ||
+        (out_stride & 3) || out_stride < 1100 || out_stride > (1u << 20) || ((uintptr_t)out & 3))
+        return INCCL_ERR_ARG;
+    int rc = ensure_tables();
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    launch_claim(s, frames, stride, count, ports, action, psn_out, tmpl, st);
+    ApplyArgs a = apply_args(s, frames, stride, count, ports, action, psn_out);
+    a.out = out;
+    a.out_stride = (int64_t)out_stride;
+    a.out_len = out_len;
+    const bool o16 = ((out_stride & 15) == 0) && (((uintptr_t)out & 15) == 0);
+    rc = o16 ? launch_apply<true, true>(a, st) : launch_apply<true, false>(a, st);
+    if (rc) return rc;
+    const int64_t need = ((int64_t)count + kWave * kEgressWaves - 1) / (kWave * kEgressWaves);
+    const int64_t cap = num_cus();
+    hipLaunchKernelGGL(k_replay, dim3((unsigned)(need < cap ? need : cap)), dim3(kWave * kEgressWaves), 0, st, *s, frames,
+                       (int64_t)stride, (int64_t)count, ports, (const int32_t*)action, (const uint32_t*)psn_out, tmpl, out,
+                       (int64_t)out_stride, out_len);
     return (int)hipGetLastError();
 }
 
@@ -1763,50 +1820,33 @@ int inccl_k_switch_egress(const InccSwitchState* s, const uint8_t* in_frames, si
     int rc = ensure_tables();
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    // persistent grid: the CRC tables are loaded once per block
+    // persistent grid (the CRC tables are loaded once per block), three 8-wave
+    // blocks per CU: 24 waves, the measured optimum (profiles/r03/egress_waves/)
     const int64_t need = ((int64_t)count + kEgressWaves - 1) / kEgressWaves;
-    const int64_t cap = (int64_t)num_cus() * blocks_per_cu("INCCL_EGRESS_BLOCKS_PER_CU", 3);
+    const int64_t cap = (int64_t)num_cus() * 3;
     const int eg = (int)(need < cap ? (need < 1 ? 1 : need) : cap);
-    // fan-in 2, 3, 4, 8: the straight-line kernel (k_egress_fixed); others, or
-    // $INCCL_EGRESS_GENERIC=1 (A/B), the generic one
-    static const bool generic = [] {
-        const char* e = getenv("INCCL_EGRESS_GENERIC");
-        return e && atoi(e) != 0;
-    }();
     const bool o16 = ((out_stride & 15) == 0) && (((uintptr_t)out & 15) == 0);
-    // non-temporal output stores (the frames are not re-read here): egress 65.3 vs
-    // 71.0 us (sc1 70.2-70.4, sc1|nt 67.6-68.0), and the next batch's apply 55.5 vs
-    // 65.2 us, no longer behind 144 MB of dirty lines (profiles/r03/store_policy/);
-    // $INCCL_EGRESS_NT=0 for A/B
-    static const bool nt = [] {
-        const char* e = getenv("INCCL_EGRESS_NT");
-        return !(e && atoi(e) == 0);
-    }();
+    // non-temporal frame stores (the frames are not re-read here): egress 65.3 vs
+    // 71.0 us, and the next batch's apply no longer starts behind 144 MB of dirty
+    // lines (profiles/r03/store_policy/)
     const dim3 g(eg), b(kWave * kEgressWaves);
     const int64_t is = (int64_t)in_stride, os = (int64_t)out_stride, n = (int64_t)count;
 #define INCCL_EGRESS_FIXED(F)                                                                                   \
     case F:                                                                                                     \
-        if (o16 && nt)                                                                                          \
+        if (o16)                                                                                                \
             hipLaunchKernelGGL((k_egress_fixed<F, true, kAuxNt>), g, b, 0, st, *s, in_frames, is, n, ports,     \
                                action, psns, tmpl, out, os, out_len);                                           \
-        else if (o16)                                                                                           \
-            hipLaunchKernelGGL((k_egress_fixed<F, true>), g, b, 0, st, *s, in_frames, is, n, ports, action,    \
-                               psns, tmpl, out, os, out_len);                                                   \
-        else if (nt)                                                                                            \
+        else                                                                                                    \
             hipLaunchKernelGGL((k_egress_fixed<F, false, kAuxNt>), g, b, 0, st, *s, in_frames, is, n, ports,    \
                                action, psns, tmpl, out, os, out_len);                                           \
-        else                                                                                                    \
-            hipLaunchKernelGGL((k_egress_fixed<F, false>), g, b, 0, st, *s, in_frames, is, n, ports, action,   \
-                               psns, tmpl, out, os, out_len);                                                   \
         return (int)hipGetLastError();
-    if (!generic) {
-        switch (s->fan_in) {
-            INCCL_EGRESS_FIXED(2)
-            INCCL_EGRESS_FIXED(3)
-            INCCL_EGRESS_FIXED(4)
-            INCCL_EGRESS_FIXED(8)
-        default: break;
-        }
+    // fan-in 2, 3, 4, 8: the straight-line kernel; others the generic one
+    switch (s->fan_in) {
+        INCCL_EGRESS_FIXED(2)
+        INCCL_EGRESS_FIXED(3)
+        INCCL_EGRESS_FIXED(4)
+        INCCL_EGRESS_FIXED(8)
+    default: break;
     }
 #undef INCCL_EGRESS_FIXED
     hipLaunchKernelGGL(k_egress, g, b, 0, st, *s, in_frames, is, n, ports, action, psns, tmpl, out, os, out_len);

@@ -5,7 +5,8 @@
  * CPU thread (nts.c:508-530).  Here the state lives in HBM and frames are
  * processed in batches: ingress launches (parse + idempotent add + the recycle,
  * clear_state_data(psn + window), nts.c:303-483, :235-242, :367) and one egress
- * launch (frame build + ICRC, util.c:331-442).  No host state changes per batch,
+ * launch (frame build + ICRC, util.c:331-442) -- or one batch call whose apply
+ * kernel builds the broadcast frames itself (inccl_switch_batch).  No host state changes per batch,
  * so a batch's launches can be captured in a hipGraph and replayed.  A batch must span
  * fewer than slots/2 PSNs -- the reference's window of 8 packets over 16 slots
  * (nts.c:21-22) has the same ratio. */
@@ -44,13 +45,14 @@ struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device)
     struct inccl_switch *sw = (struct inccl_switch *)calloc(1, sizeof(*sw));
     if (!sw) return NULL;
     const size_t agg = (size_t)slots * 256 * sizeof(int32_t);
-    const size_t arr = (size_t)slots * sizeof(uint32_t);
+    const size_t arr = (size_t)slots * 2 * sizeof(uint64_t);
     const size_t deg = (size_t)slots * sizeof(int32_t);
     const size_t reth = (size_t)slots * (size_t)fan_in * 16;
     const size_t first = (size_t)slots * (size_t)fan_in * 8;
-    const size_t gen = 8;   /* the batch-generation word (zeroed with the state) */
-    sw->bytes = agg + arr + deg + reth + gen + first;
-    sw->first_off = agg + arr + deg + reth + gen;
+    const size_t gen = 16;   /* the batch-generation words (zeroed with the state) */
+    const size_t hdr = 62 * 84;   /* the batch call's header images and ICRC terms */
+    sw->first_off = (agg + arr + deg + reth + gen + hdr + 7) & ~(size_t)7;
+    sw->bytes = sw->first_off + first;
     hipError_t e = hipMalloc(&sw->mem, sw->bytes);
     if (e == hipSuccess) e = hipMemset(sw->mem, 0, sw->first_off);
     if (e == hipSuccess) e = hipMemset((char *)sw->mem + sw->first_off, 0xFF, first);   /* no batch yet */
@@ -62,10 +64,11 @@ struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device)
     }
     char *p = (char *)sw->mem;
     sw->st.agg = (int32_t *)p;
-    sw->st.arrival = (uint32_t *)(p + agg);
+    sw->st.arrival = (uint64_t *)(p + agg);
     sw->st.degree = (int32_t *)(p + agg + arr);
     sw->st.reth = (uint32_t *)(p + agg + arr + deg);
     sw->st.gen = (uint32_t *)(p + agg + arr + deg + reth);
+    sw->st.hdr = (uint32_t *)(p + agg + arr + deg + reth + gen);
     sw->st.first = (uint64_t *)(p + sw->first_off);
     sw->st.slots = slots;
     sw->st.fan_in = fan_in;
@@ -114,6 +117,19 @@ int inccl_switch_ingress(struct inccl_switch *sw, const uint8_t *frames_dev, siz
      * sequence, like the reference's globals) */
     return kerr2(inccl_k_switch_ingress(&sw->st, frames_dev, stride, count, ports_dev, action_dev, psn_dev, stream),
                  "inccl_switch_ingress");
+}
+
+int inccl_switch_batch(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
+                       const int32_t *ports_dev, int32_t *action_dev, uint32_t *psn_dev,
+                       const struct inccl_frame_template *templates_dev, uint8_t *out_dev, size_t out_stride,
+                       int32_t *out_len_dev, void *stream)
+{
+    if (!sw) return inccl_set_error(INCCL_ERR_ARG, "switch is NULL");
+    if (count && stride < INCCL_FRAME_MIN_STRIDE)
+        return inccl_set_error(INCCL_ERR_ARG, "inccl_switch_batch: stride %zu below %d", stride, INCCL_FRAME_MIN_STRIDE);
+    return kerr2(inccl_k_switch_batch(&sw->st, frames_dev, stride, count, ports_dev, action_dev, psn_dev,
+                                      templates_dev, out_dev, out_stride, out_len_dev, stream),
+                 "inccl_switch_batch");
 }
 
 int inccl_switch_egress(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,

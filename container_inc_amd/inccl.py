@@ -470,6 +470,38 @@ class GpuSwitch:
                                           _stream_handle(stream)), "inccl_switch_ingress")
         return action, psn
 
+    def _out_args(self, frames, count, templates, out_stride, out, out_len):
+        torch = _torch()
+        if templates.dtype != torch.uint8 or templates.numel() != 28 * self.fan_in:
+            raise ValueError("templates: fan_in x 28-byte inccl_frame_template records (uint8)")
+        if out is None:
+            out = torch.empty((count * self.fan_in, out_stride), dtype=torch.uint8, device=frames.device)
+        elif out.dtype != torch.uint8 or out.dim() != 2 or out.shape[0] < count * self.fan_in:
+            raise ValueError("out: uint8 [count * fan_in, out_stride]")
+        if out_len is None:
+            out_len = torch.empty(count * self.fan_in, dtype=torch.int32, device=frames.device)
+        _dev_ptr(out, torch.uint8, "out")
+        _dev_ptr(out_len, torch.int32, "out_len", count * self.fan_in)
+        return out, out_len
+
+    def batch(self, frames, ports, templates, out_stride: int = 1152, stream=None, out=None, out_len=None,
+              action=None, psn=None):
+        """ingress + egress of one batch in one call (inccl_switch_batch): the
+        same actions, PSNs, rows and lengths as ingress() then egress()."""
+        torch = _torch()
+        ptr, count, stride = _frames_arg(frames)
+        pp = _dev_ptr(ports, torch.int32, "ports", count)
+        out, out_len = self._out_args(frames, count, templates, out_stride, out, out_len)
+        if action is None:
+            action = torch.empty(count, dtype=torch.int32, device=frames.device)
+        if psn is None:
+            psn = torch.empty(count, dtype=torch.int32, device=frames.device)
+        check(load().inccl_switch_batch(self.handle, ptr, stride, count, pp, _dev_ptr(action, torch.int32, "action", count),
+                                        _dev_ptr(psn, torch.int32, "psn", count),
+                                        _dev_ptr(templates, torch.uint8, "templates"), out.data_ptr(), out.shape[1],
+                                        out_len.data_ptr(), _stream_handle(stream)), "inccl_switch_batch")
+        return action, psn, out, out_len
+
     def egress(self, frames, ports, action, psn, templates, out_stride: int = 1152, stream=None, out=None,
                out_len=None):
         """Row i * fan_in + c is child c's frame for input frame i; out_len says
@@ -477,17 +509,8 @@ class GpuSwitch:
         buffer held: `out` / `out_len` may be passed in and reused."""
         torch = _torch()
         ptr, count, stride = _frames_arg(frames)
-        if templates.dtype != torch.uint8 or templates.numel() != 28 * self.fan_in:
-            raise ValueError("templates: fan_in x 28-byte inccl_frame_template records (uint8)")
-        if out is None:
-            out = torch.empty((count * self.fan_in, out_stride), dtype=torch.uint8, device=frames.device)
-        elif out.dtype != torch.uint8 or out.dim() != 2 or out.shape[0] < count * self.fan_in:
-            raise ValueError("out: uint8 [count * fan_in, out_stride]")
+        out, out_len = self._out_args(frames, count, templates, out_stride, out, out_len)
         out_stride = out.shape[1]
-        if out_len is None:
-            out_len = torch.empty(count * self.fan_in, dtype=torch.int32, device=frames.device)
-        _dev_ptr(out, torch.uint8, "out")
-        _dev_ptr(out_len, torch.int32, "out_len", count * self.fan_in)
         check(load().inccl_switch_egress(self.handle, ptr, stride, count, _dev_ptr(ports, torch.int32, "ports", count),
                                          _dev_ptr(action, torch.int32, "action", count),
                                          _dev_ptr(psn, torch.int32, "psn", count),

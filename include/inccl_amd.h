@@ -240,8 +240,8 @@ int inccl_allreduce_f32_host(struct inccl_communicator *comm, const float *src_h
 /* ---------- the reference switch's dataplane on the GPU ----------
  * non_termination_switch.c:303-501 (parse, per-PSN first-arrival aggregation,
  * broadcast / replay) and util.c:331-442 (egress frame build, payload htonl,
- * RoCE ICRC), batched: a batch of ingress frames -> one ingress launch -> one
- * egress launch.  Frames live in device memory at a fixed `stride` (multiple of
+ * RoCE ICRC), batched: a batch of ingress frames -> ingress (claim + apply) ->
+ * egress, or one inccl_switch_batch call.  Frames live in device memory at a fixed `stride` (multiple of
  * 4 B, at least 64; every read stays inside a frame's row).  Frame order within
  * a batch is the arrival order: the actions are exactly those of the reference
  * processing the batch's frames one at a time (the first copy of a (psn, port)
@@ -288,6 +288,15 @@ int inccl_switch_egress(struct inccl_switch *sw, const uint8_t *frames_dev, size
                         const int32_t *ports_dev, const int32_t *action_dev, const uint32_t *psn_dev,
                         const struct inccl_frame_template *templates_dev, uint8_t *out_dev, size_t out_stride,
                         int32_t *out_len_dev, void *stream);
+/* inccl_switch_ingress followed by inccl_switch_egress of the same batch, in
+ * one call (the reference's pipeline() runs both per frame): the same actions,
+ * state, out rows and lengths, but the aggregating kernel builds every
+ * COMPLETED frame's broadcast straight from the aggregate in its registers
+ * (the aggregate is not read back), and only REPLAY resends take a second pass. */
+int inccl_switch_batch(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
+                       const int32_t *ports_dev, int32_t *action_dev, uint32_t *psn_dev,
+                       const struct inccl_frame_template *templates_dev, uint8_t *out_dev, size_t out_stride,
+                       int32_t *out_len_dev, void *stream);
 /* RoCE ICRC (util.c:250-286) of `count` frames: icrc_dev[i] as the frame would store it (host order). */
 int inccl_icrc_frames(const uint8_t *frames_dev, size_t stride, size_t count, uint32_t *icrc_dev, void *stream);
 

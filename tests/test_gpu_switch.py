@@ -1,7 +1,10 @@
 """The reference switch's dataplane on the GPU vs the oracle (gpu): RoCE ICRC
 (util.c:250-286) against the captured frame of test.c and oracle-built frames;
 batched ingress (non_termination_switch.c:303-483: first-arrival add,
-retransmit drop / replay) and egress frames (util.c:331-442) byte-exact."""
+retransmit drop / replay) and egress frames (util.c:331-442) byte-exact.  Every
+batch test runs both ways of driving the switch: `split` (inccl_switch_ingress
+then inccl_switch_egress) and `batch` (inccl_switch_batch: the aggregating
+kernel emits the broadcasts itself, REPLAYs in a second pass)."""
 import json
 import os
 
@@ -83,6 +86,19 @@ def test_icrc_row_strides_odd_counts(gpu, orc, stride, count):
         assert int(c) == orc.icrc(f), len(f)
 
 
+MODES = ["split", "batch"]
+
+
+def _run(sw, mode, fr, pt, tmpl_dev, out_stride=STRIDE, stream=None, out=None, out_len=None):
+    """One batch through the switch either way: (action, psn, out, out_len)."""
+    if mode == "batch":
+        return sw.batch(fr, pt, tmpl_dev, out_stride=out_stride, stream=stream, out=out, out_len=out_len)
+    action, psn = sw.ingress(fr, pt, stream=stream)
+    out, out_len = sw.egress(fr, pt, action, psn, tmpl_dev, out_stride=out_stride, stream=stream, out=out,
+                             out_len=out_len)
+    return action, psn, out, out_len
+
+
 def _templates(fan_in):
     from container_inc_amd.inccl import FRAME_TEMPLATE_DTYPE
     t = np.zeros(fan_in, FRAME_TEMPLATE_DTYPE)
@@ -109,9 +125,10 @@ def _expected_frame(orc, t, c, agg, psn, op, reth):
 # Stride 1100 (4-byte but not 16-byte aligned rows): ingress's 2-byte payload
 # loads and egress's dword stores instead of the 16-byte paths.
 # Fan-in 2, 3, 4 and 8 take the straight-line egress (k_egress_fixed), others the generic one.
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("fan_in,stride", [(1, STRIDE), (2, STRIDE), (3, STRIDE), (4, STRIDE), (8, STRIDE), (20, STRIDE),
                                            (31, STRIDE), (2, 1100), (4, 1100), (8, 1100), (5, 1100)])
-def test_switch_batches(gpu, orc, fan_in, stride):
+def test_switch_batches(gpu, orc, fan_in, stride, mode):
     import torch
     from container_inc_amd import inccl
     rng = np.random.default_rng(100 + fan_in)
@@ -145,8 +162,7 @@ def test_switch_batches(gpu, orc, fan_in, stride):
             ports.append(port)
         fr = _rows(frames, gpu, stride)
         pt = torch.tensor(ports, dtype=torch.int32, device=gpu)
-        action, psn_out = sw.ingress(fr, pt)
-        out, out_len = sw.egress(fr, pt, action, psn_out, tmpl_dev, out_stride=stride)
+        action, psn_out, out, out_len = _run(sw, mode, fr, pt, tmpl_dev, out_stride=stride)
         torch.cuda.synchronize()
         action, psn_out = action.cpu().numpy(), psn_out.cpu().numpy()
         out, out_len = out.cpu().numpy(), out_len.cpu().numpy()
@@ -199,8 +215,9 @@ def test_switch_rejects_bad_frames(gpu, orc):
 # the per-round rotation of each wave's frame offset wrapping.  Every emitted
 # row is checked (length, payload = htonl of the wrap-around sum, ICRC), and a
 # sample of rows including the batch's last ones byte-exact against the oracle.
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("fan_in,P", [(2, 40000), (3, 21111), (4, 9999)])
-def test_switch_large_batch_all_frames(gpu, orc, fan_in, P):
+def test_switch_large_batch_all_frames(gpu, orc, fan_in, P, mode):
     import torch
     from container_inc_amd import inccl
     rng = np.random.default_rng(300 + fan_in)
@@ -229,8 +246,7 @@ def test_switch_large_batch_all_frames(gpu, orc, fan_in, P):
     tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
     fr = torch.from_numpy(frames).to(gpu)
     pt = torch.from_numpy(port).to(gpu)
-    action, psn_out = sw.ingress(fr, pt)
-    out, out_len = sw.egress(fr, pt, action, psn_out, tmpl_dev)
+    action, psn_out, out, out_len = _run(sw, mode, fr, pt, tmpl_dev)
     torch.cuda.synchronize()
     act = action.cpu().numpy()
     assert np.array_equal(psn_out.cpu().numpy(), psn)
@@ -271,8 +287,9 @@ def test_switch_large_batch_all_frames(gpu, orc, fan_in, P):
     sw.destroy()
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("fan_in,seed", [(2, 1), (2, 2), (3, 3)])
-def test_switch_serial_order_vs_oracle_reference_ring(gpu, orc, fan_in, seed):
+def test_switch_serial_order_vs_oracle_reference_ring(gpu, orc, fan_in, seed, mode):
     """The reference's own ring (16 slots, window 8 with slot psn+8 cleared at
     completion, nts.c:21-25, :367) fed one frame sequence: the oracle processes
     it serially (orc_switch_ingress), the GPU in batches of at most eight
@@ -317,8 +334,7 @@ def test_switch_serial_order_vs_oracle_reference_ring(gpu, orc, fan_in, seed):
                 counted_reth[(p, c)] = rb
         fr = _rows(frames, gpu, stride)
         pt = torch.tensor(ports, dtype=torch.int32, device=gpu)
-        action, psn_out = sw.ingress(fr, pt)
-        out, out_len = sw.egress(fr, pt, action, psn_out, tmpl_dev, out_stride=stride)
+        action, psn_out, out, out_len = _run(sw, mode, fr, pt, tmpl_dev, out_stride=stride)
         torch.cuda.synchronize()
         act = action.cpu().numpy().tolist()
         assert act == rcs, (b, seq, act, rcs)
@@ -365,10 +381,12 @@ def test_switch_short_stride_rejected(gpu, orc):
     sw.destroy()
 
 
-def test_switch_batch_graph_replay(gpu, orc):
-    """One batch's launches (ingress: claim / apply / commit, then egress)
-    captured once in a hipGraph and replayed over new frame contents: the
-    batch generation is a device word the commit advances, so every replay is
+@pytest.mark.parametrize("mode", MODES)
+def test_switch_batch_graph_replay(gpu, orc, mode):
+    """One batch's launches (ingress: claim / apply, then egress; or the batch
+    call's claim / apply / replay) captured once in a hipGraph and replayed over
+    new frame contents: the batch generation is a device word the last apply
+    block advances, so every replay is
     a new batch (first-copy keys of the previous replay never count).  Batches
     alternate between the two halves of the PSN ring (each recycles the other's
     slots, nts.c:367); every replay's actions, payload sums and ICRCs are
@@ -430,14 +448,12 @@ def test_switch_batch_graph_replay(gpu, orc):
     psn, op_of, pay, frames = batch(0)
     fr.copy_(torch.from_numpy(frames))
     torch.cuda.synchronize()
-    a, q = sw.ingress(fr, pt, stream=st)
-    sw.egress(fr, pt, a, q, tmpl_dev, stream=st, out=out, out_len=out_len)
+    a, q, _, _ = _run(sw, mode, fr, pt, tmpl_dev, stream=st, out=out, out_len=out_len)
     torch.cuda.synchronize()
     check(psn, op_of, pay, a, q, out, out_len)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=st):
-        ga, gq = sw.ingress(fr, pt, stream=st)
-        sw.egress(fr, pt, ga, gq, tmpl_dev, stream=st, out=out, out_len=out_len)
+        ga, gq, _, _ = _run(sw, mode, fr, pt, tmpl_dev, stream=st, out=out, out_len=out_len)
     for b in range(1, 5):
         psn, op_of, pay, frames = batch(b)
         fr.copy_(torch.from_numpy(frames))
@@ -449,9 +465,105 @@ def test_switch_batch_graph_replay(gpu, orc):
     psn, op_of, pay, frames = batch(5)
     fr.copy_(torch.from_numpy(frames))
     torch.cuda.synchronize()
-    a, q = sw.ingress(fr, pt, stream=st)
-    sw.egress(fr, pt, a, q, tmpl_dev, stream=st, out=out, out_len=out_len)
+    a, q, _, _ = _run(sw, mode, fr, pt, tmpl_dev, stream=st, out=out, out_len=out_len)
     torch.cuda.synchronize()
     check(psn, op_of, pay, a, q, out, out_len)
     del g
+    sw.destroy()
+
+
+@pytest.mark.parametrize("fan_in", [2, 3])
+def test_switch_split_and_batch_agree(gpu, orc, fan_in):
+    """The two ways of driving the switch, fed the same frame sequence on two
+    switches: identical actions, PSNs, out rows (every emitted byte) and
+    lengths, batch after batch, with retransmits spread across waves (random
+    arrival order) and PSNs whose ports straddle batches."""
+    import torch
+    rng = np.random.default_rng(1300 + fan_in)
+    from container_inc_amd import inccl
+    slots = 64
+    sws = {m: inccl.GpuSwitch(fan_in, slots) for m in MODES}
+    tmpl_dev = torch.from_numpy(_templates(fan_in).view(np.uint8).copy()).to(gpu)
+    pending = []
+    for b in range(8):
+        keys = [(p, c) for p in range(4 * b, 4 * b + 6) for c in range(fan_in)]
+        keys = [k for k in keys if k not in pending]
+        carry = [keys[i] for i in rng.choice(len(keys), size=len(keys) // 3, replace=False)]   # arrive next batch
+        now = [k for k in keys if k not in carry] + pending
+        now += [now[i] for i in rng.choice(len(now), size=len(now) // 4, replace=False)]     # retransmits
+        now = [now[i] for i in rng.permutation(len(now))]
+        pending = carry
+        frames = []
+        for (p, c) in now:
+            op = [0x06, 0x07, 0x07, 0x08][p % 4]
+            pay = rng.integers(INT32_MIN, INT32_MAX, 256, dtype=np.int64, endpoint=True).astype(np.int32)
+            frames.append(orc.build_data_frame(pay, psn=p, opcode=op, qp=0x11, with_reth=op == 0x06,
+                                               reth=rng.integers(0, 256, 16, dtype=np.uint8).tobytes() if op == 0x06 else None))
+        fr = _rows(frames, gpu)
+        pt = torch.tensor([c for (_, c) in now], dtype=torch.int32, device=gpu)
+        res = {}
+        for m in MODES:
+            a, q, o, ln = _run(sws[m], m, fr, pt, tmpl_dev,
+                               out=torch.zeros((len(now) * fan_in, STRIDE), dtype=torch.uint8, device=gpu))
+            torch.cuda.synchronize()
+            res[m] = (a.cpu().numpy(), q.cpu().numpy(), o.cpu().numpy(), ln.cpu().numpy())
+        for x, y in zip(res["split"], res["batch"]):
+            assert np.array_equal(x, y), b
+        for p in sorted({p for (p, _) in now}):
+            assert np.array_equal(inccl_slot(sws["split"], p, gpu), inccl_slot(sws["batch"], p, gpu)), (b, p)
+    for sw in sws.values():
+        sw.destroy()
+
+
+def inccl_slot(sw, psn, dev):
+    """The aggregator words of `psn`'s slot (inccl_switch_slot), as uint32."""
+    import ctypes
+    import torch
+    from container_inc_amd._lib import load, runtime_libs
+    ptr = load().inccl_switch_slot(sw.handle, ctypes.c_uint32(psn))
+    buf = torch.empty(256, dtype=torch.int32, device=dev)
+    hip = ctypes.CDLL(runtime_libs()["libamdhip64"])   # the HIP runtime this process already runs on
+    torch.cuda.synchronize()
+    assert hip.hipMemcpy(ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(1024), 3) == 0
+    return buf.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_switch_slot_after_recycle(gpu, orc, mode):
+    """inccl_switch_slot's documented behaviour around a recycle (nts.c:235-242,
+    :367): while a PSN's slot holds arrivals its words are the wrap-around sum
+    so far; completing PSN p recycles slot p + slots/2, whose words are then
+    stale (the GPU does not zero them, unlike the reference's memset); the next
+    counted arrival into that slot sums from zero, not from the stale words."""
+    import torch
+    from container_inc_amd import inccl
+    fan_in, slots = 2, 16
+    sw = inccl.GpuSwitch(fan_in, slots)
+    tmpl_dev = torch.from_numpy(_templates(fan_in).view(np.uint8).copy()).to(gpu)
+    rng = np.random.default_rng(1400)
+
+    def frame(p, pay):
+        return orc.build_data_frame(pay, psn=p, opcode=0x07, qp=0x11)
+
+    def send(items):
+        fr = _rows([frame(p, pay) for (p, _, pay) in items], gpu)
+        pt = torch.tensor([c for (_, c, _) in items], dtype=torch.int32, device=gpu)
+        a, _, _, _ = _run(sw, mode, fr, pt, tmpl_dev)
+        torch.cuda.synchronize()
+        return a.cpu().numpy().tolist()
+
+    pay = {k: rng.integers(INT32_MIN, INT32_MAX, 256, dtype=np.int64, endpoint=True).astype(np.int32)
+           for k in [(9, 0), (9, 1), (1, 0), (1, 1), (25, 0), (25, 1)]}
+    # PSN 9 (slot 9) completes: its words are the sum
+    assert send([(9, 0, pay[(9, 0)]), (9, 1, pay[(9, 1)])]) == [inccl.SW_ABSORBED, inccl.SW_COMPLETED]
+    want9 = orc.sum_q32([pay[(9, 0)], pay[(9, 1)]]).view(np.uint32)
+    assert np.array_equal(inccl_slot(sw, 9, gpu), want9)
+    # PSN 1 completes and recycles slot 1 + 8 = 9: the words stay (stale)
+    assert send([(1, 0, pay[(1, 0)]), (1, 1, pay[(1, 1)])]) == [inccl.SW_ABSORBED, inccl.SW_COMPLETED]
+    assert np.array_equal(inccl_slot(sw, 9, gpu), want9)
+    # PSN 25 -> slot 9 again: its first counted arrival sums from zero
+    assert send([(25, 1, pay[(25, 1)])]) == [inccl.SW_ABSORBED]
+    assert np.array_equal(inccl_slot(sw, 25, gpu), pay[(25, 1)].view(np.uint32))
+    assert send([(25, 0, pay[(25, 0)])]) == [inccl.SW_COMPLETED]
+    assert np.array_equal(inccl_slot(sw, 25, gpu), orc.sum_q32([pay[(25, 0)], pay[(25, 1)]]).view(np.uint32))
     sw.destroy()

@@ -1,10 +1,11 @@
 #!/bin/bash
-# Round 3: counters of the tuned switch kernels (claim / apply / commit / egress /
-# ICRC): SQ issue and wait cycles, LDS bank conflicts, and HBM traffic (FETCH_SIZE,
-# WRITE_SIZE in their own passes; gfx950: double FETCH_SIZE for wide streaming reads).
+# Counters of the switch kernels over tools/switch_bench.py: SQ issue and wait
+# cycles, instruction mix, LDS bank conflicts, and HBM traffic (FETCH_SIZE and
+# WRITE_SIZE in passes of their own; gfx950: double FETCH_SIZE for wide
+# streaming reads).  Usage: gpu_pmc_switch.sh [tag]; writes gpurun_out/pmcsw<tag>/.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 3
-O=gpurun_out/r03pmcsw
+O=gpurun_out/pmcsw${1:-}
 mkdir -p $O
 export TMPDIR=/tmp
 run() {  # run <name> <counters...>
@@ -16,4 +17,5 @@ run pmc2 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_
 run pmc3 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD
 run pmc4 FETCH_SIZE
 run pmc5 WRITE_SIZE
-python3 tools/pmc_summary.py $O/pmc*/pmc_counter_collection.csv | grep -v rocclr
+python3 tools/pmc_summary.py $O/pmc*/pmc_counter_collection.csv | grep -v rocclr > $O/summary.txt
+cat $O/summary.txt

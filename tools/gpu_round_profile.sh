@@ -25,6 +25,6 @@ for k in fused quant_sum bf16; do
 done
 echo "pmc ok"
 if [ -z "$SKIP_REHEARSAL" ]; then
-  bash tools/gpu_rehearse_n2_sweep.sh || exit 8
+  bash tools/gpu_rehearse.sh 2 20 5 || exit 8
 fi
 echo done

@@ -5,7 +5,8 @@ Workload: fan_in children x P packets of 1 KiB payload (RoCEv2 frames of 1082 B,
 one WRITE_FIRST with RETH every 4th PSN), batches alternating over the two halves of the PSN ring: ingress (parse + serial-order
 idempotent add) -> egress (fan_in frames per PSN: build + htonl + ICRC) -> recycle.
 Reports payload GB/s = fan_in * P * 1024 / t (ingress payload bytes), frames/s,
-and the same for the ICRC kernel alone.  CPU leg: oracle orc_switch_ingress +
+for both ways of driving the switch (split: ingress + egress calls; batch: one
+inccl_switch_batch call), and the same for the ICRC kernel alone.  CPU leg: oracle orc_switch_ingress +
 orc_build_data_frame (the reference's per-packet loop, 1 core)."""
 import json
 import os
@@ -67,68 +68,75 @@ def main():
     out_len = torch.empty(fan_in * P * fan_in, dtype=torch.int32, device=dev)
     batch = [0]
 
-    def run():
+    def run(mode):
         x = fr if batch[0] % 2 == 0 else fr_b
         batch[0] += 1
+        if mode == "batch":
+            a, q, o, ln = sw.batch(x, pt, tmpl_dev, stream=st, out=out, out_len=out_len)
+            return a, o, ln
         a, q = sw.ingress(x, pt, stream=st)
         o, ln = sw.egress(x, pt, a, q, tmpl_dev, stream=st, out=out, out_len=out_len)
         return a, o, ln
 
-    a, o, ln = run()
-    torch.cuda.synchronize()
-    acts = a.cpu().numpy()
-    assert (acts == inccl.SW_COMPLETED).sum() == P, "every psn completes once"
-    # spot-check egress frames against the oracle
-    for f in rng.choice(len(acts), 8, replace=False):
-        if acts[f] != inccl.SW_COMPLETED:
-            continue
-        p = int(psn[f])
-        agg = O.sum_q32([pay[p * fan_in + c] for c in range(fan_in)])
-        op = 0x06 if p % 4 == 0 else (0x08 if p % 4 == 3 else 0x07)
-        want = O.build_data_frame(agg, psn=p, opcode=op, qp=0x11, with_reth=(op == 0x06), reth=bytes(16))
-        got = o[f * fan_in].cpu().numpy()[: len(want)].tobytes()
-        assert got == want, f"egress frame {f} differs from the oracle"
+    def check(mode):
+        a, o, ln = run(mode)
+        torch.cuda.synchronize()
+        acts = a.cpu().numpy()
+        assert (acts == inccl.SW_COMPLETED).sum() == P, f"{mode}: every psn completes once"
+        # spot-check egress frames against the oracle (this batch's PSNs are p or p + P)
+        base_psn = 0 if (batch[0] - 1) % 2 == 0 else P
+        for f in rng.choice(len(acts), 8, replace=False):
+            if acts[f] != inccl.SW_COMPLETED:
+                continue
+            p = int(psn[f])
+            agg = O.sum_q32([pay[p * fan_in + c] for c in range(fan_in)])
+            op = 0x06 if p % 4 == 0 else (0x08 if p % 4 == 3 else 0x07)
+            want = O.build_data_frame(agg, psn=p + base_psn, opcode=op, qp=0x11, with_reth=(op == 0x06), reth=bytes(16))
+            got = o[f * fan_in].cpu().numpy()[: len(want)].tobytes()
+            assert got == want, f"{mode}: egress frame {f} differs from the oracle"
+
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     iters = 10
-    run()   # batch B: recycles batch A's half
-    with torch.cuda.stream(st):
-        e0.record(st)
-        for _ in range(iters):
-            run()
-        e1.record(st)
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    a, o, ln = run()   # every PSN of every later batch still completes exactly once
-    torch.cuda.synchronize()
-    assert (a.cpu().numpy() == inccl.SW_COMPLETED).sum() == P
     payload_bytes = fan_in * P * 1024
-    print(json.dumps({"what": "GPU switch dataplane batch (ingress claim/apply+recycle/commit + egress; no reset)", "fan_in": fan_in,
-                      "psns": P, "ingress_frames": fan_in * P, "egress_frames": fan_in * P, "ms": round(ms, 4),
-                      "payload_GBs": round(payload_bytes / (ms * 1e-3) / 1e9, 2),
-                      "frames_per_s": round(2 * fan_in * P / (ms * 1e-3), 1)}), flush=True)
-    # the same batches captured in a hipGraph (two batches, one per half of the
-    # ring) and replayed: no launch gaps between the batch's kernels
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=st):
-        run()
-        run()
-    g.replay()
-    torch.cuda.synchronize()
-    reps = 5
-    with torch.cuda.stream(st):
-        e0.record(st)
-        for _ in range(reps):
-            g.replay()
-        e1.record(st)
-    torch.cuda.synchronize()
-    ms_g = e0.elapsed_time(e1) / (2 * reps)
-    a, o, ln = run()   # eager again after the replays: still one completion per PSN
-    torch.cuda.synchronize()
-    assert (a.cpu().numpy() == inccl.SW_COMPLETED).sum() == P
-    del g
-    print(json.dumps({"what": "GPU switch dataplane batch, hipGraph-replayed (claim / apply / commit / egress)",
-                      "fan_in": fan_in, "psns": P, "ms": round(ms_g, 4),
-                      "payload_GBs": round(payload_bytes / (ms_g * 1e-3) / 1e9, 2)}), flush=True)
+    for mode in ("split", "batch"):
+        check(mode)
+        run(mode)   # the other half of the ring
+        with torch.cuda.stream(st):
+            e0.record(st)
+            for _ in range(iters):
+                run(mode)
+            e1.record(st)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / iters
+        check(mode)   # every PSN of every later batch still completes exactly once
+        print(json.dumps({"what": "GPU switch dataplane batch, eager: " +
+                                  ("inccl_switch_ingress (claim / apply) + inccl_switch_egress" if mode == "split" else
+                                   "inccl_switch_batch (claim / apply + broadcast / replay pass)"),
+                          "mode": mode, "fan_in": fan_in, "psns": P, "ingress_frames": fan_in * P,
+                          "egress_frames": fan_in * P, "ms": round(ms, 4),
+                          "payload_GBs": round(payload_bytes / (ms * 1e-3) / 1e9, 2),
+                          "frames_per_s": round(2 * fan_in * P / (ms * 1e-3), 1)}), flush=True)
+        # the same batches captured in a hipGraph (two batches, one per half of
+        # the ring) and replayed: no launch gaps between the batch's kernels
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            run(mode)
+            run(mode)
+        g.replay()
+        torch.cuda.synchronize()
+        reps = 5
+        with torch.cuda.stream(st):
+            e0.record(st)
+            for _ in range(reps):
+                g.replay()
+            e1.record(st)
+        torch.cuda.synchronize()
+        ms_g = e0.elapsed_time(e1) / (2 * reps)
+        check(mode)   # eager again after the replays: still one completion per PSN
+        del g
+        print(json.dumps({"what": "GPU switch dataplane batch, hipGraph-replayed", "mode": mode,
+                          "fan_in": fan_in, "psns": P, "ms": round(ms_g, 4),
+                          "payload_GBs": round(payload_bytes / (ms_g * 1e-3) / 1e9, 2)}), flush=True)
     icrc_out = torch.empty(fan_in * P, dtype=torch.int32, device=dev)
     with torch.cuda.stream(st):
         inccl.icrc_frames(fr, stream=st)
