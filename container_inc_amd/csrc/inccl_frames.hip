@@ -952,7 +952,9 @@ __global__ __launch_bounds__(kWave * 8) void k_egress_fixed(INCCL_EGRESS_FIXED_A
 // and nothing changes on the host per batch, so a captured batch (hipGraph)
 // tags every replay anew.
 // ---------------------------------------------------------------------------
-constexpr int kActPending = 0x100;   // claim -> apply: a data frame still to classify, | its opcode
+// claim -> apply: a data frame still to classify: kActPending | WRITE_FIRST << 9 | opcode
+// (the final actions are all below 0x100)
+constexpr int kActPending = 0x100;
 constexpr int kClaimBlock = 256;
 
 // (~gen << 32) | (frame << 1) | wf: the minimum over a (slot, port)'s keys is the
@@ -1038,7 +1040,7 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
             atomicAdd(&s.degree[slot], 1);                       // nts.c:351 / :431
             atomicMin(reinterpret_cast<unsigned long long*>(&s.first[(size_t)slot * s.fan_in + port]),
                       (unsigned long long)first_key(g, f, wf));
-            act = kActPending | op;
+            act = kActPending | (wf ? 0x200 : 0) | op;
         }
     }
     action[f] = act;
@@ -1051,11 +1053,11 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
 // A wave's work on its pair is three dependent memory round trips at most, and
 // in the common case -- every port of a PSN arriving as consecutive frames,
 // the reference's hosts posting one message each (api.c:293-327) -- two:
-//   1. the claim results (action | opcode, port, PSN) and, on 16-byte aligned
-//      rows, both rows' payload chunks, loaded before anything is known about
-//      the frames (lane l the 16-byte chunk 3 + l of each row, lanes 0 and 1
-//      also chunks 67 and 68: the payload starts 6 bytes into chunk 3 or 4,
-//      whichever the opcode says, so both placements are covered);
+//   1. the claim results (action | WRITE_FIRST | opcode, port, PSN) and, on
+//      16-byte aligned rows, both rows' payload chunks, loaded before anything
+//      is known about the frames (lane l the 16-byte chunk 3 + l of each row,
+//      lanes 0 and 1 also chunks 67 and 68: the payload starts 6 bytes into
+//      chunk 3 or 4, whichever the opcode says, so both placements are covered);
 //   2. the slot state, lane-parallel: lanes 32 k + p hold frame k's port p
 //      (first-copy key), lanes 32 k and 32 k + 1 its two tagged arrival words;
 //      in the batch call also the RETH keeper;
@@ -1071,10 +1073,16 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
 // summed from zero without reading them and nothing else reads a slot before
 // its next counted arrival rewrites them), and in the batch call builds the
 // completed PSN's fan_in broadcast frames (nts.c:447-453, util.c:331-442) from
-// the aggregate in its registers.  Waves are short and not persistent: a wave
-// leaves once its stores are issued and the next starts, which hides the
-// latency a persistent loop would wait out before every next round trip (on
-// gfx9 loads and stores retire in order on one counter).
+// the aggregate in its registers.
+//
+// The split call's apply runs one pair per wave in short-lived blocks (a wave
+// leaves once its stores are issued and the next starts).  The batch call's
+// runs persistent blocks that load the egress tables (57 KiB) once; its waves
+// walk the pairs.  The counters (profiles/r04/) put these kernels' VALU issue
+// near the limit, so the code spends instructions sparingly: lane-rotation
+// addresses are computed once, the WRITE_FIRST flag travels in the claim
+// result, the payload CRC takes byte lookups, and the header chunks are the
+// template image ORed with one patch per PSN.
 //
 // Arrival bitmap: every frame classifies against the bitmap as it was before
 // the batch, while the summing wave writes the new one in the same launch.  A
@@ -1084,7 +1092,8 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
 // pre-batch bitmap (64-bit accesses are single-copy atomic).  The recycle
 // writes both words (no frame of the batch reads that slot).
 // ---------------------------------------------------------------------------
-constexpr int kApplyWaves = 8;
+constexpr int kApplyWaves = 8;    // split call: one pair per wave, 8-wave blocks
+constexpr int kEmitWaves = 16;    // batch call: persistent 16-wave blocks
 
 struct ApplyArgs {
     InccSwitchState s;
@@ -1126,144 +1135,164 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
 }
 
-// The batch call's egress tables in LDS.  The payload's ICRC contribution is
-// P = XOR over lanes of Z_{16 (63 - lane)}(crc of lane's 16 bytes); the shift
-// is taken in two steps, Z_{16 (7 - lane % 8)} then, once the 8 lanes of a
-// group are XORed, Z_{128 (7 - lane / 8)}: 8 KiB of tables where one step
-// would need 32 KiB, so that a short-lived block loads them cheaply.
-__device__ uint32_t g_ls[8][16][8];   // [nibble][value][lane % 8] = Z_{16 (7 - lane % 8)}(value << 4 nibble)
-__device__ uint32_t g_gs[8][16][8];   // [nibble][value][lane / 8] = Z_{128 (7 - lane / 8)}(value << 4 nibble)
+// lane l + 1's value (lane 63 gets lane 0's), through a precomputed address
+__device__ __forceinline__ uint32_t from_next(uint32_t v, int next4)
+{
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(next4, (int)v);
+}
+
+// The batch call's egress tables in LDS, once per persistent block.
+__device__ uint32_t g_segb[16][256];   // [byte j of a 16-byte segment][value] = Z_{15-j}(T[value])
 
 struct EmitLds {
-    uint32_t seg[16][2][16];          // segment byte j: Z_{15-j}(T[value << 4 nibble]) (g_seg rows 1-16)
-    uint32_t ls[8][16][8];
-    uint32_t gs[8][16][8];
+    uint32_t segb[16][256];
+    uint32_t lane16[8][16][kWave];
     uint32_t var[kVarRows][2][16];
     uint32_t hcrc[2 * 31];
     __attribute__((aligned(16))) uint8_t img[2 * 31][kHdrImg];
 };
-constexpr int kEmitFixedU4 = (sizeof(uint32_t) * (16 * 2 * 16 + 2 * 8 * 16 * 8 + kVarRows * 2 * 16)) / 16;
 
-template <bool kEmit>
-struct ApplyShared {};
-template <>
-struct ApplyShared<true> {
-    EmitLds t;
-};
-
-// t.ls / t.gs applied to c: 8 nibble lookups at column col
-__device__ __forceinline__ uint32_t shift8(const uint32_t (*tab)[16][8], uint32_t c, int col)
-{
-    const uint32_t lo = opaque_u32(c & 0x0F0F0F0Fu), hi = opaque_u32((c >> 4) & 0x0F0F0F0Fu);
-    uint32_t v[8];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        v[2 * b] = tab[2 * b][(uint8_t)(lo >> (8 * b))][col];
-        v[2 * b + 1] = tab[2 * b + 1][(uint8_t)(hi >> (8 * b))][col];
-    }
-    return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
-}
-
-// P for the aggregate whose bytes (big-endian, memory order) lane l holds in a[]
-__device__ __forceinline__ uint32_t payload_crc(const EmitLds& t, const uint32_t (&a)[4], int lane)
+// P ^ V_op,psn, in every lane: the payload's contribution to the ICRC (lane l's
+// 16 bytes a[] -- memory order, little-endian words -- as 16 byte lookups, then
+// shifted past the segments after it, Z_{16 (63 - l)}, as 8 nibble lookups)
+// plus the opcode and PSN bytes' (lanes 0-4, already shifted to the message
+// end), XORed over the wave.
+__device__ __forceinline__ uint32_t payload_term(const EmitLds& t, const uint32_t (&a)[4], uint32_t var, int lane)
 {
     uint32_t c = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t lo = opaque_u32(a[k] & 0x0F0F0F0Fu), hi = opaque_u32((a[k] >> 4) & 0x0F0F0F0Fu);
-        uint32_t v[8];
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t v0 = t.segb[4 * j][a[j] & 0xFFu], v1 = t.segb[4 * j + 1][(a[j] >> 8) & 0xFFu];
+        const uint32_t v2 = t.segb[4 * j + 2][(a[j] >> 16) & 0xFFu], v3 = t.segb[4 * j + 3][a[j] >> 24];
+        c = xor3(c, v0, v1) ^ xor3(v2, v3, 0u);
+        c = opaque_u32(c);   // four lookups in flight at a time: registers for the occupancy
+    }
+    const uint32_t clo = opaque_u32(c & 0x0F0F0F0Fu), chi = opaque_u32((c >> 4) & 0x0F0F0F0Fu);
+    uint32_t s[8];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            v[2 * b] = t.seg[4 * k + b][0][(uint8_t)(lo >> (8 * b))];
-            v[2 * b + 1] = t.seg[4 * k + b][1][(uint8_t)(hi >> (8 * b))];
-        }
-        c = xor3(xor3(xor3(c, v[0], v[1]), v[2], v[3]), xor3(v[4], v[5], v[6]), v[7]);
+    for (int b = 0; b < 4; ++b) {
+        s[2 * b] = t.lane16[2 * b][(uint8_t)(clo >> (8 * b))][lane];
+        s[2 * b + 1] = t.lane16[2 * b + 1][(uint8_t)(chi >> (8 * b))][lane];
     }
-    c = shift8(t.ls, c, lane & 7);
-    // XOR the group of 8: quads, then the half-row mirror
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x141, 0xF, 0xF, false);   // row_half_mirror
-    c = shift8(t.gs, c, lane >> 3);
-    // XOR the 8 groups: the row mirror pairs them, the row broadcasts end in lane 63
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x140, 0xF, 0xF, false);   // row_mirror
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x142, 0xA, 0xF, false);   // row_bcast15 -> rows 1, 3
-    c ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x143, 0xC, 0xF, false);   // row_bcast31 -> rows 2, 3
-    return (uint32_t)__builtin_amdgcn_readlane((int)c, 63);
+    return wave_xor(xor3(xor3(s[0], s[1], s[2]), xor3(s[3], s[4], s[5]), xor3(s[6], s[7], var)));
 }
 
-// Child c's frame of one aggregate into `row`: the header chunks (lanes below
-// hchunks) from the template image with the opcode (byte 42), the PSN (50-53),
-// the RETH R (54-69, util.c:409-417) and the payload's first 10 bytes (a0..a2
-// of lane 0) patched in; the payload chunks (pcs: output chunk hchunks + l)
-// from registers; the ICRC by linearity, ~(P ^ V_op,psn ^ H_c ^ V_reth) with
-// pc = P ^ V_op,psn (util.c:424-426).  Every lane stores: what it must not
-// write goes past the row (dropped).
-template <bool kOut16>
-__device__ __forceinline__ void emit_child(const EmitLds& t, int c, int wf, uint32_t op, uint32_t pw, uint32_t pc,
-                                           const uint32_t (&pcs)[4], uint32_t a0, uint32_t a1, uint32_t a2,
-                                           uint32_t a3, const uint32_t (&R)[4], uint8_t* row, int64_t out_stride,
-                                           int lane)
+// per-lane constants of a wave
+struct LaneK {
+    int lane, next4;   // lane, 4 * (lane + 1 mod 64): ds_bpermute address of the next lane
+};
+
+// What apply knows about one frame of its pair.
+struct FrameK {
+    int act, port;
+    uint32_t psn, slot, op, wf;
+    bool live;
+};
+
+// The batch call's broadcast of one completed PSN: fan_in frames into rows
+// fd * fan_in + c, from the aggregate acc (this lane's four words).
+template <bool kOut16, class RethOf>
+__device__ __forceinline__ void emit_broadcast(const ApplyArgs& A, const EmitLds& t, const LaneK& L, const u4& acc,
+                                               int64_t fd, uint32_t opd, uint32_t wfd, uint32_t psn, int fan,
+                                               RethOf reth_of)
 {
-    const int doff = 54 + 16 * wf;
-    const int hchunks = doff / 16 + 1;
-    uint32_t vr = 0;
-    if (wf) {
-        // lane k < 16: RETH byte k = byte k & 3 of word k >> 2
-        const uint32_t rk = (lane & 8) ? ((lane & 4) ? R[3] : R[2]) : ((lane & 4) ? R[1] : R[0]);
-        vr = wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
-    }
-    const uint32_t crc = ~(pc ^ t.hcrc[2 * c + wf] ^ vr);
-    const uint32_t psn_hi = (pw >> 24) | (((pw >> 16) & 0xFFu) << 8);    // frame bytes 50, 51 (util.c:386)
+    const int lane = L.lane;
+    uint32_t a[4];   // this lane's 16 payload bytes, big-endian (util.c:403-405), memory order
+    a[0] = __builtin_bswap32(acc.x);
+    a[1] = __builtin_bswap32(acc.y);
+    a[2] = __builtin_bswap32(acc.z);
+    a[3] = __builtin_bswap32(acc.w);
+    const uint32_t pw = psn | 0x80000000u;
+    // the opcode and PSN bytes' terms (util.c:378, :386), lanes 0-4
+    const uint32_t vb = lane == 0 ? opd : (pw >> (8 * (4 - lane))) & 0xFFu;
+    const uint32_t var = lane < 5 ? var_crc(t, (int)wfd, lane, vb) : 0u;
+    const uint32_t pc = payload_term(t, a, var, lane);
+    // payload chunk hchunks + l: bytes 10-15 of lane l, 0-9 of lane l + 1; the
+    // last one (lane 63): bytes 1018-1023, the ICRC (host order), zero padding
+    const uint32_t n0 = from_next(a[0], L.next4), n1 = from_next(a[1], L.next4), n2 = from_next(a[2], L.next4);
+    const bool last = lane == kWave - 1;
+    const uint32_t p0 = __builtin_amdgcn_alignbyte(a[3], a[2], 2);
+    const uint32_t p1 = __builtin_amdgcn_alignbyte(n0, a[3], 2);
+    const uint32_t p2 = __builtin_amdgcn_alignbyte(n1, n0, 2);
+    const uint32_t p3 = last ? 0u : __builtin_amdgcn_alignbyte(n2, n1, 2);
+    const uint32_t t63 = a[3] >> 16;
+    // the header chunks' PSN-wide patch over the template images (which hold
+    // zeros there): opcode (byte 42), PSN (50-53), and the payload's first 10
+    // bytes after the BTH (no RETH) or after the RETH (lane 4's chunk)
+    const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)a[0], 0);
+    const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)a[1], 0);
+    const uint32_t a2 = (uint32_t)__builtin_amdgcn_readlane((int)a[2], 0);
+    const uint32_t psn_hi = (pw >> 24) | (((pw >> 16) & 0xFFu) << 8);    // frame bytes 50, 51
     const uint32_t psn_lo = ((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8);   // bytes 52, 53
-    const u4 img = reinterpret_cast<const u4*>(t.img[2 * c + wf])[lane < 5 ? lane : 0];
-    uint32_t h0 = img.x, h1 = img.y, h2 = img.z, h3 = img.w;
-    if (lane == 2) h2 = (h2 & 0xFF00FFFFu) | (op << 16);
-    if (lane == 3) {
-        const uint32_t b0 = wf ? R[0] : a0, b1 = wf ? R[1] : a1, b2 = wf ? R[2] : a2;   // bytes 54-63
-        h0 = (h0 & 0xFFFFu) | (psn_hi << 16);
-        h1 = psn_lo | (b0 << 16);
-        h2 = __builtin_amdgcn_alignbyte(b1, b0, 2);
-        h3 = __builtin_amdgcn_alignbyte(b2, b1, 2);
-    }
-    if (lane == 4) {                                                    // RETH frames only: bytes 64-79
-        h0 = __builtin_amdgcn_alignbyte(R[3], R[2], 2);
-        h1 = (R[3] >> 16) | (a0 << 16);
-        h2 = __builtin_amdgcn_alignbyte(a1, a0, 2);
-        h3 = __builtin_amdgcn_alignbyte(a2, a1, 2);
-    }
-    const u4 h = {h0, h1, h2, h3};
-    const __amdgpu_buffer_rsrc_t orow = uniform_rsrc(row, out_stride);
-    // the last chunk (lane 63): payload bytes 1018-1023, the ICRC stored host
-    // order (LE), two bytes of zero padding
-    const u4 v = lane < kWave - 1 ? u4{pcs[0], pcs[1], pcs[2], pcs[3]}
-                                  : u4{pcs[0], (a3 >> 16) | ((crc & 0xFFFFu) << 16), crc >> 16, 0u};
+    const uint32_t q1 = a0 << 16, q2 = __builtin_amdgcn_alignbyte(a1, a0, 2), q3 = __builtin_amdgcn_alignbyte(a2, a1, 2);
+    const int pl = wfd ? 4 : 3;   // the lane whose chunk ends with the payload's first 10 bytes
+    u4 patch;
+    patch.x = lane == 3 ? psn_hi << 16 : 0u;
+    patch.y = lane == 3 ? psn_lo : 0u;
+    patch.y |= lane == pl ? q1 : 0u;
+    patch.z = lane == pl ? q2 : (lane == 2 ? opd << 16 : 0u);
+    patch.w = lane == pl ? q3 : 0u;
+    const int hchunks = 4 + (int)wfd;
     const int ho = lane < hchunks ? 16 * lane : kOobOffset, po = 16 * (hchunks + lane);
-    if (kOut16) {
-        __builtin_amdgcn_raw_buffer_store_b128(h, orow, ho, 0, kAuxNt);
-        __builtin_amdgcn_raw_buffer_store_b128(v, orow, po, 0, kAuxNt);
-    } else {
-        __builtin_amdgcn_raw_buffer_store_b32(h.x, orow, ho, 0, kAuxNt);
-        __builtin_amdgcn_raw_buffer_store_b32(h.y, orow, ho + 4, 0, kAuxNt);
-        __builtin_amdgcn_raw_buffer_store_b32(h.z, orow, ho + 8, 0, kAuxNt);
-        __builtin_amdgcn_raw_buffer_store_b32(h.w, orow, ho + 12, 0, kAuxNt);
-        __builtin_amdgcn_raw_buffer_store_b32(v.x, orow, po, 0, kAuxNt);
-        __builtin_amdgcn_raw_buffer_store_b32(v.y, orow, po + 4, 0, kAuxNt);
-        __builtin_amdgcn_raw_buffer_store_b32(v.z, orow, po + 8, 0, kAuxNt);
-        // lane 63 stops at the frame's 4-byte-rounded end
-        __builtin_amdgcn_raw_buffer_store_b32(v.w, orow, lane < kWave - 1 ? po + 12 : kOobOffset, 0, kAuxNt);
+    for (int c = 0; c < fan; ++c) {
+        u4 h = reinterpret_cast<const u4*>(t.img[2 * c + wfd])[lane < 5 ? lane : 0];
+        h.x |= patch.x;
+        h.y |= patch.y;
+        h.z |= patch.z;
+        h.w |= patch.w;
+        uint32_t crc = pc ^ t.hcrc[2 * c + wfd];
+        if (wfd) {
+            // child c's RETH (util.c:409-417): bytes 54-69, lane 3's chunk from
+            // byte 6 on and lane 4's first 6 bytes; its ICRC term, lanes 0-15
+            uint32_t R[4];
+            reth_of(c, R);
+            const uint32_t R0 = R[0], R1 = R[1], R2 = R[2], R3 = R[3];
+            if (lane == 3) {
+                h.y |= R0 << 16;
+                h.z = __builtin_amdgcn_alignbyte(R1, R0, 2);
+                h.w = __builtin_amdgcn_alignbyte(R2, R1, 2);
+            }
+            if (lane == 4) {
+                h.x = __builtin_amdgcn_alignbyte(R3, R2, 2);
+                h.y |= R3 >> 16;
+            }
+            const uint32_t rk = (lane & 8) ? ((lane & 4) ? R3 : R2) : ((lane & 4) ? R1 : R0);
+            crc ^= wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
+        }
+        crc = ~crc;   // util.c:424-426
+        const u4 v = {p0, last ? t63 | (crc << 16) : p1, last ? crc >> 16 : p2, p3};
+        const __amdgpu_buffer_rsrc_t orow = uniform_rsrc(A.out + (fd * fan + c) * A.out_stride, A.out_stride);
+        if (kOut16) {
+            __builtin_amdgcn_raw_buffer_store_b128(h, orow, ho, 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b128(v, orow, po, 0, kAuxNt);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(h.x, orow, ho, 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(h.y, orow, ho + 4, 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(h.z, orow, ho + 8, 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(h.w, orow, ho + 12, 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(v.x, orow, po, 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(v.y, orow, po + 4, 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(v.z, orow, po + 8, 0, kAuxNt);
+            // lane 63 stops at the frame's 4-byte-rounded end
+            __builtin_amdgcn_raw_buffer_store_b32(v.w, orow, last ? kOobOffset : po + 12, 0, kAuxNt);
+        }
     }
 }
 
+// One pair of frames (2 pidx, 2 pidx + 1): classify, sum, and (batch call)
+// broadcast.  g = the batch generation.
 template <bool kEmit, bool kOut16>
-__global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_apply(ApplyArgs A)
+__device__ __forceinline__ void apply_pair(const ApplyArgs& A, const int32_t* __restrict__ act_in,
+                                           const int32_t* __restrict__ ports_in, const uint32_t* __restrict__ psns_in,
+                                           int64_t pidx, uint32_t g, const EmitLds* tp, const LaneK& L)
 {
     const InccSwitchState& s = A.s;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
-    const int fan = s.fan_in;
+    // the lane number through an opaque copy: what the pair derives from it is
+    // computed per pair, not hoisted out of the persistent loop into registers
+    // held for the whole kernel (the occupancy is what hides this kernel's latency)
+    const int lane = (int)opaque_u32((uint32_t)L.lane), fan = s.fan_in;
     const int64_t count = A.count, stride = A.stride;
-    const int64_t pidx = (int64_t)blockIdx.x * kApplyWaves + w;   // this wave's pair
-    const bool have = 2 * pidx < count;   // (a wave without a pair still joins its block's table load)
+    const bool have = 2 * pidx < count;
     const int64_t f0 = have ? 2 * pidx : 0;
     const bool in1 = have && f0 + 1 < count;
     const int64_t f1 = in1 ? f0 + 1 : f0;
@@ -1278,85 +1307,61 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_apply(ApplyArgs 
             e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane < 2 ? rb + 1072 + 16 * lane : kOobOffset, 0, 0);
         }
     }
-    const uint32_t g = s.gen[1];   // this batch's generation (claim's)
-    int act[2], port[2];
-    uint32_t psn[2];
-    act[0] = A.action[f0];
-    act[1] = A.action[f1];
-    port[0] = A.ports[f0];
-    port[1] = A.ports[f1];
-    psn[0] = A.psns[f0];
-    psn[1] = A.psns[f1];
-    if (!have) act[0] = INCCL_SW_IGNORED;
-    if (!in1) act[1] = INCCL_SW_IGNORED;
-    // the batch call's tables, while round trip 1 is in flight
-    __shared__ ApplyShared<kEmit> sh;
-    if constexpr (kEmit) {
-        // the four fixed tables are one contiguous run of u4 in EmitLds, read
-        // from their own arrays; two u4 per thread (clamped indices: a thread
-        // past the end rewrites the last entry)
-        constexpr int kThreads = kWave * kApplyWaves;
-        auto src = [&](int i) -> u4 {
-            constexpr int n0 = 16 * 2 * 16 / 4, n1 = n0 + 8 * 16 * 8 / 4, n2 = n1 + 8 * 16 * 8 / 4;
-            return i < n0 ? reinterpret_cast<const u4*>(&g_seg[1][0][0])[i]
-                 : i < n1 ? reinterpret_cast<const u4*>(&g_ls[0][0][0])[i - n0]
-                 : i < n2 ? reinterpret_cast<const u4*>(&g_gs[0][0][0])[i - n1]
-                          : reinterpret_cast<const u4*>(&g_var[0][0][0])[i - n2];
-        };
-        const int i0 = (int)threadIdx.x < kEmitFixedU4 ? (int)threadIdx.x : kEmitFixedU4 - 1;
-        const int i1 = (int)threadIdx.x + kThreads < kEmitFixedU4 ? (int)threadIdx.x + kThreads : kEmitFixedU4 - 1;
-        const u4 v0 = src(i0), v1 = src(i1);
-        // this fan-in's header images and terms (claim's first wave wrote them)
-        const int nh = 2 * fan * (kHdrImg / 4), nt = nh + 2 * fan;
-        int j[3];
-        uint32_t hv[3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            j[r] = (int)threadIdx.x + r * kThreads < nt ? (int)threadIdx.x + r * kThreads : nt - 1;
-            hv[r] = j[r] < nh ? s.hdr[j[r]] : s.hdr[2 * 31 * (kHdrImg / 4) + (j[r] - nh)];
-        }
-        u4* tf = reinterpret_cast<u4*>(&sh.t.seg[0][0][0]);
-        tf[i0] = v0;
-        tf[i1] = v1;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            if (j[r] < nh) reinterpret_cast<uint32_t*>(&sh.t.img[0][0])[j[r]] = hv[r];
-            else sh.t.hcrc[j[r] - nh] = hv[r];
-        }
-        __syncthreads();
-    }
+    // the claim results, as scalar loads (the kernel's read-only views of
+    // action / ports / PSNs, so that they arrive apart from the payloads and
+    // round trip 2 can be issued before those land)
+    FrameK F[2];
+    F[0].act = have ? act_in[f0] : INCCL_SW_IGNORED;
+    F[1].act = in1 ? act_in[f1] : INCCL_SW_IGNORED;
+    F[0].port = ports_in[f0];
+    F[1].port = ports_in[f1];
+    F[0].psn = psns_in[f0];
+    F[1].psn = psns_in[f1];
     const uint32_t tag = ~g, result_bit = 1u << fan, smask = s.slots - 1;
-    if (blockIdx.x == 0 && threadIdx.x == 0) s.gen[0] = g;   // the next batch's claim adds one
-    bool live[2];
-    uint32_t op[2], wf[2], slot[2];
-    uint32_t P[2][4], R[2][4];   // each frame's payload words (this lane's four) and RETH words (uniform)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        live[k] = (act[k] & ~0xFF) == kActPending;
-        op[k] = (uint32_t)act[k] & 0xFFu;
-        wf[k] = is_write_first((uint8_t)op[k]) ? 1u : 0u;
-        slot[k] = psn[k] & smask;
+        FrameK& f = F[k];
+        f.live = (f.act & kActPending) != 0;
+        f.op = (uint32_t)f.act & 0xFFu;
+        f.wf = ((uint32_t)f.act >> 9) & 1u;
+        f.slot = f.psn & smask;
+    }
+    // round trip 2, lane-parallel over the two frames: half h = lane / 32 is
+    // frame h; lane 32 h + p < 32 h + fan_in loads port p's first-copy key,
+    // lanes 32 h and 32 h + 1 the two tagged arrival words
+    const int hf = lane >> 5, pl = lane & 31;
+    const bool live_h = hf ? F[1].live : F[0].live;
+    const uint32_t slot_h = hf ? F[1].slot : F[0].slot;
+    const uint64_t key = live_h && pl < fan ? s.first[(size_t)slot_h * fan + pl] : 0ull;
+    const uint64_t av = live_h && pl < 2 ? s.arrival[2 * (size_t)slot_h + pl] : 0ull;
+    uint32_t keep[2] = {0u, 0u};   // the batch call: the RETH keeper of each frame's slot
+    if (kEmit) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (F[k].live) keep[k] = s.reth[(size_t)F[k].slot * fan * 4 + (lane < 4 * fan ? lane : 0)];
+    }
+    // each frame's payload words (this lane's four) and RETH words (uniform),
+    // from the chunks of round trip 1 while round trip 2 is in flight
+    uint32_t P[2][4], R[2][4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const FrameK& f = F[k];
 #pragma unroll
         for (int j = 0; j < 4; ++j) P[k][j] = R[k][j] = 0u;
-        if (!live[k]) continue;
+        if (!f.live) continue;
         if (A.wide) {
             // chunk 4 + lane (lane 63: chunk 67) and 5 + lane (lane 62: 67, lane 63: 68)
-            uint32_t y0 = (uint32_t)__shfl_down((int)x[k].x, 1, kWave), y1 = (uint32_t)__shfl_down((int)x[k].y, 1, kWave);
-            const uint32_t c67x = (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 0);
-            const uint32_t c67y = (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 0);
-            if (lane == kWave - 1) {
-                y0 = c67x;
-                y1 = c67y;
-            }
-            if (wf[k]) {
-                uint32_t y2 = (uint32_t)__shfl_down((int)x[k].z, 1, kWave), y3 = (uint32_t)__shfl_down((int)x[k].w, 1, kWave);
-                uint32_t z0 = (uint32_t)__shfl_down((int)y0, 1, kWave), z1 = (uint32_t)__shfl_down((int)y1, 1, kWave);
-                if (lane == kWave - 1) {
-                    y2 = (uint32_t)__builtin_amdgcn_readlane((int)e[k].z, 0);
-                    y3 = (uint32_t)__builtin_amdgcn_readlane((int)e[k].w, 0);
-                    z0 = (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 1);
-                    z1 = (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 1);
-                }
+            const bool last = lane == kWave - 1;
+            uint32_t y0 = from_next(x[k].x, L.next4), y1 = from_next(x[k].y, L.next4);
+            y0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 0) : y0;
+            y1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 0) : y1;
+            if (f.wf) {
+                uint32_t y2 = from_next(x[k].z, L.next4), y3 = from_next(x[k].w, L.next4);
+                uint32_t z0 = from_next(y0, L.next4), z1 = from_next(y1, L.next4);
+                y2 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].z, 0) : y2;
+                y3 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].w, 0) : y3;
+                z0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 1) : z0;
+                z1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 1) : z1;
                 payload_from_chunks(u4{y0, y1, y2, y3}, z0, z1, P[k]);
                 // the RETH, bytes 54-69: bytes 6-15 of chunk 3 (lane 0), 0-5 of chunk 4 (lane 1)
                 const uint32_t c3y = (uint32_t)__builtin_amdgcn_readlane((int)x[k].y, 0);
@@ -1373,27 +1378,14 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_apply(ApplyArgs 
             }
         } else {
             const uint8_t* fr = A.frames + (f0 + k) * stride;
-            payload16(fr, wf[k], lane, false, P[k]);
-            if (wf[k]) reth_words(fr, lane, R[k]);
+            payload16(fr, f.wf, lane, false, P[k]);
+            if (f.wf) reth_words(fr, lane, R[k]);
         }
-    }
-    // round trip 2, lane-parallel over the two frames: half h = lane / 32 is
-    // frame h; lane 32 h + p < 32 h + fan_in loads port p's first-copy key,
-    // lanes 32 h and 32 h + 1 the two tagged arrival words
-    const int hf = lane >> 5, pl = lane & 31;
-    const bool live_h = hf ? live[1] : live[0];
-    const uint32_t slot_h = hf ? slot[1] : slot[0];
-    const uint64_t key = live_h && pl < fan ? s.first[(size_t)slot_h * fan + pl] : 0ull;
-    const uint64_t av = live_h && pl < 2 ? s.arrival[2 * (size_t)slot_h + pl] : 0ull;
-    uint32_t keep[2] = {0u, 0u};   // the batch call: the RETH keeper of each frame's slot
-    if (kEmit) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-            if (live[k]) keep[k] = s.reth[(size_t)slot[k] * fan * 4 + (lane < 4 * fan ? lane : 0)];
     }
     uint32_t pre[2];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) pre[k] = live[k] ? arrival_before(readlane64(av, 32 * k), readlane64(av, 32 * k + 1), g) : 0u;
+    for (int k = 0; k < 2; ++k)
+        pre[k] = F[k].live ? arrival_before(readlane64(av, 32 * k), readlane64(av, 32 * k + 1), g) : 0u;
     // classify (nts.c:353-372): lane 32 h + p < fan_in says when frame h's port
     // p counts, as 1 + frame index; 0 = before the batch, ~0 = not in this batch
     const uint32_t pre_h = hf ? pre[1] : pre[0];
@@ -1402,50 +1394,50 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_apply(ApplyArgs 
     if (live_h && pl < fan) {
         const bool in_batch = (uint32_t)(key >> 32) == tag;
         const uint32_t ef = ((uint32_t)key) >> 1;
-        at = (pre_h & (1u << pl)) ? 0u : (in_batch ? ef + 1u : 0xFFFFFFFFu);
+        const bool before = (pre_h >> pl) & 1u;
+        at = before ? 0u : (in_batch ? ef + 1u : 0xFFFFFFFFu);
         mine = in_batch ? ef : 0xFFFFFFFFu;
         fo = (uint32_t)key;                                 // frame << 1 | wf
-        counted = in_batch && !(pre_h & (1u << pl));
+        counted = in_batch && !before;
     }
     const uint64_t bal = __ballot(counted);
     uint32_t d = at;                                        // max over each half: the completing arrival
 #pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) {
-        const uint32_t v = (uint32_t)__shfl_xor((int)d, o, kWave);
-        d = v > d ? v : d;
-    }
+    for (int o = 16; o >= 1; o >>= 1) d = max(d, (uint32_t)__shfl_xor((int)d, o, kWave));
     int out_act[2];
     bool lead[2], counted_me[2];
     uint32_t cports[2], done_at[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        out_act[k] = act[k];
+        const FrameK& f = F[k];
+        out_act[k] = f.act;
         cports[k] = (uint32_t)(bal >> (32 * k));
         done_at[k] = (uint32_t)__builtin_amdgcn_readlane((int)d, 32 * k);
         lead[k] = counted_me[k] = false;
-        if (!live[k]) continue;
-        const uint32_t f = (uint32_t)(f0 + k);
-        const uint32_t mk = (uint32_t)__builtin_amdgcn_readlane((int)mine, 32 * k + port[k]);
+        if (!f.live) continue;
+        const uint32_t fi = (uint32_t)(f0 + k);
+        const uint32_t mk = (uint32_t)__builtin_amdgcn_readlane((int)mine, 32 * k + f.port);
         const uint32_t dk = done_at[k];
-        const bool arrival = !(pre[k] & (1u << port[k])) && mk == f;   // the counted arrival: nts.c:359-363
+        const bool arrival = !((pre[k] >> f.port) & 1u) && mk == fi;   // the counted arrival: nts.c:359-363
         counted_me[k] = arrival;
         if (arrival) {
-            out_act[k] = (dk == f + 1u) ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
+            out_act[k] = (dk == fi + 1u) ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
         } else {                                                 // retransmit: nts.c:353-357
             const bool done_before = (pre[k] & result_bit) != 0;
-            const bool done_earlier = dk != 0u && dk != 0xFFFFFFFFu && dk - 1u < f;
+            const bool done_earlier = dk != 0u && dk != 0xFFFFFFFFu && dk - 1u < fi;
             out_act[k] = (done_before || done_earlier) ? INCCL_SW_REPLAY : INCCL_SW_DROPPED;
         }
-        lead[k] = arrival && port[k] == __builtin_ctz(cports[k]);
+        lead[k] = arrival && f.port == __builtin_ctz(cports[k]);
     }
     // the leaders: sum, store, bitmap, recycle, broadcast
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         if (!lead[k]) continue;
+        const FrameK& f = F[k];
         u4 acc = {0u, 0u, 0u, 0u};
         // a slot whose bitmap was empty before the batch holds zeros (reset,
         // or recycled since its last use), so its partial is not read
-        if (pre[k] != 0u) acc = reinterpret_cast<const u4*>(s.agg + (size_t)slot[k] * kLanes)[lane];
+        if (pre[k] != 0u) acc = reinterpret_cast<const u4*>(s.agg + (size_t)f.slot * kLanes)[lane];
         for (uint32_t m = cports[k]; m; m &= m - 1) {
             const uint32_t ek = (uint32_t)__builtin_amdgcn_readlane((int)fo, 32 * k + __builtin_ctz(m));
             const int64_t fe = (int64_t)(ek >> 1);
@@ -1464,77 +1456,58 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_apply(ApplyArgs 
             acc.z += q[2];
             acc.w += q[3];
         }
-        __builtin_nontemporal_store(acc, reinterpret_cast<u4*>(s.agg + (size_t)slot[k] * kLanes) + lane);
+        __builtin_nontemporal_store(acc, reinterpret_cast<u4*>(s.agg + (size_t)f.slot * kLanes) + lane);
         const bool complete = done_at[k] != 0xFFFFFFFFu;
         if (lane == 0)
-            s.arrival[2 * (size_t)slot[k] + (g & 1u)] =
+            s.arrival[2 * (size_t)f.slot + (g & 1u)] =
                 ((uint64_t)g << 32) | (pre[k] | cports[k] | (complete ? result_bit : 0u));   // nts.c:359, :366
         if (!complete) continue;
         {   // clear_state_data(psn + WINDOW), nts.c:235-242, :367
-            const uint32_t rs = (psn[k] + (s.slots >> 1)) & smask;
+            const uint32_t rs = (f.psn + (s.slots >> 1)) & smask;
             for (int i = lane; i < fan * 4; i += kWave) s.reth[(size_t)rs * fan * 4 + i] = 0u;
             if (lane < 2) s.arrival[2 * (size_t)rs + lane] = (uint64_t)g << 32;
             if (lane == 0) s.degree[rs] = 0;
         }
         if constexpr (kEmit) {
-            const EmitLds& t = sh.t;
             // the broadcast of the completing frame fd (nts.c:447-453): its
             // opcode, this PSN, each child's RETH as the keeper now holds it
             const int64_t fd = (int64_t)done_at[k] - 1;
-            uint32_t opd;
-            if (fd == f0) opd = op[0];
-            else if (in1 && fd == f1) opd = op[1];
-            else {
+            uint32_t opd, wfd;
+            if (fd == f0) {
+                opd = F[0].op;
+                wfd = F[0].wf;
+            } else if (in1 && fd == f1) {
+                opd = F[1].op;
+                wfd = F[1].wf;
+            } else {
                 const uint32_t w10 = reinterpret_cast<const uint32_t*>(A.frames + fd * stride)[10 + (lane & 1)];
                 opd = ((uint32_t)__builtin_amdgcn_readlane((int)w10, 0) >> 16) & 0xFFu;
+                wfd = is_write_first((uint8_t)opd) ? 1u : 0u;
             }
-            const int wfd = is_write_first((uint8_t)opd) ? 1 : 0;
-            uint32_t a[4];   // this lane's 16 payload bytes, big-endian (util.c:403-405), memory order
-            a[0] = __builtin_bswap32(acc.x);
-            a[1] = __builtin_bswap32(acc.y);
-            a[2] = __builtin_bswap32(acc.z);
-            a[3] = __builtin_bswap32(acc.w);
-            uint32_t nx[3];
+            // child c's RETH as the keeper holds it after this batch
+            auto reth_of = [&](int c, uint32_t (&r)[4]) {
+                const uint32_t ec = (uint32_t)__builtin_amdgcn_readlane((int)fo, 32 * k + c);
+                if (((cports[k] >> c) & 1u) && (ec & 1u)) {   // counted in this batch from a WRITE_FIRST copy
+                    const int64_t fe = (int64_t)(ec >> 1);
+                    if (fe == f0) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j) nx[j] = (uint32_t)__shfl_down((int)a[j], 1, kWave);
-            const uint32_t pcs[4] = {__builtin_amdgcn_alignbyte(a[3], a[2], 2), __builtin_amdgcn_alignbyte(nx[0], a[3], 2),
-                                     __builtin_amdgcn_alignbyte(nx[1], nx[0], 2), __builtin_amdgcn_alignbyte(nx[2], nx[1], 2)};
-            const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)a[0], 0);
-            const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)a[1], 0);
-            const uint32_t a2 = (uint32_t)__builtin_amdgcn_readlane((int)a[2], 0);
-            const uint32_t pw = psn[k] | 0x80000000u;
-            // P, and the opcode and PSN bytes (util.c:378, :386) on lanes 0-4
-            const uint32_t vb = lane < 5 ? var_crc(t, wfd, lane, lane == 0 ? opd : (pw >> (8 * (4 - lane))) & 0xFFu) : 0u;
-            const uint32_t pc = payload_crc(t, a, lane) ^ (uint32_t)__builtin_amdgcn_readlane((int)vb, 0) ^
-                                (uint32_t)__builtin_amdgcn_readlane((int)vb, 1) ^ (uint32_t)__builtin_amdgcn_readlane((int)vb, 2) ^
-                                (uint32_t)__builtin_amdgcn_readlane((int)vb, 3) ^ (uint32_t)__builtin_amdgcn_readlane((int)vb, 4);
-            for (int c = 0; c < fan; ++c) {
-                uint32_t Rc[4] = {0u, 0u, 0u, 0u};
-                if (wfd) {
-                    const uint32_t ec = (uint32_t)__builtin_amdgcn_readlane((int)fo, 32 * k + c);
-                    if (((cports[k] >> c) & 1u) && (ec & 1u)) {   // counted in this batch from a WRITE_FIRST copy
-                        const int64_t fe = (int64_t)(ec >> 1);
-                        if (fe == f0) {
+                        for (int j = 0; j < 4; ++j) r[j] = R[0][j];
+                    } else if (in1 && fe == f1) {
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) Rc[j] = R[0][j];
-                        } else if (in1 && fe == f1) {
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) Rc[j] = R[1][j];
-                        } else {
-                            reth_words(A.frames + fe * stride, lane, Rc);
-                        }
-                    } else if (c < kWave / 4) {                 // the keeper, as loaded
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) Rc[j] = (uint32_t)__builtin_amdgcn_readlane((int)keep[k], 4 * c + j);
+                        for (int j = 0; j < 4; ++j) r[j] = R[1][j];
                     } else {
-                        const uint32_t v = s.reth[((size_t)slot[k] * fan + c) * 4 + (lane & 3)];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) Rc[j] = (uint32_t)__builtin_amdgcn_readlane((int)v, j);
+                        reth_words(A.frames + fe * stride, lane, r);
                     }
+                } else if (c < kWave / 4) {                 // the keeper, as loaded
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) r[j] = (uint32_t)__builtin_amdgcn_readlane((int)keep[k], 4 * c + j);
+                } else {
+                    const uint32_t v = s.reth[((size_t)f.slot * fan + c) * 4 + (lane & 3)];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) r[j] = (uint32_t)__builtin_amdgcn_readlane((int)v, j);
                 }
-                emit_child<kOut16>(t, c, wfd, opd, pw, pc, pcs, a0, a1, a2, a[3], Rc, A.out + (fd * fan + c) * A.out_stride,
-                                   A.out_stride, lane);
-            }
+            };
+            emit_broadcast<kOut16>(A, *tp, L, acc, fd, opd, wfd, f.psn, fan, reth_of);
         }
     }
     // every frame: its action, its RETH into the keeper if it is a counted
@@ -1542,18 +1515,69 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_apply(ApplyArgs 
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         if (k == 0 ? !have : !in1) continue;
-        const int64_t f = f0 + k;
-        if (live[k] && lane == 0) A.action[f] = out_act[k];
-        if (counted_me[k] && wf[k] && lane < 4)
-            s.reth[((size_t)slot[k] * fan + port[k]) * 4 + lane] =
+        const FrameK& f = F[k];
+        const int64_t fi = f0 + k;
+        if (f.live && lane == 0) A.action[fi] = out_act[k];
+        if (counted_me[k] && f.wf && lane < 4)
+            s.reth[((size_t)f.slot * fan + f.port) * 4 + lane] =
                 lane == 0 ? R[k][0] : lane == 1 ? R[k][1] : lane == 2 ? R[k][2] : R[k][3];
         if (kEmit && lane < fan) {
             const int fin = out_act[k];
-            const int total = 54 + 16 * (int)wf[k] + kLanes * 4 + 4;   // util.c:341-345
-            A.out_len[f * fan + lane] =
-                (live[k] && (fin == INCCL_SW_COMPLETED || (fin == INCCL_SW_REPLAY && lane == port[k]))) ? total : 0;
+            const int total = 54 + 16 * (int)f.wf + kLanes * 4 + 4;   // util.c:341-345
+            A.out_len[fi * fan + lane] =
+                (f.live && (fin == INCCL_SW_COMPLETED || (fin == INCCL_SW_REPLAY && lane == f.port))) ? total : 0;
         }
     }
+}
+
+// The claim results are read through separate restrict views of the same
+// arrays (act_in == A.action): every entry is read by one wave before that wave
+// writes it, so the reads are of claim's values.
+#define INCCL_APPLY_ARGS                                                                                        \
+    ApplyArgs A, const int32_t *__restrict__ act_in, const int32_t *__restrict__ ports_in,                     \
+        const uint32_t *__restrict__ psns_in
+
+// the split call: one pair per wave, short-lived blocks
+__global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_apply(INCCL_APPLY_ARGS)
+{
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    const LaneK L{lane, ((lane + 1) & (kWave - 1)) * 4};
+    const uint32_t g = A.s.gen[1];   // this batch's generation (claim's)
+    apply_pair<false, true>(A, act_in, ports_in, psns_in, (int64_t)blockIdx.x * kApplyWaves + w, g, nullptr, L);
+    // the next batch's claim adds one (stored last: a store before the claim
+    // results' loads would keep the compiler from reading them as scalars)
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.s.gen[0] = g;
+}
+
+// the batch call: persistent blocks, the egress tables loaded once per block
+template <bool kOut16>
+__global__ __launch_bounds__(kWave* kEmitWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_ingress_apply_emit(
+    INCCL_APPLY_ARGS)
+{
+    __shared__ EmitLds t;
+    const InccSwitchState& s = A.s;
+    const int fan = s.fan_in;
+    {
+        constexpr int kFixed = (int)(sizeof(t.segb) + sizeof(t.lane16) + sizeof(t.var)) / 16;
+        constexpr int n0 = (int)sizeof(t.segb) / 16, n1 = n0 + (int)sizeof(t.lane16) / 16;
+        u4* dst = reinterpret_cast<u4*>(&t.segb[0][0]);
+        for (int i = threadIdx.x; i < kFixed; i += blockDim.x)
+            dst[i] = i < n0 ? reinterpret_cast<const u4*>(&g_segb[0][0])[i]
+                   : i < n1 ? reinterpret_cast<const u4*>(&g_lane16[0][0][0])[i - n0]
+                            : reinterpret_cast<const u4*>(&g_var[0][0][0])[i - n1];
+        // this fan-in's header images and ICRC terms (claim's first wave wrote them)
+        const int nh = 2 * fan * (kHdrImg / 4);
+        for (int i = threadIdx.x; i < nh; i += blockDim.x) reinterpret_cast<uint32_t*>(&t.img[0][0])[i] = s.hdr[i];
+        for (int i = threadIdx.x; i < 2 * fan; i += blockDim.x) t.hcrc[i] = s.hdr[2 * 31 * (kHdrImg / 4) + i];
+    }
+    __syncthreads();
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    const LaneK L{lane, ((lane + 1) & (kWave - 1)) * 4};
+    const uint32_t g = s.gen[1];
+    const int64_t pairs = (A.count + 1) >> 1, step = (int64_t)gridDim.x * kEmitWaves;
+    for (int64_t p = (int64_t)blockIdx.x * kEmitWaves + w; p < pairs; p += step)
+        apply_pair<true, kOut16>(A, act_in, ports_in, psns_in, p, g, &t, L);
+    if (blockIdx.x == 0 && threadIdx.x == 0) s.gen[0] = g;
 }
 
 // The batch call's REPLAY resends (nts.c:353-356 / :435-438), after apply: a
@@ -1603,8 +1627,7 @@ uint32_t host_seg34[kSeg2][2][16];
 uint32_t host_lane_shift32[8][16][32];
 uint32_t host_var[5 + kVarBytes][2][16];
 uint32_t host_z1024[8][16];
-uint32_t host_ls[8][16][8];
-uint32_t host_gs[8][16][8];
+uint32_t host_segb[16][256];
 bool g_tables_ready[64];
 std::mutex g_tables_mu;
 
@@ -1653,17 +1676,9 @@ int ensure_tables()
                 x = zeros_append(x, 16);
             }
         }
-    // the batch call's two-step payload shift: Z_{16 (7 - s)} and Z_{128 (7 - s)}
-    for (int n = 0; n < 8; ++n)
-        for (uint32_t v = 0; v < 16; ++v) {
-            uint32_t x = v << (4 * n), y = x;
-            for (int c = 7; c >= 0; --c) {
-                host_ls[n][v][c] = x;
-                host_gs[n][v][c] = y;
-                x = zeros_append(x, 16);
-                y = zeros_append(y, 128);
-            }
-        }
+    // the batch call's payload segments: byte j of 16 -> Z_{15-j}(T[value])
+    for (int j = 0; j < 16; ++j)
+        for (uint32_t v = 0; v < 256; ++v) host_segb[j][v] = zeros_append(host_tab[v], 15 - j);
     for (int wf = 0; wf < 2; ++wf) {
         const int hdr = wf ? 60 : 44;   // ICRC message bytes before the payload (frame 10 .. doff - 1)
         for (int k = 0; k < kVarBytes; ++k) {
@@ -1679,8 +1694,7 @@ int ensure_tables()
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_z1024), host_z1024, sizeof(host_z1024));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg34), host_seg34, sizeof(host_seg34));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane_shift32), host_lane_shift32, sizeof(host_lane_shift32));
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_ls), host_ls, sizeof(host_ls));
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_gs), host_gs, sizeof(host_gs));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_segb), host_segb, sizeof(host_segb));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_tab), host_tab, sizeof(host_tab));
     if (e != hipSuccess) return (int)e;
     if (dev >= 0 && dev < 64) g_tables_ready[dev] = true;
@@ -1701,13 +1715,30 @@ int num_cus()
     return cus;
 }
 
-// one wave per pair of frames, short-lived blocks
-template <bool kEmit, bool kOut16>
+// split call: one wave per pair of frames, short-lived blocks
 int launch_apply(const ApplyArgs& a, hipStream_t st)
 {
     const int64_t pairs = (a.count + 1) / 2, blocks = (pairs + kApplyWaves - 1) / kApplyWaves;
-    hipLaunchKernelGGL((k_ingress_apply<kEmit, kOut16>), dim3((unsigned)(blocks < 1 ? 1 : blocks)),
-                       dim3(kWave * kApplyWaves), 0, st, a);
+    hipLaunchKernelGGL(k_ingress_apply, dim3((unsigned)(blocks < 1 ? 1 : blocks)), dim3(kWave * kApplyWaves), 0, st, a,
+                       (const int32_t*)a.action, a.ports, a.psns);
+    return (int)hipGetLastError();
+}
+
+// batch call: persistent blocks, as many as fit beside each other
+template <bool kOut16>
+int launch_apply_emit(const ApplyArgs& a, hipStream_t st)
+{
+    static const int per_cu = [] {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_ingress_apply_emit<kOut16>, kWave * kEmitWaves, 0) !=
+                hipSuccess || n < 1)
+            n = 1;
+        return n;
+    }();
+    const int64_t pairs = (a.count + 1) / 2, need = (pairs + kEmitWaves - 1) / kEmitWaves;
+    const int64_t cap = (int64_t)num_cus() * per_cu;
+    hipLaunchKernelGGL(k_ingress_apply_emit<kOut16>, dim3((unsigned)(need < cap ? (need < 1 ? 1 : need) : cap)),
+                       dim3(kWave * kEmitWaves), 0, st, a, (const int32_t*)a.action, a.ports, a.psns);
     return (int)hipGetLastError();
 }
 
@@ -1778,7 +1809,7 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
     if (check_batch_args(s, frames, stride, count, ports, action, psn_out)) return INCCL_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     launch_claim(s, frames, stride, count, ports, action, psn_out, nullptr, st);
-    return launch_apply<false, true>(apply_args(s, frames, stride, count, ports, action, psn_out), st);
+    return launch_apply(apply_args(s, frames, stride, count, ports, action, psn_out), st);
 }
 
 int inccl_k_switch_batch(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count,
@@ -1798,7 +1829,7 @@ int inccl_k_switch_batch(const InccSwitchState* s, const uint8_t* frames, size_t
     a.out_stride = (int64_t)out_stride;
     a.out_len = out_len;
     const bool o16 = ((out_stride & 15) == 0) && (((uintptr_t)out & 15) == 0);
-    rc = o16 ? launch_apply<true, true>(a, st) : launch_apply<true, false>(a, st);
+    rc = o16 ? launch_apply_emit<true>(a, st) : launch_apply_emit<false>(a, st);
     if (rc) return rc;
     const int64_t need = ((int64_t)count + kWave * kEgressWaves - 1) / (kWave * kEgressWaves);
     const int64_t cap = num_cus();

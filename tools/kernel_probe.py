@@ -2,6 +2,7 @@
 by rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE) and used for tuning sweeps.
 
     python tools/kernel_probe.py --kernel fused --R 2 --mib 256 --iters 20
+    python tools/kernel_probe.py --kernel fused --R 2 --mib 256 --sets 4   # cold: four sets rotated
     python tools/kernel_probe.py --sweep
 """
 import argparse
@@ -22,6 +23,8 @@ def main():
     p.add_argument("--grid-cap", type=int, default=0)
     p.add_argument("--no-nt", action="store_true")
     p.add_argument("--sweep", action="store_true")
+    p.add_argument("--sets", type=int, default=1,
+                   help="fused: rotate this many independent input/output sets (cold when they exceed the caches)")
     a = p.parse_args()
     import torch
     import container_inc_amd
@@ -31,7 +34,10 @@ def main():
     n = a.mib * (1 << 20) // 4
     R = a.R
     g = torch.Generator(device=dev).manual_seed(1000)
-    xs = [torch.randn(n, generator=g, device=dev) for _ in range(R)]
+    sets = [[torch.randn(n, generator=g, device=dev) for _ in range(R)] for _ in range(max(1, a.sets))]
+    xs = sets[0]
+    outs = [torch.empty(n, device=dev) for _ in range(max(1, a.sets))]
+    turn = [0]
     qs = [torch.randint(-2 ** 26, 2 ** 26, (n,), device=dev, dtype=torch.int32) for _ in range(R)]
     outf = torch.empty(n, device=dev)
     outq = torch.empty(n, device=dev, dtype=torch.int32)
@@ -43,7 +49,9 @@ def main():
     def run(kind):
         s = st.cuda_stream
         if kind == "fused":
-            inccl.reduce_f32(xs, 25, out=outf, stream=s)
+            i = turn[0] % len(sets)
+            turn[0] += 1
+            inccl.reduce_f32(sets[i], 25, out=outs[i], stream=s)
         elif kind == "quant_sum":
             inccl.quant_sum(xs, 25, out=outq, stream=s)
         elif kind == "quantise":
@@ -89,8 +97,8 @@ def main():
         return
     inccl.set_tuning(a.grid_cap, not a.no_nt)
     ms, gbs = timeit(a.kernel, a.iters)
-    print(json.dumps({"kernel": a.kernel, "R": R, "n": n, "ms": round(ms, 5), "GBs": round(gbs, 1),
-                      "alg_bytes": alg_bytes(a.kernel)}))
+    print(json.dumps({"kernel": a.kernel, "R": R, "n": n, "sets": a.sets, "ms": round(ms, 5), "GBs": round(gbs, 1),
+                      "frac": round(gbs / 8000.0, 4), "alg_bytes": alg_bytes(a.kernel)}))
 
 
 if __name__ == "__main__":

@@ -4,7 +4,7 @@
 // its operands on die.  Variants: the product kernel at several geometries and
 // cache policies, a per-XCD contiguous tile mapping, and memory-only references
 // (2-read + 1-write add, copy) timed the same way.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I container_inc_amd/csrc tools/tune/tune_cold.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I container_inc_amd/csrc tools/tune/tune_cold.hip -o tools/tune/tune_cold
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -22,7 +22,8 @@ using namespace inccl_dev;
         }                                                                             \
     } while (0)
 
-constexpr int S = 4;
+constexpr int kMaxSets = 4;
+static int S = 4;   // sets rotated (argv[2]); 1 = every launch on the same set
 
 __global__ void k_fill(float* p, int64_t n, uint32_t seed)
 {
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(BLOCK) void k_copy(const u32x4* __restrict__ a, u32
 }
 
 static hipEvent_t e0, e1;
-static float *A[S], *B[S], *O[S];
+static float *A[kMaxSets], *B[kMaxSets], *O[kMaxSets];
 static int64_t n, n4;
 
 static bool g_hot = false;   // hot: every launch on set 0 (the bench's repeated step)
@@ -245,27 +246,44 @@ static void refs()
     report("copy_ref", BLOCK, 1, 1, 1, 1, ms, 8.0 * n);
 }
 
-int main()
+// usage: tune_cold [MiB per bucket = 256] [sets = 4] [gap bytes]; e.g. 1024 1: the 1 GiB bucket, 3 GiB per launch
+int main(int argc, char** argv)
 {
-    n = 1ll << 26;
+    const int64_t mib = argc > 1 ? atoll(argv[1]) : 256;
+    S = argc > 2 ? atoi(argv[2]) : 4;
+    if (S < 1 || S > kMaxSets) S = 4;
+    n = mib << 18;
     n4 = n >> 2;
+    // argv[3] = gap: the three buckets of a set carved from one allocation with
+    // `gap` bytes between them (DRAM channel / bank placement), else three allocations
+    const int64_t gap = argc > 3 ? atoll(argv[3]) : -1;
     for (int s = 0; s < S; ++s) {
-        CHECK(hipMalloc(&A[s], n * 4));
-        CHECK(hipMalloc(&B[s], n * 4));
-        CHECK(hipMalloc(&O[s], n * 4));
+        if (gap >= 0) {
+            char* base = nullptr;
+            CHECK(hipMalloc(&base, 3 * n * 4 + 2 * gap));
+            A[s] = (float*)base;
+            B[s] = (float*)(base + n * 4 + gap);
+            O[s] = (float*)(base + 2 * (n * 4 + gap));
+        } else {
+            CHECK(hipMalloc(&A[s], n * 4));
+            CHECK(hipMalloc(&B[s], n * 4));
+            CHECK(hipMalloc(&O[s], n * 4));
+        }
         hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, A[s], n, 1u + 3 * s);
         hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, B[s], n, 2u + 3 * s);
     }
     CHECK(hipDeviceSynchronize());
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    for (int rep = 0; rep < 4; ++rep) {
-        g_hot = rep & 1;
-        product<512, 1, true, kStoreWT>(1);   // the product (write-through stores)
-        product<512, 1, true, kStoreNT>(1);   // round 1's product (nontemporal stores)
-        product<512, 2, true, kStoreWT>(1);
+    for (int rep = 0; rep < (S > 1 ? 4 : 2); ++rep) {
+        g_hot = S > 1 ? (rep & 1) : 0;
+        product<512, 2, true, kStoreWT>(1);   // the product since round 2 (write-through stores, 512 x 2)
+        product<512, 1, true, kStoreWT>(1);
+        product<512, 2, true, kStoreNT>(1);
         product<1024, 1, true, kStoreWT>(1);
-        policy2<512, 1, 2, 16>();
+        product<256, 2, true, kStoreWT>(1);
+        product<512, 4, true, kStoreWT>(1);
+        product<512, 2, false, kStoreWT>(1);
         refs<512>();
     }
     return 0;

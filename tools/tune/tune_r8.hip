@@ -48,8 +48,18 @@ __global__ __launch_bounds__(BLOCK) void k_sum8(SrcPtrs s, u32x4* __restrict__ o
 }
 
 static hipEvent_t e0, e1;
-static float* X[R];
+static float* XS[2][R];   // input sets (argv[1] = 2: launches alternate between them, cold)
+static float* OS[2];
+static int g_sets = 1, g_turn = 0;
+static float** X = XS[0];
 static float* O;
+// the next launch's set
+static void next_set()
+{
+    const int s = g_turn++ % g_sets;
+    X = XS[s];
+    O = OS[s];
+}
 static int64_t n, n4;
 
 template <class F>
@@ -79,25 +89,31 @@ static void product(int depth)
 {
     const int64_t tiles = n4 / ((int64_t)BLOCK * U);
     const int64_t grid = tiles / depth;
-    SrcPtrs p = {};
-    for (int r = 0; r < R; ++r) p.p[r] = X[r];
     Scale sc{25, nullptr, R};
     float ms = time_ms([&]() {
+        next_set();
+        SrcPtrs p = {};
+        for (int r = 0; r < R; ++r) p.p[r] = X[r];
         hipLaunchKernelGGL((k_stream_vec<F32, F32, R, NT, BLOCK, U, kStoreWT>), dim3((unsigned)grid), dim3(BLOCK), 0, 0,
                            p, O, n4, sc);
     });
     report("fused", BLOCK, U, grid, NT, ms);
 }
 
-int main()
+// usage: tune_r8 [sets = 1]; 2 alternates two input / output sets (4.5 GiB: cold)
+int main(int argc, char** argv)
 {
+    g_sets = argc > 1 && atoi(argv[1]) == 2 ? 2 : 1;
     n = 1ll << 26;
     n4 = n >> 2;
-    for (int r = 0; r < R; ++r) {
-        CHECK(hipMalloc(&X[r], n * 4));
-        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, X[r], n, 11u + r);
+    for (int s = 0; s < g_sets; ++s) {
+        for (int r = 0; r < R; ++r) {
+            CHECK(hipMalloc(&XS[s][r], n * 4));
+            hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, XS[s][r], n, 11u + r + 16 * s);
+        }
+        CHECK(hipMalloc(&OS[s], n * 4));
     }
-    CHECK(hipMalloc(&O, n * 4));
+    next_set();
     CHECK(hipDeviceSynchronize());
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
@@ -112,9 +128,10 @@ int main()
         product<1024, 1, true>(2);
         product<1024, 1, true>(4);
         product<512, 1, true>(4);
-        SrcPtrs p = {};
-        for (int r = 0; r < R; ++r) p.p[r] = X[r];
         float ms = time_ms([&]() {
+            next_set();
+            SrcPtrs p = {};
+            for (int r = 0; r < R; ++r) p.p[r] = X[r];
             hipLaunchKernelGGL((k_sum8<512>), dim3((unsigned)(n4 / 512)), dim3(512), 0, 0, p, (u32x4*)O, n4);
         });
         report("sum8_memory_ref", 512, 1, n4 / 512, 1, ms);
