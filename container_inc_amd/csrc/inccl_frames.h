@@ -24,7 +24,6 @@ typedef struct InccSwitchState {
     uint32_t *gen;       /* gen[0]: batches ingested so far.  A batch's claim tags it first-copy keys with
                           * g = gen[0] + 1 and stores g in gen[1]; its apply reads gen[1] and stores g in
                           * gen[0], so that a captured batch (hipGraph) tags every replay anew */
-    uint32_t *hdr;       /* batch call: [62][80 B] header images, then [62] ICRC header terms (claim writes them) */
     uint32_t slots;      /* power of two */
     int fan_in;
 } InccSwitchState;

@@ -8,27 +8,25 @@
 // A batch of frames (frame index = arrival order) goes through
 //   k_ingress_claim   a lane per frame: parse + validate, degree, and the
 //                     first copy of every (slot, port) by a batch-tagged atomicMin
-//   k_ingress_apply   persistent, a wave per two consecutive frames: classify
-//                     in the reference's serial order (nts.c:353-372), sum each
-//                     slot's counted arrivals into its aggregate (:361-363), the
-//                     arrival bitmap, the RETH keeper (:442), the recycle
-//                     (:235-242, :367) -- and in the batch call
-//                     (inccl_switch_batch) the broadcast frames of every PSN that
-//                     completes (:447-453, util.c:331-442) straight from the
-//                     aggregate in registers
-//   k_egress_fixed<F> / k_egress   (inccl_switch_egress) every output frame of a
-//                     batch from the state ingress left: COMPLETED broadcasts and
-//                     REPLAY resends (:353-356)
-//   k_replay          (inccl_switch_batch) the REPLAY resends, after apply
-// The ICRC is linear over GF(2), so every CRC here is a XOR of table lookups
-// (nibble planes, one SDWA byte select per lookup, three-way XORs) reduced over
-// the wave with DPP -- no serial byte loop.
+//   k_ingress_classify  a lane per frame: classify in the reference's serial
+//                     order (nts.c:353-372), the arrival bitmap, the RETH keeper
+//                     (:442), the recycle (:235-242, :367)
+//   k_ingress_sum     a wave per two consecutive frames: each completed or
+//                     absorbed PSN's counted arrivals summed into its aggregate
+//                     (:361-363)
+//   k_egress<F>       persistent, a wave per input frame: the COMPLETED
+//                     broadcasts (:447-453) and REPLAY resends (:353-356) from the
+//                     state ingress left, frames per util.c:331-442
+// inccl_switch_ingress runs the first three, inccl_switch_egress the last,
+// inccl_switch_batch all four.  The ICRC is linear over GF(2), so every CRC
+// here is a XOR of table lookups reduced over the wave with DPP -- no serial
+// byte loop.
 //
 // State on the GPU (slots = PSN ring size, power of two; the reference uses 16):
 //   agg[slots][256] int32        aggregator        (nts.c:55)
 //   arrival[slots][2] uint64     port bitmap + bit fan_in = "result known" (nts.c:59, :366),
 //                                tagged with the batch that wrote it, double-buffered by
-//                                batch parity (k_ingress_apply)
+//                                batch parity (k_ingress_classify)
 //   degree[slots] int32          arrivals incl. retransmits (nts.c:60, :351)
 //   reth[slots][fan_in][16 B]    RETH of each child's WRITE_FIRST (nts.c:57, :442)
 #include <hip/hip_runtime.h>
@@ -44,16 +42,12 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kWin = 1088;            // ICRC window: the longest message (1098-B frame from byte 10)
 constexpr int kFrameMax = 1152;
-constexpr int kSeg = 17;              // egress segment table rows (row j: Z_{16-j})
-constexpr int kEgressWaves = 8;       // 512-lane blocks, three per CU, persistent grid
 constexpr int kLanes = 256;           // int32 lanes per packet (nts.c:55)
 constexpr int kAuxNt = 2;   // buffer instruction cache policy: nt (streaming, not re-read)
 constexpr int kOobOffset = 0x7FFFFFF0;   // past any row: a buffer store there is dropped, a load returns 0
 
 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-
-__device__ uint32_t g_seg[kSeg][2][16];       // [byte j][nibble][value] = Z_{16-j}(T[value << 4 nibble]), T = util.c:141-150
 
 // frame bytes that read as 0xFF while the ICRC runs: 10-13 carry the CRC init
 // (the 4 x 0xFF prefix), the rest are the ICRC masks of util.c:266-270 (tos,
@@ -75,6 +69,10 @@ __device__ __forceinline__ uint32_t opaque_u32(uint32_t v)
     asm("" : "+v"(v));
     return v;
 }
+
+// a value nothing reads on the path where it is left so (no instruction sets it)
+__device__ __forceinline__ uint32_t unset() { return __builtin_nondeterministic_value(0u); }
+__device__ __forceinline__ u4 unset4() { return u4{unset(), unset(), unset(), unset()}; }
 
 // a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
@@ -317,16 +315,6 @@ __device__ __forceinline__ void payload16(const uint8_t* fr, uint32_t wf, int la
     }
 }
 
-// The 16 RETH bytes of the frame at `fr` (bytes 54-69, util.c:409-417) as four
-// little-endian words, wave-uniform (2-byte loads: the RETH is 2-byte aligned).
-__device__ __forceinline__ void reth_words(const uint8_t* fr, int lane, uint32_t (&r)[4])
-{
-    const uint16_t* h = reinterpret_cast<const uint16_t*>(fr + 54);
-    const uint32_t v = lane < 4 ? ((uint32_t)h[2 * lane] | ((uint32_t)h[2 * lane + 1] << 16)) : 0u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, i);
-}
-
 __device__ __forceinline__ void put16(uint8_t* p, uint32_t v)
 {
     p[0] = (uint8_t)(v >> 8);
@@ -396,51 +384,6 @@ __device__ uint32_t g_z1024[8][16];                   // Z_1024(value << 4 nibbl
 constexpr int kVarRows = 5 + kVarBytes;
 __device__ __forceinline__ constexpr int var_row(int wf, int k) { return wf ? 5 + k : k; }
 
-template <int kImgs>
-struct EgressLdsT {
-    uint32_t seg[kSeg][2][16];      // g_seg: rows 1..16 are a 16-byte segment's Z_{15-j}
-    uint32_t lane16[8][16][kWave];
-    uint32_t var[kVarRows][2][16];
-    uint32_t z1024[8][16];
-    uint32_t hcrc[kImgs];           // H_c for (child, RETH flag)
-};
-using EgressLds = EgressLdsT<2 * 31>;
-
-// What one egress wave needs from global memory for input frame f: loaded one
-// frame ahead of its use (k_egress), so these dependent loads overlap the
-// previous frame's build instead of stalling the wave.
-struct EgressIn {
-    int act, port;
-    uint32_t psn, slot;
-    uint32_t op;        // bytes 40-43 of the input frame across lanes (opcode: lane 2)
-    uint32_t reth;      // lane 4c+i: word i of child c's RETH (c < 16)
-    int32_t agg[4];     // words 4 lane .. 4 lane + 3 of the slot's aggregate: this lane's 16 payload bytes
-};
-
-// Branch-free, so that no wait is needed until egress_emit uses the values: the
-// RETH and aggregate words are loaded whatever the action (the slot index is in
-// range for any PSN).
-__device__ __forceinline__ EgressIn egress_fetch(const InccSwitchState& s, const uint8_t* __restrict__ in_frames,
-                                                 int64_t in_stride, const int32_t* __restrict__ ports,
-                                                 const int32_t* __restrict__ action,
-                                                 const uint32_t* __restrict__ psns, int64_t f, int lane)
-{
-    EgressIn e;
-    const int fan = s.fan_in;
-    e.act = action[f];
-    e.port = ports[f];
-    e.psn = psns[f];
-    // a lane-varying load stays in a VGPR, where a uniform one would be read into
-    // an SGPR at once -- and that wait would also drain the previous frame's stores
-    e.op = in_frames[f * in_stride + 40 + (lane & 3)];
-    e.slot = e.psn & (s.slots - 1);
-    e.reth = lane < 4 * fan ? s.reth[(size_t)e.slot * fan * 4 + lane] : 0u;
-    typedef int32_t i4 __attribute__((ext_vector_type(4)));
-    const i4 v = reinterpret_cast<const i4*>(s.agg + (size_t)e.slot * kLanes)[lane];   // one dwordx4 per lane
-    e.agg[0] = v.x; e.agg[1] = v.y; e.agg[2] = v.z; e.agg[3] = v.w;
-    return e;
-}
-
 __device__ __forceinline__ uint32_t wave_xor(uint32_t c)
 {
     // the DPP XOR-reduction of icrc_wave: lane 63 ends with the whole wave's XOR
@@ -453,482 +396,12 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t c)
     return (uint32_t)__builtin_amdgcn_readlane((int)c, 63);
 }
 
-// A 16-byte segment's raw CRC (bytes in memory order in a[0..3], little-endian
-// words) shifted by Z_{16 (63 - sh_lane)}.
-template <class L>
-__device__ __forceinline__ uint32_t seg16_crc(const L& t, const uint32_t (&a)[4], int sh_lane)
-{
-    // nibble planes, one SDWA byte select per lookup, XORs three at a time (icrc_wave)
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t lo = opaque_u32(a[k] & 0x0F0F0F0Fu), hi = opaque_u32((a[k] >> 4) & 0x0F0F0F0Fu);
-        uint32_t v[8];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            v[2 * b] = t.seg[4 * k + b + 1][0][(uint8_t)(lo >> (8 * b))];
-            v[2 * b + 1] = t.seg[4 * k + b + 1][1][(uint8_t)(hi >> (8 * b))];
-        }
-        c = xor3(xor3(xor3(c, v[0], v[1]), v[2], v[3]), xor3(v[4], v[5], v[6]), v[7]);
-    }
-    const uint32_t clo = opaque_u32(c & 0x0F0F0F0Fu), chi = opaque_u32((c >> 4) & 0x0F0F0F0Fu);
-    uint32_t v[8];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        v[2 * b] = t.lane16[2 * b][(uint8_t)(clo >> (8 * b))][sh_lane];
-        v[2 * b + 1] = t.lane16[2 * b + 1][(uint8_t)(chi >> (8 * b))][sh_lane];
-    }
-    return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
-}
-
+// a variable byte's ICRC term (k: 0 opcode, 1-4 PSN, 5-20 RETH), already shifted to the message end
 template <class L>
 __device__ __forceinline__ uint32_t var_crc(const L& t, int wf, int k, uint32_t b)
 {
     return t.var[var_row(wf, k)][0][b & 15u] ^ t.var[var_row(wf, k)][1][(b >> 4) & 15u];
 }
-
-// H_c for every (child, RETH flag) of the block's templates: quad q of wave w
-// takes pair i = 16 w + q.  The header part of the message (doff - 10 bytes:
-// 44, or 60 with RETH) is right-aligned in a 64-byte window (leading zeros do
-// not change a raw CRC); lane s of the quad takes window bytes 16 s .. 16 s + 15.
-template <class L>
-__device__ void header_crcs(L& t, const uint8_t (*himg)[kHdrImg], int fan, int w, int lane)
-{
-    const int i = w * 16 + (lane >> 2), s = lane & 3;
-    uint32_t c = 0;
-    if (i < 2 * fan) {
-        const int wf = i & 1;
-        const int hdr = wf ? 60 : 44;
-        uint32_t a[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int p = 16 * s + 4 * k + b - (64 - hdr);   // header byte; frame byte p + 10
-                uint32_t byte = 0;
-                if (p >= 0) {
-                    const int fo = p + 10;
-                    bool ff = fo < 14;
-#pragma unroll
-                    for (int m = 4; m < kNumMasked; ++m) ff = ff || fo == masked_pos(m);
-                    byte = ff ? 0xFFu : himg[i][fo];
-                }
-                v |= byte << (8 * b);
-            }
-            a[k] = v;
-        }
-        c = seg16_crc(t, a, 60 + s);
-    }
-    c ^= (uint32_t)__shfl_xor((int)c, 1, kWave);
-    c ^= (uint32_t)__shfl_xor((int)c, 2, kWave);
-    uint32_t r = 0;
-#pragma unroll
-    for (int n = 0; n < 8; ++n) r ^= t.z1024[n][(c >> (4 * n)) & 15u];   // past the 1024-byte payload
-    if (i < 2 * fan && s == 0) t.hcrc[i] = r;
-}
-
-// The CRC tables, the 2 * fan_in header images and their constant ICRC terms
-// into the block's LDS (ends with a block barrier).  Blocks of 8 waves: quad
-// q of wave w computes header term 16 w + q (2 * 31 at most).
-template <class L>
-__device__ void egress_setup(L& t, uint8_t (*himg)[kHdrImg], const InccFrameTemplate* __restrict__ tmpl, int fan, int w,
-                             int lane)
-{
-    for (int i = threadIdx.x; i < kSeg * 2 * 16; i += blockDim.x) (&t.seg[0][0][0])[i] = (&g_seg[0][0][0])[i];
-    for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) (&t.lane16[0][0][0])[i] = (&g_lane16[0][0][0])[i];
-    for (int i = threadIdx.x; i < kVarRows * 2 * 16; i += blockDim.x) (&t.var[0][0][0])[i] = (&g_var[0][0][0])[i];
-    for (int i = threadIdx.x; i < 8 * 16; i += blockDim.x) (&t.z1024[0][0])[i] = (&g_z1024[0][0])[i];
-    for (int i = threadIdx.x; i < 2 * fan; i += blockDim.x) build_header_image(himg[i], tmpl[i >> 1], (i & 1) != 0);
-    __syncthreads();
-    header_crcs(t, himg, fan, w, lane);
-    __syncthreads();
-}
-
-// Every output frame of input frame f (rows f * fan_in + c): all fan_in children
-// on COMPLETED (the broadcast, nts.c:368-371), the sender's child on REPLAY
-// (nts.c:353-356).
-//
-// The payload (htonl of the aggregate, util.c:403-405 / :419-421) goes from
-// registers straight to the output rows.  Lane l holds payload bytes
-// [16 l, 16 l + 16), i.e. frame bytes doff + 16 l ..; doff (54, or 70 with a
-// RETH) is 6 mod 16, so 16-byte output chunk doff/16 + 1 + l is lane l's bytes
-// 10..15 followed by lane l+1's bytes 0..9: one funnel shift with the next
-// lane's words, built once per input frame and stored once per child.  The
-// chunks before it (the header, with the payload's first 10 bytes) are staged
-// in a 80-byte LDS buffer per wave; lane 63 stores the last chunk: payload
-// bytes 1018-1023 and the ICRC.  No per-child pass over the payload touches LDS.
-__device__ void egress_emit(const InccSwitchState& s, const EgressIn& e, const uint8_t (*himg)[kHdrImg],
-                            uint8_t* __restrict__ out, int64_t out_stride, bool out16, int32_t* __restrict__ out_len,
-                            const EgressLds& t, uint8_t* hbuf, int64_t f, int lane)
-{
-    const int fan = s.fan_in;
-    const bool all = e.act == INCCL_SW_COMPLETED;
-    const bool one = e.act == INCCL_SW_REPLAY && e.port >= 0 && e.port < fan;
-    const uint32_t op = (uint32_t)__shfl((int)e.op, 2, kWave) & 0xFFu;
-    const int wf = is_write_first((uint8_t)op) ? 1 : 0;
-    const int doff = 54 + 16 * wf;
-    const int hchunks = doff / 16 + 1;         // 4 (or 5) chunks: header + payload bytes 0-9
-    const int total = doff + kLanes * 4 + 4;   // util.c:341-345
-    if (lane < fan) out_len[f * fan + lane] = (all || (one && lane == e.port)) ? total : 0;
-    if (!all && !one) return;
-    // this lane's 16 payload bytes (big-endian words, util.c:403-405), memory order
-    uint32_t a[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] = __builtin_bswap32((uint32_t)e.agg[k]);
-    uint32_t nx[3];                            // lane l+1's first 12 bytes
-#pragma unroll
-    for (int k = 0; k < 3; ++k) nx[k] = (uint32_t)__shfl_down((int)a[k], 1, kWave);
-    // output chunk hchunks + lane (lanes 0-62): bytes 10-15 of mine, 0-9 of the next lane's
-    const uint32_t pc0 = __builtin_amdgcn_alignbyte(a[3], a[2], 2);
-    const uint32_t pc1 = __builtin_amdgcn_alignbyte(nx[0], a[3], 2);
-    const uint32_t pc2 = __builtin_amdgcn_alignbyte(nx[1], nx[0], 2);
-    const uint32_t pc3 = __builtin_amdgcn_alignbyte(nx[2], nx[1], 2);
-    // the payload's first 10 bytes into the header buffer (doff = 2 mod 4), once
-    {
-        const uint32_t a0 = (uint32_t)__shfl((int)a[0], 0, kWave), a1 = (uint32_t)__shfl((int)a[1], 0, kWave);
-        const uint32_t a2 = (uint32_t)__shfl((int)a[2], 0, kWave);
-        if (lane == 0) *reinterpret_cast<uint16_t*>(hbuf + doff) = (uint16_t)a0;
-        if (lane == 1) *reinterpret_cast<uint32_t*>(hbuf + doff + 2) = __builtin_amdgcn_alignbyte(a1, a0, 2);
-        if (lane == 2) *reinterpret_cast<uint32_t*>(hbuf + doff + 6) = __builtin_amdgcn_alignbyte(a2, a1, 2);
-    }
-    // P ^ V_op,psn: the payload's contribution (this lane's segment) and, on
-    // lanes 0-4, the opcode and the four PSN bytes (util.c:378, :386)
-    const uint32_t pw = e.psn | 0x80000000u;
-    uint32_t pv = seg16_crc(t, a, lane);
-    if (lane < 5) {
-        const uint32_t b = lane == 0 ? op : (pw >> (8 * (4 - lane))) & 0xFFu;
-        pv ^= var_crc(t, wf, lane, b);
-    }
-    const uint32_t pc = wave_xor(pv);
-    const int c0 = all ? 0 : e.port, c1 = all ? fan : e.port + 1;
-    for (int c = c0; c < c1; ++c) {
-        // child c's RETH words (reth_keeper[slot][c], nts.c:442): lane 4c+i of
-        // e.reth for c < 16, else from memory
-        uint32_t r = 0, rk = 0;
-        if (wf) {
-            const int src = (4 * c + (lane & 3)) & (kWave - 1);
-            r = (uint32_t)__shfl((int)e.reth, src, kWave);
-            if (c >= kWave / 4) r = s.reth[((size_t)e.slot * fan + c) * 4 + (lane & 3)];
-            // lane k < 16: RETH byte k = byte k & 3 of word k >> 2
-            rk = (uint32_t)__shfl((int)r, lane >> 2, kWave);
-        }
-        uint32_t vr = 0;
-        if (wf) vr = wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
-        const uint32_t crc = ~(pc ^ t.hcrc[2 * c + wf] ^ vr);   // util.c:424-426
-        // header words 0-12 (bytes 0-51) from the image, opcode and PSN patched in
-        if (lane < 13) {
-            uint32_t hw = reinterpret_cast<const uint32_t*>(himg[2 * c + wf])[lane];
-            if (lane == 10) hw = (hw & 0xFF00FFFFu) | (op << 16);                            // byte 42
-            if (lane == 12) hw = (hw & 0x0000FFFFu) | ((pw >> 24) << 16) | (((pw >> 16) & 0xFFu) << 24);   // 50-51
-            reinterpret_cast<uint32_t*>(hbuf)[lane] = hw;
-        } else if (lane == 13) {                                                               // 52-53
-            *reinterpret_cast<uint16_t*>(hbuf + 52) = (uint16_t)(((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8));
-        }
-        if (wf) {                                                   // util.c:409-417: bytes 54-69
-            const int k = lane - 14;                                // lanes 14..18
-            const uint32_t rlo = (uint32_t)__shfl((int)r, (k - 1) & 3, kWave);
-            const uint32_t rhi = (uint32_t)__shfl((int)r, k & 3, kWave);
-            if (k == 0) *reinterpret_cast<uint16_t*>(hbuf + 54) = (uint16_t)rhi;
-            else if (k >= 1 && k <= 3) *reinterpret_cast<uint32_t*>(hbuf + 52 + 4 * k) = __builtin_amdgcn_alignbyte(rhi, rlo, 2);
-            else if (k == 4) *reinterpret_cast<uint16_t*>(hbuf + 68) = (uint16_t)(rlo >> 16);
-        }
-        __builtin_amdgcn_wave_barrier();
-        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-        uint8_t* o = out + (f * fan + c) * out_stride;
-        // header chunks (lanes 0 .. hchunks-1) from LDS
-        if (lane < hchunks) {
-            const u4 h = reinterpret_cast<const u4*>(hbuf)[lane];
-            if (out16) reinterpret_cast<u4*>(o)[lane] = h;
-            else {
-                uint32_t* o32 = reinterpret_cast<uint32_t*>(o) + 4 * lane;
-                o32[0] = h.x; o32[1] = h.y; o32[2] = h.z; o32[3] = h.w;
-            }
-        }
-        // payload chunks (lanes 0-62) and the last chunk (lane 63: payload bytes
-        // 1018-1023, the ICRC stored host order (LE), two bytes of zero padding)
-        const u4 v = lane < kWave - 1 ? u4{pc0, pc1, pc2, pc3}
-                                      : u4{pc0, (a[3] >> 16) | ((crc & 0xFFFFu) << 16), crc >> 16, 0u};
-        if (out16) reinterpret_cast<u4*>(o)[hchunks + lane] = v;
-        else {
-            uint32_t* o32 = reinterpret_cast<uint32_t*>(o) + 4 * (hchunks + lane);
-            o32[0] = v.x; o32[1] = v.y; o32[2] = v.z;
-            if (lane < kWave - 1) o32[3] = v.w;   // lane 63: stop at the frame's 4-byte-rounded end
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-// Egress (nts.c:365-372 / :447-453 broadcast, :353-356 / :435-438 replay;
-// frames per util.c:331-442): wave f builds input frame f's output frames.
-// Persistent: each wave walks its input frames with the next one's inputs in
-// flight.
-__global__ __launch_bounds__(kWave* kEgressWaves) void k_egress(InccSwitchState s, const uint8_t* __restrict__ in_frames,
-                                                               int64_t in_stride, int64_t count,
-                                                               const int32_t* __restrict__ ports,
-                                                               const int32_t* __restrict__ action,
-                                                               const uint32_t* __restrict__ psns,
-                                                               const InccFrameTemplate* __restrict__ tmpl,
-                                                               uint8_t* __restrict__ out, int64_t out_stride,
-                                                               int32_t* __restrict__ out_len)
-{
-    __shared__ EgressLds t;
-    __shared__ __attribute__((aligned(16))) uint8_t buf[kEgressWaves][80];   // per wave: header chunks
-    __shared__ __attribute__((aligned(16))) uint8_t himg[2 * 31][kHdrImg];
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
-    egress_setup(t, himg, tmpl, s.fan_in, w, lane);
-    const bool out16 = ((out_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
-    // Round r covers frames [r * step, (r + 1) * step); in round r this wave
-    // takes frame r * step + (wave + r) mod step.  Rotating the offset by one per
-    // round balances the waves: only every fan_in-th input frame of a PSN
-    // completes it and emits, and with a fixed offset (step is even) the waves of
-    // the other residues would idle while the rest built every output frame.
-    // Once a round's frame is past count, every later round's is too.
-    const int64_t step = (int64_t)gridDim.x * kEgressWaves;
-    int64_t rot = (int64_t)blockIdx.x * kEgressWaves + w, base = 0;
-    int64_t f = rot;
-    if (f >= count) return;
-    auto next = [&]() {
-        base += step;
-        rot = rot + 1 == step ? 0 : rot + 1;
-        return base + rot;
-    };
-    // two register sets used alternately (no copy between them: a copy would
-    // wait on every outstanding store of the previous frame too)
-    EgressIn a = egress_fetch(s, in_frames, in_stride, ports, action, psns, f, lane), b;
-    for (;;) {
-        int64_t fn = next();
-        if (fn < count) b = egress_fetch(s, in_frames, in_stride, ports, action, psns, fn, lane);
-        egress_emit(s, a, himg, out, out_stride, out16, out_len, t, buf[w], f, lane);
-        f = fn;
-        if (f >= count) break;
-        fn = next();
-        if (fn < count) a = egress_fetch(s, in_frames, in_stride, ports, action, psns, fn, lane);
-        egress_emit(s, b, himg, out, out_stride, out16, out_len, t, buf[w], f, lane);
-        f = fn;
-        if (f >= count) break;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Egress with a fixed fan-in (2, 3, 4 or 8): the same frames as k_egress, with
-// every frame issuing the same global-memory instructions.
-//
-// gfx9 counts loads and stores on one counter (vmcnt), retired in issue order.
-// The compiler waits for a loaded value with "vmcnt <= number of memory
-// instructions issued after it" -- and where paths that issue different numbers
-// of stores join (an absorbed frame returns early, a REPLAY emits one child, a
-// COMPLETED fan_in), it can only wait conservatively.  k_egress's ISA shows
-// vmcnt(0) at the top of every frame: it waits for the previous frame's stores
-// AND for the next frame's prefetch, which then hides nothing.  Here the
-// children loop is unrolled, the loads are unconditional (the last frame is
-// re-read past the end), all CRC work sits in branches without memory
-// instructions, and every store is predicated on the lane (exec mask), not
-// branched around.
-// ---------------------------------------------------------------------------
-
-// egress_fetch with the RETH words through a buffer resource (lanes past
-// 4 fan_in read out of range and get 0): no predicated load
-template <int kFan>
-__device__ __forceinline__ EgressIn egress_fetch_fixed(const InccSwitchState& s, const uint8_t* __restrict__ in_frames,
-                                                       int64_t in_stride, const int32_t* __restrict__ ports,
-                                                       const int32_t* __restrict__ action,
-                                                       const uint32_t* __restrict__ psns, int64_t f, int lane)
-{
-    EgressIn e;
-    e.act = action[f];
-    e.port = ports[f];
-    e.psn = psns[f];
-    e.op = in_frames[f * in_stride + 40 + (lane & 3)];
-    e.slot = e.psn & (s.slots - 1);
-    const __amdgpu_buffer_rsrc_t rr =
-        __builtin_amdgcn_make_buffer_rsrc(s.reth + (size_t)e.slot * kFan * 4, 0, 16 * kFan, 0x00020000);
-    e.reth = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rr, lane < 4 * kFan ? 4 * lane : kOobOffset, 0, 0);
-    // the slot's aggregate only for a frame that emits (COMPLETED / REPLAY): an
-    // absorbed frame's load goes past the buffer (no memory traffic)
-    typedef int32_t i4 __attribute__((ext_vector_type(4)));
-    const bool emits = e.act == INCCL_SW_COMPLETED || e.act == INCCL_SW_REPLAY;
-    const i4 v = (i4)__builtin_amdgcn_raw_buffer_load_b128(
-        __builtin_amdgcn_make_buffer_rsrc(s.agg + (size_t)e.slot * kLanes, 0, 1024, 0x00020000),
-        emits ? 16 * lane : kOobOffset, 0, 0);
-    e.agg[0] = v.x; e.agg[1] = v.y; e.agg[2] = v.z; e.agg[3] = v.w;
-    return e;
-}
-
-template <int kFan, bool kOut16, int kAux, class L>
-__device__ __forceinline__ void egress_emit_fixed(const EgressIn& e, const uint8_t (*himg)[kHdrImg],
-                                                  uint8_t* __restrict__ out, int64_t out_stride,
-                                                  int32_t* __restrict__ out_len, const L& t, int64_t f, int lane)
-{
-    const bool all = e.act == INCCL_SW_COMPLETED;
-    const bool one = e.act == INCCL_SW_REPLAY && e.port >= 0 && e.port < kFan;
-    const uint32_t op = (uint32_t)__shfl((int)e.op, 2, kWave) & 0xFFu;
-    const int wf = is_write_first((uint8_t)op) ? 1 : 0;
-    const int doff = 54 + 16 * wf;
-    const int hchunks = doff / 16 + 1;
-    const int total = doff + kLanes * 4 + 4;   // util.c:341-345
-    {
-        const __amdgpu_buffer_rsrc_t lr = __builtin_amdgcn_make_buffer_rsrc(out_len + f * kFan, 0, 4 * kFan, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32((all || (one && lane == e.port)) ? total : 0, lr,
-                                              lane < kFan ? 4 * lane : kOobOffset, 0, 0);
-    }
-    uint32_t a[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] = __builtin_bswap32((uint32_t)e.agg[k]);
-    uint32_t nx[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) nx[k] = (uint32_t)__shfl_down((int)a[k], 1, kWave);
-    const uint32_t pc0 = __builtin_amdgcn_alignbyte(a[3], a[2], 2);
-    const uint32_t pc1 = __builtin_amdgcn_alignbyte(nx[0], a[3], 2);
-    const uint32_t pc2 = __builtin_amdgcn_alignbyte(nx[1], nx[0], 2);
-    const uint32_t pc3 = __builtin_amdgcn_alignbyte(nx[2], nx[1], 2);
-    const uint32_t pw = e.psn | 0x80000000u;
-    // the payload's first 10 bytes (words 0-2 of lane 0, memory order): they
-    // end the header chunks
-    const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)a[0], 0);
-    const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)a[1], 0);
-    const uint32_t a2 = (uint32_t)__builtin_amdgcn_readlane((int)a[2], 0);
-    uint32_t pc = 0;
-    if (all || one) {
-        uint32_t pv = seg16_crc(t, a, lane);
-        if (lane < 5) {
-            const uint32_t b = lane == 0 ? op : (pw >> (8 * (4 - lane))) & 0xFFu;
-            pv ^= var_crc(t, wf, lane, b);
-        }
-        pc = wave_xor(pv);
-    }
-    const uint32_t psn_hi = (pw >> 24) | (((pw >> 16) & 0xFFu) << 8);    // frame bytes 50, 51 (util.c:386)
-    const uint32_t psn_lo = ((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8);   // bytes 52, 53
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int c = 0; c < kFan; ++c) {
-        const bool act_c = all || (one && c == e.port);
-        uint32_t crc = 0;
-        // child c's RETH words (reth_keeper[slot][c], nts.c:442), wave-uniform
-        const uint32_t R0 = (uint32_t)__builtin_amdgcn_readlane((int)e.reth, 4 * c);
-        const uint32_t R1 = (uint32_t)__builtin_amdgcn_readlane((int)e.reth, 4 * c + 1);
-        const uint32_t R2 = (uint32_t)__builtin_amdgcn_readlane((int)e.reth, 4 * c + 2);
-        const uint32_t R3 = (uint32_t)__builtin_amdgcn_readlane((int)e.reth, 4 * c + 3);
-        if (act_c) {
-            uint32_t vr = 0;
-            if (wf) {
-                // lane k < 16: RETH byte k = byte k & 3 of word k >> 2
-                const uint32_t rk = (lane & 8) ? ((lane & 4) ? R3 : R2) : ((lane & 4) ? R1 : R0);
-                vr = wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
-            }
-            crc = ~(pc ^ t.hcrc[2 * c + wf] ^ vr);   // util.c:424-426
-        }
-        // header chunk `lane` (< hchunks) built in registers: the template image's
-        // 16 bytes (util.c:348-388) with the opcode (byte 42), the PSN (50-53), the
-        // RETH (54-69, util.c:409-417) and the payload's first 10 bytes patched in
-        const u4 img = reinterpret_cast<const u4*>(himg[2 * c + wf])[lane < 5 ? lane : 0];
-        uint32_t h0 = img.x, h1 = img.y, h2 = img.z, h3 = img.w;
-        if (lane == 2) h2 = (h2 & 0xFF00FFFFu) | (op << 16);
-        if (lane == 3) {
-            const uint32_t b0 = wf ? R0 : a0, b1 = wf ? R1 : a1, b2 = wf ? R2 : a2;   // bytes 54-63
-            h0 = (h0 & 0xFFFFu) | (psn_hi << 16);
-            h1 = psn_lo | (b0 << 16);
-            h2 = __builtin_amdgcn_alignbyte(b1, b0, 2);
-            h3 = __builtin_amdgcn_alignbyte(b2, b1, 2);
-        }
-        if (lane == 4) {                                                // RETH frames only: bytes 64-79
-            h0 = __builtin_amdgcn_alignbyte(R3, R2, 2);
-            h1 = (R3 >> 16) | (a0 << 16);
-            h2 = __builtin_amdgcn_alignbyte(a1, a0, 2);
-            h3 = __builtin_amdgcn_alignbyte(a2, a1, 2);
-        }
-        const u4 h = {h0, h1, h2, h3};
-        const __amdgpu_buffer_rsrc_t orow =
-            __builtin_amdgcn_make_buffer_rsrc(out + (f * kFan + c) * out_stride, 0, (int)out_stride, 0x00020000);
-        const bool sh = act_c && lane < hchunks;
-        const u4 v = lane < kWave - 1 ? u4{pc0, pc1, pc2, pc3}
-                                      : u4{pc0, (a[3] >> 16) | ((crc & 0xFFFFu) << 16), crc >> 16, 0u};
-        const int ho = sh ? 16 * lane : kOobOffset, po = act_c ? 16 * (hchunks + lane) : kOobOffset;
-        if (kOut16) {
-            __builtin_amdgcn_raw_buffer_store_b128(h, orow, ho, 0, kAux);
-            __builtin_amdgcn_raw_buffer_store_b128(v, orow, po, 0, kAux);
-        } else {
-            __builtin_amdgcn_raw_buffer_store_b32(h.x, orow, ho, 0, kAux);
-            __builtin_amdgcn_raw_buffer_store_b32(h.y, orow, ho + 4, 0, kAux);
-            __builtin_amdgcn_raw_buffer_store_b32(h.z, orow, ho + 8, 0, kAux);
-            __builtin_amdgcn_raw_buffer_store_b32(h.w, orow, ho + 12, 0, kAux);
-            __builtin_amdgcn_raw_buffer_store_b32(v.x, orow, po, 0, kAux);
-            __builtin_amdgcn_raw_buffer_store_b32(v.y, orow, po + 4, 0, kAux);
-            __builtin_amdgcn_raw_buffer_store_b32(v.z, orow, po + 8, 0, kAux);
-            // lane 63 stops at the frame's 4-byte-rounded end
-            __builtin_amdgcn_raw_buffer_store_b32(v.w, orow, lane < kWave - 1 ? po + 12 : kOobOffset, 0, kAux);
-        }
-    }
-}
-
-template <int kFan, bool kOut16, int kEgW, int kAux>
-__device__ __forceinline__ void egress_fixed_body(InccSwitchState s,
-                                                                      const uint8_t* __restrict__ in_frames,
-                                                                      int64_t in_stride, int64_t count,
-                                                                      const int32_t* __restrict__ ports,
-                                                                      const int32_t* __restrict__ action,
-                                                                      const uint32_t* __restrict__ psns,
-                                                                      const InccFrameTemplate* __restrict__ tmpl,
-                                                                      uint8_t* __restrict__ out, int64_t out_stride,
-                                                                      int32_t* __restrict__ out_len)
-{
-    __shared__ EgressLdsT<2 * kFan> t;   // header terms and images for this fan-in only
-    __shared__ __attribute__((aligned(16))) uint8_t himg[2 * kFan][kHdrImg];
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
-    egress_setup(t, himg, tmpl, kFan, w, lane);
-    // the rotation of k_egress; frames past the end re-read the last one (a fixed
-    // instruction stream) and are never emitted
-    const int64_t step = (int64_t)gridDim.x * kEgW;
-    int64_t rot = (int64_t)blockIdx.x * kEgW + w, base = 0;
-    int64_t f = rot;
-    if (f >= count) return;
-    auto next = [&]() {
-        base += step;
-        rot = rot + 1 == step ? 0 : rot + 1;
-        return base + rot;
-    };
-    auto clamp = [&](int64_t x) { return x < count ? x : count - 1; };
-    EgressIn a = egress_fetch_fixed<kFan>(s, in_frames, in_stride, ports, action, psns, f, lane), b;
-    {
-        // as many stores as one frame emits, all dropped (a zero-size buffer): the
-        // loop is entered with the same memory-instruction history as from its
-        // back edge, so its first half's waits are not shortened by the merge
-        const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(out_len, 0, 0, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < (kOut16 ? 2 * kFan + 1 : 8 * kFan + 1); ++i)
-            __builtin_amdgcn_raw_buffer_store_b32(0, none, 4 * i, 0, 0);   // distinct offsets: kept
-    }
-    // two register sets used alternately, the fetch one frame ahead (two ahead,
-    // with three sets, measured the same: 73.9 vs 73.6-74.4 us)
-    for (;;) {
-        int64_t fn = next();
-        b = egress_fetch_fixed<kFan>(s, in_frames, in_stride, ports, action, psns, clamp(fn), lane);
-        egress_emit_fixed<kFan, kOut16, kAux>(a, himg, out, out_stride, out_len, t, f, lane);
-        f = fn;
-        if (f >= count) break;
-        fn = next();
-        a = egress_fetch_fixed<kFan>(s, in_frames, in_stride, ports, action, psns, clamp(fn), lane);
-        egress_emit_fixed<kFan, kOut16, kAux>(b, himg, out, out_stride, out_len, t, f, lane);
-        f = fn;
-        if (f >= count) break;
-    }
-}
-
-#define INCCL_EGRESS_FIXED_ARGS                                                                                      \
-    InccSwitchState s, const uint8_t *__restrict__ in_frames, int64_t in_stride, int64_t count,                      \
-        const int32_t *__restrict__ ports, const int32_t *__restrict__ action, const uint32_t *__restrict__ psns,    \
-        const InccFrameTemplate *__restrict__ tmpl, uint8_t *__restrict__ out, int64_t out_stride,                   \
-        int32_t *__restrict__ out_len
-// 8-wave blocks, three per CU = 24 waves: the measured optimum (profiles/r03/egress_waves/: 8 / 16 / 24 / 28
-// waves per CU = 95.5 / 74.8 / 71.0 / 82-83 us)
-template <int kFan, bool kOut16, int kAux = 0>
-__global__ __launch_bounds__(kWave * 8) void k_egress_fixed(INCCL_EGRESS_FIXED_ARGS)
-{
-    egress_fixed_body<kFan, kOut16, 8, kAux>(s, in_frames, in_stride, count, ports, action, psns, tmpl, out, out_stride,
-                                       out_len);
-}
-#undef INCCL_EGRESS_FIXED_ARGS
-
 
 // ---------------------------------------------------------------------------
 // Ingress (nts.c:303-483, root branch) reproduces the reference's one-frame-at-
@@ -966,57 +439,14 @@ __device__ __forceinline__ uint64_t first_key(uint32_t gen, int64_t f, bool wf)
     return ((uint64_t)(~gen) << 32) | ((uint64_t)(uint32_t)f << 1) | (wf ? 1u : 0u);
 }
 
-// The batch call's per-child header terms, once per batch (claim's first wave):
-// lane i < 2 fan_in builds child i/2's header image with RETH flag i&1
-// (util.c:348-388; opcode, PSN and RETH left zero) and its ICRC term H =
-// Z_1024(raw CRC of frame bytes 10 .. doff-1 with the CRC init and the masks as
-// 0xFF) (util.c:250-286), into s.hdr: 2 * 31 images of 80 bytes, then the terms.
-__device__ uint32_t g_tab[256];   // util.c:141-150
-
-__device__ void header_terms(const InccSwitchState& s, const InccFrameTemplate* __restrict__ tmpl, int lane,
-                             uint8_t (*img)[kHdrImg], uint32_t* tab)
-{
-    for (int i = lane; i < 256; i += kWave) tab[i] = g_tab[i];
-    const int fan = s.fan_in;
-    if (lane < 2 * fan) build_header_image(img[lane], tmpl[lane >> 1], (lane & 1) != 0);
-    __builtin_amdgcn_wave_barrier();
-    if (lane >= 2 * fan) return;
-    const int wf = lane & 1, hdr = wf ? 60 : 44;
-    uint32_t c = 0;
-    for (int p = 0; p < hdr; ++p) {
-        const int fo = p + 10;
-        bool ff = fo < 14;
-#pragma unroll
-        for (int m = 4; m < kNumMasked; ++m) ff = ff || fo == masked_pos(m);
-        const uint32_t b = ff ? 0xFFu : img[lane][fo];
-        c = (c >> 8) ^ tab[(c ^ b) & 0xFFu];
-    }
-    uint32_t r = 0;
-#pragma unroll
-    for (int n = 0; n < 8; ++n) r ^= g_z1024[n][(c >> (4 * n)) & 15u];   // past the 1024-byte payload
-    uint32_t* out = s.hdr + lane * (kHdrImg / 4);
-    const uint32_t* im = reinterpret_cast<const uint32_t*>(img[lane]);
-#pragma unroll
-    for (int i = 0; i < kHdrImg / 4; ++i) out[i] = im[i];
-    s.hdr[2 * 31 * (kHdrImg / 4) + lane] = r;
-}
-
 __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s, const uint8_t* __restrict__ frames,
                                                                int64_t stride, int64_t count,
                                                                const int32_t* __restrict__ ports,
                                                                int32_t* __restrict__ action,
-                                                               uint32_t* __restrict__ psn_out,
-                                                               const InccFrameTemplate* __restrict__ tmpl)
+                                                               uint32_t* __restrict__ psn_out)
 {
     const uint32_t g = *s.gen + 1u;   // this batch's generation
-    if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) s.gen[1] = g;
-        if (tmpl && threadIdx.x < kWave) {
-            __shared__ __attribute__((aligned(16))) uint8_t img[2 * 31][kHdrImg];
-            __shared__ uint32_t tab[256];
-            header_terms(s, tmpl, threadIdx.x, img, tab);
-        }
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) s.gen[1] = g;
     const int64_t f = (int64_t)blockIdx.x * kClaimBlock + threadIdx.x;
     if (f >= count) return;
     // rows are 4-byte aligned and at least 64 bytes: the header fields from four
@@ -1048,52 +478,17 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
 }
 
 // ---------------------------------------------------------------------------
-// Apply (after claim): one wave per two consecutive frames.
-//
-// A wave's work on its pair is three dependent memory round trips at most, and
-// in the common case -- every port of a PSN arriving as consecutive frames,
-// the reference's hosts posting one message each (api.c:293-327) -- two:
-//   1. the claim results (action | WRITE_FIRST | opcode, port, PSN) and, on
-//      16-byte aligned rows, both rows' payload chunks, loaded before anything
-//      is known about the frames (lane l the 16-byte chunk 3 + l of each row,
-//      lanes 0 and 1 also chunks 67 and 68: the payload starts 6 bytes into
-//      chunk 3 or 4, whichever the opcode says, so both placements are covered);
-//   2. the slot state, lane-parallel: lanes 32 k + p hold frame k's port p
-//      (first-copy key), lanes 32 k and 32 k + 1 its two tagged arrival words;
-//      in the batch call also the RETH keeper;
-//   3. only when needed: the slot's partial from earlier batches (its bitmap
-//      was not empty), the payload of a counted copy another wave holds.
-// The slot's counted arrivals of this batch are summed by ONE wave -- the one
-// holding the lowest counted port's first copy -- into the slot's partial with
-// plain loads and stores: the same wrap-around sum as one atomic add per
-// arrival (nts.c:361-363 / :443-445; integer addition commutes).  That wave
-// also writes the slot's new arrival bitmap, recycles slot psn + slots/2 when
-// the PSN completes (nts.c:235-242, :367: bitmap, degree and RETH keeper; the
-// 1 KiB of aggregator words are left, since a slot whose bitmap is empty is
-// summed from zero without reading them and nothing else reads a slot before
-// its next counted arrival rewrites them), and in the batch call builds the
-// completed PSN's fan_in broadcast frames (nts.c:447-453, util.c:331-442) from
-// the aggregate in its registers.
-//
-// The split call's apply runs one pair per wave in short-lived blocks (a wave
-// leaves once its stores are issued and the next starts).  The batch call's
-// runs persistent blocks that load the egress tables (57 KiB) once; its waves
-// walk the pairs.  The counters (profiles/r04/) put these kernels' VALU issue
-// near the limit, so the code spends instructions sparingly: lane-rotation
-// addresses are computed once, the WRITE_FIRST flag travels in the claim
-// result, the payload CRC takes byte lookups, and the header chunks are the
-// template image ORed with one patch per PSN.
+// Classify + sum (after claim).
 //
 // Arrival bitmap: every frame classifies against the bitmap as it was before
-// the batch, while the summing wave writes the new one in the same launch.  A
+// the batch, while the PSN's leader writes the new one in the same launch.  A
 // slot holds two 64-bit words {bits, tag = the batch that wrote them}; batch g
 // writes word g & 1 only, and reads the newer of the words whose tag is not g.
 // Whether a reader sees a word before or after batch g's store, it gets the
 // pre-batch bitmap (64-bit accesses are single-copy atomic).  The recycle
 // writes both words (no frame of the batch reads that slot).
 // ---------------------------------------------------------------------------
-constexpr int kApplyWaves = 8;    // split call: one pair per wave, 8-wave blocks
-constexpr int kEmitWaves = 16;    // batch call: persistent 16-wave blocks
+constexpr int kApplyWaves = 8;    // the sum kernel: one pair per wave, 8-wave blocks
 
 struct ApplyArgs {
     InccSwitchState s;
@@ -1102,9 +497,6 @@ struct ApplyArgs {
     const int32_t* ports;
     int32_t* action;
     const uint32_t* psns;
-    uint8_t* out;                    // batch call: the output rows and lengths
-    int64_t out_stride;
-    int32_t* out_len;
     int wide;                        // 16-byte aligned rows
 };
 
@@ -1115,12 +507,6 @@ __device__ __forceinline__ uint32_t arrival_before(uint64_t w0, uint64_t w1, uin
     const uint32_t t0 = (uint32_t)(w0 >> 32), t1 = (uint32_t)(w1 >> 32);
     const uint32_t d0 = t0 == g ? 0xFFFFFFFFu : g - t0, d1 = t1 == g ? 0xFFFFFFFFu : g - t1;
     return d0 <= d1 ? (uint32_t)w0 : (uint32_t)w1;
-}
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
-{
-    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
 }
 
 // A buffer resource over [base, base + bytes) whose fields are wave-uniform by
@@ -1141,23 +527,259 @@ __device__ __forceinline__ uint32_t from_next(uint32_t v, int next4)
     return (uint32_t)__builtin_amdgcn_ds_bpermute(next4, (int)v);
 }
 
-// The batch call's egress tables in LDS, once per persistent block.
+// ---------------------------------------------------------------------------
+// The classification in a lane-per-frame kernel, the payload sums in a kernel
+// whose waves need one dependent round trip (the per-pair kernel that did both
+// waited on three: claim results, then keys and arrival words, then payloads;
+// 50.2 us against 5.5 + 34.5 us per 131 072-frame batch, profiles/r04/).
+//
+// k_ingress_classify, a lane per frame, decides everything but the sums: each
+// lane reads its slot's two tagged arrival words and the first-copy keys of
+// all fan_in ports, classifies its frame (nts.c:353-372), writes
+// a counted WRITE_FIRST copy's RETH into the keeper (:442), and the lane of the
+// PSN's leader (the lowest counted port's first copy) writes the slot's new
+// arrival word and recycles slot psn + slots/2 on completion (:235-242, :367).
+// A leader's action word carries what its sum needs until k_ingress_sum
+// rewrites it: kActLeader, kActPartial (the slot held arrivals before the
+// batch), kActOwnWf (its own WRITE_FIRST flag), and for fan_in <= 8 the counted
+// ports (bits 16-23) and each counted copy's WRITE_FIRST flag (bits 24-31);
+// above 8 ports kActKeys: the sum takes the counted ports from the slot's two
+// arrival words and each other copy from its key.  Every other frame's action
+// is final here.
+//
+// k_ingress_sum, a wave per two consecutive frames: the rows' payload chunks
+// are loaded with the action words, before anything is known (lane l the
+// 16-byte chunk 3 + l of each row, lanes 0 and 1 also chunks 67 and 68: the
+// payload starts 6 bytes into chunk 3 or 4, whichever the opcode says, so both
+// placements are covered); a leader then sums its counted copies -- its own payload, the
+// other frame of the pair if that is a counted copy of the PSN (the common
+// case: a PSN's ports arriving as consecutive frames), else the copy the key
+// names -- and the slot's partial, stores the sum and its final action.
+// ---------------------------------------------------------------------------
+constexpr int kActLeader = 0x100, kActPartial = 0x200, kActOwnWf = 0x400, kActKeys = 0x800;
+constexpr int kClassifyBlock = 256;
+
+__global__ __launch_bounds__(kClassifyBlock) void k_ingress_classify(InccSwitchState s,
+                                                                     const uint8_t* __restrict__ frames,
+                                                                     int64_t stride, int64_t count,
+                                                                     const int32_t* __restrict__ ports,
+                                                                     int32_t* __restrict__ action,
+                                                                     const uint32_t* __restrict__ psns)
+{
+    const uint32_t g = s.gen[1];   // this batch's generation (claim's)
+    const int64_t f = (int64_t)blockIdx.x * kClassifyBlock + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) s.gen[0] = g;   // the next batch's claim adds one
+    if (f >= count) return;
+    const int act = action[f];
+    if (!(act & kActPending)) return;   // ACK, INVALID, IGNORED: final at claim
+    const int fan = s.fan_in, port = ports[f];
+    const uint32_t psn = psns[f], slot = psn & (s.slots - 1), wf = ((uint32_t)act >> 9) & 1u;
+    const uint32_t tag = ~g, result_bit = 1u << fan;
+    const uint32_t pre = arrival_before(s.arrival[2 * (size_t)slot], s.arrival[2 * (size_t)slot + 1], g);
+    // the PSN's ports: which count in this batch (first copy, not in before),
+    // when each counts (1 + frame index; 0 = before the batch, ~0 = not yet)
+    uint32_t cports = 0, wfs = 0, done = 0, mine = 0xFFFFFFFFu;
+    for (int p = 0; p < fan; ++p) {
+        const uint64_t key = s.first[(size_t)slot * fan + p];
+        const bool in_batch = (uint32_t)(key >> 32) == tag, before = (pre >> p) & 1u;
+        const uint32_t ef = (uint32_t)key >> 1;
+        done = max(done, before ? 0u : (in_batch ? ef + 1u : 0xFFFFFFFFu));
+        if (in_batch && !before) {
+            cports |= 1u << p;
+            wfs |= ((uint32_t)key & 1u) << p;
+        }
+        if (p == port) mine = in_batch ? ef : 0xFFFFFFFFu;
+    }
+    const uint32_t fi = (uint32_t)f;
+    const bool counted = !((pre >> port) & 1u) && mine == fi;   // nts.c:359-363
+    int fin;
+    if (counted) {
+        fin = done == fi + 1u ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
+        if (wf) {   // the RETH into the keeper (nts.c:442): frame bytes 54-69, 4-byte aligned row
+            const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + f * stride);
+            const uint32_t w13 = fw[13], w14 = fw[14], w15 = fw[15], w16 = fw[16], w17 = fw[17];
+            uint32_t* kp = s.reth + ((size_t)slot * fan + port) * 4;
+            kp[0] = __builtin_amdgcn_alignbyte(w14, w13, 2);
+            kp[1] = __builtin_amdgcn_alignbyte(w15, w14, 2);
+            kp[2] = __builtin_amdgcn_alignbyte(w16, w15, 2);
+            kp[3] = __builtin_amdgcn_alignbyte(w17, w16, 2);
+        }
+    } else {   // retransmit: nts.c:353-357
+        const bool done_before = (pre & result_bit) != 0;
+        const bool done_earlier = done != 0u && done != 0xFFFFFFFFu && done - 1u < fi;
+        fin = (done_before || done_earlier) ? INCCL_SW_REPLAY : INCCL_SW_DROPPED;
+    }
+    if (!(counted && port == __builtin_ctz(cports))) {
+        action[f] = fin;
+        return;
+    }
+    // the leader: the slot's new arrival word, the recycle, the sum's orders
+    const bool complete = done != 0xFFFFFFFFu;
+    s.arrival[2 * (size_t)slot + (g & 1u)] =
+        ((uint64_t)g << 32) | (pre | cports | (complete ? result_bit : 0u));   // nts.c:359, :366
+    if (complete) {   // clear_state_data(psn + WINDOW), nts.c:235-242, :367
+        const uint32_t rs = (psn + (s.slots >> 1)) & (s.slots - 1);
+        for (int i = 0; i < fan * 4; ++i) s.reth[(size_t)rs * fan * 4 + i] = 0u;
+        s.arrival[2 * (size_t)rs] = (uint64_t)g << 32;
+        s.arrival[2 * (size_t)rs + 1] = (uint64_t)g << 32;
+        s.degree[rs] = 0;
+    }
+    action[f] = fin | kActLeader | (pre ? kActPartial : 0) | (wf ? kActOwnWf : 0) |
+                (fan <= 8 ? (int)((cports << 16) | (wfs << 24)) : kActKeys);
+}
+
+// the sum kernel: one pair per wave, short-lived blocks
+__global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A, const int32_t* __restrict__ act_in,
+                                                                    const int32_t* __restrict__ ports_in,
+                                                                    const uint32_t* __restrict__ psns_in)
+{
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    const int next4 = ((lane + 1) & (kWave - 1)) * 4;
+    const InccSwitchState& s = A.s;
+    const int fan = s.fan_in;
+    const int64_t count = A.count, stride = A.stride, pidx = (int64_t)blockIdx.x * kApplyWaves + w;
+    const bool have = 2 * pidx < count;
+    const int64_t f0 = have ? 2 * pidx : 0;
+    const bool in1 = have && f0 + 1 < count;
+    const int64_t f1 = in1 ? f0 + 1 : f0;
+    // one round trip: both rows' payload chunks (lane l chunk 3 + l; lanes 0, 1
+    // chunks 67, 68) with the action words (scalar)
+    u4 x[2] = {}, e[2] = {};
+    if (A.wide) {
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(A.frames + f0 * stride, have ? (in1 ? 2 : 1) * stride : 0);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int rb = k * (int)stride;
+            x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, rb + 48 + 16 * lane, 0, 0);
+            e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane < 2 ? rb + 1072 + 16 * lane : kOobOffset, 0, 0);
+        }
+    }
+    int act[2];
+    act[0] = have ? act_in[f0] : 0;
+    act[1] = in1 ? act_in[f1] : 0;
+    if (!((act[0] | act[1]) & kActLeader)) return;
+    const int port[2] = {ports_in[f0], ports_in[f1]};
+    const uint32_t psn[2] = {psns_in[f0], psns_in[f1]};
+    // payload words 4 lane .. 4 lane + 3 of pair frame k (payload at byte 54 + 16 wf)
+    auto payload_of = [&](int k, uint32_t wf, uint32_t (&P)[4]) {
+        if (A.wide) {
+            const bool last = lane == kWave - 1;
+            uint32_t y0 = from_next(x[k].x, next4), y1 = from_next(x[k].y, next4);
+            y0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 0) : y0;
+            y1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 0) : y1;
+            if (wf) {
+                uint32_t y2 = from_next(x[k].z, next4), y3 = from_next(x[k].w, next4);
+                uint32_t z0 = from_next(y0, next4), z1 = from_next(y1, next4);
+                y2 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].z, 0) : y2;
+                y3 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].w, 0) : y3;
+                z0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 1) : z0;
+                z1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 1) : z1;
+                payload_from_chunks(u4{y0, y1, y2, y3}, z0, z1, P);
+            } else {
+                payload_from_chunks(x[k], y0, y1, P);
+            }
+        } else {
+            payload16(A.frames + (f0 + k) * stride, wf, lane, false, P);
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (!(act[k] & kActLeader)) continue;
+        const int o = k ^ 1;
+        const uint32_t slot = psn[k] & (s.slots - 1);
+        const bool keys = (act[k] & kActKeys) != 0;
+        uint32_t cports, wfs;
+        if (!keys) {
+            cports = ((uint32_t)act[k] >> 16) & 0xFFu;
+            wfs = (uint32_t)act[k] >> 24;
+        } else {   // fan_in > 8: the counted ports are the new arrival word's bits that the old one lacks
+            const uint32_t g = s.gen[0];
+            const uint64_t w0 = s.arrival[2 * (size_t)slot], w1 = s.arrival[2 * (size_t)slot + 1];
+            const uint32_t now = (uint32_t)((uint32_t)(w0 >> 32) == g ? w0 : w1);
+            cports = now & ~arrival_before(w0, w1, g) & ((1u << fan) - 1u);
+            wfs = 0;   // unused: every port but the leader's own is read through its key
+        }
+        const uint32_t own_wf = (act[k] & kActOwnWf) ? 1u : 0u;
+        u4 acc = {0u, 0u, 0u, 0u};
+        if (act[k] & kActPartial) acc = reinterpret_cast<const u4*>(s.agg + (size_t)slot * kLanes)[lane];
+        for (uint32_t m = cports; m; m &= m - 1) {
+            const int p = __builtin_ctz(m);
+            uint32_t q[4];
+            const int fo = act[o] & 0xFF;
+            if (p == port[k]) {
+                payload_of(k, own_wf, q);
+            } else if (!keys && (k == 0 ? in1 : true) && psn[o] == psn[k] && port[o] == p &&
+                       (fo == INCCL_SW_ABSORBED || fo == INCCL_SW_COMPLETED)) {
+                payload_of(o, (wfs >> p) & 1u, q);
+            } else {
+                const uint64_t key = s.first[(size_t)slot * fan + p];
+                payload16(A.frames + (int64_t)((uint32_t)key >> 1) * stride, (uint32_t)key & 1u, lane, A.wide != 0, q);
+            }
+            acc.x += q[0];
+            acc.y += q[1];
+            acc.z += q[2];
+            acc.w += q[3];
+        }
+        __builtin_nontemporal_store(acc, reinterpret_cast<u4*>(s.agg + (size_t)slot * kLanes) + lane);
+        if (lane == 0) A.action[f0 + k] = act[k] & 0xFF;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Egress (nts.c:365-372 / :447-453 broadcast, :353-356 / :435-438 replay;
+// frames per util.c:331-442): every output frame of input frame f, rows
+// f * fan_in + c -- all fan_in children on COMPLETED, the sender's child on
+// REPLAY -- from the slot's aggregate and RETH keeper as ingress left them.
+//
+// Persistent 16-wave blocks, two per CU: each block loads the CRC tables into
+// LDS and builds the 2 fan_in header images and their ICRC terms H_c once.  A
+// wave then walks input frames, one per iteration, with the next frame's
+// aggregate and keeper and the claim results of the frame after that in
+// flight.  Loads and stores retire in order on one counter (vmcnt), so that
+// the compiler can wait for a prefetched load without also waiting for the
+// stores issued after it, every iteration issues the same memory instructions:
+// the children loop unrolled for a fixed fan-in (2, 3, 4, 8), every load and
+// store unconditional -- a frame that emits nothing, or a child that gets no
+// frame, is given a zero-size buffer (its loads return 0, its stores are
+// dropped, neither reaches memory) -- and all CRC work in branches without
+// memory instructions.  Two register sets take alternate frames (a copy
+// between them would wait for the load in flight).
+//
+// Round r of a wave covers frames [r step, (r + 1) step), step = the grid's
+// waves; in round r wave v takes frame r step + (v + r) mod step.  Rotating
+// by one per round balances the waves: only every fan_in-th frame of a PSN
+// completes it, and with a fixed offset (step is even) the waves of the other
+// residues would idle while the rest built every output frame.
+//
+// The payload goes from registers to the rows: lane l holds payload bytes
+// [16 l, 16 l + 16) (htonl of the aggregate, util.c:403-405 / :419-421), frame
+// bytes doff + 16 l ..; doff (54, or 70 with a RETH) is 6 mod 16, so 16-byte
+// output chunk doff / 16 + 1 + l is lane l's bytes 10-15 then lane l + 1's
+// bytes 0-9: built once per input frame, stored once per child.  Lane 63's
+// chunk ends the frame: payload bytes 1018-1023, the ICRC (host order), two
+// bytes of zero padding.  The header chunks are the child's template image
+// (LDS) ORed with one patch per input frame (opcode, PSN, the payload's first
+// 10 bytes) and, with a RETH, the child's 16 RETH bytes.  The ICRC is
+// ~(P ^ V_op,psn ^ H_c ^ V_reth,c) (above): one payload reduction per input
+// frame, one RETH reduction per RETH child.
+// ---------------------------------------------------------------------------
+constexpr int kEgressWaves = 16;
+
 __device__ uint32_t g_segb[16][256];   // [byte j of a 16-byte segment][value] = Z_{15-j}(T[value])
 
-struct EmitLds {
+struct EgressLds {
     uint32_t segb[16][256];
     uint32_t lane16[8][16][kWave];
     uint32_t var[kVarRows][2][16];
-    uint32_t hcrc[2 * 31];
+    uint32_t z1024[8][16];
+    uint32_t hcrc[2 * 31];                                  // H_c for (child, RETH flag)
     __attribute__((aligned(16))) uint8_t img[2 * 31][kHdrImg];
 };
 
-// P ^ V_op,psn, in every lane: the payload's contribution to the ICRC (lane l's
-// 16 bytes a[] -- memory order, little-endian words -- as 16 byte lookups, then
-// shifted past the segments after it, Z_{16 (63 - l)}, as 8 nibble lookups)
-// plus the opcode and PSN bytes' (lanes 0-4, already shifted to the message
-// end), XORed over the wave.
-__device__ __forceinline__ uint32_t payload_term(const EmitLds& t, const uint32_t (&a)[4], uint32_t var, int lane)
+// The raw CRC of 16 bytes (a[]: memory order, little-endian words) as 16 byte
+// lookups, shifted past the (63 - sh_lane) 16-byte segments after it
+// (Z_{16 (63 - sh_lane)}) as 8 nibble lookups.
+__device__ __forceinline__ uint32_t seg16(const EgressLds& t, const uint32_t (&a)[4], int sh_lane)
 {
     uint32_t c = 0;
 #pragma unroll
@@ -1171,97 +793,245 @@ __device__ __forceinline__ uint32_t payload_term(const EmitLds& t, const uint32_
     uint32_t s[8];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-        s[2 * b] = t.lane16[2 * b][(uint8_t)(clo >> (8 * b))][lane];
-        s[2 * b + 1] = t.lane16[2 * b + 1][(uint8_t)(chi >> (8 * b))][lane];
+        s[2 * b] = t.lane16[2 * b][(uint8_t)(clo >> (8 * b))][sh_lane];
+        s[2 * b + 1] = t.lane16[2 * b + 1][(uint8_t)(chi >> (8 * b))][sh_lane];
     }
-    return wave_xor(xor3(xor3(s[0], s[1], s[2]), xor3(s[3], s[4], s[5]), xor3(s[6], s[7], var)));
+    return xor3(xor3(s[0], s[1], s[2]), xor3(s[3], s[4], s[5]), s[6]) ^ s[7];
 }
 
-// per-lane constants of a wave
-struct LaneK {
-    int lane, next4;   // lane, 4 * (lane + 1 mod 64): ds_bpermute address of the next lane
-};
-
-// What apply knows about one frame of its pair.
-struct FrameK {
-    int act, port;
-    uint32_t psn, slot, op, wf;
-    bool live;
-};
-
-// The batch call's broadcast of one completed PSN: fan_in frames into rows
-// fd * fan_in + c, from the aggregate acc (this lane's four words).
-template <bool kOut16, class RethOf>
-__device__ __forceinline__ void emit_broadcast(const ApplyArgs& A, const EmitLds& t, const LaneK& L, const u4& acc,
-                                               int64_t fd, uint32_t opd, uint32_t wfd, uint32_t psn, int fan,
-                                               RethOf reth_of)
+// The tables, the 2 fan_in header images and their ICRC terms H_c into the
+// block's LDS (ends with a block barrier).  H_c: quad i of the block takes
+// image i; the header part of the ICRC message (doff - 10 bytes: 44, or 60
+// with a RETH) is right-aligned in a 64-byte window (leading zeros do not
+// change a raw CRC), lane q of the quad takes window bytes 16 q .. 16 q + 15,
+// and the quad's XOR is shifted past the 1024-byte payload.
+__device__ void egress_setup(EgressLds& t, const InccFrameTemplate* __restrict__ tmpl, int fan)
 {
-    const int lane = L.lane;
-    uint32_t a[4];   // this lane's 16 payload bytes, big-endian (util.c:403-405), memory order
-    a[0] = __builtin_bswap32(acc.x);
-    a[1] = __builtin_bswap32(acc.y);
-    a[2] = __builtin_bswap32(acc.z);
-    a[3] = __builtin_bswap32(acc.w);
-    const uint32_t pw = psn | 0x80000000u;
-    // the opcode and PSN bytes' terms (util.c:378, :386), lanes 0-4
-    const uint32_t vb = lane == 0 ? opd : (pw >> (8 * (4 - lane))) & 0xFFu;
-    const uint32_t var = lane < 5 ? var_crc(t, (int)wfd, lane, vb) : 0u;
-    const uint32_t pc = payload_term(t, a, var, lane);
-    // payload chunk hchunks + l: bytes 10-15 of lane l, 0-9 of lane l + 1; the
-    // last one (lane 63): bytes 1018-1023, the ICRC (host order), zero padding
-    const uint32_t n0 = from_next(a[0], L.next4), n1 = from_next(a[1], L.next4), n2 = from_next(a[2], L.next4);
-    const bool last = lane == kWave - 1;
-    const uint32_t p0 = __builtin_amdgcn_alignbyte(a[3], a[2], 2);
-    const uint32_t p1 = __builtin_amdgcn_alignbyte(n0, a[3], 2);
-    const uint32_t p2 = __builtin_amdgcn_alignbyte(n1, n0, 2);
-    const uint32_t p3 = last ? 0u : __builtin_amdgcn_alignbyte(n2, n1, 2);
-    const uint32_t t63 = a[3] >> 16;
-    // the header chunks' PSN-wide patch over the template images (which hold
-    // zeros there): opcode (byte 42), PSN (50-53), and the payload's first 10
-    // bytes after the BTH (no RETH) or after the RETH (lane 4's chunk)
-    const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)a[0], 0);
-    const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)a[1], 0);
-    const uint32_t a2 = (uint32_t)__builtin_amdgcn_readlane((int)a[2], 0);
-    const uint32_t psn_hi = (pw >> 24) | (((pw >> 16) & 0xFFu) << 8);    // frame bytes 50, 51
-    const uint32_t psn_lo = ((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8);   // bytes 52, 53
-    const uint32_t q1 = a0 << 16, q2 = __builtin_amdgcn_alignbyte(a1, a0, 2), q3 = __builtin_amdgcn_alignbyte(a2, a1, 2);
-    const int pl = wfd ? 4 : 3;   // the lane whose chunk ends with the payload's first 10 bytes
-    u4 patch;
-    patch.x = lane == 3 ? psn_hi << 16 : 0u;
-    patch.y = lane == 3 ? psn_lo : 0u;
-    patch.y |= lane == pl ? q1 : 0u;
-    patch.z = lane == pl ? q2 : (lane == 2 ? opd << 16 : 0u);
-    patch.w = lane == pl ? q3 : 0u;
-    const int hchunks = 4 + (int)wfd;
-    const int ho = lane < hchunks ? 16 * lane : kOobOffset, po = 16 * (hchunks + lane);
-    for (int c = 0; c < fan; ++c) {
-        u4 h = reinterpret_cast<const u4*>(t.img[2 * c + wfd])[lane < 5 ? lane : 0];
-        h.x |= patch.x;
-        h.y |= patch.y;
-        h.z |= patch.z;
-        h.w |= patch.w;
-        uint32_t crc = pc ^ t.hcrc[2 * c + wfd];
-        if (wfd) {
-            // child c's RETH (util.c:409-417): bytes 54-69, lane 3's chunk from
-            // byte 6 on and lane 4's first 6 bytes; its ICRC term, lanes 0-15
-            uint32_t R[4];
-            reth_of(c, R);
-            const uint32_t R0 = R[0], R1 = R[1], R2 = R[2], R3 = R[3];
-            if (lane == 3) {
-                h.y |= R0 << 16;
-                h.z = __builtin_amdgcn_alignbyte(R1, R0, 2);
-                h.w = __builtin_amdgcn_alignbyte(R2, R1, 2);
+    for (int i = threadIdx.x; i < 16 * 256; i += blockDim.x) (&t.segb[0][0])[i] = (&g_segb[0][0])[i];
+    for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) (&t.lane16[0][0][0])[i] = (&g_lane16[0][0][0])[i];
+    for (int i = threadIdx.x; i < kVarRows * 2 * 16; i += blockDim.x) (&t.var[0][0][0])[i] = (&g_var[0][0][0])[i];
+    for (int i = threadIdx.x; i < 8 * 16; i += blockDim.x) (&t.z1024[0][0])[i] = (&g_z1024[0][0])[i];
+    for (int i = threadIdx.x; i < 2 * fan; i += blockDim.x) build_header_image(t.img[i], tmpl[i >> 1], (i & 1) != 0);
+    __syncthreads();
+    const int i = threadIdx.x >> 2, q = threadIdx.x & 3;
+    uint32_t c = 0;
+    if (i < 2 * fan) {
+        const int hdr = (i & 1) ? 60 : 44;
+        uint32_t a[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int p = 16 * q + 4 * k + b - (64 - hdr);   // header byte; frame byte p + 10
+                uint32_t byte = 0;
+                if (p >= 0) {
+                    const int fo = p + 10;
+                    bool ff = fo < 14;                             // the 4 x 0xFF CRC prefix (util.c:262)
+#pragma unroll
+                    for (int m = 4; m < kNumMasked; ++m) ff = ff || fo == masked_pos(m);   // util.c:266-270
+                    byte = ff ? 0xFFu : t.img[i][fo];
+                }
+                v |= byte << (8 * b);
             }
-            if (lane == 4) {
-                h.x = __builtin_amdgcn_alignbyte(R3, R2, 2);
-                h.y |= R3 >> 16;
-            }
-            const uint32_t rk = (lane & 8) ? ((lane & 4) ? R3 : R2) : ((lane & 4) ? R1 : R0);
-            crc ^= wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
+            a[k] = v;
         }
-        crc = ~crc;   // util.c:424-426
-        const u4 v = {p0, last ? t63 | (crc << 16) : p1, last ? crc >> 16 : p2, p3};
-        const __amdgpu_buffer_rsrc_t orow = uniform_rsrc(A.out + (fd * fan + c) * A.out_stride, A.out_stride);
+        c = seg16(t, a, kWave - 4 + q);
+    }
+    c ^= (uint32_t)__shfl_xor((int)c, 1, kWave);
+    c ^= (uint32_t)__shfl_xor((int)c, 2, kWave);
+    uint32_t r = 0;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) r ^= t.z1024[n][(c >> (4 * n)) & 15u];
+    if (i < 2 * fan && q == 0) t.hcrc[i] = r;
+    __syncthreads();
+}
+
+// What egress reads and writes (the kernel argument; 32-bit frame indices:
+// count < 2^31).
+struct EgressArgs {
+    const int32_t* agg;
+    const uint32_t* reth;
+    const uint8_t* frames;
+    const int32_t* ports;
+    const int32_t* action;
+    const uint32_t* psns;
+    const InccFrameTemplate* tmpl;
+    uint8_t* out;
+    int32_t* out_len;
+    uint32_t stride, out_stride, count, smask;
+    int fan;
+};
+
+// One input frame as an egress wave knows it: three wave-uniform words (two
+// frames are in flight at a time, so they are packed)
+struct EgressF {
+    uint32_t f, psn;
+    uint32_t bits;   // opcode | WRITE_FIRST << 8 | in << 9 | all << 10 | one << 11 | port << 16
+    __device__ uint32_t op() const { return bits & 0xFFu; }
+    __device__ uint32_t wf() const { return (bits >> 8) & 1u; }
+    __device__ bool in() const { return (bits >> 9) & 1u; }     // f < count
+    __device__ bool all() const { return (bits >> 10) & 1u; }   // COMPLETED: every child
+    __device__ bool one() const { return (bits >> 11) & 1u; }   // REPLAY: child port()
+    __device__ uint32_t port() const { return bits >> 16; }
+};
+
+// Lanes 0-3 load frame f's action, port, PSN and header dword 10 (opcode: byte
+// 42), lanes 4-63 again the same four: one vector load, counted on vmcnt with
+// the rest.  Each lane's array base and element size are set once (MetaLane),
+// so the address is one multiply-add.  Past the end: the last frame's (unused).
+struct MetaLane {
+    const uint8_t* base;
+    uint32_t scale;
+};
+
+__device__ __forceinline__ MetaLane meta_lane(const EgressArgs& A, int lane)
+{
+    MetaLane m;
+    const int k = lane & 3;
+    m.base = k == 0   ? reinterpret_cast<const uint8_t*>(A.action)
+             : k == 1 ? reinterpret_cast<const uint8_t*>(A.ports)
+             : k == 2 ? reinterpret_cast<const uint8_t*>(A.psns)
+                      : A.frames + 40;
+    m.scale = k == 3 ? A.stride : 4u;
+    return m;
+}
+
+__device__ __forceinline__ uint32_t egress_meta(const EgressArgs& A, const MetaLane& ml, uint32_t f)
+{
+    const uint32_t fc = f < A.count ? f : A.count - 1;
+    return *reinterpret_cast<const uint32_t*>(ml.base + (size_t)fc * ml.scale);
+}
+
+__device__ __forceinline__ EgressF egress_decode(const EgressArgs& A, uint32_t m, uint32_t f)
+{
+    EgressF e;
+    e.f = f;
+    const int act = __builtin_amdgcn_readlane((int)m, 0);
+    const uint32_t port = (uint32_t)__builtin_amdgcn_readlane((int)m, 1);
+    e.psn = (uint32_t)__builtin_amdgcn_readlane((int)m, 2);
+    const uint32_t op = ((uint32_t)__builtin_amdgcn_readlane((int)m, 3) >> 16) & 0xFFu;
+    const bool in = f < A.count;
+    const bool one = in && act == INCCL_SW_REPLAY && port < (uint32_t)A.fan;
+    e.bits = op | (is_write_first((uint8_t)op) ? 1u << 8 : 0u) | (in ? 1u << 9 : 0u) |
+             (in && act == INCCL_SW_COMPLETED ? 1u << 10 : 0u) | (one ? 1u << 11 : 0u) | ((port & 0xFFFFu) << 16);
+    return e;
+}
+
+// the slot's aggregate (this lane's four words) and RETH keeper (lane 4 c + j:
+// word j of child c's, c < 16); nothing for a frame that emits nothing
+__device__ __forceinline__ void egress_load(const EgressArgs& A, const EgressF& e, int lane, u4& acc, uint32_t& keep)
+{
+    const bool em = e.all() || e.one();
+    const uint32_t slot = e.psn & A.smask;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<int32_t*>(A.agg) + (size_t)slot * kLanes, 0, em ? kLanes * 4 : 0, 0x00020000);
+    acc = __builtin_amdgcn_raw_buffer_load_b128(ra, 16 * lane, 0, 0);
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(A.reth) + (size_t)slot * A.fan * 4, 0, em && e.wf() ? 16 * A.fan : 0, 0x00020000);
+    keep = __builtin_amdgcn_raw_buffer_load_b32(rk, 4 * lane, 0, 0);
+}
+
+// Frame e's output rows and their lengths.
+template <int kFan, bool kOut16, int kX = 0>
+__device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs& A, const EgressF& e, const u4& acc,
+                                            uint32_t keep, int lane)
+{
+    const int fan = kFan ? kFan : A.fan;
+    const uint32_t wf = e.wf(), op = e.op(), port = e.port();
+    const bool all = e.all(), one = e.one();
+    const bool em_any = all || one;
+    if (!(kX & 8)) {   // row lengths, lanes c < fan_in (util.c:341-345)
+        const int total = 54 + 16 * (int)wf + kLanes * 4 + 4;
+        const __amdgpu_buffer_rsrc_t rl =
+            __builtin_amdgcn_make_buffer_rsrc(A.out_len + (size_t)e.f * fan, 0, e.in() ? 4 * fan : 0, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(
+            (all || (one && (uint32_t)lane == port)) ? (uint32_t)total : 0u, rl, 4 * lane, 0, 0);
+    }
+    const bool last = lane == kWave - 1;
+    // (a frame that emits nothing stores nowhere: its values are left undefined)
+    uint32_t pc = unset(), p0 = unset(), p1 = unset(), p2 = unset(), p3 = unset();
+    u4 patch = unset4();
+    if (em_any) {
+        uint32_t a[4];   // this lane's 16 payload bytes, big-endian (util.c:403-405), memory order
+        a[0] = __builtin_bswap32(acc.x);
+        a[1] = __builtin_bswap32(acc.y);
+        a[2] = __builtin_bswap32(acc.z);
+        a[3] = __builtin_bswap32(acc.w);
+        const uint32_t pw = e.psn | 0x80000000u;   // ack-request bit + PSN (util.c:386)
+        // P ^ V_op,psn: the payload segment's term, and on lanes 0-4 the opcode's
+        // and the PSN bytes' (util.c:378, :386)
+        const uint32_t vb = lane == 0 ? op : (pw >> (8 * (4 - lane))) & 0xFFu;
+        const uint32_t var = lane < 5 ? var_crc(t, (int)wf, lane, vb) : 0u;
+        pc = (kX & 1) ? var : wave_xor(seg16(t, a, lane) ^ var);
+        const int next4 = ((lane + 1) & (kWave - 1)) * 4;
+        const uint32_t n0 = from_next(a[0], next4), n1 = from_next(a[1], next4), n2 = from_next(a[2], next4);
+        p0 = __builtin_amdgcn_alignbyte(a[3], a[2], 2);
+        p1 = last ? a[3] >> 16 : __builtin_amdgcn_alignbyte(n0, a[3], 2);
+        p2 = last ? 0u : __builtin_amdgcn_alignbyte(n1, n0, 2);
+        p3 = last ? 0u : __builtin_amdgcn_alignbyte(n2, n1, 2);
+        // the header chunks' patch over the template images (zeros there):
+        // opcode (byte 42), PSN (50-53), and the payload's first 10 bytes after
+        // the BTH (no RETH) or after the RETH (lane 4's chunk)
+        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)a[0], 0);
+        const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)a[1], 0);
+        const uint32_t a2 = (uint32_t)__builtin_amdgcn_readlane((int)a[2], 0);
+        const uint32_t psn_hi = (pw >> 24) | (((pw >> 16) & 0xFFu) << 8);    // frame bytes 50, 51
+        const uint32_t psn_lo = ((pw >> 8) & 0xFFu) | ((pw & 0xFFu) << 8);   // bytes 52, 53
+        const uint32_t q1 = a0 << 16, q2 = __builtin_amdgcn_alignbyte(a1, a0, 2);
+        const uint32_t q3 = __builtin_amdgcn_alignbyte(a2, a1, 2);
+        const int pl = wf ? 4 : 3;   // the lane whose chunk ends with the payload's first 10 bytes
+        patch.x = lane == 3 ? psn_hi << 16 : 0u;
+        patch.y = (lane == 3 ? psn_lo : 0u) | (lane == pl ? q1 : 0u);
+        patch.z = lane == pl ? q2 : (lane == 2 ? op << 16 : 0u);
+        patch.w = lane == pl ? q3 : 0u;
+    }
+    const int hchunks = 4 + (int)wf;   // header + the payload's first 10 bytes
+    const int ho = lane < hchunks ? 16 * lane : kOobOffset, po = 16 * (hchunks + lane);
+    const uint32_t emit_mask = all ? (1u << fan) - 1u : (one ? 1u << port : 0u);   // children that get a frame
+    uint8_t* row = A.out + (size_t)e.f * fan * A.out_stride;
+    constexpr int kUnroll = kFan ? kFan : 1;
+#pragma unroll kUnroll
+    for (int c = 0; c < fan; ++c) {
+        const bool em = (emit_mask >> c) & 1u;
+        u4 h = unset4(), v = unset4();
+        if (em) {
+            h = reinterpret_cast<const u4*>(t.img[2 * c + wf])[lane < 5 ? lane : 0];
+            h.x |= patch.x;
+            h.y |= patch.y;
+            h.z |= patch.z;
+            h.w |= patch.w;
+            uint32_t crc = pc ^ t.hcrc[2 * c + wf];
+            if (wf && !(kX & 4)) {
+                // child c's RETH (reth_keeper[slot][c], nts.c:442; util.c:409-417):
+                // bytes 54-69, lane 3's chunk from byte 6 on and lane 4's first 6
+                // bytes; its ICRC term on lanes 0-15
+                uint32_t R[4];
+                if (kFan || c < kWave / 4) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) R[j] = (uint32_t)__builtin_amdgcn_readlane((int)keep, 4 * c + j);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) R[j] = A.reth[((size_t)(e.psn & A.smask) * fan + c) * 4 + j];
+                }
+                if (lane == 3) {
+                    h.y |= R[0] << 16;
+                    h.z = __builtin_amdgcn_alignbyte(R[1], R[0], 2);
+                    h.w = __builtin_amdgcn_alignbyte(R[2], R[1], 2);
+                }
+                if (lane == 4) {
+                    h.x = __builtin_amdgcn_alignbyte(R[3], R[2], 2);
+                    h.y |= R[3] >> 16;
+                }
+                const uint32_t rk = (lane & 8) ? ((lane & 4) ? R[3] : R[2]) : ((lane & 4) ? R[1] : R[0]);
+                crc ^= wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
+            }
+            crc = ~crc;   // util.c:424-426
+            v = u4{p0, last ? p1 | (crc << 16) : p1, last ? crc >> 16 : p2, p3};
+        }
+        const __amdgpu_buffer_rsrc_t orow =
+            __builtin_amdgcn_make_buffer_rsrc(row, 0, em && !(kX & 2) ? (int)A.out_stride : 0, 0x00020000);
+        row += A.out_stride;
         if (kOut16) {
             __builtin_amdgcn_raw_buffer_store_b128(h, orow, ho, 0, kAuxNt);
             __builtin_amdgcn_raw_buffer_store_b128(v, orow, po, 0, kAuxNt);
@@ -1279,349 +1049,170 @@ __device__ __forceinline__ void emit_broadcast(const ApplyArgs& A, const EmitLds
     }
 }
 
-// One pair of frames (2 pidx, 2 pidx + 1): classify, sum, and (batch call)
-// broadcast.  g = the batch generation.
-template <bool kEmit, bool kOut16>
-__device__ __forceinline__ void apply_pair(const ApplyArgs& A, const int32_t* __restrict__ act_in,
-                                           const int32_t* __restrict__ ports_in, const uint32_t* __restrict__ psns_in,
-                                           int64_t pidx, uint32_t g, const EmitLds* tp, const LaneK& L)
-{
-    const InccSwitchState& s = A.s;
-    // the lane number through an opaque copy: what the pair derives from it is
-    // computed per pair, not hoisted out of the persistent loop into registers
-    // held for the whole kernel (the occupancy is what hides this kernel's latency)
-    const int lane = (int)opaque_u32((uint32_t)L.lane), fan = s.fan_in;
-    const int64_t count = A.count, stride = A.stride;
-    const bool have = 2 * pidx < count;
-    const int64_t f0 = have ? 2 * pidx : 0;
-    const bool in1 = have && f0 + 1 < count;
-    const int64_t f1 = in1 ? f0 + 1 : f0;
-    // round trip 1: the payload chunks of both rows, and the claim results
-    u4 x[2] = {}, e[2] = {};
-    if (A.wide) {
-        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(A.frames + f0 * stride, have ? (in1 ? 2 : 1) * stride : 0);
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int rb = k * (int)stride;
-            x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, rb + 48 + 16 * lane, 0, 0);
-            e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane < 2 ? rb + 1072 + 16 * lane : kOobOffset, 0, 0);
-        }
-    }
-    // the claim results, as scalar loads (the kernel's read-only views of
-    // action / ports / PSNs, so that they arrive apart from the payloads and
-    // round trip 2 can be issued before those land)
-    FrameK F[2];
-    F[0].act = have ? act_in[f0] : INCCL_SW_IGNORED;
-    F[1].act = in1 ? act_in[f1] : INCCL_SW_IGNORED;
-    F[0].port = ports_in[f0];
-    F[1].port = ports_in[f1];
-    F[0].psn = psns_in[f0];
-    F[1].psn = psns_in[f1];
-    const uint32_t tag = ~g, result_bit = 1u << fan, smask = s.slots - 1;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        FrameK& f = F[k];
-        f.live = (f.act & kActPending) != 0;
-        f.op = (uint32_t)f.act & 0xFFu;
-        f.wf = ((uint32_t)f.act >> 9) & 1u;
-        f.slot = f.psn & smask;
-    }
-    // round trip 2, lane-parallel over the two frames: half h = lane / 32 is
-    // frame h; lane 32 h + p < 32 h + fan_in loads port p's first-copy key,
-    // lanes 32 h and 32 h + 1 the two tagged arrival words
-    const int hf = lane >> 5, pl = lane & 31;
-    const bool live_h = hf ? F[1].live : F[0].live;
-    const uint32_t slot_h = hf ? F[1].slot : F[0].slot;
-    const uint64_t key = live_h && pl < fan ? s.first[(size_t)slot_h * fan + pl] : 0ull;
-    const uint64_t av = live_h && pl < 2 ? s.arrival[2 * (size_t)slot_h + pl] : 0ull;
-    uint32_t keep[2] = {0u, 0u};   // the batch call: the RETH keeper of each frame's slot
-    if (kEmit) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-            if (F[k].live) keep[k] = s.reth[(size_t)F[k].slot * fan * 4 + (lane < 4 * fan ? lane : 0)];
-    }
-    // each frame's payload words (this lane's four) and RETH words (uniform),
-    // from the chunks of round trip 1 while round trip 2 is in flight
-    uint32_t P[2][4], R[2][4];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const FrameK& f = F[k];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) P[k][j] = R[k][j] = 0u;
-        if (!f.live) continue;
-        if (A.wide) {
-            // chunk 4 + lane (lane 63: chunk 67) and 5 + lane (lane 62: 67, lane 63: 68)
-            const bool last = lane == kWave - 1;
-            uint32_t y0 = from_next(x[k].x, L.next4), y1 = from_next(x[k].y, L.next4);
-            y0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 0) : y0;
-            y1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 0) : y1;
-            if (f.wf) {
-                uint32_t y2 = from_next(x[k].z, L.next4), y3 = from_next(x[k].w, L.next4);
-                uint32_t z0 = from_next(y0, L.next4), z1 = from_next(y1, L.next4);
-                y2 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].z, 0) : y2;
-                y3 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].w, 0) : y3;
-                z0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 1) : z0;
-                z1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 1) : z1;
-                payload_from_chunks(u4{y0, y1, y2, y3}, z0, z1, P[k]);
-                // the RETH, bytes 54-69: bytes 6-15 of chunk 3 (lane 0), 0-5 of chunk 4 (lane 1)
-                const uint32_t c3y = (uint32_t)__builtin_amdgcn_readlane((int)x[k].y, 0);
-                const uint32_t c3z = (uint32_t)__builtin_amdgcn_readlane((int)x[k].z, 0);
-                const uint32_t c3w = (uint32_t)__builtin_amdgcn_readlane((int)x[k].w, 0);
-                const uint32_t c4x = (uint32_t)__builtin_amdgcn_readlane((int)x[k].x, 1);
-                const uint32_t c4y = (uint32_t)__builtin_amdgcn_readlane((int)x[k].y, 1);
-                R[k][0] = __builtin_amdgcn_alignbyte(c3z, c3y, 2);
-                R[k][1] = __builtin_amdgcn_alignbyte(c3w, c3z, 2);
-                R[k][2] = __builtin_amdgcn_alignbyte(c4x, c3w, 2);
-                R[k][3] = __builtin_amdgcn_alignbyte(c4y, c4x, 2);
-            } else {
-                payload_from_chunks(x[k], y0, y1, P[k]);
-            }
-        } else {
-            const uint8_t* fr = A.frames + (f0 + k) * stride;
-            payload16(fr, f.wf, lane, false, P[k]);
-            if (f.wf) reth_words(fr, lane, R[k]);
-        }
-    }
-    uint32_t pre[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        pre[k] = F[k].live ? arrival_before(readlane64(av, 32 * k), readlane64(av, 32 * k + 1), g) : 0u;
-    // classify (nts.c:353-372): lane 32 h + p < fan_in says when frame h's port
-    // p counts, as 1 + frame index; 0 = before the batch, ~0 = not in this batch
-    const uint32_t pre_h = hf ? pre[1] : pre[0];
-    uint32_t at = 0, mine = 0xFFFFFFFFu, fo = 0xFFFFFFFFu;
-    bool counted = false;
-    if (live_h && pl < fan) {
-        const bool in_batch = (uint32_t)(key >> 32) == tag;
-        const uint32_t ef = ((uint32_t)key) >> 1;
-        const bool before = (pre_h >> pl) & 1u;
-        at = before ? 0u : (in_batch ? ef + 1u : 0xFFFFFFFFu);
-        mine = in_batch ? ef : 0xFFFFFFFFu;
-        fo = (uint32_t)key;                                 // frame << 1 | wf
-        counted = in_batch && !before;
-    }
-    const uint64_t bal = __ballot(counted);
-    uint32_t d = at;                                        // max over each half: the completing arrival
-#pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) d = max(d, (uint32_t)__shfl_xor((int)d, o, kWave));
-    int out_act[2];
-    bool lead[2], counted_me[2];
-    uint32_t cports[2], done_at[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const FrameK& f = F[k];
-        out_act[k] = f.act;
-        cports[k] = (uint32_t)(bal >> (32 * k));
-        done_at[k] = (uint32_t)__builtin_amdgcn_readlane((int)d, 32 * k);
-        lead[k] = counted_me[k] = false;
-        if (!f.live) continue;
-        const uint32_t fi = (uint32_t)(f0 + k);
-        const uint32_t mk = (uint32_t)__builtin_amdgcn_readlane((int)mine, 32 * k + f.port);
-        const uint32_t dk = done_at[k];
-        const bool arrival = !((pre[k] >> f.port) & 1u) && mk == fi;   // the counted arrival: nts.c:359-363
-        counted_me[k] = arrival;
-        if (arrival) {
-            out_act[k] = (dk == fi + 1u) ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
-        } else {                                                 // retransmit: nts.c:353-357
-            const bool done_before = (pre[k] & result_bit) != 0;
-            const bool done_earlier = dk != 0u && dk != 0xFFFFFFFFu && dk - 1u < fi;
-            out_act[k] = (done_before || done_earlier) ? INCCL_SW_REPLAY : INCCL_SW_DROPPED;
-        }
-        lead[k] = arrival && f.port == __builtin_ctz(cports[k]);
-    }
-    // the leaders: sum, store, bitmap, recycle, broadcast
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        if (!lead[k]) continue;
-        const FrameK& f = F[k];
-        u4 acc = {0u, 0u, 0u, 0u};
-        // a slot whose bitmap was empty before the batch holds zeros (reset,
-        // or recycled since its last use), so its partial is not read
-        if (pre[k] != 0u) acc = reinterpret_cast<const u4*>(s.agg + (size_t)f.slot * kLanes)[lane];
-        for (uint32_t m = cports[k]; m; m &= m - 1) {
-            const uint32_t ek = (uint32_t)__builtin_amdgcn_readlane((int)fo, 32 * k + __builtin_ctz(m));
-            const int64_t fe = (int64_t)(ek >> 1);
-            uint32_t q[4];
-            if (fe == f0) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) q[j] = P[0][j];
-            } else if (in1 && fe == f1) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) q[j] = P[1][j];
-            } else {
-                payload16(A.frames + fe * stride, ek & 1u, lane, A.wide != 0, q);
-            }
-            acc.x += q[0];
-            acc.y += q[1];
-            acc.z += q[2];
-            acc.w += q[3];
-        }
-        __builtin_nontemporal_store(acc, reinterpret_cast<u4*>(s.agg + (size_t)f.slot * kLanes) + lane);
-        const bool complete = done_at[k] != 0xFFFFFFFFu;
-        if (lane == 0)
-            s.arrival[2 * (size_t)f.slot + (g & 1u)] =
-                ((uint64_t)g << 32) | (pre[k] | cports[k] | (complete ? result_bit : 0u));   // nts.c:359, :366
-        if (!complete) continue;
-        {   // clear_state_data(psn + WINDOW), nts.c:235-242, :367
-            const uint32_t rs = (f.psn + (s.slots >> 1)) & smask;
-            for (int i = lane; i < fan * 4; i += kWave) s.reth[(size_t)rs * fan * 4 + i] = 0u;
-            if (lane < 2) s.arrival[2 * (size_t)rs + lane] = (uint64_t)g << 32;
-            if (lane == 0) s.degree[rs] = 0;
-        }
-        if constexpr (kEmit) {
-            // the broadcast of the completing frame fd (nts.c:447-453): its
-            // opcode, this PSN, each child's RETH as the keeper now holds it
-            const int64_t fd = (int64_t)done_at[k] - 1;
-            uint32_t opd, wfd;
-            if (fd == f0) {
-                opd = F[0].op;
-                wfd = F[0].wf;
-            } else if (in1 && fd == f1) {
-                opd = F[1].op;
-                wfd = F[1].wf;
-            } else {
-                const uint32_t w10 = reinterpret_cast<const uint32_t*>(A.frames + fd * stride)[10 + (lane & 1)];
-                opd = ((uint32_t)__builtin_amdgcn_readlane((int)w10, 0) >> 16) & 0xFFu;
-                wfd = is_write_first((uint8_t)opd) ? 1u : 0u;
-            }
-            // child c's RETH as the keeper holds it after this batch
-            auto reth_of = [&](int c, uint32_t (&r)[4]) {
-                const uint32_t ec = (uint32_t)__builtin_amdgcn_readlane((int)fo, 32 * k + c);
-                if (((cports[k] >> c) & 1u) && (ec & 1u)) {   // counted in this batch from a WRITE_FIRST copy
-                    const int64_t fe = (int64_t)(ec >> 1);
-                    if (fe == f0) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) r[j] = R[0][j];
-                    } else if (in1 && fe == f1) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) r[j] = R[1][j];
-                    } else {
-                        reth_words(A.frames + fe * stride, lane, r);
-                    }
-                } else if (c < kWave / 4) {                 // the keeper, as loaded
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) r[j] = (uint32_t)__builtin_amdgcn_readlane((int)keep[k], 4 * c + j);
-                } else {
-                    const uint32_t v = s.reth[((size_t)f.slot * fan + c) * 4 + (lane & 3)];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) r[j] = (uint32_t)__builtin_amdgcn_readlane((int)v, j);
-                }
-            };
-            emit_broadcast<kOut16>(A, *tp, L, acc, fd, opd, wfd, f.psn, fan, reth_of);
-        }
-    }
-    // every frame: its action, its RETH into the keeper if it is a counted
-    // WRITE_FIRST (nts.c:442), and (batch call) its rows' lengths
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        if (k == 0 ? !have : !in1) continue;
-        const FrameK& f = F[k];
-        const int64_t fi = f0 + k;
-        if (f.live && lane == 0) A.action[fi] = out_act[k];
-        if (counted_me[k] && f.wf && lane < 4)
-            s.reth[((size_t)f.slot * fan + f.port) * 4 + lane] =
-                lane == 0 ? R[k][0] : lane == 1 ? R[k][1] : lane == 2 ? R[k][2] : R[k][3];
-        if (kEmit && lane < fan) {
-            const int fin = out_act[k];
-            const int total = 54 + 16 * (int)f.wf + kLanes * 4 + 4;   // util.c:341-345
-            A.out_len[fi * fan + lane] =
-                (f.live && (fin == INCCL_SW_COMPLETED || (fin == INCCL_SW_REPLAY && lane == f.port))) ? total : 0;
-        }
-    }
-}
-
-// The claim results are read through separate restrict views of the same
-// arrays (act_in == A.action): every entry is read by one wave before that wave
-// writes it, so the reads are of claim's values.
-#define INCCL_APPLY_ARGS                                                                                        \
-    ApplyArgs A, const int32_t *__restrict__ act_in, const int32_t *__restrict__ ports_in,                     \
-        const uint32_t *__restrict__ psns_in
-
-// the split call: one pair per wave, short-lived blocks
-__global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_apply(INCCL_APPLY_ARGS)
-{
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
-    const LaneK L{lane, ((lane + 1) & (kWave - 1)) * 4};
-    const uint32_t g = A.s.gen[1];   // this batch's generation (claim's)
-    apply_pair<false, true>(A, act_in, ports_in, psns_in, (int64_t)blockIdx.x * kApplyWaves + w, g, nullptr, L);
-    // the next batch's claim adds one (stored last: a store before the claim
-    // results' loads would keep the compiler from reading them as scalars)
-    if (blockIdx.x == 0 && threadIdx.x == 0) A.s.gen[0] = g;
-}
-
-// the batch call: persistent blocks, the egress tables loaded once per block
-template <bool kOut16>
-__global__ __launch_bounds__(kWave* kEmitWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_ingress_apply_emit(
-    INCCL_APPLY_ARGS)
-{
-    __shared__ EmitLds t;
-    const InccSwitchState& s = A.s;
-    const int fan = s.fan_in;
-    {
-        constexpr int kFixed = (int)(sizeof(t.segb) + sizeof(t.lane16) + sizeof(t.var)) / 16;
-        constexpr int n0 = (int)sizeof(t.segb) / 16, n1 = n0 + (int)sizeof(t.lane16) / 16;
-        u4* dst = reinterpret_cast<u4*>(&t.segb[0][0]);
-        for (int i = threadIdx.x; i < kFixed; i += blockDim.x)
-            dst[i] = i < n0 ? reinterpret_cast<const u4*>(&g_segb[0][0])[i]
-                   : i < n1 ? reinterpret_cast<const u4*>(&g_lane16[0][0][0])[i - n0]
-                            : reinterpret_cast<const u4*>(&g_var[0][0][0])[i - n1];
-        // this fan-in's header images and ICRC terms (claim's first wave wrote them)
-        const int nh = 2 * fan * (kHdrImg / 4);
-        for (int i = threadIdx.x; i < nh; i += blockDim.x) reinterpret_cast<uint32_t*>(&t.img[0][0])[i] = s.hdr[i];
-        for (int i = threadIdx.x; i < 2 * fan; i += blockDim.x) t.hcrc[i] = s.hdr[2 * 31 * (kHdrImg / 4) + i];
-    }
-    __syncthreads();
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
-    const LaneK L{lane, ((lane + 1) & (kWave - 1)) * 4};
-    const uint32_t g = s.gen[1];
-    const int64_t pairs = (A.count + 1) >> 1, step = (int64_t)gridDim.x * kEmitWaves;
-    for (int64_t p = (int64_t)blockIdx.x * kEmitWaves + w; p < pairs; p += step)
-        apply_pair<true, kOut16>(A, act_in, ports_in, psns_in, p, g, &t, L);
-    if (blockIdx.x == 0 && threadIdx.x == 0) s.gen[0] = g;
-}
-
-// The batch call's REPLAY resends (nts.c:353-356 / :435-438), after apply: a
-// slot that completed earlier in the same batch has its aggregate only now.
-// Each block scans its share of the actions; a block with no REPLAY leaves
-// before loading any table (the common case: no retransmits).
-__global__ __launch_bounds__(kWave* kEgressWaves) void k_replay(InccSwitchState s, const uint8_t* __restrict__ in_frames,
-                                                                int64_t in_stride, int64_t count,
-                                                                const int32_t* __restrict__ ports,
-                                                                const int32_t* __restrict__ action,
-                                                                const uint32_t* __restrict__ psns,
-                                                                const InccFrameTemplate* __restrict__ tmpl,
-                                                                uint8_t* __restrict__ out, int64_t out_stride,
-                                                                int32_t* __restrict__ out_len)
+// kFan: 2, 3, 4 or 8 (the children loop unrolled), or 0 (A.fan, a loop).
+// kOut16: 16-byte aligned output rows.
+template <int kFan, bool kOut16, int kX = 0>
+__global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_egress(
+    EgressArgs A)
 {
     __shared__ EgressLds t;
-    __shared__ __attribute__((aligned(16))) uint8_t buf[kEgressWaves][80];
-    __shared__ __attribute__((aligned(16))) uint8_t himg[2 * 31][kHdrImg];
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
-    const int64_t per = ((count + gridDim.x - 1) / gridDim.x + kWave - 1) / kWave * kWave;
-    const int64_t b0 = (int64_t)blockIdx.x * per, b1 = b0 + per < count ? b0 + per : count;
-    int any = 0;
-    for (int64_t f = b0 + threadIdx.x; f < b1; f += blockDim.x) any |= action[f] == INCCL_SW_REPLAY;
-    if (!__syncthreads_or(any)) return;
-    egress_setup(t, himg, tmpl, s.fan_in, w, lane);
-    const bool out16 = ((out_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
-    for (int64_t base = b0 + (int64_t)w * kWave; base < b1; base += (int64_t)kEgressWaves * kWave) {
-        const int64_t f = base + lane;
-        uint64_t m = __ballot(f < b1 && action[f] == INCCL_SW_REPLAY);
-        while (m) {
-            const int64_t fr = base + __builtin_ctzll(m);
-            m &= m - 1;
-            const EgressIn e = egress_fetch(s, in_frames, in_stride, ports, action, psns, fr, lane);
-            egress_emit(s, e, himg, out, out_stride, out16, out_len, t, buf[w], fr, lane);
-        }
+    egress_setup(t, A.tmpl, kFan ? kFan : A.fan);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane0 = threadIdx.x % kWave;
+    const uint32_t step = gridDim.x * kEgressWaves, count = A.count;
+    const uint32_t rot0 = blockIdx.x * kEgressWaves + w;
+    // this wave's frames: f_r = r step + (rot0 + r) mod step for r < n (every
+    // round before count / step, and that round if its frame is below count)
+    const uint32_t rounds = count / step, rem = count % step;
+    const uint32_t n = rounds + ((rot0 + rounds) % step < rem ? 1u : 0u);
+    if (n == 0) return;
+    uint32_t cb = 0, cr = rot0;   // the cursor: the newest frame whose claim results were requested
+    auto advance = [&]() {
+        cb += step;
+        cr = cr + 1 == step ? 0 : cr + 1;
+        return cb + cr;
+    };
+    // the lane number through an opaque copy per use: what a frame derives from
+    // it is computed per frame, not hoisted out of the loop into registers held
+    // for the whole kernel
+    auto ln = [&]() { return (int)opaque_u32((uint32_t)lane0); };
+    const MetaLane ml = meta_lane(A, lane0);
+    // Two frames per iteration, set a then set b; entering iteration j the
+    // claim results of frame 2j (ma, decoded) and 2j+1 (mb, in flight) and
+    // frame 2j's aggregate and keeper (in flight) were issued.  A frame at or
+    // past n is past count: it emits nothing and its stores are dropped.
+    uint32_t fa = rot0, fb = advance();
+    const uint32_t ma = egress_meta(A, ml, fa);
+    uint32_t mb = egress_meta(A, ml, fb);
+    EgressF ea = egress_decode(A, ma, fa), eb;
+    u4 acca, accb;
+    uint32_t keepa, keepb;
+    egress_load(A, ea, ln(), acca, keepa);
+    if (kFan) {
+        // as many dropped stores as an iteration issues: the loop is entered
+        // with its back edge's memory history, so its waits are counts, not 0
+        const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(A.out_len, 0, 0, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 1 + kFan * (kOut16 ? 2 : 8); ++k)
+            __builtin_amdgcn_raw_buffer_store_b32(0u, none, 16 * k, 0, 0);   // apart: none is merged away
+    }
+    for (uint32_t j = 0;; j += 2) {
+        const uint32_t fa2 = advance();
+        const uint32_t ma2 = egress_meta(A, ml, fa2);
+        eb = egress_decode(A, mb, fb);
+        egress_load(A, eb, ln(), accb, keepb);
+        egress_emit<kFan, kOut16, kX>(t, A, ea, acca, keepa, ln());
+        fb = advance();
+        mb = egress_meta(A, ml, fb);
+        ea = egress_decode(A, ma2, fa2);
+        egress_load(A, ea, ln(), acca, keepa);
+        egress_emit<kFan, kOut16, kX>(t, A, eb, accb, keepb, ln());
+        if (j + 2 >= n) break;
     }
 }
 
+
+// Chunked egress (experiment): a wave takes kC consecutive input frames at a
+// time, lane l frame c kC + l; their claim results and opcodes in four vector
+// loads, the row lengths of the whole chunk lane-parallel, then only the frames
+// that emit, two register sets alternating, each frame's aggregate and keeper
+// one frame ahead.
+template <int kFan, bool kOut16, int kC, int kD>
+__global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_egress_chunk(
+    EgressArgs A)
+{
+    __shared__ EgressLds t;
+    const int fan = kFan ? kFan : A.fan;
+    egress_setup(t, A.tmpl, fan);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane0 = threadIdx.x % kWave;
+    const uint32_t count = A.count, chunks = (count + kC - 1) / kC;
+    const uint32_t nw = gridDim.x * kEgressWaves;
+    auto ln = [&]() { return (int)opaque_u32((uint32_t)lane0); };
+    for (uint32_t ch = blockIdx.x * kEgressWaves + w; ch < chunks; ch += nw) {
+        const int lane = ln();
+        const uint32_t f0 = ch * kC, nf = min((uint32_t)kC, count - f0);
+        const int off = lane < (int)nf ? 4 * lane : kOobOffset;
+        const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<int32_t*>(A.action) + f0, 0, 4 * kC, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<int32_t*>(A.ports) + f0, 0, 4 * kC, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t*>(A.psns) + f0, 0, 4 * kC, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(A.frames) + (size_t)f0 * A.stride, 0, (int)(kC * A.stride), 0x00020000);
+        const int act = (int)__builtin_amdgcn_raw_buffer_load_b32(ra, off, 0, 0);
+        const uint32_t port = __builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, 0);
+        const uint32_t psn = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+        const uint32_t w10 = __builtin_amdgcn_raw_buffer_load_b32(
+            rf, lane < (int)nf ? lane * (int)A.stride + 40 : kOobOffset, 0, 0);
+        const uint32_t op = (w10 >> 16) & 0xFFu;
+        const bool in = lane < (int)nf;
+        const bool all = in && act == INCCL_SW_COMPLETED;
+        const bool one = in && act == INCCL_SW_REPLAY && port < (uint32_t)fan;
+        const uint32_t bits = op | (is_write_first((uint8_t)op) ? 1u << 8 : 0u) | (in ? 1u << 9 : 0u) |
+                              (all ? 1u << 10 : 0u) | (one ? 1u << 11 : 0u) | ((port & 0xFFFFu) << 16);
+        {   // the chunk's row lengths: entry e = f fan + c, lane-parallel (util.c:341-345)
+            const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+                A.out_len + (size_t)f0 * fan, 0, (int)(4 * nf * fan), 0x00020000);
+            for (int k = 0; k < (kC * fan + kWave - 1) / kWave; ++k) {
+                const int e = lane + kWave * k, fr = e / fan, c = e - fr * fan;
+                const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (fr & (kWave - 1)), (int)bits);
+                const bool on = ((b >> 10) & 1u) || (((b >> 11) & 1u) && (b >> 16) == (uint32_t)c);
+                const uint32_t total = 54 + 16 * ((b >> 8) & 1u) + kLanes * 4 + 4;
+                __builtin_amdgcn_raw_buffer_store_b32(on ? total : 0u, rl, 4 * e, 0, 0);
+            }
+        }
+        uint64_t m = __ballot(all || one);
+        if (!m) continue;
+        auto take = [&](EgressF& e) {   // the next emitting frame of the chunk, or none
+            if (m) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1;
+                e.f = f0 + b;
+                e.psn = (uint32_t)__builtin_amdgcn_readlane((int)psn, b);
+                e.bits = (uint32_t)__builtin_amdgcn_readlane((int)bits, b);
+            } else {
+                e.f = f0;
+                e.psn = 0;
+                e.bits = 0;
+            }
+        };
+        // a ring of kD + 1 frames: frame j's aggregate and keeper are loaded kD
+        // frames before it is emitted
+        constexpr int kR = kD + 1;
+        EgressF E[kR];
+        u4 acc[kR];
+        uint32_t keep[kR];
+#pragma unroll
+        for (int r = 0; r < kD; ++r) {
+            take(E[r]);
+            egress_load(A, E[r], ln(), acc[r], keep[r]);
+        }
+        if (kFan) {
+            const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(A.out_len, 0, 0, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < kD * kFan * (kOut16 ? 2 : 8); ++k)
+                __builtin_amdgcn_raw_buffer_store_b32(0u, none, 16 * k, 0, 0);
+        }
+        for (;;) {
+            bool more = true;
+#pragma unroll
+            for (int r = 0; r < kR; ++r) {
+                const int ld = (r + kD) % kR;
+                take(E[ld]);
+                egress_load(A, E[ld], ln(), acc[ld], keep[ld]);
+                egress_emit<kFan, kOut16, 8>(t, A, E[r], acc[r], keep[r], ln());
+                more = more && E[(r + 1) % kR].in();
+                if (!more) break;
+            }
+            if (!more) break;
+        }
+    }
+}
 
 // ---------------------------------------------------------------------------
 // host: CRC tables (util.c:141-159) and the zero-append operators
 // ---------------------------------------------------------------------------
 uint32_t host_tab[256];
-uint32_t host_seg[kSeg][2][16];
 uint32_t host_lane16[8][16][kWave];
 uint32_t host_seg34[kSeg2][2][16];
 uint32_t host_lane_shift32[8][16][32];
@@ -1649,9 +1240,6 @@ int ensure_tables()
         for (int j = 0; j < 8; ++j) c = (c >> 1) ^ ((c & 1u) ? 0xEDB88320u : 0u);
         host_tab[i] = c;
     }
-    for (int j = 0; j < kSeg; ++j)
-        for (int h = 0; h < 2; ++h)
-            for (uint32_t v = 0; v < 16; ++v) host_seg[j][h][v] = zeros_append(host_tab[v << (4 * h)], kSeg - 1 - j);
     // the standalone ICRC (k_icrc): 34-byte segments, Z_{34 (31 - lane')}; Z_n is
     // linear, Z_{n+34}(x) = Z_34(Z_n(x)), so lanes are filled from 31 down
     for (int j = 0; j < kSeg2; ++j)
@@ -1676,7 +1264,7 @@ int ensure_tables()
                 x = zeros_append(x, 16);
             }
         }
-    // the batch call's payload segments: byte j of 16 -> Z_{15-j}(T[value])
+    // egress: byte j of a 16-byte segment -> Z_{15-j}(T[value])
     for (int j = 0; j < 16; ++j)
         for (uint32_t v = 0; v < 256; ++v) host_segb[j][v] = zeros_append(host_tab[v], 15 - j);
     for (int wf = 0; wf < 2; ++wf) {
@@ -1688,14 +1276,12 @@ int ensure_tables()
                     if (wf || k < 5) host_var[wf ? 5 + k : k][h][v] = p < hdr ? zeros_append(host_tab[v << (4 * h)], hdr - 1 - p + 1024) : 0u;
         }
     }
-    e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg), host_seg, sizeof(host_seg));
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane16), host_lane16, sizeof(host_lane16));
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane16), host_lane16, sizeof(host_lane16));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_var), host_var, sizeof(host_var));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_z1024), host_z1024, sizeof(host_z1024));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg34), host_seg34, sizeof(host_seg34));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane_shift32), host_lane_shift32, sizeof(host_lane_shift32));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_segb), host_segb, sizeof(host_segb));
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_tab), host_tab, sizeof(host_tab));
     if (e != hipSuccess) return (int)e;
     if (dev >= 0 && dev < 64) g_tables_ready[dev] = true;
     return 0;
@@ -1715,31 +1301,99 @@ int num_cus()
     return cus;
 }
 
-// split call: one wave per pair of frames, short-lived blocks
+// classify (a lane per frame), then sum (a wave per pair of frames, short-lived blocks)
 int launch_apply(const ApplyArgs& a, hipStream_t st)
 {
+    const dim3 lanes((unsigned)((a.count + kClassifyBlock - 1) / kClassifyBlock));
+    hipLaunchKernelGGL(k_ingress_classify, lanes, dim3(kClassifyBlock), 0, st, a.s, a.frames, a.stride, a.count, a.ports,
+                       a.action, a.psns);
     const int64_t pairs = (a.count + 1) / 2, blocks = (pairs + kApplyWaves - 1) / kApplyWaves;
-    hipLaunchKernelGGL(k_ingress_apply, dim3((unsigned)(blocks < 1 ? 1 : blocks)), dim3(kWave * kApplyWaves), 0, st, a,
+    hipLaunchKernelGGL(k_ingress_sum, dim3((unsigned)(blocks < 1 ? 1 : blocks)), dim3(kWave * kApplyWaves), 0, st, a,
                        (const int32_t*)a.action, a.ports, a.psns);
     return (int)hipGetLastError();
 }
 
-// batch call: persistent blocks, as many as fit beside each other
-template <bool kOut16>
-int launch_apply_emit(const ApplyArgs& a, hipStream_t st)
+template <int kFan, bool kOut16, int kC, int kD>
+int launch_egress_chunk(const EgressArgs& a, hipStream_t st)
 {
     static const int per_cu = [] {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_ingress_apply_emit<kOut16>, kWave * kEmitWaves, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_egress_chunk<kFan, kOut16, kC, kD>, kWave * kEgressWaves, 0) !=
                 hipSuccess || n < 1)
             n = 1;
         return n;
     }();
-    const int64_t pairs = (a.count + 1) / 2, need = (pairs + kEmitWaves - 1) / kEmitWaves;
-    const int64_t cap = (int64_t)num_cus() * per_cu;
-    hipLaunchKernelGGL(k_ingress_apply_emit<kOut16>, dim3((unsigned)(need < cap ? (need < 1 ? 1 : need) : cap)),
-                       dim3(kWave * kEmitWaves), 0, st, a, (const int32_t*)a.action, a.ports, a.psns);
+    const int64_t chunks = ((int64_t)a.count + kC - 1) / kC;
+    const int64_t need = (chunks + kEgressWaves - 1) / kEgressWaves, cap = (int64_t)num_cus() * per_cu;
+    hipLaunchKernelGGL((k_egress_chunk<kFan, kOut16, kC, kD>), dim3((unsigned)(need < cap ? (need < 1 ? 1 : need) : cap)),
+                       dim3(kWave * kEgressWaves), 0, st, a);
     return (int)hipGetLastError();
+}
+
+// persistent egress: as many blocks as fit beside each other (two per CU)
+template <int kFan, bool kOut16, int kX = 0>
+int launch_egress_t(const EgressArgs& a, hipStream_t st)
+{
+    static const int per_cu = [] {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_egress<kFan, kOut16, kX>, kWave * kEgressWaves, 0) !=
+                hipSuccess || n < 1)
+            n = 1;
+        return n;
+    }();
+    const int64_t need = ((int64_t)a.count + kEgressWaves - 1) / kEgressWaves, cap = (int64_t)num_cus() * per_cu;
+    hipLaunchKernelGGL((k_egress<kFan, kOut16, kX>), dim3((unsigned)(need < cap ? (need < 1 ? 1 : need) : cap)),
+                       dim3(kWave * kEgressWaves), 0, st, a);
+    return (int)hipGetLastError();
+}
+
+template <bool kOut16>
+int launch_egress_o(const EgressArgs& a, hipStream_t st)
+{
+    switch (a.fan) {   // fan-in 2, 3, 4, 8: the children loop unrolled; others a loop
+    case 2: {
+        static const int x = getenv("INCCL_T_EGRESS_X") ? atoi(getenv("INCCL_T_EGRESS_X")) : 0;
+        if (x == 1) return launch_egress_t<2, kOut16, 1>(a, st);
+        if (x == 2) return launch_egress_t<2, kOut16, 2>(a, st);
+        if (x == 4) return launch_egress_t<2, kOut16, 4>(a, st);
+        if (x == 3) return launch_egress_t<2, kOut16, 3>(a, st);
+        if (x == 7) return launch_egress_t<2, kOut16, 7>(a, st);
+        if (x == 16) return launch_egress_chunk<2, kOut16, 16, 1>(a, st);
+        if (x == 162) return launch_egress_chunk<2, kOut16, 16, 2>(a, st);
+        if (x == 163) return launch_egress_chunk<2, kOut16, 16, 3>(a, st);
+        if (x == 322) return launch_egress_chunk<2, kOut16, 32, 2>(a, st);
+        if (x == 323) return launch_egress_chunk<2, kOut16, 32, 3>(a, st);
+        if (x == 324) return launch_egress_chunk<2, kOut16, 32, 4>(a, st);
+        return launch_egress_t<2, kOut16>(a, st);
+    }
+    case 3: return launch_egress_t<3, kOut16>(a, st);
+    case 4: return launch_egress_t<4, kOut16>(a, st);
+    case 8: return launch_egress_t<8, kOut16>(a, st);
+    default: return launch_egress_t<0, kOut16>(a, st);
+    }
+}
+
+int launch_egress(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count, const int32_t* ports,
+                  const int32_t* action, const uint32_t* psns, const InccFrameTemplate* tmpl, uint8_t* out,
+                  size_t out_stride, int32_t* out_len, hipStream_t st)
+{
+    EgressArgs a{};
+    a.agg = s->agg;
+    a.reth = s->reth;
+    a.frames = frames;
+    a.ports = ports;
+    a.action = action;
+    a.psns = psns;
+    a.tmpl = tmpl;
+    a.out = out;
+    a.out_len = out_len;
+    a.stride = (uint32_t)stride;
+    a.out_stride = (uint32_t)out_stride;
+    a.count = (uint32_t)count;
+    a.smask = s->slots - 1;
+    a.fan = s->fan_in;
+    const bool o16 = ((out_stride & 15) == 0) && (((uintptr_t)out & 15) == 0);
+    return o16 ? launch_egress_o<true>(a, st) : launch_egress_o<false>(a, st);
 }
 
 int check_batch_args(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count, const int32_t* ports,
@@ -1768,11 +1422,19 @@ ApplyArgs apply_args(const InccSwitchState* s, const uint8_t* frames, size_t str
 }
 
 void launch_claim(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count, const int32_t* ports,
-                  int32_t* action, uint32_t* psn_out, const InccFrameTemplate* tmpl, hipStream_t st)
+                  int32_t* action, uint32_t* psn_out, hipStream_t st)
 {
     const dim3 lanes((unsigned)(((int64_t)count + kClaimBlock - 1) / kClaimBlock));
     hipLaunchKernelGGL(k_ingress_claim, lanes, dim3(kClaimBlock), 0, st, *s, frames, (int64_t)stride, (int64_t)count,
-                       ports, action, psn_out, tmpl);
+                       ports, action, psn_out);
+}
+
+int egress_args_ok(const InccSwitchState* s, const uint8_t* frames, const int32_t* ports, const int32_t* action,
+                   const uint32_t* psns, const InccFrameTemplate* tmpl, const uint8_t* out, size_t out_stride,
+                   const int32_t* out_len)
+{
+    return s && frames && ports && action && psns && tmpl && out && out_len && !(out_stride & 3) &&
+           out_stride >= 1100 && out_stride <= (1u << 20) && !((uintptr_t)out & 3);
 }
 
 }  // namespace
@@ -1808,35 +1470,26 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
     if (count == 0) return 0;
     if (check_batch_args(s, frames, stride, count, ports, action, psn_out)) return INCCL_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
-    launch_claim(s, frames, stride, count, ports, action, psn_out, nullptr, st);
+    launch_claim(s, frames, stride, count, ports, action, psn_out, st);
     return launch_apply(apply_args(s, frames, stride, count, ports, action, psn_out), st);
 }
 
+// ingress then egress of one batch: claim, apply, egress on one stream
 int inccl_k_switch_batch(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count,
                          const int32_t* ports, int32_t* action, uint32_t* psn_out, const InccFrameTemplate* tmpl,
                          uint8_t* out, size_t out_stride, int32_t* out_len, void* stream)
 {
     if (count == 0) return 0;
-    if (check_batch_args(s, frames, stride, count, ports, action, psn_out) || !tmpl || !out || !out_len ||
-        (out_stride & 3) || out_stride < 1100 || out_stride > (1u << 20) || ((uintptr_t)out & 3))
+    if (check_batch_args(s, frames, stride, count, ports, action, psn_out) ||
+        !egress_args_ok(s, frames, ports, action, psn_out, tmpl, out, out_stride, out_len))
         return INCCL_ERR_ARG;
     int rc = ensure_tables();
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    launch_claim(s, frames, stride, count, ports, action, psn_out, tmpl, st);
-    ApplyArgs a = apply_args(s, frames, stride, count, ports, action, psn_out);
-    a.out = out;
-    a.out_stride = (int64_t)out_stride;
-    a.out_len = out_len;
-    const bool o16 = ((out_stride & 15) == 0) && (((uintptr_t)out & 15) == 0);
-    rc = o16 ? launch_apply_emit<true>(a, st) : launch_apply_emit<false>(a, st);
+    launch_claim(s, frames, stride, count, ports, action, psn_out, st);
+    rc = launch_apply(apply_args(s, frames, stride, count, ports, action, psn_out), st);
     if (rc) return rc;
-    const int64_t need = ((int64_t)count + kWave * kEgressWaves - 1) / (kWave * kEgressWaves);
-    const int64_t cap = num_cus();
-    hipLaunchKernelGGL(k_replay, dim3((unsigned)(need < cap ? need : cap)), dim3(kWave * kEgressWaves), 0, st, *s, frames,
-                       (int64_t)stride, (int64_t)count, ports, (const int32_t*)action, (const uint32_t*)psn_out, tmpl, out,
-                       (int64_t)out_stride, out_len);
-    return (int)hipGetLastError();
+    return launch_egress(s, frames, stride, count, ports, action, psn_out, tmpl, out, out_stride, out_len, st);
 }
 
 int inccl_k_switch_egress(const InccSwitchState* s, const uint8_t* in_frames, size_t in_stride, size_t count,
@@ -1845,43 +1498,14 @@ int inccl_k_switch_egress(const InccSwitchState* s, const uint8_t* in_frames, si
                           void* stream)
 {
     if (count == 0) return 0;
-    if (!s || !in_frames || !ports || !action || !psns || !tmpl || !out || !out_len || (out_stride & 3) ||
-        out_stride < 1100 || ((uintptr_t)out & 3))
+    if (!egress_args_ok(s, in_frames, ports, action, psns, tmpl, out, out_stride, out_len) || (in_stride & 3) ||
+        in_stride < INCCL_FRAME_MIN_STRIDE || in_stride > (1u << 20) || ((uintptr_t)in_frames & 3) ||
+        count >= 0x7FFFFFFFull)
         return INCCL_ERR_ARG;
     int rc = ensure_tables();
     if (rc) return rc;
-    hipStream_t st = (hipStream_t)stream;
-    // persistent grid (the CRC tables are loaded once per block), three 8-wave
-    // blocks per CU: 24 waves, the measured optimum (profiles/r03/egress_waves/)
-    const int64_t need = ((int64_t)count + kEgressWaves - 1) / kEgressWaves;
-    const int64_t cap = (int64_t)num_cus() * 3;
-    const int eg = (int)(need < cap ? (need < 1 ? 1 : need) : cap);
-    const bool o16 = ((out_stride & 15) == 0) && (((uintptr_t)out & 15) == 0);
-    // non-temporal frame stores (the frames are not re-read here): egress 65.3 vs
-    // 71.0 us, and the next batch's apply no longer starts behind 144 MB of dirty
-    // lines (profiles/r03/store_policy/)
-    const dim3 g(eg), b(kWave * kEgressWaves);
-    const int64_t is = (int64_t)in_stride, os = (int64_t)out_stride, n = (int64_t)count;
-#define INCCL_EGRESS_FIXED(F)                                                                                   \
-    case F:                                                                                                     \
-        if (o16)                                                                                                \
-            hipLaunchKernelGGL((k_egress_fixed<F, true, kAuxNt>), g, b, 0, st, *s, in_frames, is, n, ports,     \
-                               action, psns, tmpl, out, os, out_len);                                           \
-        else                                                                                                    \
-            hipLaunchKernelGGL((k_egress_fixed<F, false, kAuxNt>), g, b, 0, st, *s, in_frames, is, n, ports,    \
-                               action, psns, tmpl, out, os, out_len);                                           \
-        return (int)hipGetLastError();
-    // fan-in 2, 3, 4, 8: the straight-line kernel; others the generic one
-    switch (s->fan_in) {
-        INCCL_EGRESS_FIXED(2)
-        INCCL_EGRESS_FIXED(3)
-        INCCL_EGRESS_FIXED(4)
-        INCCL_EGRESS_FIXED(8)
-    default: break;
-    }
-#undef INCCL_EGRESS_FIXED
-    hipLaunchKernelGGL(k_egress, g, b, 0, st, *s, in_frames, is, n, ports, action, psns, tmpl, out, os, out_len);
-    return (int)hipGetLastError();
+    return launch_egress(s, in_frames, in_stride, count, ports, action, psns, tmpl, out, out_stride, out_len,
+                         (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -50,8 +50,7 @@ struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device)
     const size_t reth = (size_t)slots * (size_t)fan_in * 16;
     const size_t first = (size_t)slots * (size_t)fan_in * 8;
     const size_t gen = 16;   /* the batch-generation words (zeroed with the state) */
-    const size_t hdr = 62 * 84;   /* the batch call's header images and ICRC terms */
-    sw->first_off = (agg + arr + deg + reth + gen + hdr + 7) & ~(size_t)7;
+    sw->first_off = (agg + arr + deg + reth + gen + 7) & ~(size_t)7;
     sw->bytes = sw->first_off + first;
     hipError_t e = hipMalloc(&sw->mem, sw->bytes);
     if (e == hipSuccess) e = hipMemset(sw->mem, 0, sw->first_off);
@@ -68,7 +67,6 @@ struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device)
     sw->st.degree = (int32_t *)(p + agg + arr);
     sw->st.reth = (uint32_t *)(p + agg + arr + deg);
     sw->st.gen = (uint32_t *)(p + agg + arr + deg + reth);
-    sw->st.hdr = (uint32_t *)(p + agg + arr + deg + reth + gen);
     sw->st.first = (uint64_t *)(p + sw->first_off);
     sw->st.slots = slots;
     sw->st.fan_in = fan_in;
