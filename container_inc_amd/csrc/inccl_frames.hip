@@ -6,15 +6,16 @@
 // :141-195 (crc32), :106-127 (ipv4_checksum).
 //
 // A batch of frames (frame index = arrival order) goes through
-//   k_ingress_claim   a lane per frame: parse + validate, degree, and the
-//                     first copy of every (slot, port) by a batch-tagged atomicMin
+//   k_ingress_claim   a lane per frame: parse + validate, and the first copy of
+//                     every (slot, port) by a batch-tagged atomicMin
 //   k_ingress_classify  a lane per frame: classify in the reference's serial
 //                     order (nts.c:353-372), the arrival bitmap, the RETH keeper
 //                     (:442), the recycle (:235-242, :367)
 //   k_ingress_sum     a wave per two consecutive frames: each completed or
 //                     absorbed PSN's counted arrivals summed into its aggregate
-//                     (:361-363)
-//   k_egress<F>       persistent, a wave per input frame: the COMPLETED
+//                     (:361-363), every data frame counted in its slot's degree
+//                     (:351)
+//   k_egress<F>       persistent, a wave per 16 input frames: the COMPLETED
 //                     broadcasts (:447-453) and REPLAY resends (:353-356) from the
 //                     state ingress left, frames per util.c:331-442
 // inccl_switch_ingress runs the first three, inccl_switch_egress the last,
@@ -65,6 +66,12 @@ __device__ __forceinline__ int masked_pos(int i)
 // byte extracts as byte extracts (one SDWA select each) instead of folding them
 // back into a shift + mask of the original word
 __device__ __forceinline__ uint32_t opaque_u32(uint32_t v)
+{
+    asm("" : "+v"(v));
+    return v;
+}
+
+__device__ __forceinline__ uint64_t opaque64(uint64_t v)
 {
     asm("" : "+v"(v));
     return v;
@@ -326,10 +333,14 @@ __device__ __forceinline__ void put16(uint8_t* p, uint32_t v)
 // block builds the 2*fan_in images once into LDS and frames copy them word-wise.
 constexpr int kHdrImg = 80;   // 70 header bytes (with RETH slot), rows 16-byte aligned (read as 16-byte chunks)
 
-__device__ void build_header_image(uint8_t* fr, const InccFrameTemplate& h, bool wf)
+__device__ void build_header_image(uint32_t (&w)[kHdrImg / 4], const InccFrameTemplate& h, bool wf)
 {
+    // built in registers (every index a constant once unrolled), stored as words
+    uint8_t fr[kHdrImg];
     const int total = 14 + 20 + 8 + 12 + (wf ? 16 : 0) + kLanes * 4 + 4;   // util.c:341-345
+#pragma unroll
     for (int i = 0; i < kHdrImg; ++i) fr[i] = 0;
+#pragma unroll
     for (int i = 0; i < 6; ++i) {                                    // util.c:348-351
         fr[i] = h.dst_mac[i];
         fr[6 + i] = h.src_mac[i];
@@ -341,11 +352,13 @@ __device__ void build_header_image(uint8_t* fr, const InccFrameTemplate& h, bool
     ip[4] = 0x11; ip[5] = 0x11;
     put16(ip + 6, 0x4000);
     ip[8] = 0x40; ip[9] = 0x11;
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
         ip[12 + i] = (uint8_t)(h.src_ip >> (8 * i));                 // stored as-is (network order value)
         ip[16 + i] = (uint8_t)(h.dst_ip >> (8 * i));
     }
     uint32_t sum = 0;                                                // util.c:106-127
+#pragma unroll
     for (int i = 0; i < 20; i += 2) sum += ((uint32_t)ip[i] << 8) | ip[i + 1];
     while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
     put16(ip + 10, (~sum) & 0xFFFF);
@@ -357,6 +370,10 @@ __device__ void build_header_image(uint8_t* fr, const InccFrameTemplate& h, bool
     bth[2] = 0xFF; bth[3] = 0xFF;
     const uint32_t q = h.qp & 0x00FFFFFFu;
     bth[4] = (uint8_t)(q >> 24); bth[5] = (uint8_t)(q >> 16); bth[6] = (uint8_t)(q >> 8); bth[7] = (uint8_t)q;
+#pragma unroll
+    for (int i = 0; i < kHdrImg / 4; ++i)
+        w[i] = (uint32_t)fr[4 * i] | ((uint32_t)fr[4 * i + 1] << 8) | ((uint32_t)fr[4 * i + 2] << 16) |
+               ((uint32_t)fr[4 * i + 3] << 24);
 }
 
 // Egress ICRC by linearity.  The raw CRC (init 0, no final XOR) of a message
@@ -452,8 +469,12 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
     // rows are 4-byte aligned and at least 64 bytes: the header fields from four
     // dword loads (bytes 36-43 and 48-55 of the row) instead of byte loads
     const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + f * stride);
-    const uint32_t w9 = fw[9], w10 = fw[10], w12 = fw[12], w13 = fw[13];
-    const int port = ports[f];
+    // (all five loads issued before the first use, one wait: through opaque
+    // copies, since the compiler would otherwise sink some into the branches
+    // below and wait for them one after another)
+    const uint32_t w9 = opaque_u32(fw[9]), w10 = opaque_u32(fw[10]), w12 = opaque_u32(fw[12]);
+    const uint32_t w13 = opaque_u32(fw[13]);
+    const int port = (int)opaque_u32((uint32_t)ports[f]);
     const uint8_t op = (uint8_t)(w10 >> 16);                                    // byte 42
     const uint32_t psn = ((w12 >> 24) << 16) | ((w13 & 0xFFu) << 8) | ((w13 >> 8) & 0xFFu);   // bytes 51-53, nts.c:311
     const int udp_len = (int)(((w9 >> 16) & 0xFFu) << 8 | (w9 >> 24));          // bytes 38-39
@@ -467,7 +488,7 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
         if (data_len != kLanes * 4 || 54 + (wf ? 16 : 0) + kLanes * 4 > stride) act = INCCL_SW_INVALID;
         else {
             const uint32_t slot = psn & (s.slots - 1);
-            atomicAdd(&s.degree[slot], 1);                       // nts.c:351 / :431
+            // (the slot's degree counts this arrival in k_ingress_sum)
             atomicMin(reinterpret_cast<unsigned long long*>(&s.first[(size_t)slot * s.fan_in + port]),
                       (unsigned long long)first_key(g, f, wf));
             act = kActPending | (wf ? 0x200 : 0) | op;
@@ -570,39 +591,56 @@ __global__ __launch_bounds__(kClassifyBlock) void k_ingress_classify(InccSwitchS
     const int64_t f = (int64_t)blockIdx.x * kClassifyBlock + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) s.gen[0] = g;   // the next batch's claim adds one
     if (f >= count) return;
-    const int act = action[f];
+    // round trip 1: the claim results; round trip 2: the slot's arrival words,
+    // the first-copy keys (fan_in <= 8 at once) and, for a WRITE_FIRST frame,
+    // its RETH (frame bytes 54-69, 4-byte aligned row) before it is known to count
+    const int act = (int)opaque_u32((uint32_t)action[f]);
+    const int port = (int)opaque_u32((uint32_t)ports[f]);
+    const uint32_t psn = opaque_u32(psns[f]);
     if (!(act & kActPending)) return;   // ACK, INVALID, IGNORED: final at claim
-    const int fan = s.fan_in, port = ports[f];
-    const uint32_t psn = psns[f], slot = psn & (s.slots - 1), wf = ((uint32_t)act >> 9) & 1u;
+    const int fan = s.fan_in;
+    const uint32_t slot = psn & (s.slots - 1), wf = ((uint32_t)act >> 9) & 1u;
     const uint32_t tag = ~g, result_bit = 1u << fan;
-    const uint32_t pre = arrival_before(s.arrival[2 * (size_t)slot], s.arrival[2 * (size_t)slot + 1], g);
+    const uint64_t a0 = s.arrival[2 * (size_t)slot], a1 = s.arrival[2 * (size_t)slot + 1];
+    constexpr int kKeys = 8;
+    uint64_t key[kKeys];
+#pragma unroll
+    for (int p = 0; p < kKeys; ++p) key[p] = p < fan ? s.first[(size_t)slot * fan + p] : 0ull;
+    uint32_t rw[5] = {0u, 0u, 0u, 0u, 0u};
+    if (wf) {
+        const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + f * stride);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) rw[j] = fw[13 + j];
+    }
+    const uint32_t pre = arrival_before(opaque64(a0), opaque64(a1), g);
     // the PSN's ports: which count in this batch (first copy, not in before),
     // when each counts (1 + frame index; 0 = before the batch, ~0 = not yet)
     uint32_t cports = 0, wfs = 0, done = 0, mine = 0xFFFFFFFFu;
-    for (int p = 0; p < fan; ++p) {
-        const uint64_t key = s.first[(size_t)slot * fan + p];
-        const bool in_batch = (uint32_t)(key >> 32) == tag, before = (pre >> p) & 1u;
-        const uint32_t ef = (uint32_t)key >> 1;
+    auto port_key = [&](int p, uint64_t k) {
+        const bool in_batch = (uint32_t)(k >> 32) == tag, before = (pre >> p) & 1u;
+        const uint32_t ef = (uint32_t)k >> 1;
         done = max(done, before ? 0u : (in_batch ? ef + 1u : 0xFFFFFFFFu));
         if (in_batch && !before) {
             cports |= 1u << p;
-            wfs |= ((uint32_t)key & 1u) << p;
+            wfs |= ((uint32_t)k & 1u) << p;
         }
         if (p == port) mine = in_batch ? ef : 0xFFFFFFFFu;
-    }
+    };
+#pragma unroll
+    for (int p = 0; p < kKeys; ++p)
+        if (p < fan) port_key(p, key[p]);
+    for (int p = kKeys; p < fan; ++p) port_key(p, s.first[(size_t)slot * fan + p]);
     const uint32_t fi = (uint32_t)f;
     const bool counted = !((pre >> port) & 1u) && mine == fi;   // nts.c:359-363
     int fin;
     if (counted) {
         fin = done == fi + 1u ? INCCL_SW_COMPLETED : INCCL_SW_ABSORBED;   // nts.c:365
-        if (wf) {   // the RETH into the keeper (nts.c:442): frame bytes 54-69, 4-byte aligned row
-            const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + f * stride);
-            const uint32_t w13 = fw[13], w14 = fw[14], w15 = fw[15], w16 = fw[16], w17 = fw[17];
+        if (wf) {   // the RETH into the keeper (nts.c:442)
             uint32_t* kp = s.reth + ((size_t)slot * fan + port) * 4;
-            kp[0] = __builtin_amdgcn_alignbyte(w14, w13, 2);
-            kp[1] = __builtin_amdgcn_alignbyte(w15, w14, 2);
-            kp[2] = __builtin_amdgcn_alignbyte(w16, w15, 2);
-            kp[3] = __builtin_amdgcn_alignbyte(w17, w16, 2);
+            kp[0] = __builtin_amdgcn_alignbyte(rw[1], rw[0], 2);
+            kp[1] = __builtin_amdgcn_alignbyte(rw[2], rw[1], 2);
+            kp[2] = __builtin_amdgcn_alignbyte(rw[3], rw[2], 2);
+            kp[3] = __builtin_amdgcn_alignbyte(rw[4], rw[3], 2);
         }
     } else {   // retransmit: nts.c:353-357
         const bool done_before = (pre & result_bit) != 0;
@@ -657,9 +695,23 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
     int act[2];
     act[0] = have ? act_in[f0] : 0;
     act[1] = in1 ? act_in[f1] : 0;
-    if (!((act[0] | act[1]) & kActLeader)) return;
-    const int port[2] = {ports_in[f0], ports_in[f1]};
     const uint32_t psn[2] = {psns_in[f0], psns_in[f1]};
+    // every data frame's arrival into its slot's degree (nts.c:351 / :431,
+    // retransmits included), as the wave's last memory instructions: atomics
+    // issued before a wait would be waited for with it
+    auto degrees = [&]() {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int a = act[k] & 0xFF;
+            if ((k == 0 ? have : in1) && a >= INCCL_SW_ABSORBED && a <= INCCL_SW_REPLAY && lane == 0)
+                atomicAdd(&s.degree[psn[k] & (s.slots - 1)], 1);
+        }
+    };
+    if (!((act[0] | act[1]) & kActLeader)) {
+        degrees();
+        return;
+    }
+    const int port[2] = {ports_in[f0], ports_in[f1]};
     // payload words 4 lane .. 4 lane + 3 of pair frame k (payload at byte 54 + 16 wf)
     auto payload_of = [&](int k, uint32_t wf, uint32_t (&P)[4]) {
         if (A.wide) {
@@ -723,6 +775,7 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
         __builtin_nontemporal_store(acc, reinterpret_cast<u4*>(s.agg + (size_t)slot * kLanes) + lane);
         if (lane == 0) A.action[f0 + k] = act[k] & 0xFF;
     }
+    degrees();
 }
 
 // ---------------------------------------------------------------------------
@@ -733,23 +786,23 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
 //
 // Persistent 16-wave blocks, two per CU: each block loads the CRC tables into
 // LDS and builds the 2 fan_in header images and their ICRC terms H_c once.  A
-// wave then walks input frames, one per iteration, with the next frame's
-// aggregate and keeper and the claim results of the frame after that in
-// flight.  Loads and stores retire in order on one counter (vmcnt), so that
-// the compiler can wait for a prefetched load without also waiting for the
-// stores issued after it, every iteration issues the same memory instructions:
-// the children loop unrolled for a fixed fan-in (2, 3, 4, 8), every load and
-// store unconditional -- a frame that emits nothing, or a child that gets no
-// frame, is given a zero-size buffer (its loads return 0, its stores are
-// dropped, neither reaches memory) -- and all CRC work in branches without
-// memory instructions.  Two register sets take alternate frames (a copy
-// between them would wait for the load in flight).
+// wave then takes 16 consecutive input frames at a time, lane l frame l: their
+// claim results and header words in four vector loads, the row lengths of all
+// 16 x fan_in rows lane-parallel, and then only the frames that emit, one after
+// another, each frame's aggregate and keeper in flight while the frame before
+// it is built.  (A wave per input frame spent as long on the absorbed half of
+// the frames, which emit nothing, as on the rest: 58-60 against 56-57 us per
+// 131 072-frame batch, profiles/r04/.)
 //
-// Round r of a wave covers frames [r step, (r + 1) step), step = the grid's
-// waves; in round r wave v takes frame r step + (v + r) mod step.  Rotating
-// by one per round balances the waves: only every fan_in-th frame of a PSN
-// completes it, and with a fixed offset (step is even) the waves of the other
-// residues would idle while the rest built every output frame.
+// Loads and stores retire in order on one counter (vmcnt).  So that the
+// compiler can wait for the prefetched aggregate without also waiting for the
+// stores issued after it, every emitted frame issues the same memory
+// instructions: the children loop unrolled for a fixed fan-in (2, 3, 4, 8),
+// every load and store unconditional -- a frame that emits nothing, or a child
+// that gets no frame, is given a zero-size buffer (its loads return 0, its
+// stores are dropped, neither reaches memory) -- and all CRC work in branches
+// without memory instructions.  Two register sets take alternate frames (a
+// copy between them would wait for the load in flight).
 //
 // The payload goes from registers to the rows: lane l holds payload bytes
 // [16 l, 16 l + 16) (htonl of the aggregate, util.c:403-405 / :419-421), frame
@@ -764,6 +817,8 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
 // frame, one RETH reduction per RETH child.
 // ---------------------------------------------------------------------------
 constexpr int kEgressWaves = 16;
+constexpr int kEgressChunk = 16;   // input frames per wave at a time (lanes 0-15)
+constexpr int kEgressAhead = 1;    // emitting frames whose aggregate is in flight ahead of the one emitted
 
 __device__ uint32_t g_segb[16][256];   // [byte j of a 16-byte segment][value] = Z_{15-j}(T[value])
 
@@ -807,11 +862,28 @@ __device__ __forceinline__ uint32_t seg16(const EgressLds& t, const uint32_t (&a
 // and the quad's XOR is shifted past the 1024-byte payload.
 __device__ void egress_setup(EgressLds& t, const InccFrameTemplate* __restrict__ tmpl, int fan)
 {
-    for (int i = threadIdx.x; i < 16 * 256; i += blockDim.x) (&t.segb[0][0])[i] = (&g_segb[0][0])[i];
-    for (int i = threadIdx.x; i < 8 * 16 * kWave; i += blockDim.x) (&t.lane16[0][0][0])[i] = (&g_lane16[0][0][0])[i];
-    for (int i = threadIdx.x; i < kVarRows * 2 * 16; i += blockDim.x) (&t.var[0][0][0])[i] = (&g_var[0][0][0])[i];
-    for (int i = threadIdx.x; i < 8 * 16; i += blockDim.x) (&t.z1024[0][0])[i] = (&g_z1024[0][0])[i];
-    for (int i = threadIdx.x; i < 2 * fan; i += blockDim.x) build_header_image(t.img[i], tmpl[i >> 1], (i & 1) != 0);
+    // the tables as 16-byte words, every thread's loads issued before its
+    // stores (one round trip, not one per word); blocks of kEgressWaves waves
+    static_assert(kWave * kEgressWaves == 1024, "the copy below assumes 1024-thread blocks");
+    const int x = threadIdx.x;
+    const u4* gs = reinterpret_cast<const u4*>(&g_segb[0][0]);       // 1024 words
+    const u4* gl = reinterpret_cast<const u4*>(&g_lane16[0][0][0]);  // 2048
+    const u4* gv = reinterpret_cast<const u4*>(&g_var[0][0][0]);     // kVarRows * 8
+    const u4* gz = reinterpret_cast<const u4*>(&g_z1024[0][0]);      // 32
+    const u4 s0 = gs[x], l0 = gl[x], l1 = gl[x + 1024];
+    const u4 v0 = x < kVarRows * 8 ? gv[x] : u4{}, z0 = x < 32 ? gz[x] : u4{};
+    uint32_t img[kHdrImg / 4];
+    if (x < 2 * fan) build_header_image(img, tmpl[x >> 1], (x & 1) != 0);
+    reinterpret_cast<u4*>(&t.segb[0][0])[x] = s0;
+    reinterpret_cast<u4*>(&t.lane16[0][0][0])[x] = l0;
+    reinterpret_cast<u4*>(&t.lane16[0][0][0])[x + 1024] = l1;
+    if (x < kVarRows * 8) reinterpret_cast<u4*>(&t.var[0][0][0])[x] = v0;
+    if (x < 32) reinterpret_cast<u4*>(&t.z1024[0][0])[x] = z0;
+    if (x < 2 * fan) {
+#pragma unroll
+        for (int k = 0; k < kHdrImg / 16; ++k)
+            reinterpret_cast<u4*>(t.img[x])[k] = u4{img[4 * k], img[4 * k + 1], img[4 * k + 2], img[4 * k + 3]};
+    }
     __syncthreads();
     const int i = threadIdx.x >> 2, q = threadIdx.x & 3;
     uint32_t c = 0;
@@ -863,8 +935,7 @@ struct EgressArgs {
     int fan;
 };
 
-// One input frame as an egress wave knows it: three wave-uniform words (two
-// frames are in flight at a time, so they are packed)
+// One input frame as an egress wave knows it: three wave-uniform words
 struct EgressF {
     uint32_t f, psn;
     uint32_t bits;   // opcode | WRITE_FIRST << 8 | in << 9 | all << 10 | one << 11 | port << 16
@@ -875,48 +946,6 @@ struct EgressF {
     __device__ bool one() const { return (bits >> 11) & 1u; }   // REPLAY: child port()
     __device__ uint32_t port() const { return bits >> 16; }
 };
-
-// Lanes 0-3 load frame f's action, port, PSN and header dword 10 (opcode: byte
-// 42), lanes 4-63 again the same four: one vector load, counted on vmcnt with
-// the rest.  Each lane's array base and element size are set once (MetaLane),
-// so the address is one multiply-add.  Past the end: the last frame's (unused).
-struct MetaLane {
-    const uint8_t* base;
-    uint32_t scale;
-};
-
-__device__ __forceinline__ MetaLane meta_lane(const EgressArgs& A, int lane)
-{
-    MetaLane m;
-    const int k = lane & 3;
-    m.base = k == 0   ? reinterpret_cast<const uint8_t*>(A.action)
-             : k == 1 ? reinterpret_cast<const uint8_t*>(A.ports)
-             : k == 2 ? reinterpret_cast<const uint8_t*>(A.psns)
-                      : A.frames + 40;
-    m.scale = k == 3 ? A.stride : 4u;
-    return m;
-}
-
-__device__ __forceinline__ uint32_t egress_meta(const EgressArgs& A, const MetaLane& ml, uint32_t f)
-{
-    const uint32_t fc = f < A.count ? f : A.count - 1;
-    return *reinterpret_cast<const uint32_t*>(ml.base + (size_t)fc * ml.scale);
-}
-
-__device__ __forceinline__ EgressF egress_decode(const EgressArgs& A, uint32_t m, uint32_t f)
-{
-    EgressF e;
-    e.f = f;
-    const int act = __builtin_amdgcn_readlane((int)m, 0);
-    const uint32_t port = (uint32_t)__builtin_amdgcn_readlane((int)m, 1);
-    e.psn = (uint32_t)__builtin_amdgcn_readlane((int)m, 2);
-    const uint32_t op = ((uint32_t)__builtin_amdgcn_readlane((int)m, 3) >> 16) & 0xFFu;
-    const bool in = f < A.count;
-    const bool one = in && act == INCCL_SW_REPLAY && port < (uint32_t)A.fan;
-    e.bits = op | (is_write_first((uint8_t)op) ? 1u << 8 : 0u) | (in ? 1u << 9 : 0u) |
-             (in && act == INCCL_SW_COMPLETED ? 1u << 10 : 0u) | (one ? 1u << 11 : 0u) | ((port & 0xFFFFu) << 16);
-    return e;
-}
 
 // the slot's aggregate (this lane's four words) and RETH keeper (lane 4 c + j:
 // word j of child c's, c < 16); nothing for a frame that emits nothing
@@ -932,8 +961,8 @@ __device__ __forceinline__ void egress_load(const EgressArgs& A, const EgressF& 
     keep = __builtin_amdgcn_raw_buffer_load_b32(rk, 4 * lane, 0, 0);
 }
 
-// Frame e's output rows and their lengths.
-template <int kFan, bool kOut16, int kX = 0>
+// Frame e's output rows (their lengths are stored per chunk, k_egress).
+template <int kFan, bool kOut16>
 __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs& A, const EgressF& e, const u4& acc,
                                             uint32_t keep, int lane)
 {
@@ -941,13 +970,6 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
     const uint32_t wf = e.wf(), op = e.op(), port = e.port();
     const bool all = e.all(), one = e.one();
     const bool em_any = all || one;
-    if (!(kX & 8)) {   // row lengths, lanes c < fan_in (util.c:341-345)
-        const int total = 54 + 16 * (int)wf + kLanes * 4 + 4;
-        const __amdgpu_buffer_rsrc_t rl =
-            __builtin_amdgcn_make_buffer_rsrc(A.out_len + (size_t)e.f * fan, 0, e.in() ? 4 * fan : 0, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(
-            (all || (one && (uint32_t)lane == port)) ? (uint32_t)total : 0u, rl, 4 * lane, 0, 0);
-    }
     const bool last = lane == kWave - 1;
     // (a frame that emits nothing stores nowhere: its values are left undefined)
     uint32_t pc = unset(), p0 = unset(), p1 = unset(), p2 = unset(), p3 = unset();
@@ -963,7 +985,7 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
         // and the PSN bytes' (util.c:378, :386)
         const uint32_t vb = lane == 0 ? op : (pw >> (8 * (4 - lane))) & 0xFFu;
         const uint32_t var = lane < 5 ? var_crc(t, (int)wf, lane, vb) : 0u;
-        pc = (kX & 1) ? var : wave_xor(seg16(t, a, lane) ^ var);
+        pc = wave_xor(seg16(t, a, lane) ^ var);
         const int next4 = ((lane + 1) & (kWave - 1)) * 4;
         const uint32_t n0 = from_next(a[0], next4), n1 = from_next(a[1], next4), n2 = from_next(a[2], next4);
         p0 = __builtin_amdgcn_alignbyte(a[3], a[2], 2);
@@ -1002,7 +1024,7 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
             h.z |= patch.z;
             h.w |= patch.w;
             uint32_t crc = pc ^ t.hcrc[2 * c + wf];
-            if (wf && !(kX & 4)) {
+            if (wf) {
                 // child c's RETH (reth_keeper[slot][c], nts.c:442; util.c:409-417):
                 // bytes 54-69, lane 3's chunk from byte 6 on and lane 4's first 6
                 // bytes; its ICRC term on lanes 0-15
@@ -1030,7 +1052,7 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
             v = u4{p0, last ? p1 | (crc << 16) : p1, last ? crc >> 16 : p2, p3};
         }
         const __amdgpu_buffer_rsrc_t orow =
-            __builtin_amdgcn_make_buffer_rsrc(row, 0, em && !(kX & 2) ? (int)A.out_stride : 0, 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc(row, 0, em ? (int)A.out_stride : 0, 0x00020000);
         row += A.out_stride;
         if (kOut16) {
             __builtin_amdgcn_raw_buffer_store_b128(h, orow, ho, 0, kAuxNt);
@@ -1051,94 +1073,29 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
 
 // kFan: 2, 3, 4 or 8 (the children loop unrolled), or 0 (A.fan, a loop).
 // kOut16: 16-byte aligned output rows.
-template <int kFan, bool kOut16, int kX = 0>
+template <int kFan, bool kOut16>
 __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_egress(
-    EgressArgs A)
-{
-    __shared__ EgressLds t;
-    egress_setup(t, A.tmpl, kFan ? kFan : A.fan);
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane0 = threadIdx.x % kWave;
-    const uint32_t step = gridDim.x * kEgressWaves, count = A.count;
-    const uint32_t rot0 = blockIdx.x * kEgressWaves + w;
-    // this wave's frames: f_r = r step + (rot0 + r) mod step for r < n (every
-    // round before count / step, and that round if its frame is below count)
-    const uint32_t rounds = count / step, rem = count % step;
-    const uint32_t n = rounds + ((rot0 + rounds) % step < rem ? 1u : 0u);
-    if (n == 0) return;
-    uint32_t cb = 0, cr = rot0;   // the cursor: the newest frame whose claim results were requested
-    auto advance = [&]() {
-        cb += step;
-        cr = cr + 1 == step ? 0 : cr + 1;
-        return cb + cr;
-    };
-    // the lane number through an opaque copy per use: what a frame derives from
-    // it is computed per frame, not hoisted out of the loop into registers held
-    // for the whole kernel
-    auto ln = [&]() { return (int)opaque_u32((uint32_t)lane0); };
-    const MetaLane ml = meta_lane(A, lane0);
-    // Two frames per iteration, set a then set b; entering iteration j the
-    // claim results of frame 2j (ma, decoded) and 2j+1 (mb, in flight) and
-    // frame 2j's aggregate and keeper (in flight) were issued.  A frame at or
-    // past n is past count: it emits nothing and its stores are dropped.
-    uint32_t fa = rot0, fb = advance();
-    const uint32_t ma = egress_meta(A, ml, fa);
-    uint32_t mb = egress_meta(A, ml, fb);
-    EgressF ea = egress_decode(A, ma, fa), eb;
-    u4 acca, accb;
-    uint32_t keepa, keepb;
-    egress_load(A, ea, ln(), acca, keepa);
-    if (kFan) {
-        // as many dropped stores as an iteration issues: the loop is entered
-        // with its back edge's memory history, so its waits are counts, not 0
-        const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(A.out_len, 0, 0, 0x00020000);
-#pragma unroll
-        for (int k = 0; k < 1 + kFan * (kOut16 ? 2 : 8); ++k)
-            __builtin_amdgcn_raw_buffer_store_b32(0u, none, 16 * k, 0, 0);   // apart: none is merged away
-    }
-    for (uint32_t j = 0;; j += 2) {
-        const uint32_t fa2 = advance();
-        const uint32_t ma2 = egress_meta(A, ml, fa2);
-        eb = egress_decode(A, mb, fb);
-        egress_load(A, eb, ln(), accb, keepb);
-        egress_emit<kFan, kOut16, kX>(t, A, ea, acca, keepa, ln());
-        fb = advance();
-        mb = egress_meta(A, ml, fb);
-        ea = egress_decode(A, ma2, fa2);
-        egress_load(A, ea, ln(), acca, keepa);
-        egress_emit<kFan, kOut16, kX>(t, A, eb, accb, keepb, ln());
-        if (j + 2 >= n) break;
-    }
-}
-
-
-// Chunked egress (experiment): a wave takes kC consecutive input frames at a
-// time, lane l frame c kC + l; their claim results and opcodes in four vector
-// loads, the row lengths of the whole chunk lane-parallel, then only the frames
-// that emit, two register sets alternating, each frame's aggregate and keeper
-// one frame ahead.
-template <int kFan, bool kOut16, int kC, int kD>
-__global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_egress_chunk(
     EgressArgs A)
 {
     __shared__ EgressLds t;
     const int fan = kFan ? kFan : A.fan;
     egress_setup(t, A.tmpl, fan);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane0 = threadIdx.x % kWave;
-    const uint32_t count = A.count, chunks = (count + kC - 1) / kC;
+    const uint32_t count = A.count, chunks = (count + kEgressChunk - 1) / kEgressChunk;
     const uint32_t nw = gridDim.x * kEgressWaves;
     auto ln = [&]() { return (int)opaque_u32((uint32_t)lane0); };
     for (uint32_t ch = blockIdx.x * kEgressWaves + w; ch < chunks; ch += nw) {
         const int lane = ln();
-        const uint32_t f0 = ch * kC, nf = min((uint32_t)kC, count - f0);
+        const uint32_t f0 = ch * kEgressChunk, nf = min((uint32_t)kEgressChunk, count - f0);
         const int off = lane < (int)nf ? 4 * lane : kOobOffset;
         const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<int32_t*>(A.action) + f0, 0, 4 * kC, 0x00020000);
+            const_cast<int32_t*>(A.action) + f0, 0, 4 * kEgressChunk, 0x00020000);
         const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<int32_t*>(A.ports) + f0, 0, 4 * kC, 0x00020000);
+            const_cast<int32_t*>(A.ports) + f0, 0, 4 * kEgressChunk, 0x00020000);
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint32_t*>(A.psns) + f0, 0, 4 * kC, 0x00020000);
+            const_cast<uint32_t*>(A.psns) + f0, 0, 4 * kEgressChunk, 0x00020000);
         const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(A.frames) + (size_t)f0 * A.stride, 0, (int)(kC * A.stride), 0x00020000);
+            const_cast<uint8_t*>(A.frames) + (size_t)f0 * A.stride, 0, (int)(kEgressChunk * A.stride), 0x00020000);
         const int act = (int)__builtin_amdgcn_raw_buffer_load_b32(ra, off, 0, 0);
         const uint32_t port = __builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, 0);
         const uint32_t psn = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
@@ -1153,7 +1110,7 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
         {   // the chunk's row lengths: entry e = f fan + c, lane-parallel (util.c:341-345)
             const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
                 A.out_len + (size_t)f0 * fan, 0, (int)(4 * nf * fan), 0x00020000);
-            for (int k = 0; k < (kC * fan + kWave - 1) / kWave; ++k) {
+            for (int k = 0; k < (kEgressChunk * fan + kWave - 1) / kWave; ++k) {
                 const int e = lane + kWave * k, fr = e / fan, c = e - fr * fan;
                 const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (fr & (kWave - 1)), (int)bits);
                 const bool on = ((b >> 10) & 1u) || (((b >> 11) & 1u) && (b >> 16) == (uint32_t)c);
@@ -1163,45 +1120,52 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
         }
         uint64_t m = __ballot(all || one);
         if (!m) continue;
-        auto take = [&](EgressF& e) {   // the next emitting frame of the chunk, or none
+        // a frame of the ring is its lane in the chunk (-1: none); its words
+        // are read from the chunk's registers where used
+        auto take = [&]() {
+            int b = -1;
             if (m) {
-                const int b = __builtin_ctzll(m);
+                b = __builtin_ctzll(m);
                 m &= m - 1;
-                e.f = f0 + b;
-                e.psn = (uint32_t)__builtin_amdgcn_readlane((int)psn, b);
-                e.bits = (uint32_t)__builtin_amdgcn_readlane((int)bits, b);
-            } else {
-                e.f = f0;
-                e.psn = 0;
-                e.bits = 0;
             }
+            return b;
         };
-        // a ring of kD + 1 frames: frame j's aggregate and keeper are loaded kD
-        // frames before it is emitted
-        constexpr int kR = kD + 1;
-        EgressF E[kR];
+        auto frame = [&](int b) {
+            EgressF e;
+            e.f = f0 + (uint32_t)max(b, 0);
+            e.psn = b >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)psn, b) : 0u;
+            e.bits = b >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)bits, b) : 0u;
+            return e;
+        };
+        // a ring of kEgressAhead + 1 frames: a frame's aggregate and keeper are
+        // loaded kEgressAhead emitting frames before it is built (deeper rings,
+        // 2 and 3, measured no faster: the stores bound this loop)
+        constexpr int kR = kEgressAhead + 1;
+        int B[kR];
         u4 acc[kR];
         uint32_t keep[kR];
 #pragma unroll
-        for (int r = 0; r < kD; ++r) {
-            take(E[r]);
-            egress_load(A, E[r], ln(), acc[r], keep[r]);
+        for (int r = 0; r < kEgressAhead; ++r) {
+            B[r] = take();
+            egress_load(A, frame(B[r]), ln(), acc[r], keep[r]);
         }
         if (kFan) {
+            // as many dropped stores as the frames ahead will issue: the loop is
+            // entered with its back edge's memory history, so its waits are counts
             const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(A.out_len, 0, 0, 0x00020000);
 #pragma unroll
-            for (int k = 0; k < kD * kFan * (kOut16 ? 2 : 8); ++k)
+            for (int k = 0; k < kEgressAhead * kFan * (kOut16 ? 2 : 8); ++k)
                 __builtin_amdgcn_raw_buffer_store_b32(0u, none, 16 * k, 0, 0);
         }
         for (;;) {
             bool more = true;
 #pragma unroll
             for (int r = 0; r < kR; ++r) {
-                const int ld = (r + kD) % kR;
-                take(E[ld]);
-                egress_load(A, E[ld], ln(), acc[ld], keep[ld]);
-                egress_emit<kFan, kOut16, 8>(t, A, E[r], acc[r], keep[r], ln());
-                more = more && E[(r + 1) % kR].in();
+                const int ld = (r + kEgressAhead) % kR;
+                B[ld] = take();
+                egress_load(A, frame(B[ld]), ln(), acc[ld], keep[ld]);
+                egress_emit<kFan, kOut16>(t, A, frame(B[r]), acc[r], keep[r], ln());
+                more = B[(r + 1) % kR] >= 0;
                 if (!more) break;
             }
             if (!more) break;
@@ -1313,36 +1277,21 @@ int launch_apply(const ApplyArgs& a, hipStream_t st)
     return (int)hipGetLastError();
 }
 
-template <int kFan, bool kOut16, int kC, int kD>
-int launch_egress_chunk(const EgressArgs& a, hipStream_t st)
-{
-    static const int per_cu = [] {
-        int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_egress_chunk<kFan, kOut16, kC, kD>, kWave * kEgressWaves, 0) !=
-                hipSuccess || n < 1)
-            n = 1;
-        return n;
-    }();
-    const int64_t chunks = ((int64_t)a.count + kC - 1) / kC;
-    const int64_t need = (chunks + kEgressWaves - 1) / kEgressWaves, cap = (int64_t)num_cus() * per_cu;
-    hipLaunchKernelGGL((k_egress_chunk<kFan, kOut16, kC, kD>), dim3((unsigned)(need < cap ? (need < 1 ? 1 : need) : cap)),
-                       dim3(kWave * kEgressWaves), 0, st, a);
-    return (int)hipGetLastError();
-}
-
-// persistent egress: as many blocks as fit beside each other (two per CU)
-template <int kFan, bool kOut16, int kX = 0>
+// persistent egress: a wave per chunk of kEgressChunk frames, as many blocks as
+// fit beside each other (two per CU)
+template <int kFan, bool kOut16>
 int launch_egress_t(const EgressArgs& a, hipStream_t st)
 {
     static const int per_cu = [] {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_egress<kFan, kOut16, kX>, kWave * kEgressWaves, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_egress<kFan, kOut16>, kWave * kEgressWaves, 0) !=
                 hipSuccess || n < 1)
             n = 1;
         return n;
     }();
-    const int64_t need = ((int64_t)a.count + kEgressWaves - 1) / kEgressWaves, cap = (int64_t)num_cus() * per_cu;
-    hipLaunchKernelGGL((k_egress<kFan, kOut16, kX>), dim3((unsigned)(need < cap ? (need < 1 ? 1 : need) : cap)),
+    const int64_t chunks = ((int64_t)a.count + kEgressChunk - 1) / kEgressChunk;
+    const int64_t need = (chunks + kEgressWaves - 1) / kEgressWaves, cap = (int64_t)num_cus() * per_cu;
+    hipLaunchKernelGGL((k_egress<kFan, kOut16>), dim3((unsigned)(need < cap ? (need < 1 ? 1 : need) : cap)),
                        dim3(kWave * kEgressWaves), 0, st, a);
     return (int)hipGetLastError();
 }
@@ -1351,21 +1300,7 @@ template <bool kOut16>
 int launch_egress_o(const EgressArgs& a, hipStream_t st)
 {
     switch (a.fan) {   // fan-in 2, 3, 4, 8: the children loop unrolled; others a loop
-    case 2: {
-        static const int x = getenv("INCCL_T_EGRESS_X") ? atoi(getenv("INCCL_T_EGRESS_X")) : 0;
-        if (x == 1) return launch_egress_t<2, kOut16, 1>(a, st);
-        if (x == 2) return launch_egress_t<2, kOut16, 2>(a, st);
-        if (x == 4) return launch_egress_t<2, kOut16, 4>(a, st);
-        if (x == 3) return launch_egress_t<2, kOut16, 3>(a, st);
-        if (x == 7) return launch_egress_t<2, kOut16, 7>(a, st);
-        if (x == 16) return launch_egress_chunk<2, kOut16, 16, 1>(a, st);
-        if (x == 162) return launch_egress_chunk<2, kOut16, 16, 2>(a, st);
-        if (x == 163) return launch_egress_chunk<2, kOut16, 16, 3>(a, st);
-        if (x == 322) return launch_egress_chunk<2, kOut16, 32, 2>(a, st);
-        if (x == 323) return launch_egress_chunk<2, kOut16, 32, 3>(a, st);
-        if (x == 324) return launch_egress_chunk<2, kOut16, 32, 4>(a, st);
-        return launch_egress_t<2, kOut16>(a, st);
-    }
+    case 2: return launch_egress_t<2, kOut16>(a, st);
     case 3: return launch_egress_t<3, kOut16>(a, st);
     case 4: return launch_egress_t<4, kOut16>(a, st);
     case 8: return launch_egress_t<8, kOut16>(a, st);

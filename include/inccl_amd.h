@@ -290,9 +290,7 @@ int inccl_switch_egress(struct inccl_switch *sw, const uint8_t *frames_dev, size
                         int32_t *out_len_dev, void *stream);
 /* inccl_switch_ingress followed by inccl_switch_egress of the same batch, in
  * one call (the reference's pipeline() runs both per frame): the same actions,
- * state, out rows and lengths, but the aggregating kernel builds every
- * COMPLETED frame's broadcast straight from the aggregate in its registers
- * (the aggregate is not read back), and only REPLAY resends take a second pass. */
+ * state, out rows and lengths, from the same kernels on `stream`. */
 int inccl_switch_batch(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
                        const int32_t *ports_dev, int32_t *action_dev, uint32_t *psn_dev,
                        const struct inccl_frame_template *templates_dev, uint8_t *out_dev, size_t out_stride,

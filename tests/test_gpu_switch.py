@@ -3,8 +3,7 @@
 batched ingress (non_termination_switch.c:303-483: first-arrival add,
 retransmit drop / replay) and egress frames (util.c:331-442) byte-exact.  Every
 batch test runs both ways of driving the switch: `split` (inccl_switch_ingress
-then inccl_switch_egress) and `batch` (inccl_switch_batch: the aggregating
-kernel emits the broadcasts itself, REPLAYs in a second pass)."""
+then inccl_switch_egress) and `batch` (inccl_switch_batch: both in one call)."""
 import json
 import os
 

@@ -112,8 +112,8 @@ def main():
         ms = e0.elapsed_time(e1) / iters
         check(mode)   # every PSN of every later batch still completes exactly once
         print(json.dumps({"what": "GPU switch dataplane batch, eager: " +
-                                  ("inccl_switch_ingress (claim / apply) + inccl_switch_egress" if mode == "split" else
-                                   "inccl_switch_batch (claim / apply + broadcast / replay pass)"),
+                                  ("inccl_switch_ingress (claim / classify / sum) + inccl_switch_egress" if mode == "split" else
+                                   "inccl_switch_batch (claim / classify / sum / egress in one call)"),
                           "mode": mode, "fan_in": fan_in, "psns": P, "ingress_frames": fan_in * P,
                           "egress_frames": fan_in * P, "ms": round(ms, 4),
                           "payload_GBs": round(payload_bytes / (ms * 1e-3) / 1e9, 2),
