@@ -45,6 +45,7 @@ constexpr int kWin = 1088;            // ICRC window: the longest message (1098-
 constexpr int kFrameMax = 1152;
 constexpr int kLanes = 256;           // int32 lanes per packet (nts.c:55)
 constexpr int kAuxNt = 2;   // buffer instruction cache policy: nt (streaming, not re-read)
+constexpr int kAuxSc1 = 16;   // buffer instruction cache policy: sc1 (write-through)
 constexpr int kOobOffset = 0x7FFFFFF0;   // past any row: a buffer store there is dropped, a load returns 0
 
 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
@@ -772,7 +773,12 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
             acc.z += q[2];
             acc.w += q[3];
         }
-        __builtin_nontemporal_store(acc, reinterpret_cast<u4*>(s.agg + (size_t)slot * kLanes) + lane);
+        // write-through (sc1): the sum goes to memory and stays in the caches
+        // for egress, which reads it next (49.7-50.0 vs 51.8-52.1 us for egress
+        // against non-temporal stores; the sum kernel itself unchanged,
+        // profiles/r04/switch/agg_store_policy.txt)
+        __builtin_amdgcn_raw_buffer_store_b128(acc, uniform_rsrc(s.agg + (size_t)slot * kLanes, kLanes * 4), 16 * lane, 0,
+                                               kAuxSc1);
         if (lane == 0) A.action[f0 + k] = act[k] & 0xFF;
     }
     degrees();
@@ -1079,29 +1085,46 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
 {
     __shared__ EgressLds t;
     const int fan = kFan ? kFan : A.fan;
-    egress_setup(t, A.tmpl, fan);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane0 = threadIdx.x % kWave;
     const uint32_t count = A.count, chunks = (count + kEgressChunk - 1) / kEgressChunk;
     const uint32_t nw = gridDim.x * kEgressWaves;
     auto ln = [&]() { return (int)opaque_u32((uint32_t)lane0); };
-    for (uint32_t ch = blockIdx.x * kEgressWaves + w; ch < chunks; ch += nw) {
+    // a chunk's claim results and header words (lane l: frame f0 + l; past the
+    // end or past count: zero-size reads)
+    struct ChunkIn {
+        uint32_t act, port, psn, w10;
+    };
+    auto chunk_in = [&](uint32_t ch) {
         const int lane = ln();
-        const uint32_t f0 = ch * kEgressChunk, nf = min((uint32_t)kEgressChunk, count - f0);
+        const uint32_t f0 = ch * kEgressChunk, nf = ch < chunks ? min((uint32_t)kEgressChunk, count - f0) : 0u;
         const int off = lane < (int)nf ? 4 * lane : kOobOffset;
         const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<int32_t*>(A.action) + f0, 0, 4 * kEgressChunk, 0x00020000);
+            const_cast<int32_t*>(A.action) + (ch < chunks ? f0 : 0), 0, 4 * kEgressChunk, 0x00020000);
         const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<int32_t*>(A.ports) + f0, 0, 4 * kEgressChunk, 0x00020000);
+            const_cast<int32_t*>(A.ports) + (ch < chunks ? f0 : 0), 0, 4 * kEgressChunk, 0x00020000);
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint32_t*>(A.psns) + f0, 0, 4 * kEgressChunk, 0x00020000);
+            const_cast<uint32_t*>(A.psns) + (ch < chunks ? f0 : 0), 0, 4 * kEgressChunk, 0x00020000);
         const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(A.frames) + (size_t)f0 * A.stride, 0, (int)(kEgressChunk * A.stride), 0x00020000);
-        const int act = (int)__builtin_amdgcn_raw_buffer_load_b32(ra, off, 0, 0);
-        const uint32_t port = __builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, 0);
-        const uint32_t psn = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
-        const uint32_t w10 = __builtin_amdgcn_raw_buffer_load_b32(
-            rf, lane < (int)nf ? lane * (int)A.stride + 40 : kOobOffset, 0, 0);
-        const uint32_t op = (w10 >> 16) & 0xFFu;
+            const_cast<uint8_t*>(A.frames) + (size_t)(ch < chunks ? f0 : 0) * A.stride, 0,
+            (int)(kEgressChunk * A.stride), 0x00020000);
+        ChunkIn c;
+        c.act = __builtin_amdgcn_raw_buffer_load_b32(ra, off, 0, 0);
+        c.port = __builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, 0);
+        c.psn = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+        c.w10 = __builtin_amdgcn_raw_buffer_load_b32(rf, lane < (int)nf ? lane * (int)A.stride + 40 : kOobOffset, 0, 0);
+        return c;
+    };
+    // the wave's first chunk is read while the block sets up its tables
+    uint32_t ch = blockIdx.x * kEgressWaves + w;
+    ChunkIn cin = chunk_in(ch);
+    egress_setup(t, A.tmpl, fan);
+    for (; ch < chunks; ch += nw) {
+        if (ch != blockIdx.x * kEgressWaves + w) cin = chunk_in(ch);
+        const int lane = ln();
+        const uint32_t f0 = ch * kEgressChunk, nf = min((uint32_t)kEgressChunk, count - f0);
+        const int act = (int)cin.act;
+        const uint32_t port = cin.port, psn = cin.psn;
+        const uint32_t op = (cin.w10 >> 16) & 0xFFu;
         const bool in = lane < (int)nf;
         const bool all = in && act == INCCL_SW_COMPLETED;
         const bool one = in && act == INCCL_SW_REPLAY && port < (uint32_t)fan;
