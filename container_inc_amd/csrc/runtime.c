@@ -76,7 +76,10 @@ static void query_release(void)
     if (init && shut && info && init() == 0) {   /* reference-counted: HIP holds its own */
         const char *b = NULL;
         if (info(HSA_AMD_SYSTEM_INFO_BUILD_VERSION_ATTR, &b) == 0 && b) {
-            snprintf(g_build, sizeof(g_build), "%s", b);
+            /* the string comes quoted ("\"1.18.0-rocm-rel-7.0-...\""): kept without the quotes */
+            const size_t n = strlen(b);
+            const int q = n >= 2 && b[0] == '"' && b[n - 1] == '"';
+            snprintf(g_build, sizeof(g_build), "%.*s", (int)(q ? n - 2 : n), q ? b + 1 : b);
             g_release = inccl_hsa_release_of(b);
         }
         shut();
