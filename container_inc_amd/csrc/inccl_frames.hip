@@ -1016,6 +1016,22 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
     }
     const int hchunks = 4 + (int)wf;   // header + the payload's first 10 bytes
     const int ho = lane < hchunks ? 16 * lane : kOobOffset, po = 16 * (hchunks + lane);
+    // 16-byte rows: a row is two stores, chunks 0-63 (lane l: chunk l) and
+    // 64-67 or 64-68 (lanes 0-3 or 0-4), so that every 64-byte write request
+    // but the row's last is whole (header and payload as separate stores split
+    // the request at the header's end: 19 requests per row against 17).  Lane
+    // l then carries payload chunk l - hchunks (mod 64), the payload rotated
+    // by hchunks lanes, once per input frame; the chunk that ends the frame
+    // (the ICRC's) lands on lane hchunks - 1 of the second store.
+    u4 pr = unset4();
+    if (kOut16 && em_any) {
+        const int from = ((lane - hchunks) & (kWave - 1)) * 4;
+        pr.x = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)p0);
+        pr.y = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)p1);
+        pr.z = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)p2);
+        pr.w = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)p3);
+    }
+    const bool tail = lane == hchunks - 1;   // the frame's last chunk, in the second store
     const uint32_t emit_mask = all ? (1u << fan) - 1u : (one ? 1u << port : 0u);   // children that get a frame
     uint8_t* row = A.out + (size_t)e.f * fan * A.out_stride;
     constexpr int kUnroll = kFan ? kFan : 1;
@@ -1055,14 +1071,20 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
                 crc ^= wave_xor(lane < 16 ? var_crc(t, 1, 5 + lane, (rk >> (8 * (lane & 3))) & 0xFFu) : 0u);
             }
             crc = ~crc;   // util.c:424-426
-            v = u4{p0, last ? p1 | (crc << 16) : p1, last ? crc >> 16 : p2, p3};
+            if (kOut16) {
+                v = u4{pr.x, tail ? pr.y | (crc << 16) : pr.y, tail ? crc >> 16 : pr.z, pr.w};
+                h = lane < hchunks ? h : pr;
+            } else {
+                v = u4{p0, last ? p1 | (crc << 16) : p1, last ? crc >> 16 : p2, p3};
+            }
         }
         const __amdgpu_buffer_rsrc_t orow =
             __builtin_amdgcn_make_buffer_rsrc(row, 0, em ? (int)A.out_stride : 0, 0x00020000);
         row += A.out_stride;
         if (kOut16) {
-            __builtin_amdgcn_raw_buffer_store_b128(h, orow, ho, 0, kAuxNt);
-            __builtin_amdgcn_raw_buffer_store_b128(v, orow, po, 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b128(h, orow, 16 * lane, 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b128(v, orow, lane < hchunks ? 16 * (kWave + lane) : kOobOffset, 0,
+                                                   kAuxNt);
         } else {
             __builtin_amdgcn_raw_buffer_store_b32(h.x, orow, ho, 0, kAuxNt);
             __builtin_amdgcn_raw_buffer_store_b32(h.y, orow, ho + 4, 0, kAuxNt);
