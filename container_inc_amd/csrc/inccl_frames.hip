@@ -713,27 +713,34 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
         return;
     }
     const int port[2] = {ports_in[f0], ports_in[f1]};
-    // payload words 4 lane .. 4 lane + 3 of pair frame k (payload at byte 54 + 16 wf)
-    auto payload_of = [&](int k, uint32_t wf, uint32_t (&P)[4]) {
-        if (A.wide) {
-            const bool last = lane == kWave - 1;
-            uint32_t y0 = from_next(x[k].x, next4), y1 = from_next(x[k].y, next4);
-            y0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 0) : y0;
-            y1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 0) : y1;
-            if (wf) {
-                uint32_t y2 = from_next(x[k].z, next4), y3 = from_next(x[k].w, next4);
-                uint32_t z0 = from_next(y0, next4), z1 = from_next(y1, next4);
-                y2 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].z, 0) : y2;
-                y3 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].w, 0) : y3;
-                z0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].x, 1) : z0;
-                z1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)e[k].y, 1) : z1;
-                payload_from_chunks(u4{y0, y1, y2, y3}, z0, z1, P);
-            } else {
-                payload_from_chunks(x[k], y0, y1, P);
-            }
+    // payload words 4 lane .. 4 lane + 3 of a row, from its chunks: xx = chunk
+    // 3 + lane, ee = chunks 67, 68 on lanes 0, 1 (payload at byte 54 + 16 wf)
+    auto extract = [&](const u4& xx, const u4& ee, uint32_t wf, uint32_t (&P)[4]) {
+        const bool last = lane == kWave - 1;
+        uint32_t y0 = from_next(xx.x, next4), y1 = from_next(xx.y, next4);
+        y0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.x, 0) : y0;
+        y1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.y, 0) : y1;
+        if (wf) {
+            uint32_t y2 = from_next(xx.z, next4), y3 = from_next(xx.w, next4);
+            uint32_t z0 = from_next(y0, next4), z1 = from_next(y1, next4);
+            y2 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.z, 0) : y2;
+            y3 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.w, 0) : y3;
+            z0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.x, 1) : z0;
+            z1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.y, 1) : z1;
+            payload_from_chunks(u4{y0, y1, y2, y3}, z0, z1, P);
         } else {
-            payload16(A.frames + (f0 + k) * stride, wf, lane, false, P);
+            payload_from_chunks(xx, y0, y1, P);
         }
+    };
+    auto payload_of = [&](int k, uint32_t wf, uint32_t (&P)[4]) {
+        if (A.wide) extract(x[k], e[k], wf, P);
+        else payload16(A.frames + (f0 + k) * stride, wf, lane, false, P);
+    };
+    auto add = [](u4& acc, const uint32_t (&q)[4]) {
+        acc.x += q[0];
+        acc.y += q[1];
+        acc.z += q[2];
+        acc.w += q[3];
     };
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -755,23 +762,52 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
         const uint32_t own_wf = (act[k] & kActOwnWf) ? 1u : 0u;
         u4 acc = {0u, 0u, 0u, 0u};
         if (act[k] & kActPartial) acc = reinterpret_cast<const u4*>(s.agg + (size_t)slot * kLanes)[lane];
-        for (uint32_t m = cports; m; m &= m - 1) {
-            const int p = __builtin_ctz(m);
-            uint32_t q[4];
-            const int fo = act[o] & 0xFF;
-            if (p == port[k]) {
-                payload_of(k, own_wf, q);
-            } else if (!keys && (k == 0 ? in1 : true) && psn[o] == psn[k] && port[o] == p &&
-                       (fo == INCCL_SW_ABSORBED || fo == INCCL_SW_COMPLETED)) {
-                payload_of(o, (wfs >> p) & 1u, q);
+        uint32_t rest = cports, q[4];
+        // the leader's own copy and, if it is a counted copy of this PSN, the
+        // pair's other frame: already in registers
+        if ((rest >> port[k]) & 1u) {
+            payload_of(k, own_wf, q);
+            add(acc, q);
+            rest &= ~(1u << port[k]);
+        }
+        const int fo = act[o] & 0xFF;
+        if (!keys && (k == 0 ? in1 : true) && psn[o] == psn[k] && ((rest >> port[o]) & 1u) &&
+            (fo == INCCL_SW_ABSORBED || fo == INCCL_SW_COMPLETED)) {
+            payload_of(o, (wfs >> port[o]) & 1u, q);
+            add(acc, q);
+            rest &= ~(1u << port[o]);
+        }
+        // every other counted copy, two at a time: both keys in one round
+        // trip, both rows' chunks in the next (not two round trips per copy)
+        while (rest) {
+            const int pa = __builtin_ctz(rest);
+            rest &= rest - 1;
+            const int pb = rest ? __builtin_ctz(rest) : pa;
+            const bool two = rest != 0;
+            rest &= rest - 1;
+            const uint64_t ka = s.first[(size_t)slot * fan + pa], kb = s.first[(size_t)slot * fan + pb];
+            const uint32_t fa = (uint32_t)ka >> 1, fb = (uint32_t)kb >> 1;
+            if (A.wide) {
+                const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A.frames + (int64_t)fa * stride, stride);
+                const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(A.frames + (int64_t)fb * stride, two ? stride : 0);
+                const u4 xa = __builtin_amdgcn_raw_buffer_load_b128(ra, 48 + 16 * lane, 0, 0);
+                const u4 ea = __builtin_amdgcn_raw_buffer_load_b128(ra, lane < 2 ? 1072 + 16 * lane : kOobOffset, 0, 0);
+                const u4 xb = __builtin_amdgcn_raw_buffer_load_b128(rb, 48 + 16 * lane, 0, 0);
+                const u4 eb = __builtin_amdgcn_raw_buffer_load_b128(rb, lane < 2 ? 1072 + 16 * lane : kOobOffset, 0, 0);
+                extract(xa, ea, (uint32_t)ka & 1u, q);
+                add(acc, q);
+                if (two) {
+                    extract(xb, eb, (uint32_t)kb & 1u, q);
+                    add(acc, q);
+                }
             } else {
-                const uint64_t key = s.first[(size_t)slot * fan + p];
-                payload16(A.frames + (int64_t)((uint32_t)key >> 1) * stride, (uint32_t)key & 1u, lane, A.wide != 0, q);
+                payload16(A.frames + (int64_t)fa * stride, (uint32_t)ka & 1u, lane, false, q);
+                add(acc, q);
+                if (two) {
+                    payload16(A.frames + (int64_t)fb * stride, (uint32_t)kb & 1u, lane, false, q);
+                    add(acc, q);
+                }
             }
-            acc.x += q[0];
-            acc.y += q[1];
-            acc.z += q[2];
-            acc.w += q[3];
         }
         // write-through (sc1): the sum goes to memory and stays in the caches
         // for egress, which reads it next (49.7-50.0 vs 51.8-52.1 us for egress
