@@ -123,7 +123,8 @@ def _expected_frame(orc, t, c, agg, psn, op, reth):
 # 20 children: RETH words of children 16+ are loaded directly, not shuffled from the prefetch.
 # Stride 1100 (4-byte but not 16-byte aligned rows): ingress's 2-byte payload
 # loads and egress's dword stores instead of the 16-byte paths.
-# Fan-in 2, 3, 4 and 8 take the straight-line egress (k_egress_fixed), others the generic one.
+# Fan-in 2, 3, 4 and 8 take egress instances with the children loop unrolled, others the loop; frames
+# arrive shuffled, so a PSN's copies span frame pairs (the sum reads them through their keys).
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("fan_in,stride", [(1, STRIDE), (2, STRIDE), (3, STRIDE), (4, STRIDE), (8, STRIDE), (20, STRIDE),
                                            (31, STRIDE), (2, 1100), (4, 1100), (8, 1100), (5, 1100)])
