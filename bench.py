@@ -636,6 +636,72 @@ def kernel_time_ms(fn, stream, iters: int) -> float:
     return e0.elapsed_time(e1) / iters
 
 
+
+def switch_batch(dev, fan_in: int = 2, P: int = 1 << 16, iters: int = 20) -> dict:
+    """The GPU switch dataplane (nts.c:303-501 parse / aggregate / replay,
+    util.c:331-442 egress frames + ICRC) on one batch of fan_in x P RoCEv2 data
+    frames, every port of every PSN once: `inccl_switch_batch` = claim, classify,
+    sum, egress.  Batches alternate between the two halves of a 2P-slot ring, so
+    each batch's recycle (slot psn + slots/2, nts.c:367) clears the other half
+    and no reset runs between batches.  Device time per batch from HIP events on
+    its stream.  Checked without the oracle: every PSN completes exactly once per
+    batch and every completed frame's fan_in rows carry a frame length."""
+    import numpy as np
+    import torch
+
+    from container_inc_amd import inccl
+    stride = 1152
+    n = fan_in * P
+    rng = np.random.default_rng(7)
+    psn = np.repeat(np.arange(P, dtype=np.uint32), fan_in)
+    ports = np.tile(np.arange(fan_in, dtype=np.int32), P)
+    op = np.where(psn % 4 == 0, 0x06, np.where(psn % 4 == 3, 0x08, 0x07)).astype(np.uint8)   # WRITE_FIRST, MIDDLE, LAST
+    wf = op == 0x06
+    frames = np.zeros((n, stride), np.uint8)
+    udp_len = (8 + 12 + 1024 + 4 + np.where(wf, 16, 0)).astype(np.uint32)   # nts.c:349
+    frames[:, 38], frames[:, 39] = udp_len >> 8, udp_len & 0xFF
+    frames[:, 42] = op
+    pay = rng.integers(0, 256, (n, 1024), dtype=np.uint8)
+    for sel, off in ((wf, 70), (~wf, 54)):
+        frames[sel, off:off + 1024] = pay[sel]
+
+    def with_psns(base):
+        f = frames.copy()
+        q = (psn + base) | 0x80000000
+        f[:, 50], f[:, 51], f[:, 52], f[:, 53] = q >> 24, (q >> 16) & 0xFF, (q >> 8) & 0xFF, q & 0xFF
+        return torch.from_numpy(f).to(dev)
+
+    batches = [with_psns(0), with_psns(P)]
+    pt = torch.from_numpy(ports).to(dev)
+    sw = inccl.GpuSwitch(fan_in, 2 * P)
+    tmpl = np.zeros(fan_in, inccl.FRAME_TEMPLATE_DTYPE)
+    tmpl["qp"], tmpl["src_port"], tmpl["dst_port"] = 0x11, 4791, 4791
+    tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(dev)
+    st = torch.cuda.Stream(device=dev)
+    out = torch.empty((n * fan_in, stride), dtype=torch.uint8, device=dev)
+    out_len = torch.empty(n * fan_in, dtype=torch.int32, device=dev)
+    action = torch.empty(n, dtype=torch.int32, device=dev)
+    psn_out = torch.empty(n, dtype=torch.int32, device=dev)
+    turn = [0]
+
+    def one():
+        x = batches[turn[0] % 2]
+        turn[0] += 1
+        sw.batch(x, pt, tmpl_dev, stream=st.cuda_stream, out=out, out_len=out_len, action=action, psn=psn_out)
+
+    one()
+    torch.cuda.synchronize()
+    a = action.cpu().numpy()
+    lens = out_len.cpu().numpy().reshape(n, fan_in)
+    done = a == inccl.SW_COMPLETED
+    ok = int(done.sum()) == P and bool((lens[done] > 0).all()) and bool((lens[~done] == 0).all())
+    ms = kernel_time_ms(one, st, iters)
+    sw.destroy()
+    return {"what": "inccl_switch_batch: claim / classify / sum / egress (frames + ICRC) of one batch",
+            "fan_in": fan_in, "psns": P, "frames": n, "us_per_batch": round(ms * 1e3, 2),
+            "payload_GBs": round(n * 1024 / (ms * 1e-3) / 1e9, 1), "frames_per_s": round(n / (ms * 1e-3)),
+            "every_psn_completes_once": ok, "timing": "HIP events on the batch's stream, eager calls"}
+
 def n1_sizes(dev, R: int, k: int, sizes_mib=(4, 64, 256, 1024)) -> list:
     """north_star's bucket sizes at N = 1: the fused kernel on R resident buckets
     of each size, GB/s of buckets reduced and the kernel's HBM roofline fraction.
@@ -1428,6 +1494,7 @@ def main():
         extra("r_variants", lambda: r_variants(dev, k, n))
         extra("numerics_vs_exact", lambda: numerics_vs_exact(dev, n))
         extra("bf16", lambda: bf16_buckets(dev, R, k))
+        extra("switch_batch", lambda: switch_batch(dev))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         extra("cpu_baseline", lambda: cpu_baseline(n, R, k, a.cpu_seconds))
         extra("cpu_baseline_allcores", lambda: cpu_baseline_allcores(n, R, k, min(a.cpu_seconds, 5.0)))
