@@ -428,9 +428,9 @@ __device__ __forceinline__ uint32_t var_crc(const L& t, int wf, int k, uint32_t 
 // its PSN's other ports came BEFORE f, so:
 //   claim   (a lane per frame) parse + validate; per (slot, port) an atomicMin
 //           of a batch-tagged frame index finds the first copy in the batch
-//   apply   the first copy of a pair whose port bit was not set before the
-//           batch is the arrival that counts: it adds its payload (nts.c:359-
-//           363) and keeps its RETH (:442).  The PSN completes at the LAST of
+//   classify + sum   the first copy of a pair whose port bit was not set
+//           before the batch is the arrival that counts: it adds its payload
+//           (nts.c:359-363) and keeps its RETH (:442).  The PSN completes at the LAST of
 //           its ports' counted arrivals (the max over ports of the first index;
 //           ports already in before the batch count as earlier than every
 //           frame): that frame is COMPLETED (:365-372), the others ABSORBED.
@@ -438,19 +438,20 @@ __device__ __forceinline__ uint32_t var_crc(const L& t, int wf, int k, uint32_t 
 //           before the batch or at an earlier frame of it (:354-356), else
 //           DROPPED.
 // Batch generation: claim tags its first-copy keys with g = gen[0] + 1 and
-// publishes g in gen[1]; apply reads g from gen[1] and stores it to gen[0] for
-// the next batch.  Each word is written while no kernel of the batch reads it,
+// publishes g in gen[1]; classify reads g from gen[1] and stores it to gen[0]
+// for the next batch.  Each word is written while no kernel of the batch reads it,
 // and nothing changes on the host per batch, so a captured batch (hipGraph)
 // tags every replay anew.
 // ---------------------------------------------------------------------------
-// claim -> apply: a data frame still to classify: kActPending | WRITE_FIRST << 9 | opcode
-// (the final actions are all below 0x100)
+// claim -> classify: a data frame still to classify: kActPending | WRITE_FIRST << 9 |
+// opcode (the final actions are all below 0x100; classify replaces the word,
+// and the same bit then marks a leader for the sum, kActLeader)
 constexpr int kActPending = 0x100;
 constexpr int kClaimBlock = 256;
 
 // (~gen << 32) | (frame << 1) | wf: the minimum over a (slot, port)'s keys is the
 // newest batch's earliest copy (the frame index dominates bit 0), and bit 0 tells
-// apply where that copy's payload starts (byte 54, or 70 after a RETH) without
+// classify and the sum where that copy's payload starts (byte 54, or 70 after a RETH) without
 // another dependent load.  Frame indices stay below 2^31.
 __device__ __forceinline__ uint64_t first_key(uint32_t gen, int64_t f, bool wf)
 {
@@ -510,7 +511,7 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
 // pre-batch bitmap (64-bit accesses are single-copy atomic).  The recycle
 // writes both words (no frame of the batch reads that slot).
 // ---------------------------------------------------------------------------
-constexpr int kApplyWaves = 8;    // the sum kernel: one pair per wave, 8-wave blocks
+constexpr int kApplyWaves = 8;    // the sum kernel: one pair per wave, 8-wave blocks (1, 2, 4, 16: 35.1-36.4 us, no better)
 
 struct ApplyArgs {
     InccSwitchState s;
@@ -1490,7 +1491,7 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
     return launch_apply(apply_args(s, frames, stride, count, ports, action, psn_out), st);
 }
 
-// ingress then egress of one batch: claim, apply, egress on one stream
+// ingress then egress of one batch: claim, classify, sum, egress on one stream
 int inccl_k_switch_batch(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count,
                          const int32_t* ports, int32_t* action, uint32_t* psn_out, const InccFrameTemplate* tmpl,
                          uint8_t* out, size_t out_stride, int32_t* out_len, void* stream)
