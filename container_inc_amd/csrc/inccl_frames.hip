@@ -15,7 +15,7 @@
 //                     absorbed PSN's counted arrivals summed into its aggregate
 //                     (:361-363), every data frame counted in its slot's degree
 //                     (:351)
-//   k_egress<F>       persistent, a wave per 16 input frames: the COMPLETED
+//   k_egress<F>       persistent, a wave per 4 input frames at a time: the COMPLETED
 //                     broadcasts (:447-453) and REPLAY resends (:353-356) from the
 //                     state ingress left, frames per util.c:331-442
 // inccl_switch_ingress runs the first three, inccl_switch_egress the last,
@@ -829,13 +829,16 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
 //
 // Persistent 16-wave blocks, two per CU: each block loads the CRC tables into
 // LDS and builds the 2 fan_in header images and their ICRC terms H_c once.  A
-// wave then takes 16 consecutive input frames at a time, lane l frame l: their
-// claim results and header words in four vector loads, the row lengths of all
-// 16 x fan_in rows lane-parallel, and then only the frames that emit, one after
-// another, each frame's aggregate and keeper in flight while the frame before
-// it is built.  (A wave per input frame spent as long on the absorbed half of
-// the frames, which emit nothing, as on the rest: 58-60 against 56-57 us per
-// 131 072-frame batch, profiles/r04/.)
+// wave then takes egress_chunk(fan_in) consecutive input frames at a time (a chunk),
+// lane l frame l: their claim results and header words in four vector loads,
+// the row lengths of all its frames' fan_in rows lane-parallel, and then
+// only the frames that emit, one after another, each frame's aggregate and
+// keeper in flight while the frame before it is built, and the wave's next
+// chunk's claim results in flight while this chunk is built.  (A wave per input
+// frame spent as long on the absorbed half of the frames, which emit nothing,
+// as on the rest: 58-60 against 56-57 us per 131 072-frame batch.  Chunks of
+// 16 / 8 / 4 / 2 frames with the next chunk read ahead: 49.9 / 47.1-47.6 /
+// 45.4-45.6 / 50.8 us, profiles/r04/switch/egress_chunk_sweep.txt.)
 //
 // Loads and stores retire in order on one counter (vmcnt).  So that the
 // compiler can wait for the prefetched aggregate without also waiting for the
@@ -860,7 +863,13 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
 // frame, one RETH reduction per RETH child.
 // ---------------------------------------------------------------------------
 constexpr int kEgressWaves = 16;
-constexpr int kEgressChunk = 16;   // input frames per wave at a time (lanes 0-15)
+// input frames per wave at a time: 4 up to fan-in 8; 16 above, where most
+// chunks of 4 would hold no completing frame (fan-in 16: 48.3 us with 4, 43.0
+// with 16; fan-in 5: 29.2 with 4, 32.3 with 16)
+__host__ __device__ constexpr uint32_t egress_chunk(int fan)
+{
+    return fan <= 8 ? 4u : 16u;
+}
 constexpr int kEgressAhead = 1;    // emitting frames whose aggregate is in flight ahead of the one emitted
 
 __device__ uint32_t g_segb[16][256];   // [byte j of a 16-byte segment][value] = Z_{15-j}(T[value])
@@ -1144,6 +1153,7 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
 {
     __shared__ EgressLds t;
     const int fan = kFan ? kFan : A.fan;
+    const uint32_t kEgressChunk = egress_chunk(fan);   // (a constant for the unrolled fan-ins)
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane0 = threadIdx.x % kWave;
     const uint32_t count = A.count, chunks = (count + kEgressChunk - 1) / kEgressChunk;
     const uint32_t nw = gridDim.x * kEgressWaves;
@@ -1178,12 +1188,13 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
     ChunkIn cin = chunk_in(ch);
     egress_setup(t, A.tmpl, fan);
     for (; ch < chunks; ch += nw) {
-        if (ch != blockIdx.x * kEgressWaves + w) cin = chunk_in(ch);
+        const ChunkIn cur = cin;
+        cin = chunk_in(ch + nw);   // the wave's next chunk, read while this one is built (past the end: nothing)
         const int lane = ln();
         const uint32_t f0 = ch * kEgressChunk, nf = min((uint32_t)kEgressChunk, count - f0);
-        const int act = (int)cin.act;
-        const uint32_t port = cin.port, psn = cin.psn;
-        const uint32_t op = (cin.w10 >> 16) & 0xFFu;
+        const int act = (int)cur.act;
+        const uint32_t port = cur.port, psn = cur.psn;
+        const uint32_t op = (cur.w10 >> 16) & 0xFFu;
         const bool in = lane < (int)nf;
         const bool all = in && act == INCCL_SW_COMPLETED;
         const bool one = in && act == INCCL_SW_REPLAY && port < (uint32_t)fan;
@@ -1359,7 +1370,7 @@ int launch_apply(const ApplyArgs& a, hipStream_t st)
     return (int)hipGetLastError();
 }
 
-// persistent egress: a wave per chunk of kEgressChunk frames, as many blocks as
+// persistent egress: a wave per chunk of egress_chunk(fan_in) frames, as many blocks as
 // fit beside each other (two per CU)
 template <int kFan, bool kOut16>
 int launch_egress_t(const EgressArgs& a, hipStream_t st)
@@ -1371,7 +1382,7 @@ int launch_egress_t(const EgressArgs& a, hipStream_t st)
             n = 1;
         return n;
     }();
-    const int64_t chunks = ((int64_t)a.count + kEgressChunk - 1) / kEgressChunk;
+    const int64_t chunks = ((int64_t)a.count + egress_chunk(a.fan) - 1) / egress_chunk(a.fan);
     const int64_t need = (chunks + kEgressWaves - 1) / kEgressWaves, cap = (int64_t)num_cus() * per_cu;
     hipLaunchKernelGGL((k_egress<kFan, kOut16>), dim3((unsigned)(need < cap ? (need < 1 ? 1 : need) : cap)),
                        dim3(kWave * kEgressWaves), 0, st, a);
