@@ -118,12 +118,15 @@ def main():
                           "egress_frames": fan_in * P, "ms": round(ms, 4),
                           "payload_GBs": round(payload_bytes / (ms * 1e-3) / 1e9, 2),
                           "frames_per_s": round(2 * fan_in * P / (ms * 1e-3), 1)}), flush=True)
-        # the same batches captured in a hipGraph (two batches, one per half of
-        # the ring) and replayed: no launch gaps between the batch's kernels
+        # the same batches captured in a hipGraph (SW_GRAPH_BATCHES batches,
+        # even: alternating halves of the ring) and replayed: no launch gaps
+        # between the captured kernels, one graph launch per replay
+        nb = int(os.environ.get("SW_GRAPH_BATCHES", "2"))
+        assert nb >= 2 and nb % 2 == 0, "SW_GRAPH_BATCHES: an even count (the batches alternate ring halves)"
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=st):
-            run(mode)
-            run(mode)
+            for _ in range(nb):
+                run(mode)
         g.replay()
         torch.cuda.synchronize()
         reps = 5
@@ -133,10 +136,10 @@ def main():
                 g.replay()
             e1.record(st)
         torch.cuda.synchronize()
-        ms_g = e0.elapsed_time(e1) / (2 * reps)
+        ms_g = e0.elapsed_time(e1) / (nb * reps)
         check(mode)   # eager again after the replays: still one completion per PSN
         del g
-        print(json.dumps({"what": "GPU switch dataplane batch, hipGraph-replayed", "mode": mode,
+        print(json.dumps({"what": "GPU switch dataplane batch, hipGraph-replayed", "mode": mode, "batches_per_graph": nb,
                           "fan_in": fan_in, "psns": P, "ms": round(ms_g, 4),
                           "payload_GBs": round(payload_bytes / (ms_g * 1e-3) / 1e9, 2)}), flush=True)
     icrc_out = torch.empty(fan_in * P, dtype=torch.int32, device=dev)
