@@ -1,8 +1,10 @@
-"""Copy a GPU evidence pass (tools/gpu_round_profile.sh) from gpurun_out/ into
-profiles/ (tracked): bench JSON, rocprofv3 kernel stats, PMC counter CSVs, and
-the per-launch HBM traffic summary profiles/pmc_traffic.json that bench.py reads.
+"""Copy a GPU evidence pass (tools/gpu_round_profile.sh, plus a smoke.log if one
+was written) from gpurun_out/ into profiles/rNN/round_profile/ (tracked): bench
+JSON, rocprofv3 kernel stats, PMC counter CSVs, the GPU test log, the 2-rank
+rehearsal line; and rebuild the per-launch HBM traffic summary
+profiles/pmc_traffic.json that bench.py reads.
 
-    python tools/update_profiles.py --round 1 [--src gpurun_out]
+    python tools/update_profiles.py --round 4 [--src gpurun_out]
 
 Traffic correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE and WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide coalesced streaming
@@ -33,18 +35,16 @@ def main():
     p.add_argument("--mib", type=int, default=256)
     p.add_argument("--R", type=int, default=2)
     a = p.parse_args()
-    tag = f"r{a.round:02d}"
     prof = os.path.join(ROOT, "profiles")
-    os.makedirs(os.path.join(prof, f"{tag}_pmc"), exist_ok=True)
+    dest = os.path.join(prof, f"r{a.round:02d}", "round_profile")
+    os.makedirs(dest, exist_ok=True)
     src = a.src
-    if os.path.exists(os.path.join(src, "bench.json")):
-        shutil.copy(os.path.join(src, "bench.json"), os.path.join(prof, f"{tag}_bench_n1.json"))
-    if os.path.exists(os.path.join(src, "prof", "run_kernel_stats.csv")):
-        shutil.copy(os.path.join(src, "prof", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_bench_n1_kernel_stats.csv"))
-    if os.path.exists(os.path.join(src, "prof_bf16", "run_kernel_stats.csv")):
-        shutil.copy(os.path.join(src, "prof_bf16", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_bf16_kernel_stats.csv"))
-    if os.path.exists(os.path.join(src, "bench_profiled.json")):
-        shutil.copy(os.path.join(src, "bench_profiled.json"), os.path.join(prof, f"{tag}_bench_n1_under_rocprof.json"))
+    for name, out in (("bench.json", "bench.json"), (os.path.join("prof", "run_kernel_stats.csv"), "bench_kernel_stats.csv"),
+                      ("bench_profiled.json", "bench_profiled.json"),
+                      (os.path.join("prof_bf16", "run_kernel_stats.csv"), "bf16_kernel_stats.csv"),
+                      ("pytest_gpu.log", "pytest_gpu.log"), ("rehearse_n2.json", "rehearse_n2.json"), ("smoke.log", "smoke.log")):
+        if os.path.exists(os.path.join(src, name)):
+            shutil.copy(os.path.join(src, name), os.path.join(dest, out))
     traffic_path = os.path.join(prof, "pmc_traffic.json")
     traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
     for k, (kname, needle, esize) in KERNELS.items():
@@ -55,8 +55,8 @@ def main():
             continue
         f, nf = mean_counter(f_csv, needle)
         w, nw = mean_counter(w_csv, needle)
-        shutil.copy(f_csv, os.path.join(prof, f"{tag}_pmc", f"{k}_fetch_size.csv"))
-        shutil.copy(w_csv, os.path.join(prof, f"{tag}_pmc", f"{k}_write_size.csv"))
+        shutil.copy(f_csv, os.path.join(dest, f"pmc_{k}_FETCH_SIZE.csv"))
+        shutil.copy(w_csv, os.path.join(dest, f"pmc_{k}_WRITE_SIZE.csv"))
         alg = (a.R + 1) * esize * n
         hbm = (2 * f + w) * 1024
         traffic[f"{kname} R={a.R} n={n}"] = {
