@@ -39,12 +39,20 @@ constexpr int kTail = 4;                // 16-B chunks past the first 1024 B (10
 constexpr int kOob = 0x40000000;        // an offset past every buffer: the access is dropped
 
 // G PSNs per chunk; PERSIST: a grid of 2 blocks per CU walks the chunks, else a
-// wave per chunk.  READ: load the aggregate.  AUX: store cache policy.
-template <int G, bool PERSIST, bool READ, int AUX>
+// wave per chunk.  READ: load the aggregate.  AUX: store cache policy.  ALU:
+// dependent VALU operations per PSN on its aggregate before its rows are
+// stored; LDS: random 4-byte LDS table lookups per PSN among them (the frame
+// work's stand-ins: how much compute the traffic hides)
+template <int G, bool PERSIST, bool READ, int AUX, int ALU = 0, int LDS = 0>
 __global__ __launch_bounds__(kWave* kWaves) void k_egress_mem(const u4* __restrict__ agg, uint8_t* __restrict__ out,
                                                              uint32_t* __restrict__ out_len)
 {
+    __shared__ uint32_t tab[LDS ? 4096 : 1];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    if (LDS) {
+        for (int i = threadIdx.x; i < 4096; i += blockDim.x) tab[i] = (uint32_t)i * 2654435761u;
+        __syncthreads();
+    }
     const uint32_t chunks = kPsns / G;
     const uint32_t nw = PERSIST ? gridDim.x * kWaves : chunks;
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<u4*>(agg), 0, kPsns * 1024, 0x00020000);
@@ -66,6 +74,18 @@ __global__ __launch_bounds__(kWave* kWaves) void k_egress_mem(const u4* __restri
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const uint32_t p = ch * G + g;
+            if (ALU || LDS) {
+                uint32_t h = a[g].x ^ a[g].y ^ a[g].z ^ a[g].w;
+#pragma unroll
+                for (int i = 0; i < ALU; i += 2) {   // two dependent VALU operations per step
+                    h ^= h << 7;
+                    h = __builtin_amdgcn_alignbyte(h, h ^ 0x9E3779B9u, 1);
+                }
+                uint32_t x = 0;   // independent lookups, as the ICRC's (random words of one table)
+#pragma unroll
+                for (int i = 0; i < LDS; ++i) x ^= tab[((h >> (i % 20)) + 97u * (uint32_t)i) & 4095u];
+                a[g].w ^= h ^ x;
+            }
 #pragma unroll
             for (int c = 0; c < kFan; ++c) {
                 const int64_t row = (int64_t)(2 * p + 1) * kFan + c;
@@ -80,11 +100,11 @@ __global__ __launch_bounds__(kWave* kWaves) void k_egress_mem(const u4* __restri
 
 static hipEvent_t e0, e1;
 
-template <int G, bool PERSIST, bool READ, int AUX>
+template <int G, bool PERSIST, bool READ, int AUX, int ALU = 0, int LDS = 0>
 static void run(const char* name, const u4* agg, uint8_t* out, uint32_t* len, int cus, int iters)
 {
     const int blocks = PERSIST ? 2 * cus : (kPsns / G + kWaves - 1) / kWaves;
-    auto launch = [&]() { k_egress_mem<G, PERSIST, READ, AUX><<<blocks, kWave * kWaves>>>(agg, out, len); };
+    auto launch = [&]() { k_egress_mem<G, PERSIST, READ, AUX, ALU, LDS><<<blocks, kWave * kWaves>>>(agg, out, len); };
     for (int i = 0; i < 3; ++i) launch();
     CHECK(hipEventRecord(e0));
     for (int i = 0; i < iters; ++i) launch();
@@ -98,8 +118,9 @@ static void run(const char* name, const u4* agg, uint8_t* out, uint32_t* len, in
     const double alg = (double)kPsns * 1024 + (double)kPsns * kFan * 1090;
     const double stored = (double)kPsns * kFan * (1024 + 16 * kTail);
     printf("{\"variant\": \"%s\", \"chunk_psns\": %d, \"persistent\": %s, \"read\": %s, \"store_aux\": %d, "
+           "\"valu_per_psn\": %d, \"lds_per_psn\": %d, "
            "\"us\": %.2f, \"egress_alg_TBs\": %.3f, \"frac_of_8TBs\": %.3f, \"store_TBs\": %.3f}\n",
-           name, G, PERSIST ? "true" : "false", READ ? "true" : "false", AUX, us, alg / us * 1e-6, alg / us * 1e-6 / 8.0,
+           name, G, PERSIST ? "true" : "false", READ ? "true" : "false", AUX, ALU, LDS, us, alg / us * 1e-6, alg / us * 1e-6 / 8.0,
            stored / us * 1e-6);
     fflush(stdout);
 }
@@ -129,6 +150,13 @@ int main(int argc, char** argv)
     run<4, true, true, 2>("4 psns per chunk, nt", agg, out, len, cus, iters);
     run<2, false, true, 2>("wave per chunk, nt", agg, out, len, cus, iters);
     run<2, false, false, 2>("wave per chunk, stores only, nt", agg, out, len, cus, iters);
+    // the egress shape with compute stand-ins per PSN (the product: about 228
+    // VALU and 40 LDS reads per emitting frame)
+    run<2, true, true, 2, 100, 0>("egress shape + 100 VALU", agg, out, len, cus, iters);
+    run<2, true, true, 2, 200, 0>("egress shape + 200 VALU", agg, out, len, cus, iters);
+    run<2, true, true, 2, 400, 0>("egress shape + 400 VALU", agg, out, len, cus, iters);
+    run<2, true, true, 2, 0, 40>("egress shape + 40 LDS lookups", agg, out, len, cus, iters);
+    run<2, true, true, 2, 200, 40>("egress shape + 200 VALU + 40 LDS lookups", agg, out, len, cus, iters);
     CHECK(hipFree(agg));
     CHECK(hipFree(out));
     CHECK(hipFree(len));
