@@ -43,7 +43,7 @@ constexpr int kOob = 0x40000000;        // an offset past every buffer: the acce
 // dependent VALU operations per PSN on its aggregate before its rows are
 // stored; LDS: random 4-byte LDS table lookups per PSN among them (the frame
 // work's stand-ins: how much compute the traffic hides)
-template <int G, bool PERSIST, bool READ, int AUX, int ALU = 0, int LDS = 0>
+template <int G, bool PERSIST, bool READ, int AUX, int ALU = 0, int LDS = 0, int ILP = 1>
 __global__ __launch_bounds__(kWave* kWaves) void k_egress_mem(const u4* __restrict__ agg, uint8_t* __restrict__ out,
                                                              uint32_t* __restrict__ out_len)
 {
@@ -75,12 +75,22 @@ __global__ __launch_bounds__(kWave* kWaves) void k_egress_mem(const u4* __restri
         for (int g = 0; g < G; ++g) {
             const uint32_t p = ch * G + g;
             if (ALU || LDS) {
-                uint32_t h = a[g].x ^ a[g].y ^ a[g].z ^ a[g].w;
+                // ALU operations in ILP independent chains (two dependent
+                // operations per step of a chain)
+                uint32_t hc[ILP];
 #pragma unroll
-                for (int i = 0; i < ALU; i += 2) {   // two dependent VALU operations per step
-                    h ^= h << 7;
-                    h = __builtin_amdgcn_alignbyte(h, h ^ 0x9E3779B9u, 1);
+                for (int k = 0; k < ILP; ++k) hc[k] = a[g][k & 3] + (uint32_t)k;
+#pragma unroll
+                for (int i = 0; i < ALU / ILP; i += 2) {
+#pragma unroll
+                    for (int k = 0; k < ILP; ++k) {
+                        hc[k] ^= hc[k] << 7;
+                        hc[k] = __builtin_amdgcn_alignbyte(hc[k], hc[k] ^ 0x9E3779B9u, 1);
+                    }
                 }
+                uint32_t h = 0;
+#pragma unroll
+                for (int k = 0; k < ILP; ++k) h ^= hc[k];
                 uint32_t x = 0;   // independent lookups, as the ICRC's (random words of one table)
 #pragma unroll
                 for (int i = 0; i < LDS; ++i) x ^= tab[((h >> (i % 20)) + 97u * (uint32_t)i) & 4095u];
@@ -100,11 +110,11 @@ __global__ __launch_bounds__(kWave* kWaves) void k_egress_mem(const u4* __restri
 
 static hipEvent_t e0, e1;
 
-template <int G, bool PERSIST, bool READ, int AUX, int ALU = 0, int LDS = 0>
+template <int G, bool PERSIST, bool READ, int AUX, int ALU = 0, int LDS = 0, int ILP = 1>
 static void run(const char* name, const u4* agg, uint8_t* out, uint32_t* len, int cus, int iters)
 {
     const int blocks = PERSIST ? 2 * cus : (kPsns / G + kWaves - 1) / kWaves;
-    auto launch = [&]() { k_egress_mem<G, PERSIST, READ, AUX, ALU, LDS><<<blocks, kWave * kWaves>>>(agg, out, len); };
+    auto launch = [&]() { k_egress_mem<G, PERSIST, READ, AUX, ALU, LDS, ILP><<<blocks, kWave * kWaves>>>(agg, out, len); };
     for (int i = 0; i < 3; ++i) launch();
     CHECK(hipEventRecord(e0));
     for (int i = 0; i < iters; ++i) launch();
@@ -118,9 +128,9 @@ static void run(const char* name, const u4* agg, uint8_t* out, uint32_t* len, in
     const double alg = (double)kPsns * 1024 + (double)kPsns * kFan * 1090;
     const double stored = (double)kPsns * kFan * (1024 + 16 * kTail);
     printf("{\"variant\": \"%s\", \"chunk_psns\": %d, \"persistent\": %s, \"read\": %s, \"store_aux\": %d, "
-           "\"valu_per_psn\": %d, \"lds_per_psn\": %d, "
+           "\"valu_per_psn\": %d, \"valu_chains\": %d, \"lds_per_psn\": %d, "
            "\"us\": %.2f, \"egress_alg_TBs\": %.3f, \"frac_of_8TBs\": %.3f, \"store_TBs\": %.3f}\n",
-           name, G, PERSIST ? "true" : "false", READ ? "true" : "false", AUX, ALU, LDS, us, alg / us * 1e-6, alg / us * 1e-6 / 8.0,
+           name, G, PERSIST ? "true" : "false", READ ? "true" : "false", AUX, ALU, ILP, LDS, us, alg / us * 1e-6, alg / us * 1e-6 / 8.0,
            stored / us * 1e-6);
     fflush(stdout);
 }
@@ -157,6 +167,9 @@ int main(int argc, char** argv)
     run<2, true, true, 2, 400, 0>("egress shape + 400 VALU", agg, out, len, cus, iters);
     run<2, true, true, 2, 0, 40>("egress shape + 40 LDS lookups", agg, out, len, cus, iters);
     run<2, true, true, 2, 200, 40>("egress shape + 200 VALU + 40 LDS lookups", agg, out, len, cus, iters);
+    run<2, true, true, 2, 200, 0, 4>("egress shape + 200 VALU in 4 chains", agg, out, len, cus, iters);
+    run<2, true, true, 2, 400, 0, 4>("egress shape + 400 VALU in 4 chains", agg, out, len, cus, iters);
+    run<2, true, true, 2, 200, 40, 4>("egress shape + 200 VALU in 4 chains + 40 LDS lookups", agg, out, len, cus, iters);
     CHECK(hipFree(agg));
     CHECK(hipFree(out));
     CHECK(hipFree(len));
