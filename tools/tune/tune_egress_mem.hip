@@ -108,6 +108,63 @@ __global__ __launch_bounds__(kWave* kWaves) void k_egress_mem(const u4* __restri
     }
 }
 
+// Split waves (an upper bound for a specialised egress, no hand-over between
+// them): waves 0-7 of each block do the memory-only loop (chunks of 2 PSNs),
+// waves 8-15 read the same PSNs' aggregates and do ALU VALU operations per PSN in
+// four chains, writing 4 B per PSN (the ICRC a store wave would need).
+template <int ALU>
+__global__ __launch_bounds__(kWave* kWaves) void k_egress_split(const u4* __restrict__ agg, uint8_t* __restrict__ out,
+                                                               uint32_t* __restrict__ out_len, uint32_t* __restrict__ crc)
+{
+    constexpr int G = 2;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    const bool storer = w < kWaves / 2;
+    const uint32_t chunks = kPsns / G, nw = gridDim.x * (kWaves / 2);
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<u4*>(agg), 0, kPsns * 1024, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro =
+        __builtin_amdgcn_make_buffer_rsrc(out, 0, kPsns * 2 * kFan * kStride, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rl =
+        __builtin_amdgcn_make_buffer_rsrc(out_len, 0, 4 * kPsns * 2 * kFan, 0x00020000);
+    for (uint32_t ch = blockIdx.x * (kWaves / 2) + (w % (kWaves / 2)); ch < chunks; ch += nw) {
+        u4 a[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) a[g] = __builtin_amdgcn_raw_buffer_load_b128(ra, (int)((ch * G + g) * 1024 + 16 * lane), 0, 0);
+        if (storer) {
+            __builtin_amdgcn_raw_buffer_store_b32(lane & 2 ? 1086u : 0u, rl,
+                                                  lane < 2 * G * kFan ? (int)(4 * (ch * 2 * G * kFan + lane)) : kOob, 0, 0);
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const uint32_t p = ch * G + g;
+#pragma unroll
+                for (int c = 0; c < kFan; ++c) {
+                    const int64_t row = (int64_t)(2 * p + 1) * kFan + c;
+                    const u4 v = a[g] + (uint32_t)c;
+                    __builtin_amdgcn_raw_buffer_store_b128(v, ro, (int)(row * kStride + 16 * lane), 0, 2);
+                    __builtin_amdgcn_raw_buffer_store_b128(v, ro, lane < kTail ? (int)(row * kStride + 1024 + 16 * lane) : kOob,
+                                                           0, 2);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                uint32_t hc[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) hc[k] = a[g][k] + (uint32_t)k;
+#pragma unroll
+                for (int i = 0; i < ALU / 4; i += 2) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        hc[k] ^= hc[k] << 7;
+                        hc[k] = __builtin_amdgcn_alignbyte(hc[k], hc[k] ^ 0x9E3779B9u, 1);
+                    }
+                }
+                const uint32_t h = hc[0] ^ hc[1] ^ hc[2] ^ hc[3];
+                if (lane == 0) crc[ch * G + g] = h;
+            }
+        }
+    }
+}
+
 static hipEvent_t e0, e1;
 
 template <int G, bool PERSIST, bool READ, int AUX, int ALU = 0, int LDS = 0, int ILP = 1>
@@ -132,6 +189,24 @@ static void run(const char* name, const u4* agg, uint8_t* out, uint32_t* len, in
            "\"us\": %.2f, \"egress_alg_TBs\": %.3f, \"frac_of_8TBs\": %.3f, \"store_TBs\": %.3f}\n",
            name, G, PERSIST ? "true" : "false", READ ? "true" : "false", AUX, ALU, ILP, LDS, us, alg / us * 1e-6, alg / us * 1e-6 / 8.0,
            stored / us * 1e-6);
+    fflush(stdout);
+}
+
+template <int ALU>
+static void run_split(const char* name, const u4* agg, uint8_t* out, uint32_t* len, uint32_t* crc, int cus, int iters)
+{
+    auto launch = [&]() { k_egress_split<ALU><<<2 * cus, kWave * kWaves>>>(agg, out, len, crc); };
+    for (int i = 0; i < 3; ++i) launch();
+    CHECK(hipEventRecord(e0));
+    for (int i = 0; i < iters; ++i) launch();
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1e3 * ms / iters;
+    const double alg = (double)kPsns * 1024 + (double)kPsns * kFan * 1090;
+    printf("{\"variant\": \"%s\", \"valu_per_psn\": %d, \"us\": %.2f, \"egress_alg_TBs\": %.3f}\n", name, ALU, us,
+           alg / us * 1e-6);
     fflush(stdout);
 }
 
@@ -170,6 +245,12 @@ int main(int argc, char** argv)
     run<2, true, true, 2, 200, 0, 4>("egress shape + 200 VALU in 4 chains", agg, out, len, cus, iters);
     run<2, true, true, 2, 400, 0, 4>("egress shape + 400 VALU in 4 chains", agg, out, len, cus, iters);
     run<2, true, true, 2, 200, 40, 4>("egress shape + 200 VALU in 4 chains + 40 LDS lookups", agg, out, len, cus, iters);
+    uint32_t* crc;
+    CHECK(hipMalloc(&crc, (size_t)kPsns * 4));
+    run_split<0>("split waves: 8 store + 8 read-only", agg, out, len, crc, cus, iters);
+    run_split<200>("split waves: 8 store + 8 with 200 VALU in 4 chains", agg, out, len, crc, cus, iters);
+    run_split<400>("split waves: 8 store + 8 with 400 VALU in 4 chains", agg, out, len, crc, cus, iters);
+    CHECK(hipFree(crc));
     CHECK(hipFree(agg));
     CHECK(hipFree(out));
     CHECK(hipFree(len));
