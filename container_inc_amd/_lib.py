@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libinccl_amd.so")
@@ -151,9 +152,19 @@ def runtime_libs() -> dict:
         c, ld = ctypes.c_int(0), ctypes.c_int(0)
         if lib.inccl_rccl_version(ctypes.byref(c), ctypes.byref(ld)) == 0:
             found["rccl_compiled"], found["rccl_loaded"] = c.value, ld.value
-        found["hsa_release"] = int(lib.inccl_hsa_runtime_release())
-        found["hsa_build"] = lib.inccl_hsa_runtime_build().decode(errors="replace")
-        found["ipc_max_bytes"] = int(lib.inccl_ipc_max_bytes())
+        # the HSA queries initialise HIP (hipInit + hsa_init, csrc/runtime.c):
+        # only asked in a process that has initialised the GPU already, so that
+        # reporting versions never initialises it behind the caller's back (a
+        # launcher that forks or relaunches afterwards must not have a GPU
+        # context)
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_initialized():
+            found["hsa_release"] = int(lib.inccl_hsa_runtime_release())
+            found["hsa_build"] = lib.inccl_hsa_runtime_build().decode(errors="replace")
+            found["ipc_max_bytes"] = int(lib.inccl_ipc_max_bytes())
+        else:
+            found["hsa_release"] = found["hsa_build"] = found["ipc_max_bytes"] = None
+            found["hsa_note"] = "not queried: the GPU is not initialised in this process (the query would do it)"
     return found
 
 

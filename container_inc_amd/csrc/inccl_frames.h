@@ -15,14 +15,15 @@ extern "C" {
 /* device-side state of one root switch (pointers into one allocation) */
 typedef struct InccSwitchState {
     int32_t *agg;        /* [slots][256]        non_termination_switch.c:55 */
-    uint64_t *arrival;   /* [slots][2]          nts.c:59: {bitmap, tag = the batch that wrote it}, double-buffered
-                          * by batch parity so a batch reads the bitmap as it was before it (k_ingress_apply) */
+    uint64_t *arrival;   /* [slots][2]          nts.c:59: {bitmap, tag = the batch that wrote it}, double-buffered:
+                          * batch g reads the newer word not tagged g and its leader overwrites the other one,
+                          * so every frame of the batch sees the bitmap as it was before it (k_ingress_classify) */
     int32_t *degree;     /* [slots]             nts.c:60 */
     uint32_t *reth;      /* [slots][fan_in][4]  nts.c:57 */
     uint64_t *first;     /* [slots][fan_in]     batch-tagged index of the first copy in a batch:
                           * (~gen << 32) | frame, atomicMin -> the earliest frame of the newest batch */
-    uint32_t *gen;       /* gen[0]: batches ingested so far.  A batch's claim tags it first-copy keys with
-                          * g = gen[0] + 1 and stores g in gen[1]; its apply reads gen[1] and stores g in
+    uint32_t *gen;       /* gen[0]: batches ingested so far.  A batch's claim tags its first-copy keys with
+                          * g = gen[0] + 1 and stores g in gen[1]; its classify reads gen[1] and stores g in
                           * gen[0], so that a captured batch (hipGraph) tags every replay anew */
     uint32_t slots;      /* power of two */
     int fan_in;

@@ -17,7 +17,8 @@
 //                     (:351)
 //   k_egress<F>       persistent, a wave per 4 input frames at a time: the COMPLETED
 //                     broadcasts (:447-453) and REPLAY resends (:353-356) from the
-//                     state ingress left, frames per util.c:331-442
+//                     state ingress left, and the ACK reflections (:403-406),
+//                     frames per util.c:331-442
 // inccl_switch_ingress runs the first three, inccl_switch_egress the last,
 // inccl_switch_batch all four.  The ICRC is linear over GF(2), so every CRC
 // here is a XOR of table lookups reduced over the wave with DPP -- no serial
@@ -330,15 +331,19 @@ __device__ __forceinline__ void put16(uint8_t* p, uint32_t v)
 }
 
 // Header image of child c's egress frames (util.c:348-388) with opcode and PSN
-// left zero: identical for every frame of that child and RETH flag, so each
-// block builds the 2*fan_in images once into LDS and frames copy them word-wise.
+// left zero: identical for every frame of that child and kind, so each block
+// builds the 3*fan_in images once into LDS and frames copy them word-wise.
+// Kinds: data (PACKET_TYPE_DATA), RETH (PACKET_TYPE_RETH) and ACK
+// (PACKET_TYPE_ACK: opcode 0x11 in the image, PSN and AETH left zero).
 constexpr int kHdrImg = 80;   // 70 header bytes (with RETH slot), rows 16-byte aligned (read as 16-byte chunks)
+constexpr int kImgReth = 1, kImgAck = 2;   // (kind 0: data)
+constexpr int kAckLen = 14 + 20 + 8 + 12 + 4 + 4;   // 62 B: headers, AETH, ICRC (util.c:341-343)
 
-__device__ void build_header_image(uint32_t (&w)[kHdrImg / 4], const InccFrameTemplate& h, bool wf)
+__device__ void build_header_image(uint32_t (&w)[kHdrImg / 4], const InccFrameTemplate& h, int kind)
 {
     // built in registers (every index a constant once unrolled), stored as words
     uint8_t fr[kHdrImg];
-    const int total = 14 + 20 + 8 + 12 + (wf ? 16 : 0) + kLanes * 4 + 4;   // util.c:341-345
+    const int total = kind == kImgAck ? kAckLen : 14 + 20 + 8 + 12 + (kind == kImgReth ? 16 : 0) + kLanes * 4 + 4;   // util.c:341-345
 #pragma unroll
     for (int i = 0; i < kHdrImg; ++i) fr[i] = 0;
 #pragma unroll
@@ -368,6 +373,7 @@ __device__ void build_header_image(uint32_t (&w)[kHdrImg / 4], const InccFrameTe
     put16(udp + 2, h.dst_port);
     put16(udp + 4, (uint32_t)(total - 14 - 20));
     uint8_t* bth = udp + 8;                                          // util.c:376-388
+    bth[0] = kind == kImgAck ? 0x11 : 0x00;                          // util.c:377-380
     bth[2] = 0xFF; bth[3] = 0xFF;
     const uint32_t q = h.qp & 0x00FFFFFFu;
     bth[4] = (uint8_t)(q >> 24); bth[5] = (uint8_t)(q >> 16); bth[6] = (uint8_t)(q >> 8); bth[7] = (uint8_t)q;
@@ -396,6 +402,10 @@ constexpr int kVarBytes = 21;   // opcode, 4 PSN bytes, 16 RETH bytes
 __device__ uint32_t g_lane16[8][16][kWave];            // [nibble][value][lane] = Z_{16 (63 - lane)}(value << 4 nibble)
 __device__ uint32_t g_var[5 + kVarBytes][2][16];     // [var_row(reth, byte)][nibble][value]: contribution at the message end
 __device__ uint32_t g_z1024[8][16];                   // Z_1024(value << 4 nibble)
+// The ACK's ICRC message is frame bytes 10-57 (48 B, no payload): its variable
+// bytes are the PSN (frame 51-53) and the AETH (54-57, util.c:391-395)
+constexpr int kAckVar = 7, kAckMsg = 48;
+__device__ uint32_t g_ackvar[kAckVar][2][16];       // [byte 51 + k][nibble][value]: contribution at the message end
 
 // variable-byte rows: a RETH-less frame's 5 (opcode, PSN) at rows 0-4, a RETH
 // frame's 21 (opcode, PSN, RETH) at rows 5-25
@@ -505,11 +515,17 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
 //
 // Arrival bitmap: every frame classifies against the bitmap as it was before
 // the batch, while the PSN's leader writes the new one in the same launch.  A
-// slot holds two 64-bit words {bits, tag = the batch that wrote them}; batch g
-// writes word g & 1 only, and reads the newer of the words whose tag is not g.
-// Whether a reader sees a word before or after batch g's store, it gets the
-// pre-batch bitmap (64-bit accesses are single-copy atomic).  The recycle
-// writes both words (no frame of the batch reads that slot).
+// slot holds two 64-bit words {bits, tag = the batch that wrote them}.  Batch g
+// reads the newer of the words whose tag is not g (arrival_before), and its
+// leader overwrites the OTHER word -- the one arrival_before did not select --
+// with tag g.  The selected word is then never touched during batch g, so a
+// reader gets the pre-batch bitmap whether it loads before or after the
+// leader's store (64-bit accesses are single-copy atomic; after the store the
+// overwritten word carries tag g and is skipped).  Overwriting a fixed word
+// (say g & 1) would be wrong: when the slot's last arrivals came in batch g - 2
+// and none in g - 1, word g & 1 IS the pre-batch bitmap, and a reader after the
+// store would fall back to the older word.  The recycle writes both words (no
+// frame of the batch reads that slot).
 // ---------------------------------------------------------------------------
 constexpr int kApplyWaves = 8;    // the sum kernel: one pair per wave, 8-wave blocks (1, 2, 4, 16: 35.1-36.4 us, no better)
 
@@ -523,13 +539,18 @@ struct ApplyArgs {
     int wide;                        // 16-byte aligned rows
 };
 
-// the arrival bitmap as it was before batch g: the newer of the two tagged
-// words that batch g did not write (nts.c:59)
-__device__ __forceinline__ uint32_t arrival_before(uint64_t w0, uint64_t w1, uint32_t g)
+// which of a slot's two tagged words holds the arrival bitmap as it was before
+// batch g (nts.c:59): the newer of those whose tag is not g (0 or 1)
+__device__ __forceinline__ uint32_t arrival_sel(uint64_t w0, uint64_t w1, uint32_t g)
 {
     const uint32_t t0 = (uint32_t)(w0 >> 32), t1 = (uint32_t)(w1 >> 32);
     const uint32_t d0 = t0 == g ? 0xFFFFFFFFu : g - t0, d1 = t1 == g ? 0xFFFFFFFFu : g - t1;
-    return d0 <= d1 ? (uint32_t)w0 : (uint32_t)w1;
+    return d0 <= d1 ? 0u : 1u;
+}
+
+__device__ __forceinline__ uint32_t arrival_before(uint64_t w0, uint64_t w1, uint32_t g)
+{
+    return arrival_sel(w0, w1, g) ? (uint32_t)w1 : (uint32_t)w0;
 }
 
 // A buffer resource over [base, base + bytes) whose fields are wave-uniform by
@@ -614,7 +635,8 @@ __global__ __launch_bounds__(kClassifyBlock) void k_ingress_classify(InccSwitchS
 #pragma unroll
         for (int j = 0; j < 5; ++j) rw[j] = fw[13 + j];
     }
-    const uint32_t pre = arrival_before(opaque64(a0), opaque64(a1), g);
+    const uint32_t sel = arrival_sel(opaque64(a0), opaque64(a1), g);
+    const uint32_t pre = (uint32_t)(sel ? a1 : a0);
     // the PSN's ports: which count in this batch (first copy, not in before),
     // when each counts (1 + frame index; 0 = before the batch, ~0 = not yet)
     uint32_t cports = 0, wfs = 0, done = 0, mine = 0xFFFFFFFFu;
@@ -653,9 +675,10 @@ __global__ __launch_bounds__(kClassifyBlock) void k_ingress_classify(InccSwitchS
         action[f] = fin;
         return;
     }
-    // the leader: the slot's new arrival word, the recycle, the sum's orders
+    // the leader: the slot's new arrival word (over the word that does NOT hold
+    // the pre-batch bitmap, see above), the recycle, the sum's orders
     const bool complete = done != 0xFFFFFFFFu;
-    s.arrival[2 * (size_t)slot + (g & 1u)] =
+    s.arrival[2 * (size_t)slot + (sel ^ 1u)] =
         ((uint64_t)g << 32) | (pre | cports | (complete ? result_bit : 0u));   // nts.c:359, :366
     if (complete) {   // clear_state_data(psn + WINDOW), nts.c:235-242, :367
         const uint32_t rs = (psn + (s.slots >> 1)) & (s.slots - 1);
@@ -743,6 +766,7 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
         acc.z += q[2];
         acc.w += q[3];
     };
+    const uint32_t g = s.gen[0];   // this batch's generation (classify stored it)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         if (!(act[k] & kActLeader)) continue;
@@ -754,7 +778,6 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
             cports = ((uint32_t)act[k] >> 16) & 0xFFu;
             wfs = (uint32_t)act[k] >> 24;
         } else {   // fan_in > 8: the counted ports are the new arrival word's bits that the old one lacks
-            const uint32_t g = s.gen[0];
             const uint64_t w0 = s.arrival[2 * (size_t)slot], w1 = s.arrival[2 * (size_t)slot + 1];
             const uint32_t now = (uint32_t)((uint32_t)(w0 >> 32) == g ? w0 : w1);
             cports = now & ~arrival_before(w0, w1, g) & ((1u << fan) - 1u);
@@ -787,10 +810,14 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
             const bool two = rest != 0;
             rest &= rest - 1;
             const uint64_t ka = s.first[(size_t)slot * fan + pa], kb = s.first[(size_t)slot * fan + pb];
-            const uint32_t fa = (uint32_t)ka >> 1, fb = (uint32_t)kb >> 1;
+            // a counted port's key is this batch's (tag ~g) by construction; any
+            // other key's frame index would name a row of an earlier batch --
+            // possibly past this one's end -- so it is never read
+            const bool va = (uint32_t)(ka >> 32) == ~g, vb = two && (uint32_t)(kb >> 32) == ~g;
+            const uint32_t fa = va ? (uint32_t)ka >> 1 : 0u, fb = vb ? (uint32_t)kb >> 1 : 0u;
             if (A.wide) {
-                const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A.frames + (int64_t)fa * stride, stride);
-                const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(A.frames + (int64_t)fb * stride, two ? stride : 0);
+                const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A.frames + (int64_t)fa * stride, va ? stride : 0);
+                const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(A.frames + (int64_t)fb * stride, vb ? stride : 0);
                 const u4 xa = __builtin_amdgcn_raw_buffer_load_b128(ra, 48 + 16 * lane, 0, 0);
                 const u4 ea = __builtin_amdgcn_raw_buffer_load_b128(ra, lane < 2 ? 1072 + 16 * lane : kOobOffset, 0, 0);
                 const u4 xb = __builtin_amdgcn_raw_buffer_load_b128(rb, 48 + 16 * lane, 0, 0);
@@ -802,9 +829,11 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
                     add(acc, q);
                 }
             } else {
-                payload16(A.frames + (int64_t)fa * stride, (uint32_t)ka & 1u, lane, false, q);
-                add(acc, q);
-                if (two) {
+                if (va) {
+                    payload16(A.frames + (int64_t)fa * stride, (uint32_t)ka & 1u, lane, false, q);
+                    add(acc, q);
+                }
+                if (vb) {
                     payload16(A.frames + (int64_t)fb * stride, (uint32_t)kb & 1u, lane, false, q);
                     add(acc, q);
                 }
@@ -879,8 +908,9 @@ struct EgressLds {
     uint32_t lane16[8][16][kWave];
     uint32_t var[kVarRows][2][16];
     uint32_t z1024[8][16];
-    uint32_t hcrc[2 * 31];                                  // H_c for (child, RETH flag)
-    __attribute__((aligned(16))) uint8_t img[2 * 31][kHdrImg];
+    uint32_t ackvar[kAckVar][2][16];
+    uint32_t hcrc[3 * 31];                                  // H_c: [2 c + RETH flag] data, [2 fan_in + c] ACK
+    __attribute__((aligned(16))) uint8_t img[3 * 31][kHdrImg];
 };
 
 // The raw CRC of 16 bytes (a[]: memory order, little-endian words) as 16 byte
@@ -906,12 +936,13 @@ __device__ __forceinline__ uint32_t seg16(const EgressLds& t, const uint32_t (&a
     return xor3(xor3(s[0], s[1], s[2]), xor3(s[3], s[4], s[5]), s[6]) ^ s[7];
 }
 
-// The tables, the 2 fan_in header images and their ICRC terms H_c into the
+// The tables, the 3 fan_in header images and their ICRC terms H_c into the
 // block's LDS (ends with a block barrier).  H_c: quad i of the block takes
 // image i; the header part of the ICRC message (doff - 10 bytes: 44, or 60
-// with a RETH) is right-aligned in a 64-byte window (leading zeros do not
-// change a raw CRC), lane q of the quad takes window bytes 16 q .. 16 q + 15,
-// and the quad's XOR is shifted past the 1024-byte payload.
+// with a RETH; an ACK's whole 48-byte message) is right-aligned in a 64-byte
+// window (leading zeros do not change a raw CRC), lane q of the quad takes
+// window bytes 16 q .. 16 q + 15, and the quad's XOR of a data image is
+// shifted past the 1024-byte payload.
 __device__ void egress_setup(EgressLds& t, const InccFrameTemplate* __restrict__ tmpl, int fan)
 {
     // the tables as 16-byte words, every thread's loads issued before its
@@ -923,15 +954,18 @@ __device__ void egress_setup(EgressLds& t, const InccFrameTemplate* __restrict__
     const u4* gv = reinterpret_cast<const u4*>(&g_var[0][0][0]);     // kVarRows * 8
     const u4* gz = reinterpret_cast<const u4*>(&g_z1024[0][0]);      // 32
     const u4 s0 = gs[x], l0 = gl[x], l1 = gl[x + 1024];
+    const u4* ga = reinterpret_cast<const u4*>(&g_ackvar[0][0][0]);  // kAckVar * 8
     const u4 v0 = x < kVarRows * 8 ? gv[x] : u4{}, z0 = x < 32 ? gz[x] : u4{};
+    const u4 av = x < kAckVar * 8 ? ga[x] : u4{};
     uint32_t img[kHdrImg / 4];
-    if (x < 2 * fan) build_header_image(img, tmpl[x >> 1], (x & 1) != 0);
+    if (x < 3 * fan) build_header_image(img, tmpl[x < 2 * fan ? x >> 1 : x - 2 * fan], x < 2 * fan ? (x & 1) : kImgAck);
     reinterpret_cast<u4*>(&t.segb[0][0])[x] = s0;
     reinterpret_cast<u4*>(&t.lane16[0][0][0])[x] = l0;
     reinterpret_cast<u4*>(&t.lane16[0][0][0])[x + 1024] = l1;
     if (x < kVarRows * 8) reinterpret_cast<u4*>(&t.var[0][0][0])[x] = v0;
     if (x < 32) reinterpret_cast<u4*>(&t.z1024[0][0])[x] = z0;
-    if (x < 2 * fan) {
+    if (x < kAckVar * 8) reinterpret_cast<u4*>(&t.ackvar[0][0][0])[x] = av;
+    if (x < 3 * fan) {
 #pragma unroll
         for (int k = 0; k < kHdrImg / 16; ++k)
             reinterpret_cast<u4*>(t.img[x])[k] = u4{img[4 * k], img[4 * k + 1], img[4 * k + 2], img[4 * k + 3]};
@@ -939,8 +973,8 @@ __device__ void egress_setup(EgressLds& t, const InccFrameTemplate* __restrict__
     __syncthreads();
     const int i = threadIdx.x >> 2, q = threadIdx.x & 3;
     uint32_t c = 0;
-    if (i < 2 * fan) {
-        const int hdr = (i & 1) ? 60 : 44;
+    if (i < 3 * fan) {
+        const int hdr = i >= 2 * fan ? kAckMsg : (i & 1) ? 60 : 44;
         uint32_t a[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -967,7 +1001,8 @@ __device__ void egress_setup(EgressLds& t, const InccFrameTemplate* __restrict__
     uint32_t r = 0;
 #pragma unroll
     for (int n = 0; n < 8; ++n) r ^= t.z1024[n][(c >> (4 * n)) & 15u];
-    if (i < 2 * fan && q == 0) t.hcrc[i] = r;
+    if (i >= 2 * fan) r = c;   // an ACK has no payload after its header
+    if (i < 3 * fan && q == 0) t.hcrc[i] = r;
     __syncthreads();
 }
 
@@ -1145,6 +1180,54 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
     }
 }
 
+// ACK reflection (nts.c:403-406; send_roce_ack :284-298, a PACKET_TYPE_ACK
+// frame per util.c:331-442): every ACK input frame j of a chunk (its claim
+// result INCCL_SW_ACK, bit 12 of its lane's `bits`) sends one 62-B frame back
+// to its own port, row (f0 + j) fan_in + port: the port's ACK image (opcode
+// 0x11) with the PSN (bytes 51-53, no ack-request bit) and the AETH
+// htonl((psn + 1) | 0x1f000000) (54-57) patched in, and the ICRC ~(H_ack,c ^
+// the 7 variable bytes' terms).  Lane 4 j + q writes the frame's 16-byte chunk
+// q (bytes 62-63 are written as zero).  Per-lane rows: plain global stores
+// under the ACK lanes' mask, issued before the chunk's data frames.
+template <bool kOut16>
+__device__ __forceinline__ void egress_acks(const EgressLds& t, const EgressArgs& A, uint32_t f0, uint32_t bits,
+                                            uint32_t psn, int fan, int lane)
+{
+    const int j = lane >> 2, q = lane & 3;
+    const uint32_t bj = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * j, (int)bits);
+    const uint32_t pj = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * j, (int)psn) & 0x00FFFFFFu;
+    const bool ak = j < (int)egress_chunk(fan) && ((bj >> 12) & 1u);
+    if (!__ballot(ak)) return;
+    if (!ak) return;
+    const uint32_t c = bj >> 16, msn = pj + 1u;
+    const uint32_t aeth = msn | 0x1f000000u;
+    // the variable bytes (frame 51 .. 57): PSN bytes 2..0, AETH bytes 3..0 (big-endian)
+    uint32_t crc = t.hcrc[2 * fan + c];
+#pragma unroll
+    for (int k = 0; k < kAckVar; ++k) {
+        const uint32_t b = k < 3 ? (pj >> (8 * (2 - k))) & 0xFFu : (aeth >> (8 * (6 - k))) & 0xFFu;
+        crc ^= t.ackvar[k][0][b & 15u] ^ t.ackvar[k][1][b >> 4];
+    }
+    crc = ~crc;   // util.c:424-426
+    u4 v = reinterpret_cast<const u4*>(t.img[2 * fan + c])[q];
+    if (q == 3) {   // bytes 48-63: QPN low bytes (image), 0, PSN, AETH, ICRC (host order), 2 zero bytes
+        v.x |= ((pj >> 16) & 0xFFu) << 24;
+        v.y = ((pj >> 8) & 0xFFu) | ((pj & 0xFFu) << 8) | ((aeth >> 24) << 16) | (((aeth >> 16) & 0xFFu) << 24);
+        v.z = ((aeth >> 8) & 0xFFu) | ((aeth & 0xFFu) << 8) | (crc << 16);
+        v.w = crc >> 16;
+    }
+    uint8_t* row = A.out + ((size_t)(f0 + (uint32_t)j) * fan + c) * A.out_stride + 16 * q;
+    if (kOut16) {
+        *reinterpret_cast<u4*>(row) = v;
+    } else {
+        uint32_t* w = reinterpret_cast<uint32_t*>(row);
+        w[0] = v.x;
+        w[1] = v.y;
+        w[2] = v.z;
+        w[3] = v.w;
+    }
+}
+
 // kFan: 2, 3, 4 or 8 (the children loop unrolled), or 0 (A.fan, a loop).
 // kOut16: 16-byte aligned output rows.
 template <int kFan, bool kOut16>
@@ -1198,19 +1281,24 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
         const bool in = lane < (int)nf;
         const bool all = in && act == INCCL_SW_COMPLETED;
         const bool one = in && act == INCCL_SW_REPLAY && port < (uint32_t)fan;
+        const bool ack = in && act == INCCL_SW_ACK && port < (uint32_t)fan;
         const uint32_t bits = op | (is_write_first((uint8_t)op) ? 1u << 8 : 0u) | (in ? 1u << 9 : 0u) |
-                              (all ? 1u << 10 : 0u) | (one ? 1u << 11 : 0u) | ((port & 0xFFFFu) << 16);
+                              (all ? 1u << 10 : 0u) | (one ? 1u << 11 : 0u) | (ack ? 1u << 12 : 0u) |
+                              ((port & 0xFFFFu) << 16);
         {   // the chunk's row lengths: entry e = f fan + c, lane-parallel (util.c:341-345)
             const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
                 A.out_len + (size_t)f0 * fan, 0, (int)(4 * nf * fan), 0x00020000);
             for (int k = 0; k < (kEgressChunk * fan + kWave - 1) / kWave; ++k) {
                 const int e = lane + kWave * k, fr = e / fan, c = e - fr * fan;
                 const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (fr & (kWave - 1)), (int)bits);
-                const bool on = ((b >> 10) & 1u) || (((b >> 11) & 1u) && (b >> 16) == (uint32_t)c);
+                const bool mine = (b >> 16) == (uint32_t)c;
+                const bool on = ((b >> 10) & 1u) || (((b >> 11) & 1u) && mine);
                 const uint32_t total = 54 + 16 * ((b >> 8) & 1u) + kLanes * 4 + 4;
-                __builtin_amdgcn_raw_buffer_store_b32(on ? total : 0u, rl, 4 * e, 0, 0);
+                const uint32_t len = on ? total : (((b >> 12) & 1u) && mine ? (uint32_t)kAckLen : 0u);
+                __builtin_amdgcn_raw_buffer_store_b32(len, rl, 4 * e, 0, 0);
             }
         }
+        egress_acks<kOut16>(t, A, f0, bits, psn, fan, lane);
         uint64_t m = __ballot(all || one);
         if (!m) continue;
         // a frame of the ring is its lane in the chunk (-1: none); its words
@@ -1275,6 +1363,7 @@ uint32_t host_seg34[kSeg2][2][16];
 uint32_t host_lane_shift32[8][16][32];
 uint32_t host_var[5 + kVarBytes][2][16];
 uint32_t host_z1024[8][16];
+uint32_t host_ackvar[kAckVar][2][16];
 uint32_t host_segb[16][256];
 bool g_tables_ready[64];
 std::mutex g_tables_mu;
@@ -1333,7 +1422,12 @@ int ensure_tables()
                     if (wf || k < 5) host_var[wf ? 5 + k : k][h][v] = p < hdr ? zeros_append(host_tab[v << (4 * h)], hdr - 1 - p + 1024) : 0u;
         }
     }
+    // the ACK: byte 51 + k of the frame is message byte 41 + k of 48
+    for (int k = 0; k < kAckVar; ++k)
+        for (int h = 0; h < 2; ++h)
+            for (uint32_t v = 0; v < 16; ++v) host_ackvar[k][h][v] = zeros_append(host_tab[v << (4 * h)], kAckMsg - 1 - (41 + k));
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_lane16), host_lane16, sizeof(host_lane16));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_ackvar), host_ackvar, sizeof(host_ackvar));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_var), host_var, sizeof(host_var));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_z1024), host_z1024, sizeof(host_z1024));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_seg34), host_seg34, sizeof(host_seg34));

@@ -3,10 +3,11 @@
  * The reference's root switch keeps its aggregation state in globals
  * (non_termination_switch.c:55-60) and processes one frame at a time on one
  * CPU thread (nts.c:508-530).  Here the state lives in HBM and frames are
- * processed in batches: ingress launches (parse + idempotent add + the recycle,
- * clear_state_data(psn + window), nts.c:303-483, :235-242, :367) and one egress
- * launch (frame build + ICRC, util.c:331-442) -- or one batch call whose apply
- * kernel builds the broadcast frames itself (inccl_switch_batch).  No host state changes per batch,
+ * processed in batches: ingress launches (claim, classify, sum: parse +
+ * idempotent add + the recycle, clear_state_data(psn + window), nts.c:303-483,
+ * :235-242, :367) and one egress launch (broadcast / replay frames and ACK
+ * reflections, frame build + ICRC, util.c:331-442) -- or one inccl_switch_batch
+ * call that issues the same four launches on one stream.  No host state changes per batch,
  * so a batch's launches can be captured in a hipGraph and replayed.  A batch must span
  * fewer than slots/2 PSNs -- the reference's window of 8 packets over 16 slots
  * (nts.c:21-22) has the same ratio. */

@@ -23,10 +23,15 @@
 /* ------------------------------------------------------------------ */
 /* rccl                                                                 */
 /* ------------------------------------------------------------------ */
+/* the result code's text and RCCL's own account of the failure
+ * (ncclGetLastError: the calling thread's last error message, e.g. why
+ * ncclCommInitRank refused -- "invalid usage" alone does not say) */
 static int nccl_check(ncclResult_t r, const char *what)
 {
     if (r == ncclSuccess) return 0;
-    return inccl_set_error(INCCL_ERR_NCCL, "%s: %s", what, ncclGetErrorString(r));
+    const char *last = ncclGetLastError(NULL);
+    return inccl_set_error(INCCL_ERR_NCCL, "%s: %s%s%s", what, ncclGetErrorString(r), last && *last ? ": " : "",
+                           last && *last ? last : "");
 }
 
 /* a collective's own return code, then the communicator's asynchronous error

@@ -121,7 +121,11 @@ const char *inccl_group_transport(const struct inccl_group *group);
  * (whole MiB, at least 1 MiB).  inccl_ipc_max_bytes: this process;
  * inccl_group_ipc_max_bytes: the smallest over the group's ranks, agreed at
  * creation -- a bucket whose IPC buffer would exceed it is refused on every
- * rank alike. */
+ * rank alike.  The first call of inccl_ipc_max_bytes, inccl_hsa_runtime_release
+ * or inccl_hsa_runtime_build in a process INITIALISES HIP (hipInit) and briefly
+ * HSA (hsa_init / hsa_shut_down) to ask the runtime: do not call them in a
+ * process that must stay free of a GPU context (one that will fork or exec
+ * GPU work). */
 size_t inccl_ipc_max_bytes(void);
 size_t inccl_group_ipc_max_bytes(const struct inccl_group *group);
 /* The ROCm release of the HSA runtime this process mapped, as that runtime
@@ -239,9 +243,9 @@ int inccl_allreduce_f32_host(struct inccl_communicator *comm, const float *src_h
 
 /* ---------- the reference switch's dataplane on the GPU ----------
  * non_termination_switch.c:303-501 (parse, per-PSN first-arrival aggregation,
- * broadcast / replay) and util.c:331-442 (egress frame build, payload htonl,
- * RoCE ICRC), batched: a batch of ingress frames -> ingress (claim + apply) ->
- * egress, or one inccl_switch_batch call.  Frames live in device memory at a fixed `stride` (multiple of
+ * broadcast / replay, ACK reflection) and util.c:331-442 (egress frame build,
+ * payload htonl, RoCE ICRC), batched: a batch of ingress frames -> ingress
+ * (claim, classify, sum) -> egress, or one inccl_switch_batch call.  Frames live in device memory at a fixed `stride` (multiple of
  * 4 B, at least 64; every read stays inside a frame's row).  Frame order within
  * a batch is the arrival order: the actions are exactly those of the reference
  * processing the batch's frames one at a time (the first copy of a (psn, port)
@@ -253,7 +257,7 @@ int inccl_allreduce_f32_host(struct inccl_communicator *comm, const float *src_h
 #define INCCL_SW_COMPLETED 2  /* first arrival completing the slot: broadcast (nts.c:365-372) */
 #define INCCL_SW_DROPPED 3    /* retransmit into an incomplete slot (nts.c:353) */
 #define INCCL_SW_REPLAY 4     /* retransmit of a completed slot: resend to its port (nts.c:354-356) */
-#define INCCL_SW_ACK 5        /* UP ACK: reflected by the host (nts.c:403-406) */
+#define INCCL_SW_ACK 5        /* UP ACK: egress reflects a 62-B ACK to its port (nts.c:403-406) */
 #define INCCL_SW_INVALID 6    /* bad port or payload length (nts.c:350) */
 
 /* One child connection (the fields of util.h connection_t that egress uses). */
@@ -280,8 +284,10 @@ const int32_t *inccl_switch_slot(struct inccl_switch *sw, uint32_t psn);
 int inccl_switch_ingress(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
                          const int32_t *ports_dev, int32_t *action_dev, uint32_t *psn_dev, void *stream);
 /* For every COMPLETED frame i: fan_in egress frames to children c at
- * out_dev[(i*fan_in + c) * out_stride]; for every REPLAY frame: one frame to
- * its port.  out_len_dev[i*fan_in + c] = frame bytes or 0 (bytes past a frame, up to its 16-byte
+ * out_dev[(i*fan_in + c) * out_stride] with frame i's opcode (and, for a
+ * WRITE_FIRST / WRITE_ONLY opcode, child c's kept RETH); for every REPLAY frame:
+ * one such frame to its port; for every ACK frame: the 62-B ACK of
+ * send_roce_ack (opcode 0x11, its PSN, AETH MSN = PSN + 1) to its port.  out_len_dev[i*fan_in + c] = frame bytes or 0 (bytes past a frame, up to its 16-byte
  * rounded length, are written as zero or left as they were).  templates_dev holds
  * fan_in inccl_frame_template records (device memory). */
 int inccl_switch_egress(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,

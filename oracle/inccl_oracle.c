@@ -198,60 +198,91 @@ uint32_t orc_checksum_q32(const int32_t *q, size_t n, uint64_t index_base)
 /* ------------------------------------------------------------------ */
 /* root-switch aggregation (nts.c:231-250, :303-501)                    */
 /* ------------------------------------------------------------------ */
-#define SLOT(psn) ((psn) % ORC_SW_SLOTS)          /* nts.c:25 Idx() */
+#define SLOT(sw, psn) ((psn) & ((sw)->slots - 1))    /* nts.c:25 Idx(): psn % N, N a power of two */
+
+size_t orc_switch_bytes(void) { return sizeof(orc_switch); }
+
+const int32_t *orc_switch_slot(const orc_switch *sw, uint32_t psn) { return sw->aggregator[SLOT(sw, psn)]; }
+
+int orc_switch_init_ring(orc_switch *sw, int fan_in, uint32_t slots)
+{
+    if (fan_in < 1 || fan_in > ORC_MAX_FAN_IN || slots < 2 || slots > ORC_SW_MAX_SLOTS || (slots & (slots - 1)))
+        return -1;
+    memset(sw, 0, sizeof(*sw));
+    sw->fan_in = fan_in;
+    sw->slots = slots;
+    sw->window = slots / 2;                                    /* nts.c:21-22: N = 2 * WINDOW_SIZE */
+    return 0;
+}
 
 void orc_switch_init(orc_switch *sw, int fan_in)
 {
-    memset(sw, 0, sizeof(*sw));
-    sw->fan_in = fan_in;
+    orc_switch_init_ring(sw, fan_in, ORC_SW_SLOTS);            /* the reference's ring: 16 slots, window 8 */
 }
 
 static void sw_clear(orc_switch *sw, uint32_t psn)
 {
     /* nts.c:235-242 clear_state_data */
-    const int s = SLOT(psn);
+    const uint32_t s = SLOT(sw, psn);
     sw->arrival_state[s] = 0;
     sw->degree[s] = 0;
+    memset(sw->reth_keeper[s], 0, sizeof(sw->reth_keeper[s]));
     memset(sw->aggregator[s], 0, sizeof(sw->aggregator[s]));
 }
 
-static inline int sw_all_fan_in(const orc_switch *sw, int s)
+static inline int sw_all_fan_in(const orc_switch *sw, uint32_t s)
 {
     const uint32_t mask = 0xffffffffu >> (32 - sw->fan_in);   /* nts.c:29 */
     return (sw->arrival_state[s] & mask) == mask;              /* nts.c:244-246 */
 }
 
-int orc_switch_ingress(orc_switch *sw, int port, uint32_t psn,
-                       const uint32_t *payload_be, uint32_t *egress_be)
+/* The root branch of nts.c:347-374 / :427-455 for one counted-or-not data
+ * packet; the RETH of a WRITE_FIRST packet (NULL otherwise) goes into the
+ * keeper with the first transmission (nts.c:442). */
+static int sw_data(orc_switch *sw, int port, uint32_t psn, const uint8_t *payload_be_bytes, const uint8_t *reth)
 {
-    const int s = SLOT(psn);
+    const uint32_t s = SLOT(sw, psn);
     const uint32_t port_bit = 1u << port;
     const uint32_t result_bit = 1u << sw->fan_in;              /* bit FAN_IN (nts.c:366) */
-    sw->degree[s] += 1;                                        /* nts.c:351 */
+    sw->degree[s] += 1;                                        /* nts.c:351, :431 */
 
-    if (sw->arrival_state[s] & port_bit) {                     /* nts.c:353 retransmit */
-        if (sw->arrival_state[s] & result_bit) {               /* nts.c:354-356 replay */
-            for (int i = 0; i < ORC_LANES; ++i) egress_be[i] = to_be((uint32_t)sw->aggregator[s][i]);
+    if (sw->arrival_state[s] & port_bit) {                     /* nts.c:353 / :435 retransmit */
+        if (sw->arrival_state[s] & result_bit) {               /* nts.c:354-356 / :436-438 replay */
             sw->replays++;
             return ORC_SW_REPLAY;
         }
         return ORC_SW_DROPPED;
     }
-    /* first transmission: nts.c:359-363 */
+    /* first transmission: nts.c:359-363 / :441-445 */
     sw->arrival_state[s] |= port_bit;
+    if (reth) memcpy(sw->reth_keeper[s][port], reth, ORC_RETH_HDR);
     {
         uint32_t *acc = (uint32_t *)sw->aggregator[s];
-        for (int i = 0; i < ORC_LANES; ++i) acc[i] += to_be(payload_be[i]);
+        for (int i = 0; i < ORC_LANES; ++i) {
+            uint32_t w;
+            memcpy(&w, payload_be_bytes + 4 * i, 4);
+            acc[i] += to_be(w);                                /* ntohl */
+        }
     }
     sw->adds++;
-    if (sw_all_fan_in(sw, s)) {                                /* nts.c:365-372 */
+    if (sw_all_fan_in(sw, s)) {                                /* nts.c:365-372 / :447-453 */
         sw->arrival_state[s] |= result_bit;
-        sw_clear(sw, psn + ORC_SW_WINDOW);                     /* nts.c:367 */
-        /* egress re-encode (util.c:403-405) */
-        for (int i = 0; i < ORC_LANES; ++i) egress_be[i] = to_be((uint32_t)sw->aggregator[s][i]);
+        sw_clear(sw, psn + sw->window);                        /* nts.c:367 / :449 */
         return ORC_SW_BROADCAST;
     }
     return ORC_SW_ABSORBED;
+}
+
+int orc_switch_ingress(orc_switch *sw, int port, uint32_t psn,
+                       const uint32_t *payload_be, uint32_t *egress_be)
+{
+    const int rc = sw_data(sw, port, psn, (const uint8_t *)payload_be, NULL);
+    if (rc == ORC_SW_REPLAY || rc == ORC_SW_BROADCAST) {
+        /* egress re-encode (util.c:403-405) */
+        const uint32_t s = SLOT(sw, psn);
+        for (int i = 0; i < ORC_LANES; ++i) egress_be[i] = to_be((uint32_t)sw->aggregator[s][i]);
+    }
+    return rc;
 }
 
 /* ------------------------------------------------------------------ */
@@ -332,12 +363,18 @@ static inline void put32(uint8_t *p, uint32_t v)
     p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
 }
 
-size_t orc_build_data_frame(uint8_t *frame, const orc_frame_hdr *h, const int32_t *payload_host,
-                            int n_words, int with_reth, const uint8_t *reth16)
+/* util.c:331-442 build_eth_packet, for its three packet types the switch
+ * sends: PACKET_TYPE_DATA (payload, no RETH), PACKET_TYPE_RETH (RETH +
+ * payload) and PACKET_TYPE_ACK (AETH, no payload). */
+enum { PKT_DATA, PKT_RETH, PKT_ACK };
+
+static size_t build_frame(uint8_t *frame, int type, const orc_frame_hdr *h, const int32_t *payload_host, int n_words,
+                          uint32_t msn, const uint8_t *reth16)
 {
-    const int data_len = n_words * 4;
+    const int data_len = type == PKT_ACK ? 0 : n_words * 4;
     size_t total = ORC_ETH_HDR + ORC_IP_HDR + ORC_UDP_HDR + ORC_BTH_HDR + (size_t)data_len + ORC_ICRC_LEN;
-    if (with_reth) total += ORC_RETH_HDR;                               /* util.c:341-345 */
+    if (type == PKT_ACK) total += ORC_AETH_HDR;                         /* util.c:342-343 */
+    else if (type == PKT_RETH) total += ORC_RETH_HDR;                   /* util.c:344-345 */
     uint8_t *eth = frame;
     memcpy(eth, h->dst_mac, 6);                                         /* util.c:349-351 */
     memcpy(eth + 6, h->src_mac, 6);
@@ -358,18 +395,90 @@ size_t orc_build_data_frame(uint8_t *frame, const orc_frame_hdr *h, const int32_
     put16(udp + 4, (uint16_t)(total - ORC_ETH_HDR - ORC_IP_HDR));
     udp[6] = 0; udp[7] = 0;
     uint8_t *bth = udp + ORC_UDP_HDR;                                   /* util.c:376-388 */
-    bth[0] = h->opcode; bth[1] = 0x00; bth[2] = 0xFF; bth[3] = 0xFF;
+    bth[0] = type == PKT_ACK ? 0x11 : h->opcode; bth[1] = 0x00; bth[2] = 0xFF; bth[3] = 0xFF;
     put32(bth + 4, h->qp & 0x00FFFFFFu);
-    put32(bth + 8, h->psn | 0x80000000u);
+    put32(bth + 8, type == PKT_ACK ? h->psn : (h->psn | 0x80000000u)); /* ack request on data (util.c:385-388) */
     uint8_t *d = bth + ORC_BTH_HDR;
-    if (with_reth) {                                                    /* util.c:409-417 */
-        if (reth16) memcpy(d, reth16, ORC_RETH_HDR); else memset(d, 0, ORC_RETH_HDR);
-        d += ORC_RETH_HDR;
+    if (type == PKT_ACK) {                                              /* util.c:391-397 */
+        put32(d, msn | 0x1f000000u);
+    } else {
+        if (type == PKT_RETH) {                                         /* util.c:409-417 */
+            if (reth16) memcpy(d, reth16, ORC_RETH_HDR); else memset(d, 0, ORC_RETH_HDR);
+            d += ORC_RETH_HDR;
+        }
+        for (int i = 0; i < n_words; ++i) put32(d + 4 * i, (uint32_t)payload_host[i]);   /* util.c:403-405, :419-421 */
     }
-    for (int i = 0; i < n_words; ++i) put32(d + 4 * i, (uint32_t)payload_host[i]);   /* util.c:403-405 */
     const uint32_t icrc = orc_icrc(frame);                              /* util.c:425-426 */
     memcpy(frame + total - ORC_ICRC_LEN, &icrc, 4);                     /* stored host order */
     return total;
+}
+
+size_t orc_build_data_frame(uint8_t *frame, const orc_frame_hdr *h, const int32_t *payload_host,
+                            int n_words, int with_reth, const uint8_t *reth16)
+{
+    return build_frame(frame, with_reth ? PKT_RETH : PKT_DATA, h, payload_host, n_words, 0, reth16);
+}
+
+size_t orc_build_ack_frame(uint8_t *frame, const orc_frame_hdr *h, uint32_t msn)
+{
+    return build_frame(frame, PKT_ACK, h, NULL, 0, msn, NULL);
+}
+
+/* nts.c:252-298: the connection's fields as build_eth_packet takes them (src =
+ * my_*, dst = peer_*, QPN = peer_qp) */
+static void conn_hdr(orc_frame_hdr *h, const orc_conn *c, uint32_t psn, uint8_t opcode)
+{
+    memcpy(h->src_mac, c->my_mac, 6);
+    memcpy(h->dst_mac, c->peer_mac, 6);
+    h->src_ip = c->my_ip;
+    h->dst_ip = c->peer_ip;
+    h->src_port = c->my_port;
+    h->dst_port = c->peer_port;
+    h->qp = c->peer_qp;
+    h->psn = psn;
+    h->opcode = opcode;
+}
+
+static int is_data_op(uint8_t op) { return op == 0x00 || op == 0x01 || op == 0x02 || op == 0x04 || op == 0x07 || op == 0x08; }
+static int is_wf_op(uint8_t op) { return op == 0x06 || op == 0x0A; }
+
+int orc_switch_pipeline(orc_switch *sw, const orc_conn *conns, int port, const uint8_t *frame, size_t row_len,
+                        uint8_t *out, size_t out_stride, int *out_len)
+{
+    for (int c = 0; c < sw->fan_in; ++c) out_len[c] = 0;
+    /* the root has children only: a port outside them (the reference's DOWN_*
+     * path, nts.c:408-426, :484-499, is a non-root switch's) is refused */
+    if (port < 0 || port >= sw->fan_in || row_len < 64) return ORC_SW_INVALID;
+    /* parser, nts.c:307-344 */
+    const uint8_t op = frame[42];
+    const uint32_t psn = ((uint32_t)frame[51] << 16) | ((uint32_t)frame[52] << 8) | frame[53];   /* :311 */
+    const int udp_len = ((int)frame[38] << 8) | frame[39];
+    orc_frame_hdr h;
+    if (op == 0x11) {                                          /* UP_ACK: reflect (nts.c:403-406, :284-298) */
+        conn_hdr(&h, &conns[port], psn, 0x11);
+        out_len[port] = (int)orc_build_ack_frame(out + (size_t)port * out_stride, &h, psn + 1);
+        return ORC_SW_ACK;
+    }
+    if (!is_data_op(op) && !is_wf_op(op)) return ORC_SW_IGNORED;
+    const int wf = is_wf_op(op);
+    const int data_len = udp_len - ORC_BTH_HDR - ORC_UDP_HDR - ORC_ICRC_LEN - (wf ? ORC_RETH_HDR : 0);   /* :349, :429 */
+    const size_t doff = 54 + (wf ? ORC_RETH_HDR : 0);
+    if (data_len != ORC_PAYLOAD_LEN || doff + ORC_PAYLOAD_LEN > row_len) return ORC_SW_INVALID;   /* assert, :350 */
+    const int rc = sw_data(sw, port, psn, frame + doff, wf ? frame + 54 : NULL);
+    if (rc != ORC_SW_BROADCAST && rc != ORC_SW_REPLAY) return rc;
+    /* send_roce_data (no RETH) for a data packet, send_roce_data_with_reth with
+     * the child's kept RETH for a WRITE_FIRST one; both with THIS packet's
+     * opcode (nts.c:355, :370, :437, :452) */
+    const uint32_t s = SLOT(sw, psn);
+    int32_t agg[ORC_LANES];
+    memcpy(agg, sw->aggregator[s], sizeof(agg));
+    const int c0 = rc == ORC_SW_BROADCAST ? 0 : port, c1 = rc == ORC_SW_BROADCAST ? sw->fan_in : port + 1;
+    for (int c = c0; c < c1; ++c) {
+        conn_hdr(&h, &conns[c], psn, op);
+        out_len[c] = (int)orc_build_data_frame(out + (size_t)c * out_stride, &h, agg, ORC_LANES, wf,
+                                               wf ? sw->reth_keeper[s][c] : NULL);
+    }
+    return rc;
 }
 
 /* ------------------------------------------------------------------ */

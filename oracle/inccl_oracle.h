@@ -93,17 +93,26 @@ int   orc_choose_scale(float absmax, int R);
 uint32_t orc_checksum_q32(const int32_t *q, size_t n, uint64_t index_base);
 
 /* ---------------- switch aggregation pipeline (root switch) ---------------- */
-/* State of nts.c:55-60 restated for one root switch with fan_in children. */
+/* State of nts.c:55-60 restated for one root switch with fan_in children.  The
+ * reference's ring is N = 16 slots with window 8 (nts.c:21-22); the ring here
+ * may be any power of two up to ORC_SW_MAX_SLOTS, with window = slots / 2. */
+#define ORC_SW_MAX_SLOTS 1024
 typedef struct orc_switch {
     int      fan_in;
-    int32_t  aggregator[ORC_SW_SLOTS][ORC_LANES];   /* nts.c:55 */
-    uint32_t arrival_state[ORC_SW_SLOTS];           /* nts.c:59 bitmap */
-    int      degree[ORC_SW_SLOTS];                  /* nts.c:60 */
-    uint64_t adds;                                  /* packets actually summed */
-    uint64_t replays;                               /* retransmits answered from the slot */
+    uint32_t slots, window;
+    int32_t  aggregator[ORC_SW_MAX_SLOTS][ORC_LANES];                      /* nts.c:55 */
+    uint32_t arrival_state[ORC_SW_MAX_SLOTS];                              /* nts.c:59 bitmap */
+    int      degree[ORC_SW_MAX_SLOTS];                                     /* nts.c:60 */
+    uint8_t  reth_keeper[ORC_SW_MAX_SLOTS][ORC_MAX_FAN_IN][ORC_RETH_HDR];  /* nts.c:57 */
+    uint64_t adds;                                                         /* packets actually summed */
+    uint64_t replays;                                                      /* retransmits answered from the slot */
 } orc_switch;
 
-void orc_switch_init(orc_switch *sw, int fan_in);
+size_t orc_switch_bytes(void);                      /* sizeof(orc_switch), for callers that allocate it */
+const int32_t *orc_switch_slot(const orc_switch *sw, uint32_t psn);   /* aggregator[Idx(psn)] (nts.c:55) */
+void orc_switch_init(orc_switch *sw, int fan_in);   /* the reference's 16-slot ring */
+/* 0, or -1 for fan_in outside 1..31 or slots not a power of two in 2..ORC_SW_MAX_SLOTS */
+int orc_switch_init_ring(orc_switch *sw, int fan_in, uint32_t slots);
 /* One UP data packet from child `port` with PSN `psn` and a big-endian payload of
  * ORC_LANES words (nts.c:347-374 / :427-455, root branch).
  * Returns:  ORC_SW_ABSORBED  first arrival, aggregate not complete yet
@@ -112,9 +121,39 @@ void orc_switch_init(orc_switch *sw, int fan_in);
  *           ORC_SW_REPLAY    retransmit of a completed slot; egress_be holds the aggregate
  *                            to send back to `port` only (nts.c:353-356)
  *           ORC_SW_DROPPED   retransmit of an incomplete slot (nts.c:353 with no result) */
-enum { ORC_SW_ABSORBED = 0, ORC_SW_BROADCAST = 1, ORC_SW_REPLAY = 2, ORC_SW_DROPPED = 3 };
+enum { ORC_SW_ABSORBED = 0, ORC_SW_BROADCAST = 1, ORC_SW_REPLAY = 2, ORC_SW_DROPPED = 3,
+       ORC_SW_ACK = 4, ORC_SW_IGNORED = 5, ORC_SW_INVALID = 6 };
 int orc_switch_ingress(orc_switch *sw, int port, uint32_t psn,
                        const uint32_t *payload_be, uint32_t *egress_be);
+
+/* A child connection: the util.h connection_t fields that send_roce_data /
+ * _with_reth / send_roce_ack hand to build_eth_packet (nts.c:252-298) -- src =
+ * my_*, dst = peer_*, BTH QPN = peer_qp.  Same 28-byte layout as the engine's
+ * struct inccl_frame_template. */
+typedef struct orc_conn {
+    uint8_t  my_mac[6], peer_mac[6];
+    uint32_t my_ip, peer_ip;        /* as stored in the IP header */
+    uint16_t my_port, peer_port;    /* host order */
+    uint32_t peer_qp;
+} orc_conn;
+
+/* The whole of pipeline() (nts.c:303-501, root branch) for one frame from child
+ * `port`, frames in -> frames out: parse (opcode, PSN :311-344), UP_DATA and
+ * UP_WRITE_FIRST_ONLY aggregation with the RETH keeper (:347-374, :427-455),
+ * UP_ACK reflection (:403-406).  Row c of `out` (stride out_stride) receives
+ * the frame sent to child c and out_len[c] its length (0: none sent):
+ *   ORC_SW_BROADCAST  every child: the aggregate with the completing packet's
+ *                     opcode, with child c's kept RETH if that opcode is
+ *                     WRITE_FIRST / WRITE_ONLY (send_roce_data_with_reth)
+ *   ORC_SW_REPLAY     child `port`: the same, with the retransmit's opcode
+ *   ORC_SW_ACK        child `port`: the 62-B ACK (opcode 0x11, AETH) for the PSN
+ *   ORC_SW_ABSORBED / DROPPED  nothing
+ *   ORC_SW_IGNORED    opcode the pipeline has no case for: nothing, no state
+ *   ORC_SW_INVALID    port >= fan_in (the root has no parent) or a payload
+ *                     length other than 1024 B (the reference asserts, :350)
+ * row_len bounds the frame's bytes (a payload past it is INVALID). */
+int orc_switch_pipeline(orc_switch *sw, const orc_conn *conns, int port, const uint8_t *frame, size_t row_len,
+                        uint8_t *out, size_t out_stride, int *out_len);
 
 /* ---------------- RoCEv2 framing + ICRC ---------------- */
 /* util.c:141-195: reflected CRC-32 (poly 0xEDB88320), init ~0, final ~. */
@@ -135,6 +174,10 @@ typedef struct orc_frame_hdr {
 } orc_frame_hdr;
 size_t orc_build_data_frame(uint8_t *frame, const orc_frame_hdr *h, const int32_t *payload_host,
                             int n_words, int with_reth, const uint8_t *reth16);
+/* util.c:331-442 for PACKET_TYPE_ACK (send_roce_ack, nts.c:284-298): opcode 0x11,
+ * BTH PSN without the ack-request bit, AETH syn_msn = htonl(msn | 0x1f000000)
+ * (util.c:342-343, :379-380, :387-388, :391-395); h->opcode is not used.  62 B. */
+size_t orc_build_ack_frame(uint8_t *frame, const orc_frame_hdr *h, uint32_t msn);
 
 /* ---------------- windowed host driver + switch, single-process loopback ---------------- */
 /* Drives R ranks through api.c:403-452 (inccl_allreduce_write: 2-message window,

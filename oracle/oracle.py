@@ -19,7 +19,8 @@ LIB_PATH = os.path.join(HERE, "liborc.so")
 PAYLOAD_COUNT = 1024   # api.h:40
 LANES = 256            # nts.c:55
 SW_SLOTS = 16          # nts.c:22
-SW_ABSORBED, SW_BROADCAST, SW_REPLAY, SW_DROPPED = 0, 1, 2, 3
+SW_ABSORBED, SW_BROADCAST, SW_REPLAY, SW_DROPPED, SW_ACK, SW_IGNORED, SW_INVALID = range(7)
+FRAME_ROW = 1152       # an output row of orc_switch_pipeline (the longest frame is 1098 B)
 
 _lib = None
 
@@ -65,6 +66,16 @@ def lib():
         L.orc_checksum_q32.argtypes = [P, sz, ctypes.c_uint64]
         L.orc_checksum_q32.restype = ctypes.c_uint32
         L.orc_switch_init.argtypes = [P, ctypes.c_int]
+        L.orc_switch_bytes.argtypes = []
+        L.orc_switch_bytes.restype = sz
+        L.orc_switch_init_ring.argtypes = [P, ctypes.c_int, ctypes.c_uint32]
+        L.orc_switch_init_ring.restype = ctypes.c_int
+        L.orc_switch_slot.argtypes = [P, ctypes.c_uint32]
+        L.orc_switch_slot.restype = P
+        L.orc_switch_pipeline.argtypes = [P, P, ctypes.c_int, P, sz, P, sz, P]
+        L.orc_switch_pipeline.restype = ctypes.c_int
+        L.orc_build_ack_frame.argtypes = [P, P, ctypes.c_uint32]
+        L.orc_build_ack_frame.restype = sz
         L.orc_switch_ingress.argtypes = [P, ctypes.c_int, ctypes.c_uint32, P, P]
         L.orc_switch_ingress.restype = ctypes.c_int
         L.orc_crc32.argtypes = [P, sz]
@@ -194,13 +205,14 @@ def checksum_q32(q: np.ndarray, index_base: int = 0) -> int:
 
 # ---- switch (nts.c:303-501) ----
 class Switch:
-    """Root switch with `fan_in` children (nts.c state, restated)."""
+    """Root switch with `fan_in` children (nts.c state, restated); `slots` is
+    the PSN ring (the reference's is 16, window 8: nts.c:21-22)."""
 
-    _SIZE = 4 + SW_SLOTS * LANES * 4 + SW_SLOTS * 4 + SW_SLOTS * 4 + 4 + 8 + 8 + 64
-
-    def __init__(self, fan_in: int):
-        self._buf = np.zeros(self._SIZE, np.uint8)
-        lib().orc_switch_init(_p(self._buf), int(fan_in))
+    def __init__(self, fan_in: int, slots: int = SW_SLOTS):
+        self.fan_in = int(fan_in)
+        self._buf = np.zeros(int(lib().orc_switch_bytes()), np.uint8)
+        if lib().orc_switch_init_ring(_p(self._buf), self.fan_in, int(slots)) != 0:
+            raise ValueError(f"orc switch: fan_in {fan_in}, slots {slots}")
 
     def ingress(self, port: int, psn: int, payload_be: np.ndarray):
         payload_be = np.ascontiguousarray(payload_be, dtype=np.uint32)
@@ -208,6 +220,25 @@ class Switch:
         egress = np.zeros(LANES, np.uint32)
         rc = lib().orc_switch_ingress(_p(self._buf), int(port), int(psn), _p(payload_be), _p(egress))
         return rc, egress
+
+    def slot(self, psn: int) -> np.ndarray:
+        """The aggregator words of `psn`'s slot (uint32 copy)."""
+        a = lib().orc_switch_slot(_p(self._buf), int(psn))
+        return np.ctypeslib.as_array((ctypes.c_uint32 * LANES).from_address(a)).copy()
+
+    def pipeline(self, conns: np.ndarray, port: int, frame: bytes, row_len: int | None = None):
+        """nts.c:303-501 on one frame (orc_switch_pipeline): (action, [frame
+        bytes sent to child c, or None]).  `conns` holds fan_in 28-byte
+        connection records (the engine's FRAME_TEMPLATE_DTYPE layout)."""
+        c = np.ascontiguousarray(conns).view(np.uint8)
+        assert c.size == 28 * self.fan_in
+        row = max(len(frame), 64) if row_len is None else int(row_len)
+        fb = np.zeros(max(row, len(frame), 64), np.uint8)
+        fb[: len(frame)] = np.frombuffer(bytes(frame), np.uint8)
+        out = np.zeros((self.fan_in, FRAME_ROW), np.uint8)
+        ln = np.zeros(self.fan_in, np.int32)
+        rc = lib().orc_switch_pipeline(_p(self._buf), _p(c), int(port), _p(fb), row, _p(out), FRAME_ROW, _p(ln))
+        return rc, [out[i, : ln[i]].tobytes() if ln[i] else None for i in range(self.fan_in)]
 
 
 # ---- framing (util.c) ----
@@ -246,6 +277,21 @@ def build_data_frame(payload_host: np.ndarray, psn: int, opcode: int, qp: int = 
         rb = np.frombuffer(reth, np.uint8).copy()
     n = lib().orc_build_data_frame(_p(frame), ctypes.byref(h), _p(payload_host), payload_host.size,
                                    1 if with_reth else 0, _p(rb) if rb is not None else None)
+    return frame[:n].tobytes()
+
+
+def build_ack_frame(psn: int, msn: int | None = None, qp: int = 0x11, src_ip: int = 0, dst_ip: int = 0,
+                    src_port: int = 4791, dst_port: int = 4791, src_mac: bytes = bytes(6),
+                    dst_mac: bytes = bytes(6)) -> bytes:
+    """util.c:331-442 PACKET_TYPE_ACK (send_roce_ack: msn = psn + 1, nts.c:292)."""
+    h = FrameHdr()
+    for i in range(6):
+        h.src_mac[i] = src_mac[i]
+        h.dst_mac[i] = dst_mac[i]
+    h.src_ip, h.dst_ip, h.src_port, h.dst_port = src_ip, dst_ip, src_port, dst_port
+    h.qp, h.psn, h.opcode = qp, psn, 0x11
+    frame = np.zeros(128, np.uint8)
+    n = lib().orc_build_ack_frame(_p(frame), ctypes.byref(h), (psn + 1) if msn is None else int(msn))
     return frame[:n].tobytes()
 
 

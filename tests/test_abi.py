@@ -55,6 +55,32 @@ def test_library_has_no_unresolved_internal_symbols(lib):
     assert not undef, undef
 
 
+def test_rccl_symbols_resolve_in_every_librccl_it_may_bind(lib):
+    """libinccl_amd.so is compiled against /opt/rocm's RCCL headers but, in a
+    Python process that imported torch first, binds torch's bundled librccl (the
+    same soname; BENCH "runtime": rccl_compiled 22707, rccl_loaded 22606).
+    Every nccl* symbol the library imports must be defined -- as a function --
+    in both copies, or a multi-GPU call would fail only at bind time on an
+    8-GPU node.  The ABI-relevant constants (ncclUniqueId size, the int32 / sum
+    enum values) are checked against the header the library was built with."""
+    import container_inc_amd as cia
+    from container_inc_amd._lib import runtime_libs
+    out = subprocess.check_output(["nm", "-D", "--undefined-only", cia.LIB_PATH], text=True)
+    need = {ln.split()[-1] for ln in out.splitlines() if ln.split()[-1].startswith("nccl")}
+    assert {"ncclReduceScatter", "ncclAllGather", "ncclCommInitRank", "ncclGetLastError"} <= need
+    import torch  # noqa: F401 -- the process a user runs: torch first, then the library
+    bound = runtime_libs().get("librccl")
+    copies = {p for p in (bound, "/opt/rocm/lib/librccl.so.1") if p and os.path.exists(p)}
+    assert bound, "no librccl mapped in this process"
+    for path in copies:
+        have = exported_symbols(path)
+        missing = sorted(need - have)
+        assert not missing, f"{path} lacks {missing}"
+    hdr = open("/opt/rocm/include/rccl/rccl.h").read()
+    assert re.search(r"#define\s+NCCL_UNIQUE_ID_BYTES\s+128\b", hdr)
+    assert re.search(r"ncclInt32\s*=\s*2\b", hdr) and re.search(r"ncclSum\s*=\s*0\b", hdr)
+
+
 def test_python_binding_covers_abi():
     from container_inc_amd._lib import SIGNATURES
     assert set(SIGNATURES) == declared_functions()

@@ -213,6 +213,93 @@ def _gpu_count():
     return torch.cuda.device_count()   # does not initialise the GPU in this process
 
 
+def _config45_main(rank, world, port, q, engine, device):
+    """BASELINE configs 4 and 5 as the 8-GPU bench runs them, one process per
+    GPU: R = 2 resident 256 MiB fp32 buckets per rank (config 4) and one 4 KiB
+    bucket (config 5's smallest, one reference message), inputs made on the
+    GPU from torch.Generator(seed + rank) as bench.py makes them.  Every rank
+    regenerates every rank's inputs on its own GPU and checks its result on a
+    lane sample -- 2^16 strided lanes plus both sides of every shard boundary
+    -- bit for bit against the oracle."""
+    try:
+        if engine not in RCCL_ENGINES:
+            os.environ["INCCL_ENGINE"] = engine
+        os.environ["INCCL_DEVICE"] = str(device)
+        os.environ["INCCL_BOOT_TIMEOUT"] = "120"
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        from container_inc_amd import inccl
+        from oracle import oracle as O
+        torch.cuda.set_device(device)
+        dev = torch.device("cuda", device)
+        grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=device)
+        assert grp is not None, "group create failed"
+        comm = inccl.inccl_communicator_create(grp, 0)
+        if engine in RCCL_ENGINES:
+            comm.set_engine(engine)
+        assert comm.engine == engine
+        results = []
+        for n, seed in ((64 << 20, 1000), (1024, 7000)):
+            def bucket(r, i):
+                g = torch.Generator(device=dev)
+                g.manual_seed(seed + 100 * i + r)
+                return torch.randn(n, generator=g, device=dev, dtype=torch.float32)
+            srcs = [bucket(rank, i) for i in range(2)]
+            out = torch.full((n,), float("nan"), device=dev)
+            torch.cuda.synchronize()
+            for _ in range(3):   # repeated: the bench's back-to-back steps
+                comm.allreduce_f32(srcs, out=out, scale_exp=25, stream=comm.stream)
+            torch.cuda.synchronize()
+            lanes = set(range(0, n, max(1, n // (1 << 16))))
+            for w in range(1, world):
+                b = w * n // world
+                lanes |= {max(0, b - 1), b, min(n - 1, b + 1)}
+            idx = torch.tensor(sorted(lanes), dtype=torch.int64, device=dev)
+            every = [bucket(r, i)[idx].cpu().numpy() for r in range(world) for i in range(2)]
+            want = O.reduce_f32(every, 25)
+            got = out[idx].cpu().numpy()
+            results.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
+            results.append(not bool(torch.isnan(out).any()))
+            del srcs, out
+            torch.cuda.empty_cache()
+        comm.destroy()
+        grp.destroy()
+        q.put((rank, results, None))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("engine", ["rccl", "ar", "a2a", "p2p", "ll", "mesh", "meshw"])
+def test_configs_4_5_one_gpu_per_rank(gpu, engine):
+    """BASELINE configs 4 (2 x 256 MiB per rank) and 5 (4 KiB) across every
+    visible GPU (at most 8), one process per GPU, each engine, sampled-lane
+    oracle parity (_config45_main).  Skipped on a one-GPU box."""
+    world = min(_gpu_count(), 8)
+    if world < 2:
+        pytest.skip("needs two or more GPUs (one process per GPU)")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_config45_main, args=(r, world, port, q, engine, r)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, ok, err = q.get(timeout=240)
+            res[r] = (ok, err)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        ok, err = res[r]
+        assert err is None, f"rank {r}: {err}"
+        assert all(ok), f"rank {r}: {ok}"
+
+
 @pytest.mark.parametrize("engine", ["rccl", "ar", "a2a", "p2p", "ll", "mesh", "meshw"])
 def test_engines_one_gpu_per_rank(gpu, engine):
     """the multi-GPU paths with one process per GPU, as the

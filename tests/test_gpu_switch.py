@@ -120,11 +120,69 @@ def _expected_frame(orc, t, c, agg, psn, op, reth):
                                 src_mac=bytes(t[c]["src_mac"]), dst_mac=bytes(t[c]["dst_mac"]))
 
 
+DATA_OPS = (0x00, 0x01, 0x02, 0x04, 0x07, 0x08)   # SEND FIRST/MIDDLE/LAST/ONLY, WRITE MIDDLE/LAST (nts.c:314-319)
+WF_OPS = (0x06, 0x0A)                               # WRITE FIRST / ONLY: a RETH before the payload (nts.c:327-328)
+ACK = 0x11
+
+
+def _act_map(orc, inccl):
+    return {orc.SW_ABSORBED: inccl.SW_ABSORBED, orc.SW_BROADCAST: inccl.SW_COMPLETED, orc.SW_REPLAY: inccl.SW_REPLAY,
+            orc.SW_DROPPED: inccl.SW_DROPPED, orc.SW_ACK: inccl.SW_ACK, orc.SW_IGNORED: inccl.SW_IGNORED,
+            orc.SW_INVALID: inccl.SW_INVALID}
+
+
+def _host_frame(orc, rng, psn, port, op):
+    """A frame a host sends the switch: an ACK for `psn`, or a data / WRITE_FIRST
+    packet with a random payload (and a random RETH); opcode 0x64 is one
+    pipeline() has no case for."""
+    if op == ACK:
+        return orc.build_ack_frame(psn, qp=0x40 + port, src_ip=0x0A000001 + port)
+    pay = rng.integers(INT32_MIN, INT32_MAX, 256, dtype=np.int64, endpoint=True).astype(np.int32)
+    wf = op in WF_OPS
+    f = orc.build_data_frame(pay, psn=psn, opcode=0x07 if op == 0x64 else op, qp=0x11, with_reth=wf,
+                             reth=rng.integers(0, 256, 16, dtype=np.uint8).tobytes() if wf else None,
+                             src_ip=0x0A000001 + port)
+    if op == 0x64:
+        f = f[:42] + bytes([0x64]) + f[43:]
+    return f
+
+
+def _random_op(rng):
+    r = rng.random()
+    return int(rng.choice(WF_OPS)) if r < 0.3 else int(rng.choice(DATA_OPS))
+
+
+def _check_vs_pipeline(orc, inccl, ref, tmpl, frames, ports, stride, action, out, out_len, tag):
+    """Every frame of the batch through the oracle's serial pipeline()
+    (orc_switch_pipeline, nts.c:303-501 frames in -> frames out): the GPU's
+    action, and every row it sent (or did not), byte for byte.  Returns how
+    often each oracle action occurred."""
+    amap = _act_map(orc, inccl)
+    fan = ref.fan_in
+    seen = {}
+    for i, (f, port) in enumerate(zip(frames, ports)):
+        rc, outs = ref.pipeline(tmpl, port, f, stride)
+        seen[rc] = seen.get(rc, 0) + 1
+        assert int(action[i]) == amap[rc], (tag, i, port, f[42], int(action[i]), amap[rc])
+        for c in range(fan):
+            row = i * fan + c
+            if outs[c] is None:
+                assert out_len[row] == 0, (tag, i, c)
+            else:
+                assert out_len[row] == len(outs[c]), (tag, i, c, int(out_len[row]), len(outs[c]))
+                assert bytes(out[row, : len(outs[c])]) == outs[c], (tag, i, c)
+    return seen
+
+
 # 20 children: RETH words of children 16+ are loaded directly, not shuffled from the prefetch.
 # Stride 1100 (4-byte but not 16-byte aligned rows): ingress's 2-byte payload
 # loads and egress's dword stores instead of the 16-byte paths.
 # Fan-in 2, 3, 4 and 8 take egress instances with the children loop unrolled, others the loop; frames
 # arrive shuffled, so a PSN's copies span frame pairs (the sum reads them through their keys).
+# Every copy of a frame carries its own opcode -- SEND, WRITE and WRITE_FIRST / ONLY
+# mixed within one PSN -- and ACKs, frames with an opcode the switch ignores and
+# frames on a port past fan_in are interleaved; the expected actions and frames
+# come from the oracle's serial pipeline() on the same sequence.
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("fan_in,stride", [(1, STRIDE), (2, STRIDE), (3, STRIDE), (4, STRIDE), (8, STRIDE), (20, STRIDE),
                                            (31, STRIDE), (2, 1100), (4, 1100), (8, 1100), (5, 1100)])
@@ -134,64 +192,39 @@ def test_switch_batches(gpu, orc, fan_in, stride, mode):
     rng = np.random.default_rng(100 + fan_in)
     slots, per_batch, batches = 64, 8, 5
     sw = inccl.GpuSwitch(fan_in, slots)
+    ref = orc.Switch(fan_in, slots)
     tmpl = _templates(fan_in)
     tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
-    payload, reth, opcode = {}, {}, {}
-    completed = set()
-    seen = set()
+    total = {}
     for b in range(batches):
-        psns = list(range(b * per_batch, (b + 1) * per_batch))
-        frames, ports, keys = [], [], []
-        for p in psns:
-            opcode[p] = [0x06, 0x07, 0x07, 0x08][p % 4]
-            for port in range(fan_in):
-                payload[(p, port)] = rng.integers(INT32_MIN, INT32_MAX, 256, dtype=np.int64, endpoint=True).astype(np.int32)
-                reth[(p, port)] = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
-                keys.append((p, port))
+        keys = [(p, port) for p in range(b * per_batch, (b + 1) * per_batch) for port in range(fan_in)]
         # retransmits: some of this batch's frames twice, and some of the previous batch's
         dups = [keys[i] for i in rng.choice(len(keys), size=len(keys) // 4, replace=False)]
-        old = [(p, port) for (p, port) in payload if p < b * per_batch and p >= (b - 1) * per_batch]
+        old = [(p, port) for p in range(max(0, (b - 1) * per_batch), b * per_batch) for port in range(fan_in)]
         olds = [old[i] for i in rng.choice(len(old), size=min(3, len(old)), replace=False)] if old else []
-        order = keys + dups + olds
-        perm = rng.permutation(len(order))
-        order = [order[i] for i in perm]
-        for (p, port) in order:
-            wf = opcode[p] in (0x06, 0x0A)
-            frames.append(orc.build_data_frame(payload[(p, port)], psn=p, opcode=opcode[p], qp=0x11, with_reth=wf,
-                                               reth=reth[(p, port)] if wf else None, src_ip=0x0A000001 + port))
-            ports.append(port)
+        items = [(p, port, _random_op(rng)) for (p, port) in keys + dups + olds]
+        # ACKs for any PSN, frames the switch ignores, a frame on a port past fan_in
+        items += [(int(rng.integers(0, 1 << 24)), int(rng.integers(0, fan_in)), ACK) for _ in range(2 * fan_in + 2)]
+        items += [(b * per_batch, 0, 0x64), (b * per_batch + 1, fan_in, 0x07)]
+        items = [items[i] for i in rng.permutation(len(items))]
+        frames = [_host_frame(orc, rng, p, port, op) for (p, port, op) in items]
+        ports = [port for (_, port, _) in items]
         fr = _rows(frames, gpu, stride)
         pt = torch.tensor(ports, dtype=torch.int32, device=gpu)
         action, psn_out, out, out_len = _run(sw, mode, fr, pt, tmpl_dev, out_stride=stride)
         torch.cuda.synchronize()
         action, psn_out = action.cpu().numpy(), psn_out.cpu().numpy()
         out, out_len = out.cpu().numpy(), out_len.cpu().numpy()
-        # the batch in frame order is the reference's serial order (nts.c:353-372):
-        # the first copy of a pair counts, the PSN completes at its last port's
-        # counted copy, later copies REPLAY once it has completed, else DROP
-        done_psn = set(completed)
-        for i, (p, port) in enumerate(order):
-            assert psn_out[i] == p
-            if (p, port) in seen:
-                want = inccl.SW_REPLAY if p in done_psn else inccl.SW_DROPPED
-            else:
-                seen.add((p, port))
-                full = all((p, c) in seen for c in range(fan_in))
-                want = inccl.SW_COMPLETED if full else inccl.SW_ABSORBED
-                if full:
-                    done_psn.add(p)
-            assert action[i] == want, (i, p, port, int(action[i]), want)
-        for i, (p, port) in enumerate(order):
-            agg = orc.sum_q32([payload[(p, c)] for c in range(fan_in)])
-            for c in range(fan_in):
-                row = i * fan_in + c
-                if action[i] == inccl.SW_COMPLETED or (action[i] == inccl.SW_REPLAY and c == port):
-                    want = _expected_frame(orc, tmpl, c, agg, p, opcode[p], reth[(p, c)])
-                    assert out_len[row] == len(want), (i, c)
-                    assert bytes(out[row, : len(want)]) == want, (i, c)
-                else:
-                    assert out_len[row] == 0
-        completed |= set(psns)
+        for i, (p, port, op) in enumerate(items):
+            if port < fan_in:
+                assert psn_out[i] == p, (i, p)
+        for k, v in _check_vs_pipeline(orc, inccl, ref, tmpl, frames, ports, stride, action, out, out_len, b).items():
+            total[k] = total.get(k, 0) + v
+    want = [orc.SW_BROADCAST, orc.SW_REPLAY, orc.SW_ACK, orc.SW_IGNORED, orc.SW_INVALID]
+    if fan_in > 1:   # (one child: every first copy completes its PSN)
+        want += [orc.SW_ABSORBED, orc.SW_DROPPED]
+    for k in want:
+        assert total.get(k, 0) > 0, (k, total)
     sw.destroy()
 
 
@@ -291,11 +324,13 @@ def test_switch_large_batch_all_frames(gpu, orc, fan_in, P, mode):
 @pytest.mark.parametrize("fan_in,seed", [(2, 1), (2, 2), (3, 3)])
 def test_switch_serial_order_vs_oracle_reference_ring(gpu, orc, fan_in, seed, mode):
     """The reference's own ring (16 slots, window 8 with slot psn+8 cleared at
-    completion, nts.c:21-25, :367) fed one frame sequence: the oracle processes
-    it serially (orc_switch_ingress), the GPU in batches of at most eight
-    consecutive PSNs.  Every copy of a frame carries a DIFFERENT payload, so the
-    actions, which copy is counted, and every emitted frame must all agree.
-    Retransmits land before, at and after their PSN's completion."""
+    completion, nts.c:21-25, :367) fed one frame sequence: the oracle's
+    pipeline() processes it serially, the GPU in batches of at most eight
+    consecutive PSNs.  Every copy of a frame carries a DIFFERENT payload and its
+    own opcode, so the actions, which copy is counted (and whose RETH is kept),
+    which opcode each broadcast and replay carries, and every emitted frame must
+    all agree.  Retransmits land before, at and after their PSN's completion;
+    ACKs are reflected in between."""
     stride = 1100 if seed == 2 else STRIDE   # seed 2: rows 4- but not 16-byte aligned
     import torch
     from container_inc_amd import inccl
@@ -305,10 +340,7 @@ def test_switch_serial_order_vs_oracle_reference_ring(gpu, orc, fan_in, seed, mo
     ref = orc.Switch(fan_in)
     tmpl = _templates(fan_in)
     tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
-    orc_act = {orc.SW_ABSORBED: inccl.SW_ABSORBED, orc.SW_BROADCAST: inccl.SW_COMPLETED,
-               orc.SW_REPLAY: inccl.SW_REPLAY, orc.SW_DROPPED: inccl.SW_DROPPED}
-    counted_reth = {}
-    n_checked = {"COMPLETED": 0, "REPLAY": 0, "DROPPED": 0}
+    total = {}
     for b in range(12):
         new = list(range(4 * b, 4 * b + 4))
         recent = list(range(max(0, 4 * b - 4), 4 * b + 4))   # at most eight consecutive PSNs
@@ -318,42 +350,79 @@ def test_switch_serial_order_vs_oracle_reference_ring(gpu, orc, fan_in, seed, mo
         for _ in range(3 * fan_in):
             p, c = int(rng.choice(recent)), int(rng.integers(0, fan_in))
             seq.insert(int(rng.integers(0, len(seq) + 1)), (p, c))
-        frames, ports, rcs, eg = [], [], [], []
-        for (p, c) in seq:
-            op = [0x06, 0x07, 0x07, 0x08][p % 4]
-            pay = rng.integers(INT32_MIN, INT32_MAX, 256, dtype=np.int64, endpoint=True).astype(np.int32)
-            rb = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
-            wf = op == 0x06
-            frames.append(orc.build_data_frame(pay, psn=p, opcode=op, qp=0x11, with_reth=wf, reth=rb if wf else None,
-                                               src_ip=0x0A000001 + c))
-            ports.append(c)
-            rc, e = ref.ingress(c, p, pay.astype(">i4").view(np.uint32))   # serial, in frame order
-            rcs.append(orc_act[rc])
-            eg.append(e.copy())
-            if rc in (orc.SW_ABSORBED, orc.SW_BROADCAST):
-                counted_reth[(p, c)] = rb
+        items = [(p, c, _random_op(rng)) for (p, c) in seq]
+        for _ in range(fan_in):
+            items.insert(int(rng.integers(0, len(items) + 1)), (int(rng.choice(recent)), int(rng.integers(0, fan_in)), ACK))
+        frames = [_host_frame(orc, rng, p, c, op) for (p, c, op) in items]
+        ports = [c for (_, c, _) in items]
         fr = _rows(frames, gpu, stride)
         pt = torch.tensor(ports, dtype=torch.int32, device=gpu)
         action, psn_out, out, out_len = _run(sw, mode, fr, pt, tmpl_dev, out_stride=stride)
         torch.cuda.synchronize()
-        act = action.cpu().numpy().tolist()
-        assert act == rcs, (b, seq, act, rcs)
-        out, out_len = out.cpu().numpy(), out_len.cpu().numpy()
-        for i, (p, port) in enumerate(seq):
-            op = [0x06, 0x07, 0x07, 0x08][p % 4]
-            agg = eg[i].byteswap().view(np.int32)   # the oracle's egress words (util.c:403-405) in host order
-            for c in range(fan_in):
-                row = i * fan_in + c
-                emit = act[i] == inccl.SW_COMPLETED or (act[i] == inccl.SW_REPLAY and c == port)
-                if emit:
-                    want = _expected_frame(orc, tmpl, c, agg, p, op, counted_reth.get((p, c), bytes(16)))
-                    assert out_len[row] == len(want) and bytes(out[row, : len(want)]) == want, (b, i, c)
-                else:
-                    assert out_len[row] == 0, (b, i, c)
-            name = {inccl.SW_COMPLETED: "COMPLETED", inccl.SW_REPLAY: "REPLAY", inccl.SW_DROPPED: "DROPPED"}
-            if act[i] in name:
-                n_checked[name[act[i]]] += 1
-    assert all(v > 0 for v in n_checked.values()), n_checked   # every serial outcome occurred
+        act, out, out_len = action.cpu().numpy(), out.cpu().numpy(), out_len.cpu().numpy()
+        for k, v in _check_vs_pipeline(orc, inccl, ref, tmpl, frames, ports, stride, act, out, out_len, b).items():
+            total[k] = total.get(k, 0) + v
+    for k in (orc.SW_BROADCAST, orc.SW_REPLAY, orc.SW_DROPPED, orc.SW_ACK):
+        assert total.get(k, 0) > 0, total   # every serial outcome occurred
+    sw.destroy()
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("fan_in", [3, 16, 20])
+def test_switch_arrivals_in_same_parity_batches(gpu, orc, fan_in, mode):
+    """A PSN whose counted arrivals fall in batches g and g + 2 with none in
+    g + 1 (and again in g + 4): batch g + 2 must classify against the bitmap
+    batch g left, whichever of the slot's two arrival words holds it.  The PSN's
+    frames in one batch are spread over more than 256 frames (different
+    classify blocks and sum waves) by ACK and ignored-opcode fillers, and its
+    retransmits of ports counted in batch g come both before and after the
+    batch's leader.  Fan-in 16 and 20 take the sum's key path (counted ports from
+    the arrival words).  Actions and frames vs the oracle's serial pipeline()."""
+    import torch
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(1500 + fan_in)
+    sw = inccl.GpuSwitch(fan_in, 16)
+    ref = orc.Switch(fan_in)
+    tmpl = _templates(fan_in)
+    tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
+
+    def fill(n):
+        return [(int(rng.integers(0, 1 << 24)), int(rng.integers(0, fan_in)), ACK if rng.random() < 0.5 else 0x64)
+                for _ in range(n)]
+
+    half = fan_in // 2
+    P, Q = 5, 6            # PSN 5 spans batches; PSN 6 completes in the batches between (recycles slot 14)
+    plan = [
+        # batch g: half of P's ports, far apart
+        [it for c in range(half) for it in [(P, c, _random_op(rng))] + fill(150)],
+        # batch g + 1: Q completes; nothing for P
+        [(Q, c, _random_op(rng)) for c in range(fan_in)] + fill(300),
+        # batch g + 2: retransmits of g's ports, then the rest of P's ports (the
+        # leader is the lowest of them), then more retransmits after it
+        fill(20) + [(P, 0, _random_op(rng))] + fill(280) +
+        [it for c in range(half, fan_in - 1) for it in [(P, c, _random_op(rng))] + fill(40)] +
+        [(P, c, _random_op(rng)) for c in range(half)] + fill(300) + [(P, c, _random_op(rng)) for c in range(half)],
+        # batch g + 3: nothing for P
+        fill(100) + [(Q, 0, _random_op(rng))],
+        # batch g + 4: P's last port completes it, retransmits after it replay
+        fill(10) + [(P, half, _random_op(rng))] + fill(300) + [(P, fan_in - 1, _random_op(rng))] + fill(270) +
+        [(P, c, _random_op(rng)) for c in range(fan_in)],
+        # batch g + 5: only retransmits of P
+        [(P, c, _random_op(rng)) for c in range(fan_in)] + fill(300) + [(P, 0, _random_op(rng))],
+    ]
+    total = {}
+    for b, items in enumerate(plan):
+        frames = [_host_frame(orc, rng, p, c, op) for (p, c, op) in items]
+        ports = [c for (_, c, _) in items]
+        fr = _rows(frames, gpu)
+        pt = torch.tensor(ports, dtype=torch.int32, device=gpu)
+        action, _, out, out_len = _run(sw, mode, fr, pt, tmpl_dev)
+        torch.cuda.synchronize()
+        act, out, out_len = action.cpu().numpy(), out.cpu().numpy(), out_len.cpu().numpy()
+        for k, v in _check_vs_pipeline(orc, inccl, ref, tmpl, frames, ports, STRIDE, act, out, out_len, b).items():
+            total[k] = total.get(k, 0) + v
+        assert np.array_equal(inccl_slot(sw, P, gpu), ref.slot(P)), b
+    assert total.get(orc.SW_DROPPED, 0) >= 2 * half and total.get(orc.SW_REPLAY, 0) >= fan_in, total
     sw.destroy()
 
 
@@ -383,11 +452,11 @@ def test_switch_short_stride_rejected(gpu, orc):
 
 @pytest.mark.parametrize("mode", MODES)
 def test_switch_batch_graph_replay(gpu, orc, mode):
-    """One batch's launches (ingress: claim / apply, then egress; or the batch
-    call's claim / apply / replay) captured once in a hipGraph and replayed over
-    new frame contents: the batch generation is a device word the last apply
-    block advances, so every replay is
-    a new batch (first-copy keys of the previous replay never count).  Batches
+    """One batch's launches (claim, classify, sum, egress -- from the ingress +
+    egress calls or from the batch call) captured once in a hipGraph and
+    replayed over new frame contents: the batch generation is a device word
+    that claim and classify advance, so every replay is a new batch (first-copy
+    keys of the previous replay never count).  Batches
     alternate between the two halves of the PSN ring (each recycles the other's
     slots, nts.c:367); every replay's actions, payload sums and ICRCs are
     checked, then eager calls continue on the same state."""

@@ -202,3 +202,127 @@ def test_frame_layout(orc):
     assert int.from_bytes(fr[-4:], "little") == orc.icrc(fr)
     fr2 = orc.build_data_frame(payload, psn=8, opcode=0x06, with_reth=True)
     assert len(fr2) == 1098
+
+
+# ---------------- ACK reflection and the frame-level pipeline ----------------
+def test_ack_frame_matches_captured_ack(orc):
+    """orc_build_ack_frame (util.c:331-442, PACKET_TYPE_ACK) against the soft-RoCE
+    ACK captured in test.c:4-22: PSN 0, MSN 1, QPN 0x11.  Every byte agrees but
+    the IP identification (the reference's builder writes 0x1111, util.c:358;
+    the kernel that sent the captured frame wrote 0x2695) and the IP checksum
+    that covers it; with those two fields taken from the capture the ICRC is
+    the captured one (test.c:21)."""
+    g = json.load(open(os.path.join(GOLDEN, "icrc_test_c.json")))
+    cap = bytes.fromhex(g["frame_hex"])
+    fr = orc.build_ack_frame(0, msn=1, qp=0x11, dst_mac=cap[0:6], src_mac=cap[6:12],
+                             src_ip=int.from_bytes(cap[26:30], "little"), dst_ip=int.from_bytes(cap[30:34], "little"),
+                             src_port=int.from_bytes(cap[34:36], "big"), dst_port=int.from_bytes(cap[36:38], "big"))
+    assert len(fr) == 62 and len(cap) == 58
+    diff = [i for i in range(58) if fr[i] != cap[i]]
+    assert diff and set(diff) <= {18, 19, 24, 25}, diff
+    assert fr[42] == 0x11 and fr[50:54] == bytes(4) and fr[54:58] == bytes.fromhex("1f000001")
+    patched = bytearray(fr)
+    patched[18:20], patched[24:26] = cap[18:20], cap[24:26]
+    assert orc.icrc(bytes(patched)) == g["icrc_u32"]
+    assert int.from_bytes(fr[58:62], "little") == orc.icrc(fr)
+
+
+def _conns(fan_in):
+    dt = np.dtype([("src_mac", np.uint8, 6), ("dst_mac", np.uint8, 6), ("src_ip", "<u4"), ("dst_ip", "<u4"),
+                   ("src_port", "<u2"), ("dst_port", "<u2"), ("qp", "<u4")])
+    t = np.zeros(fan_in, dt)
+    for c in range(fan_in):
+        t[c]["src_mac"] = [2, 0, 0, 0, 0, c]
+        t[c]["dst_mac"] = [4, 0, 0, 0, 1, c]
+        t[c]["src_ip"], t[c]["dst_ip"] = 0x0100000A + c, 0x0200000A + c
+        t[c]["src_port"], t[c]["dst_port"], t[c]["qp"] = 4791, 5000 + c, 0x300 + c
+    return t
+
+
+def _conn_kw(t, c):
+    return dict(qp=int(t[c]["qp"]), src_ip=int(t[c]["src_ip"]), dst_ip=int(t[c]["dst_ip"]),
+                src_port=int(t[c]["src_port"]), dst_port=int(t[c]["dst_port"]),
+                src_mac=bytes(t[c]["src_mac"]), dst_mac=bytes(t[c]["dst_mac"]))
+
+
+def test_pipeline_frames_opcodes_and_reth(orc):
+    """orc_switch_pipeline (nts.c:303-501, root) against the payload-level
+    orc_switch_ingress and the frame builder: the broadcast takes the completing
+    packet's opcode and each child's kept RETH (nts.c:442, :452), a replay the
+    retransmit's opcode and the retransmitting child's RETH (:437), a data
+    opcode's egress has no RETH (:355, :370) even when the counted copies were
+    WRITE_FIRST; ACKs reflect to their port (:403-406); other opcodes and bad
+    frames change nothing."""
+    fan = 3
+    t = _conns(fan)
+    sw, ref = orc.Switch(fan), orc.Switch(fan)
+    rng = np.random.default_rng(5)
+    pay = {c: rng.integers(INT32_MIN, INT32_MAX, 256, dtype=np.int64, endpoint=True).astype(np.int32) for c in range(fan)}
+    reth = {c: rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for c in range(fan)}
+    psn = 9
+    # child 0 WRITE_FIRST, child 1 SEND_ONLY (0x04), child 2 WRITE_ONLY (0x0A): completes with RETH
+    ops = {0: 0x06, 1: 0x04, 2: 0x0A}
+    for c in range(fan):
+        wf = ops[c] in (0x06, 0x0A)
+        fr = orc.build_data_frame(pay[c], psn=psn, opcode=ops[c], with_reth=wf, reth=reth[c] if wf else None)
+        rc, outs = sw.pipeline(t, c, fr)
+        rc2, _ = ref.ingress(c, psn, _be(pay[c]))
+        assert rc == rc2
+    assert rc == orc.SW_BROADCAST
+    agg = orc.sum_q32(list(pay.values()))
+    for c in range(fan):
+        kept = reth[c] if ops[c] in (0x06, 0x0A) else bytes(16)   # child 1's copy had no RETH: the keeper stays 0
+        assert outs[c] == orc.build_data_frame(agg, psn=psn, opcode=0x0A, with_reth=True, reth=kept, **_conn_kw(t, c))
+    # retransmit of child 1 as SEND_MIDDLE (0x01): replay to child 1 only, no RETH, opcode 0x01
+    rc, outs = sw.pipeline(t, 1, orc.build_data_frame(pay[1], psn=psn, opcode=0x01))
+    assert rc == orc.SW_REPLAY and outs[0] is None and outs[2] is None
+    assert outs[1] == orc.build_data_frame(agg, psn=psn, opcode=0x01, **_conn_kw(t, 1))
+    # retransmit of child 0 as WRITE_FIRST: its kept RETH
+    rc, outs = sw.pipeline(t, 0, orc.build_data_frame(pay[0], psn=psn, opcode=0x06, with_reth=True, reth=bytes(16)))
+    assert rc == orc.SW_REPLAY
+    assert outs[0] == orc.build_data_frame(agg, psn=psn, opcode=0x06, with_reth=True, reth=reth[0], **_conn_kw(t, 0))
+    # a PSN whose counted copies were WRITE_FIRST but whose completing packet is WRITE_MIDDLE: no RETH out
+    for c in range(fan):
+        op = 0x07 if c == fan - 1 else 0x06
+        rc, outs = sw.pipeline(t, c, orc.build_data_frame(pay[c], psn=10, opcode=op, with_reth=op == 0x06,
+                                                          reth=reth[c] if op == 0x06 else None))
+    assert rc == orc.SW_BROADCAST
+    for c in range(fan):
+        assert outs[c] == orc.build_data_frame(agg, psn=10, opcode=0x07, **_conn_kw(t, c))
+    # ACK reflection: to the ACK's port, PSN and MSN = PSN + 1, state untouched
+    ack = orc.build_ack_frame(0x123456, qp=0x77)
+    rc, outs = sw.pipeline(t, 2, ack)
+    assert rc == orc.SW_ACK and outs[0] is None and outs[1] is None
+    assert outs[2] == orc.build_ack_frame(0x123456, msn=0x123457, **_conn_kw(t, 2))
+    # an opcode pipeline() has no case for; a bad port; a short payload
+    other = bytearray(orc.build_data_frame(pay[0], psn=11, opcode=0x07))
+    other[42] = 0x64
+    assert sw.pipeline(t, 0, bytes(other))[0] == orc.SW_IGNORED
+    assert sw.pipeline(t, fan, orc.build_data_frame(pay[0], psn=11, opcode=0x07))[0] == orc.SW_INVALID
+    assert sw.pipeline(t, 0, orc.build_data_frame(pay[0][:100], psn=11, opcode=0x07))[0] == orc.SW_INVALID
+    # none of those touched PSN 11's slot: its first real copies still count
+    rc, _ = sw.pipeline(t, 0, orc.build_data_frame(pay[0], psn=11, opcode=0x07))
+    assert rc == orc.SW_ABSORBED
+
+
+def test_pipeline_ack_msn_wraps(orc):
+    """PSN 0xFFFFFF: MSN = PSN + 1 = 2^24, so AETH = htonl(0x1f000000 | 2^24) (util.c:394)."""
+    t = _conns(1)
+    sw = orc.Switch(1)
+    rc, outs = sw.pipeline(t, 0, orc.build_ack_frame(0xFFFFFF))
+    assert rc == orc.SW_ACK
+    assert outs[0][50:54] == bytes.fromhex("00ffffff") and outs[0][54:58] == bytes.fromhex("1f000000")
+
+
+def test_pipeline_ring_sizes(orc):
+    """A ring larger than the reference's: window = slots / 2, so completing PSN p
+    recycles slot p + slots/2 (nts.c:367 with N generalised)."""
+    for slots in (16, 64, 1024):
+        sw = orc.Switch(2, slots)
+        one = _be(np.ones(256, np.int32))
+        sw.ingress(0, 3 + slots // 2, one)                # an arrival in the slot that PSN 3 will recycle
+        sw.ingress(0, 3, one)
+        assert sw.ingress(1, 3, one)[0] == orc.SW_BROADCAST
+        assert sw.ingress(0, 3 + slots // 2, one)[0] == orc.SW_ABSORBED   # recycled: counts again
+    with pytest.raises(ValueError):
+        orc.Switch(2, 24)
