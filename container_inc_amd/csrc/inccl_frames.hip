@@ -1190,14 +1190,14 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
 // q (bytes 62-63 are written as zero).  Per-lane rows: plain global stores
 // under the ACK lanes' mask, issued before the chunk's data frames.
 template <bool kOut16>
-__device__ __forceinline__ void egress_acks(const EgressLds& t, const EgressArgs& A, uint32_t f0, uint32_t bits,
-                                            uint32_t psn, int fan, int lane)
+__device__ __forceinline__ void egress_acks(const EgressLds& t, const EgressArgs& A, uint32_t f0, bool ack,
+                                            uint32_t bits, uint32_t psn, int fan, int lane)
 {
+    if (!__ballot(ack)) return;   // (lane l: frame f0 + l; most chunks hold no ACK)
     const int j = lane >> 2, q = lane & 3;
     const uint32_t bj = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * j, (int)bits);
     const uint32_t pj = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * j, (int)psn) & 0x00FFFFFFu;
     const bool ak = j < (int)egress_chunk(fan) && ((bj >> 12) & 1u);
-    if (!__ballot(ak)) return;
     if (!ak) return;
     const uint32_t c = bj >> 16, msn = pj + 1u;
     const uint32_t aeth = msn | 0x1f000000u;
@@ -1298,7 +1298,7 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
                 __builtin_amdgcn_raw_buffer_store_b32(len, rl, 4 * e, 0, 0);
             }
         }
-        egress_acks<kOut16>(t, A, f0, bits, psn, fan, lane);
+        egress_acks<kOut16>(t, A, f0, ack, bits, psn, fan, lane);
         uint64_t m = __ballot(all || one);
         if (!m) continue;
         // a frame of the ring is its lane in the chunk (-1: none); its words
