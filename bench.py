@@ -38,7 +38,8 @@ Extra JSON fields:
                     and checked bit for bit by the C oracle (also per engine
                     candidate, sweep row and bf16 row, on smaller samples)
   runtime           the HIP / HSA / RCCL libraries this rank mapped
-  sizes             N = 1: north_star's 4/64/256/1024 MiB buckets, kernel GB/s + HBM fraction
+  sizes             N = 1: 4 KiB .. 1 GiB buckets (north_star's 4/64/256/1024 MiB among them):
+                    call latency eager / prepared / graph-replayed, kernel time, GB/s + HBM fraction
   roofline_cold     N = 1: the fused kernel rotating through input sets far larger
                     than the 256 MiB Infinity Cache
   r_variants        N = 1: config 2's R = 1 and R = 8 at 256 MiB, repeated and rotated
@@ -70,6 +71,25 @@ T_START = time.monotonic()
 STAGE = {"stage": "start"}
 KEEPER = [None]   # rank 0's LineKeeper
 RESULT = [None]   # the result dict once the headline is measured
+PHASES = {}       # wall seconds of each phase of the run, in order (the line's "phase_s")
+SWEEP_ROWS = []   # N > 1: the size sweep's rows as they finish (the line's "sweep")
+
+
+class Phase:
+    """Records the wall seconds of one phase of the run into PHASES."""
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        self.t0 = time.monotonic()
+        return self
+
+    def __exit__(self, *exc):
+        PHASES[self.name] = round(time.monotonic() - self.t0, 1)
+        if KEEPER[0] is not None:
+            KEEPER[0].update()
+        return False
 
 
 def set_stage(stage: str) -> None:
@@ -477,7 +497,12 @@ def graph_replay_us(comm, xs, out, k: int, st, world: int, want, per: int = 20, 
     return dt, same
 
 
-def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: float, rows: list) -> list:
+SMALL_ENGINES = ("rccl", "ar", "p2p", "ll", "mesh", "meshw")   # buckets up to 1 MiB
+LARGE_ENGINES = ("rccl", "ar", "a2a", "p2p", "mesh", "meshw")
+
+
+def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: float, rows: list,
+               want=lambda eng: True, ref_of=None) -> list:
     """BASELINE config 5 at N > 1 (and north_star's 1024 MiB point): per bucket
     size and engine, host wall time per call over back-to-back calls (max over
     ranks), GB/s, the xGMI link fraction, whether the results of two
@@ -485,12 +510,27 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: 
     sampled oracle check of each engine's result (`parity_vs_oracle`).
     Rows are appended to `rows` as they finish (the watchdog reports a partial
     sweep).  A size is started only while every rank is within
-    `soft_budget_s` of process start; the rest are skipped and listed."""
+    `soft_budget_s` of process start; the rest are skipped and listed.
+
+    `want(engine)` selects this pass's engines: the sweep runs in two passes
+    (RCCL first, so that its rows exist before anything else runs, then the
+    rest).  `ref_of` maps a size to the engine whose results were the
+    reference in an earlier pass; that engine is re-run untimed first, so the
+    later pass compares against the same reference."""
     import torch
     import torch.distributed as dist
+    ref_of = {} if ref_of is None else ref_of
     for b in SWEEP_BYTES:
+        engines = SMALL_ENGINES if b <= (1 << 20) else LARGE_ENGINES
+        only = os.environ.get("INCCL_BENCH_SWEEP_ENGINES")   # debugging aid: a subset, in this order
+        if only:
+            engines = tuple(e for e in only.split(",") if e in engines)
+        engines = tuple(e for e in engines if want(e))
+        if not engines:
+            continue
         if agree([time.monotonic() - T_START], world)[0] > soft_budget_s:
-            rows.append({"bucket_bytes": b, "skipped": f"run past {soft_budget_s:.0f} s from process start"})
+            rows.append({"bucket_bytes": b, "engines": list(engines),
+                         "skipped": f"run past {soft_budget_s:.0f} s from process start"})
             continue
         n = b // 4
         lanes = oracle_lanes(n, world, 1, 4096)
@@ -506,11 +546,18 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: 
         iters = 50 if b <= (1 << 20) else (10 if b <= (256 << 20) else 4)
         # the reference engine is the first that passes on every rank: RCCL, or
         # else the host-synchronised p2p exchange, before the in-kernel ll protocol
-        engines = (("rccl", "ar", "p2p", "ll", "mesh", "meshw") if b <= (1 << 20)
-                   else ("rccl", "ar", "a2a", "p2p", "mesh", "meshw"))
-        only = os.environ.get("INCCL_BENCH_SWEEP_ENGINES")   # debugging aid: a subset, in this order
-        if only:
-            engines = tuple(e for e in only.split(",") if e in engines)
+        if b in ref_of:   # an earlier pass's reference, recomputed untimed
+            set_stage(f"sweep {b} B reference {ref_of[b]}")
+            ok = 1
+            try:
+                comm.set_engine(ref_of[b])
+                got, _ = run_verified(comm, ref_of[b], 1, inputs, out, k, st, None)
+            except Exception as e:  # noqa: BLE001
+                print(f"rank {rank}: sweep {b} B reference {ref_of[b]} failed: {e}", file=sys.stderr, flush=True)
+                ok, got = 0, None
+            if agree([0.0 if ok else 1.0], world)[0] == 0.0:
+                refs = (got[0], got[1])
+            del got
         for eng in engines:
             set_stage(f"sweep {b} B engine {eng}")
             ok, dt, same, got = 1, float("inf"), False, None
@@ -536,6 +583,7 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: 
             good, ident = v[1] == 0.0, v[2] == 0.0
             if good and ident and refs is None:
                 refs = (got[0], got[1])
+                ref_of[b] = eng
             if rank == 0:
                 print(f"sweep {b} B {eng}: ok={good} identical={ident} us={v[0] * 1e6:.1f}", file=sys.stderr,
                       flush=True)
@@ -637,15 +685,20 @@ def kernel_time_ms(fn, stream, iters: int) -> float:
 
 
 
-def switch_batch(dev, fan_in: int = 2, P: int = 1 << 16, iters: int = 20) -> dict:
-    """The GPU switch dataplane (nts.c:303-501 parse / aggregate / replay,
-    util.c:331-442 egress frames + ICRC) on one batch of fan_in x P RoCEv2 data
-    frames, every port of every PSN once: `inccl_switch_batch` = claim, classify,
-    sum, egress.  Batches alternate between the two halves of a 2P-slot ring, so
-    each batch's recycle (slot psn + slots/2, nts.c:367) clears the other half
-    and no reset runs between batches.  Device time per batch from HIP events on
-    its stream.  Checked without the oracle: every PSN completes exactly once per
-    batch and every completed frame's fan_in rows carry a frame length."""
+def switch_batch(dev, fan_in: int = 2, P: int = 1 << 16, iters: int = 20, acks: bool = False) -> dict:
+    """The GPU switch dataplane (nts.c:303-501 parse / aggregate / replay / ACK
+    reflection, util.c:331-442 egress frames + ICRC) on one batch of fan_in x P
+    RoCEv2 data frames, every port of every PSN once: `inccl_switch_batch` =
+    claim, classify, sum, egress.  acks=True: every data frame is followed by
+    its sender's ACK for that PSN (the reference's RDMA-WRITE flow: each
+    downstream packet draws an ACK that the switch reflects, nts.c:403-406), so
+    the batch holds 2 fan_in P frames and egress also builds fan_in P 62-B ACKs.
+    Batches alternate between the two halves of a 2P-slot ring, so each batch's
+    recycle (slot psn + slots/2, nts.c:367) clears the other half and no reset
+    runs between batches.  Device time per batch from HIP events on its stream.
+    Checked without the oracle: every PSN completes exactly once per batch,
+    every completed frame's fan_in rows carry a frame length and every ACK its
+    port's 62-B row."""
     import numpy as np
     import torch
 
@@ -664,10 +717,18 @@ def switch_batch(dev, fan_in: int = 2, P: int = 1 << 16, iters: int = 20) -> dic
     pay = rng.integers(0, 256, (n, 1024), dtype=np.uint8)
     for sel, off in ((wf, 70), (~wf, 54)):
         frames[sel, off:off + 1024] = pay[sel]
+    is_ack = np.zeros(n, bool)
+    if acks:   # data frame i at row 2 i, its sender's ACK at row 2 i + 1
+        both = np.zeros((2 * n, stride), np.uint8)
+        both[0::2] = frames
+        both[1::2, 38], both[1::2, 39], both[1::2, 42] = 0, 28, 0x11   # 62-B ACK: UDP length 28, opcode 0x11
+        frames, psn, ports = both, np.repeat(psn, 2), np.repeat(ports, 2)
+        is_ack = np.tile(np.array([False, True]), n)
+    total = len(frames)
 
     def with_psns(base):
         f = frames.copy()
-        q = (psn + base) | 0x80000000
+        q = np.where(is_ack, psn + base, (psn + base) | 0x80000000)   # ACKs carry no ack-request bit (util.c:387-388)
         f[:, 50], f[:, 51], f[:, 52], f[:, 53] = q >> 24, (q >> 16) & 0xFF, (q >> 8) & 0xFF, q & 0xFF
         return torch.from_numpy(f).to(dev)
 
@@ -678,10 +739,10 @@ def switch_batch(dev, fan_in: int = 2, P: int = 1 << 16, iters: int = 20) -> dic
     tmpl["qp"], tmpl["src_port"], tmpl["dst_port"] = 0x11, 4791, 4791
     tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(dev)
     st = torch.cuda.Stream(device=dev)
-    out = torch.empty((n * fan_in, stride), dtype=torch.uint8, device=dev)
-    out_len = torch.empty(n * fan_in, dtype=torch.int32, device=dev)
-    action = torch.empty(n, dtype=torch.int32, device=dev)
-    psn_out = torch.empty(n, dtype=torch.int32, device=dev)
+    out = torch.empty((total * fan_in, stride), dtype=torch.uint8, device=dev)
+    out_len = torch.empty(total * fan_in, dtype=torch.int32, device=dev)
+    action = torch.empty(total, dtype=torch.int32, device=dev)
+    psn_out = torch.empty(total, dtype=torch.int32, device=dev)
     turn = [0]
 
     def one():
@@ -692,61 +753,107 @@ def switch_batch(dev, fan_in: int = 2, P: int = 1 << 16, iters: int = 20) -> dic
     one()
     torch.cuda.synchronize()
     a = action.cpu().numpy()
-    lens = out_len.cpu().numpy().reshape(n, fan_in)
+    lens = out_len.cpu().numpy().reshape(total, fan_in)
     done = a == inccl.SW_COMPLETED
-    ok = int(done.sum()) == P and bool((lens[done] > 0).all()) and bool((lens[~done] == 0).all())
+    ok = int(done.sum()) == P and bool((lens[done] > 0).all())
+    if acks:
+        ack_rows = lens[is_ack, :]
+        ok = ok and bool((a[is_ack] == inccl.SW_ACK).all())
+        ok = ok and bool((ack_rows[np.arange(n), ports[is_ack]] == 62).all()) and int((ack_rows > 0).sum()) == n
+        ok = ok and bool((lens[~done & ~is_ack] == 0).all())
+    else:
+        ok = ok and bool((lens[~done] == 0).all())
     ms = kernel_time_ms(one, st, iters)
     sw.destroy()
-    return {"what": "inccl_switch_batch: claim / classify / sum / egress (frames + ICRC) of one batch",
-            "fan_in": fan_in, "psns": P, "frames": n, "us_per_batch": round(ms * 1e3, 2),
-            "payload_GBs": round(n * 1024 / (ms * 1e-3) / 1e9, 1), "frames_per_s": round(n / (ms * 1e-3)),
-            "every_psn_completes_once": ok, "timing": "HIP events on the batch's stream, eager calls"}
+    return {"what": "inccl_switch_batch: claim / classify / sum / egress (frames + ICRC) of one batch"
+                    + (", every data frame followed by its sender's ACK (reflected, nts.c:403-406)" if acks else ""),
+            "fan_in": fan_in, "psns": P, "frames": total, "data_frames": n, "ack_frames": n if acks else 0,
+            "us_per_batch": round(ms * 1e3, 2), "payload_GBs": round(n * 1024 / (ms * 1e-3) / 1e9, 1),
+            "frames_per_s": round(total / (ms * 1e-3)), "every_psn_completes_once": ok,
+            "timing": "HIP events on the batch's stream, eager calls"}
 
-def n1_sizes(dev, R: int, k: int, sizes_mib=(4, 64, 256, 1024)) -> list:
-    """north_star's bucket sizes at N = 1: the fused kernel on R resident buckets
-    of each size, GB/s of buckets reduced and the kernel's HBM roofline fraction.
 
-    `kernel_us` is per launch of `per` back-to-back launches captured in one
-    hipGraph and replayed (HIP events on the replay stream): the device rate.
-    `eager_us` is per call through the C ABI from Python, which at 4 MiB is
-    bound by the host (~7 us per ctypes call against ~3 us of kernel;
-    tools/tune/tune_small.hip, profiles/r02/tune_small.jsonl)."""
+SIZES_BYTES = (4 << 10, 64 << 10, 1 << 20, 4 << 20, 64 << 20, 256 << 20, 1 << 30)
+
+
+def host_us_per_call(fn, iters: int) -> float:
+    """Host wall time per call of `fn` over `iters` back-to-back calls (one
+    synchronisation at the end): what a caller of a stream-ordered API sees."""
+    import torch
+    for _ in range(max(3, iters // 10)):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters * 1e6
+
+
+def n1_sizes(dev, R: int, k: int, sizes=SIZES_BYTES) -> list:
+    """north_star's bucket sizes at N = 1 (4/64/256/1024 MiB) and the small-bucket
+    regime below them (4 KiB = one reference message, api.h:39; 64 KiB; 1 MiB):
+    the fused kernel on R resident buckets of each size.  Per size:
+
+      eager_us     inccl.reduce_f32 from Python, host time per call over
+                   back-to-back calls: what a caller of the plain API sees
+      prepared_us  the same bucket through a prepared op (inccl_op_run: the
+                   arguments bound once, one ctypes argument per call)
+      graph1_us    a hipGraph holding one call, replayed per call
+      kernel_us    a hipGraph holding `per` calls, per call: the device rate of
+                   back-to-back kernels (HIP events on the replay stream)
+      GBps_buckets R * bucket bytes / eager_us (the call); GBps_buckets_prepared
+                   likewise; hbm_frac from kernel_us against 8 TB/s"""
     import torch
 
     from container_inc_amd import inccl
     rows = []
     st = torch.cuda.Stream(device=dev)
-    for mib in sizes_mib:
-        n = mib * (1 << 20) // 4
+    for b in sizes:
+        n = b // 4
         gen = torch.Generator(device=dev)
         gen.manual_seed(1000)
         xs = [torch.randn(n, generator=gen, device=dev) for _ in range(R)]
         out = torch.empty(n, device=dev)
         torch.cuda.synchronize()
-        iters = max(50, min(400, (8 << 30) // (mib << 20)))
-        call = lambda: inccl.reduce_f32(xs, k, out=out, stream=st.cuda_stream)  # noqa: E731
-        eager = kernel_time_ms(call, st, iters)
+        iters = int(max(20, min(3000, (8 << 30) // (b * R + b))))
+        h = st.cuda_stream
+        call = lambda: inccl.reduce_f32(xs, k, out=out, stream=h)  # noqa: E731
+        eager = host_us_per_call(call, iters)
+        op = inccl.prepare_reduce_f32(xs, k, out=out, stream=h)
+        prepared = host_us_per_call(op, iters)
+        op.destroy()
         per = max(10, min(100, iters // 4))
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=st):
-            for _ in range(per):
-                call()
-        reps = max(2, iters // per)
-        with torch.cuda.stream(st):   # replay() launches on the current stream
-            g.replay()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            for _ in range(reps):
+        res = {}
+        for cnt in (1, per):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                for _ in range(cnt):
+                    call()
+            reps = max(4, iters // cnt)
+            with torch.cuda.stream(st):   # replay() launches on the current stream
                 g.replay()
-            e1.record(st)
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / (reps * per)
-        del g
+                if cnt == 1:
+                    res[cnt] = host_us_per_call(g.replay, reps)
+                else:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                    for _ in range(reps):
+                        g.replay()
+                    e1.record(st)
+                    torch.cuda.synchronize()
+                    res[cnt] = e0.elapsed_time(e1) * 1e3 / (reps * cnt)
+            del g
+        kernel_us = res[per]
         alg = (R + 1) * 4 * n
-        rows.append({"bucket_mib": mib, "kernel_us": round(ms * 1e3, 2), "eager_us": round(eager * 1e3, 2),
-                     "GBps_buckets": round(R * 4 * n / (ms * 1e-3) / 1e9, 1),
-                     "hbm_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
-                     "hbm_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+        rows.append({"bucket_bytes": b, "bucket_mib": round(b / (1 << 20), 6),
+                     "eager_us": round(eager, 2), "prepared_us": round(prepared, 2),
+                     "graph1_us": round(res[1], 2), "kernel_us": round(kernel_us, 2),
+                     "GBps_buckets": round(R * b / (eager * 1e-6) / 1e9, 1),
+                     "GBps_buckets_prepared": round(R * b / (prepared * 1e-6) / 1e9, 1),
+                     "GBps_buckets_kernel": round(R * b / (kernel_us * 1e-6) / 1e9, 1),
+                     "hbm_GBps": round(alg / (kernel_us * 1e-6) / 1e9, 1),
+                     "hbm_frac": round(alg / (kernel_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)})
         del xs, out
     torch.cuda.empty_cache()
     return rows
@@ -1123,7 +1230,7 @@ def main():
         best = None
         for eng, ch, env in cand_list:
             set_stage(f"engine tuning (phase {phase}): {eng} chunks={ch} {env or ''}")
-            ok, dt, same, got = 1, float("inf"), False, None
+            ok, dt, same, got, err = 1, float("inf"), False, None, None
             os.environ.update(env)
             try:
                 comm.set_engine(eng)
@@ -1139,7 +1246,7 @@ def main():
                 dt = (time.perf_counter() - t0) / TUNE_CALLS
             except Exception as e:  # noqa: BLE001
                 print(f"rank {rank}: engine {eng} chunks {ch} {env} failed: {e}", file=sys.stderr, flush=True)
-                ok = 0
+                ok, err = 0, str(e)[:400]
             for key in env:
                 os.environ.pop(key, None)
             v = agree([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0], world)
@@ -1159,7 +1266,9 @@ def main():
             tuning.append({"engine": eng, "chunks": ch, "env": env or None, "phase": phase, "ok": v[1] == 0.0,
                            "bit_identical": v[1] == 0.0 and v[2] == 0.0, "verified": good,
                            "oracle_mismatches": par["mismatches"] if par else None,
-                           "ms": round(v[0] * 1e3, 3) if v[1] == 0.0 else None})
+                           "ms": round(v[0] * 1e3, 3) if v[1] == 0.0 else None,
+                           # rank 0's error text (RCCL's own reason, ncclGetLastError, included)
+                           **({"error": err} if err else {})})
             if good and (best is None or v[0] < best[0]):
                 best = (v[0], eng, ch, env)
             del got
@@ -1379,31 +1488,63 @@ def main():
 
     def publish(res: dict, stage: str) -> None:
         """From now on every way the run can end prints `res`."""
+        res["phase_s"] = PHASES
+        if world > 1 and not a.no_sweep:
+            res["sweep"] = SWEEP_ROWS
         RESULT[0] = res
         watchdog.on_fire = on_overrun
         set_stage(stage)
 
     measured = []   # (measurement, line) per headline measurement, in order
+    PHASES["startup"] = round(time.monotonic() - T_START, 1)
+    sweep_soft = float(os.environ.get("INCCL_BENCH_SWEEP_SOFT", "300"))
+    sweep_refs = {}   # bucket bytes -> the sweep's reference engine (pass 1), for pass 2
+
+    def sweep_pass(name, want):
+        """One pass of the size sweep; an exception (the same on every rank:
+        the collectives are symmetric) is recorded in the line instead of
+        costing the headline."""
+        with Phase(name):
+            try:
+                size_sweep(comm, dev, R, k, rank, world, sweep_soft, SWEEP_ROWS, want=want, ref_of=sweep_refs)
+            except Exception as e:  # noqa: BLE001
+                print(f"rank {rank}: {name} failed: {e!r}", file=sys.stderr, flush=True)
+                RESULT[0][name + "_error"] = repr(e)
+
     if world == 1:
-        m = measure("fused", 1, {})
-        dominant_kernel()
+        with Phase("headline"):
+            m = measure("fused", 1, {})
+            dominant_kernel()
         measured.append((m, build_res(m)))
         publish(measured[-1][1], "headline measured")
     else:
-        best1 = tune(phases[0], 1)
+        # Order, for a first run on a real node: the RCCL headline, then the
+        # RCCL rows of the size sweep, and only then this library's IPC
+        # engines (tuning, a possible faster headline, their sweep rows), bf16
+        # and host_e2e -- whatever hangs or overruns later leaves the RCCL
+        # headline and sweep in the line (watchdog / line keeper)
+        with Phase("tune_rccl"):
+            best1 = tune(phases[0], 1)
         if best1 is not None:
-            m = measure(best1[1], best1[2], best1[3])
-            dominant_kernel()
+            with Phase("headline_rccl"):
+                m = measure(best1[1], best1[2], best1[3])
+                dominant_kernel()
             measured.append((m, build_res(m)))
-            publish(measured[-1][1], f"headline measured on {m['engine']}; phase 2 (IPC engines) next")
+            publish(measured[-1][1], f"headline measured on {m['engine']}; RCCL sweep next")
+            if not a.no_sweep:
+                for key in best1[3]:   # the sweep runs every engine with its defaults
+                    os.environ.pop(key, None)
+                sweep_pass("sweep_rccl", lambda eng: eng == "rccl")
         if os.environ.get("INCCL_BENCH_TEST_DIE") == "phase2" and rank == 0:   # test hook: rank 0 dies in phase 2
             import signal
             os.kill(os.getpid(), signal.SIGKILL)
-        best2 = tune(phases[1], 2)
+        with Phase("tune_ipc"):
+            best2 = tune(phases[1], 2)
         phase2_error = None
         if best2 is not None and (best1 is None or best2[0] < best1[0]):
             try:
-                m = measure(best2[1], best2[2], best2[3])
+                with Phase("headline_ipc"):
+                    m = measure(best2[1], best2[2], best2[3])
             except Exception as e:  # noqa: BLE001 -- an engine error is the same on every rank
                 if not measured:
                     raise
@@ -1432,6 +1573,9 @@ def main():
             for mm, ln in measured]
         if phase2_error:
             best[1]["phase2_error"] = phase2_error
+        for key in ("sweep_rccl_error",):   # carried over from the phase-1 line
+            if key in measured[0][1] and key not in best[1]:
+                best[1][key] = measured[0][1][key]
         publish(best[1], "headline measured")
         comm.set_engine(best[0]["engine"])
         os.environ.update(best[0]["env"])
@@ -1443,49 +1587,46 @@ def main():
     if world > 1 and not a.no_sweep:
         for key in chosen[2]:   # the sweep runs every engine with its defaults
             os.environ.pop(key, None)
-        # The sweep and the bf16 key run after the headline is measured.  They
-        # drive engines never before run across separate GPUs; a size is only
-        # started while the run is inside the soft budget, and a collective that
-        # hangs is ended by the watchdog (headline line + partial sweep, rc 3).
-        soft = float(os.environ.get("INCCL_BENCH_SWEEP_SOFT", "300"))
-        res["sweep"] = []
+        # The rest of the sweep and the bf16 key drive engines never before run
+        # across separate GPUs; a size is only started while the run is inside
+        # the soft budget, and a collective that hangs is ended by the watchdog
+        # (headline line + partial sweep, rc 3).
         if os.environ.get("INCCL_BENCH_TEST_HANG") == "1" and rank == 0:   # test hook: a stuck rank 0
             set_stage("INCCL_BENCH_TEST_HANG sleep on rank 0")
             time.sleep(1e9)
-        # an exception here (the same on every rank: the keys' collectives are
-        # symmetric) is recorded in the line instead of costing the headline
-        try:
-            size_sweep(comm, dev, R, k, rank, world, soft, res["sweep"])
-        except Exception as e:  # noqa: BLE001
-            print(f"rank {rank}: sweep failed: {e!r}", file=sys.stderr, flush=True)
-            res["sweep_error"] = repr(e)
-        if agree([time.monotonic() - T_START], world)[0] <= soft:
-            try:
-                res["bf16"] = bf16_engines(comm, dev, R, rank, world)
-            except Exception as e:  # noqa: BLE001
-                print(f"rank {rank}: bf16 key failed: {e!r}", file=sys.stderr, flush=True)
-                res["bf16"] = {"error": repr(e)}
-        else:
-            res["bf16"] = {"skipped": f"run past {soft:.0f} s from process start"}
+        sweep_pass("sweep_other", lambda eng: eng != "rccl")
+        with Phase("bf16"):
+            if agree([time.monotonic() - T_START], world)[0] <= sweep_soft:
+                try:
+                    res["bf16"] = bf16_engines(comm, dev, R, rank, world)
+                except Exception as e:  # noqa: BLE001
+                    print(f"rank {rank}: bf16 key failed: {e!r}", file=sys.stderr, flush=True)
+                    res["bf16"] = {"error": repr(e)}
+            else:
+                res["bf16"] = {"skipped": f"run past {sweep_soft:.0f} s from process start"}
         comm.set_engine(chosen[0])
         # north_star: the path starts and ends in host memory -- the end-to-end
         # rate with pinned H2D / D2H, at this N too
-        if agree([time.monotonic() - T_START], world)[0] <= soft:
-            set_stage("host_e2e at N > 1")
-            try:
-                res["host_e2e"] = host_e2e(comm, k, world=world)
-            except Exception as e:  # noqa: BLE001
-                print(f"rank {rank}: host_e2e failed: {e!r}", file=sys.stderr, flush=True)
-                res["host_e2e"] = {"error": repr(e)}
+        with Phase("host_e2e"):
+            if agree([time.monotonic() - T_START], world)[0] <= sweep_soft:
+                set_stage("host_e2e at N > 1")
+                try:
+                    res["host_e2e"] = host_e2e(comm, k, world=world)
+                except Exception as e:  # noqa: BLE001
+                    print(f"rank {rank}: host_e2e failed: {e!r}", file=sys.stderr, flush=True)
+                    res["host_e2e"] = {"error": repr(e)}
+            else:
+                res["host_e2e"] = {"skipped": f"run past {sweep_soft:.0f} s from process start"}
     def extra(key, fn):
         """An N = 1 extra key (one process, no collectives): a failure is recorded
         in the key instead of costing the headline line."""
         set_stage(f"extra key {key}")
-        try:
-            res[key] = fn()
-        except Exception as e:  # noqa: BLE001
-            print(f"bench: extra key {key} failed: {e!r}", file=sys.stderr, flush=True)
-            res[key] = {"error": repr(e)}
+        with Phase(key):
+            try:
+                res[key] = fn()
+            except Exception as e:  # noqa: BLE001
+                print(f"bench: extra key {key} failed: {e!r}", file=sys.stderr, flush=True)
+                res[key] = {"error": repr(e)}
 
     if world == 1 and not a.no_extras:
         extra("host_e2e", lambda: host_e2e(comm, k))
@@ -1495,6 +1636,7 @@ def main():
         extra("numerics_vs_exact", lambda: numerics_vs_exact(dev, n))
         extra("bf16", lambda: bf16_buckets(dev, R, k))
         extra("switch_batch", lambda: switch_batch(dev))
+        extra("switch_batch_acks", lambda: switch_batch(dev, acks=True))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         extra("cpu_baseline", lambda: cpu_baseline(n, R, k, a.cpu_seconds))
         extra("cpu_baseline_allcores", lambda: cpu_baseline_allcores(n, R, k, min(a.cpu_seconds, 5.0)))

@@ -45,6 +45,9 @@ SIGNATURES = {
     "inccl_checksum_q32": (_I, [_P, _SZ, _U64, _P, _I, _P]),
     "inccl_choose_scale": (_I, [_F, _I]),
     "inccl_set_tuning": (None, [_I, _I]),
+    "inccl_op_create": (_P, [_I, _I, _P, _I, _P, _SZ, _I, _I, _P]),
+    "inccl_op_run": (_I, [_P]),
+    "inccl_op_destroy": (_I, [_P]),
     "inccl_group_create_ex": (_P, [_I, _I, _S, _I, _I]),
     "inccl_group_create_local": (_P, [_I, _I, _S, _I]),
     "inccl_group_rank": (_I, [_P]),

@@ -102,6 +102,67 @@ int inccl_stream_op(int in_kind, int out_kind, const void *const *srcs_dev, int 
     return kerr(inccl_k_stream(in_kind, out_kind, srcs_dev, R, dst_dev, n, scale_exp, amax_bits_dev, scale_R, stream));
 }
 
+/* ---- prepared stream ops ---- */
+struct inccl_op {
+    int in_kind, out_kind, R, scale_exp, scale_R;
+    const void *srcs[INCCL_MAX_LOCAL_INPUTS];
+    void *dst;
+    size_t n;
+    void *stream;
+};
+
+static int kind_pair_ok(int in_kind, int out_kind)
+{
+    const int plain = (in_kind == INCCL_KIND_F32 || in_kind == INCCL_KIND_Q32 || in_kind == INCCL_KIND_Q32BE) &&
+                      (out_kind == INCCL_KIND_F32 || out_kind == INCCL_KIND_Q32 || out_kind == INCCL_KIND_Q32BE);
+    const int bf16 = (in_kind == INCCL_KIND_BF16 && (out_kind == INCCL_KIND_BF16 || out_kind == INCCL_KIND_Q32)) ||
+                     (in_kind == INCCL_KIND_Q32 && out_kind == INCCL_KIND_BF16);
+    return plain || bf16;
+}
+
+struct inccl_op *inccl_op_create(int in_kind, int out_kind, const void *const *srcs_dev, int R, void *dst_dev,
+                                 size_t n, int scale_exp, int scale_R, void *stream)
+{
+    if (!kind_pair_ok(in_kind, out_kind) || !srcs_dev || R < 1 || R > INCCL_MAX_LOCAL_INPUTS ||
+        (n > 0 && !dst_dev) || scale_exp < INCCL_SCALE_MIN || scale_exp > INCCL_SCALE_MAX || scale_R < 0) {
+        inccl_set_error(INCCL_ERR_ARG, "inccl_op_create: invalid argument");
+        return NULL;
+    }
+    for (int r = 0; r < R; ++r)
+        if (!srcs_dev[r] && n > 0) {
+            inccl_set_error(INCCL_ERR_ARG, "inccl_op_create: srcs[%d] is NULL", r);
+            return NULL;
+        }
+    struct inccl_op *op = (struct inccl_op *)calloc(1, sizeof(*op));
+    if (!op) {
+        inccl_set_error(INCCL_ERR_NOMEM, "inccl_op_create: out of memory");
+        return NULL;
+    }
+    op->in_kind = in_kind;
+    op->out_kind = out_kind;
+    op->R = R;
+    op->scale_exp = scale_exp;
+    op->scale_R = scale_R;
+    for (int r = 0; r < R; ++r) op->srcs[r] = srcs_dev[r];
+    op->dst = dst_dev;
+    op->n = n;
+    op->stream = stream;
+    return op;
+}
+
+int inccl_op_run(struct inccl_op *op)
+{
+    if (!op) return inccl_set_error(INCCL_ERR_ARG, "inccl_op_run: op is NULL");
+    return kerr(inccl_k_stream(op->in_kind, op->out_kind, op->srcs, op->R, op->dst, op->n, op->scale_exp, NULL,
+                               op->scale_R, op->stream));
+}
+
+int inccl_op_destroy(struct inccl_op *op)
+{
+    free(op);
+    return 0;
+}
+
 int inccl_quantise_f32(const float *x_dev, int32_t *q_dev, size_t n, int scale_exp, int wire_be, void *stream)
 {
     const void *s[1] = {x_dev};

@@ -98,6 +98,58 @@ def stream_op(in_kind: int, out_kind: int, srcs, out=None, scale_exp: int = 0, n
     return out
 
 
+class PreparedOp:
+    """``stream_op`` with its arguments checked and bound once (inccl_op_create):
+    each call is then one ctypes call with one argument and one kernel launch,
+    for small buckets whose per-call cost is launch and marshalling, not HBM.
+    Holds references to the bound tensors; call destroy() (or drop it) when done."""
+
+    def __init__(self, in_kind: int, out_kind: int, srcs, out, scale_exp: int, scale_R: int = 0, stream=None):
+        torch = _torch()
+        srcs = list(srcs)
+        if len(srcs) < 1 or len(srcs) > MAX_LOCAL_INPUTS:
+            raise ValueError(f"1..{MAX_LOCAL_INPUTS} inputs per launch, got {len(srcs)}")
+        in_dt, out_dt = getattr(torch, _TORCH_KIND[in_kind]), getattr(torch, _TORCH_KIND[out_kind])
+        n = srcs[0].numel()
+        ptrs = [_dev_ptr(s, in_dt, f"srcs[{i}]", n) for i, s in enumerate(srcs)]
+        if out is None:
+            out = torch.empty(n, dtype=out_dt, device=srcs[0].device)
+        optr = _dev_ptr(out, out_dt, "out", n)
+        if int(scale_exp) == SCALE_AUTO:
+            raise ValueError("a prepared op takes a fixed scale exponent")
+        self.srcs, self.out, self.stream = srcs, out, stream   # kept alive while bound
+        lib = load()
+        h = lib.inccl_op_create(in_kind, out_kind, _ptr_array(ptrs), len(ptrs), optr, n, _check_scale(scale_exp),
+                                int(scale_R), _stream_handle(stream))
+        if not h:
+            raise IncclError(lib.inccl_last_error().decode(errors="replace"))
+        self._h = ctypes.c_void_p(h)
+        self._run = lib.inccl_op_run
+
+    def __call__(self):
+        rc = self._run(self._h)
+        if rc:
+            check(rc, "inccl_op_run")
+        return self.out
+
+    def destroy(self):
+        if self._h is not None:
+            load().inccl_op_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:  # noqa: BLE001 -- interpreter teardown
+            pass
+
+
+def prepare_reduce_f32(srcs, scale_exp: int, out=None, stream=None) -> PreparedOp:
+    """A prepared ``reduce_f32`` (the fused single-GPU bucket reduce)."""
+    srcs = list(srcs)
+    return PreparedOp(KIND_F32, KIND_F32, srcs, out, scale_exp, scale_R=len(srcs), stream=stream)
+
+
 def quantise(x, scale_exp: int, wire_be: bool = False, out=None, stream=None):
     """fp32 -> int32 fixed point (+ optional htonl, api.c:300-302)."""
     return stream_op(KIND_F32, KIND_Q32BE if wire_be else KIND_Q32, [x], out, scale_exp, stream=stream)

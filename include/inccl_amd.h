@@ -85,6 +85,19 @@ int inccl_sum_dequant_q32(const int32_t *const *srcs_dev, int R, float *dst_dev,
  * derives k from that device word and scale_R contributors instead of scale_exp. */
 int inccl_stream_op(int in_kind, int out_kind, const void *const *srcs_dev, int R, void *dst_dev, size_t n,
                     int scale_exp, const uint32_t *amax_bits_dev, int scale_R, void *stream);
+/* A prepared stream op: inccl_stream_op's arguments (a fixed scale exponent)
+ * checked and bound once, so that each run is one kernel launch with no
+ * argument marshalling -- for small buckets, whose launch costs more than their
+ * kernel (4 MiB fused, R = 2: ~2.2 us of device time), called through a
+ * binding such as Python's ctypes, where building the arguments of every call
+ * costs several us more.  The bound buffers and stream must outlive the op.
+ * inccl_op_run launches on the bound stream, stream-ordered like the call it
+ * prepares; NULL from create = invalid arguments (inccl_last_error). */
+struct inccl_op;
+struct inccl_op *inccl_op_create(int in_kind, int out_kind, const void *const *srcs_dev, int R, void *dst_dev,
+                                 size_t n, int scale_exp, int scale_R, void *stream);
+int inccl_op_run(struct inccl_op *op);
+int inccl_op_destroy(struct inccl_op *op);
 /* max |x| over R buckets into *amax_bits_dev (float bits; NaN ignored).  The word
  * is zeroed first when zero_first != 0, else max-accumulated. */
 int inccl_absmax_f32(const float *const *srcs_dev, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
