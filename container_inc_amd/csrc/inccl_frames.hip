@@ -527,7 +527,12 @@ __global__ __launch_bounds__(kClaimBlock) void k_ingress_claim(InccSwitchState s
 // store would fall back to the older word.  The recycle writes both words (no
 // frame of the batch reads that slot).
 // ---------------------------------------------------------------------------
-constexpr int kApplyWaves = 8;    // the sum kernel: one pair per wave, 8-wave blocks (1, 2, 4, 16: 35.1-36.4 us, no better)
+constexpr int kApplyWaves = 8;    // the sum kernel: 8-wave blocks (1, 2, 4, 16: 35.1-36.4 us, no better)
+// consecutive frames per sum wave.  Groups of 4 read a fan-in-2 PSN's copies
+// from registers even with an ACK between them (ACK batch: sum 40.8-42.0 us
+// against 56.6-57.2) but cost 2.2 us on data-only batches (37.5-37.7 against
+// 35.2-35.5): not kept (profiles/r05/switch/sum_variants.txt)
+constexpr int kSumGroup = 2;
 
 struct ApplyArgs {
     InccSwitchState s;
@@ -563,6 +568,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
     const int n = __builtin_amdgcn_readfirstlane((int)bytes);
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+
+// A row's payload tail that lane 63 needs past its own chunk (chunk 67, and
+// with a RETH the first half of chunk 68), as 8-byte loads on lanes 0-2: lane 0
+// chunk 67 dwords 0-1, lane 1 its dwords 2-3, lane 2 chunk 68 dwords 0-1
+__device__ __forceinline__ u2 tail_chunks(__amdgpu_buffer_rsrc_t rs, int rb, int lane)
+{
+    return __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(rs, lane < 3 ? rb + 1072 + 8 * lane : kOobOffset,
+                                                                      0, 0));
 }
 
 // lane l + 1's value (lane 63 gets lane 0's), through a precomputed address
@@ -691,55 +705,72 @@ __global__ __launch_bounds__(kClassifyBlock) void k_ingress_classify(InccSwitchS
                 (fan <= 8 ? (int)((cports << 16) | (wfs << 24)) : kActKeys);
 }
 
-// the sum kernel: one pair per wave, short-lived blocks
+// the sum kernel: one group of kSumGroup consecutive frames per wave, short-lived blocks
 __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A, const int32_t* __restrict__ act_in,
                                                                     const int32_t* __restrict__ ports_in,
                                                                     const uint32_t* __restrict__ psns_in)
 {
+    constexpr int G = kSumGroup;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     const int next4 = ((lane + 1) & (kWave - 1)) * 4;
     const InccSwitchState& s = A.s;
     const int fan = s.fan_in;
-    const int64_t count = A.count, stride = A.stride, pidx = (int64_t)blockIdx.x * kApplyWaves + w;
-    const bool have = 2 * pidx < count;
-    const int64_t f0 = have ? 2 * pidx : 0;
-    const bool in1 = have && f0 + 1 < count;
-    const int64_t f1 = in1 ? f0 + 1 : f0;
-    // one round trip: both rows' payload chunks (lane l chunk 3 + l; lanes 0, 1
-    // chunks 67, 68) with the action words (scalar)
-    u4 x[2] = {}, e[2] = {};
-    if (A.wide) {
-        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(A.frames + f0 * stride, have ? (in1 ? 2 : 1) * stride : 0);
+    const int64_t count = A.count, stride = A.stride, gidx = (int64_t)blockIdx.x * kApplyWaves + w;
+    const int64_t f0 = G * gidx < count ? G * gidx : 0;
+    const int nin = G * gidx < count ? (int)(count - f0 < G ? count - f0 : G) : 0;   // frames of the group (0: none)
+    // round trip 1: the action words (scalar).  Round trip 2: the payload
+    // chunks of the rows that hold a counted copy (lane l chunk 3 + l, and the
+    // tail past lane 63's) -- an ACK, retransmit or invalid row gets a
+    // zero-size buffer, so its loads move no bytes.  (One round trip with every
+    // row loaded speculatively costs the same on data-only batches, 35.1-35.4
+    // against 35.2-35.5 us, and reads every ACK row too: 65.3-66.1 against
+    // 56.6-57.2 us with an ACK after every data frame;
+    // profiles/r05/switch/sum_variants.txt)
+    int act[G];
+    uint32_t psn[G];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int rb = k * (int)stride;
-            x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, rb + 48 + 16 * lane, 0, 0);
-            e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane < 2 ? rb + 1072 + 16 * lane : kOobOffset, 0, 0);
+    for (int k = 0; k < G; ++k) {
+        act[k] = k < nin ? act_in[f0 + k] : 0;
+        psn[k] = k < nin ? psns_in[f0 + k] : 0u;
+    }
+    u4 x[G] = {};
+    u2 e[G] = {};
+    if (A.wide) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int fk = act[k] & 0xFF;
+            const bool counted = (act[k] & kActLeader) || fk == INCCL_SW_ABSORBED || fk == INCCL_SW_COMPLETED;
+            const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(A.frames + (f0 + k) * stride, counted ? stride : 0);
+            x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, 48 + 16 * lane, 0, 0);
+            e[k] = tail_chunks(rs, 0, lane);
         }
     }
-    int act[2];
-    act[0] = have ? act_in[f0] : 0;
-    act[1] = in1 ? act_in[f1] : 0;
-    const uint32_t psn[2] = {psns_in[f0], psns_in[f1]};
     // every data frame's arrival into its slot's degree (nts.c:351 / :431,
     // retransmits included), as the wave's last memory instructions: atomics
     // issued before a wait would be waited for with it
     auto degrees = [&]() {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < G; ++k) {
             const int a = act[k] & 0xFF;
-            if ((k == 0 ? have : in1) && a >= INCCL_SW_ABSORBED && a <= INCCL_SW_REPLAY && lane == 0)
+            if (k < nin && a >= INCCL_SW_ABSORBED && a <= INCCL_SW_REPLAY && lane == 0)
                 atomicAdd(&s.degree[psn[k] & (s.slots - 1)], 1);
         }
     };
-    if (!((act[0] | act[1]) & kActLeader)) {
+    int any = 0;
+#pragma unroll
+    for (int k = 0; k < G; ++k) any |= act[k];
+    if (!(any & kActLeader)) {
         degrees();
         return;
     }
-    const int port[2] = {ports_in[f0], ports_in[f1]};
+    int port[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) port[k] = k < nin ? ports_in[f0 + k] : -1;
     // payload words 4 lane .. 4 lane + 3 of a row, from its chunks: xx = chunk
     // 3 + lane, ee = chunks 67, 68 on lanes 0, 1 (payload at byte 54 + 16 wf)
-    auto extract = [&](const u4& xx, const u4& ee, uint32_t wf, uint32_t (&P)[4]) {
+    // (ee: the tail chunks' dwords, tail_chunks: lane 0 chunk 67 dwords 0-1,
+    // lane 1 its dwords 2-3, lane 2 chunk 68 dwords 0-1)
+    auto extract = [&](const u4& xx, const u2& ee, uint32_t wf, uint32_t (&P)[4]) {
         const bool last = lane == kWave - 1;
         uint32_t y0 = from_next(xx.x, next4), y1 = from_next(xx.y, next4);
         y0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.x, 0) : y0;
@@ -747,10 +778,10 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
         if (wf) {
             uint32_t y2 = from_next(xx.z, next4), y3 = from_next(xx.w, next4);
             uint32_t z0 = from_next(y0, next4), z1 = from_next(y1, next4);
-            y2 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.z, 0) : y2;
-            y3 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.w, 0) : y3;
-            z0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.x, 1) : z0;
-            z1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.y, 1) : z1;
+            y2 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.x, 1) : y2;
+            y3 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.y, 1) : y3;
+            z0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.x, 2) : z0;
+            z1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.y, 2) : z1;
             payload_from_chunks(u4{y0, y1, y2, y3}, z0, z1, P);
         } else {
             payload_from_chunks(xx, y0, y1, P);
@@ -768,9 +799,8 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
     };
     const uint32_t g = s.gen[0];   // this batch's generation (classify stored it)
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < G; ++k) {
         if (!(act[k] & kActLeader)) continue;
-        const int o = k ^ 1;
         const uint32_t slot = psn[k] & (s.slots - 1);
         const bool keys = (act[k] & kActKeys) != 0;
         uint32_t cports, wfs;
@@ -787,19 +817,27 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
         u4 acc = {0u, 0u, 0u, 0u};
         if (act[k] & kActPartial) acc = reinterpret_cast<const u4*>(s.agg + (size_t)slot * kLanes)[lane];
         uint32_t rest = cports, q[4];
-        // the leader's own copy and, if it is a counted copy of this PSN, the
-        // pair's other frame: already in registers
+        // the leader's own copy and every counted copy of this PSN among the
+        // group's other frames: already in registers (a PSN's ports arriving
+        // close together, with or without an ACK between them, is the common
+        // case).  A counted copy is the only frame of its (psn, port) whose
+        // action is ABSORBED or COMPLETED.
         if ((rest >> port[k]) & 1u) {
             payload_of(k, own_wf, q);
             add(acc, q);
             rest &= ~(1u << port[k]);
         }
-        const int fo = act[o] & 0xFF;
-        if (!keys && (k == 0 ? in1 : true) && psn[o] == psn[k] && ((rest >> port[o]) & 1u) &&
-            (fo == INCCL_SW_ABSORBED || fo == INCCL_SW_COMPLETED)) {
-            payload_of(o, (wfs >> port[o]) & 1u, q);
-            add(acc, q);
-            rest &= ~(1u << port[o]);
+#pragma unroll
+        for (int o = 0; o < G; ++o) {
+            if (o == k || keys || o >= nin) continue;
+            const int fo = act[o] & 0xFF;
+            // (a counted copy's port is one of the switch's: the shift is in range)
+            if ((fo == INCCL_SW_ABSORBED || fo == INCCL_SW_COMPLETED) && psn[o] == psn[k] &&
+                ((rest >> (port[o] & 31)) & 1u)) {
+                payload_of(o, (wfs >> port[o]) & 1u, q);
+                add(acc, q);
+                rest &= ~(1u << port[o]);
+            }
         }
         // every other counted copy, two at a time: both keys in one round
         // trip, both rows' chunks in the next (not two round trips per copy)
@@ -819,9 +857,9 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
                 const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A.frames + (int64_t)fa * stride, va ? stride : 0);
                 const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(A.frames + (int64_t)fb * stride, vb ? stride : 0);
                 const u4 xa = __builtin_amdgcn_raw_buffer_load_b128(ra, 48 + 16 * lane, 0, 0);
-                const u4 ea = __builtin_amdgcn_raw_buffer_load_b128(ra, lane < 2 ? 1072 + 16 * lane : kOobOffset, 0, 0);
+                const u2 ea = tail_chunks(ra, 0, lane);
                 const u4 xb = __builtin_amdgcn_raw_buffer_load_b128(rb, 48 + 16 * lane, 0, 0);
-                const u4 eb = __builtin_amdgcn_raw_buffer_load_b128(rb, lane < 2 ? 1072 + 16 * lane : kOobOffset, 0, 0);
+                const u2 eb = tail_chunks(rb, 0, lane);
                 extract(xa, ea, (uint32_t)ka & 1u, q);
                 add(acc, q);
                 if (two) {
@@ -1458,7 +1496,7 @@ int launch_apply(const ApplyArgs& a, hipStream_t st)
     const dim3 lanes((unsigned)((a.count + kClassifyBlock - 1) / kClassifyBlock));
     hipLaunchKernelGGL(k_ingress_classify, lanes, dim3(kClassifyBlock), 0, st, a.s, a.frames, a.stride, a.count, a.ports,
                        a.action, a.psns);
-    const int64_t pairs = (a.count + 1) / 2, blocks = (pairs + kApplyWaves - 1) / kApplyWaves;
+    const int64_t groups = (a.count + kSumGroup - 1) / kSumGroup, blocks = (groups + kApplyWaves - 1) / kApplyWaves;
     hipLaunchKernelGGL(k_ingress_sum, dim3((unsigned)(blocks < 1 ? 1 : blocks)), dim3(kWave * kApplyWaves), 0, st, a,
                        (const int32_t*)a.action, a.ports, a.psns);
     return (int)hipGetLastError();
