@@ -560,7 +560,7 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: 
             del got
         for eng in engines:
             set_stage(f"sweep {b} B engine {eng}")
-            ok, dt, same, got = 1, float("inf"), False, None
+            ok, dt, dtp, same, got = 1, float("inf"), float("inf"), False, None
             try:
                 comm.set_engine(eng)
                 got, same = run_verified(comm, eng, 1, inputs, out, k, st, refs)
@@ -576,10 +576,27 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: 
                     comm.allreduce_f32(inputs[0], out=out, scale_exp=k, stream=st.cuda_stream)
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) / iters
+                # up to 4 MiB, the same call prepared once
+                # (inccl_op_create_allreduce_f32): without the per-call argument
+                # marshalling of the binding (above that it is noise)
+                dtp = float("nan")
+                if b <= (4 << 20):
+                    op = comm.prepare_allreduce_f32(inputs[0], out=out, scale_exp=k, stream=st.cuda_stream)
+                    for _ in range(max(3, iters // 2)):
+                        op()
+                    torch.cuda.synchronize()
+                    dist.barrier()
+                    t0 = time.perf_counter()
+                    for _ in range(iters):
+                        op()
+                    torch.cuda.synchronize()
+                    dtp = (time.perf_counter() - t0) / iters
+                    op.destroy()
             except Exception as e:  # noqa: BLE001
                 print(f"rank {rank}: sweep {b} B engine {eng} failed: {e}", file=sys.stderr, flush=True)
                 ok = 0
-            v = agree([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0], world)
+            v = agree([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0,
+                       dtp if ok else float("inf")], world)
             good, ident = v[1] == 0.0, v[2] == 0.0
             if good and ident and refs is None:
                 refs = (got[0], got[1])
@@ -589,6 +606,7 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: 
                       flush=True)
             row = {"bucket_bytes": b, "engine": eng, "ok": good, "bit_identical": good and ident,
                    "us": round(v[0] * 1e6, 2) if good else None,
+                   "prepared_us": round(v[3] * 1e6, 2) if good and b <= (4 << 20) else None,
                    "algbw_GBps": round(b / v[0] / 1e9, 2) if good else None,
                    "value_GBps": round(world * R * b / v[0] / 1e9, 2) if good else None}
             if good:

@@ -104,7 +104,8 @@ int inccl_stream_op(int in_kind, int out_kind, const void *const *srcs_dev, int 
 
 /* ---- prepared stream ops ---- */
 struct inccl_op {
-    int in_kind, out_kind, R, scale_exp, scale_R;
+    struct inccl_communicator *comm;   /* NULL: a stream op; else an fp32 allreduce of comm */
+    int in_kind, out_kind, R, scale_exp, scale_R, chunks;
     const void *srcs[INCCL_MAX_LOCAL_INPUTS];
     void *dst;
     size_t n;
@@ -150,9 +151,31 @@ struct inccl_op *inccl_op_create(int in_kind, int out_kind, const void *const *s
     return op;
 }
 
+struct inccl_op *inccl_op_create_allreduce_f32(struct inccl_communicator *comm, const float *const *srcs_dev, int R,
+                                               float *dst_dev, size_t n, int scale_exp, int chunks, void *stream)
+{
+    if (!comm) {
+        inccl_set_error(INCCL_ERR_ARG, "inccl_op_create_allreduce_f32: comm is NULL");
+        return NULL;
+    }
+    if (scale_exp == INCCL_SCALE_AUTO) {   /* the auto scale is a per-call absmax: nothing to bind */
+        inccl_set_error(INCCL_ERR_ARG, "inccl_op_create_allreduce_f32: a prepared op takes a fixed scale exponent");
+        return NULL;
+    }
+    struct inccl_op *op = inccl_op_create(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n,
+                                          scale_exp, R, stream);
+    if (!op) return NULL;
+    op->comm = comm;
+    op->chunks = chunks;
+    return op;
+}
+
 int inccl_op_run(struct inccl_op *op)
 {
     if (!op) return inccl_set_error(INCCL_ERR_ARG, "inccl_op_run: op is NULL");
+    if (op->comm)
+        return inccl_allreduce_f32_pipelined(op->comm, (const float *const *)op->srcs, op->R, (float *)op->dst, op->n,
+                                             op->scale_exp, op->chunks, op->stream);
     return kerr(inccl_k_stream(op->in_kind, op->out_kind, op->srcs, op->R, op->dst, op->n, op->scale_exp, NULL,
                                op->scale_R, op->stream));
 }

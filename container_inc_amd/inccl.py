@@ -99,12 +99,15 @@ def stream_op(in_kind: int, out_kind: int, srcs, out=None, scale_exp: int = 0, n
 
 
 class PreparedOp:
-    """``stream_op`` with its arguments checked and bound once (inccl_op_create):
-    each call is then one ctypes call with one argument and one kernel launch,
-    for small buckets whose per-call cost is launch and marshalling, not HBM.
-    Holds references to the bound tensors; call destroy() (or drop it) when done."""
+    """``stream_op`` (or, with ``comm``, ``Communicator.allreduce_f32``) with its
+    arguments checked and bound once (inccl_op_create /
+    inccl_op_create_allreduce_f32): each call is then one ctypes call with one
+    argument, for small buckets whose per-call cost is launch and marshalling,
+    not HBM.  Holds references to the bound tensors; call destroy() (or drop
+    it) when done -- before the communicator, for a prepared allreduce."""
 
-    def __init__(self, in_kind: int, out_kind: int, srcs, out, scale_exp: int, scale_R: int = 0, stream=None):
+    def __init__(self, in_kind: int, out_kind: int, srcs, out, scale_exp: int, scale_R: int = 0, stream=None,
+                 comm=None, chunks: int = 1):
         torch = _torch()
         srcs = list(srcs)
         if len(srcs) < 1 or len(srcs) > MAX_LOCAL_INPUTS:
@@ -117,10 +120,14 @@ class PreparedOp:
         optr = _dev_ptr(out, out_dt, "out", n)
         if int(scale_exp) == SCALE_AUTO:
             raise ValueError("a prepared op takes a fixed scale exponent")
-        self.srcs, self.out, self.stream = srcs, out, stream   # kept alive while bound
+        self.srcs, self.out, self.stream, self.comm = srcs, out, stream, comm   # kept alive while bound
         lib = load()
-        h = lib.inccl_op_create(in_kind, out_kind, _ptr_array(ptrs), len(ptrs), optr, n, _check_scale(scale_exp),
-                                int(scale_R), _stream_handle(stream))
+        if comm is None:
+            h = lib.inccl_op_create(in_kind, out_kind, _ptr_array(ptrs), len(ptrs), optr, n, _check_scale(scale_exp),
+                                    int(scale_R), _stream_handle(stream))
+        else:
+            h = lib.inccl_op_create_allreduce_f32(comm.handle, _ptr_array(ptrs), len(ptrs), optr, n,
+                                                  _check_scale(scale_exp), int(chunks), _stream_handle(stream))
         if not h:
             raise IncclError(lib.inccl_last_error().decode(errors="replace"))
         self._h = ctypes.c_void_p(h)
@@ -356,6 +363,10 @@ class Communicator:
                                                   _check_scale(scale_exp), int(chunks), _stream_handle(stream))
         check(rc, "inccl_allreduce_f32")
         return out
+
+    def prepare_allreduce_f32(self, srcs, out=None, scale_exp: int = 25, chunks: int = 1, stream=None) -> PreparedOp:
+        """``allreduce_f32`` with its arguments bound once: ``op()`` runs it."""
+        return PreparedOp(KIND_F32, KIND_F32, srcs, out, scale_exp, stream=stream, comm=self, chunks=chunks)
 
     def allreduce_bf16(self, srcs, out=None, scale_exp: int = SCALE_AUTO, stream=None):
         """bfloat16 buckets (include/inccl_amd.h inccl_allreduce_bf16)."""

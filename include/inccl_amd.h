@@ -213,6 +213,13 @@ int inccl_allreduce_f32(struct inccl_communicator *comm, const float *const *src
  * inccl_allreduce_f32. */
 int inccl_allreduce_f32_pipelined(struct inccl_communicator *comm, const float *const *srcs_dev, int R,
                                   float *dst_dev, size_t n, int scale_exp, int chunks, void *stream);
+/* A prepared inccl_allreduce_f32_pipelined (see inccl_op_create): a fixed scale
+ * exponent, the same arguments on every run -- for the small-message regime,
+ * where marshalling a call costs as much as the collective.  Collective like
+ * the call it prepares: every rank runs its op for every call.  Destroy with
+ * inccl_op_destroy before the communicator. */
+struct inccl_op *inccl_op_create_allreduce_f32(struct inccl_communicator *comm, const float *const *srcs_dev, int R,
+                                               float *dst_dev, size_t n, int scale_exp, int chunks, void *stream);
 /* Device int32 allreduce (sum, wrap): the arithmetic of inccl_allreduce_write
  * without the host copies. */
 int inccl_allreduce_q32(struct inccl_communicator *comm, const int32_t *src_dev, int32_t *dst_dev, size_t n,

@@ -87,6 +87,20 @@ def _rank_main(rank, world, port, cases, q, engine="p2p", device=0):
             torch.cuda.synchronize()
             for o in outs:
                 results.append(bool(np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32))))
+        # a prepared allreduce (inccl_op_create_allreduce_f32): the same result
+        # from the bound call, run back to back
+        for R, n, k, seed in ((2, 4099, 25, 61), (2, 1 << 20, 24, 62)):
+            xs = _inputs(world, R, n, seed)
+            want = O.reduce_f32([x for per in xs for x in per], k)
+            srcs = [torch.from_numpy(x).to(dev) for x in xs[rank]]
+            out = torch.full((n,), float("nan"), device=dev)
+            torch.cuda.synchronize()
+            op = comm.prepare_allreduce_f32(srcs, out=out, scale_exp=k, stream=comm.stream)
+            for _ in range(3):
+                op()
+            torch.cuda.synchronize()
+            results.append(bool(np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))))
+            op.destroy()
         # in place, dst = srcs[0] (the DDP hook's call, container_inc_amd/ddp.py): a
         # bucket inside the ll slot and one above it
         for R, n, k, seed in ((1, 200_003, "auto", 41), (2, 1 << 20, 25, 42)):
