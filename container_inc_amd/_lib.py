@@ -71,6 +71,8 @@ SIGNATURES = {
     "inccl_allreduce_f32_pipelined": (_I, [_P, _P, _I, _P, _SZ, _I, _I, _P]),
     "inccl_allreduce_bf16": (_I, [_P, _P, _I, _P, _SZ, _I, _P]),
     "inccl_absmax_bf16": (_I, [_P, _I, _SZ, _P, _I, _P]),
+    "inccl_allreduce_f16": (_I, [_P, _P, _I, _P, _SZ, _I, _P]),
+    "inccl_absmax_f16": (_I, [_P, _I, _SZ, _P, _I, _P]),
     "inccl_allreduce_q32": (_I, [_P, _P, _P, _SZ, _P]),
     "inccl_allreduce_f32_host": (_I, [_P, _P, _P, _SZ, _I, _SZ]),
     "inccl_host_register": (_I, [_P, _P, _SZ]),

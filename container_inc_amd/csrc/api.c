@@ -116,9 +116,11 @@ static int kind_pair_ok(int in_kind, int out_kind)
 {
     const int plain = (in_kind == INCCL_KIND_F32 || in_kind == INCCL_KIND_Q32 || in_kind == INCCL_KIND_Q32BE) &&
                       (out_kind == INCCL_KIND_F32 || out_kind == INCCL_KIND_Q32 || out_kind == INCCL_KIND_Q32BE);
-    const int bf16 = (in_kind == INCCL_KIND_BF16 && (out_kind == INCCL_KIND_BF16 || out_kind == INCCL_KIND_Q32)) ||
-                     (in_kind == INCCL_KIND_Q32 && out_kind == INCCL_KIND_BF16);
-    return plain || bf16;
+    int half = 0;
+    for (int h = INCCL_KIND_BF16; h <= INCCL_KIND_F16; ++h)
+        half = half || (in_kind == h && (out_kind == h || out_kind == INCCL_KIND_Q32)) ||
+               (in_kind == INCCL_KIND_Q32 && out_kind == h);
+    return plain || half;
 }
 
 struct inccl_op *inccl_op_create(int in_kind, int out_kind, const void *const *srcs_dev, int R, void *dst_dev,
@@ -211,6 +213,13 @@ int inccl_absmax_f32(const float *const *srcs_dev, int R, size_t n, uint32_t *am
 {
     if (!srcs_dev) return inccl_set_error(INCCL_ERR_ARG, "srcs is NULL");
     return kerr(inccl_k_absmax(srcs_dev, R, n, amax_bits_dev, zero_first, stream));
+}
+
+int inccl_absmax_f16(const uint16_t *const *srcs_dev, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
+                     void *stream)
+{
+    if (!srcs_dev) return inccl_set_error(INCCL_ERR_ARG, "srcs is NULL");
+    return kerr(inccl_k_absmax_f16(srcs_dev, R, n, amax_bits_dev, zero_first, stream));
 }
 
 int inccl_absmax_bf16(const uint16_t *const *srcs_dev, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
@@ -730,8 +739,9 @@ static int resolve_scale(struct inccl_communicator *c, int kind, const void *con
             return inccl_set_error(INCCL_ERR_ARG, "scale_exp %d out of range", scale_exp);
         return 0;
     }
-    int rc = kind == INCCL_KIND_BF16 ? inccl_absmax_bf16((const uint16_t *const *)srcs, R, n, c->d_words, 1, st)
-                                     : inccl_absmax_f32((const float *const *)srcs, R, n, c->d_words, 1, st);
+    int rc = kind == INCCL_KIND_BF16  ? inccl_absmax_bf16((const uint16_t *const *)srcs, R, n, c->d_words, 1, st)
+             : kind == INCCL_KIND_F16 ? inccl_absmax_f16((const uint16_t *const *)srcs, R, n, c->d_words, 1, st)
+                                      : inccl_absmax_f32((const float *const *)srcs, R, n, c->d_words, 1, st);
     if (rc) return rc;
     const int W = c->group->world_size;
     if (W > 1 && c->group->transport == INCCL_TRANSPORT_RCCL &&
@@ -879,15 +889,18 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
     return 0;
 }
 
-/* bfloat16 buckets: the fp32 path's arithmetic on the widened values.  The
- * int32 partial sums travel as in the fp32 path (the switch's aggregate,
- * nts.c:361-363); only the result's format differs, so the "rccl" engine's
- * all-gather moves 2 bytes per element instead of 4. */
-int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev,
-                         size_t n, int scale_exp, void *stream)
+/* 2-byte buckets (kind INCCL_KIND_BF16 or INCCL_KIND_F16): the fp32 path's
+ * arithmetic on the widened values.  The int32 partial sums travel as in the
+ * fp32 path (the switch's aggregate, nts.c:361-363); only the result's format
+ * differs, so the "rccl" engine's all-gather moves 2 bytes per element instead
+ * of 4 (an all-gather copies bytes: the same one serves both formats).  The
+ * mesh and p2p engines' 2-byte result kernels are bf16's; fp16 buckets take
+ * their int32 exchange and dequantise after it. */
+static int allreduce_16(struct inccl_communicator *c, int kind, const uint16_t *const *srcs_dev, int R,
+                        uint16_t *dst_dev, size_t n, int scale_exp, void *stream)
 {
     if (!c || !srcs_dev || R < 1 || R > INCCL_MAX_LOCAL_INPUTS || (!dst_dev && n))
-        return inccl_set_error(INCCL_ERR_ARG, "bad allreduce_bf16 args");
+        return inccl_set_error(INCCL_ERR_ARG, "bad allreduce_%s args", kind == INCCL_KIND_F16 ? "f16" : "bf16");
     for (int r = 0; r < R; ++r)
         if (!srcs_dev[r] && n) return inccl_set_error(INCCL_ERR_ARG, "srcs[%d] is NULL", r);
     if (n == 0) return 0;
@@ -897,13 +910,13 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
     const uint32_t *amax = NULL;
     int k = 0;
     {
-        const int rc = resolve_scale(c, INCCL_KIND_BF16, srcs, R, n, scale_exp, st, &amax, &k);
+        const int rc = resolve_scale(c, kind, srcs, R, n, scale_exp, st, &amax, &k);
         if (rc) return rc;
     }
     const int scale_R = R * W;
     const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: RS/AG path even at world 1 */
     if (W == 1 && !(fs && atoi(fs) != 0))   /* one fused HBM pass */
-        return kerr(inccl_k_stream_s(INCCL_KIND_BF16, INCCL_KIND_BF16, srcs, R, dst_dev, n, k, amax, scale_R,
+        return kerr(inccl_k_stream_s(kind, kind, srcs, R, dst_dev, n, k, amax, scale_R,
                                      c->out_shift, st));
 
     if (c->engine == INCCL_ENGINE_RCCL || c->group->transport == INCCL_TRANSPORT_LOCAL) {
@@ -918,7 +931,7 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
             if (rc) return rc;
         }
         int32_t *qsend = (int32_t *)c->d_q32, *qrecv = qsend + total;
-        rc = kerr(inccl_k_stream(INCCL_KIND_BF16, INCCL_KIND_Q32, srcs, R, qsend, n, k, amax, scale_R, st));
+        rc = kerr(inccl_k_stream(kind, INCCL_KIND_Q32, srcs, R, qsend, n, k, amax, scale_R, st));
         if (rc) return rc;
         if (total > n) INCCL_HIP(hipMemsetAsync(qsend + n, 0, (total - n) * sizeof(int32_t), st));
         rc = inccl_tp_reduce_scatter_q32(c, qsend, qrecv, shard, st);
@@ -926,7 +939,7 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
         uint16_t *gather = in_place ? dst_dev : (uint16_t *)c->d_f32;
         const size_t lo = (size_t)me * shard;
         const void *s1[1] = {qrecv};
-        rc = kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_BF16, s1, 1, gather + lo, shard, k, amax, scale_R,
+        rc = kerr(inccl_k_stream_s(INCCL_KIND_Q32, kind, s1, 1, gather + lo, shard, k, amax, scale_R,
                                    c->out_shift, st));
         if (rc) return rc;
         rc = inccl_tp_all_gather_bf16(c, gather + lo, gather, shard, st);
@@ -935,10 +948,11 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
         return 0;
     }
     /* the mesh engines: the persistent kernel with bf16 sources and results (mesh.c) */
-    if (c->engine == INCCL_ENGINE_MESH && c->group->transport == INCCL_TRANSPORT_RCCL)
+    if (kind == INCCL_KIND_BF16 && c->engine == INCCL_ENGINE_MESH && c->group->transport == INCCL_TRANSPORT_RCCL)
         return inccl_mesh_piece_bf16(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
     /* the p2p engine: bf16 result shards gathered over xGMI (p2p.c) */
-    if (c->engine == INCCL_ENGINE_P2P && c->group->transport == INCCL_TRANSPORT_RCCL && ((uintptr_t)dst_dev & 3u) == 0)
+    if (kind == INCCL_KIND_BF16 && c->engine == INCCL_ENGINE_P2P && c->group->transport == INCCL_TRANSPORT_RCCL &&
+        ((uintptr_t)dst_dev & 3u) == 0)
         return inccl_p2p_piece_bf16(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
     /* every other engine (and a p2p dst that is not 4-B aligned): its int32
      * allreduce of the quantised partials (RCCL all-reduce for "ar" / "a2a",
@@ -946,13 +960,25 @@ int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *sr
     int rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
     if (rc) return rc;
     int32_t *q = (int32_t *)c->d_q32;
-    rc = kerr(inccl_k_stream(INCCL_KIND_BF16, INCCL_KIND_Q32, srcs, R, q, n, k, amax, scale_R, st));
+    rc = kerr(inccl_k_stream(kind, INCCL_KIND_Q32, srcs, R, q, n, k, amax, scale_R, st));
     if (rc) return rc;
     rc = inccl_tp_allreduce_q32(c, q, q, n, st);
     if (rc) return rc;
     const void *s1[1] = {q};
-    return kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_BF16, s1, 1, dst_dev, n, k, amax, scale_R,
+    return kerr(inccl_k_stream_s(INCCL_KIND_Q32, kind, s1, 1, dst_dev, n, k, amax, scale_R,
                                  c->out_shift, st));
+}
+
+int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev,
+                         size_t n, int scale_exp, void *stream)
+{
+    return allreduce_16(c, INCCL_KIND_BF16, srcs_dev, R, dst_dev, n, scale_exp, stream);
+}
+
+int inccl_allreduce_f16(struct inccl_communicator *c, const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev,
+                        size_t n, int scale_exp, void *stream)
+{
+    return allreduce_16(c, INCCL_KIND_F16, srcs_dev, R, dst_dev, n, scale_exp, stream);
 }
 
 /* ------------------------------------------------------------------ */

@@ -21,6 +21,8 @@ int inccl_k_stream_s(int in_kind, int out_kind, const void *const *srcs, int R, 
 int inccl_k_absmax(const float *const *srcs, int R, size_t n, uint32_t *amax_bits_dev, int zero_first, void *stream);
 int inccl_k_absmax_bf16(const uint16_t *const *srcs, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
                         void *stream);
+int inccl_k_absmax_f16(const uint16_t *const *srcs, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
+                        void *stream);
 int inccl_k_checksum(const int32_t *q, size_t n, uint64_t index_base, uint32_t *out_dev, int zero_first,
                      void *stream);
 void inccl_k_set_tuning(int grid_cap, int nt_loads);

@@ -73,13 +73,13 @@ __global__ __launch_bounds__(kBlock) void k_stream16_scalar(SrcPtrs src, void* _
         uint32_t acc = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            if constexpr (IN == BF16)
-                acc += bf16_quant(reinterpret_cast<const uint16_t*>(src.p[r])[i], scale);
+            if constexpr (is16(IN))
+                acc += quant16<IN>(reinterpret_cast<const uint16_t*>(src.p[r])[i], scale);
             else
                 acc += reinterpret_cast<const uint32_t*>(src.p[r])[i];
         }
-        if constexpr (OUT == BF16)
-            reinterpret_cast<uint16_t*>(dst)[i] = (uint16_t)deq_bf16x2(acc, 0u, inv);
+        if constexpr (is16(OUT))
+            reinterpret_cast<uint16_t*>(dst)[i] = (uint16_t)deq16x2<OUT>(acc, 0u, inv);
         else
             reinterpret_cast<uint32_t*>(dst)[i] = acc;
     }
@@ -111,31 +111,40 @@ __device__ __forceinline__ uint32_t abs_bits(uint32_t b)
     return a > 0x7f800000u ? 0u : a;
 }
 
-// absmax over bf16 buckets, as the fp32 bits of the widened values
+// absmax over 2-byte buckets (E: BF16 or F16), as the fp32 bits of the widened values
 __device__ __forceinline__ uint32_t abs_bits_bf16(uint32_t h) { return abs_bits(h << 16); }
+__device__ __forceinline__ uint32_t abs_bits_f16(uint32_t h) { return abs_bits(__float_as_uint(f16_widen(h))); }
+template <int E>
+__device__ __forceinline__ uint32_t abs_bits16(uint32_t h)
+{
+    if constexpr (E == F16) return abs_bits_f16(h);
+    else return abs_bits_bf16(h);
+}
 
-template <bool B16>
+// element kind of k_absmax: F32, BF16 or F16
+template <int E>
 __device__ __forceinline__ uint32_t amax_quad(u32x4 x)
 {
-    if constexpr (B16)
-        return max(max(max(abs_bits_bf16(x.x & 0xffffu), abs_bits_bf16(x.x >> 16)),
-                       max(abs_bits_bf16(x.y & 0xffffu), abs_bits_bf16(x.y >> 16))),
-                   max(max(abs_bits_bf16(x.z & 0xffffu), abs_bits_bf16(x.z >> 16)),
-                       max(abs_bits_bf16(x.w & 0xffffu), abs_bits_bf16(x.w >> 16))));
+    if constexpr (E != F32)
+        return max(max(max(abs_bits16<E>(x.x & 0xffffu), abs_bits16<E>(x.x >> 16)),
+                       max(abs_bits16<E>(x.y & 0xffffu), abs_bits16<E>(x.y >> 16))),
+                   max(max(abs_bits16<E>(x.z & 0xffffu), abs_bits16<E>(x.z >> 16)),
+                       max(abs_bits16<E>(x.w & 0xffffu), abs_bits16<E>(x.w >> 16))));
     else
         return max(max(abs_bits(x.x), abs_bits(x.y)), max(abs_bits(x.z), abs_bits(x.w)));
 }
 
-// max |x| over R buckets of fp32 (B16 = false) or bf16 (B16 = true) elements.
+// max |x| over R buckets of fp32 (E = F32), bf16 or fp16 elements.
 // Geometry from tools/tune/tune_absmax.hip (R = 2 x 256 MiB fp32,
 // profiles/r02/tune_absmax.jsonl): 512 lanes x 2 quads per input and step, all
 // 2R loads in flight before the first compare, grid capped at 2 workgroups per
 // CU -- 0.83-0.84 of HBM, against 0.73 for the round-1 form (256 x 1, 8 per CU).
 constexpr int kAmBlock = 512, kAmU = 2;
 
-template <int R, bool B16>
+template <int R, int E>
 __global__ __launch_bounds__(kAmBlock) void k_absmax(SrcPtrs src, int64_t n, uint32_t* __restrict__ out, int vec)
 {
+    constexpr bool B16 = E != F32;
     constexpr int EPQ = B16 ? 8 : 4;   // elements per 16-B quad
     __shared__ uint32_t part[kAmBlock / 64];
     uint32_t m = 0;
@@ -155,7 +164,7 @@ __global__ __launch_bounds__(kAmBlock) void k_absmax(SrcPtrs src, int64_t n, uin
         for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int u = 0; u < kAmU; ++u) {
-                const uint32_t a = amax_quad<B16>(v[r][u]);
+                const uint32_t a = amax_quad<E>(v[r][u]);
                 m = m > a ? m : a;
             }
     }
@@ -163,7 +172,7 @@ __global__ __launch_bounds__(kAmBlock) void k_absmax(SrcPtrs src, int64_t n, uin
 #pragma unroll
     for (int r = 0; r < R; ++r)
         for (int64_t i = nq * EPQ + (int64_t)blockIdx.x * kAmBlock + threadIdx.x; i < n; i += stride) {
-            const uint32_t a = B16 ? abs_bits_bf16(reinterpret_cast<const uint16_t*>(src.p[r])[i])
+            const uint32_t a = B16 ? abs_bits16<E>(reinterpret_cast<const uint16_t*>(src.p[r])[i])
                                    : abs_bits(reinterpret_cast<const uint32_t*>(src.p[r])[i]);
             m = m > a ? m : a;
         }
@@ -350,6 +359,9 @@ int dispatch(int in_kind, int out_kind, const void* const* srcs, int R, void* ds
     if (in_kind == BF16 && out_kind == BF16) return launch_stream16<BF16, BF16>(srcs, R, dst, n, sc, st);
     if (in_kind == BF16 && out_kind == Q32) return launch_stream16<BF16, Q32>(srcs, R, dst, n, sc, st);
     if (in_kind == Q32 && out_kind == BF16) return launch_stream16<Q32, BF16>(srcs, R, dst, n, sc, st);
+    if (in_kind == F16 && out_kind == F16) return launch_stream16<F16, F16>(srcs, R, dst, n, sc, st);
+    if (in_kind == F16 && out_kind == Q32) return launch_stream16<F16, Q32>(srcs, R, dst, n, sc, st);
+    if (in_kind == Q32 && out_kind == F16) return launch_stream16<Q32, F16>(srcs, R, dst, n, sc, st);
 #define INCCL_CASE(I, O) \
     if (in_kind == I && out_kind == O) return launch_stream<I, O>(srcs, R, dst, n, sc, st);
     INCCL_CASE(F32, F32) INCCL_CASE(F32, Q32) INCCL_CASE(F32, Q32BE)
@@ -365,9 +377,10 @@ bool scale_ok(int k) { return k >= INCCL_SCALE_MIN && k <= INCCL_SCALE_MAX; }
 
 namespace {
 
-template <bool B16>
+template <int E>
 int launch_absmax(const void* const* srcs, int R, size_t n, uint32_t* amax_bits_dev, int zero_first, hipStream_t st)
 {
+    constexpr bool B16 = E != F32;
     if (R < 1 || R > kMaxR || amax_bits_dev == nullptr) return INCCL_ERR_ARG;
     SrcPtrs s = {};
     int vec = 1;
@@ -387,7 +400,7 @@ int launch_absmax(const void* const* srcs, int R, size_t n, uint32_t* amax_bits_
     switch (R) {
 #define INCCL_AM(RR)                                                                                             \
     case RR:                                                                                                     \
-        hipLaunchKernelGGL((k_absmax<RR, B16>), dim3(grid), dim3(kAmBlock), 0, st, s, (int64_t)n, amax_bits_dev, vec); \
+        hipLaunchKernelGGL((k_absmax<RR, E>), dim3(grid), dim3(kAmBlock), 0, st, s, (int64_t)n, amax_bits_dev, vec); \
         break;
         INCCL_AM(1) INCCL_AM(2) INCCL_AM(3) INCCL_AM(4) INCCL_AM(5) INCCL_AM(6) INCCL_AM(7) INCCL_AM(8)
 #undef INCCL_AM
@@ -417,15 +430,22 @@ int inccl_k_stream(int in_kind, int out_kind, const void* const* srcs, int R, vo
 
 int inccl_k_absmax(const float* const* srcs, int R, size_t n, uint32_t* amax_bits_dev, int zero_first, void* stream)
 {
-    return launch_absmax<false>(reinterpret_cast<const void* const*>(srcs), R, n, amax_bits_dev, zero_first,
-                                (hipStream_t)stream);
+    return launch_absmax<F32>(reinterpret_cast<const void* const*>(srcs), R, n, amax_bits_dev, zero_first,
+                              (hipStream_t)stream);
 }
 
 int inccl_k_absmax_bf16(const uint16_t* const* srcs, int R, size_t n, uint32_t* amax_bits_dev, int zero_first,
                         void* stream)
 {
-    return launch_absmax<true>(reinterpret_cast<const void* const*>(srcs), R, n, amax_bits_dev, zero_first,
+    return launch_absmax<BF16>(reinterpret_cast<const void* const*>(srcs), R, n, amax_bits_dev, zero_first,
                                (hipStream_t)stream);
+}
+
+int inccl_k_absmax_f16(const uint16_t* const* srcs, int R, size_t n, uint32_t* amax_bits_dev, int zero_first,
+                       void* stream)
+{
+    return launch_absmax<F16>(reinterpret_cast<const void* const*>(srcs), R, n, amax_bits_dev, zero_first,
+                              (hipStream_t)stream);
 }
 
 int inccl_k_checksum(const int32_t* q, size_t n, uint64_t index_base, uint32_t* out_dev, int zero_first, void* stream)

@@ -15,7 +15,7 @@ namespace inccl_dev {
 constexpr int kBlock = 256;   // default workgroup size
 constexpr int kMaxR = INCCL_MAX_LOCAL_INPUTS;
 
-enum Kind { F32 = 0, Q32 = 1, Q32BE = 2, BF16 = 3 };
+enum Kind { F32 = 0, Q32 = 1, Q32BE = 2, BF16 = 3, F16 = 4 };
 
 struct SrcPtrs {
     const void* p[kMaxR];
@@ -219,15 +219,48 @@ __device__ __forceinline__ uint32_t deq_bf16x2(uint32_t a, uint32_t b, float inv
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2));
 }
 
-// out = OUT(sum_r IN(src_r)) over 8-element groups; IN, OUT in {BF16, Q32},
-// not both Q32.  A workgroup owns BLOCK * U groups per tile; every load of the
-// tile is issued before the arithmetic; full tiles store write-through (sc1)
-// through a buffer resource as k_stream_vec does.
+// ---- IEEE binary16 (fp16) buckets: the same kernel, another 2-byte format ----
+// A half widens to fp32 exactly (v_cvt_f32_f16: subnormals, Inf, NaN kept), so
+// quantisation is again the fp32 rule on the widened value; the dequantised
+// fp32 sum narrows with round to nearest even (v_cvt_f16_f32 under the default
+// mode), overflowing to +-Inf past 65504 as IEEE narrowing does
+// (orc_f32_to_f16).
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float f16_widen(uint32_t h) { return (float)__builtin_bit_cast(_Float16, (uint16_t)h); }
+
+__device__ __forceinline__ uint32_t f16_quant(uint32_t h, float scale) { return quant_sat(f16_widen(h) * scale); }
+
+__device__ __forceinline__ uint32_t deq_f16x2(uint32_t a, uint32_t b, float inv)
+{
+    const f32x2 f = {(float)(int32_t)a * inv, (float)(int32_t)b * inv};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, f16x2));
+}
+
+// a 2-byte format's element h (low 16 bits) quantised, and a pair of sums narrowed
+template <int K>
+__device__ __forceinline__ uint32_t quant16(uint32_t h, float scale)
+{
+    if constexpr (K == F16) return f16_quant(h, scale);
+    else return bf16_quant(h, scale);
+}
+template <int K>
+__device__ __forceinline__ uint32_t deq16x2(uint32_t a, uint32_t b, float inv)
+{
+    if constexpr (K == F16) return deq_f16x2(a, b, inv);
+    else return deq_bf16x2(a, b, inv);
+}
+constexpr bool is16(int k) { return k == BF16 || k == F16; }
+
+// out = OUT(sum_r IN(src_r)) over 8-element groups; IN, OUT in {BF16, F16,
+// Q32}, not both Q32.  A workgroup owns BLOCK * U groups per tile; every load
+// of the tile is issued before the arithmetic; full tiles store write-through
+// (sc1) through a buffer resource as k_stream_vec does.
 template <int IN, int OUT, int R, int BLOCK, int U>
 __global__ __launch_bounds__(BLOCK) void k_stream16(SrcPtrs src, void* __restrict__ dst, int64_t n8, Scale sc)
 {
-    constexpr int VI = IN == BF16 ? 1 : 2;    // u32x4 per group per input
-    constexpr int VO = OUT == BF16 ? 1 : 2;   // u32x4 per group of output
+    constexpr int VI = is16(IN) ? 1 : 2;    // u32x4 per group per input
+    constexpr int VO = is16(OUT) ? 1 : 2;   // u32x4 per group of output
     const int k = resolve_k(sc);
     const float scale = pow2f(k);
     const float inv = deq_scale(sc, k);
@@ -256,12 +289,12 @@ __global__ __launch_bounds__(BLOCK) void k_stream16(SrcPtrs src, void* __restric
             uint32_t acc[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                if constexpr (IN == BF16) {
+                if constexpr (is16(IN)) {
                     const u32x4 x = v[u][r][0];
-                    acc[0] += bf16_quant(x.x & 0xffffu, scale); acc[1] += bf16_quant(x.x >> 16, scale);
-                    acc[2] += bf16_quant(x.y & 0xffffu, scale); acc[3] += bf16_quant(x.y >> 16, scale);
-                    acc[4] += bf16_quant(x.z & 0xffffu, scale); acc[5] += bf16_quant(x.z >> 16, scale);
-                    acc[6] += bf16_quant(x.w & 0xffffu, scale); acc[7] += bf16_quant(x.w >> 16, scale);
+                    acc[0] += quant16<IN>(x.x & 0xffffu, scale); acc[1] += quant16<IN>(x.x >> 16, scale);
+                    acc[2] += quant16<IN>(x.y & 0xffffu, scale); acc[3] += quant16<IN>(x.y >> 16, scale);
+                    acc[4] += quant16<IN>(x.z & 0xffffu, scale); acc[5] += quant16<IN>(x.z >> 16, scale);
+                    acc[6] += quant16<IN>(x.w & 0xffffu, scale); acc[7] += quant16<IN>(x.w >> 16, scale);
                 } else {
                     const u32x4 a = v[u][r][0], b = v[u][r][1];
                     acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
@@ -269,11 +302,11 @@ __global__ __launch_bounds__(BLOCK) void k_stream16(SrcPtrs src, void* __restric
                 }
             }
             u32x4 o[VO];
-            if constexpr (OUT == BF16) {
-                o[0].x = deq_bf16x2(acc[0], acc[1], inv);
-                o[0].y = deq_bf16x2(acc[2], acc[3], inv);
-                o[0].z = deq_bf16x2(acc[4], acc[5], inv);
-                o[0].w = deq_bf16x2(acc[6], acc[7], inv);
+            if constexpr (is16(OUT)) {
+                o[0].x = deq16x2<OUT>(acc[0], acc[1], inv);
+                o[0].y = deq16x2<OUT>(acc[2], acc[3], inv);
+                o[0].z = deq16x2<OUT>(acc[4], acc[5], inv);
+                o[0].w = deq16x2<OUT>(acc[6], acc[7], inv);
             } else {
                 o[0] = u32x4{acc[0], acc[1], acc[2], acc[3]};
                 o[VO - 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};

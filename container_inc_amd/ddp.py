@@ -16,11 +16,12 @@ rank picks the largest exponent whose int32 sum cannot overflow
 of its largest element.  The averaged result is bit-identical to the oracle's
 ``reduce_f32`` of the same buckets divided by the world size.
 
-fp32 and bf16 CUDA buckets are accepted (bf16 through ``inccl_allreduce_bf16``:
-the same int32 sums, the result rounded to bf16).  For a power-of-two world the
-mean comes out of the dequantise stage itself (``inccl_comm_set_average``: scale
-2^-(k + log2 W)), for fp32 and bf16 alike; otherwise the hook divides by W in
-torch.  Anything else raises (no silent fallback to another collective).
+fp32, bf16 and fp16 CUDA buckets are accepted (bf16 / fp16 through
+``inccl_allreduce_bf16`` / ``_f16``: the same int32 sums, the result rounded to
+the bucket's format).  For a power-of-two world the mean comes out of the
+dequantise stage itself (``inccl_comm_set_average``: scale 2^-(k + log2 W)),
+for every format alike; otherwise the hook divides by W in torch.  Anything
+else raises (no silent fallback to another collective).
 """
 from __future__ import annotations
 
@@ -75,9 +76,10 @@ def allreduce_hook(state: HookState, bucket):
     import torch
 
     buf = bucket.buffer()
-    if buf.dtype not in (torch.float32, torch.bfloat16):
-        raise IncclError(f"inccl DDP hook: fp32 or bf16 gradient buckets only, got {buf.dtype}")
-    reduce = state.comm.allreduce_f32 if buf.dtype == torch.float32 else state.comm.allreduce_bf16
+    name = {torch.float32: "allreduce_f32", torch.bfloat16: "allreduce_bf16", torch.float16: "allreduce_f16"}.get(buf.dtype)
+    if name is None:
+        raise IncclError(f"inccl DDP hook: fp32, bf16 or fp16 gradient buckets only, got {buf.dtype}")
+    reduce = getattr(state.comm, name)
     w = state.world_size
     divide = state.average and w > 1 and not state.fold_average()
     if not buf.is_cuda:   # reaches the communicator, which refuses it ("must live on the GPU")

@@ -20,7 +20,7 @@ import numpy as np
 
 from ._lib import IncclError, check, load
 
-KIND_F32, KIND_Q32, KIND_Q32BE, KIND_BF16 = 0, 1, 2, 3
+KIND_F32, KIND_Q32, KIND_Q32BE, KIND_BF16, KIND_F16 = 0, 1, 2, 3, 4
 SCALE_MIN, SCALE_MAX, SCALE_AUTO = -64, 64, 0x7FFFFFFF
 MAX_LOCAL_INPUTS = 8
 PAYLOAD_LEN = 1024           # util.h:85
@@ -70,7 +70,8 @@ def _check_scale(k: int) -> int:
     return k
 
 
-_TORCH_KIND = {KIND_F32: "float32", KIND_Q32: "int32", KIND_Q32BE: "int32", KIND_BF16: "bfloat16"}
+_TORCH_KIND = {KIND_F32: "float32", KIND_Q32: "int32", KIND_Q32BE: "int32", KIND_BF16: "bfloat16",
+               KIND_F16: "float16"}
 
 
 def stream_op(in_kind: int, out_kind: int, srcs, out=None, scale_exp: int = 0, n: int | None = None,
@@ -189,6 +190,23 @@ def sum_dequant(srcs, scale_exp: int, in_be: bool = False, out=None, stream=None
 def reduce_bf16(srcs, scale_exp: int, out=None, stream=None):
     """Fused single-GPU bfloat16 bucket reduce: bf16_rne(dequant(sum_r quant(srcs[r])))."""
     return stream_op(KIND_BF16, KIND_BF16, list(srcs), out, scale_exp, scale_R=len(srcs), stream=stream)
+
+
+def reduce_f16(srcs, scale_exp: int, out=None, stream=None):
+    """Fused single-GPU fp16 bucket reduce: f16_rne(dequant(sum_r quant(srcs[r])))."""
+    return stream_op(KIND_F16, KIND_F16, list(srcs), out, scale_exp, scale_R=len(srcs), stream=stream)
+
+
+def absmax_f16(srcs, stream=None) -> float:
+    torch = _torch()
+    n = srcs[0].numel()
+    ptrs = [_dev_ptr(s, torch.float16, f"srcs[{i}]", n) for i, s in enumerate(srcs)]
+    word = torch.zeros(4, dtype=torch.int32, device=srcs[0].device)
+    rc = load().inccl_absmax_f16(_ptr_array(ptrs), len(ptrs), n, _dev_ptr(word, torch.int32, "word", 1), 1,
+                                 _stream_handle(stream))
+    check(rc, "inccl_absmax_f16")
+    bits = int(word[0].item()) & 0xFFFFFFFF
+    return float(np.array([bits], np.uint32).view(np.float32)[0])
 
 
 def absmax_bf16(srcs, stream=None) -> float:
@@ -367,6 +385,22 @@ class Communicator:
     def prepare_allreduce_f32(self, srcs, out=None, scale_exp: int = 25, chunks: int = 1, stream=None) -> PreparedOp:
         """``allreduce_f32`` with its arguments bound once: ``op()`` runs it."""
         return PreparedOp(KIND_F32, KIND_F32, srcs, out, scale_exp, stream=stream, comm=self, chunks=chunks)
+
+    def allreduce_f16(self, srcs, out=None, scale_exp: int = SCALE_AUTO, stream=None):
+        """IEEE fp16 buckets (include/inccl_amd.h inccl_allreduce_f16)."""
+        torch = _torch()
+        srcs = list(srcs)
+        if not 1 <= len(srcs) <= MAX_LOCAL_INPUTS:
+            raise ValueError(f"1..{MAX_LOCAL_INPUTS} local buckets, got {len(srcs)}")
+        n = srcs[0].numel()
+        ptrs = [_dev_ptr(s, torch.float16, f"srcs[{i}]", n) for i, s in enumerate(srcs)]
+        if out is None:
+            out = torch.empty(n, dtype=torch.float16, device=srcs[0].device)
+        optr = _dev_ptr(out, torch.float16, "out", n)
+        rc = load().inccl_allreduce_f16(self.handle, _ptr_array(ptrs), len(ptrs), optr, n, _check_scale(scale_exp),
+                                        _stream_handle(stream))
+        check(rc, "inccl_allreduce_f16")
+        return out
 
     def allreduce_bf16(self, srcs, out=None, scale_exp: int = SCALE_AUTO, stream=None):
         """bfloat16 buckets (include/inccl_amd.h inccl_allreduce_bf16)."""

@@ -52,6 +52,9 @@ extern "C" {
 #define INCCL_KIND_BF16 3    /* bfloat16 gradient (2-byte elements): quantised as the fp32 it
                                 widens to exactly; dequantised as bf16_rne((float)s * 2^-k).
                                 Pairs: BF16->BF16, BF16->Q32, Q32->BF16 */
+#define INCCL_KIND_F16 4     /* IEEE binary16 gradient: quantised as the fp32 it widens to exactly;
+                                dequantised as f16_rne((float)s * 2^-k) (+-Inf past 65504).
+                                Pairs: F16->F16, F16->Q32, Q32->F16 */
 
 const char *inccl_last_error(void);
 const char *inccl_version(void);
@@ -254,6 +257,18 @@ int inccl_allreduce_bf16(struct inccl_communicator *comm, const uint16_t *const 
 /* max |x| over R bf16 buckets into *amax_bits_dev (as fp32 bits; NaN ignored). */
 int inccl_absmax_bf16(const uint16_t *const *srcs_dev, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
                       void *stream);
+
+/* IEEE binary16 buckets (uint16_t bit patterns), the same arithmetic:
+ * dst = f16_rne( (float)( sum over ranks, sum over r<R  quant(srcs[r]) ) * 2^-k ).
+ * world == 1: one fused kernel, (R + 1) * 2 * n HBM bytes.  world > 1: "rccl"
+ * and the in-process transport as bf16 (int32 reduce-scatter, 2-byte
+ * all-gather); every other engine: quant+local sum -> its int32 allreduce ->
+ * dequantise.  dst may alias srcs[0]. */
+int inccl_allreduce_f16(struct inccl_communicator *comm, const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev,
+                        size_t n, int scale_exp, void *stream);
+/* max |x| over R fp16 buckets into *amax_bits_dev (as fp32 bits; NaN ignored). */
+int inccl_absmax_f16(const uint16_t *const *srcs_dev, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
+                     void *stream);
 
 /* Host-memory fp32 allreduce (BASELINE config 3): src/dst in host memory,
  * pipelined H2D / reduce / D2H over `bucket_bytes` buckets on three streams.

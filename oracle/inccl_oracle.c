@@ -174,6 +174,93 @@ float orc_absmax_bf16(const uint16_t *const *srcs, int R, size_t n)
     return m;
 }
 
+/* IEEE binary16: widening is exact; narrowing rounds to nearest even, past
+ * 65504 to +-Inf (the halfway point 65520 rounds to Inf: 65504's last mantissa
+ * bit is odd), below 2^-14 to subnormals (gradual underflow), NaN kept quiet. */
+float orc_f16_to_f32(uint16_t h)
+{
+    const uint32_t sign = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1Fu, m = h & 0x3FFu;
+    union { uint32_t u; float f; } c;
+    if (e == 0x1F) c.u = sign | 0x7F800000u | (m << 13);
+    else if (e == 0) {
+        c.f = (float)m * 5.9604644775390625e-08f;   /* m * 2^-24, exact */
+        c.u |= sign;
+    } else c.u = sign | ((e + 112u) << 23) | (m << 13);
+    return c.f;
+}
+
+uint16_t orc_f32_to_f16(float f)
+{
+    union { uint32_t u; float f; } c;
+    c.f = f;
+    const uint32_t sign = (c.u >> 16) & 0x8000u, ax = c.u & 0x7FFFFFFFu;
+    if (ax > 0x7F800000u) return (uint16_t)(sign | 0x7E00u | ((ax >> 13) & 0x3FFu));
+    if (ax >= 0x477FF000u) return (uint16_t)(sign | 0x7C00u);        /* >= 65520: Inf */
+    const uint32_t e = ax >> 23, m = ax & 0x7FFFFFu;
+    if (ax >= 0x38800000u) {                                          /* normal half */
+        uint32_t h = ((e - 112u) << 10) | (m >> 13);
+        const uint32_t rem = m & 0x1FFFu;
+        if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;       /* a carry moves into the exponent */
+        return (uint16_t)(sign | h);
+    }
+    if (ax <= 0x33000000u) return (uint16_t)sign;                     /* <= 2^-25: zero (2^-25 ties to even) */
+    const uint32_t mm = m | 0x800000u, sh = 126u - e;                 /* subnormal: 14 <= sh <= 24 */
+    uint32_t h = mm >> sh;
+    const uint32_t rem = mm & ((1u << sh) - 1u), half = 1u << (sh - 1u);
+    if (rem > half || (rem == half && (h & 1u))) ++h;
+    return (uint16_t)(sign | h);
+}
+
+void orc_f16_to_f32_n(const uint16_t *h, float *f, size_t n)
+{
+    for (size_t i = 0; i < n; ++i) f[i] = orc_f16_to_f32(h[i]);
+}
+
+void orc_f32_to_f16_n(const float *f, uint16_t *h, size_t n)
+{
+    for (size_t i = 0; i < n; ++i) h[i] = orc_f32_to_f16(f[i]);
+}
+
+void orc_reduce_f16(const uint16_t *const *srcs, int R, uint16_t *dst, size_t n, int k)
+{
+    const float s = pow2f(-k);
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t acc = 0;
+        for (int r = 0; r < R; ++r) acc += (uint32_t)orc_quantise_one(orc_f16_to_f32(srcs[r][i]), k);
+        dst[i] = orc_f32_to_f16((float)(int32_t)acc * s);
+    }
+}
+
+void orc_quant_sum_f16(const uint16_t *const *srcs, int R, int32_t *dst, size_t n, int k)
+{
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t acc = 0;
+        for (int r = 0; r < R; ++r) acc += (uint32_t)orc_quantise_one(orc_f16_to_f32(srcs[r][i]), k);
+        dst[i] = (int32_t)acc;
+    }
+}
+
+void orc_sum_dequant_f16(const int32_t *const *srcs, int R, uint16_t *dst, size_t n, int k)
+{
+    const float s = pow2f(-k);
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t acc = 0;
+        for (int r = 0; r < R; ++r) acc += (uint32_t)srcs[r][i];
+        dst[i] = orc_f32_to_f16((float)(int32_t)acc * s);
+    }
+}
+
+float orc_absmax_f16(const uint16_t *const *srcs, int R, size_t n)
+{
+    float m = 0.0f;
+    for (int r = 0; r < R; ++r)
+        for (size_t i = 0; i < n; ++i) {
+            float a = fabsf(orc_f16_to_f32(srcs[r][i]));
+            if (a > m) m = a;
+        }
+    return m;
+}
+
 int orc_choose_scale(float absmax, int R)
 {
     if (!(absmax > 0.0f)) return ORC_SCALE_MAX;

@@ -86,6 +86,17 @@ void orc_reduce_bf16(const uint16_t *const *srcs, int R, uint16_t *dst, size_t n
 void orc_quant_sum_bf16(const uint16_t *const *srcs, int R, int32_t *dst, size_t n, int k);
 void orc_sum_dequant_bf16(const int32_t *const *srcs, int R, uint16_t *dst, size_t n, int k);
 float orc_absmax_bf16(const uint16_t *const *srcs, int R, size_t n);
+/* IEEE binary16 buckets: widening exact; narrowing to nearest even, +-Inf past
+ * 65504, subnormals below 2^-14 (pinned against numpy's float16 in
+ * tests/test_oracle_f16.py) */
+float orc_f16_to_f32(uint16_t h);
+uint16_t orc_f32_to_f16(float f);
+void orc_f16_to_f32_n(const uint16_t *h, float *f, size_t n);
+void orc_f32_to_f16_n(const float *f, uint16_t *h, size_t n);
+void orc_reduce_f16(const uint16_t *const *srcs, int R, uint16_t *dst, size_t n, int k);
+void orc_quant_sum_f16(const uint16_t *const *srcs, int R, int32_t *dst, size_t n, int k);
+void orc_sum_dequant_f16(const int32_t *const *srcs, int R, uint16_t *dst, size_t n, int k);
+float orc_absmax_f16(const uint16_t *const *srcs, int R, size_t n);
 /* Largest k with R*absmax*2^k <= 2^30 (one bit of headroom), clamped to
  * [ORC_SCALE_MIN, ORC_SCALE_MAX]; absmax == 0 -> ORC_SCALE_MAX; Inf -> ORC_SCALE_MIN. */
 int   orc_choose_scale(float absmax, int R);

@@ -61,6 +61,17 @@ def lib():
         L.orc_sum_dequant_bf16.argtypes = [P, ctypes.c_int, P, sz, ctypes.c_int]
         L.orc_absmax_bf16.argtypes = [P, ctypes.c_int, sz]
         L.orc_absmax_bf16.restype = ctypes.c_float
+        L.orc_f16_to_f32.argtypes = [ctypes.c_uint16]
+        L.orc_f16_to_f32.restype = ctypes.c_float
+        L.orc_f32_to_f16.argtypes = [ctypes.c_float]
+        L.orc_f32_to_f16.restype = ctypes.c_uint16
+        L.orc_f16_to_f32_n.argtypes = [P, P, sz]
+        L.orc_f32_to_f16_n.argtypes = [P, P, sz]
+        L.orc_reduce_f16.argtypes = [P, ctypes.c_int, P, sz, ctypes.c_int]
+        L.orc_quant_sum_f16.argtypes = [P, ctypes.c_int, P, sz, ctypes.c_int]
+        L.orc_sum_dequant_f16.argtypes = [P, ctypes.c_int, P, sz, ctypes.c_int]
+        L.orc_absmax_f16.argtypes = [P, ctypes.c_int, sz]
+        L.orc_absmax_f16.restype = ctypes.c_float
         L.orc_choose_scale.argtypes = [ctypes.c_float, ctypes.c_int]
         L.orc_choose_scale.restype = ctypes.c_int
         L.orc_checksum_q32.argtypes = [P, sz, ctypes.c_uint64]
@@ -192,6 +203,47 @@ def sum_dequant_bf16(srcs, k: int) -> np.ndarray:
 def absmax_bf16(srcs) -> float:
     srcs = [np.ascontiguousarray(s, dtype=np.uint16) for s in srcs]
     return float(lib().orc_absmax_bf16(_ptr_array(srcs), len(srcs), srcs[0].size))
+
+
+# ---- IEEE binary16 buckets (uint16 bit patterns) ----
+def f16_to_f32(h: np.ndarray) -> np.ndarray:
+    h = np.ascontiguousarray(h, dtype=np.uint16).ravel()
+    out = np.empty(h.size, np.float32)
+    lib().orc_f16_to_f32_n(_p(h), _p(out), h.size)
+    return out
+
+
+def f32_to_f16(x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32).ravel()
+    out = np.empty(x.size, np.uint16)
+    lib().orc_f32_to_f16_n(_p(x), _p(out), x.size)
+    return out
+
+
+def reduce_f16(srcs, k: int) -> np.ndarray:
+    srcs = [np.ascontiguousarray(s, dtype=np.uint16) for s in srcs]
+    out = np.empty(srcs[0].shape, np.uint16)
+    lib().orc_reduce_f16(_ptr_array(srcs), len(srcs), _p(out), out.size, int(k))
+    return out
+
+
+def quant_sum_f16(srcs, k: int) -> np.ndarray:
+    srcs = [np.ascontiguousarray(s, dtype=np.uint16) for s in srcs]
+    out = np.empty(srcs[0].shape, np.int32)
+    lib().orc_quant_sum_f16(_ptr_array(srcs), len(srcs), _p(out), out.size, int(k))
+    return out
+
+
+def sum_dequant_f16(srcs, k: int) -> np.ndarray:
+    srcs = [np.ascontiguousarray(s, dtype=np.int32) for s in srcs]
+    out = np.empty(srcs[0].shape, np.uint16)
+    lib().orc_sum_dequant_f16(_ptr_array(srcs), len(srcs), _p(out), out.size, int(k))
+    return out
+
+
+def absmax_f16(srcs) -> float:
+    srcs = [np.ascontiguousarray(s, dtype=np.uint16) for s in srcs]
+    return float(lib().orc_absmax_f16(_ptr_array(srcs), len(srcs), srcs[0].size))
 
 
 def choose_scale(amax: float, R: int) -> int:

@@ -43,32 +43,47 @@ class GlooStandIn:
         out.copy_(torch.from_numpy(O.reduce_f32(every, k)))
         return out
 
-    def allreduce_bf16(self, srcs, out=None, scale_exp=25, stream=None):
+    def _allreduce_16(self, srcs, out, scale_exp, absmax, reduce, dtype):
         import torch
         import torch.distributed as dist
         from container_inc_amd import inccl
-        from oracle import oracle as O
         W = self.group.world_size
         # gloo has no 16-bit types: the bit patterns travel widened to int32
         mine = srcs[0].contiguous().view(torch.int16).to(torch.int32)
         got = [torch.empty_like(mine) for _ in range(W)]
         dist.all_gather(got, mine)
         every = [g.numpy().astype(np.uint16) for g in got]
-        k = O.choose_scale(O.absmax_bf16(every), W) if scale_exp == inccl.SCALE_AUTO else scale_exp
-        out.copy_(torch.from_numpy(O.reduce_bf16(every, k).view(np.int16)).view(torch.bfloat16))
+        k = O_choose(absmax(every), W) if scale_exp == inccl.SCALE_AUTO else scale_exp
+        out.copy_(torch.from_numpy(reduce(every, k).view(np.int16)).view(dtype))
         return out
+
+    def allreduce_bf16(self, srcs, out=None, scale_exp=25, stream=None):
+        import torch
+        from oracle import oracle as O
+        return self._allreduce_16(srcs, out, scale_exp, O.absmax_bf16, O.reduce_bf16, torch.bfloat16)
+
+    def allreduce_f16(self, srcs, out=None, scale_exp=25, stream=None):
+        import torch
+        from oracle import oracle as O
+        return self._allreduce_16(srcs, out, scale_exp, O.absmax_f16, O.reduce_f16, torch.float16)
+
+
+def O_choose(amax, W):
+    from oracle import oracle as O
+    return O.choose_scale(amax, W)
 
 
 def _bits(t):
-    """bit patterns of an fp32 (uint32) or bf16 (uint16) tensor as numpy"""
+    """bit patterns of an fp32 (uint32) or bf16 / fp16 (uint16) tensor as numpy"""
     import torch
-    if t.dtype == torch.bfloat16:
+    if t.dtype in (torch.bfloat16, torch.float16):
         return t.detach().view(torch.int16).cpu().numpy().view(np.uint16)
     return t.detach().cpu().numpy().view(np.uint32)
 
 
 def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine="p2p", boot_port=None):
-    """dtype "bf16": a bf16 model, so DDP's buckets are bf16 (inccl_allreduce_bf16);
+    """dtype "bf16" / "f16": a bf16 / fp16 model, so DDP's buckets are bf16 / fp16
+    (inccl_allreduce_bf16 / _f16);
     as_view: gradient_as_bucket_view=True (the grads are views of the buckets);
     boot_port: the library bootstrap's port, chosen free by the parent (gloo uses `port`)."""
     try:
@@ -99,7 +114,7 @@ def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine=
         model = torch.nn.Sequential(torch.nn.Linear(96, 512), torch.nn.Tanh(), torch.nn.Linear(512, 500),
                                     torch.nn.Tanh(), torch.nn.Linear(500, 300), torch.nn.Tanh(),
                                     torch.nn.Linear(300, 10)).to(dev)
-        wdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        wdt = {"bf16": torch.bfloat16, "f16": torch.float16}.get(dtype, torch.float32)
         model = model.to(wdt)
         import copy
         local = copy.deepcopy(model)   # non-DDP twin: this rank's own gradients
@@ -132,10 +147,11 @@ def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine=
             for before, after in seen:
                 allb = [None] * world
                 dist.all_gather_object(allb, _bits(before).tobytes())
-                if dtype == "bf16":
+                if dtype in ("bf16", "f16"):
                     every = [np.frombuffer(b, np.uint16) for b in allb]
-                    k = O.choose_scale(O.absmax_bf16(every), world)
-                    s16 = torch.from_numpy(O.reduce_bf16(every, k).view(np.int16)).view(torch.bfloat16)
+                    absmax, reduce = (O.absmax_bf16, O.reduce_bf16) if dtype == "bf16" else (O.absmax_f16, O.reduce_f16)
+                    k = O.choose_scale(absmax(every), world)
+                    s16 = torch.from_numpy(reduce(every, k).view(np.int16)).view(wdt)
                     want = _bits(s16 / world)   # the hook's div_ (exact for W = 2, 4)
                 else:
                     every = [np.frombuffer(b, np.float32) for b in allb]
@@ -147,7 +163,9 @@ def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine=
             # lane: W quantisation errors of 2^-(k+1) each, divided by W, at the
             # smallest scale any bucket can have (k from the largest |grad| of all),
             # plus the rounding of the sum to the bucket's format (2^-23 relative for
-            # fp32, 2^-8 for bf16, doubled for slack)
+            # fp32, 2^-8 for bf16, 2^-11 for fp16, doubled for slack); fp16 adds its
+            # subnormal spacing 2^-24 as an absolute floor (the sum's rounding and the
+            # hook's div_ each lose up to half of it, doubled for slack)
             opt_local.zero_grad()
             torch.nn.functional.mse_loss(local(x), y).backward()
             means, ddp_grads = [], []
@@ -160,7 +178,9 @@ def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine=
                 ddp_grads.append(p.grad.detach().float().cpu().numpy().astype(np.float64).ravel())
             k = O.choose_scale(np.float32(max(a for _, a in means)), world)
             for (mean, _), got in zip(means, ddp_grads):
-                bound = 2.0 ** -(k + 1) + np.abs(mean) * (2.0 ** -7 if dtype == "bf16" else 2.0 ** -23)
+                rel = {"bf16": 2.0 ** -7, "f16": 2.0 ** -10}.get(dtype, 2.0 ** -23)
+                floor = 2.0 ** -23 if dtype == "f16" else 0.0
+                bound = 2.0 ** -(k + 1) + np.abs(mean) * rel + floor
                 report["grad_err"] = max(report["grad_err"], float(np.max(np.abs(got - mean) / bound)))
             opt.step()
             # the local twin follows the DDP model so the next iteration starts equal

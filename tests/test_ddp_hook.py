@@ -39,7 +39,8 @@ def run_world(world, mode, timeout, dtype="f32", as_view=False, engine="p2p"):
     return res
 
 
-@pytest.mark.parametrize("world,dtype,as_view", [(2, "f32", False), (2, "bf16", False), (2, "f32", True)])
+@pytest.mark.parametrize("world,dtype,as_view", [(2, "f32", False), (2, "bf16", False), (2, "f16", False),
+                                                 (2, "f32", True)])
 def test_ddp_hook_plumbing_gloo(orc, world, dtype, as_view):
     res = run_world(world, "cpu", 300, dtype, as_view)
     for r, rep in res.items():
@@ -52,7 +53,7 @@ def test_ddp_hook_plumbing_gloo(orc, world, dtype, as_view):
         assert rep["grad_err"] <= 1.0, rep
 
 
-def test_ddp_hook_refuses_non_fp32():
+def test_ddp_hook_refuses_other_formats():
     import torch
 
     from container_inc_amd import ddp
@@ -60,7 +61,7 @@ def test_ddp_hook_refuses_non_fp32():
 
     class Bucket:
         def buffer(self):
-            return torch.zeros(8, dtype=torch.float16)   # neither fp32 nor bf16
+            return torch.zeros(8, dtype=torch.float64)   # neither fp32, bf16 nor fp16
 
     with pytest.raises(IncclError):
         ddp.allreduce_hook(ddp.HookState(comm=None), Bucket())

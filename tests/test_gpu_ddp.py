@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("world,dtype,as_view,engine", [(2, "f32", False, "p2p"), (4, "f32", False, "p2p"),
                                                         (2, "bf16", False, "p2p"), (4, "bf16", True, "p2p"),
-                                                        (2, "f32", False, "mesh"), (4, "bf16", False, "meshw")])
+                                                        (2, "f32", False, "mesh"), (4, "bf16", False, "meshw"),
+                                                        (2, "f16", False, "p2p")])
 def test_ddp_hook_gpu(gpu, orc, world, dtype, as_view, engine):
     res = run_world(world, "gpu", 240, dtype, as_view, engine)
     for r, rep in res.items():
