@@ -47,6 +47,7 @@ Extra JSON fields:
   host_e2e          N = 1: BASELINE config 3, 1 GiB pinned host fp32 in 64 MiB buckets
   api_allreduce_write N = 1: the reference's entry point on a 256 MiB host int32
                     message, registered and unregistered
+  f16               N = 1: the same for IEEE float16 buckets (k_stream16<F16,F16,R>)
   bf16              N = 1: R bf16 buckets of 256 MiB (k_stream16), repeated and rotated;
                     N > 1: inccl_allreduce_bf16 on the rccl, p2p, mesh and meshw engines, verified
   sweep             N > 1: 4 KiB .. 256 MiB and 1 GiB per engine, verified with
@@ -942,27 +943,29 @@ def r_variants(dev, k: int, n: int, rs=(1, 8)) -> list:
     return rows
 
 
-def bf16_buckets(dev, R: int, k: int, mib: int = 256) -> dict:
-    """bfloat16 gradient buckets (inccl_reduce_bf16 = k_stream16<BF16,BF16,R>): R
-    resident `mib` MiB bf16 buckets, repeated and rotated through two sets.
-    Algorithmic bytes (R + 1) * 2 * n.  Parity: tests/test_gpu_bf16.py."""
+def bf16_buckets(dev, R: int, k: int, mib: int = 256, fmt: str = "bf16") -> dict:
+    """bfloat16 (fmt "bf16") or float16 ("f16") gradient buckets (inccl_reduce_bf16 /
+    _f16 = k_stream16<BF16,BF16,R> / <F16,F16,R>): R resident `mib` MiB buckets,
+    repeated and rotated through two sets.  Algorithmic bytes (R + 1) * 2 * n.
+    Parity: tests/test_gpu_bf16.py, tests/test_gpu_f16.py."""
     import torch
 
     from container_inc_amd import inccl
+    dtype, reduce = {"bf16": (torch.bfloat16, inccl.reduce_bf16), "f16": (torch.float16, inccl.reduce_f16)}[fmt]
     n = mib * (1 << 20) // 2
     st = torch.cuda.Stream(device=dev)
     gen = torch.Generator(device=dev)
     gen.manual_seed(4000)
-    groups = [([torch.randn(n, generator=gen, device=dev).to(torch.bfloat16) for _ in range(R)],
-               torch.empty(n, device=dev, dtype=torch.bfloat16)) for _ in range(2)]
+    groups = [([torch.randn(n, generator=gen, device=dev).to(dtype) for _ in range(R)],
+               torch.empty(n, device=dev, dtype=dtype)) for _ in range(2)]
     torch.cuda.synchronize()
-    hot = kernel_time_ms(lambda: inccl.reduce_bf16(groups[0][0], k, out=groups[0][1], stream=st.cuda_stream), st, 40)
+    hot = kernel_time_ms(lambda: reduce(groups[0][0], k, out=groups[0][1], stream=st.cuda_stream), st, 40)
     it = [0]
 
     def rotated():
         xs, out = groups[it[0] % 2]
         it[0] += 1
-        inccl.reduce_bf16(xs, k, out=out, stream=st.cuda_stream)
+        reduce(xs, k, out=out, stream=st.cuda_stream)
 
     cold = kernel_time_ms(rotated, st, 40)
     alg = (R + 1) * 2 * n
@@ -1653,6 +1656,7 @@ def main():
         extra("r_variants", lambda: r_variants(dev, k, n))
         extra("numerics_vs_exact", lambda: numerics_vs_exact(dev, n))
         extra("bf16", lambda: bf16_buckets(dev, R, k))
+        extra("f16", lambda: bf16_buckets(dev, R, k, fmt="f16"))
         extra("switch_batch", lambda: switch_batch(dev))
         extra("switch_batch_acks", lambda: switch_batch(dev, acks=True))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
