@@ -893,9 +893,9 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
  * arithmetic on the widened values.  The int32 partial sums travel as in the
  * fp32 path (the switch's aggregate, nts.c:361-363); only the result's format
  * differs, so the "rccl" engine's all-gather moves 2 bytes per element instead
- * of 4 (an all-gather copies bytes: the same one serves both formats).  The
- * mesh and p2p engines' 2-byte result kernels are bf16's; fp16 buckets take
- * their int32 exchange and dequantise after it. */
+ * of 4 (an all-gather copies bytes: the same one serves both formats), and the
+ * mesh and p2p engines' reduce kernels narrow to the bucket's format before
+ * their result exchange. */
 static int allreduce_16(struct inccl_communicator *c, int kind, const uint16_t *const *srcs_dev, int R,
                         uint16_t *dst_dev, size_t n, int scale_exp, void *stream)
 {
@@ -947,13 +947,12 @@ static int allreduce_16(struct inccl_communicator *c, int kind, const uint16_t *
         if (!in_place) INCCL_HIP(hipMemcpyAsync(dst_dev, gather, n * sizeof(uint16_t), hipMemcpyDeviceToDevice, st));
         return 0;
     }
-    /* the mesh engines: the persistent kernel with bf16 sources and results (mesh.c) */
-    if (kind == INCCL_KIND_BF16 && c->engine == INCCL_ENGINE_MESH && c->group->transport == INCCL_TRANSPORT_RCCL)
-        return inccl_mesh_piece_bf16(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
-    /* the p2p engine: bf16 result shards gathered over xGMI (p2p.c) */
-    if (kind == INCCL_KIND_BF16 && c->engine == INCCL_ENGINE_P2P && c->group->transport == INCCL_TRANSPORT_RCCL &&
-        ((uintptr_t)dst_dev & 3u) == 0)
-        return inccl_p2p_piece_bf16(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+    /* the mesh engines: the persistent kernel with 2-byte sources and results (mesh.c) */
+    if (c->engine == INCCL_ENGINE_MESH && c->group->transport == INCCL_TRANSPORT_RCCL)
+        return inccl_mesh_piece16(c, kind, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+    /* the p2p engine: 2-byte result shards gathered over xGMI (p2p.c) */
+    if (c->engine == INCCL_ENGINE_P2P && c->group->transport == INCCL_TRANSPORT_RCCL && ((uintptr_t)dst_dev & 3u) == 0)
+        return inccl_p2p_piece16(c, kind, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
     /* every other engine (and a p2p dst that is not 4-B aligned): its int32
      * allreduce of the quantised partials (RCCL all-reduce for "ar" / "a2a",
      * the p2p exchange for the IPC engines) */

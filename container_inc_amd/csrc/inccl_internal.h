@@ -151,8 +151,9 @@ int inccl_rccl_alltoall_q32(struct inccl_communicator *c, const int32_t *send, i
 /* p2p engine */
 int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
                     const uint32_t *amax, int scale_R, hipStream_t st);
-int inccl_p2p_piece_bf16(struct inccl_communicator *c, const uint16_t *const *srcs, int R, uint16_t *dst, size_t n,
-                         int k, const uint32_t *amax, int scale_R, hipStream_t st);
+/* 2-byte buckets, kind INCCL_KIND_BF16 or INCCL_KIND_F16 */
+int inccl_p2p_piece16(struct inccl_communicator *c, int kind, const uint16_t *const *srcs, int R, uint16_t *dst,
+                      size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st);
 void inccl_p2p_release(struct inccl_communicator *c);
 /* int32 allreduce (wrapping sum) over the p2p engine's IPC buffers: the
  * reference API's inccl_allreduce_write on a multi-process group without RCCL */
@@ -168,8 +169,8 @@ uint64_t inccl_wait_ticks(struct inccl_group *g);   /* bound of an in-kernel wai
 /* mesh engine (mesh.c) */
 int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
                      const uint32_t *amax, int scale_R, hipStream_t st);
-int inccl_mesh_piece_bf16(struct inccl_communicator *c, const uint16_t *const *srcs, int R, uint16_t *dst, size_t n,
-                          int k, const uint32_t *amax, int scale_R, hipStream_t st);
+int inccl_mesh_piece16(struct inccl_communicator *c, int kind, const uint16_t *const *srcs, int R, uint16_t *dst,
+                       size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st);
 void inccl_mesh_release(struct inccl_communicator *c);
 
 /* local transport */

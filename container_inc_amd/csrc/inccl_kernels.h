@@ -33,9 +33,10 @@ int inccl_k_peer_reduce(const void *const *peers, int W, float *dst, size_t n, i
                         const uint32_t *amax_bits_dev, int scale_R, int out_shift, void *stream);
 int inccl_k_peer_gather(const void *const *src, const int64_t *off, const int64_t *cnt, int nseg, void *dst,
                         void *stream);
-/* the pull-reduce with bf16 results: dst[i] = bf16(dequant(sum_j peers[j][i])), n % 4 == 0, dst 8-B aligned */
-int inccl_k_peer_reduce_bf16(const void *const *peers, int W, uint16_t *dst, size_t n, int scale_exp,
-                             const uint32_t *amax_bits_dev, int scale_R, int out_shift, void *stream);
+/* the pull-reduce with 2-byte results: dst[i] = narrow(dequant(sum_j peers[j][i])), narrow = bf16 (kind
+ * INCCL_KIND_BF16) or fp16 (INCCL_KIND_F16) round to nearest even, n % 4 == 0, dst 8-B aligned */
+int inccl_k_peer_reduce16(int kind, const void *const *peers, int W, uint16_t *dst, size_t n, int scale_exp,
+                          const uint32_t *amax_bits_dev, int scale_R, int out_shift, void *stream);
 /* the same gather for 2-byte elements (counts and even offsets in elements; dst 4-B aligned) */
 int inccl_k_peer_gather16(const void *const *src, const int64_t *off, const int64_t *cnt, int nseg, void *dst,
                           void *stream);
@@ -85,7 +86,7 @@ struct inccl_mesh_launch {
     uint32_t *peer_resin[INCCL_MAX_LOCAL_INPUTS];      /* every rank's result inbox (push_res) */
     const uint32_t *own_resin;
     int push_res;                                      /* 1: reduce pushes results, gather copies locally */
-    int b16;                                           /* 1: src / dst hold bf16 (uint16_t) elements */
+    int kind16;                                        /* 0: fp32 src / dst; INCCL_KIND_BF16 / _F16: 2-byte ones */
     uint32_t *peer_sig[INCCL_MAX_LOCAL_INPUTS];        /* every rank's signal array */
     const uint32_t *own_sig;
     uint32_t *ctr;                                     /* own words: calls, retired, ticket, abort */

@@ -87,7 +87,7 @@ struct MeshArgs {
     uint32_t* ctr;                       // [0] calls done, [1] retired, [2] ticket, [3] abort
     uint32_t* err;                       // host-mapped error word
     uint64_t timeout_ticks;
-    int nchunks, W, me, lag, vec_src, vec_dst, push_res, b16;
+    int nchunks, W, me, lag, vec_src, vec_dst, push_res;
     Scale sc;
 };
 
@@ -139,11 +139,11 @@ __device__ __forceinline__ int64_t chunk_len(const MeshArgs& a, int c)
 }
 
 // push(c, j): partial sums of chunk c of shard j -> rank j's inbox, slot me.
-// B16: the sources are bf16 (8 bytes per quad of elements); the partials are
-// int32 either way.
+// E = BF16 / F16: the sources are 2-byte (8 bytes per quad of elements); E = 0:
+// fp32.  The partials are int32 either way.
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-template <int R, bool B16>
+template <int R, int E>
 __device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float scale)
 {
     const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;   // global element index
@@ -153,7 +153,7 @@ __device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float s
     const bool full = a.vec_src && lo + 4 * nq <= a.n;
     for (int64_t q0 = threadIdx.x; q0 < nq; q0 += (int64_t)kMeshBlock * kMeshU) {
         u32x4 acc[kMeshU];
-        if (full && B16) {
+        if (full && is16(E)) {
             u32x2 x[kMeshU][R];
 #pragma unroll
             for (int u = 0; u < kMeshU; ++u) {
@@ -168,10 +168,10 @@ __device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float s
                 acc[u] = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    acc[u].x += bf16_quant(x[u][r].x & 0xffffu, scale);
-                    acc[u].y += bf16_quant(x[u][r].x >> 16, scale);
-                    acc[u].z += bf16_quant(x[u][r].y & 0xffffu, scale);
-                    acc[u].w += bf16_quant(x[u][r].y >> 16, scale);
+                    acc[u].x += quant16<E>(x[u][r].x & 0xffffu, scale);
+                    acc[u].y += quant16<E>(x[u][r].x >> 16, scale);
+                    acc[u].z += quant16<E>(x[u][r].y & 0xffffu, scale);
+                    acc[u].w += quant16<E>(x[u][r].y >> 16, scale);
                 }
             }
         } else if (full) {
@@ -207,8 +207,8 @@ __device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float s
                         if (i < a.n)
 #pragma unroll
                             for (int r = 0; r < R; ++r)
-                                s[e] += B16 ? bf16_quant(reinterpret_cast<const uint16_t*>(a.src.p[r])[i], scale)
-                                            : quant1(reinterpret_cast<const float*>(a.src.p[r])[i], scale);
+                                s[e] += is16(E) ? quant16<E>(reinterpret_cast<const uint16_t*>(a.src.p[r])[i], scale)
+                                                : quant1(reinterpret_cast<const float*>(a.src.p[r])[i], scale);
                     }
                 acc[u] = u32x4{s[0], s[1], s[2], s[3]};
             }
@@ -224,9 +224,10 @@ __device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float s
     if (threadIdx.x == 0) st_sys(a.peer_sig[j] + arrive_idx(a.me, c), epoch);
 }
 
-// reduce(c): my shard's chunk c = dequant(sum over the W inbox slots); B16: the
-// result chunk is bf16 (8 bytes per quad), at element offsets in 2-byte units
-template <bool B16>
+// reduce(c): my shard's chunk c = dequant(sum over the W inbox slots); E = BF16 /
+// F16: the result chunk is 2-byte (8 bytes per quad), at element offsets in
+// 2-byte units
+template <int E>
 __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
 {
     bool ok = true;
@@ -238,7 +239,7 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
 #pragma unroll
     for (int j = 0; j < kMaxR; ++j)
         in[j] = rsrc(a.own_inbox + (int64_t)(j < a.W ? j : 0) * a.inbox_stride + (int64_t)c * a.chunk, bytes);
-    constexpr int ES = B16 ? 2 : 4;   // result element bytes
+    constexpr int ES = is16(E) ? 2 : 4;   // result element bytes
     const uint32_t obytes = (uint32_t)(nq * 4 * ES);
     const __amdgpu_buffer_rsrc_t res = rsrc(reinterpret_cast<const char*>(a.own_res) + (int64_t)c * a.chunk * ES, obytes);
     __amdgpu_buffer_rsrc_t outs[kMaxR];   // push_res: my slot of every rank's result inbox
@@ -269,8 +270,8 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
                 acc.z += x[u][j].z;
                 acc.w += x[u][j].w;
             }
-            if constexpr (B16) {
-                const u32x2 o = {deq_bf16x2(acc.x, acc.y, inv), deq_bf16x2(acc.z, acc.w, inv)};
+            if constexpr (is16(E)) {
+                const u32x2 o = {deq16x2<E>(acc.x, acc.y, inv), deq16x2<E>(acc.z, acc.w, inv)};
                 if (a.push_res) {
 #pragma unroll
                     for (int j = 0; j < kMaxR; ++j)
@@ -343,7 +344,7 @@ __device__ bool do_gather(const MeshArgs& a, int c, int j, uint32_t epoch)
     return true;
 }
 
-// gather(c, j) of a bf16 result: 8 elements per 16-B access, a ragged end of
+// gather(c, j) of a 2-byte result: 8 elements per 16-B access, a ragged end of
 // the bucket element by element
 __device__ bool do_gather16(const MeshArgs& a, int c, int j, uint32_t epoch)
 {
@@ -388,7 +389,7 @@ __device__ bool do_gather16(const MeshArgs& a, int c, int j, uint32_t epoch)
     return true;
 }
 
-template <int R, bool B16>
+template <int R, int E>
 __global__ __launch_bounds__(kMeshBlock) void k_mesh(MeshArgs a)
 {
     __shared__ int s_ticket;
@@ -409,14 +410,14 @@ __global__ __launch_bounds__(kMeshBlock) void k_mesh(MeshArgs a)
         if (t >= total) break;
         const int s = t / per_slot, pos = t - s * per_slot;
         if (pos < W) {
-            if (s < a.nchunks) do_push<R, B16>(a, s, (a.me + 1 + pos) % W, epoch, scale);
+            if (s < a.nchunks) do_push<R, E>(a, s, (a.me + 1 + pos) % W, epoch, scale);
         } else if (pos == W) {
             const int c = s - a.lag;
-            if (c >= 0 && c < a.nchunks && !do_reduce<B16>(a, c, epoch, inv)) break;
+            if (c >= 0 && c < a.nchunks && !do_reduce<E>(a, c, epoch, inv)) break;
         } else {
             const int c = s - 2 * a.lag;
             const int jj = (a.me + pos - W) % W;
-            if (c >= 0 && c < a.nchunks && !(B16 ? do_gather16(a, c, jj, epoch) : do_gather(a, c, jj, epoch))) break;
+            if (c >= 0 && c < a.nchunks && !(is16(E) ? do_gather16(a, c, jj, epoch) : do_gather(a, c, jj, epoch))) break;
         }
     }
     // retire: the last workgroup resets the ticket and advances the call counter
@@ -438,7 +439,7 @@ extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
 {
     if (!l || l->R < 1 || l->R > kMaxR || l->W < 1 || l->W > kMaxR || l->me < 0 || l->me >= l->W || l->grid < 1 ||
         l->nchunks < 1 || l->nchunks > INCCL_MESH_MAX_CHUNKS || l->lag < 1 || (l->shard & 63) || (l->chunk & 63) ||
-        l->chunk == 0 || (size_t)l->nchunks * l->chunk < l->shard || l->shard > l->inbox_stride ||
+        l->chunk == 0 || (l->kind16 != 0 && l->kind16 != BF16 && l->kind16 != F16) || (size_t)l->nchunks * l->chunk < l->shard || l->shard > l->inbox_stride ||
         (size_t)l->W * l->shard < l->n || l->chunk > ((size_t)1 << 26))
         return INCCL_ERR_ARG;
     MeshArgs a{};
@@ -456,7 +457,6 @@ extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
     }
     a.own_resin = l->own_resin;
     a.push_res = l->push_res ? 1 : 0;
-    a.b16 = l->b16 ? 1 : 0;
     if (a.push_res && (l->own_resin == nullptr || l->peer_resin[0] == nullptr)) return INCCL_ERR_ARG;
     a.own_inbox = l->own_inbox;
     a.own_res = l->own_res;
@@ -480,10 +480,12 @@ extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
     const dim3 g((unsigned)l->grid), b(kMeshBlock);
 #define INCCL_MESH_CASE(RR)                                                  \
     case RR:                                                                 \
-        if (l->b16)                                                          \
-            hipLaunchKernelGGL((k_mesh<RR, true>), g, b, 0, st, a);          \
+        if (l->kind16 == F16)                                                \
+            hipLaunchKernelGGL((k_mesh<RR, F16>), g, b, 0, st, a);           \
+        else if (l->kind16 == BF16)                                          \
+            hipLaunchKernelGGL((k_mesh<RR, BF16>), g, b, 0, st, a);          \
         else                                                                 \
-            hipLaunchKernelGGL((k_mesh<RR, false>), g, b, 0, st, a);         \
+            hipLaunchKernelGGL((k_mesh<RR, 0>), g, b, 0, st, a);             \
         break;
     switch (l->R) {
         INCCL_MESH_CASE(1) INCCL_MESH_CASE(2) INCCL_MESH_CASE(3) INCCL_MESH_CASE(4) INCCL_MESH_CASE(5)

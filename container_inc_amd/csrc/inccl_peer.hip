@@ -86,12 +86,12 @@ __global__ __launch_bounds__(BLOCK) void k_peer_reduce(SrcPtrs src, float* __res
     }
 }
 
-// The pull-reduce with a bf16 result (inccl_allreduce_bf16 on the p2p engine):
-// the same 16-B system-scope loads of 4 int32 partials per peer and lane, summed,
-// dequantised and narrowed (v_cvt_pk_bf16_f32) into 8 bytes per lane,
-// written through.
-template <int R, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_peer_reduce_bf16(SrcPtrs src, uint16_t* __restrict__ dst, int64_t n4, Scale sc)
+// The pull-reduce with a 2-byte result (inccl_allreduce_bf16 / _f16 on the p2p
+// engine): the same 16-B system-scope loads of 4 int32 partials per peer and
+// lane, summed, dequantised and narrowed (v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32,
+// K = BF16 / F16) into 8 bytes per lane, written through.
+template <int R, int BLOCK, int K>
+__global__ __launch_bounds__(BLOCK) void k_peer_reduce16(SrcPtrs src, uint16_t* __restrict__ dst, int64_t n4, Scale sc)
 {
     const float inv = deq_scale(sc, resolve_k(sc));
     for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n4; base += (int64_t)gridDim.x * BLOCK) {
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(BLOCK) void k_peer_reduce_bf16(SrcPtrs src, uint16_
                 acc.w += v[r].w;
             }
             typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-            const u32x2 o = {deq_bf16x2(acc.x, acc.y, inv), deq_bf16x2(acc.z, acc.w, inv)};
+            const u32x2 o = {deq16x2<K>(acc.x, acc.y, inv), deq16x2<K>(acc.z, acc.w, inv)};
             __builtin_amdgcn_raw_buffer_store_b64(o, rsrc(dst + base * 4, tile_in / 2), (int)(threadIdx.x * 8u), 0,
                                                   kAuxWT);
         }
@@ -213,10 +213,11 @@ extern "C" int inccl_k_peer_reduce(const void* const* peers, int W, float* dst, 
     return e == hipSuccess ? 0 : (int)e;
 }
 
-extern "C" int inccl_k_peer_reduce_bf16(const void* const* peers, int W, uint16_t* dst, size_t n, int scale_exp,
-                                        const uint32_t* amax_bits_dev, int scale_R, int out_shift, void* stream)
+extern "C" int inccl_k_peer_reduce16(int kind, const void* const* peers, int W, uint16_t* dst, size_t n,
+                                     int scale_exp, const uint32_t* amax_bits_dev, int scale_R, int out_shift,
+                                     void* stream)
 {
-    if (W < 1 || W > kMaxR || dst == nullptr || (n & 3) != 0 || (reinterpret_cast<uintptr_t>(dst) & 7u) != 0)
+    if ((kind != BF16 && kind != F16) || W < 1 || W > kMaxR || dst == nullptr || (n & 3) != 0 || (reinterpret_cast<uintptr_t>(dst) & 7u) != 0)
         return INCCL_ERR_ARG;
     if (n == 0) return 0;
     SrcPtrs s = {};
@@ -231,8 +232,11 @@ extern "C" int inccl_k_peer_reduce_bf16(const void* const* peers, int W, uint16_
 #define INCCL_PR16(WW)                                                                                                \
     case WW: {                                                                                                         \
         constexpr int B = Geometry<WW>::BLOCK;                                                                         \
-        hipLaunchKernelGGL((k_peer_reduce_bf16<WW, B>), dim3((unsigned)((n4 + B - 1) / B)), dim3(B), 0, st, s, dst, n4, \
-                           sc);                                                                                        \
+        const dim3 g((unsigned)((n4 + B - 1) / B));                                                                    \
+        if (kind == F16)                                                                                               \
+            hipLaunchKernelGGL((k_peer_reduce16<WW, B, F16>), g, dim3(B), 0, st, s, dst, n4, sc);                      \
+        else                                                                                                           \
+            hipLaunchKernelGGL((k_peer_reduce16<WW, B, BF16>), g, dim3(B), 0, st, s, dst, n4, sc);                     \
         break;                                                                                                         \
     }
         INCCL_PR16(1) INCCL_PR16(2) INCCL_PR16(3) INCCL_PR16(4) INCCL_PR16(5) INCCL_PR16(6) INCCL_PR16(7)

@@ -220,7 +220,7 @@ static size_t mesh_chunk(size_t shard)
     return ch;
 }
 
-static int mesh_piece(struct inccl_communicator *c, int b16, const void *const *srcs, int R, void *dst, size_t n,
+static int mesh_piece(struct inccl_communicator *c, int kind16, const void *const *srcs, int R, void *dst, size_t n,
                       int k, const uint32_t *amax, int scale_R, hipStream_t st)
 {
     const int W = c->group->world_size, me = c->group->rank;
@@ -252,7 +252,7 @@ static int mesh_piece(struct inccl_communicator *c, int b16, const void *const *
     for (int r = 0; r < R; ++r) l.src[r] = (const float *)srcs[r];
     l.R = R;
     l.dst = (float *)dst;
-    l.b16 = b16;
+    l.kind16 = kind16;
     l.n = n;
     l.shard = shard;
     l.chunk = chunk;
@@ -299,10 +299,11 @@ int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int
     return mesh_piece(c, 0, (const void *const *)srcs, R, dst, n, k, amax, scale_R, st);
 }
 
-/* bf16 buckets: the same kernel with bf16 sources, int32 partials and a bf16
- * result, so the xGMI bytes are 4 + 2 per element instead of 4 + 4 */
-int inccl_mesh_piece_bf16(struct inccl_communicator *c, const uint16_t *const *srcs, int R, uint16_t *dst, size_t n,
-                          int k, const uint32_t *amax, int scale_R, hipStream_t st)
+/* bf16 / fp16 buckets: the same kernel with 2-byte sources, int32 partials and a
+ * 2-byte result, so the xGMI bytes are 4 + 2 per element instead of 4 + 4 */
+int inccl_mesh_piece16(struct inccl_communicator *c, int kind, const uint16_t *const *srcs, int R, uint16_t *dst,
+                       size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st)
 {
-    return mesh_piece(c, 1, (const void *const *)srcs, R, dst, n, k, amax, scale_R, st);
+    if (kind != INCCL_KIND_BF16 && kind != INCCL_KIND_F16) return inccl_set_error(INCCL_ERR_ARG, "mesh: bad kind %d", kind);
+    return mesh_piece(c, kind, (const void *const *)srcs, R, dst, n, k, amax, scale_R, st);
 }

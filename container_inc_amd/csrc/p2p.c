@@ -225,14 +225,14 @@ int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int 
     return 0;
 }
 
-/* bfloat16 buckets over the same buffers and barriers: quant + local sum of the
- * bf16 buckets -> part; barrier; shard `me` pulled from every peer, summed,
- * dequantised and narrowed to bf16 in one kernel into res (2-byte elements at
- * me * shard); barrier; every rank's bf16 result shard gathered -- 2 bytes per
- * element over xGMI instead of the int32 allreduce's 4.  dst must be 4-byte
+/* bfloat16 / float16 buckets (kind) over the same buffers and barriers: quant +
+ * local sum of the 2-byte buckets -> part; barrier; shard `me` pulled from every
+ * peer, summed, dequantised and narrowed in one kernel into res (2-byte elements
+ * at me * shard); barrier; every rank's 2-byte result shard gathered -- 2 bytes
+ * per element over xGMI instead of the int32 allreduce's 4.  dst must be 4-byte
  * aligned. */
-int inccl_p2p_piece_bf16(struct inccl_communicator *c, const uint16_t *const *srcs, int R, uint16_t *dst, size_t n,
-                         int k, const uint32_t *amax, int scale_R, hipStream_t st)
+int inccl_p2p_piece16(struct inccl_communicator *c, int kind, const uint16_t *const *srcs, int R, uint16_t *dst,
+                      size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st)
 {
     const int W = c->group->world_size, me = c->group->rank;
     if (W > INCCL_MAX_LOCAL_INPUTS) return inccl_set_error(INCCL_ERR_ARG, "p2p engine supports up to %d GPUs",
@@ -241,17 +241,16 @@ int inccl_p2p_piece_bf16(struct inccl_communicator *c, const uint16_t *const *sr
     int rc = p2p_ensure(c, total);
     if (rc) return rc;
     if (c->p2p_last_stream && c->p2p_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[8], 0));
-    rc = inccl_k_stream(INCCL_KIND_BF16, INCCL_KIND_Q32, (const void *const *)srcs, R, c->p2p_part, n, k, amax,
-                        scale_R, st);
-    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p bf16 quant+sum launch failed (%d)", rc);
+    rc = inccl_k_stream(kind, INCCL_KIND_Q32, (const void *const *)srcs, R, c->p2p_part, n, k, amax, scale_R, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p 16-bit quant+sum launch failed (%d)", rc);
     if (total > n) INCCL_HIP(hipMemsetAsync(c->p2p_part + n, 0, (total - n) * sizeof(int32_t), st));
     rc = sync_and_barrier(c, st);
     if (rc) return rc;
     const void *peer[INCCL_MAX_LOCAL_INPUTS];
     for (int j = 0; j < W; ++j) peer[j] = c->p2p_peer_part[j] + (size_t)me * shard;
-    rc = inccl_k_peer_reduce_bf16(peer, W, (uint16_t *)c->p2p_res + (size_t)me * shard, shard, k, amax, scale_R,
-                                  c->out_shift, st);
-    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p bf16 reduce-scatter launch failed (%d)", rc);
+    rc = inccl_k_peer_reduce16(kind, peer, W, (uint16_t *)c->p2p_res + (size_t)me * shard, shard, k, amax, scale_R,
+                               c->out_shift, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p 16-bit reduce-scatter launch failed (%d)", rc);
     rc = sync_and_barrier(c, st);
     if (rc) return rc;
     const void *src[INCCL_MAX_LOCAL_INPUTS];
@@ -263,7 +262,7 @@ int inccl_p2p_piece_bf16(struct inccl_communicator *c, const uint16_t *const *sr
         cnt[j] = lo >= n ? 0 : (int64_t)((n - lo) < shard ? (n - lo) : shard);
     }
     rc = inccl_k_peer_gather16(src, off, cnt, W, dst, st);
-    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p bf16 gather launch failed (%d)", rc);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p 16-bit gather launch failed (%d)", rc);
     INCCL_HIP(hipEventRecord(c->ev[8], st));
     c->p2p_last_stream = st;
     return 0;

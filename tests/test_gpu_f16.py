@@ -192,10 +192,11 @@ def _ipc_rank(rank, world, port, q, engine):
         q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "mesh"), (4, "meshw"), (2, "ll")])
+@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "mesh"), (3, "mesh"), (4, "meshw"), (2, "ll")])
 def test_allreduce_f16_ipc_multiprocess(gpu, world, engine):
-    """The IPC engines with fp16 buckets: quantise + local sum, that engine's
-    int32 exchange, dequantise to fp16; one process per rank on GPU 0."""
+    """The IPC engines with fp16 buckets, one process per rank on GPU 0: p2p,
+    mesh and meshw narrow to fp16 in their reduce kernel and exchange 2-byte
+    results; ll runs its int32 allreduce and dequantises to fp16 after it."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
