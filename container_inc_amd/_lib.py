@@ -49,6 +49,7 @@ SIGNATURES = {
     "inccl_op_run": (_I, [_P]),
     "inccl_op_destroy": (_I, [_P]),
     "inccl_op_create_allreduce_f32": (_P, [_P, _P, _I, _P, _SZ, _I, _I, _P]),
+    "inccl_op_create_allreduce16": (_P, [_P, _I, _P, _I, _P, _SZ, _I, _P]),
     "inccl_group_create_ex": (_P, [_I, _I, _S, _I, _I]),
     "inccl_group_create_local": (_P, [_I, _I, _S, _I]),
     "inccl_group_rank": (_I, [_P]),

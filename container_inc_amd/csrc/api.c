@@ -104,7 +104,7 @@ int inccl_stream_op(int in_kind, int out_kind, const void *const *srcs_dev, int 
 
 /* ---- prepared stream ops ---- */
 struct inccl_op {
-    struct inccl_communicator *comm;   /* NULL: a stream op; else an fp32 allreduce of comm */
+    struct inccl_communicator *comm;   /* NULL: a stream op; else an allreduce of comm (in_kind: its format) */
     int in_kind, out_kind, R, scale_exp, scale_R, chunks;
     const void *srcs[INCCL_MAX_LOCAL_INPUTS];
     void *dst;
@@ -172,9 +172,33 @@ struct inccl_op *inccl_op_create_allreduce_f32(struct inccl_communicator *comm, 
     return op;
 }
 
+static int allreduce_16(struct inccl_communicator *c, int kind, const uint16_t *const *srcs_dev, int R,
+                        uint16_t *dst_dev, size_t n, int scale_exp, void *stream);
+
+struct inccl_op *inccl_op_create_allreduce16(struct inccl_communicator *comm, int kind,
+                                             const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev, size_t n,
+                                             int scale_exp, void *stream)
+{
+    if (!comm || (kind != INCCL_KIND_BF16 && kind != INCCL_KIND_F16)) {
+        inccl_set_error(INCCL_ERR_ARG, "inccl_op_create_allreduce16: comm is NULL or kind is not BF16 / F16");
+        return NULL;
+    }
+    if (scale_exp == INCCL_SCALE_AUTO) {
+        inccl_set_error(INCCL_ERR_ARG, "inccl_op_create_allreduce16: a prepared op takes a fixed scale exponent");
+        return NULL;
+    }
+    struct inccl_op *op = inccl_op_create(kind, kind, (const void *const *)srcs_dev, R, dst_dev, n, scale_exp, R, stream);
+    if (!op) return NULL;
+    op->comm = comm;
+    return op;
+}
+
 int inccl_op_run(struct inccl_op *op)
 {
     if (!op) return inccl_set_error(INCCL_ERR_ARG, "inccl_op_run: op is NULL");
+    if (op->comm && op->in_kind != INCCL_KIND_F32)
+        return allreduce_16(op->comm, op->in_kind, (const uint16_t *const *)op->srcs, op->R, (uint16_t *)op->dst, op->n,
+                            op->scale_exp, op->stream);
     if (op->comm)
         return inccl_allreduce_f32_pipelined(op->comm, (const float *const *)op->srcs, op->R, (float *)op->dst, op->n,
                                              op->scale_exp, op->chunks, op->stream);

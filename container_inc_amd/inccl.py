@@ -100,9 +100,9 @@ def stream_op(in_kind: int, out_kind: int, srcs, out=None, scale_exp: int = 0, n
 
 
 class PreparedOp:
-    """``stream_op`` (or, with ``comm``, ``Communicator.allreduce_f32``) with its
-    arguments checked and bound once (inccl_op_create /
-    inccl_op_create_allreduce_f32): each call is then one ctypes call with one
+    """``stream_op`` (or, with ``comm``, ``Communicator.allreduce_f32`` / ``_bf16``
+    / ``_f16``) with its arguments checked and bound once (inccl_op_create /
+    inccl_op_create_allreduce_f32 / _allreduce16): each call is then one ctypes call with one
     argument, for small buckets whose per-call cost is launch and marshalling,
     not HBM.  Holds references to the bound tensors; call destroy() (or drop
     it) when done -- before the communicator, for a prepared allreduce."""
@@ -126,9 +126,12 @@ class PreparedOp:
         if comm is None:
             h = lib.inccl_op_create(in_kind, out_kind, _ptr_array(ptrs), len(ptrs), optr, n, _check_scale(scale_exp),
                                     int(scale_R), _stream_handle(stream))
-        else:
+        elif in_kind == KIND_F32:
             h = lib.inccl_op_create_allreduce_f32(comm.handle, _ptr_array(ptrs), len(ptrs), optr, n,
                                                   _check_scale(scale_exp), int(chunks), _stream_handle(stream))
+        else:
+            h = lib.inccl_op_create_allreduce16(comm.handle, in_kind, _ptr_array(ptrs), len(ptrs), optr, n,
+                                                _check_scale(scale_exp), _stream_handle(stream))
         if not h:
             raise IncclError(lib.inccl_last_error().decode(errors="replace"))
         self._h = ctypes.c_void_p(h)
@@ -385,6 +388,14 @@ class Communicator:
     def prepare_allreduce_f32(self, srcs, out=None, scale_exp: int = 25, chunks: int = 1, stream=None) -> PreparedOp:
         """``allreduce_f32`` with its arguments bound once: ``op()`` runs it."""
         return PreparedOp(KIND_F32, KIND_F32, srcs, out, scale_exp, stream=stream, comm=self, chunks=chunks)
+
+    def prepare_allreduce_bf16(self, srcs, out=None, scale_exp: int = 25, stream=None) -> PreparedOp:
+        """``allreduce_bf16`` with its arguments bound once: ``op()`` runs it."""
+        return PreparedOp(KIND_BF16, KIND_BF16, srcs, out, scale_exp, stream=stream, comm=self)
+
+    def prepare_allreduce_f16(self, srcs, out=None, scale_exp: int = 25, stream=None) -> PreparedOp:
+        """``allreduce_f16`` with its arguments bound once: ``op()`` runs it."""
+        return PreparedOp(KIND_F16, KIND_F16, srcs, out, scale_exp, stream=stream, comm=self)
 
     def allreduce_f16(self, srcs, out=None, scale_exp: int = SCALE_AUTO, stream=None):
         """IEEE fp16 buckets (include/inccl_amd.h inccl_allreduce_f16)."""

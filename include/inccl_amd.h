@@ -223,6 +223,11 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *comm, const float *
  * inccl_op_destroy before the communicator. */
 struct inccl_op *inccl_op_create_allreduce_f32(struct inccl_communicator *comm, const float *const *srcs_dev, int R,
                                                float *dst_dev, size_t n, int scale_exp, int chunks, void *stream);
+/* The same for 2-byte buckets: a prepared inccl_allreduce_bf16 (kind
+ * INCCL_KIND_BF16) or inccl_allreduce_f16 (INCCL_KIND_F16). */
+struct inccl_op *inccl_op_create_allreduce16(struct inccl_communicator *comm, int kind,
+                                             const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev, size_t n,
+                                             int scale_exp, void *stream);
 /* Device int32 allreduce (sum, wrap): the arithmetic of inccl_allreduce_write
  * without the host copies. */
 int inccl_allreduce_q32(struct inccl_communicator *comm, const int32_t *src_dev, int32_t *dst_dev, size_t n,

@@ -199,6 +199,15 @@ def _p2p_rank(rank, world, port, q, engine="p2p"):
                                 stream=comm.stream)   # in place
             torch.cuda.synchronize()
             ok.append(bool(np.array_equal(_host(srcs[0]), want)))
+            if k != "auto":   # prepared (inccl_op_create_allreduce16), run twice on fresh inputs
+                srcs = [_dev(h, dev) for h in hs[rank]]
+                out.fill_(float("nan"))
+                op = comm.prepare_allreduce_bf16(srcs, out=out, scale_exp=k, stream=comm.stream)
+                for _ in range(2):
+                    op()
+                    torch.cuda.synchronize()
+                    ok.append(bool(np.array_equal(_host(out), want)))
+                op.destroy()
         comm.destroy()
         grp.destroy()
         q.put((rank, ok, None))

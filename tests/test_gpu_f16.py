@@ -1,7 +1,8 @@
 """IEEE fp16 buckets on the GPU (gpu): the k_stream16 kernels with F16
 (F16->F16, F16->Q32, Q32->F16), the fp16 absmax, and inccl_allreduce_f16 over
 the in-process transport (reduce-scatter int32 + 2-byte all-gather), RCCL at
-world 1, and the IPC engines' int32 exchange with one process per rank -- all
+world 1, and the IPC engines with one process per rank (p2p / mesh / meshw:
+2-byte result exchange; ll: int32 exchange), plain and prepared -- all
 bit-exact against the oracle's fp16 restatement (tests/test_oracle_f16.py pins
 it to numpy's IEEE binary16)."""
 import multiprocessing as mp
@@ -181,10 +182,24 @@ def _ipc_rank(rank, world, port, q, engine):
             comm.allreduce_f16(srcs, out=out, scale_exp=inccl.SCALE_AUTO if k == "auto" else k, stream=comm.stream)
             torch.cuda.synchronize()
             ok.append(bool(np.array_equal(_host(out), want)))
+            odd = torch.empty(n + 1, dtype=torch.float16, device=dev)[1:]   # 2-B aligned: the int32-allreduce path
+            torch.cuda.synchronize()
+            comm.allreduce_f16(srcs, out=odd, scale_exp=inccl.SCALE_AUTO if k == "auto" else k, stream=comm.stream)
+            torch.cuda.synchronize()
+            ok.append(bool(np.array_equal(_host(odd), want)))
             comm.allreduce_f16(srcs, out=srcs[0], scale_exp=inccl.SCALE_AUTO if k == "auto" else k,
                                stream=comm.stream)   # in place
             torch.cuda.synchronize()
             ok.append(bool(np.array_equal(_host(srcs[0]), want)))
+            if k != "auto":   # prepared (inccl_op_create_allreduce16), run twice on fresh inputs
+                srcs = [_dev(h, dev) for h in hs[rank]]
+                out.fill_(float("nan"))
+                op = comm.prepare_allreduce_f16(srcs, out=out, scale_exp=k, stream=comm.stream)
+                for _ in range(2):
+                    op()
+                    torch.cuda.synchronize()
+                    ok.append(bool(np.array_equal(_host(out), want)))
+                op.destroy()
         comm.destroy()
         grp.destroy()
         q.put((rank, ok, None))
