@@ -18,7 +18,7 @@ echo "bench ok"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-extras --json-out gpurun_out/bench_profiled.json > gpurun_out/prof.log 2>&1 || { echo prof failed; tail -20 gpurun_out/prof.log; exit 6; }
 grep -h k_stream gpurun_out/prof/run_kernel_stats.csv | cut -c1-200
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bf16 -o run --output-format csv -- python3 tools/kernel_probe.py --kernel bf16 --R 2 --mib 256 --iters 50 > gpurun_out/prof_bf16.log 2>&1 || { echo prof bf16 failed; tail -20 gpurun_out/prof_bf16.log; exit 6; }
-for k in fused quant_sum bf16; do
+for k in fused quant_sum bf16 f16; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${k}_$c -o pmc -- python3 tools/kernel_probe.py --kernel $k --R 2 --mib 256 --iters 5 > gpurun_out/pmc_${k}_$c.log 2>&1 || { echo "pmc $k $c failed"; tail gpurun_out/pmc_${k}_$c.log; exit 7; }
   done

@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--kernel", default="fused", choices=["fused", "quant_sum", "dequant", "sum_q32", "absmax", "quantise", "bf16"])
+    p.add_argument("--kernel", default="fused", choices=["fused", "quant_sum", "dequant", "sum_q32", "absmax", "quantise", "bf16", "f16"])
     p.add_argument("--R", type=int, default=2)
     p.add_argument("--mib", type=int, default=256)
     p.add_argument("--iters", type=int, default=20)
@@ -41,9 +41,11 @@ def main():
     qs = [torch.randint(-2 ** 26, 2 ** 26, (n,), device=dev, dtype=torch.int32) for _ in range(R)]
     outf = torch.empty(n, device=dev)
     outq = torch.empty(n, device=dev, dtype=torch.int32)
-    n16 = a.mib * (1 << 20) // 2   # bf16 buckets of the same size in bytes
-    hs = [torch.randn(n16, generator=g, device=dev).to(torch.bfloat16) for _ in range(R)] if a.kernel == "bf16" else []
-    outh = torch.empty(n16, device=dev, dtype=torch.bfloat16) if a.kernel == "bf16" else None
+    n16 = a.mib * (1 << 20) // 2   # bf16 / fp16 buckets of the same size in bytes
+    dt16 = torch.float16 if a.kernel == "f16" else torch.bfloat16
+    is16 = a.kernel in ("bf16", "f16")
+    hs = [torch.randn(n16, generator=g, device=dev).to(dt16) for _ in range(R)] if is16 else []
+    outh = torch.empty(n16, device=dev, dtype=dt16) if is16 else None
     st = torch.cuda.Stream(device=dev)
 
     def run(kind):
@@ -64,10 +66,12 @@ def main():
             inccl.absmax_word(xs, stream=s)
         elif kind == "bf16":
             inccl.reduce_bf16(hs, 25, out=outh, stream=s)
+        elif kind == "f16":
+            inccl.reduce_f16(hs, 25, out=outh, stream=s)
 
     def alg_bytes(kind):
         return {"fused": (R + 1) * 4 * n, "quant_sum": (R + 1) * 4 * n, "quantise": 8 * n, "dequant": 8 * n,
-                "sum_q32": (R + 1) * 4 * n, "absmax": R * 4 * n, "bf16": (R + 1) * 2 * n16}[kind]
+                "sum_q32": (R + 1) * 4 * n, "absmax": R * 4 * n, "bf16": (R + 1) * 2 * n16, "f16": (R + 1) * 2 * n16}[kind]
 
     def timeit(kind, iters):
         for _ in range(3):

@@ -19,7 +19,7 @@ import shutil
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # probe kind -> (traffic key's kernel name, substring of the mangled name, bytes per element)
 KERNELS = {"fused": ("k_stream_vec<F32,F32,R>", "k_stream_vec", 4), "quant_sum": ("k_stream_vec<F32,Q32,R>", "k_stream_vec", 4),
-           "bf16": ("k_stream16<BF16,BF16,R>", "k_stream16", 2)}
+           "bf16": ("k_stream16<BF16,BF16,R>", "k_stream16", 2), "f16": ("k_stream16<F16,F16,R>", "k_stream16", 2)}
 
 
 def mean_counter(path, needle):
