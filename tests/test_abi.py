@@ -194,3 +194,58 @@ def test_no_device_means_loud_failure(lib):
     g = inccl.inccl_group_create(1, 0, "127.0.0.1")
     assert g is None
     assert lib.inccl_last_error()
+
+
+def _prototypes():
+    """name -> (return type text, [parameter type texts]) for every function
+    declared in the public headers (comments stripped; prototypes may span lines)."""
+    protos = {}
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        text = re.sub(r"//[^\n]*", "", text)
+        for m in re.finditer(r"([A-Za-z_][\w \t\*]*?)\b(inccl_\w+)\s*\(([^;{]*?)\)\s*;", text, flags=re.S):
+            ret, name, params = m.group(1).strip(), m.group(2), " ".join(m.group(3).split())
+            plist = [] if params in ("", "void") else [p.strip() for p in params.split(",")]
+            protos[name] = (ret, plist)
+    return protos
+
+
+def _ctype_class(c_text):
+    """the ctypes class a C parameter / return type must be bound with"""
+    import ctypes
+    t = c_text.replace("const", " ").strip()
+    if "*" in t:
+        return "char*" if re.match(r"^char\s*\*\s*\w*$", t) else "ptr"
+    base = t.split()[-1] if t.split() else t
+    return {"int": ctypes.c_int, "int32_t": ctypes.c_int, "uint32_t": ctypes.c_uint32, "size_t": ctypes.c_size_t,
+            "uint64_t": ctypes.c_uint64, "int64_t": ctypes.c_int64, "float": ctypes.c_float, "void": None,
+            "unsigned": ctypes.c_uint, "long": ctypes.c_long}.get(base, base)
+
+
+def test_python_binding_matches_prototypes():
+    """Every binding in _lib.SIGNATURES has the header prototype's argument count
+    and, argument by argument, the same C type class (pointer, char*, int,
+    uint32_t, size_t, ...): a binding that drifted from its header would pass
+    arguments in the wrong registers on the GPU box."""
+    import ctypes
+    from container_inc_amd._lib import SIGNATURES
+    protos = _prototypes()
+    assert set(protos) == set(SIGNATURES)
+    ptr_ok = {ctypes.c_void_p, ctypes.c_char_p}
+    for name, (restype, argtypes) in SIGNATURES.items():
+        ret, params = protos[name]
+        assert len(argtypes) == len(params), (name, params, argtypes)
+        for i, (p, a) in enumerate(zip(params, argtypes)):
+            m = re.match(r"^(.*[\s\*])\w+$", p)   # drop the parameter's name
+            want = _ctype_class(m.group(1) if m else p)
+            if want == "ptr":
+                assert a in ptr_ok, (name, i, p, a)
+            elif want == "char*":
+                assert a in ptr_ok, (name, i, p, a)
+            else:
+                assert a is want, (name, i, p, a)
+        rwant = _ctype_class(ret)
+        if rwant in ("ptr", "char*"):
+            assert restype in ptr_ok, (name, ret, restype)
+        else:
+            assert restype is rwant, (name, ret, restype)
