@@ -68,6 +68,7 @@ SIGNATURES = {
     "inccl_comm_ipc_mem_kind": (_I, [_P, _S]),
     "inccl_comm_clear_error": (_I, [_P]),
     "inccl_comm_set_average": (_I, [_P, _I]),
+    "inccl_comm_set_nonfinite": (_I, [_P, _I]),
     "inccl_allreduce_f32": (_I, [_P, _P, _I, _P, _SZ, _I, _P]),
     "inccl_allreduce_f32_pipelined": (_I, [_P, _P, _I, _P, _SZ, _I, _I, _P]),
     "inccl_allreduce_bf16": (_I, [_P, _P, _I, _P, _SZ, _I, _P]),

@@ -655,6 +655,15 @@ int inccl_comm_set_average(struct inccl_communicator *comm, int on)
     return 0;
 }
 
+int inccl_comm_set_nonfinite(struct inccl_communicator *comm, int mode)
+{
+    if (!comm) return inccl_set_error(INCCL_ERR_ARG, "NULL communicator");
+    if (mode != INCCL_NONFINITE_SATURATE && mode != INCCL_NONFINITE_NAN)
+        return inccl_set_error(INCCL_ERR_ARG, "set_nonfinite: unknown mode %d", mode);
+    comm->nonfinite = mode;
+    return 0;
+}
+
 int inccl_comm_clear_error(struct inccl_communicator *comm)
 {
     if (!comm) return inccl_set_error(INCCL_ERR_ARG, "comm is NULL");
@@ -747,8 +756,9 @@ static int allreduce_piece(struct inccl_communicator *c, const float *const *src
 }
 
 /* The scale of one allreduce.  A fixed exponent passes through.  INCCL_SCALE_AUTO
- * takes the absmax of the local buckets (kind F32 or BF16) and its max over the
- * group.  On the IPC engines that max is agreed on the host anyway (the node's
+ * takes the absmax of the local buckets (kind F32, BF16 or F16) and its max over
+ * the group (with bit 31 set when a rank saw a NaN or +-Inf and the
+ * communicator propagates them, inccl_comm_set_nonfinite).  On the IPC engines that max is agreed on the host anyway (the node's
  * shared memory), so the host also picks the exponent (inccl_choose_scale, the
  * host twin of the kernels' choose_scale): *k_out, no device word, no copy
  * back.  Otherwise the max stays on the device (*amax_out) for the kernels to
@@ -763,9 +773,10 @@ static int resolve_scale(struct inccl_communicator *c, int kind, const void *con
             return inccl_set_error(INCCL_ERR_ARG, "scale_exp %d out of range", scale_exp);
         return 0;
     }
-    int rc = kind == INCCL_KIND_BF16  ? inccl_absmax_bf16((const uint16_t *const *)srcs, R, n, c->d_words, 1, st)
-             : kind == INCCL_KIND_F16 ? inccl_absmax_f16((const uint16_t *const *)srcs, R, n, c->d_words, 1, st)
-                                      : inccl_absmax_f32((const float *const *)srcs, R, n, c->d_words, 1, st);
+    const int zf = 1 | (c->nonfinite == INCCL_NONFINITE_NAN ? INCCL_ABSMAX_FLAG_NONFINITE : 0);
+    int rc = kind == INCCL_KIND_BF16  ? inccl_absmax_bf16((const uint16_t *const *)srcs, R, n, c->d_words, zf, st)
+             : kind == INCCL_KIND_F16 ? inccl_absmax_f16((const uint16_t *const *)srcs, R, n, c->d_words, zf, st)
+                                      : inccl_absmax_f32((const float *const *)srcs, R, n, c->d_words, zf, st);
     if (rc) return rc;
     const int W = c->group->world_size;
     if (W > 1 && c->group->transport == INCCL_TRANSPORT_RCCL &&
@@ -775,6 +786,13 @@ static int resolve_scale(struct inccl_communicator *c, int kind, const void *con
         INCCL_HIP(hipStreamSynchronize(st));
         rc = inccl_group_allreduce_max_u32(c->group, &v);
         if (rc) return rc;
+        if (v >> 31) {   /* a non-finite input somewhere (INCCL_NONFINITE_NAN): the kernels see the flag */
+            INCCL_HIP(hipMemcpyAsync(c->d_words, &v, sizeof(v), hipMemcpyHostToDevice, st));
+            INCCL_HIP(hipStreamSynchronize(st));
+            *amax_out = c->d_words;
+            *k_out = 0;
+            return 0;
+        }
         float amax;
         memcpy(&amax, &v, sizeof(amax));
         *k_out = inccl_choose_scale(amax, R * W);

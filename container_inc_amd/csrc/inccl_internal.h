@@ -83,6 +83,7 @@ struct inccl_communicator {
      * handles; each GPU pulls its shard from all peers over xGMI */
     int engine;                  /* INCCL_ENGINE_* */
     int out_shift;               /* log2(world) when results are averaged (inccl_comm_set_average), else 0 */
+    int nonfinite;               /* INCCL_NONFINITE_* (inccl_comm_set_nonfinite) */
     size_t p2p_cap;              /* elements per buffer */
     int32_t *p2p_part;           /* this rank's quantised partial sums (W * shard) */
     float *p2p_res;              /* this rank's dequantised shard lives at rank * shard */

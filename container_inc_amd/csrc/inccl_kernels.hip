@@ -105,33 +105,40 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
 
 // |x| bits of a float; NaN -> 0 (ignored, as orc_absmax_f32).  Non-negative
 // IEEE floats order like their bit patterns, so max over bits == max over values.
+// NF (INCCL_ABSMAX_FLAG_NONFINITE): a NaN or +-Inf instead sets bit 31, which
+// no |x| has, so the max over every element -- and over the ranks -- carries it
+// (deq_scale then makes every result NaN).
+template <bool NF = false>
 __device__ __forceinline__ uint32_t abs_bits(uint32_t b)
 {
     const uint32_t a = b & 0x7fffffffu;
-    return a > 0x7f800000u ? 0u : a;
+    if constexpr (NF) return a >= 0x7f800000u ? 0x80000000u | a : a;
+    else return a > 0x7f800000u ? 0u : a;
 }
 
 // absmax over 2-byte buckets (E: BF16 or F16), as the fp32 bits of the widened values
-__device__ __forceinline__ uint32_t abs_bits_bf16(uint32_t h) { return abs_bits(h << 16); }
-__device__ __forceinline__ uint32_t abs_bits_f16(uint32_t h) { return abs_bits(__float_as_uint(f16_widen(h))); }
-template <int E>
+template <bool NF>
+__device__ __forceinline__ uint32_t abs_bits_bf16(uint32_t h) { return abs_bits<NF>(h << 16); }
+template <bool NF>
+__device__ __forceinline__ uint32_t abs_bits_f16(uint32_t h) { return abs_bits<NF>(__float_as_uint(f16_widen(h))); }
+template <int E, bool NF>
 __device__ __forceinline__ uint32_t abs_bits16(uint32_t h)
 {
-    if constexpr (E == F16) return abs_bits_f16(h);
-    else return abs_bits_bf16(h);
+    if constexpr (E == F16) return abs_bits_f16<NF>(h);
+    else return abs_bits_bf16<NF>(h);
 }
 
 // element kind of k_absmax: F32, BF16 or F16
-template <int E>
+template <int E, bool NF>
 __device__ __forceinline__ uint32_t amax_quad(u32x4 x)
 {
     if constexpr (E != F32)
-        return max(max(max(abs_bits16<E>(x.x & 0xffffu), abs_bits16<E>(x.x >> 16)),
-                       max(abs_bits16<E>(x.y & 0xffffu), abs_bits16<E>(x.y >> 16))),
-                   max(max(abs_bits16<E>(x.z & 0xffffu), abs_bits16<E>(x.z >> 16)),
-                       max(abs_bits16<E>(x.w & 0xffffu), abs_bits16<E>(x.w >> 16))));
+        return max(max(max(abs_bits16<E, NF>(x.x & 0xffffu), abs_bits16<E, NF>(x.x >> 16)),
+                       max(abs_bits16<E, NF>(x.y & 0xffffu), abs_bits16<E, NF>(x.y >> 16))),
+                   max(max(abs_bits16<E, NF>(x.z & 0xffffu), abs_bits16<E, NF>(x.z >> 16)),
+                       max(abs_bits16<E, NF>(x.w & 0xffffu), abs_bits16<E, NF>(x.w >> 16))));
     else
-        return max(max(abs_bits(x.x), abs_bits(x.y)), max(abs_bits(x.z), abs_bits(x.w)));
+        return max(max(abs_bits<NF>(x.x), abs_bits<NF>(x.y)), max(abs_bits<NF>(x.z), abs_bits<NF>(x.w)));
 }
 
 // max |x| over R buckets of fp32 (E = F32), bf16 or fp16 elements.
@@ -141,7 +148,7 @@ __device__ __forceinline__ uint32_t amax_quad(u32x4 x)
 // CU -- 0.83-0.84 of HBM, against 0.73 for the round-1 form (256 x 1, 8 per CU).
 constexpr int kAmBlock = 512, kAmU = 2;
 
-template <int R, int E>
+template <int R, int E, bool NF>
 __global__ __launch_bounds__(kAmBlock) void k_absmax(SrcPtrs src, int64_t n, uint32_t* __restrict__ out, int vec)
 {
     constexpr bool B16 = E != F32;
@@ -164,7 +171,7 @@ __global__ __launch_bounds__(kAmBlock) void k_absmax(SrcPtrs src, int64_t n, uin
         for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int u = 0; u < kAmU; ++u) {
-                const uint32_t a = amax_quad<E>(v[r][u]);
+                const uint32_t a = amax_quad<E, NF>(v[r][u]);
                 m = m > a ? m : a;
             }
     }
@@ -172,8 +179,8 @@ __global__ __launch_bounds__(kAmBlock) void k_absmax(SrcPtrs src, int64_t n, uin
 #pragma unroll
     for (int r = 0; r < R; ++r)
         for (int64_t i = nq * EPQ + (int64_t)blockIdx.x * kAmBlock + threadIdx.x; i < n; i += stride) {
-            const uint32_t a = B16 ? abs_bits16<E>(reinterpret_cast<const uint16_t*>(src.p[r])[i])
-                                   : abs_bits(reinterpret_cast<const uint32_t*>(src.p[r])[i]);
+            const uint32_t a = B16 ? abs_bits16<E, NF>(reinterpret_cast<const uint16_t*>(src.p[r])[i])
+                                   : abs_bits<NF>(reinterpret_cast<const uint32_t*>(src.p[r])[i]);
             m = m > a ? m : a;
         }
     m = wave_max_u32(m);
@@ -389,10 +396,12 @@ int launch_absmax(const void* const* srcs, int R, size_t n, uint32_t* amax_bits_
         s.p[r] = srcs[r];
         vec = vec && aligned16(srcs[r]);
     }
-    if (zero_first) {
+    if (zero_first & ~(1 | INCCL_ABSMAX_FLAG_NONFINITE)) return INCCL_ERR_ARG;
+    if (zero_first & 1) {
         hipError_t e = hipMemsetAsync(amax_bits_dev, 0, sizeof(uint32_t), st);
         if (e != hipSuccess) return (int)e;
     }
+    const bool nf = (zero_first & INCCL_ABSMAX_FLAG_NONFINITE) != 0;
     if (n == 0) return 0;
     const int64_t tiles = ((int64_t)(n / (B16 ? 8 : 4)) + (int64_t)kAmBlock * kAmU - 1) / ((int64_t)kAmBlock * kAmU);
     const int64_t cap = (int64_t)num_cus() * 2;
@@ -400,7 +409,12 @@ int launch_absmax(const void* const* srcs, int R, size_t n, uint32_t* amax_bits_
     switch (R) {
 #define INCCL_AM(RR)                                                                                             \
     case RR:                                                                                                     \
-        hipLaunchKernelGGL((k_absmax<RR, E>), dim3(grid), dim3(kAmBlock), 0, st, s, (int64_t)n, amax_bits_dev, vec); \
+        if (nf)                                                                                                  \
+            hipLaunchKernelGGL((k_absmax<RR, E, true>), dim3(grid), dim3(kAmBlock), 0, st, s, (int64_t)n,         \
+                               amax_bits_dev, vec);                                                              \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_absmax<RR, E, false>), dim3(grid), dim3(kAmBlock), 0, st, s, (int64_t)n,        \
+                               amax_bits_dev, vec);                                                              \
         break;
         INCCL_AM(1) INCCL_AM(2) INCCL_AM(3) INCCL_AM(4) INCCL_AM(5) INCCL_AM(6) INCCL_AM(7) INCCL_AM(8)
 #undef INCCL_AM

@@ -50,7 +50,15 @@ __device__ __forceinline__ int choose_scale(float amax, int R)
     return k;
 }
 
-__device__ __forceinline__ float deq_scale(const Scale& s, int k) { return pow2f(-k - s.out_shift); }
+// the dequantise multiplier 2^-(k + out_shift); NaN when the auto scale's word
+// carries bit 31 (INCCL_ABSMAX_FLAG_NONFINITE: some input of some rank was NaN
+// or +-Inf), so that every result of the call is NaN
+__device__ __forceinline__ float deq_scale(const Scale& s, int k)
+{
+    const float inv = pow2f(-k - s.out_shift);
+    if (s.amax_bits != nullptr && (__builtin_nontemporal_load(s.amax_bits) >> 31)) return __builtin_nanf("");
+    return inv;
+}
 
 __device__ __forceinline__ int resolve_k(const Scale& s)
 {

@@ -13,7 +13,12 @@ the bucket averaged over the ranks, as DDP's built-in allreduce hook does.
 Numerics: the scale defaults to ``SCALE_AUTO`` -- the bucket's absmax over every
 rank picks the largest exponent whose int32 sum cannot overflow
 (``orc_choose_scale``), so a bucket of any magnitude keeps ~30 significant bits
-of its largest element.  The averaged result is bit-identical to the oracle's
+of its largest element.  Non-finite gradients: the hook switches its
+communicator to ``set_nonfinite(True)``, so a NaN or +-Inf in any rank's bucket
+makes the whole averaged bucket NaN on every rank -- a mixed-precision loss
+scaler (``torch.amp.GradScaler``) then sees the overflow and skips the step, as
+it would after a float allreduce.  (The quantiser alone would map NaN to 0 and
+saturate +-Inf: a finite, wrong gradient.)  The averaged result is bit-identical to the oracle's
 ``reduce_f32`` of the same buckets divided by the world size.
 
 fp32, bf16 and fp16 CUDA buckets are accepted (bf16 / fp16 through
@@ -43,6 +48,8 @@ class HookState:
     average: bool = True
     calls: int = 0
     folded: bool | None = None   # the mean comes out of the dequantise stage (inccl_comm_set_average)
+    propagate_nonfinite: bool = True   # NaN / +-Inf anywhere -> the bucket is NaN (inccl_comm_set_nonfinite)
+    _nonfinite_set: bool = False
 
     def fold_average(self) -> bool:
         """Once: let the engine return the mean (power-of-two worlds: 2^-log2 W is
@@ -58,6 +65,13 @@ class HookState:
                 except IncclError:
                     pass
         return self.folded
+
+    def apply_nonfinite(self) -> None:
+        """Once: the communicator's non-finite mode (auto scale only)."""
+        if not self._nonfinite_set:
+            self._nonfinite_set = True
+            if hasattr(self.comm, "set_nonfinite"):
+                self.comm.set_nonfinite(self.propagate_nonfinite)
 
     @property
     def world_size(self) -> int:
@@ -80,6 +94,7 @@ def allreduce_hook(state: HookState, bucket):
     if name is None:
         raise IncclError(f"inccl DDP hook: fp32, bf16 or fp16 gradient buckets only, got {buf.dtype}")
     reduce = getattr(state.comm, name)
+    state.apply_nonfinite()
     w = state.world_size
     divide = state.average and w > 1 and not state.fold_average()
     if not buf.is_cuda:   # reaches the communicator, which refuses it ("must live on the GPU")

@@ -23,6 +23,8 @@ from ._lib import IncclError, check, load
 KIND_F32, KIND_Q32, KIND_Q32BE, KIND_BF16, KIND_F16 = 0, 1, 2, 3, 4
 SCALE_MIN, SCALE_MAX, SCALE_AUTO = -64, 64, 0x7FFFFFFF
 MAX_LOCAL_INPUTS = 8
+ABSMAX_FLAG_NONFINITE = 2        # inccl_amd.h INCCL_ABSMAX_FLAG_NONFINITE
+NONFINITE_SATURATE, NONFINITE_NAN = 0, 1
 PAYLOAD_LEN = 1024           # util.h:85
 MESSAGE_SIZE = 4 * PAYLOAD_LEN   # api.h:39
 PAYLOAD_COUNT = MESSAGE_SIZE // 4  # api.h:40
@@ -237,6 +239,21 @@ def absmax_word(srcs, word=None, stream=None):
     return word
 
 
+def absmax_bits(srcs, nonfinite_flag: bool = False, stream=None) -> int:
+    """The raw absmax word (fp32 bits of max |x|) of fp32 / bf16 / fp16 buckets;
+    nonfinite_flag: INCCL_ABSMAX_FLAG_NONFINITE (a NaN or +-Inf sets bit 31)."""
+    torch = _torch()
+    n = srcs[0].numel()
+    fn, dt = {torch.float32: ("inccl_absmax_f32", torch.float32), torch.bfloat16: ("inccl_absmax_bf16", torch.bfloat16),
+              torch.float16: ("inccl_absmax_f16", torch.float16)}[srcs[0].dtype]
+    ptrs = [_dev_ptr(s, dt, f"srcs[{i}]", n) for i, s in enumerate(srcs)]
+    word = torch.zeros(4, dtype=torch.int32, device=srcs[0].device)
+    rc = getattr(load(), fn)(_ptr_array(ptrs), len(ptrs), n, _dev_ptr(word, torch.int32, "word", 1),
+                             1 | (ABSMAX_FLAG_NONFINITE if nonfinite_flag else 0), _stream_handle(stream))
+    check(rc, fn)
+    return int(word[0].item()) & 0xFFFFFFFF
+
+
 def absmax(srcs, stream=None) -> float:
     w = absmax_word(srcs, stream=stream)
     bits = int(w[0].item()) & 0xFFFFFFFF
@@ -350,6 +367,13 @@ class Communicator:
         """Results of allreduce_f32 / _bf16 become the mean over ranks (power-of-two
         worlds; raises IncclError otherwise).  Bit-identical to sum / W."""
         check(load().inccl_comm_set_average(self.handle, 1 if on else 0), "inccl_comm_set_average")
+
+    def set_nonfinite(self, propagate: bool = True) -> None:
+        """propagate=True (INCCL_NONFINITE_NAN): a NaN or +-Inf in any rank's
+        buckets makes every element of an auto-scaled allreduce's result NaN, as a
+        loss scaler needs to see; False restores the quantiser's spec (NaN -> 0,
+        +-Inf saturates).  Set it alike on every rank."""
+        check(load().inccl_comm_set_nonfinite(self.handle, 1 if propagate else 0), "inccl_comm_set_nonfinite")
 
     # -- reference collectives on host int32 arrays (api.c:330-452) --
     def allreduce_write(self, src: np.ndarray, length: int, dst: np.ndarray) -> None:

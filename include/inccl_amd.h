@@ -102,7 +102,12 @@ struct inccl_op *inccl_op_create(int in_kind, int out_kind, const void *const *s
 int inccl_op_run(struct inccl_op *op);
 int inccl_op_destroy(struct inccl_op *op);
 /* max |x| over R buckets into *amax_bits_dev (float bits; NaN ignored).  The word
- * is zeroed first when zero_first != 0, else max-accumulated. */
+ * is zeroed first when bit 0 of zero_first is set, else max-accumulated.  With
+ * INCCL_ABSMAX_FLAG_NONFINITE also set in zero_first, a NaN or +-Inf element sets
+ * bit 31 of the word instead (which no |x| has, so a max over words and ranks
+ * keeps it); a kernel handed such a word as its auto scale dequantises every
+ * element to NaN (inccl_comm_set_nonfinite). */
+#define INCCL_ABSMAX_FLAG_NONFINITE 2
 int inccl_absmax_f32(const float *const *srcs_dev, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
                      void *stream);
 /* Position-weighted linear checksum sum_i (2(base+i)+1)*q[i] mod 2^32 into *out_dev. */
@@ -202,6 +207,17 @@ int inccl_comm_clear_error(struct inccl_communicator *comm);
  * dividing the sum by W, without the extra pass over the bucket.  Only for a
  * power-of-two world size (else INCCL_ERR_ARG).  Set it alike on every rank. */
 int inccl_comm_set_average(struct inccl_communicator *comm, int on);
+/* What a NaN or +-Inf input does to an INCCL_SCALE_AUTO allreduce of this
+ * communicator.  INCCL_NONFINITE_SATURATE (the default, the quantiser's spec):
+ * NaN quantises to 0 and +-Inf saturates, so the result stays finite.
+ * INCCL_NONFINITE_NAN: if any element of any rank's buckets is NaN or +-Inf,
+ * every element of the result is NaN on every rank -- what a mixed-precision
+ * loss scaler needs to see to skip the step -- at no extra pass (the flag rides
+ * in the auto scale's max word).  A fixed scale exponent is unaffected.  Set it
+ * alike on every rank. */
+#define INCCL_NONFINITE_SATURATE 0
+#define INCCL_NONFINITE_NAN 1
+int inccl_comm_set_nonfinite(struct inccl_communicator *comm, int mode);
 
 /* Device-resident fp32 allreduce of R local buckets per rank:
  *   dst = dequant( sum over ranks, sum over r<R  quant(srcs[r]) )

@@ -246,6 +246,34 @@ def absmax_f16(srcs) -> float:
     return float(lib().orc_absmax_f16(_ptr_array(srcs), len(srcs), srcs[0].size))
 
 
+# ---- non-finite inputs under INCCL_NONFINITE_NAN (this library's own spec,
+# include/inccl_amd.h inccl_comm_set_nonfinite / INCCL_ABSMAX_FLAG_NONFINITE;
+# the reference has no floats) ----
+def widened_bits(src, kind: str = "f32") -> np.ndarray:
+    """fp32 bit patterns of an fp32 / bf16 / fp16 bucket's elements, widened exactly"""
+    if kind == "f32":
+        return np.ascontiguousarray(src, dtype=np.float32).view(np.uint32).ravel()
+    if kind == "bf16":
+        return np.ascontiguousarray(src, dtype=np.uint16).astype(np.uint32).ravel() << 16
+    return f16_to_f32(src).view(np.uint32)
+
+
+def absmax_word_flagged(srcs, kind: str = "f32") -> int:
+    """The absmax word with INCCL_ABSMAX_FLAG_NONFINITE: max over |x| bits, where a
+    NaN or +-Inf element counts as bit 31 | its |x| bits"""
+    m = 0
+    for s in srcs:
+        a = widened_bits(s, kind) & np.uint32(0x7FFFFFFF)
+        w = np.where(a >= np.uint32(0x7F800000), a | np.uint32(0x80000000), a)
+        if w.size:
+            m = max(m, int(w.max()))
+    return m
+
+
+def any_nonfinite(srcs, kind: str = "f32") -> bool:
+    return bool(absmax_word_flagged(srcs, kind) >> 31)
+
+
 def choose_scale(amax: float, R: int) -> int:
     return int(lib().orc_choose_scale(ctypes.c_float(amax), int(R)))
 

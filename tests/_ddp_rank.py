@@ -29,6 +29,11 @@ class GlooStandIn:
 
     def __init__(self, world):
         self.group = types.SimpleNamespace(world_size=world)
+        self.nonfinite = False
+
+    def set_nonfinite(self, propagate=True):
+        """inccl_comm_set_nonfinite: under auto scale, a NaN / +-Inf anywhere makes the result NaN"""
+        self.nonfinite = bool(propagate)
 
     def allreduce_f32(self, srcs, out=None, scale_exp=25, chunks=1, stream=None):
         import torch
@@ -39,6 +44,8 @@ class GlooStandIn:
         got = [torch.empty_like(srcs[0]) for _ in range(W)]
         dist.all_gather(got, srcs[0].contiguous())
         every = [g.numpy() for g in got]
+        if self.nonfinite and scale_exp == inccl.SCALE_AUTO and O.any_nonfinite(every, "f32"):
+            return out.fill_(float("nan"))
         k = O.choose_scale(O.absmax(every), W) if scale_exp == inccl.SCALE_AUTO else scale_exp
         out.copy_(torch.from_numpy(O.reduce_f32(every, k)))
         return out
@@ -53,6 +60,10 @@ class GlooStandIn:
         got = [torch.empty_like(mine) for _ in range(W)]
         dist.all_gather(got, mine)
         every = [g.numpy().astype(np.uint16) for g in got]
+        kind = "f16" if dtype == torch.float16 else "bf16"
+        from oracle import oracle as O
+        if self.nonfinite and scale_exp == inccl.SCALE_AUTO and O.any_nonfinite(every, kind):
+            return out.fill_(float("nan"))
         k = O_choose(absmax(every), W) if scale_exp == inccl.SCALE_AUTO else scale_exp
         out.copy_(torch.from_numpy(reduce(every, k).view(np.int16)).view(dtype))
         return out
@@ -81,9 +92,15 @@ def _bits(t):
     return t.detach().cpu().numpy().view(np.uint32)
 
 
-def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine="p2p", boot_port=None):
+def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine="p2p", boot_port=None,
+        poison=None):
     """dtype "bf16" / "f16": a bf16 / fp16 model, so DDP's buckets are bf16 / fp16
     (inccl_allreduce_bf16 / _f16);
+    poison "propagate" / "saturate": one iteration whose last rank has an infinite
+    target (every local gradient of that rank non-finite), with the hook's
+    communicator propagating non-finite inputs or not; the report then holds
+    ``found_inf`` (a loss scaler's check on this rank's averaged .grad) and
+    ``all_nan``;
     as_view: gradient_as_bucket_view=True (the grads are views of the buckets);
     boot_port: the library bootstrap's port, chosen free by the parent (gloo uses `port`)."""
     try:
@@ -120,7 +137,7 @@ def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine=
         local = copy.deepcopy(model)   # non-DDP twin: this rank's own gradients
         net = DDP(model, device_ids=[0] if mode == "gpu" else None, bucket_cap_mb=0.25,
                   gradient_as_bucket_view=as_view)
-        state = ddp.HookState(comm=comm)
+        state = ddp.HookState(comm=comm, propagate_nonfinite=poison != "saturate")
         seen = []
 
         def hook(st, bucket):
@@ -134,6 +151,25 @@ def run(rank, world, port, q, mode, iters=2, dtype="f32", as_view=False, engine=
         opt_local = torch.optim.SGD(local.parameters(), lr=0.05)
         report = {"buckets": [], "bit_exact": True, "grad_err": 0.0}
         gen = torch.Generator().manual_seed(100 + rank)
+        if poison:
+            x = torch.randn(64, 96, generator=gen).to(dev, wdt)
+            y = torch.randn(64, 10, generator=gen).to(dev, wdt)
+            if rank == world - 1:
+                y[0, 0] = float("inf")
+            opt.zero_grad()
+            torch.nn.functional.mse_loss(net(x), y).backward()
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            grads = [p.grad.detach().float() for p in net.module.parameters()]
+            report["found_inf"] = bool(any(not torch.isfinite(g).all() for g in grads))
+            report["all_nan"] = bool(all(torch.isnan(g).all() for g in grads))
+            report["calls"] = state.calls
+            q.put((rank, report))
+            if mode == "gpu":
+                comm.destroy()
+                grp.destroy()
+            dist.destroy_process_group()
+            return
         for it in range(iters):
             x = torch.randn(64, 96, generator=gen).to(dev, wdt)
             y = (torch.randn(64, 10, generator=gen) * (10.0 ** it)).to(dev, wdt)   # later iterations: larger grads

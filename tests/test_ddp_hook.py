@@ -24,12 +24,13 @@ def _free_ports(n):
     return ports
 
 
-def run_world(world, mode, timeout, dtype="f32", as_view=False, engine="p2p"):
+def run_world(world, mode, timeout, dtype="f32", as_view=False, engine="p2p", poison=None):
     import _ddp_rank
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port, boot_port = _free_ports(2)
-    ps = [ctx.Process(target=_ddp_rank.run, args=(r, world, port, q, mode, 2, dtype, as_view, engine, boot_port))
+    ps = [ctx.Process(target=_ddp_rank.run, args=(r, world, port, q, mode, 2, dtype, as_view, engine, boot_port,
+                                                  poison))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -51,6 +52,25 @@ def test_ddp_hook_plumbing_gloo(orc, world, dtype, as_view):
         assert rep["calls"] == sum(rep["buckets"])
         assert rep["bit_exact"], rep
         assert rep["grad_err"] <= 1.0, rep
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+def test_ddp_hook_nonfinite_gloo(orc, dtype):
+    """One rank's gradients overflow.  The hook propagates it: every rank's
+    averaged gradients are all NaN, so a loss scaler skips the step on every
+    rank alike.  Without propagation (the quantiser's spec) an fp32 bucket's
+    other rank sees finite gradients -- the divergence the default prevents.
+    (An fp16 bucket's saturated sum overflows fp16 on narrowing, so there the
+    spec happens to yield Inf too.)"""
+    res = run_world(2, "cpu", 300, dtype, poison="propagate")
+    for r, rep in res.items():
+        assert "error" not in rep, rep.get("tb")
+        assert rep["found_inf"] and rep["all_nan"], (r, rep)
+    if dtype != "f32":
+        return
+    res = run_world(2, "cpu", 300, dtype, poison="saturate")
+    assert "error" not in res[0], res[0].get("tb")
+    assert not res[0]["found_inf"], res[0]
 
 
 def test_ddp_hook_refuses_other_formats():

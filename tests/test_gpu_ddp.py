@@ -23,3 +23,13 @@ def test_ddp_hook_gpu(gpu, orc, world, dtype, as_view, engine):
         assert rep["calls"] == sum(rep["buckets"])
         assert rep["bit_exact"], rep
         assert rep["grad_err"] <= 1.0, rep
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_ddp_hook_gpu_nonfinite(gpu, orc, dtype):
+    """The real library: one rank's overflow makes every rank's averaged
+    gradients NaN (inccl_comm_set_nonfinite through the hook), p2p engine."""
+    res = run_world(2, "gpu", 240, dtype, poison="propagate")
+    for r, rep in res.items():
+        assert "error" not in rep, rep.get("tb")
+        assert rep["found_inf"] and rep["all_nan"], (r, rep)

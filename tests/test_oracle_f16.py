@@ -67,3 +67,19 @@ def test_f16_known_answers(orc):
     # a sum that dequantises below the smallest subnormal: 3 * 2^-26 = 0.75 * 2^-24 rounds up to it
     q = np.array([3], np.int32)
     assert int(orc.sum_dequant_f16([q], 26)[0]) == 0x0001
+
+
+def test_absmax_word_flagged(orc):
+    """The INCCL_ABSMAX_FLAG_NONFINITE word's restatement: finite buckets give
+    the plain absmax bits; an Inf gives bit 31 | 0x7f800000; a NaN sets bit 31."""
+    import numpy as np
+    x = np.array([1.5, -3.25, 0.0], np.float32)
+    assert orc.absmax_word_flagged([x]) == int(np.float32(3.25).view(np.uint32))
+    assert orc.absmax_word_flagged([x, np.array([np.inf], np.float32)]) == 0x80000000 | 0x7F800000
+    assert orc.absmax_word_flagged([np.array([np.nan, 1.0], np.float32)]) >> 31 == 1
+    h = np.array([1.0, -2.0], np.float16).view(np.uint16)
+    assert orc.absmax_word_flagged([h], "f16") == int(np.float32(2.0).view(np.uint32))
+    assert orc.any_nonfinite([np.array([np.inf], np.float16).view(np.uint16)], "f16")
+    b = np.array([0x3F80, 0xFF80], np.uint16)   # bf16 1.0, -Inf
+    assert orc.absmax_word_flagged([b], "bf16") == 0x80000000 | 0x7F800000
+    assert not orc.any_nonfinite([np.array([0x3F80], np.uint16)], "bf16")
