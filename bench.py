@@ -47,7 +47,8 @@ Extra JSON fields:
   host_e2e          N = 1: BASELINE config 3, 1 GiB pinned host fp32 in 64 MiB buckets
   api_allreduce_write N = 1: the reference's entry point on a 256 MiB host int32
                     message, registered and unregistered
-  f16               N = 1: the same for IEEE float16 buckets (k_stream16<F16,F16,R>)
+  f16               N = 1: the same for IEEE float16 buckets (k_stream16<F16,F16,R>);
+                    N > 1: inccl_allreduce_f16 on the same engines as bf16, verified
   bf16              N = 1: R bf16 buckets of 256 MiB (k_stream16), repeated and rotated;
                     N > 1: inccl_allreduce_bf16 on the rccl, p2p, mesh and meshw engines, verified
   sweep             N > 1: 4 KiB .. 256 MiB and 1 GiB per engine, verified with
@@ -240,10 +241,11 @@ def oracle_lanes(n: int, world: int, chunks: int, target: int) -> "list[int]":
     return sorted(lanes)
 
 
-def oracle_check(srcs, out, lanes, k: int, rank: int, world: int, bf16: bool = False) -> dict:
+def oracle_check(srcs, out, lanes, k: int, rank: int, world: int, fmt: str = "f32") -> dict:
     """The C oracle as the checker of an N-rank result (outside any timed
     region): every rank's R inputs and its output at `lanes` are gathered to
-    rank 0 over gloo; rank 0 runs orc_reduce_f32 (orc_reduce_bf16) on all W*R
+    rank 0 over gloo; rank 0 runs orc_reduce_f32 (orc_reduce_bf16 / _f16 for
+    fmt "bf16" / "f16") on all W*R
     inputs -- the reference's sum over every child, non_termination_switch.c:361-372,
     behind the quantiser -- and compares every rank's output bit for bit."""
     import numpy as np
@@ -252,21 +254,23 @@ def oracle_check(srcs, out, lanes, k: int, rank: int, world: int, bf16: bool = F
     idx = torch.as_tensor(lanes, dtype=torch.int64, device=out.device)
     rows = [s.index_select(0, idx) for s in srcs] + [out.index_select(0, idx)]
     mine = torch.stack(rows).cpu()
-    # gloo gathers no 16-bit integers: bf16 bit patterns travel widened to int32
-    mine = mine.view(torch.int16).to(torch.int32) if bf16 else mine.view(torch.int32)
+    # gloo gathers no 16-bit integers: 16-bit patterns travel widened to int32
+    b16 = fmt != "f32"
+    mine = mine.view(torch.int16).to(torch.int32) if b16 else mine.view(torch.int32)
     if world > 1:
         bucket = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
         dist.gather(mine, gather_list=bucket, dst=0)
     else:
         bucket = [mine]
     res = {"lanes": len(lanes), "ranks": world, "mismatches": None,
-           "checker": "oracle/inccl_oracle.c " + ("orc_reduce_bf16" if bf16 else "orc_reduce_f32")}
+           "checker": "oracle/inccl_oracle.c orc_reduce_" + fmt}
     if rank == 0:
         from oracle import oracle as O
         R = len(srcs)
         arr = [b.numpy() for b in bucket]
-        if bf16:
-            want = O.reduce_bf16([a[j].astype(np.uint16) for a in arr for j in range(R)], k).view(np.uint16)
+        if b16:
+            red = O.reduce_bf16 if fmt == "bf16" else O.reduce_f16
+            want = red([a[j].astype(np.uint16) for a in arr for j in range(R)], k).view(np.uint16)
             got = [a[R].astype(np.uint16) for a in arr]
         else:
             want = O.reduce_f32([a[j].view(np.float32) for a in arr for j in range(R)], k).view(np.uint32)
@@ -624,52 +628,54 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: 
     return rows
 
 
-def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256) -> list:
-    """N > 1: R resident `mib` MiB bf16 buckets per rank through inccl_allreduce_bf16
-    on the engines with a bf16 result exchange (rccl: ncclAllGather of bf16; p2p:
-    bf16 result shards gathered; mesh / meshw: bf16 result chunks), each verified
+def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256, fmt: str = "bf16") -> list:
+    """N > 1: R resident `mib` MiB bf16 (fmt "f16": IEEE fp16) buckets per rank
+    through inccl_allreduce_bf16 / _f16 on the engines with a 2-byte result
+    exchange (rccl: ncclAllGather of 2-byte words; p2p: 2-byte result shards
+    gathered; mesh / meshw: 2-byte result chunks), each verified
     bit-identical to the first engine that passes on every rank over two
     alternating input sets; wall time per call, max over ranks, and the xGMI link
     fraction of its (W-1)/W * n * (4 + 2) bytes."""
     import torch
     import torch.distributed as dist
 
-    from container_inc_amd import inccl
     n = mib * (1 << 20) // 2
+    dtype = torch.float16 if fmt == "f16" else torch.bfloat16
+    allreduce = comm.allreduce_f16 if fmt == "f16" else comm.allreduce_bf16
     inputs = []
     for seed in (9000, 9500):
         gen = torch.Generator(device=dev)
         gen.manual_seed(seed + rank)
-        inputs.append([torch.randn(n, generator=gen, device=dev).to(torch.bfloat16) for _ in range(R)])
-    out = torch.empty(n, device=dev, dtype=torch.bfloat16)
+        inputs.append([torch.randn(n, generator=gen, device=dev).to(dtype) for _ in range(R)])
+    out = torch.empty(n, device=dev, dtype=dtype)
     st = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize()
     rows, refs = [], None
     lanes = oracle_lanes(n, world, 1, 1 << 16)
     for eng in ("rccl", "p2p", "mesh", "meshw"):
-        set_stage(f"bf16 {mib} MiB engine {eng}")
+        set_stage(f"{fmt} {mib} MiB engine {eng}")
         ok, dt, same = 1, float("inf"), False
         try:
             comm.set_engine(eng)
             got = []
             for xs in (inputs[0], inputs[1], inputs[0]):
-                comm.allreduce_bf16(xs, out=out, scale_exp=25, stream=st.cuda_stream)
+                allreduce(xs, out=out, scale_exp=25, stream=st.cuda_stream)
                 torch.cuda.synchronize()
                 got.append(out.clone())
                 torch.cuda.synchronize()
             same = (torch.equal(got[0], got[2]) if refs is None
                     else all(torch.equal(g, refs[i % 2]) for i, g in enumerate(got)))
             for _ in range(5):
-                comm.allreduce_bf16(inputs[0], out=out, scale_exp=25, stream=st.cuda_stream)
+                allreduce(inputs[0], out=out, scale_exp=25, stream=st.cuda_stream)
             torch.cuda.synchronize()
             dist.barrier()
             t0 = time.perf_counter()
             for _ in range(10):
-                comm.allreduce_bf16(inputs[0], out=out, scale_exp=25, stream=st.cuda_stream)
+                allreduce(inputs[0], out=out, scale_exp=25, stream=st.cuda_stream)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / 10
         except Exception as e:  # noqa: BLE001
-            print(f"rank {rank}: bf16 engine {eng} failed: {e}", file=sys.stderr, flush=True)
+            print(f"rank {rank}: {fmt} engine {eng} failed: {e}", file=sys.stderr, flush=True)
             ok, got = 0, None
         v = agree([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0], world)
         good, ident = v[1] == 0.0, v[2] == 0.0
@@ -678,7 +684,7 @@ def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256) -> li
         row = {"engine": eng, "bucket_mib": mib, "R": R, "ok": good, "bit_identical": good and ident,
                "ms": round(v[0] * 1e3, 4) if good else None}
         if good:
-            row["parity_vs_oracle"] = oracle_check(inputs[0], got[0], lanes, 25, rank, world, bf16=True)
+            row["parity_vs_oracle"] = oracle_check(inputs[0], got[0], lanes, 25, rank, world, fmt=fmt)
             link = (world - 1) * n * 6 // world
             row["GBps_buckets"] = round(world * R * 2 * n / v[0] / 1e9, 1)
             row["xgmi_frac"] = round(link / v[0] / 1e9 / ((world - 1) * XGMI_LINK_GBS_BIDIR), 4)
@@ -1625,6 +1631,15 @@ def main():
                     res["bf16"] = {"error": repr(e)}
             else:
                 res["bf16"] = {"skipped": f"run past {sweep_soft:.0f} s from process start"}
+        with Phase("f16"):
+            if agree([time.monotonic() - T_START], world)[0] <= sweep_soft:
+                try:
+                    res["f16"] = bf16_engines(comm, dev, R, rank, world, fmt="f16")
+                except Exception as e:  # noqa: BLE001
+                    print(f"rank {rank}: f16 key failed: {e!r}", file=sys.stderr, flush=True)
+                    res["f16"] = {"error": repr(e)}
+            else:
+                res["f16"] = {"skipped": f"run past {sweep_soft:.0f} s from process start"}
         comm.set_engine(chosen[0])
         # north_star: the path starts and ends in host memory -- the end-to-end
         # rate with pinned H2D / D2H, at this N too
