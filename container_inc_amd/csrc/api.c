@@ -1022,6 +1022,78 @@ int inccl_allreduce_f16(struct inccl_communicator *c, const uint16_t *const *src
     return allreduce_16(c, INCCL_KIND_F16, srcs_dev, R, dst_dev, n, scale_exp, stream);
 }
 
+/* Reduce-scatter (include/inccl_amd.h): the allreduce's arithmetic, rank `me`
+ * keeping shard me of the result.  kind F32, BF16 or F16. */
+static int reduce_scatter_any(struct inccl_communicator *c, int kind, const void *const *srcs, int R, void *dst,
+                              size_t n, int scale_exp, void *stream)
+{
+    static const char *const names[] = {"f32", "", "", "bf16", "f16"};
+    if (!c || !srcs || R < 1 || R > INCCL_MAX_LOCAL_INPUTS || (!dst && n))
+        return inccl_set_error(INCCL_ERR_ARG, "bad reduce_scatter_%s args", names[kind]);
+    for (int r = 0; r < R; ++r)
+        if (!srcs[r] && n) return inccl_set_error(INCCL_ERR_ARG, "srcs[%d] is NULL", r);
+    const int W = c->group->world_size, me = c->group->rank;
+    if (n % (size_t)W)
+        return inccl_set_error(INCCL_ERR_ARG, "reduce_scatter_%s: %zu elements do not split into %d shards",
+                               names[kind], n, W);
+    if (n == 0) return 0;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const size_t shard = n / (size_t)W;
+    const uint32_t *amax = NULL;
+    int k = 0;
+    int rc = resolve_scale(c, kind, srcs, R, n, scale_exp, st, &amax, &k);
+    if (rc) return rc;
+    const int scale_R = R * W;
+    const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: the reduce-scatter path even at world 1 */
+    if (W == 1 && !(fs && atoi(fs) != 0))   /* one fused HBM pass */
+        return kerr(inccl_k_stream_s(kind, kind, srcs, R, dst, n, k, amax, scale_R, c->out_shift, st));
+    if (c->engine == INCCL_ENGINE_RCCL || c->group->transport == INCCL_TRANSPORT_LOCAL) {
+        /* quant + local sum -> int32 reduce-scatter -> dequantise the shard */
+        rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, (n + shard) * sizeof(int32_t));
+        if (rc) return rc;
+        int32_t *qsend = (int32_t *)c->d_q32, *qrecv = qsend + n;
+        rc = kerr(inccl_k_stream(kind, INCCL_KIND_Q32, srcs, R, qsend, n, k, amax, scale_R, st));
+        if (rc) return rc;
+        rc = inccl_tp_reduce_scatter_q32(c, qsend, qrecv, shard, st);
+        if (rc) return rc;
+        const void *s1[1] = {qrecv};
+        return kerr(inccl_k_stream_s(INCCL_KIND_Q32, kind, s1, 1, dst, shard, k, amax, scale_R, c->out_shift, st));
+    }
+    const int ipc = c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH;
+    if (ipc && c->group->transport == INCCL_TRANSPORT_RCCL && !(shard & 3) &&
+        ((uintptr_t)dst & (kind == INCCL_KIND_F32 ? 15u : 7u)) == 0)
+        return inccl_p2p_reduce_scatter(c, kind, srcs, R, dst, n, k, amax, scale_R, st);
+    /* every other engine, or a shard the pull-reduce cannot take: the engine's
+     * int32 allreduce, then the shard dequantised */
+    rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
+    if (rc) return rc;
+    int32_t *q = (int32_t *)c->d_q32;
+    rc = kerr(inccl_k_stream(kind, INCCL_KIND_Q32, srcs, R, q, n, k, amax, scale_R, st));
+    if (rc) return rc;
+    rc = inccl_tp_allreduce_q32(c, q, q, n, st);
+    if (rc) return rc;
+    const void *s1[1] = {q + (size_t)me * shard};
+    return kerr(inccl_k_stream_s(INCCL_KIND_Q32, kind, s1, 1, dst, shard, k, amax, scale_R, c->out_shift, st));
+}
+
+int inccl_reduce_scatter_f32(struct inccl_communicator *c, const float *const *srcs_dev, int R, float *dst_dev,
+                             size_t n, int scale_exp, void *stream)
+{
+    return reduce_scatter_any(c, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, scale_exp, stream);
+}
+
+int inccl_reduce_scatter_bf16(struct inccl_communicator *c, const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev,
+                              size_t n, int scale_exp, void *stream)
+{
+    return reduce_scatter_any(c, INCCL_KIND_BF16, (const void *const *)srcs_dev, R, dst_dev, n, scale_exp, stream);
+}
+
+int inccl_reduce_scatter_f16(struct inccl_communicator *c, const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev,
+                             size_t n, int scale_exp, void *stream)
+{
+    return reduce_scatter_any(c, INCCL_KIND_F16, (const void *const *)srcs_dev, R, dst_dev, n, scale_exp, stream);
+}
+
 /* ------------------------------------------------------------------ */
 /* host-memory collectives                                              */
 /* ------------------------------------------------------------------ */

@@ -156,6 +156,10 @@ int inccl_p2p_piece(struct inccl_communicator *c, const float *const *srcs, int 
 int inccl_p2p_piece16(struct inccl_communicator *c, int kind, const uint16_t *const *srcs, int R, uint16_t *dst,
                       size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st);
 void inccl_p2p_release(struct inccl_communicator *c);
+/* reduce-scatter of kind F32 / BF16 / F16 buckets over the p2p buffers: n = W *
+ * shard, shard % 4 == 0; dst = the dequantised shard `me` (inccl_reduce_scatter_*) */
+int inccl_p2p_reduce_scatter(struct inccl_communicator *c, int kind, const void *const *srcs, int R, void *dst,
+                             size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st);
 /* int32 allreduce (wrapping sum) over the p2p engine's IPC buffers: the
  * reference API's inccl_allreduce_write on a multi-process group without RCCL */
 int inccl_p2p_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,

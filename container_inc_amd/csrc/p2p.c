@@ -268,6 +268,39 @@ int inccl_p2p_piece16(struct inccl_communicator *c, int kind, const uint16_t *co
     return 0;
 }
 
+/* Reduce-scatter over the same buffers: quant + local sum -> part; barrier;
+ * shard `me` pulled from every peer, summed and dequantised (narrowed for the
+ * 2-byte kinds) straight into dst; barrier, so that no rank rewrites its part
+ * (the next call's quantise) while a peer still reads it.  n = W * shard,
+ * shard % 4 == 0. */
+int inccl_p2p_reduce_scatter(struct inccl_communicator *c, int kind, const void *const *srcs, int R, void *dst,
+                             size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    if (W > INCCL_MAX_LOCAL_INPUTS) return inccl_set_error(INCCL_ERR_ARG, "p2p engine supports up to %d GPUs",
+                                                          INCCL_MAX_LOCAL_INPUTS);
+    const size_t shard = n / (size_t)W;
+    if (shard * (size_t)W != n || (shard & 3)) return inccl_set_error(INCCL_ERR_ARG, "p2p reduce-scatter: bad shard");
+    int rc = p2p_ensure(c, n);
+    if (rc) return rc;
+    if (c->p2p_last_stream && c->p2p_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[8], 0));
+    rc = inccl_k_stream(kind, INCCL_KIND_Q32, srcs, R, c->p2p_part, n, k, amax, scale_R, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p reduce-scatter quant+sum launch failed (%d)", rc);
+    rc = sync_and_barrier(c, st);
+    if (rc) return rc;
+    const void *peer[INCCL_MAX_LOCAL_INPUTS];
+    for (int j = 0; j < W; ++j) peer[j] = c->p2p_peer_part[j] + (size_t)me * shard;
+    rc = kind == INCCL_KIND_F32
+             ? inccl_k_peer_reduce(peer, W, (float *)dst, shard, k, amax, scale_R, c->out_shift, st)
+             : inccl_k_peer_reduce16(kind, peer, W, (uint16_t *)dst, shard, k, amax, scale_R, c->out_shift, st);
+    if (rc) return inccl_set_error(INCCL_ERR_HIP, "p2p reduce-scatter launch failed (%d)", rc);
+    rc = sync_and_barrier(c, st);
+    if (rc) return rc;
+    INCCL_HIP(hipEventRecord(c->ev[8], st));
+    c->p2p_last_stream = st;
+    return 0;
+}
+
 /* The int32 allreduce over the same buffers and barriers as inccl_p2p_piece,
  * with the sum left in int32 (the reference's switch add, nts.c:361-363, and
  * nothing else): copy in -> barrier -> pull + sum shard `me` from every peer ->

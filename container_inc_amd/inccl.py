@@ -437,6 +437,31 @@ class Communicator:
         check(rc, "inccl_allreduce_f16")
         return out
 
+    def reduce_scatter(self, srcs, out=None, scale_exp: int = SCALE_AUTO, stream=None):
+        """Reduce-scatter of fp32 / bf16 / fp16 buckets (include/inccl_amd.h
+        inccl_reduce_scatter_*): every rank passes R buckets of n = W * shard
+        elements and gets back its shard of the reduced result."""
+        torch = _torch()
+        srcs = list(srcs)
+        if not 1 <= len(srcs) <= MAX_LOCAL_INPUTS:
+            raise ValueError(f"1..{MAX_LOCAL_INPUTS} local buckets, got {len(srcs)}")
+        dt = srcs[0].dtype
+        fn = {torch.float32: "inccl_reduce_scatter_f32", torch.bfloat16: "inccl_reduce_scatter_bf16",
+              torch.float16: "inccl_reduce_scatter_f16"}.get(dt)
+        if fn is None:
+            raise TypeError(f"reduce_scatter: fp32, bf16 or fp16 buckets, got {dt}")
+        n, W = srcs[0].numel(), self.group.world_size
+        if n % W:
+            raise ValueError(f"reduce_scatter: {n} elements do not split into {W} shards")
+        ptrs = [_dev_ptr(s, dt, f"srcs[{i}]", n) for i, s in enumerate(srcs)]
+        if out is None:
+            out = torch.empty(n // W, dtype=dt, device=srcs[0].device)
+        optr = _dev_ptr(out, dt, "out", n // W)
+        rc = getattr(load(), fn)(self.handle, _ptr_array(ptrs), len(ptrs), optr, n, _check_scale(scale_exp),
+                                 _stream_handle(stream))
+        check(rc, fn)
+        return out
+
     def allreduce_bf16(self, srcs, out=None, scale_exp: int = SCALE_AUTO, stream=None):
         """bfloat16 buckets (include/inccl_amd.h inccl_allreduce_bf16)."""
         torch = _torch()

@@ -281,15 +281,35 @@ int inccl_absmax_bf16(const uint16_t *const *srcs_dev, int R, size_t n, uint32_t
 
 /* IEEE binary16 buckets (uint16_t bit patterns), the same arithmetic:
  * dst = f16_rne( (float)( sum over ranks, sum over r<R  quant(srcs[r]) ) * 2^-k ).
- * world == 1: one fused kernel, (R + 1) * 2 * n HBM bytes.  world > 1: "rccl"
- * and the in-process transport as bf16 (int32 reduce-scatter, 2-byte
- * all-gather); every other engine: quant+local sum -> its int32 allreduce ->
- * dequantise.  dst may alias srcs[0]. */
+ * world == 1: one fused kernel, (R + 1) * 2 * n HBM bytes.  world > 1: the
+ * engines route it as bf16 (2-byte result exchange on "rccl", the in-process
+ * transport, "p2p", "mesh" and "meshw"; "ar", "a2a", "ll": int32 allreduce,
+ * then dequantise).  dst may alias srcs[0]. */
 int inccl_allreduce_f16(struct inccl_communicator *comm, const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev,
                         size_t n, int scale_exp, void *stream);
 /* max |x| over R fp16 buckets into *amax_bits_dev (as fp32 bits; NaN ignored). */
 int inccl_absmax_f16(const uint16_t *const *srcs_dev, int R, size_t n, uint32_t *amax_bits_dev, int zero_first,
                      void *stream);
+
+/* Reduce-scatter: the allreduce's first half, for callers that keep their
+ * gradients sharded (ZeRO / FSDP-style optimisers).  Every rank passes R local
+ * buckets of n = W * shard elements; rank r receives in dst_dev (shard
+ * elements) the dequantised sum over every rank and bucket of elements
+ * [r * shard, (r + 1) * shard) -- bit-identical to that slice of the
+ * allreduce's result (the same scale, average mode and non-finite mode).
+ * n % W != 0 is INCCL_ERR_ARG.  Routes: world 1 the fused kernel; "rccl" and
+ * the in-process transport quant + local sum -> int32 reduce-scatter ->
+ * dequantise the shard; "p2p", "ll", "mesh", "meshw" (shard % 4 == 0, dst
+ * 16-B aligned for fp32, 8-B for 2-byte kinds) quant + local sum into the IPC
+ * buffer -> barrier -> one kernel pulls shard r from every peer, sums and
+ * dequantises into dst -> barrier; otherwise the engine's int32 allreduce and
+ * the shard dequantised.  dst must not alias any source. */
+int inccl_reduce_scatter_f32(struct inccl_communicator *comm, const float *const *srcs_dev, int R, float *dst_dev,
+                             size_t n, int scale_exp, void *stream);
+int inccl_reduce_scatter_bf16(struct inccl_communicator *comm, const uint16_t *const *srcs_dev, int R,
+                              uint16_t *dst_dev, size_t n, int scale_exp, void *stream);
+int inccl_reduce_scatter_f16(struct inccl_communicator *comm, const uint16_t *const *srcs_dev, int R,
+                             uint16_t *dst_dev, size_t n, int scale_exp, void *stream);
 
 /* Host-memory fp32 allreduce (BASELINE config 3): src/dst in host memory,
  * pipelined H2D / reduce / D2H over `bucket_bytes` buckets on three streams.

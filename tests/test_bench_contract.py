@@ -3,6 +3,8 @@ sweep's size list (BASELINE config 5 plus north_star's 1024 MiB point)."""
 import importlib
 import sys
 
+import pytest
+
 from conftest import ROOT
 
 
@@ -90,19 +92,22 @@ def test_watchdog_emits_line_and_exits_nonzero():
     assert line["value"] is None and "sweep 4096 B engine x" in line["error"]
 
 
-def test_oracle_check_bf16_world1(orc):
+@pytest.mark.parametrize("fmt", ["bf16", "f16"])
+def test_oracle_check_16bit_world1(orc, fmt):
     import numpy as np
     import torch
     b = _bench()
     rng = np.random.default_rng(6)
-    xs = [orc.f32_to_bf16(rng.standard_normal(700).astype(np.float32)) for _ in range(2)]
-    want = orc.reduce_bf16(xs, 25)
-    srcs = [torch.from_numpy(x.view(np.int16)).view(torch.bfloat16) for x in xs]
-    out = torch.from_numpy(want.view(np.int16).copy()).view(torch.bfloat16)
+    conv, red, dt = ((orc.f32_to_bf16, orc.reduce_bf16, torch.bfloat16) if fmt == "bf16"
+                     else (orc.f32_to_f16, orc.reduce_f16, torch.float16))
+    xs = [conv(rng.standard_normal(700).astype(np.float32)) for _ in range(2)]
+    want = red(xs, 25)
+    srcs = [torch.from_numpy(x.view(np.int16)).view(dt) for x in xs]
+    out = torch.from_numpy(want.view(np.int16).copy()).view(dt)
     lanes = b.oracle_lanes(700, 1, 1, 50)
-    assert b.oracle_check(srcs, out, lanes, 25, 0, 1, bf16=True)["mismatches"] == 0
+    assert b.oracle_check(srcs, out, lanes, 25, 0, 1, fmt=fmt)["mismatches"] == 0
     out.view(torch.int16)[lanes[2]] ^= 1
-    assert b.oracle_check(srcs, out, lanes, 25, 0, 1, bf16=True)["mismatches"] == 1
+    assert b.oracle_check(srcs, out, lanes, 25, 0, 1, fmt=fmt)["mismatches"] == 1
 
 
 def _keeper_run(body: str):

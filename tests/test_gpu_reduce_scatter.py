@@ -1,0 +1,204 @@
+"""Reduce-scatter (gpu): inccl_reduce_scatter_f32 / _bf16 / _f16, the
+allreduce's first half for sharded-gradient callers.  Rank r's result must be
+bit-identical to elements [r*shard, (r+1)*shard) of the oracle's reduce of every
+rank's buckets (orc_reduce_f32 / _bf16 / _f16), over every route: the fused
+world-1 kernel, RCCL's ncclReduceScatter at world 1, the in-process transport
+(W = 2..4, aligned and ragged shards), and one process per rank on the IPC
+engines (p2p pull-reduce into the shard; a ragged shard through the int32
+allreduce), with average mode and repeated calls (buffer reuse)."""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from test_gpu_comm import _run_ranks
+
+pytestmark = pytest.mark.gpu
+
+KINDS = ("f32", "bf16", "f16")
+
+
+def _bucket(rng, n, kind):
+    x = rng.standard_normal(n).astype(np.float32) * 2.0
+    if kind == "f32":
+        return x
+    if kind == "bf16":
+        return (x.view(np.uint32) >> 16).astype(np.uint16)
+    return x.astype(np.float16).view(np.uint16)
+
+
+def _dev(h, dev, kind):
+    import torch
+    if kind == "f32":
+        return torch.from_numpy(h).to(dev)
+    t = torch.from_numpy(h.view(np.int16)).to(dev)
+    return t.view(torch.bfloat16 if kind == "bf16" else torch.float16)
+
+
+def _host(t, kind):
+    import torch
+    if kind == "f32":
+        return t.cpu().numpy()
+    return t.view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+def _reduce(O, every, kind, k):
+    return {"f32": O.reduce_f32, "bf16": O.reduce_bf16, "f16": O.reduce_f16}[kind](every, k)
+
+
+def _auto_k(O, every, kind, RW):
+    return O.choose_scale({"f32": O.absmax, "bf16": O.absmax_bf16, "f16": O.absmax_f16}[kind](every), RW)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("world,shard,R,k", [(1, 4099, 2, "auto"), (2, 4096, 2, 25), (3, 1001, 1, "auto"),
+                                             (4, 65_540, 2, "auto"), (2, 262_144, 1, 23)])
+def test_reduce_scatter_local(gpu, orc, kind, world, shard, R, k):
+    import torch
+    from container_inc_amd import inccl
+    n = world * shard
+    rng = np.random.default_rng(world * 100 + shard % 97 + len(kind))
+    hs = [[_bucket(rng, n, kind) for _ in range(R)] for _ in range(world)]
+    every = [h for per in hs for h in per]
+    kk = _auto_k(orc, every, kind, world * R) if k == "auto" else k
+    want = _reduce(orc, every, kind, kk)
+    hub = f"rs-{kind}-{world}-{shard}-{R}"
+
+    def rank(r):
+        grp = inccl.inccl_group_create_local(world, r, hub)
+        comm = inccl.inccl_communicator_create(grp, 0)
+        srcs = [_dev(h, gpu, kind) for h in hs[r]]
+        res = []
+        for _ in range(2):   # workspace reuse
+            out = comm.reduce_scatter(srcs, scale_exp=inccl.SCALE_AUTO if k == "auto" else k, stream=comm.stream)
+            torch.cuda.synchronize()
+            res.append(_host(out, kind))
+        comm.barrier()
+        comm.destroy()
+        grp.destroy()
+        return res
+
+    for r, res in enumerate(_run_ranks(world, rank)):
+        for got in res:
+            np.testing.assert_array_equal(got, want[r * shard:(r + 1) * shard])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_reduce_scatter_average(gpu, orc, world):
+    """inccl_comm_set_average: the shard of the mean, bit-identical to sum / W."""
+    import torch
+    from container_inc_amd import inccl
+    shard = 8192
+    n = world * shard
+    rng = np.random.default_rng(world)
+    hs = [[_bucket(rng, n, "f32")] for _ in range(world)]
+    every = [h for per in hs for h in per]
+    want = orc.reduce_f32(every, 25) / np.float32(world)
+
+    def rank(r):
+        grp = inccl.inccl_group_create_local(world, r, f"rs-avg-{world}")
+        comm = inccl.inccl_communicator_create(grp, 0)
+        comm.set_average(True)
+        out = comm.reduce_scatter([_dev(hs[r][0], gpu, "f32")], scale_exp=25, stream=comm.stream)
+        torch.cuda.synchronize()
+        got = _host(out, "f32")
+        comm.barrier()
+        comm.destroy()
+        grp.destroy()
+        return got
+
+    for r, got in enumerate(_run_ranks(world, rank)):
+        np.testing.assert_array_equal(got.view(np.uint32), want[r * shard:(r + 1) * shard].view(np.uint32))
+
+
+def test_reduce_scatter_rccl_world1(gpu, orc, monkeypatch):
+    """RCCL at world 1 through the sharded route: a real ncclReduceScatter."""
+    import torch
+    from container_inc_amd import inccl
+    monkeypatch.setenv("INCCL_FORCE_RCCL", "1")
+    monkeypatch.setenv("INCCL_FORCE_SHARDED", "1")
+    monkeypatch.setenv("INCCL_MASTER_PORT", "0")
+    grp = inccl.inccl_group_create(1, 0, "127.0.0.1")
+    comm = inccl.inccl_communicator_create(grp, 0)
+    assert grp.transport == "rccl"
+    rng = np.random.default_rng(3)
+    for kind in KINDS:
+        hs = [_bucket(rng, 50_001, kind) for _ in range(2)]
+        want = _reduce(orc, hs, kind, _auto_k(orc, hs, kind, 2))
+        for eng in ("rccl", "ar"):
+            comm.set_engine(eng)
+            out = comm.reduce_scatter([_dev(h, gpu, kind) for h in hs], stream=comm.stream)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(_host(out, kind), want, err_msg=f"{kind} {eng}")
+    with pytest.raises(Exception):
+        comm.reduce_scatter([torch.zeros(10, device=gpu)], out=torch.zeros(3, device=gpu))   # wrong shard size
+    comm.destroy()
+    grp.destroy()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ipc_rank(rank, world, port, q, engine):
+    try:
+        os.environ["INCCL_ENGINE"] = engine
+        os.environ["INCCL_DEVICE"] = "0"
+        os.environ["INCCL_BOOT_TIMEOUT"] = "120"
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        from container_inc_amd import inccl
+        from oracle import oracle as O
+        dev = torch.device("cuda", 0)
+        grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=0)
+        comm = inccl.inccl_communicator_create(grp, 0)
+        ok = []
+        for kind in KINDS:
+            for shard, R, seed in ((1 << 18, 2, 1), (1001, 1, 2), (4096, 2, 3)):   # 1001: the int32-allreduce route
+                n = world * shard
+                hs = [[_bucket(np.random.default_rng(seed * 1000 + r * 10 + j), n, kind) for j in range(R)]
+                      for r in range(world)]
+                every = [h for per in hs for h in per]
+                want = _reduce(O, every, kind, _auto_k(O, every, kind, world * R))[rank * shard:(rank + 1) * shard]
+                srcs = [_dev(h, dev, kind) for h in hs[rank]]
+                for _ in range(2):
+                    out = comm.reduce_scatter(srcs, stream=comm.stream)
+                    torch.cuda.synchronize()
+                    ok.append(bool(np.array_equal(_host(out, kind), want)))
+        comm.destroy()
+        grp.destroy()
+        q.put((rank, ok, None))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "mesh"), (4, "meshw"), (2, "ll")])
+def test_reduce_scatter_ipc_multiprocess(gpu, world, engine):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ipc_rank, args=(r, world, port, q, engine)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, ok, err = q.get(timeout=240)
+            res[r] = (ok, err)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        ok, err = res[r]
+        assert err is None, f"rank {r}: {err}"
+        assert all(ok), f"rank {r}: {ok}"

@@ -146,7 +146,7 @@ def _oracle_check_rank(rank, world, port, q):
     wb = O.reduce_bf16(hb, k)
     mb = [torch.from_numpy(hb[rank * R + j].view(np.int16)).view(torch.bfloat16) for j in range(R)]
     ob = torch.from_numpy(wb.view(np.int16).copy()).view(torch.bfloat16)
-    gb = bench.oracle_check(mb, ob, bench.oracle_lanes(300, world, 1, 50), k, rank, world, bf16=True)
+    gb = bench.oracle_check(mb, ob, bench.oracle_lanes(300, world, 1, 50), k, rank, world, fmt="bf16")
     q.put((rank, good["mismatches"], bad["mismatches"], gb["mismatches"]))
     dist.destroy_process_group()
 
