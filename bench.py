@@ -51,6 +51,8 @@ Extra JSON fields:
                     N > 1: inccl_allreduce_f16 on the same engines as bf16, verified
   bf16              N = 1: R bf16 buckets of 256 MiB (k_stream16), repeated and rotated;
                     N > 1: inccl_allreduce_bf16 on the rccl, p2p, mesh and meshw engines, verified
+  reduce_scatter    N > 1: inccl_reduce_scatter_f32 of R x 256 MiB per rank on rccl and p2p, each
+                    rank's shard checked against the oracle
   sweep             N > 1: 4 KiB .. 256 MiB and 1 GiB per engine, verified with
                     alternating input sets
 """
@@ -687,7 +689,112 @@ def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256, fmt: 
             row["parity_vs_oracle"] = oracle_check(inputs[0], got[0], lanes, 25, rank, world, fmt=fmt)
             link = (world - 1) * n * 6 // world
             row["GBps_buckets"] = round(world * R * 2 * n / v[0] / 1e9, 1)
-            row["xgmi_frac"] = round(link / v[0] / 1e9 / ((world - 1) * XGMI_LINK_GBS_BIDIR), 4)
+            # both directions counted, as xgmi_roofline does: (W-1)/W * n * (4 + 2) bytes out and as many in
+            row["xgmi_frac"] = round(2 * link / v[0] / 1e9 / ((world - 1) * XGMI_LINK_GBS_BIDIR), 4)
+        rows.append(row)
+        del got
+    del inputs, out, refs
+    torch.cuda.empty_cache()
+    return rows
+
+
+def rs_oracle_check(srcs, out_shard, lanes, k: int, rank: int, world: int) -> dict:
+    """oracle_check for a reduce-scatter: every rank's inputs at `lanes` and its
+    shard's values at the lanes inside its shard go to rank 0, which runs
+    orc_reduce_f32 on all W*R inputs and compares each rank's lanes bit for bit."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    n = srcs[0].numel()
+    shard = n // world
+    idx = torch.as_tensor(lanes, dtype=torch.int64, device=out_shard.device)
+    own = [(i, l - rank * shard) for i, l in enumerate(lanes) if rank * shard <= l < (rank + 1) * shard]
+    full = torch.zeros(len(lanes), dtype=torch.float32, device=out_shard.device)
+    if own:
+        pos = torch.as_tensor([i for i, _ in own], dtype=torch.int64, device=out_shard.device)
+        loc = torch.as_tensor([j for _, j in own], dtype=torch.int64, device=out_shard.device)
+        full.index_copy_(0, pos, out_shard.index_select(0, loc))
+    mine = torch.stack([s.index_select(0, idx) for s in srcs] + [full]).cpu().view(torch.int32)
+    if world > 1:
+        bucket = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
+        dist.gather(mine, gather_list=bucket, dst=0)
+    else:
+        bucket = [mine]
+    res = {"lanes": len(lanes), "ranks": world, "mismatches": None,
+           "checker": "oracle/inccl_oracle.c orc_reduce_f32, each rank's shard"}
+    if rank == 0:
+        from oracle import oracle as O
+        R = len(srcs)
+        arr = [b.numpy() for b in bucket]
+        want = O.reduce_f32([a[j].view(np.float32) for a in arr for j in range(R)], k).view(np.uint32)
+        lane = np.asarray(lanes)
+        bad = 0
+        for r, a in enumerate(arr):
+            sel = (lane >= r * shard) & (lane < (r + 1) * shard)
+            bad += int(np.count_nonzero(a[R].view(np.uint32)[sel] != want[sel]))
+        res["mismatches"] = bad
+    return res
+
+
+def reduce_scatter_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256) -> list:
+    """N > 1: inccl_reduce_scatter_f32 of R resident `mib` MiB fp32 buckets per
+    rank (each rank keeps its 1/W shard of the reduced bucket: the sharded-
+    gradient callers' half of the allreduce) on rccl (ncclReduceScatter) and p2p
+    (pull-reduce into the shard), each verified bit-identical to the first engine
+    that passes, over two alternating input sets, and against the oracle on
+    every rank's shard; wall time per call (max over ranks) and the xGMI link
+    fraction of its (W-1)/W * n * 4 bytes."""
+    import torch
+    import torch.distributed as dist
+    n = mib * (1 << 20) // 4
+    if n % world:
+        return [{"skipped": f"{n} elements do not split into {world} shards"}]
+    inputs = []
+    for seed in (9100, 9600):
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed + rank)
+        inputs.append([torch.randn(n, generator=gen, device=dev) for _ in range(R)])
+    out = torch.empty(n // world, device=dev, dtype=torch.float32)
+    st = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize()
+    rows, refs = [], None
+    lanes = oracle_lanes(n, world, 1, 1 << 16)
+    for eng in ("rccl", "p2p"):
+        set_stage(f"reduce_scatter {mib} MiB engine {eng}")
+        ok, dt, same = 1, float("inf"), False
+        try:
+            comm.set_engine(eng)
+            got = []
+            for xs in (inputs[0], inputs[1], inputs[0]):
+                comm.reduce_scatter(xs, out=out, scale_exp=25, stream=st.cuda_stream)
+                torch.cuda.synchronize()
+                got.append(out.clone())
+            same = (torch.equal(got[0], got[2]) if refs is None
+                    else all(torch.equal(g, refs[i % 2]) for i, g in enumerate(got)))
+            for _ in range(5):
+                comm.reduce_scatter(inputs[0], out=out, scale_exp=25, stream=st.cuda_stream)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(10):
+                comm.reduce_scatter(inputs[0], out=out, scale_exp=25, stream=st.cuda_stream)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / 10
+        except Exception as e:  # noqa: BLE001
+            print(f"rank {rank}: reduce_scatter engine {eng} failed: {e}", file=sys.stderr, flush=True)
+            ok, got = 0, None
+        v = agree([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0], world)
+        good, ident = v[1] == 0.0, v[2] == 0.0
+        if good and ident and refs is None:
+            refs = (got[0], got[1])
+        row = {"engine": eng, "bucket_mib": mib, "R": R, "ok": good, "bit_identical": good and ident,
+               "ms": round(v[0] * 1e3, 4) if good else None}
+        if good:
+            row["parity_vs_oracle"] = rs_oracle_check(inputs[0], got[0], lanes, 25, rank, world)
+            link = (world - 1) * n * 4 // world
+            row["GBps_buckets"] = round(world * R * 4 * n / v[0] / 1e9, 1)
+            # both directions counted: (W-1)/W * n * 4 bytes out and as many in
+            row["xgmi_frac"] = round(2 * link / v[0] / 1e9 / ((world - 1) * XGMI_LINK_GBS_BIDIR), 4)
         rows.append(row)
         del got
     del inputs, out, refs
@@ -1640,6 +1747,15 @@ def main():
                     res["f16"] = {"error": repr(e)}
             else:
                 res["f16"] = {"skipped": f"run past {sweep_soft:.0f} s from process start"}
+        with Phase("reduce_scatter"):
+            if agree([time.monotonic() - T_START], world)[0] <= sweep_soft:
+                try:
+                    res["reduce_scatter"] = reduce_scatter_engines(comm, dev, R, rank, world)
+                except Exception as e:  # noqa: BLE001
+                    print(f"rank {rank}: reduce_scatter key failed: {e!r}", file=sys.stderr, flush=True)
+                    res["reduce_scatter"] = {"error": repr(e)}
+            else:
+                res["reduce_scatter"] = {"skipped": f"run past {sweep_soft:.0f} s from process start"}
         comm.set_engine(chosen[0])
         # north_star: the path starts and ends in host memory -- the end-to-end
         # rate with pinned H2D / D2H, at this N too
