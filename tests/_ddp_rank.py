@@ -79,6 +79,24 @@ class GlooStandIn:
         return self._allreduce_16(srcs, out, scale_exp, O.absmax_f16, O.reduce_f16, torch.float16)
 
 
+    def reduce_scatter(self, srcs, out=None, scale_exp=25, stream=None):
+        """inccl_reduce_scatter_f32 restated: this rank's shard of the oracle's reduce"""
+        import torch
+        import torch.distributed as dist
+        from container_inc_amd import inccl
+        from oracle import oracle as O
+        W, me = self.group.world_size, dist.get_rank()
+        got = [torch.empty_like(srcs[0]) for _ in range(W)]
+        dist.all_gather(got, srcs[0].contiguous())
+        every = [g.numpy() for g in got]
+        shard = every[0].size // W
+        if self.nonfinite and scale_exp == inccl.SCALE_AUTO and O.any_nonfinite(every, "f32"):
+            return out.fill_(float("nan"))
+        k = O.choose_scale(O.absmax(every), W) if scale_exp == inccl.SCALE_AUTO else scale_exp
+        out.copy_(torch.from_numpy(O.reduce_f32(every, k)[me * shard:(me + 1) * shard]))
+        return out
+
+
 def O_choose(amax, W):
     from oracle import oracle as O
     return O.choose_scale(amax, W)
