@@ -48,6 +48,8 @@ def reduce_scatter_hook(state: HookState, grad, output):
     if grad.numel() != w * output.numel() or output.dtype != grad.dtype:
         raise IncclError(f"inccl FSDP hook: a {grad.numel()}-element gradient does not shard into "
                          f"{w} x {output.numel()} ({output.dtype})")
+    if not output.is_contiguous():   # the shard is written in place: a reshaped copy would lose it
+        raise IncclError("inccl FSDP hook: the output shard must be contiguous")
     state.comm.reduce_scatter([grad.reshape(-1)], out=output.reshape(-1), scale_exp=state.scale_exp,
                               stream=_stream(grad))
     if divide:
@@ -60,6 +62,8 @@ def allreduce_hook(state: HookState, grad):
     import torch
     w, divide = _check(state, grad)
     fn = {torch.float32: "allreduce_f32", torch.bfloat16: "allreduce_bf16", torch.float16: "allreduce_f16"}[grad.dtype]
+    if not grad.is_contiguous():   # reduced in place: a reshaped copy would lose the result
+        raise IncclError("inccl FSDP hook: the gradient must be contiguous")
     flat = grad.reshape(-1)
     getattr(state.comm, fn)([flat], out=flat, scale_exp=state.scale_exp, stream=_stream(grad))
     if divide:

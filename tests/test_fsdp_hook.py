@@ -46,3 +46,7 @@ def test_fsdp_hook_refuses_bad_shapes():
         fsdp.reduce_scatter_hook(st, torch.zeros(10), torch.zeros(4))   # 10 != 2 x 4
     with pytest.raises(IncclError):
         fsdp.reduce_scatter_hook(st, torch.zeros(8, dtype=torch.float64), torch.zeros(4, dtype=torch.float64))
+    with pytest.raises(IncclError):   # a strided output shard would be written through a copy
+        fsdp.reduce_scatter_hook(st, torch.zeros(8), torch.zeros(8)[::2])
+    with pytest.raises(IncclError):
+        fsdp.allreduce_hook(st, torch.zeros(4, 4).t())
