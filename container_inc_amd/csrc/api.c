@@ -102,6 +102,41 @@ int inccl_stream_op(int in_kind, int out_kind, const void *const *srcs_dev, int 
     return kerr(inccl_k_stream(in_kind, out_kind, srcs_dev, R, dst_dev, n, scale_exp, amax_bits_dev, scale_R, stream));
 }
 
+/* ---- ordering across caller streams ----
+ * A communicator's calls share its workspaces (the int32 partials, the auto
+ * scale's max word, the gather buffer).  A call on another stream than the
+ * previous call's first waits for that call's end: ev[9], recorded at the end
+ * of every call (an event outlives its stream, so the caller may have dropped
+ * the previous stream since).  Captured calls are left to the capture's own
+ * order. */
+static int ws_enter(struct inccl_communicator *c, void *stream, int *capturing)
+{
+    const hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    INCCL_HIP(hipStreamIsCapturing(st, &cs));
+    *capturing = cs != hipStreamCaptureStatusNone;
+    if (!*capturing && c->ws_last_stream && c->ws_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[9], 0));
+    return 0;
+}
+
+static int ws_leave(struct inccl_communicator *c, void *stream, int capturing, int rc)
+{
+    const hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (rc == 0 && !capturing) {
+        INCCL_HIP(hipEventRecord(c->ev[9], st));
+        c->ws_last_stream = st;
+    }
+    return rc;
+}
+
+#define INCCL_ORDERED(c, stream, call)                              \
+    do {                                                            \
+        if (!(c)) return (call);                                    \
+        int cap_ = 0, rc_ = ws_enter((c), (stream), &cap_);         \
+        if (rc_) return rc_;                                        \
+        return ws_leave((c), (stream), cap_, (call));               \
+    } while (0)
+
 /* ---- prepared stream ops ---- */
 struct inccl_op {
     struct inccl_communicator *comm;   /* NULL: a stream op; else an allreduce of comm (in_kind: its format) */
@@ -460,7 +495,7 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
         else
             INCCL_HIP(hipStreamCreateWithPriority(&c->copy_streams[i], hipStreamNonBlocking, prio_hi));
     }
-    for (int i = 0; i < 9; ++i) INCCL_HIP(hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming));
+    for (int i = 0; i < 10; ++i) INCCL_HIP(hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming));
     INCCL_HIP(hipMalloc((void **)&c->d_words, 256));
     INCCL_HIP(hipMemset(c->d_words, 0, 256));
     c->comm_id = g->comm_seq++;
@@ -536,7 +571,7 @@ int inccl_communicator_destroy(struct inccl_communicator *comm)
     inccl_d2h_worker_destroy(comm->d2h);
     if (comm->send_payload) hipHostFree(comm->send_payload);
     if (comm->receive_payload) hipHostFree(comm->receive_payload);
-    for (int i = 0; i < 9; ++i)
+    for (int i = 0; i < 10; ++i)
         if (comm->ev[i]) hipEventDestroy(comm->ev[i]);
     if (comm->copy_streams[0]) hipStreamDestroy(comm->copy_streams[0]);
     if (comm->copy_streams[1]) hipStreamDestroy(comm->copy_streams[1]);
@@ -687,13 +722,19 @@ int inccl_comm_clear_error(struct inccl_communicator *comm)
 /* ------------------------------------------------------------------ */
 /* device-resident collectives                                          */
 /* ------------------------------------------------------------------ */
-int inccl_allreduce_q32(struct inccl_communicator *c, const int32_t *src_dev, int32_t *dst_dev, size_t n,
-                        void *stream)
+static int allreduce_q32_body(struct inccl_communicator *c, const int32_t *src_dev, int32_t *dst_dev, size_t n,
+                              void *stream)
 {
     if (!c || (!src_dev && n) || (!dst_dev && n)) return inccl_set_error(INCCL_ERR_ARG, "bad allreduce_q32 args");
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     if (n == 0) return 0;
     return inccl_tp_allreduce_q32(c, src_dev, dst_dev, n, st);
+}
+
+int inccl_allreduce_q32(struct inccl_communicator *c, const int32_t *src_dev, int32_t *dst_dev, size_t n,
+                        void *stream)
+{
+    INCCL_ORDERED(c, stream, allreduce_q32_body(c, src_dev, dst_dev, n, stream));
 }
 
 /* Variant B: quant + local sum -> grouped ncclSend/Recv of
@@ -813,8 +854,8 @@ int inccl_allreduce_f32(struct inccl_communicator *c, const float *const *srcs_d
     return inccl_allreduce_f32_pipelined(c, srcs_dev, R, dst_dev, n, scale_exp, 1, stream);
 }
 
-int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *const *srcs_dev, int R, float *dst_dev,
-                                  size_t n, int scale_exp, int chunks, void *stream)
+static int allreduce_f32_body(struct inccl_communicator *c, const float *const *srcs_dev, int R, float *dst_dev,
+                              size_t n, int scale_exp, int chunks, void *stream)
 {
     if (!c || !srcs_dev || R < 1 || R > INCCL_MAX_LOCAL_INPUTS || (!dst_dev && n))
         return inccl_set_error(INCCL_ERR_ARG, "bad allreduce_f32 args");
@@ -931,6 +972,12 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
     return 0;
 }
 
+int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *const *srcs_dev, int R, float *dst_dev,
+                                  size_t n, int scale_exp, int chunks, void *stream)
+{
+    INCCL_ORDERED(c, stream, allreduce_f32_body(c, srcs_dev, R, dst_dev, n, scale_exp, chunks, stream));
+}
+
 /* 2-byte buckets (kind INCCL_KIND_BF16 or INCCL_KIND_F16): the fp32 path's
  * arithmetic on the widened values.  The int32 partial sums travel as in the
  * fp32 path (the switch's aggregate, nts.c:361-363); only the result's format
@@ -938,8 +985,8 @@ int inccl_allreduce_f32_pipelined(struct inccl_communicator *c, const float *con
  * of 4 (an all-gather copies bytes: the same one serves both formats), and the
  * mesh and p2p engines' reduce kernels narrow to the bucket's format before
  * their result exchange. */
-static int allreduce_16(struct inccl_communicator *c, int kind, const uint16_t *const *srcs_dev, int R,
-                        uint16_t *dst_dev, size_t n, int scale_exp, void *stream)
+static int allreduce_16_body(struct inccl_communicator *c, int kind, const uint16_t *const *srcs_dev, int R,
+                             uint16_t *dst_dev, size_t n, int scale_exp, void *stream)
 {
     if (!c || !srcs_dev || R < 1 || R > INCCL_MAX_LOCAL_INPUTS || (!dst_dev && n))
         return inccl_set_error(INCCL_ERR_ARG, "bad allreduce_%s args", kind == INCCL_KIND_F16 ? "f16" : "bf16");
@@ -1010,6 +1057,12 @@ static int allreduce_16(struct inccl_communicator *c, int kind, const uint16_t *
                                  c->out_shift, st));
 }
 
+static int allreduce_16(struct inccl_communicator *c, int kind, const uint16_t *const *srcs_dev, int R,
+                        uint16_t *dst_dev, size_t n, int scale_exp, void *stream)
+{
+    INCCL_ORDERED(c, stream, allreduce_16_body(c, kind, srcs_dev, R, dst_dev, n, scale_exp, stream));
+}
+
 int inccl_allreduce_bf16(struct inccl_communicator *c, const uint16_t *const *srcs_dev, int R, uint16_t *dst_dev,
                          size_t n, int scale_exp, void *stream)
 {
@@ -1024,8 +1077,8 @@ int inccl_allreduce_f16(struct inccl_communicator *c, const uint16_t *const *src
 
 /* Reduce-scatter (include/inccl_amd.h): the allreduce's arithmetic, rank `me`
  * keeping shard me of the result.  kind F32, BF16 or F16. */
-static int reduce_scatter_any(struct inccl_communicator *c, int kind, const void *const *srcs, int R, void *dst,
-                              size_t n, int scale_exp, void *stream)
+static int reduce_scatter_body(struct inccl_communicator *c, int kind, const void *const *srcs, int R, void *dst,
+                               size_t n, int scale_exp, void *stream)
 {
     static const char *const names[] = {"f32", "", "", "bf16", "f16"};
     if (!c || !srcs || R < 1 || R > INCCL_MAX_LOCAL_INPUTS || (!dst && n))
@@ -1074,6 +1127,12 @@ static int reduce_scatter_any(struct inccl_communicator *c, int kind, const void
     if (rc) return rc;
     const void *s1[1] = {q + (size_t)me * shard};
     return kerr(inccl_k_stream_s(INCCL_KIND_Q32, kind, s1, 1, dst, shard, k, amax, scale_R, c->out_shift, st));
+}
+
+static int reduce_scatter_any(struct inccl_communicator *c, int kind, const void *const *srcs, int R, void *dst,
+                              size_t n, int scale_exp, void *stream)
+{
+    INCCL_ORDERED(c, stream, reduce_scatter_body(c, kind, srcs, R, dst, n, scale_exp, stream));
 }
 
 int inccl_reduce_scatter_f32(struct inccl_communicator *c, const float *const *srcs_dev, int R, float *dst_dev,

@@ -117,7 +117,9 @@ struct inccl_communicator {
     int nreg;
     struct inccl_copy_pool *pool;  /* host staging copies (copypool.c) */
     struct inccl_d2h_worker *d2h;  /* issues pageable D2H copies beside the H2Ds (hostdma.c) */
-    hipEvent_t ev[9];            /* [8]: p2p ordering across caller streams */
+    hipEvent_t ev[10];           /* [8]: p2p ordering across caller streams; [9]: workspace ordering
+                                  * across caller streams (ws_last_stream) */
+    hipStream_t ws_last_stream;  /* the stream of the communicator's last call (api.c ws_enter) */
     hipStream_t p2p_last_stream;
 };
 

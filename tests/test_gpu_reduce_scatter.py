@@ -202,3 +202,43 @@ def test_reduce_scatter_ipc_multiprocess(gpu, world, engine):
         ok, err = res[r]
         assert err is None, f"rank {r}: {err}"
         assert all(ok), f"rank {r}: {ok}"
+
+
+def test_calls_on_alternating_streams(gpu, orc):
+    """A communicator's calls share its workspaces (int32 partials, the auto
+    scale's word): back-to-back calls on two streams, no host sync between them,
+    inputs of different magnitude (so different scales), must each match the
+    oracle -- the second call waits for the first (api.c ws_enter)."""
+    import torch
+    from container_inc_amd import inccl
+    world, n = 2, 1 << 22
+    rng = np.random.default_rng(11)
+    xs = [[rng.standard_normal(n).astype(np.float32)] for _ in range(world)]
+    ys = [[(rng.standard_normal(n) * 1000.0).astype(np.float32)] for _ in range(world)]
+    want_x = _reduce(orc, [h for per in xs for h in per], "f32", _auto_k(orc, [h for per in xs for h in per], "f32", world))
+    want_y = _reduce(orc, [h for per in ys for h in per], "f32", _auto_k(orc, [h for per in ys for h in per], "f32", world))
+
+    def rank(r):
+        grp = inccl.inccl_group_create_local(world, r, "alt-streams")
+        comm = inccl.inccl_communicator_create(grp, 0)
+        sa, sb = torch.cuda.Stream(device=gpu), torch.cuda.Stream(device=gpu)
+        dx, dy = _dev(xs[r][0], gpu, "f32"), _dev(ys[r][0], gpu, "f32")
+        torch.cuda.synchronize()
+        res = []
+        for _ in range(3):
+            ox = comm.allreduce_f32([dx], scale_exp=inccl.SCALE_AUTO, stream=sa.cuda_stream)
+            oy = comm.allreduce_f32([dy], scale_exp=inccl.SCALE_AUTO, stream=sb.cuda_stream)
+            rx = comm.reduce_scatter([dx], stream=sa.cuda_stream)
+            torch.cuda.synchronize()
+            res.append((_host(ox, "f32"), _host(oy, "f32"), _host(rx, "f32")))
+        comm.barrier()
+        comm.destroy()
+        grp.destroy()
+        return res
+
+    shard = n // world
+    for r, res in enumerate(_run_ranks(world, rank)):
+        for gx, gy, grs in res:
+            np.testing.assert_array_equal(gx, want_x)
+            np.testing.assert_array_equal(gy, want_y)
+            np.testing.assert_array_equal(grs, want_x[r * shard:(r + 1) * shard])
