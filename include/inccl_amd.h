@@ -224,7 +224,10 @@ int inccl_comm_set_nonfinite(struct inccl_communicator *comm, int mode);
  * world == 1: one fused kernel.  world > 1: quant+local sum -> reduce-scatter
  * (int32, sum) -> dequantise own shard -> all-gather (fp32).  `scale_exp` may be
  * INCCL_SCALE_AUTO (adds an absmax pass and a 4-byte max-allreduce).
- * stream NULL = the communicator's stream.  dst may alias srcs[0]. */
+ * stream NULL = the communicator's stream.  dst may alias srcs[0].  A
+ * communicator's calls (allreduce, reduce-scatter, any format) may come on any
+ * stream: one on another stream than the previous call's waits for that call's
+ * end on the device, since they share the communicator's workspaces. */
 int inccl_allreduce_f32(struct inccl_communicator *comm, const float *const *srcs_dev, int R, float *dst_dev,
                         size_t n, int scale_exp, void *stream);
 /* Same with the bucket split into `chunks` pieces pipelined over two streams
