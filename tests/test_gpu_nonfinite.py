@@ -122,6 +122,9 @@ def test_nonfinite_local(gpu, orc, kind, world):
             _allreduce(comm, kind, ins, out)
             torch.cuda.synchronize()
             res.append(_host(out, kind))
+        rs = comm.reduce_scatter(bad_in, stream=comm.stream)   # the reduce-scatter's shard alike
+        torch.cuda.synchronize()
+        res.append(_host(rs, kind))
         comm.set_nonfinite(False)   # the quantiser's spec again: finite, whatever the input
         _allreduce(comm, kind, bad_in, out)
         torch.cuda.synchronize()
@@ -131,9 +134,11 @@ def test_nonfinite_local(gpu, orc, kind, world):
         grp.destroy()
         return res
 
-    for good, poisoned, again, spec in _run_ranks(world, rank):
+    assert n % world == 0
+    for good, poisoned, again, rs, spec in _run_ranks(world, rank):
         np.testing.assert_array_equal(good, want)
         assert _isnan(poisoned, kind).all()
+        assert rs.size == n // world and _isnan(rs, kind).all()
         np.testing.assert_array_equal(again, want)
         assert not _isnan(spec, kind).any()
 
