@@ -882,7 +882,7 @@ static int allreduce_f32_body(struct inccl_communicator *c, const float *const *
     if ((c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH) &&
         c->group->transport == INCCL_TRANSPORT_RCCL) {
         if (c->engine == INCCL_ENGINE_LL && n <= c->ll_max_bytes / sizeof(float) && W > 1)
-            return inccl_ll_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+            return inccl_ll_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, 0, 0, st);
         if (c->engine == INCCL_ENGINE_MESH) return inccl_mesh_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
         return inccl_p2p_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
     }
@@ -1113,6 +1113,12 @@ static int reduce_scatter_body(struct inccl_communicator *c, int kind, const voi
         return kerr(inccl_k_stream_s(INCCL_KIND_Q32, kind, s1, 1, dst, shard, k, amax, scale_R, c->out_shift, st));
     }
     const int ipc = c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH;
+    /* the ll engine's one kernel for a small fp32 bucket: every rank's quads
+     * published with a flag, this rank's shard summed and dequantised */
+    if (kind == INCCL_KIND_F32 && c->engine == INCCL_ENGINE_LL && c->group->transport == INCCL_TRANSPORT_RCCL &&
+        n <= c->ll_max_bytes / sizeof(float) && !(shard & 3))
+        return inccl_ll_piece(c, (const float *const *)srcs, R, (float *)dst, n, k, amax, scale_R, (size_t)me * shard,
+                              shard, st);
     if (ipc && c->group->transport == INCCL_TRANSPORT_RCCL && !(shard & 3) &&
         ((uintptr_t)dst & (kind == INCCL_KIND_F32 ? 15u : 7u)) == 0)
         return inccl_p2p_reduce_scatter(c, kind, srcs, R, dst, n, k, amax, scale_R, st);

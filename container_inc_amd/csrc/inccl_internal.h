@@ -167,9 +167,10 @@ int inccl_p2p_reduce_scatter(struct inccl_communicator *c, int kind, const void 
 int inccl_p2p_allreduce_q32(struct inccl_communicator *c, const int32_t *send, int32_t *recv, size_t n,
                             hipStream_t st);
 
-/* ll engine (ll.c): n <= c->ll_max_bytes / 4 */
+/* ll engine (ll.c): n <= c->ll_max_bytes / 4.  rs_n > 0: reduce-scatter, dst =
+ * elements [rs_lo, rs_lo + rs_n) of the result (both multiples of 4) */
 int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
-                   const uint32_t *amax, int scale_R, hipStream_t st);
+                   const uint32_t *amax, int scale_R, size_t rs_lo, size_t rs_n, hipStream_t st);
 void inccl_ll_release(struct inccl_communicator *c);
 uint64_t inccl_wait_ticks(struct inccl_group *g);   /* bound of an in-kernel wait */
 

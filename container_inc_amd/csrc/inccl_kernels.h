@@ -63,6 +63,8 @@ struct inccl_ll_launch {
     const uint32_t *amax_bits;
     int scale_R;
     int out_shift;                                     /* dequantise with 2^-(k + out_shift) */
+    size_t rs_lo, rs_n;                                /* rs_n > 0: reduce-scatter -- dst = elements
+                                                        * [rs_lo, rs_lo + rs_n) of the result (both % 4 == 0) */
 };
 int inccl_k_ll_grid(size_t n);
 int inccl_k_ll_oneshot(const struct inccl_ll_launch *l, void *stream);

@@ -57,6 +57,7 @@ struct LLArgs {
     int W, me;
     uint64_t timeout_ticks;         // s_memrealtime ticks
     Scale sc;
+    int64_t rs_lo4, rs_hi4;         // rs_hi4 > 0: reduce-scatter, dst = quads [rs_lo4, rs_hi4) of the result
 };
 
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
@@ -160,15 +161,19 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
     if constexpr (!WT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // every wave, before reading peer memory
 
     // 4. sum the W ranks' quads, dequantise into dst: all W loads of up to kU
-    //    quads in flight before the first add
+    //    quads in flight before the first add.  Reduce-scatter: only the quads
+    //    of this rank's shard, written from dst[0]
     constexpr int kU = 4;
+    const bool rs = a.rs_hi4 > 0;
+    const int64_t qlo = rs ? a.rs_lo4 : 0, qhi = rs ? a.rs_hi4 : nq;
+    const int64_t out_n = rs ? 4 * (qhi - qlo) : a.n;
     __amdgpu_buffer_rsrc_t peer[kMaxR];
     if constexpr (WT) {
 #pragma unroll
         for (int j = 0; j < kMaxR; ++j)
             if (j < a.W) peer[j] = rsrc(a.peer_data[j] + slot, (uint32_t)(nq * 16));
     }
-    const __amdgpu_buffer_rsrc_t dst_rs = rsrc(a.dst, (uint32_t)(a.n * 4));
+    const __amdgpu_buffer_rsrc_t dst_rs = rsrc(a.dst, (uint32_t)(out_n * 4));
     for (int64_t q0 = (int64_t)blockIdx.x * kLLBlock + tid; q0 < nq; q0 += stride * kU) {
         u32x4 x[kU][kMaxR];
 #pragma unroll
@@ -176,7 +181,7 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
             const int64_t q = q0 + u * stride;
 #pragma unroll
             for (int j = 0; j < kMaxR; ++j) {
-                if (j < a.W && q < nq) {
+                if (j < a.W && q >= qlo && q < qhi) {
                     if constexpr (WT) x[u][j] = __builtin_amdgcn_raw_buffer_load_b128(peer[j], (int)(q * 16), 0, kAuxSys);
                     else x[u][j] = reinterpret_cast<const u32x4*>(a.peer_data[j] + slot)[q];
                 }
@@ -186,6 +191,8 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
         for (int u = 0; u < kU; ++u) {
             const int64_t q = q0 + u * stride;
             if (q >= nq) break;
+            if (q < qlo || q >= qhi) continue;
+            const int64_t qo = q - qlo;   // the output quad
             u32x4 acc = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int j = 0; j < kMaxR; ++j)
@@ -200,13 +207,13 @@ __global__ __launch_bounds__(kLLBlock) void k_ll_oneshot(LLArgs a, int vec_src, 
             o.y = __float_as_uint((float)(int32_t)acc.y * inv);
             o.z = __float_as_uint((float)(int32_t)acc.z * inv);
             o.w = __float_as_uint((float)(int32_t)acc.w * inv);
-            if (vec_dst && 4 * q + 4 <= a.n) {
+            if (vec_dst && 4 * qo + 4 <= out_n) {
                 // write-through (sc1): nothing of dst stays dirty in this XCD's L2
-                __builtin_amdgcn_raw_buffer_store_b128(o, dst_rs, (int)(q * 16), 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(o, dst_rs, (int)(qo * 16), 0, 16);
             } else {
                 const uint32_t v[4] = {o.x, o.y, o.z, o.w};
                 for (int e = 0; e < 4; ++e)
-                    if (4 * q + e < a.n) reinterpret_cast<uint32_t*>(a.dst)[4 * q + e] = v[e];
+                    if (4 * qo + e < out_n) reinterpret_cast<uint32_t*>(a.dst)[4 * qo + e] = v[e];
             }
         }
     }
@@ -261,7 +268,8 @@ extern "C" int inccl_k_ll_grid(size_t n)
 
 extern "C" int inccl_k_ll_oneshot(const struct inccl_ll_launch* l, void* stream)
 {
-    if (!l || l->R < 1 || l->R > kMaxR || l->W < 2 || l->W > kMaxR || l->me < 0 || l->me >= l->W)
+    if (!l || l->R < 1 || l->R > kMaxR || l->W < 2 || l->W > kMaxR || l->me < 0 || l->me >= l->W ||
+        (l->rs_n && ((l->rs_lo | l->rs_n) & 3u || l->rs_lo + l->rs_n > l->n)))
         return INCCL_ERR_ARG;
     LLArgs a{};
     for (int r = 0; r < l->R; ++r) a.src.p[r] = l->src[r];
@@ -283,6 +291,8 @@ extern "C" int inccl_k_ll_oneshot(const struct inccl_ll_launch* l, void* stream)
     a.sc.amax_bits = l->amax_bits;
     a.sc.scale_R = l->scale_R;
     a.sc.out_shift = l->out_shift;
+    a.rs_lo4 = (int64_t)(l->rs_lo >> 2);
+    a.rs_hi4 = l->rs_n ? (int64_t)((l->rs_lo + l->rs_n) >> 2) : 0;
     int vs = 1;
     for (int r = 0; r < l->R; ++r) vs &= aligned16(l->src[r]) ? 1 : 0;
     const int vd = aligned16(l->dst) ? 1 : 0;

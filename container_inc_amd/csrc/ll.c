@@ -108,7 +108,7 @@ uint64_t inccl_wait_ticks(struct inccl_group *g)
 }
 
 int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
-                   const uint32_t *amax, int scale_R, hipStream_t st)
+                   const uint32_t *amax, int scale_R, size_t rs_lo, size_t rs_n, hipStream_t st)
 {
     const int W = c->group->world_size, me = c->group->rank;
     if (!c->ll_buf) {   /* the collective setup cannot run inside a graph capture */
@@ -144,6 +144,8 @@ int inccl_ll_piece(struct inccl_communicator *c, const float *const *srcs, int R
     l.amax_bits = amax;
     l.scale_R = scale_R;
     l.out_shift = c->out_shift;
+    l.rs_lo = rs_lo;
+    l.rs_n = rs_n;
     /* the parity argument needs this rank's calls in order: chain across streams
      * (inside a graph capture the caller's single capture stream orders them) */
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;

@@ -180,8 +180,10 @@ def _ipc_rank(rank, world, port, q, engine):
         q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "mesh"), (4, "meshw"), (2, "ll")])
+@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "mesh"), (4, "meshw"), (2, "ll"), (4, "ll")])
 def test_reduce_scatter_ipc_multiprocess(gpu, world, engine):
+    """ll: a small fp32 bucket (shard 4096) through the one-kernel ll reduce-
+    scatter; the others through the p2p pull-reduce or the int32 allreduce."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
