@@ -173,6 +173,8 @@ def _ipc_rank(rank, world, port, q, engine):
                     out = comm.reduce_scatter(srcs, stream=comm.stream)
                     torch.cuda.synchronize()
                     ok.append(bool(np.array_equal(_host(out, kind), want)))
+                if engine == "ll" and kind == "f32" and shard == 4096:
+                    comm.ipc_mem_kind("ll")   # raises unless the ll kernel's buffers exist: the ll route ran
         comm.destroy()
         grp.destroy()
         q.put((rank, ok, None))
