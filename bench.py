@@ -736,7 +736,8 @@ def rs_oracle_check(srcs, out_shard, lanes, k: int, rank: int, world: int) -> di
     return res
 
 
-def reduce_scatter_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256) -> list:
+def reduce_scatter_engines(comm, dev, R: int, rank: int, world: int, mib: float = 256,
+                           engines=("rccl", "p2p")) -> list:
     """N > 1: inccl_reduce_scatter_f32 of R resident `mib` MiB fp32 buckets per
     rank (each rank keeps its 1/W shard of the reduced bucket: the sharded-
     gradient callers' half of the allreduce) on rccl (ncclReduceScatter) and p2p
@@ -746,7 +747,7 @@ def reduce_scatter_engines(comm, dev, R: int, rank: int, world: int, mib: int = 
     fraction of its (W-1)/W * n * 4 bytes."""
     import torch
     import torch.distributed as dist
-    n = mib * (1 << 20) // 4
+    n = int(mib * (1 << 20)) // 4
     if n % world:
         return [{"skipped": f"{n} elements do not split into {world} shards"}]
     inputs = []
@@ -759,7 +760,7 @@ def reduce_scatter_engines(comm, dev, R: int, rank: int, world: int, mib: int = 
     torch.cuda.synchronize()
     rows, refs = [], None
     lanes = oracle_lanes(n, world, 1, 1 << 16)
-    for eng in ("rccl", "p2p"):
+    for eng in engines:
         set_stage(f"reduce_scatter {mib} MiB engine {eng}")
         ok, dt, same = 1, float("inf"), False
         try:
@@ -1751,6 +1752,9 @@ def main():
             if agree([time.monotonic() - T_START], world)[0] <= sweep_soft:
                 try:
                     res["reduce_scatter"] = reduce_scatter_engines(comm, dev, R, rank, world)
+                    for small in (1 / 16, 1.0):   # 64 KiB and 1 MiB buckets: the ll engine's one kernel too
+                        res["reduce_scatter"] += reduce_scatter_engines(comm, dev, R, rank, world, small,
+                                                                        ("rccl", "p2p", "ll"))
                 except Exception as e:  # noqa: BLE001
                     print(f"rank {rank}: reduce_scatter key failed: {e!r}", file=sys.stderr, flush=True)
                     res["reduce_scatter"] = {"error": repr(e)}
