@@ -1091,7 +1091,12 @@ static int reduce_scatter_body(struct inccl_communicator *c, int kind, const voi
                                names[kind], n, W);
     if (n == 0) return 0;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    const size_t shard = n / (size_t)W;
+    const size_t shard = n / (size_t)W, es = kind == INCCL_KIND_F32 ? 4 : 2;
+    for (int r = 0; r < R; ++r) {   /* the one-kernel routes read sources while writing dst */
+        const uintptr_t s0 = (uintptr_t)srcs[r], d0 = (uintptr_t)dst;
+        if (d0 < s0 + n * es && s0 < d0 + shard * es)
+            return inccl_set_error(INCCL_ERR_ARG, "reduce_scatter_%s: dst overlaps srcs[%d]", names[kind], r);
+    }
     const uint32_t *amax = NULL;
     int k = 0;
     int rc = resolve_scale(c, kind, srcs, R, n, scale_exp, st, &amax, &k);
