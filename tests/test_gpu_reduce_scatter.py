@@ -135,9 +135,9 @@ def test_reduce_scatter_rccl_world1(gpu, orc, monkeypatch):
             np.testing.assert_array_equal(_host(out, kind), want, err_msg=f"{kind} {eng}")
     with pytest.raises(Exception):
         comm.reduce_scatter([torch.zeros(10, device=gpu)], out=torch.zeros(3, device=gpu))   # wrong shard size
-    x = torch.zeros(64, device=gpu)
-    with pytest.raises(Exception):   # dst inside a source
-        comm.reduce_scatter([x], out=x[8:])
+    x = torch.zeros(128, device=gpu)
+    with pytest.raises(inccl.IncclError, match="overlaps"):   # a full-size dst that overlaps the source
+        comm.reduce_scatter([x[:64]], out=x[32:96])
     comm.destroy()
     grp.destroy()
 
