@@ -104,37 +104,43 @@ int inccl_stream_op(int in_kind, int out_kind, const void *const *srcs_dev, int 
 
 /* ---- ordering across caller streams ----
  * A communicator's calls share its workspaces (the int32 partials, the auto
- * scale's max word, the gather buffer).  A call on another stream than the
- * previous call's first waits for that call's end: ev[9], recorded at the end
- * of every call (an event outlives its stream, so the caller may have dropped
- * the previous stream since).  Captured calls are left to the capture's own
- * order. */
-static int ws_enter(struct inccl_communicator *c, void *stream, int *capturing)
+ * scale's max word, the gather buffer).  A call that uses one (inccl_ws_claim,
+ * before its first use) on another stream than the last such call's first
+ * waits for that call's end: ev[9], recorded at the end of every call that
+ * claimed the workspaces (an event outlives its stream, so the caller may have
+ * dropped the previous stream since).  Calls that touch no shared workspace --
+ * the single-GPU fused kernel at a fixed scale, the IPC engines on their own
+ * buffers -- record nothing: an event between back-to-back kernels costs the
+ * GPU about 3 us.  Captured calls are left to the capture's own order. */
+int inccl_ws_claim(struct inccl_communicator *c, hipStream_t st)
 {
-    const hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (c->ws_claimed) return 0;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     INCCL_HIP(hipStreamIsCapturing(st, &cs));
-    *capturing = cs != hipStreamCaptureStatusNone;
-    if (!*capturing && c->ws_last_stream && c->ws_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[9], 0));
+    c->ws_capturing = cs != hipStreamCaptureStatusNone;
+    if (!c->ws_capturing && c->ws_last_stream && c->ws_last_stream != st)
+        INCCL_HIP(hipStreamWaitEvent(st, c->ev[9], 0));
+    c->ws_claimed = 1;
+    c->ws_stream = st;
     return 0;
 }
 
-static int ws_leave(struct inccl_communicator *c, void *stream, int capturing, int rc)
+static int ws_leave(struct inccl_communicator *c, int rc)
 {
-    const hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    if (rc == 0 && !capturing) {
-        INCCL_HIP(hipEventRecord(c->ev[9], st));
-        c->ws_last_stream = st;
+    if (rc == 0 && c->ws_claimed && !c->ws_capturing) {
+        const hipError_t e = hipEventRecord(c->ev[9], c->ws_stream);
+        if (e == hipSuccess) c->ws_last_stream = c->ws_stream;
+        else rc = inccl_hip_check(e, "hipEventRecord(workspace order)");
     }
+    c->ws_claimed = 0;
     return rc;
 }
 
 #define INCCL_ORDERED(c, stream, call)                              \
     do {                                                            \
         if (!(c)) return (call);                                    \
-        int cap_ = 0, rc_ = ws_enter((c), (stream), &cap_);         \
-        if (rc_) return rc_;                                        \
-        return ws_leave((c), (stream), cap_, (call));               \
+        (c)->ws_claimed = 0;                                        \
+        return ws_leave((c), (call));                               \
     } while (0)
 
 /* ---- prepared stream ops ---- */
@@ -815,7 +821,9 @@ static int resolve_scale(struct inccl_communicator *c, int kind, const void *con
         return 0;
     }
     const int zf = 1 | (c->nonfinite == INCCL_NONFINITE_NAN ? INCCL_ABSMAX_FLAG_NONFINITE : 0);
-    int rc = kind == INCCL_KIND_BF16  ? inccl_absmax_bf16((const uint16_t *const *)srcs, R, n, c->d_words, zf, st)
+    int rc = inccl_ws_claim(c, st);   /* the max word is shared by every call */
+    if (rc) return rc;
+    rc = kind == INCCL_KIND_BF16  ? inccl_absmax_bf16((const uint16_t *const *)srcs, R, n, c->d_words, zf, st)
              : kind == INCCL_KIND_F16 ? inccl_absmax_f16((const uint16_t *const *)srcs, R, n, c->d_words, zf, st)
                                       : inccl_absmax_f32((const float *const *)srcs, R, n, c->d_words, zf, st);
     if (rc) return rc;
@@ -889,6 +897,8 @@ static int allreduce_f32_body(struct inccl_communicator *c, const float *const *
     /* RCCL's own allreduce on the int32 partials: quant + local sum -> in-place
      * ncclAllReduce(int32, sum) -> dequantise (the switch aggregate inside RCCL) */
     if (c->engine == INCCL_ENGINE_AR) {
+        rc = inccl_ws_claim(c, st);
+        if (rc) return rc;
         rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
         if (rc) return rc;
         int32_t *q = (int32_t *)c->d_q32;
@@ -905,9 +915,13 @@ static int allreduce_f32_body(struct inccl_communicator *c, const float *const *
         if (W > INCCL_MAX_LOCAL_INPUTS)
             return inccl_set_error(INCCL_ERR_ARG, "a2a engine sums at most %d shards", INCCL_MAX_LOCAL_INPUTS);
         const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
+        rc = inccl_ws_claim(c, st);
+        if (rc) return rc;
         rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, 2 * total * sizeof(int32_t));
         if (rc) return rc;
         if (total != n) {
+            rc = inccl_ws_claim(c, st);
+            if (rc) return rc;
             rc = inccl_ensure_dev(&c->d_f32, &c->d_f32_bytes, total * sizeof(float));
             if (rc) return rc;
         }
@@ -927,9 +941,13 @@ static int allreduce_f32_body(struct inccl_communicator *c, const float *const *
         ws_elems += shard * (size_t)W + shard;
         if (shard * (size_t)W != cnt) fws_elems = shard * (size_t)W;
     }
+    rc = inccl_ws_claim(c, st);
+    if (rc) return rc;
     rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, ws_elems * sizeof(int32_t));
     if (rc) return rc;
     if (fws_elems) {
+        rc = inccl_ws_claim(c, st);
+        if (rc) return rc;
         rc = inccl_ensure_dev(&c->d_f32, &c->d_f32_bytes, fws_elems * sizeof(float));
         if (rc) return rc;
     }
@@ -1012,10 +1030,14 @@ static int allreduce_16_body(struct inccl_communicator *c, int kind, const uint1
         /* quant + local sum -> reduce-scatter (int32) -> dequantise own shard to
          * bf16 -> all-gather (bf16), as allreduce_piece with a 2-byte result */
         const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
-        int rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, (total + shard) * sizeof(int32_t));
+        int rc = inccl_ws_claim(c, st);
+        if (rc) return rc;
+        rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, (total + shard) * sizeof(int32_t));
         if (rc) return rc;
         const int in_place = (total == n);
         if (!in_place) {
+            rc = inccl_ws_claim(c, st);
+            if (rc) return rc;
             rc = inccl_ensure_dev(&c->d_f32, &c->d_f32_bytes, total * sizeof(uint16_t));
             if (rc) return rc;
         }
@@ -1045,7 +1067,9 @@ static int allreduce_16_body(struct inccl_communicator *c, int kind, const uint1
     /* every other engine (and a p2p dst that is not 4-B aligned): its int32
      * allreduce of the quantised partials (RCCL all-reduce for "ar" / "a2a",
      * the p2p exchange for the IPC engines) */
-    int rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
+    int rc = inccl_ws_claim(c, st);
+    if (rc) return rc;
+    rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
     if (rc) return rc;
     int32_t *q = (int32_t *)c->d_q32;
     rc = kerr(inccl_k_stream(kind, INCCL_KIND_Q32, srcs, R, q, n, k, amax, scale_R, st));
@@ -1107,6 +1131,8 @@ static int reduce_scatter_body(struct inccl_communicator *c, int kind, const voi
         return kerr(inccl_k_stream_s(kind, kind, srcs, R, dst, n, k, amax, scale_R, c->out_shift, st));
     if (c->engine == INCCL_ENGINE_RCCL || c->group->transport == INCCL_TRANSPORT_LOCAL) {
         /* quant + local sum -> int32 reduce-scatter -> dequantise the shard */
+        rc = inccl_ws_claim(c, st);
+        if (rc) return rc;
         rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, (n + shard) * sizeof(int32_t));
         if (rc) return rc;
         int32_t *qsend = (int32_t *)c->d_q32, *qrecv = qsend + n;
@@ -1129,6 +1155,8 @@ static int reduce_scatter_body(struct inccl_communicator *c, int kind, const voi
         return inccl_p2p_reduce_scatter(c, kind, srcs, R, dst, n, k, amax, scale_R, st);
     /* every other engine, or a shard the pull-reduce cannot take: the engine's
      * int32 allreduce, then the shard dequantised */
+    rc = inccl_ws_claim(c, st);
+    if (rc) return rc;
     rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
     if (rc) return rc;
     int32_t *q = (int32_t *)c->d_q32;

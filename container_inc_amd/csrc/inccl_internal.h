@@ -119,7 +119,9 @@ struct inccl_communicator {
     struct inccl_d2h_worker *d2h;  /* issues pageable D2H copies beside the H2Ds (hostdma.c) */
     hipEvent_t ev[10];           /* [8]: p2p ordering across caller streams; [9]: workspace ordering
                                   * across caller streams (ws_last_stream) */
-    hipStream_t ws_last_stream;  /* the stream of the communicator's last call (api.c ws_enter) */
+    hipStream_t ws_last_stream;  /* the stream of the last call that used the shared workspaces */
+    hipStream_t ws_stream;       /* this call's stream, once it claimed them (inccl_ws_claim) */
+    int ws_claimed, ws_capturing;
     hipStream_t p2p_last_stream;
 };
 
@@ -222,6 +224,9 @@ static inline size_t inccl_shard_elems(size_t n, int world)
 }
 
 int inccl_ensure_dev(void **p, size_t *cur, size_t need);
+/* before a call first uses the communicator's shared workspaces (d_q32, d_f32,
+ * d_words): orders it after the last call that used them on another stream */
+int inccl_ws_claim(struct inccl_communicator *c, hipStream_t st);
 /* IPC-shared device memory polled by running kernels (ll, mesh): $INCCL_IPC_MEM */
 unsigned inccl_ipc_mem_flags(void);
 hipError_t inccl_ipc_malloc(void **p, size_t bytes);

@@ -259,7 +259,9 @@ int inccl_local_allreduce_q32(struct inccl_communicator *c, const int32_t *send,
     struct inccl_local_hub *h = c->group->hub;
     const int W = h->world_size;
     /* sum into private scratch first: recv may alias a buffer a peer is still reading */
-    int rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
+    int rc = inccl_ws_claim(c, st);
+    if (rc) return rc;
+    rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
     if (rc) return rc;
     rc = hub_publish(c, send, st);
     if (rc) return rc;
