@@ -1144,6 +1144,12 @@ static int reduce_scatter_body(struct inccl_communicator *c, int kind, const voi
         return kerr(inccl_k_stream_s(INCCL_KIND_Q32, kind, s1, 1, dst, shard, k, amax, scale_R, c->out_shift, st));
     }
     const int ipc = c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH;
+    const uintptr_t dst_align = kind == INCCL_KIND_F32 ? 15u : 7u;
+    /* the mesh engines: their one persistent kernel, each reduce writing its
+     * chunk of this rank's shard into dst (shards of whole 64-element groups) */
+    if (c->engine == INCCL_ENGINE_MESH && c->group->transport == INCCL_TRANSPORT_RCCL && !(shard % 64) &&
+        ((uintptr_t)dst & dst_align) == 0)
+        return inccl_mesh_reduce_scatter(c, kind, srcs, R, dst, n, k, amax, scale_R, st);
     /* the ll engine's one kernel for a small fp32 bucket: every rank's quads
      * published with a flag, this rank's shard summed and dequantised */
     if (kind == INCCL_KIND_F32 && c->engine == INCCL_ENGINE_LL && c->group->transport == INCCL_TRANSPORT_RCCL &&

@@ -181,6 +181,8 @@ int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int
                      const uint32_t *amax, int scale_R, hipStream_t st);
 int inccl_mesh_piece16(struct inccl_communicator *c, int kind, const uint16_t *const *srcs, int R, uint16_t *dst,
                        size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st);
+int inccl_mesh_reduce_scatter(struct inccl_communicator *c, int kind, const void *const *srcs, int R, void *dst,
+                              size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st);
 void inccl_mesh_release(struct inccl_communicator *c);
 
 /* local transport */

@@ -88,6 +88,7 @@ struct inccl_mesh_launch {
     uint32_t *peer_resin[INCCL_MAX_LOCAL_INPUTS];      /* every rank's result inbox (push_res) */
     const uint32_t *own_resin;
     int push_res;                                      /* 1: reduce pushes results, gather copies locally */
+    int rs;                                            /* 1: reduce-scatter -- dst is this rank's shard */
     int kind16;                                        /* 0: fp32 src / dst; INCCL_KIND_BF16 / _F16: 2-byte ones */
     uint32_t *peer_sig[INCCL_MAX_LOCAL_INPUTS];        /* every rank's signal array */
     const uint32_t *own_sig;

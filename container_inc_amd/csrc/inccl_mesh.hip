@@ -88,6 +88,7 @@ struct MeshArgs {
     uint32_t* err;                       // host-mapped error word
     uint64_t timeout_ticks;
     int nchunks, W, me, lag, vec_src, vec_dst, push_res;
+    int rs;                              // reduce-scatter: reduce(c) writes dst (the shard), gathers only wait
     Scale sc;
 };
 
@@ -241,9 +242,12 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
         in[j] = rsrc(a.own_inbox + (int64_t)(j < a.W ? j : 0) * a.inbox_stride + (int64_t)c * a.chunk, bytes);
     constexpr int ES = is16(E) ? 2 : 4;   // result element bytes
     const uint32_t obytes = (uint32_t)(nq * 4 * ES);
-    const __amdgpu_buffer_rsrc_t res = rsrc(reinterpret_cast<const char*>(a.own_res) + (int64_t)c * a.chunk * ES, obytes);
+    // reduce-scatter: the chunk goes straight into dst, this rank's shard
+    const char* rbase = a.rs ? reinterpret_cast<const char*>(a.dst) : reinterpret_cast<const char*>(a.own_res);
+    const __amdgpu_buffer_rsrc_t res = rsrc(rbase + (int64_t)c * a.chunk * ES, obytes);
+    const bool push = a.push_res && !a.rs;
     __amdgpu_buffer_rsrc_t outs[kMaxR];   // push_res: my slot of every rank's result inbox
-    if (a.push_res) {
+    if (push) {
 #pragma unroll
         for (int j = 0; j < kMaxR; ++j)
             outs[j] = rsrc(reinterpret_cast<const char*>(a.peer_resin[j < a.W ? j : 0]) +
@@ -272,7 +276,7 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
             }
             if constexpr (is16(E)) {
                 const u32x2 o = {deq16x2<E>(acc.x, acc.y, inv), deq16x2<E>(acc.z, acc.w, inv)};
-                if (a.push_res) {
+                if (push) {
 #pragma unroll
                     for (int j = 0; j < kMaxR; ++j)
                         if (j < a.W) __builtin_amdgcn_raw_buffer_store_b64(o, outs[j], (int)(q * 8), 0, kAuxSys);
@@ -285,7 +289,7 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
                 o.y = __float_as_uint((float)(int32_t)acc.y * inv);
                 o.z = __float_as_uint((float)(int32_t)acc.z * inv);
                 o.w = __float_as_uint((float)(int32_t)acc.w * inv);
-                if (a.push_res) {
+                if (push) {
 #pragma unroll
                     for (int j = 0; j < kMaxR; ++j)
                         if (j < a.W) st_sys16(outs[j], (uint32_t)(q * 16), o);
@@ -301,12 +305,15 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
     return true;
 }
 
-// gather(c, j): rank j's result chunk c -> dst (clipped to n)
+// gather(c, j): rank j's result chunk c -> dst (clipped to n).  Reduce-scatter:
+// the wait alone -- the call then ends only after every rank has reduced every
+// chunk, i.e. read its inbox, which is what lets the next call push into it
 __device__ bool do_gather(const MeshArgs& a, int c, int j, uint32_t epoch)
 {
     bool ok = true;
     if (threadIdx.x == 0) ok = wait_flag(a, a.own_sig + ready_idx(j, c), epoch);
     if (!__syncthreads_and(ok)) return false;
+    if (a.rs) return true;
     const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;
     if (lo >= a.n) return true;
     int64_t cnt = chunk_len(a, c);
@@ -351,6 +358,7 @@ __device__ bool do_gather16(const MeshArgs& a, int c, int j, uint32_t epoch)
     bool ok = true;
     if (threadIdx.x == 0) ok = wait_flag(a, a.own_sig + ready_idx(j, c), epoch);
     if (!__syncthreads_and(ok)) return false;
+    if (a.rs) return true;
     const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;
     if (lo >= a.n) return true;
     int64_t cnt = chunk_len(a, c);
@@ -457,6 +465,7 @@ extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
     }
     a.own_resin = l->own_resin;
     a.push_res = l->push_res ? 1 : 0;
+    a.rs = l->rs ? 1 : 0;
     if (a.push_res && (l->own_resin == nullptr || l->peer_resin[0] == nullptr)) return INCCL_ERR_ARG;
     a.own_inbox = l->own_inbox;
     a.own_res = l->own_res;

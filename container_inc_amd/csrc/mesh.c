@@ -221,10 +221,12 @@ static size_t mesh_chunk(size_t shard)
 }
 
 static int mesh_piece(struct inccl_communicator *c, int kind16, const void *const *srcs, int R, void *dst, size_t n,
-                      int k, const uint32_t *amax, int scale_R, hipStream_t st)
+                      int k, const uint32_t *amax, int scale_R, int rs, hipStream_t st)
 {
     const int W = c->group->world_size, me = c->group->rank;
     const size_t shard = inccl_shard_elems(n, W);
+    if (rs && shard * (size_t)W != n)
+        return inccl_set_error(INCCL_ERR_ARG, "mesh reduce-scatter: %zu elements are not %d shards of 64k", n, W);
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     INCCL_HIP(hipStreamIsCapturing(st, &cap));
     const int capturing = cap != hipStreamCaptureStatusNone;
@@ -268,6 +270,7 @@ static int mesh_piece(struct inccl_communicator *c, int kind16, const void *cons
     }
     l.own_resin = l.peer_resin[me];
     l.push_res = c->mesh_push;
+    l.rs = rs;
     l.own_inbox = l.peer_inbox[me];
     l.own_res = (uint32_t *)l.peer_res[me];
     l.own_sig = (const uint32_t *)c->mesh_buf;
@@ -296,7 +299,16 @@ static int mesh_piece(struct inccl_communicator *c, int kind16, const void *cons
 int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int R, float *dst, size_t n, int k,
                      const uint32_t *amax, int scale_R, hipStream_t st)
 {
-    return mesh_piece(c, 0, (const void *const *)srcs, R, dst, n, k, amax, scale_R, st);
+    return mesh_piece(c, 0, (const void *const *)srcs, R, dst, n, k, amax, scale_R, 0, st);
+}
+
+/* reduce-scatter (inccl_reduce_scatter_*): the same kernel, each reduce writing
+ * its chunk into dst (this rank's n / W elements, n % (64 W) == 0) and the
+ * gathers reduced to their waits; kind INCCL_KIND_F32, BF16 or F16 */
+int inccl_mesh_reduce_scatter(struct inccl_communicator *c, int kind, const void *const *srcs, int R, void *dst,
+                              size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st)
+{
+    return mesh_piece(c, kind == INCCL_KIND_F32 ? 0 : kind, srcs, R, dst, n, k, amax, scale_R, 1, st);
 }
 
 /* bf16 / fp16 buckets: the same kernel with 2-byte sources, int32 partials and a
@@ -305,5 +317,5 @@ int inccl_mesh_piece16(struct inccl_communicator *c, int kind, const uint16_t *c
                        size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st)
 {
     if (kind != INCCL_KIND_BF16 && kind != INCCL_KIND_F16) return inccl_set_error(INCCL_ERR_ARG, "mesh: bad kind %d", kind);
-    return mesh_piece(c, kind, (const void *const *)srcs, R, dst, n, k, amax, scale_R, st);
+    return mesh_piece(c, kind, (const void *const *)srcs, R, dst, n, k, amax, scale_R, 0, st);
 }

@@ -178,6 +178,8 @@ def _ipc_rank(rank, world, port, q, engine):
                     ok.append(bool(np.array_equal(_host(out, kind), want)))
                 if engine == "ll" and kind == "f32" and shard == 4096:
                     comm.ipc_mem_kind("ll")   # raises unless the ll kernel's buffers exist: the ll route ran
+                if engine in ("mesh", "meshw") and shard == 1 << 18:
+                    comm.ipc_mem_kind("mesh")   # the persistent kernel's reduce-scatter route ran
         comm.destroy()
         grp.destroy()
         q.put((rank, ok, None))
@@ -185,10 +187,13 @@ def _ipc_rank(rank, world, port, q, engine):
         q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "mesh"), (4, "meshw"), (2, "ll"), (4, "ll")])
+@pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "mesh"), (3, "mesh"), (4, "meshw"), (2, "ll"),
+                                         (4, "ll")])
 def test_reduce_scatter_ipc_multiprocess(gpu, world, engine):
     """ll: a small fp32 bucket (shard 4096) through the one-kernel ll reduce-
-    scatter; the others through the p2p pull-reduce or the int32 allreduce."""
+    scatter; mesh / meshw: the persistent kernel's reduce-scatter (shards of
+    whole 64-element groups); the others through the p2p pull-reduce or the
+    int32 allreduce (shard 1001)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
