@@ -304,7 +304,9 @@ int inccl_absmax_f16(const uint16_t *const *srcs_dev, int R, size_t n, uint32_t 
  * the in-process transport quant + local sum -> int32 reduce-scatter ->
  * dequantise the shard; "ll" with an fp32 bucket of at most INCCL_LL_MAX_BYTES
  * (shard % 4 == 0): its one kernel, this rank's shard summed from every peer's
- * published quads; "p2p", "ll", "mesh", "meshw" (shard % 4 == 0, dst
+ * published quads; "mesh" / "meshw" (shard % 64 == 0, dst aligned as below):
+ * the persistent kernel, each reduce writing its chunk of the shard into dst;
+ * "p2p", "ll", "mesh", "meshw" (shard % 4 == 0, dst
  * 16-B aligned for fp32, 8-B for 2-byte kinds) quant + local sum into the IPC
  * buffer -> barrier -> one kernel pulls shard r from every peer, sums and
  * dequantises into dst -> barrier; otherwise the engine's int32 allreduce and
