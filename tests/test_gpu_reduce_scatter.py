@@ -254,3 +254,44 @@ def test_calls_on_alternating_streams(gpu, orc):
             np.testing.assert_array_equal(gx, want_x)
             np.testing.assert_array_equal(gy, want_y)
             np.testing.assert_array_equal(grs, want_x[r * shard:(r + 1) * shard])
+
+
+@pytest.mark.parametrize("engine", ["rccl", "ar"])
+def test_reduce_scatter_graph_capture_world1(gpu, orc, monkeypatch, engine):
+    """inccl_reduce_scatter_f32 captured into a hipGraph on the RCCL engines
+    (world 1, the sharded route forced: a real ncclReduceScatter / ncclAllReduce
+    in the graph): three captured calls replayed with fresh inputs, bit-exact."""
+    import torch
+    from container_inc_amd import inccl
+    monkeypatch.setenv("INCCL_FORCE_RCCL", "1")
+    monkeypatch.setenv("INCCL_FORCE_SHARDED", "1")
+    monkeypatch.setenv("INCCL_MASTER_PORT", "0")
+    grp = inccl.inccl_group_create(1, 0, "127.0.0.1")
+    comm = inccl.inccl_communicator_create(grp, 0)
+    comm.set_engine(engine)
+    n = (1 << 18) + 64
+    bufs = [torch.empty(n, device=gpu) for _ in range(2)]
+    outs = [torch.empty(n, device=gpu) for _ in range(3)]
+    st = torch.cuda.Stream(device=gpu)
+    comm.reduce_scatter(bufs, out=outs[0], scale_exp=24, stream=st.cuda_stream)   # workspaces sized eagerly
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=st):
+        for o in outs:
+            comm.reduce_scatter(bufs, out=o, scale_exp=24, stream=st.cuda_stream)
+    rng = np.random.default_rng(79)
+    for _ in range(3):
+        hs = [_bucket(rng, n, "f32") for _ in range(2)]
+        for b, h in zip(bufs, hs):
+            b.copy_(torch.from_numpy(h).to(gpu))
+        for o in outs:
+            o.fill_(float("nan"))
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+        want = orc.reduce_f32(hs, 24)
+        for o in outs:
+            np.testing.assert_array_equal(_host(o, "f32"), want)
+    del graph
+    comm.destroy()
+    grp.destroy()
