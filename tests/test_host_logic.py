@@ -147,7 +147,16 @@ def _oracle_check_rank(rank, world, port, q):
     mb = [torch.from_numpy(hb[rank * R + j].view(np.int16)).view(torch.bfloat16) for j in range(R)]
     ob = torch.from_numpy(wb.view(np.int16).copy()).view(torch.bfloat16)
     gb = bench.oracle_check(mb, ob, bench.oracle_lanes(300, world, 1, 50), k, rank, world, fmt="bf16")
-    q.put((rank, good["mismatches"], bad["mismatches"], gb["mismatches"]))
+    # reduce-scatter: each rank holds only its shard of the result
+    shard = n // world
+    rs_out = torch.from_numpy(want[rank * shard:(rank + 1) * shard].copy())
+    rs_good = bench.rs_oracle_check(mine, rs_out, lanes, k, rank, world)
+    if rank == 1:   # a wrong lane inside rank 1's shard
+        inside = [l for l in lanes if shard <= l < 2 * shard][2] - shard
+        rs_out[inside] = rs_out[inside] + 1.0
+    rs_bad = bench.rs_oracle_check(mine, rs_out, lanes, k, rank, world)
+    q.put((rank, good["mismatches"], bad["mismatches"], gb["mismatches"], rs_good["mismatches"],
+           rs_bad["mismatches"]))
     dist.destroy_process_group()
 
 
@@ -166,8 +175,9 @@ def test_bench_oracle_check_gloo_world2():
     ps = [ctx.Process(target=_oracle_check_rank, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict((r, (g, b, h)) for r, g, b, h in (q.get(timeout=120) for _ in ps))
+    res = dict((t[0], t[1:]) for t in (q.get(timeout=120) for _ in ps))
     for p in ps:
         p.join(timeout=60)
-    assert res[0] == (0, 1, 0)             # rank 0 reports: clean, one bad lane, clean bf16
-    assert res[1] == (None, None, None)    # other ranks only contribute
+    # rank 0 reports: clean, one bad lane, clean bf16; reduce-scatter clean, one bad lane in rank 1's shard
+    assert res[0] == (0, 1, 0, 0, 1)
+    assert res[1] == (None,) * 5           # other ranks only contribute
