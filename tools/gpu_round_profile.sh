@@ -9,7 +9,7 @@ cd "$GRAFT_REPO_ROOT" || exit 3
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --durations=40 --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
   [ $rc -eq 0 ] || { grep -E "FAIL|Error" gpurun_out/pytest_gpu.log | head -20; exit $rc; }
 fi
