@@ -508,6 +508,8 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     const char *llb = getenv("INCCL_LL_MAX_BYTES");   /* small-bucket one-kernel path; 0 disables */
     c->ll_max_bytes = llb ? (size_t)strtoull(llb, NULL, 0) : ((size_t)1 << 20);
     if (c->ll_max_bytes > ((size_t)1 << 30)) c->ll_max_bytes = (size_t)1 << 30;   /* 32-bit buffer offsets */
+    const char *arb = getenv("INCCL_RCCL_AR_BYTES");  /* rccl engine: one all-reduce up to this; 0 disables */
+    c->rccl_ar_bytes = arb ? (size_t)strtoull(arb, NULL, 0) : ((size_t)1 << 20);
     const char *eng = getenv("INCCL_ENGINE");
     if (eng && *eng && g->transport == INCCL_TRANSPORT_RCCL) {
         int rc = inccl_comm_set_engine(c, eng);
@@ -862,6 +864,14 @@ int inccl_allreduce_f32(struct inccl_communicator *c, const float *const *srcs_d
     return inccl_allreduce_f32_pipelined(c, srcs_dev, R, dst_dev, n, scale_exp, 1, stream);
 }
 
+/* the rccl engine's small-bucket route: n int32 partials within rccl_ar_bytes
+ * (INCCL_RCCL_AR_BYTES, default 1 MiB) go through one ncclAllReduce */
+static int rccl_small(const struct inccl_communicator *c, size_t n)
+{
+    return c->engine == INCCL_ENGINE_RCCL && c->group->transport == INCCL_TRANSPORT_RCCL &&
+           n <= c->rccl_ar_bytes / sizeof(int32_t);
+}
+
 static int allreduce_f32_body(struct inccl_communicator *c, const float *const *srcs_dev, int R, float *dst_dev,
                               size_t n, int scale_exp, int chunks, void *stream)
 {
@@ -895,8 +905,10 @@ static int allreduce_f32_body(struct inccl_communicator *c, const float *const *
         return inccl_p2p_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
     }
     /* RCCL's own allreduce on the int32 partials: quant + local sum -> in-place
-     * ncclAllReduce(int32, sum) -> dequantise (the switch aggregate inside RCCL) */
-    if (c->engine == INCCL_ENGINE_AR) {
+     * ncclAllReduce(int32, sum) -> dequantise (the switch aggregate inside RCCL).
+     * The rccl engine takes it too for small buckets: one collective launch in
+     * place of two where latency, not bytes, sets the time. */
+    if (c->engine == INCCL_ENGINE_AR || rccl_small(c, n)) {
         rc = inccl_ws_claim(c, st);
         if (rc) return rc;
         rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
@@ -1026,9 +1038,10 @@ static int allreduce_16_body(struct inccl_communicator *c, int kind, const uint1
         return kerr(inccl_k_stream_s(kind, kind, srcs, R, dst_dev, n, k, amax, scale_R,
                                      c->out_shift, st));
 
-    if (c->engine == INCCL_ENGINE_RCCL || c->group->transport == INCCL_TRANSPORT_LOCAL) {
+    if ((c->engine == INCCL_ENGINE_RCCL && !rccl_small(c, n)) || c->group->transport == INCCL_TRANSPORT_LOCAL) {
         /* quant + local sum -> reduce-scatter (int32) -> dequantise own shard to
-         * bf16 -> all-gather (bf16), as allreduce_piece with a 2-byte result */
+         * bf16 -> all-gather (bf16), as allreduce_piece with a 2-byte result;
+         * small buckets fall through to the one-all-reduce route at the end */
         const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
         int rc = inccl_ws_claim(c, st);
         if (rc) return rc;

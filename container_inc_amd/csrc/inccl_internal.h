@@ -99,6 +99,8 @@ struct inccl_communicator {
     uint64_t ll_timeout_ticks;
     hipStream_t ll_last_stream;  /* ordering across caller streams (ev[7]) */
     size_t ll_max_bytes;         /* buckets up to this size take the ll kernel */
+    size_t rccl_ar_bytes;        /* rccl engine: int32 partials up to this size take one
+                                    ncclAllReduce instead of reduce-scatter + all-gather */
     /* mesh engine (large buckets, one persistent kernel per call): one IPC buffer
      * per rank = signal array + counters + inbox (W partial shards) + result shard */
     char *mesh_buf;                                        /* = mesh_reg[0]: signals + counters */

@@ -162,7 +162,9 @@ int inccl_rccl_version(int *compiled, int *loaded);
 void *inccl_comm_stream(struct inccl_communicator *comm);
 int inccl_comm_barrier(struct inccl_communicator *comm);
 /* Exchange engine of a multi-process communicator for inccl_allreduce_f32:
- *   "rccl"  quant+sum -> ncclReduceScatter(int32) -> dequant -> ncclAllGather (default)
+ *   "rccl"  quant+sum -> ncclReduceScatter(int32) -> dequant -> ncclAllGather (default);
+ *           buckets whose int32 partials fit $INCCL_RCCL_AR_BYTES (default 1 MiB) take
+ *           quant+sum -> ncclAllReduce(int32) -> dequant, as "ar"
  *   "a2a"   quant+sum -> grouped ncclSend/Recv of int32 shards -> this library's fused
  *           sum + dequantise kernel over the W shards -> ncclAllGather
  *   "p2p"   library buffers shared via HIP IPC; each GPU pulls its shard from every

@@ -455,6 +455,38 @@ def test_rccl_world1_paths(gpu, orc, force_rccl):
     grp.destroy()
 
 
+@pytest.mark.parametrize("ar_bytes", [None, "0", str(1 << 16)])
+def test_rccl_small_bucket_route(gpu, orc, force_rccl, monkeypatch, ar_bytes):
+    """The rccl engine's small buckets (int32 partials within
+    INCCL_RCCL_AR_BYTES, default 1 MiB) take one ncclAllReduce instead of
+    reduce-scatter + all-gather; 0 disables it, 64 KiB splits the sizes below
+    across both routes.  Every size and format is bit-exact either way."""
+    import torch
+    from container_inc_amd import inccl
+    if ar_bytes is not None:
+        monkeypatch.setenv("INCCL_RCCL_AR_BYTES", ar_bytes)
+    grp = inccl.inccl_group_create(1, 0, "127.0.0.1")
+    comm = inccl.inccl_communicator_create(grp, 0)
+    assert grp.transport == "rccl" and comm.engine == "rccl"
+    rng = np.random.default_rng(17)
+    for n in (1, 1000, 16384, 16385, (1 << 18) + 3, (1 << 18) + 64):
+        xs = [rng.standard_normal(n).astype(np.float32) for _ in range(2)]
+        out = comm.allreduce_f32([torch.from_numpy(x).to(gpu) for x in xs], scale_exp=inccl.SCALE_AUTO)
+        torch.cuda.synchronize()
+        k = orc.choose_scale(orc.absmax(xs), 2)
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), orc.reduce_f32(xs, k).view(np.uint32),
+                                      err_msg=str(n))
+        hs = [orc.f32_to_bf16(x) for x in xs]
+        srcs = [torch.from_numpy(h.view(np.int16)).to(gpu).view(torch.bfloat16) for h in hs]
+        out16 = torch.empty(n, dtype=torch.bfloat16, device=gpu)
+        comm.allreduce_bf16(srcs, out=out16, scale_exp=24, stream=comm.stream)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out16.view(torch.int16).cpu().numpy().view(np.uint16),
+                                      orc.reduce_bf16(hs, 24), err_msg=str(n))
+    comm.destroy()
+    grp.destroy()
+
+
 @pytest.mark.parametrize("engine,chunks", [("rccl", 1), ("rccl", 3), ("ar", 1), ("a2a", 1)])
 def test_rccl_world1_graph_capture(gpu, orc, force_rccl, engine, chunks):
     """allreduce_f32 captured into a hipGraph (as a framework that graphs its
