@@ -299,6 +299,17 @@ int orc_switch_init_ring(orc_switch *sw, int fan_in, uint32_t slots)
     sw->fan_in = fan_in;
     sw->slots = slots;
     sw->window = slots / 2;                                    /* nts.c:21-22: N = 2 * WINDOW_SIZE */
+    sw->root = 1;
+    return 0;
+}
+
+int orc_switch_init_nonroot(orc_switch *sw, int fan_in, uint32_t slots, int flags)
+{
+    /* the parent's port is bit fan_in of the bitmap, as the result bit (nts.c:59, :366) */
+    if ((flags & ~(ORC_SW_WIRE_ORDER | ORC_SW_RECYCLE)) || orc_switch_init_ring(sw, fan_in, slots) != 0)
+        return -1;
+    sw->root = 0;
+    sw->flags = flags;
     return 0;
 }
 
@@ -358,6 +369,61 @@ static int sw_data(orc_switch *sw, int port, uint32_t psn, const uint8_t *payloa
         return ORC_SW_BROADCAST;
     }
     return ORC_SW_ABSORBED;
+}
+
+/* The non-root branch of nts.c:376-400 / :457-482 for one UP data packet. */
+static int sw_data_nonroot(orc_switch *sw, int port, uint32_t psn, const uint8_t *payload_be_bytes,
+                           const uint8_t *reth)
+{
+    const uint32_t s = SLOT(sw, psn);
+    const uint32_t port_bit = 1u << port;
+    const uint32_t result_bit = 1u << sw->fan_in;              /* "received from the parent" (nts.c:378) */
+    sw->degree[s] += 1;                                        /* nts.c:351, :431 */
+
+    if (sw->arrival_state[s] & port_bit) {                     /* nts.c:377 / :458 retransmission */
+        if (sw->arrival_state[s] & result_bit) {               /* :378-380 / :459-461 replay to the port */
+            sw->replays++;
+            return ORC_SW_REPLAY;
+        }
+        /* :381-384 / :462-465: every child retransmits when none got the
+         * result, so the aggregate goes up again once per round of them */
+        if (sw_all_fan_in(sw, s) && sw->degree[s] % sw->fan_in == 0) return ORC_SW_FORWARD;
+        return ORC_SW_DROPPED;
+    }
+    /* first transmission: nts.c:388-392 / :469-474 */
+    sw->arrival_state[s] |= port_bit;
+    if (reth) memcpy(sw->reth_keeper[s][port], reth, ORC_RETH_HDR);
+    {
+        uint32_t *acc = (uint32_t *)sw->aggregator[s];
+        for (int i = 0; i < ORC_LANES; ++i) {
+            uint32_t w;
+            memcpy(&w, payload_be_bytes + 4 * i, 4);
+            acc[i] += to_be(w);                                /* ntohl */
+        }
+    }
+    sw->adds++;
+    return sw_all_fan_in(sw, s) ? ORC_SW_FORWARD : ORC_SW_ABSORBED;   /* :394-397 / :476-479 */
+}
+
+/* DOWN_DATA / DOWN_WRITE_FIRST_ONLY from the parent (nts.c:408-423 / :484-499) */
+static int sw_down(orc_switch *sw, uint32_t psn, const uint8_t *payload_be_bytes)
+{
+    const uint32_t s = SLOT(sw, psn);
+    const uint32_t result_bit = 1u << sw->fan_in;
+    /* :412 / :488: taken only once, and only after every child's arrival */
+    if ((sw->arrival_state[s] & result_bit) || !sw_all_fan_in(sw, s)) return ORC_SW_DROPPED;   /* :420-422 */
+    if (sw->flags & ORC_SW_WIRE_ORDER) {
+        for (int i = 0; i < ORC_LANES; ++i) {
+            uint32_t w;
+            memcpy(&w, payload_be_bytes + 4 * i, 4);
+            sw->aggregator[s][i] = (int32_t)to_be(w);          /* ntohl, as the UP path adds */
+        }
+    } else {
+        memcpy(sw->aggregator[s], payload_be_bytes, ORC_PAYLOAD_LEN);   /* :413 / :489, wire bytes as they are */
+    }
+    sw->arrival_state[s] |= result_bit;                        /* :414 / :490 */
+    if (sw->flags & ORC_SW_RECYCLE) sw_clear(sw, psn + sw->window);
+    return ORC_SW_DOWN;
 }
 
 int orc_switch_ingress(orc_switch *sw, int port, uint32_t psn,
@@ -529,13 +595,55 @@ static void conn_hdr(orc_frame_hdr *h, const orc_conn *c, uint32_t psn, uint8_t 
 static int is_data_op(uint8_t op) { return op == 0x00 || op == 0x01 || op == 0x02 || op == 0x04 || op == 0x07 || op == 0x08; }
 static int is_wf_op(uint8_t op) { return op == 0x06 || op == 0x0A; }
 
+/* pipeline() of a non-root switch (root == 0, nts.c:303-501): ports below
+ * fan_in are children (UP_*), port fan_in the parent (DOWN_*, :320-343). */
+static int pipeline_nonroot(orc_switch *sw, const orc_conn *conns, int port, const uint8_t *frame, size_t row_len,
+                            uint8_t *out, size_t out_stride, int *out_len)
+{
+    const int F = sw->fan_in, up = port < F;
+    const uint8_t op = frame[42];
+    const uint32_t psn = ((uint32_t)frame[51] << 16) | ((uint32_t)frame[52] << 8) | frame[53];   /* :311 */
+    const int udp_len = ((int)frame[38] << 8) | frame[39];
+    orc_frame_hdr h;
+    if (op == 0x11) {
+        if (!up) return ORC_SW_IGNORED;                        /* DOWN_ACK: "impossible" (:424-426) */
+        conn_hdr(&h, &conns[port], psn, 0x11);                 /* UP_ACK: reflect (:403-406) */
+        out_len[port] = (int)orc_build_ack_frame(out + (size_t)port * out_stride, &h, psn + 1);
+        return ORC_SW_ACK;
+    }
+    if (!is_data_op(op) && !is_wf_op(op)) return ORC_SW_IGNORED;
+    const int wf = is_wf_op(op);
+    const int data_len = udp_len - ORC_BTH_HDR - ORC_UDP_HDR - ORC_ICRC_LEN - (wf ? ORC_RETH_HDR : 0);   /* :349, :410 */
+    const size_t doff = 54 + (wf ? ORC_RETH_HDR : 0);
+    if (data_len != ORC_PAYLOAD_LEN || doff + ORC_PAYLOAD_LEN > row_len) return ORC_SW_INVALID;   /* :350, :411 */
+    const int rc = up ? sw_data_nonroot(sw, port, psn, frame + doff, wf ? frame + 54 : NULL)
+                      : sw_down(sw, psn, frame + doff);
+    if (rc != ORC_SW_FORWARD && rc != ORC_SW_REPLAY && rc != ORC_SW_DOWN) return rc;
+    /* the aggregator words re-encoded with htonl (send_roce_data[_with_reth],
+     * util.c:403-405, :419-421) and this packet's opcode */
+    const uint32_t s = SLOT(sw, psn);
+    int32_t agg[ORC_LANES];
+    memcpy(agg, sw->aggregator[s], sizeof(agg));
+    int c0 = port, c1 = port + 1;                               /* REPLAY: the retransmitting child */
+    if (rc == ORC_SW_FORWARD) c0 = F, c1 = F + 1;               /* the parent, RETH NULL (:464, :478) */
+    if (rc == ORC_SW_DOWN) c0 = 0, c1 = F;                      /* every child (:416-418, :492-494) */
+    for (int c = c0; c < c1; ++c) {
+        conn_hdr(&h, &conns[c], psn, op);
+        out_len[c] = (int)orc_build_data_frame(out + (size_t)c * out_stride, &h, agg, ORC_LANES, wf,
+                                               wf && c < F ? sw->reth_keeper[s][c] : NULL);
+    }
+    return rc;
+}
+
 int orc_switch_pipeline(orc_switch *sw, const orc_conn *conns, int port, const uint8_t *frame, size_t row_len,
                         uint8_t *out, size_t out_stride, int *out_len)
 {
-    for (int c = 0; c < sw->fan_in; ++c) out_len[c] = 0;
+    const int rows = sw->fan_in + (sw->root ? 0 : 1);          /* a non-root's row fan_in: its parent */
+    for (int c = 0; c < rows; ++c) out_len[c] = 0;
     /* the root has children only: a port outside them (the reference's DOWN_*
      * path, nts.c:408-426, :484-499, is a non-root switch's) is refused */
-    if (port < 0 || port >= sw->fan_in || row_len < 64) return ORC_SW_INVALID;
+    if (port < 0 || port >= rows || row_len < 64) return ORC_SW_INVALID;
+    if (!sw->root) return pipeline_nonroot(sw, conns, port, frame, row_len, out, out_stride, out_len);
     /* parser, nts.c:307-344 */
     const uint8_t op = frame[42];
     const uint32_t psn = ((uint32_t)frame[51] << 16) | ((uint32_t)frame[52] << 8) | frame[53];   /* :311 */

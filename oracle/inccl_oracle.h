@@ -117,7 +117,22 @@ typedef struct orc_switch {
     uint8_t  reth_keeper[ORC_SW_MAX_SLOTS][ORC_MAX_FAN_IN][ORC_RETH_HDR];  /* nts.c:57 */
     uint64_t adds;                                                         /* packets actually summed */
     uint64_t replays;                                                      /* retransmits answered from the slot */
+    int      root;                                                         /* nts.c:68: 1 root, 0 non-root */
+    int      flags;                                                        /* non-root: ORC_SW_WIRE_ORDER | ORC_SW_RECYCLE */
 } orc_switch;
+
+/* A non-root switch (nts.c:376-400, :408-423, :457-499): children on ports
+ * 0..fan_in-1, the parent on port fan_in.  flags 0 is the reference exactly:
+ * the parent's result is copied into the aggregator as wire bytes (nts.c:413,
+ * :489) and re-encoded with htonl on the way down (util.c:403-405), so every
+ * downstream word has its bytes reversed, and no slot is ever recycled
+ * (clear_state_data runs only at the root, :367, :449).  ORC_SW_WIRE_ORDER
+ * stores the result ntohl'd (children get the parent's words as sent);
+ * ORC_SW_RECYCLE clears slot psn + window when the parent's result for psn is
+ * taken, as the root does at completion. */
+#define ORC_SW_WIRE_ORDER 1
+#define ORC_SW_RECYCLE    2
+int orc_switch_init_nonroot(orc_switch *sw, int fan_in, uint32_t slots, int flags);
 
 size_t orc_switch_bytes(void);                      /* sizeof(orc_switch), for callers that allocate it */
 const int32_t *orc_switch_slot(const orc_switch *sw, uint32_t psn);   /* aggregator[Idx(psn)] (nts.c:55) */
@@ -133,7 +148,9 @@ int orc_switch_init_ring(orc_switch *sw, int fan_in, uint32_t slots);
  *                            to send back to `port` only (nts.c:353-356)
  *           ORC_SW_DROPPED   retransmit of an incomplete slot (nts.c:353 with no result) */
 enum { ORC_SW_ABSORBED = 0, ORC_SW_BROADCAST = 1, ORC_SW_REPLAY = 2, ORC_SW_DROPPED = 3,
-       ORC_SW_ACK = 4, ORC_SW_IGNORED = 5, ORC_SW_INVALID = 6 };
+       ORC_SW_ACK = 4, ORC_SW_IGNORED = 5, ORC_SW_INVALID = 6,
+       ORC_SW_FORWARD = 7,   /* non-root: the aggregate to the parent (nts.c:394-397, :476-479, resend :381-384, :462-465) */
+       ORC_SW_DOWN = 8 };    /* non-root: the parent's result taken and broadcast (nts.c:412-419, :488-495) */
 int orc_switch_ingress(orc_switch *sw, int port, uint32_t psn,
                        const uint32_t *payload_be, uint32_t *egress_be);
 
@@ -162,7 +179,17 @@ typedef struct orc_conn {
  *   ORC_SW_IGNORED    opcode the pipeline has no case for: nothing, no state
  *   ORC_SW_INVALID    port >= fan_in (the root has no parent) or a payload
  *                     length other than 1024 B (the reference asserts, :350)
- * row_len bounds the frame's bytes (a payload past it is INVALID). */
+ * row_len bounds the frame's bytes (a payload past it is INVALID).
+ * A non-root switch (orc_switch_init_nonroot) has fan_in + 1 rows and conns,
+ * row fan_in being the parent's:
+ *   ORC_SW_FORWARD    the parent: the aggregate with this packet's opcode (a
+ *                     WRITE_FIRST / WRITE_ONLY one with a zeroed RETH, :464, :478)
+ *   ORC_SW_DOWN       a packet from the parent whose result was taken: every
+ *                     child, the aggregator's words with the parent packet's
+ *                     opcode and child c's kept RETH for WRITE_FIRST / ONLY
+ *   ORC_SW_REPLAY     child `port`: the aggregator after the parent's result
+ *   ORC_SW_DROPPED    also a parent packet that is not taken (:420-422)
+ *   ORC_SW_IGNORED    also an ACK from the parent (DOWN_ACK, :424-426) */
 int orc_switch_pipeline(orc_switch *sw, const orc_conn *conns, int port, const uint8_t *frame, size_t row_len,
                         uint8_t *out, size_t out_stride, int *out_len);
 

@@ -19,7 +19,8 @@ LIB_PATH = os.path.join(HERE, "liborc.so")
 PAYLOAD_COUNT = 1024   # api.h:40
 LANES = 256            # nts.c:55
 SW_SLOTS = 16          # nts.c:22
-SW_ABSORBED, SW_BROADCAST, SW_REPLAY, SW_DROPPED, SW_ACK, SW_IGNORED, SW_INVALID = range(7)
+SW_ABSORBED, SW_BROADCAST, SW_REPLAY, SW_DROPPED, SW_ACK, SW_IGNORED, SW_INVALID, SW_FORWARD, SW_DOWN = range(9)
+SW_WIRE_ORDER, SW_RECYCLE = 1, 2   # non-root flags (orc_switch_init_nonroot)
 FRAME_ROW = 1152       # an output row of orc_switch_pipeline (the longest frame is 1098 B)
 
 _lib = None
@@ -81,6 +82,8 @@ def lib():
         L.orc_switch_bytes.restype = sz
         L.orc_switch_init_ring.argtypes = [P, ctypes.c_int, ctypes.c_uint32]
         L.orc_switch_init_ring.restype = ctypes.c_int
+        L.orc_switch_init_nonroot.argtypes = [P, ctypes.c_int, ctypes.c_uint32, ctypes.c_int]
+        L.orc_switch_init_nonroot.restype = ctypes.c_int
         L.orc_switch_slot.argtypes = [P, ctypes.c_uint32]
         L.orc_switch_slot.restype = P
         L.orc_switch_pipeline.argtypes = [P, P, ctypes.c_int, P, sz, P, sz, P]
@@ -286,13 +289,21 @@ def checksum_q32(q: np.ndarray, index_base: int = 0) -> int:
 # ---- switch (nts.c:303-501) ----
 class Switch:
     """Root switch with `fan_in` children (nts.c state, restated); `slots` is
-    the PSN ring (the reference's is 16, window 8: nts.c:21-22)."""
+    the PSN ring (the reference's is 16, window 8: nts.c:21-22).  nonroot=True:
+    a non-root switch (nts.c:376-400, :408-423, :457-499) whose parent is port
+    fan_in; `flags` SW_WIRE_ORDER / SW_RECYCLE (0: the reference exactly)."""
 
-    def __init__(self, fan_in: int, slots: int = SW_SLOTS):
+    def __init__(self, fan_in: int, slots: int = SW_SLOTS, nonroot: bool = False, flags: int = 0):
         self.fan_in = int(fan_in)
+        self.nonroot = bool(nonroot)
+        self.rows = self.fan_in + (1 if self.nonroot else 0)
         self._buf = np.zeros(int(lib().orc_switch_bytes()), np.uint8)
-        if lib().orc_switch_init_ring(_p(self._buf), self.fan_in, int(slots)) != 0:
-            raise ValueError(f"orc switch: fan_in {fan_in}, slots {slots}")
+        if self.nonroot:
+            rc = lib().orc_switch_init_nonroot(_p(self._buf), self.fan_in, int(slots), int(flags))
+        else:
+            rc = lib().orc_switch_init_ring(_p(self._buf), self.fan_in, int(slots))
+        if rc != 0:
+            raise ValueError(f"orc switch: fan_in {fan_in}, slots {slots}, flags {flags}")
 
     def ingress(self, port: int, psn: int, payload_be: np.ndarray):
         payload_be = np.ascontiguousarray(payload_be, dtype=np.uint32)
@@ -308,17 +319,18 @@ class Switch:
 
     def pipeline(self, conns: np.ndarray, port: int, frame: bytes, row_len: int | None = None):
         """nts.c:303-501 on one frame (orc_switch_pipeline): (action, [frame
-        bytes sent to child c, or None]).  `conns` holds fan_in 28-byte
-        connection records (the engine's FRAME_TEMPLATE_DTYPE layout)."""
+        bytes sent to row c, or None]).  `conns` holds one 28-byte connection
+        record per row (the engine's FRAME_TEMPLATE_DTYPE layout): fan_in
+        children, and for a non-root the parent last."""
         c = np.ascontiguousarray(conns).view(np.uint8)
-        assert c.size == 28 * self.fan_in
+        assert c.size == 28 * self.rows
         row = max(len(frame), 64) if row_len is None else int(row_len)
         fb = np.zeros(max(row, len(frame), 64), np.uint8)
         fb[: len(frame)] = np.frombuffer(bytes(frame), np.uint8)
-        out = np.zeros((self.fan_in, FRAME_ROW), np.uint8)
-        ln = np.zeros(self.fan_in, np.int32)
+        out = np.zeros((self.rows, FRAME_ROW), np.uint8)
+        ln = np.zeros(self.rows, np.int32)
         rc = lib().orc_switch_pipeline(_p(self._buf), _p(c), int(port), _p(fb), row, _p(out), FRAME_ROW, _p(ln))
-        return rc, [out[i, : ln[i]].tobytes() if ln[i] else None for i in range(self.fan_in)]
+        return rc, [out[i, : ln[i]].tobytes() if ln[i] else None for i in range(self.rows)]
 
 
 # ---- framing (util.c) ----
