@@ -906,6 +906,87 @@ def switch_batch(dev, fan_in: int = 2, P: int = 1 << 16, iters: int = 20, acks: 
             "timing": "HIP events on the batch's stream, eager calls"}
 
 
+def switch_nonroot_round(dev, fan_in: int = 2, P: int = 1 << 16, iters: int = 20) -> dict:
+    """The non-root switch (nts.c:376-400, :408-423, :457-499) on one round of
+    P PSNs: an up batch of fan_in x P child frames (every PSN's aggregate
+    FORWARDed to the parent once its last child arrives) and a down batch of
+    the parent's P results (each taken and sent to every child, DOWN).  With
+    INCCL_SW_RECYCLE (the reference never recycles a non-root slot, so its ring
+    serves one pass and no steady state exists); rounds alternate between the
+    two halves of a 2P-slot ring, each round's results clearing the other half.
+    Device time per round (both batches) from HIP events on their stream.
+    Checked without the oracle: every PSN forwards once and takes its result
+    once, and the rows written are exactly those."""
+    import numpy as np
+    import torch
+
+    from container_inc_amd import inccl
+    stride = 1152
+    rng = np.random.default_rng(8)
+    F = fan_in
+
+    def frames_for(psn, op):
+        n = len(psn)
+        f = np.zeros((n, stride), np.uint8)
+        wf = op == 0x06
+        udp_len = (8 + 12 + 1024 + 4 + np.where(wf, 16, 0)).astype(np.uint32)
+        f[:, 38], f[:, 39], f[:, 42] = udp_len >> 8, udp_len & 0xFF, op
+        pay = rng.integers(0, 256, (n, 1024), dtype=np.uint8)
+        for sel, off in ((wf, 70), (~wf, 54)):
+            f[sel, off:off + 1024] = pay[sel]
+        q = psn | 0x80000000
+        f[:, 50], f[:, 51], f[:, 52], f[:, 53] = q >> 24, (q >> 16) & 0xFF, (q >> 8) & 0xFF, q & 0xFF
+        return torch.from_numpy(f).to(dev)
+
+    up_psn = np.repeat(np.arange(P, dtype=np.uint32), F)
+    up_ports = torch.from_numpy(np.tile(np.arange(F, dtype=np.int32), P)).to(dev)
+    dn_psn = np.arange(P, dtype=np.uint32)
+    dn_ports = torch.full((P,), F, dtype=torch.int32, device=dev)
+    opof = lambda p: np.where(p % 4 == 0, 0x06, np.where(p % 4 == 3, 0x08, 0x07)).astype(np.uint8)
+    rounds = [(frames_for(up_psn + base, opof(up_psn)), frames_for(dn_psn + base, opof(dn_psn))) for base in (0, P)]
+    sw = inccl.GpuSwitch(F, 2 * P, nonroot=True, flags=inccl.SW_RECYCLE)
+    tmpl = np.zeros(F + 1, inccl.FRAME_TEMPLATE_DTYPE)
+    tmpl["qp"], tmpl["src_port"], tmpl["dst_port"] = 0x11, 4791, 4791
+    tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(dev)
+    st = torch.cuda.Stream(device=dev)
+    n_up = F * P
+    out = torch.empty((n_up * (F + 1), stride), dtype=torch.uint8, device=dev)
+    out_len = torch.empty(n_up * (F + 1), dtype=torch.int32, device=dev)
+    action = torch.empty(n_up, dtype=torch.int32, device=dev)
+    psn_out = torch.empty(n_up, dtype=torch.int32, device=dev)
+    turn = [0]
+    seen = {}
+
+    def one(check=False):
+        up, dn = rounds[turn[0] % 2]
+        turn[0] += 1
+        sw.batch(up, up_ports, tmpl_dev, stream=st.cuda_stream, out=out, out_len=out_len, action=action, psn=psn_out)
+        if check:
+            torch.cuda.synchronize()
+            seen["up"] = action.cpu().numpy().copy(), out_len.cpu().numpy().reshape(n_up, F + 1).copy()
+        sw.batch(dn, dn_ports, tmpl_dev, stream=st.cuda_stream, out=out[: P * (F + 1)], out_len=out_len[: P * (F + 1)],
+                 action=action[:P], psn=psn_out[:P])
+        if check:
+            torch.cuda.synchronize()
+            seen["dn"] = action[:P].cpu().numpy().copy(), out_len[: P * (F + 1)].cpu().numpy().reshape(P, F + 1).copy()
+
+    one(check=True)
+    a, ln = seen["up"]
+    fwd = a == inccl.SW_FORWARD
+    ok = int(fwd.sum()) == P and bool((a[~fwd] == inccl.SW_ABSORBED).all())
+    ok = ok and bool((ln[fwd, F] > 0).all() and (ln[fwd, :F] == 0).all() and (ln[~fwd] == 0).all())
+    a, ln = seen["dn"]
+    ok = ok and bool((a == inccl.SW_DOWN).all() and (ln[:, :F] > 0).all() and (ln[:, F] == 0).all())
+    ms = kernel_time_ms(one, st, iters)
+    sw.destroy()
+    frames = n_up + P
+    return {"what": "non-root inccl_switch_batch x 2 per round: the children's frames up (FORWARD to the parent), "
+                    "the parent's results down (DOWN to every child); INCCL_SW_RECYCLE",
+            "fan_in": F, "psns": P, "frames": frames, "us_per_round": round(ms * 1e3, 2),
+            "payload_GBs": round(frames * 1024 / (ms * 1e-3) / 1e9, 1), "frames_per_s": round(frames / (ms * 1e-3)),
+            "every_psn_forwards_and_takes_its_result_once": ok, "timing": "HIP events on the batches' stream, eager calls"}
+
+
 SIZES_BYTES = (4 << 10, 64 << 10, 1 << 20, 4 << 20, 64 << 20, 256 << 20, 1 << 30)
 
 
@@ -1794,6 +1875,7 @@ def main():
         extra("f16", lambda: bf16_buckets(dev, R, k, fmt="f16"))
         extra("switch_batch", lambda: switch_batch(dev))
         extra("switch_batch_acks", lambda: switch_batch(dev, acks=True))
+        extra("switch_nonroot_round", lambda: switch_nonroot_round(dev))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         extra("cpu_baseline", lambda: cpu_baseline(n, R, k, a.cpu_seconds))
         extra("cpu_baseline_allcores", lambda: cpu_baseline_allcores(n, R, k, min(a.cpu_seconds, 5.0)))

@@ -83,6 +83,8 @@ SIGNATURES = {
     "inccl_host_register": (_I, [_P, _P, _SZ]),
     "inccl_host_deregister": (_I, [_P, _P]),
     "inccl_switch_create": (_P, [_I, _U32, _I]),
+    "inccl_switch_create_nonroot": (_P, [_I, _U32, _I, _I]),
+    "inccl_switch_result": (_P, [_P, _U32]),
     "inccl_switch_destroy": (_I, [_P]),
     "inccl_switch_reset": (_I, [_P, _P]),
     "inccl_switch_slot": (_P, [_P, _U32]),

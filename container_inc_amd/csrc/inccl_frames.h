@@ -27,6 +27,19 @@ typedef struct InccSwitchState {
                           * gen[0], so that a captured batch (hipGraph) tags every replay anew */
     uint32_t slots;      /* power of two */
     int fan_in;
+    /* a non-root switch (nts.c:376-400, :408-423, :457-499; parent = port fan_in) instead of the
+     * root: agg, degree and reth as above; arrival, first and gen unused */
+    int nonroot, flags;  /* flags: INCCL_SW_WIRE_ORDER | INCCL_SW_RECYCLE */
+    int32_t *res;        /* [slots][256]        the parent's result as the reference's aggregator holds it
+                          *                     (nts.c:413: wire words; ntohl'd with INCCL_SW_WIRE_ORDER) */
+    uint32_t *bits;      /* [slots]             arrival bitmap: children, bit fan_in = parent's result (nts.c:59) */
+    uint32_t *head;      /* [slots]             the batch's frame list of each slot (~0: empty; reset by its owner) */
+    uint32_t *counted;   /* [slots][fan_in]     frame whose payload the batch adds for each child, ~0: none;
+                          *                     bit 31: WRITE_FIRST (payload at byte 70) */
+    uint32_t *down;      /* [slots]             the parent frame the batch takes, ~0: none; bit 31 as above */
+    uint32_t *work;      /* [1 + slots]         work[0]: slots with a sum or a result this batch; then their
+                          *                     PSNs, bit 31 = the slot held arrivals before the batch */
+    uint32_t *link;      /* [frames][2]         per frame: next frame of its slot's list, port | WF << 8 */
 } InccSwitchState;
 
 #define INCCL_FRAME_MIN_STRIDE 64   /* a row must hold the 62-B ACK frame (headers through the BTH) */

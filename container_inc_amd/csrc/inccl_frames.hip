@@ -889,6 +889,192 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
 }
 
 // ---------------------------------------------------------------------------
+// Non-root ingress (nts.c:376-400, :408-423, :457-499: `root` false).  A
+// non-root decides a frame from everything before it in its slot -- the
+// degree test of a resend (:382, :463) counts every earlier copy -- so each
+// slot's frames of the batch are put in arrival order and taken through the
+// reference's branches one at a time, by one lane:
+//   k_nr_claim     a lane per frame: parse + validate as the root's claim, the
+//                  parent on port fan_in; each data frame pushed onto its slot's
+//                  list (atomicExch on the slot's head: the frame that found the
+//                  list empty owns the slot for the batch)
+//   k_nr_classify  a lane per owner: the slot's frames in index order through
+//                  UP first copy / resend / replay and DOWN taken / ignored,
+//                  the RETH keeper (:470), bitmap and degree, the recycle
+//                  (INCCL_SW_RECYCLE); which frames' payloads count, and the
+//                  slot onto the batch's work list
+//   k_nr_sum       a wave per work item: the counted payloads added to the
+//                  aggregate (:390-392, :472-474) and the parent's result into
+//                  res (:413, :489)
+// A slot holds few frames of a batch (a copy per child, a resend or two, the
+// parent's): its owner keeps up to kNrList of them in its own LDS row (not a
+// register array: per-lane indices would make every access a waterfall) and
+// sorts them; a longer list is walked once per frame (same result, slower).
+// Every index read from the lists is checked against the batch's frame count,
+// so a list can never send a lane outside the batch.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr int kNrList = 16;
+
+__global__ __launch_bounds__(kClaimBlock) void k_nr_claim(InccSwitchState s, const uint8_t* __restrict__ frames,
+                                                          int64_t stride, int64_t count,
+                                                          const int32_t* __restrict__ ports,
+                                                          int32_t* __restrict__ action, uint32_t* __restrict__ psn_out)
+{
+    if (blockIdx.x == 0 && threadIdx.x == 0) s.work[0] = 0u;   // classify (the next launch) appends
+    const int64_t f = (int64_t)blockIdx.x * kClaimBlock + threadIdx.x;
+    if (f >= count) return;
+    const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + f * stride);
+    const uint32_t w9 = opaque_u32(fw[9]), w10 = opaque_u32(fw[10]), w12 = opaque_u32(fw[12]);
+    const uint32_t w13 = opaque_u32(fw[13]);
+    const int port = (int)opaque_u32((uint32_t)ports[f]);
+    const uint8_t op = (uint8_t)(w10 >> 16);                                    // byte 42
+    const uint32_t psn = ((w12 >> 24) << 16) | ((w13 & 0xFFu) << 8) | ((w13 >> 8) & 0xFFu);   // nts.c:311
+    const int udp_len = (int)(((w9 >> 16) & 0xFFu) << 8 | (w9 >> 24));
+    int act = INCCL_SW_IGNORED;
+    if (port < 0 || port > s.fan_in) act = INCCL_SW_INVALID;
+    else if (op == 0x11) act = port < s.fan_in ? INCCL_SW_ACK : INCCL_SW_IGNORED;   // UP_ACK / DOWN_ACK (:424-426)
+    else if (is_data_opcode(op) || is_write_first(op)) {
+        const bool wf = is_write_first(op);
+        const int data_len = udp_len - 12 - 8 - 4 - (wf ? 16 : 0);   // nts.c:349, :410, :429, :486
+        if (data_len != kLanes * 4 || 54 + (wf ? 16 : 0) + kLanes * 4 > stride) act = INCCL_SW_INVALID;
+        else {
+            const uint32_t slot = psn & (s.slots - 1);
+            s.link[2 * f] = atomicExch(&s.head[slot], (uint32_t)f);
+            s.link[2 * f + 1] = (uint32_t)port | (wf ? 1u << 8 : 0u);
+            act = kActPending;
+        }
+    }
+    action[f] = act;
+    psn_out[f] = psn;
+}
+
+__global__ __launch_bounds__(kClassifyBlock) void k_nr_classify(InccSwitchState s, const uint8_t* __restrict__ frames,
+                                                                int64_t stride, int64_t count,
+                                                                int32_t* __restrict__ action,
+                                                                const uint32_t* __restrict__ psns)
+{
+    const int64_t f = (int64_t)blockIdx.x * kClassifyBlock + threadIdx.x;
+    if (f >= count || action[f] != kActPending || s.link[2 * f] != kNone) return;   // owners only
+    const uint32_t psn = psns[f], slot = psn & (s.slots - 1);
+    const int fan = s.fan_in;
+    const uint32_t h0 = s.head[slot];
+    s.head[slot] = kNone;   // empty for the next batch
+    __shared__ uint32_t lds_list[kClassifyBlock][kNrList + 1];   // (+1: no two lanes' rows on one bank)
+    uint32_t* L = lds_list[threadIdx.x];
+    const uint32_t nfr = (uint32_t)count;
+    int n = 0;
+    for (uint32_t g = h0; g < nfr; g = s.link[2 * (size_t)g]) {
+        if (n < kNrList) L[n] = g;
+        ++n;
+    }
+    const bool kept = n <= kNrList;
+    if (kept)
+        for (int i = 1; i < n; ++i)   // insertion sort: arrival order
+            for (int j = i; j > 0 && L[j - 1] > L[j]; --j) {
+                const uint32_t t = L[j];
+                L[j] = L[j - 1];
+                L[j - 1] = t;
+            }
+    const uint32_t cmask = 0xFFFFFFFFu >> (32 - fan), rbit = 1u << fan;   // nts.c:29, :366
+    uint32_t B = s.bits[slot], D = (uint32_t)s.degree[slot], downf = kNone;
+    const bool partial = (B & cmask) != 0u;
+    bool summed = false;
+    uint32_t* cnt = s.counted + (size_t)slot * fan;
+    for (int q = 0; q < fan; ++q) cnt[q] = kNone;
+    int64_t prev = -1;
+    for (int i = 0; i < n; ++i) {
+        uint32_t g = kNone;
+        if (kept) g = L[i];
+        else   // the earliest frame after the previous one
+            for (uint32_t h = h0; h < nfr; h = s.link[2 * (size_t)h])
+                if ((int64_t)h > prev && h < g) g = h;
+        if (g >= nfr) break;
+        prev = g;
+        const uint32_t info = s.link[2 * (size_t)g + 1], port = info & 0xFFu, wf = (info >> 8) & 1u;
+        int act;
+        if ((int)port < fan) {
+            D += 1u;   // nts.c:351, :431
+            const uint32_t pb = 1u << port;
+            if (B & pb)   // resend (:377-385, :458-466)
+                act = (B & rbit) ? INCCL_SW_REPLAY
+                                 : (((B & cmask) == cmask && D % (uint32_t)fan == 0u) ? INCCL_SW_FORWARD
+                                                                                         : INCCL_SW_DROPPED);
+            else {   // first transmission (:387-398, :468-480)
+                B |= pb;
+                cnt[port] = g | (wf << 31);
+                summed = true;
+                if (wf) {   // the RETH into the keeper (:470): frame bytes 54-69
+                    const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + (int64_t)g * stride);
+                    uint32_t rw[5];
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) rw[j] = fw[13 + j];
+                    uint32_t* kp = s.reth + ((size_t)slot * fan + port) * 4;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) kp[j] = __builtin_amdgcn_alignbyte(rw[j + 1], rw[j], 2);
+                }
+                act = (B & cmask) == cmask ? INCCL_SW_FORWARD : INCCL_SW_ABSORBED;
+            }
+        } else if (!(B & rbit) && (B & cmask) == cmask) {   // the parent's result, taken once (:412-419)
+            B |= rbit;
+            downf = g | (wf << 31);
+            act = INCCL_SW_DOWN;
+            if (s.flags & INCCL_SW_RECYCLE) {   // clear_state_data(psn + WINDOW) as at the root (:235-242)
+                const uint32_t rs = (psn + (s.slots >> 1)) & (s.slots - 1);
+                for (int j = 0; j < fan * 4; ++j) s.reth[(size_t)rs * fan * 4 + j] = 0u;
+                s.bits[rs] = 0u;
+                s.degree[rs] = 0;
+            }
+        } else {
+            act = INCCL_SW_DROPPED;   // :420-422
+        }
+        action[g] = act;
+    }
+    s.bits[slot] = B;
+    s.degree[slot] = (int32_t)D;
+    s.down[slot] = downf;
+    if (summed || downf != kNone) s.work[1 + atomicAdd(&s.work[0], 1u)] = (psn & 0x00FFFFFFu) | (partial ? 1u << 31 : 0u);
+}
+
+constexpr int kNrSumWaves = 4;
+
+__global__ __launch_bounds__(kWave* kNrSumWaves) void k_nr_sum(InccSwitchState s, const uint8_t* __restrict__ frames,
+                                                              int64_t stride, int64_t count, int wide)
+{
+    const uint32_t n = s.work[0];
+    const int lane = threadIdx.x % kWave, fan = s.fan_in;
+    const uint32_t nw = gridDim.x * kNrSumWaves;
+    for (uint32_t i = blockIdx.x * kNrSumWaves + threadIdx.x / kWave; i < n; i += nw) {
+        const uint32_t w = s.work[1 + i], slot = w & (s.slots - 1);
+        u4 acc = {0u, 0u, 0u, 0u};
+        if (w >> 31) acc = reinterpret_cast<const u4*>(s.agg + (size_t)slot * kLanes)[lane];
+        bool any = false;
+        uint32_t P[4];
+        for (int q = 0; q < fan; ++q) {
+            const uint32_t c = s.counted[(size_t)slot * fan + q];
+            if ((c & 0x7FFFFFFFu) >= (uint64_t)count) continue;   // none (~0)
+            any = true;
+            payload16(frames + (int64_t)(c & 0x7FFFFFFFu) * stride, c >> 31, lane, wide != 0, P);
+            acc.x += P[0];
+            acc.y += P[1];
+            acc.z += P[2];
+            acc.w += P[3];
+        }
+        if (any) reinterpret_cast<u4*>(s.agg + (size_t)slot * kLanes)[lane] = acc;
+        const uint32_t d = s.down[slot];
+        if ((d & 0x7FFFFFFFu) < (uint64_t)count) {   // (~0: none)
+            payload16(frames + (int64_t)(d & 0x7FFFFFFFu) * stride, d >> 31, lane, wide != 0, P);   // ntohl'd
+            const bool wire = (s.flags & INCCL_SW_WIRE_ORDER) != 0;
+            // the reference keeps the wire bytes (memcpy, :413): the host words back to wire order
+            const u4 r = wire ? u4{P[0], P[1], P[2], P[3]}
+                              : u4{__builtin_bswap32(P[0]), __builtin_bswap32(P[1]), __builtin_bswap32(P[2]),
+                                   __builtin_bswap32(P[3])};
+            reinterpret_cast<u4*>(s.res + (size_t)slot * kLanes)[lane] = r;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Egress (nts.c:365-372 / :447-453 broadcast, :353-356 / :435-438 replay;
 // frames per util.c:331-442): every output frame of input frame f, rows
 // f * fan_in + c -- all fan_in children on COMPLETED, the sender's child on
@@ -947,8 +1133,8 @@ struct EgressLds {
     uint32_t var[kVarRows][2][16];
     uint32_t z1024[8][16];
     uint32_t ackvar[kAckVar][2][16];
-    uint32_t hcrc[3 * 31];                                  // H_c: [2 c + RETH flag] data, [2 fan_in + c] ACK
-    __attribute__((aligned(16))) uint8_t img[3 * 31][kHdrImg];
+    uint32_t hcrc[3 * 32];                                  // H_c: [2 c + RETH flag] data, [2 dests + c] ACK
+    __attribute__((aligned(16))) uint8_t img[3 * 32][kHdrImg];
 };
 
 // The raw CRC of 16 bytes (a[]: memory order, little-endian words) as 16 byte
@@ -974,7 +1160,8 @@ __device__ __forceinline__ uint32_t seg16(const EgressLds& t, const uint32_t (&a
     return xor3(xor3(s[0], s[1], s[2]), xor3(s[3], s[4], s[5]), s[6]) ^ s[7];
 }
 
-// The tables, the 3 fan_in header images and their ICRC terms H_c into the
+// The tables, the 3 `fan` header images (fan: the destinations, fan_in
+// children and a non-root's parent) and their ICRC terms H_c into the
 // block's LDS (ends with a block barrier).  H_c: quad i of the block takes
 // image i; the header part of the ICRC message (doff - 10 bytes: 44, or 60
 // with a RETH; an ACK's whole 48-byte message) is right-aligned in a 64-byte
@@ -1048,6 +1235,7 @@ __device__ void egress_setup(EgressLds& t, const InccFrameTemplate* __restrict__
 // count < 2^31).
 struct EgressArgs {
     const int32_t* agg;
+    const int32_t* res;   // a non-root's parent results (the DOWN / REPLAY payloads)
     const uint32_t* reth;
     const uint8_t* frames;
     const int32_t* ports;
@@ -1058,17 +1246,19 @@ struct EgressArgs {
     int32_t* out_len;
     uint32_t stride, out_stride, count, smask;
     int fan;
+    int dests;            // rows per input frame: fan, and a non-root's parent row fan
 };
 
 // One input frame as an egress wave knows it: three wave-uniform words
 struct EgressF {
     uint32_t f, psn;
-    uint32_t bits;   // opcode | WRITE_FIRST << 8 | in << 9 | all << 10 | one << 11 | port << 16
+    uint32_t bits;   // opcode | WRITE_FIRST << 8 | in << 9 | all << 10 | one << 11 | res << 14 | port << 16
     __device__ uint32_t op() const { return bits & 0xFFu; }
     __device__ uint32_t wf() const { return (bits >> 8) & 1u; }
     __device__ bool in() const { return (bits >> 9) & 1u; }     // f < count
     __device__ bool all() const { return (bits >> 10) & 1u; }   // COMPLETED: every child
-    __device__ bool one() const { return (bits >> 11) & 1u; }   // REPLAY: child port()
+    __device__ bool one() const { return (bits >> 11) & 1u; }   // REPLAY: child port(); FORWARD: port() = fan_in
+    __device__ bool res() const { return (bits >> 14) & 1u; }   // the payload from res (a non-root's DOWN, REPLAY)
     __device__ uint32_t port() const { return bits >> 16; }
 };
 
@@ -1079,7 +1269,7 @@ __device__ __forceinline__ void egress_load(const EgressArgs& A, const EgressF& 
     const bool em = e.all() || e.one();
     const uint32_t slot = e.psn & A.smask;
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<int32_t*>(A.agg) + (size_t)slot * kLanes, 0, em ? kLanes * 4 : 0, 0x00020000);
+        const_cast<int32_t*>(e.res() ? A.res : A.agg) + (size_t)slot * kLanes, 0, em ? kLanes * 4 : 0, 0x00020000);
     acc = __builtin_amdgcn_raw_buffer_load_b128(ra, 16 * lane, 0, 0);
     const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(A.reth) + (size_t)slot * A.fan * 4, 0, em && e.wf() ? 16 * A.fan : 0, 0x00020000);
@@ -1087,11 +1277,11 @@ __device__ __forceinline__ void egress_load(const EgressArgs& A, const EgressF& 
 }
 
 // Frame e's output rows (their lengths are stored per chunk, k_egress).
-template <int kFan, bool kOut16>
+template <int kFan, bool kOut16, bool kNR>
 __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs& A, const EgressF& e, const u4& acc,
                                             uint32_t keep, int lane)
 {
-    const int fan = kFan ? kFan : A.fan;
+    const int fan = kFan ? kFan : A.fan, dests = fan + (kNR ? 1 : 0);
     const uint32_t wf = e.wf(), op = e.op(), port = e.port();
     const bool all = e.all(), one = e.one();
     const bool em_any = all || one;
@@ -1152,10 +1342,10 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
     }
     const bool tail = lane == hchunks - 1;   // the frame's last chunk, in the second store
     const uint32_t emit_mask = all ? (1u << fan) - 1u : (one ? 1u << port : 0u);   // children that get a frame
-    uint8_t* row = A.out + (size_t)e.f * fan * A.out_stride;
-    constexpr int kUnroll = kFan ? kFan : 1;
+    uint8_t* row = A.out + (size_t)e.f * dests * A.out_stride;
+    constexpr int kUnroll = kFan ? kFan + (kNR ? 1 : 0) : 1;
 #pragma unroll kUnroll
-    for (int c = 0; c < fan; ++c) {
+    for (int c = 0; c < dests; ++c) {
         const bool em = (emit_mask >> c) & 1u;
         u4 h = unset4(), v = unset4();
         if (em) {
@@ -1168,11 +1358,16 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
             if (wf) {
                 // child c's RETH (reth_keeper[slot][c], nts.c:442; util.c:409-417):
                 // bytes 54-69, lane 3's chunk from byte 6 on and lane 4's first 6
-                // bytes; its ICRC term on lanes 0-15
+                // bytes; its ICRC term on lanes 0-15.  A non-root's parent gets a
+                // zeroed RETH (send_roce_data_with_reth(FAN_IN, NULL), :464, :478):
+                // keep's lanes past the children's 4 fan_in words read as zero
                 uint32_t R[4];
                 if (kFan || c < kWave / 4) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) R[j] = (uint32_t)__builtin_amdgcn_readlane((int)keep, 4 * c + j);
+                } else if (kNR && c == fan) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) R[j] = 0u;
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) R[j] = A.reth[((size_t)(e.psn & A.smask) * fan + c) * 4 + j];
@@ -1229,7 +1424,7 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
 // under the ACK lanes' mask, issued before the chunk's data frames.
 template <bool kOut16>
 __device__ __forceinline__ void egress_acks(const EgressLds& t, const EgressArgs& A, uint32_t f0, bool ack,
-                                            uint32_t bits, uint32_t psn, int fan, int lane)
+                                            uint32_t bits, uint32_t psn, int fan, int dests, int lane)
 {
     if (!__ballot(ack)) return;   // (lane l: frame f0 + l; most chunks hold no ACK)
     const int j = lane >> 2, q = lane & 3;
@@ -1240,21 +1435,21 @@ __device__ __forceinline__ void egress_acks(const EgressLds& t, const EgressArgs
     const uint32_t c = bj >> 16, msn = pj + 1u;
     const uint32_t aeth = msn | 0x1f000000u;
     // the variable bytes (frame 51 .. 57): PSN bytes 2..0, AETH bytes 3..0 (big-endian)
-    uint32_t crc = t.hcrc[2 * fan + c];
+    uint32_t crc = t.hcrc[2 * dests + c];
 #pragma unroll
     for (int k = 0; k < kAckVar; ++k) {
         const uint32_t b = k < 3 ? (pj >> (8 * (2 - k))) & 0xFFu : (aeth >> (8 * (6 - k))) & 0xFFu;
         crc ^= t.ackvar[k][0][b & 15u] ^ t.ackvar[k][1][b >> 4];
     }
     crc = ~crc;   // util.c:424-426
-    u4 v = reinterpret_cast<const u4*>(t.img[2 * fan + c])[q];
+    u4 v = reinterpret_cast<const u4*>(t.img[2 * dests + c])[q];
     if (q == 3) {   // bytes 48-63: QPN low bytes (image), 0, PSN, AETH, ICRC (host order), 2 zero bytes
         v.x |= ((pj >> 16) & 0xFFu) << 24;
         v.y = ((pj >> 8) & 0xFFu) | ((pj & 0xFFu) << 8) | ((aeth >> 24) << 16) | (((aeth >> 16) & 0xFFu) << 24);
         v.z = ((aeth >> 8) & 0xFFu) | ((aeth & 0xFFu) << 8) | (crc << 16);
         v.w = crc >> 16;
     }
-    uint8_t* row = A.out + ((size_t)(f0 + (uint32_t)j) * fan + c) * A.out_stride + 16 * q;
+    uint8_t* row = A.out + ((size_t)(f0 + (uint32_t)j) * dests + c) * A.out_stride + 16 * q;
     if (kOut16) {
         *reinterpret_cast<u4*>(row) = v;
     } else {
@@ -1267,13 +1462,15 @@ __device__ __forceinline__ void egress_acks(const EgressLds& t, const EgressArgs
 }
 
 // kFan: 2, 3, 4 or 8 (the children loop unrolled), or 0 (A.fan, a loop).
-// kOut16: 16-byte aligned output rows.
-template <int kFan, bool kOut16>
+// kOut16: 16-byte aligned output rows.  kNR: a non-root switch -- row fan_in
+// of each input frame is the parent's; FORWARD sends the aggregate there,
+// DOWN sends the parent's result (res) to every child, REPLAY res to one.
+template <int kFan, bool kOut16, bool kNR>
 __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_egress(
     EgressArgs A)
 {
     __shared__ EgressLds t;
-    const int fan = kFan ? kFan : A.fan;
+    const int fan = kFan ? kFan : A.fan, dests = fan + (kNR ? 1 : 0);
     const uint32_t kEgressChunk = egress_chunk(fan);   // (a constant for the unrolled fan-ins)
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane0 = threadIdx.x % kWave;
     const uint32_t count = A.count, chunks = (count + kEgressChunk - 1) / kEgressChunk;
@@ -1307,7 +1504,7 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
     // the wave's first chunk is read while the block sets up its tables
     uint32_t ch = blockIdx.x * kEgressWaves + w;
     ChunkIn cin = chunk_in(ch);
-    egress_setup(t, A.tmpl, fan);
+    egress_setup(t, A.tmpl, dests);
     for (; ch < chunks; ch += nw) {
         const ChunkIn cur = cin;
         cin = chunk_in(ch + nw);   // the wave's next chunk, read while this one is built (past the end: nothing)
@@ -1317,26 +1514,28 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
         const uint32_t port = cur.port, psn = cur.psn;
         const uint32_t op = (cur.w10 >> 16) & 0xFFu;
         const bool in = lane < (int)nf;
-        const bool all = in && act == INCCL_SW_COMPLETED;
-        const bool one = in && act == INCCL_SW_REPLAY && port < (uint32_t)fan;
+        const bool fwd = kNR && in && act == INCCL_SW_FORWARD;
+        const bool all = in && act == (kNR ? INCCL_SW_DOWN : INCCL_SW_COMPLETED);
+        const bool one = (in && act == INCCL_SW_REPLAY && port < (uint32_t)fan) || fwd;
         const bool ack = in && act == INCCL_SW_ACK && port < (uint32_t)fan;
+        const bool res = kNR && in && (act == INCCL_SW_DOWN || act == INCCL_SW_REPLAY);
         const uint32_t bits = op | (is_write_first((uint8_t)op) ? 1u << 8 : 0u) | (in ? 1u << 9 : 0u) |
                               (all ? 1u << 10 : 0u) | (one ? 1u << 11 : 0u) | (ack ? 1u << 12 : 0u) |
-                              ((port & 0xFFFFu) << 16);
-        {   // the chunk's row lengths: entry e = f fan + c, lane-parallel (util.c:341-345)
+                              (res ? 1u << 14 : 0u) | (((fwd ? (uint32_t)fan : port) & 0xFFFFu) << 16);
+        {   // the chunk's row lengths: entry e = f dests + c, lane-parallel (util.c:341-345)
             const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
-                A.out_len + (size_t)f0 * fan, 0, (int)(4 * nf * fan), 0x00020000);
-            for (int k = 0; k < (kEgressChunk * fan + kWave - 1) / kWave; ++k) {
-                const int e = lane + kWave * k, fr = e / fan, c = e - fr * fan;
+                A.out_len + (size_t)f0 * dests, 0, (int)(4 * nf * dests), 0x00020000);
+            for (int k = 0; k < (kEgressChunk * dests + kWave - 1) / kWave; ++k) {
+                const int e = lane + kWave * k, fr = e / dests, c = e - fr * dests;
                 const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (fr & (kWave - 1)), (int)bits);
                 const bool mine = (b >> 16) == (uint32_t)c;
-                const bool on = ((b >> 10) & 1u) || (((b >> 11) & 1u) && mine);
+                const bool on = (((b >> 10) & 1u) && c < fan) || (((b >> 11) & 1u) && mine);
                 const uint32_t total = 54 + 16 * ((b >> 8) & 1u) + kLanes * 4 + 4;
                 const uint32_t len = on ? total : (((b >> 12) & 1u) && mine ? (uint32_t)kAckLen : 0u);
                 __builtin_amdgcn_raw_buffer_store_b32(len, rl, 4 * e, 0, 0);
             }
         }
-        egress_acks<kOut16>(t, A, f0, ack, bits, psn, fan, lane);
+        egress_acks<kOut16>(t, A, f0, ack, bits, psn, fan, dests, lane);
         uint64_t m = __ballot(all || one);
         if (!m) continue;
         // a frame of the ring is its lane in the chunk (-1: none); its words
@@ -1373,7 +1572,7 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
             // entered with its back edge's memory history, so its waits are counts
             const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(A.out_len, 0, 0, 0x00020000);
 #pragma unroll
-            for (int k = 0; k < kEgressAhead * kFan * (kOut16 ? 2 : 8); ++k)
+            for (int k = 0; k < kEgressAhead * (kFan + (kNR ? 1 : 0)) * (kOut16 ? 2 : 8); ++k)
                 __builtin_amdgcn_raw_buffer_store_b32(0u, none, 16 * k, 0, 0);
         }
         for (;;) {
@@ -1383,7 +1582,7 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
                 const int ld = (r + kEgressAhead) % kR;
                 B[ld] = take();
                 egress_load(A, frame(B[ld]), ln(), acc[ld], keep[ld]);
-                egress_emit<kFan, kOut16>(t, A, frame(B[r]), acc[r], keep[r], ln());
+                egress_emit<kFan, kOut16, kNR>(t, A, frame(B[r]), acc[r], keep[r], ln());
                 more = B[(r + 1) % kR] >= 0;
                 if (!more) break;
             }
@@ -1504,32 +1703,32 @@ int launch_apply(const ApplyArgs& a, hipStream_t st)
 
 // persistent egress: a wave per chunk of egress_chunk(fan_in) frames, as many blocks as
 // fit beside each other (two per CU)
-template <int kFan, bool kOut16>
+template <int kFan, bool kOut16, bool kNR>
 int launch_egress_t(const EgressArgs& a, hipStream_t st)
 {
     static const int per_cu = [] {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_egress<kFan, kOut16>, kWave * kEgressWaves, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_egress<kFan, kOut16, kNR>, kWave * kEgressWaves, 0) !=
                 hipSuccess || n < 1)
             n = 1;
         return n;
     }();
     const int64_t chunks = ((int64_t)a.count + egress_chunk(a.fan) - 1) / egress_chunk(a.fan);
     const int64_t need = (chunks + kEgressWaves - 1) / kEgressWaves, cap = (int64_t)num_cus() * per_cu;
-    hipLaunchKernelGGL((k_egress<kFan, kOut16>), dim3((unsigned)(need < cap ? (need < 1 ? 1 : need) : cap)),
+    hipLaunchKernelGGL((k_egress<kFan, kOut16, kNR>), dim3((unsigned)(need < cap ? (need < 1 ? 1 : need) : cap)),
                        dim3(kWave * kEgressWaves), 0, st, a);
     return (int)hipGetLastError();
 }
 
-template <bool kOut16>
+template <bool kOut16, bool kNR>
 int launch_egress_o(const EgressArgs& a, hipStream_t st)
 {
     switch (a.fan) {   // fan-in 2, 3, 4, 8: the children loop unrolled; others a loop
-    case 2: return launch_egress_t<2, kOut16>(a, st);
-    case 3: return launch_egress_t<3, kOut16>(a, st);
-    case 4: return launch_egress_t<4, kOut16>(a, st);
-    case 8: return launch_egress_t<8, kOut16>(a, st);
-    default: return launch_egress_t<0, kOut16>(a, st);
+    case 2: return launch_egress_t<2, kOut16, kNR>(a, st);
+    case 3: return launch_egress_t<3, kOut16, kNR>(a, st);
+    case 4: return launch_egress_t<4, kOut16, kNR>(a, st);
+    case 8: return launch_egress_t<8, kOut16, kNR>(a, st);
+    default: return launch_egress_t<0, kOut16, kNR>(a, st);
     }
 }
 
@@ -1539,6 +1738,7 @@ int launch_egress(const InccSwitchState* s, const uint8_t* frames, size_t stride
 {
     EgressArgs a{};
     a.agg = s->agg;
+    a.res = s->res;
     a.reth = s->reth;
     a.frames = frames;
     a.ports = ports;
@@ -1552,8 +1752,10 @@ int launch_egress(const InccSwitchState* s, const uint8_t* frames, size_t stride
     a.count = (uint32_t)count;
     a.smask = s->slots - 1;
     a.fan = s->fan_in;
+    a.dests = s->fan_in + (s->nonroot ? 1 : 0);
     const bool o16 = ((out_stride & 15) == 0) && (((uintptr_t)out & 15) == 0);
-    return o16 ? launch_egress_o<true>(a, st) : launch_egress_o<false>(a, st);
+    if (s->nonroot) return o16 ? launch_egress_o<true, true>(a, st) : launch_egress_o<false, true>(a, st);
+    return o16 ? launch_egress_o<true, false>(a, st) : launch_egress_o<false, false>(a, st);
 }
 
 int check_batch_args(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count, const int32_t* ports,
@@ -1587,6 +1789,23 @@ void launch_claim(const InccSwitchState* s, const uint8_t* frames, size_t stride
     const dim3 lanes((unsigned)(((int64_t)count + kClaimBlock - 1) / kClaimBlock));
     hipLaunchKernelGGL(k_ingress_claim, lanes, dim3(kClaimBlock), 0, st, *s, frames, (int64_t)stride, (int64_t)count,
                        ports, action, psn_out);
+}
+
+// the non-root ingress: claim, classify (a lane per frame, owners only), sum
+// (waves over the work list; at most one item per frame)
+int launch_nr_ingress(const InccSwitchState* s, const uint8_t* frames, size_t stride, size_t count,
+                      const int32_t* ports, int32_t* action, uint32_t* psn_out, hipStream_t st)
+{
+    const int64_t n = (int64_t)count;
+    hipLaunchKernelGGL(k_nr_claim, dim3((unsigned)((n + kClaimBlock - 1) / kClaimBlock)), dim3(kClaimBlock), 0, st, *s,
+                       frames, (int64_t)stride, n, ports, action, psn_out);
+    hipLaunchKernelGGL(k_nr_classify, dim3((unsigned)((n + kClassifyBlock - 1) / kClassifyBlock)), dim3(kClassifyBlock),
+                       0, st, *s, frames, (int64_t)stride, n, action, (const uint32_t*)psn_out);
+    const int wide = ((uintptr_t)frames & 15) == 0 && (stride & 15) == 0;
+    const int64_t need = (n + kNrSumWaves - 1) / kNrSumWaves, cap = (int64_t)num_cus() * 8;
+    hipLaunchKernelGGL(k_nr_sum, dim3((unsigned)(need < cap ? need : cap)), dim3(kWave * kNrSumWaves), 0, st, *s,
+                       frames, (int64_t)stride, n, wide);
+    return (int)hipGetLastError();
 }
 
 int egress_args_ok(const InccSwitchState* s, const uint8_t* frames, const int32_t* ports, const int32_t* action,
@@ -1630,6 +1849,7 @@ int inccl_k_switch_ingress(const InccSwitchState* s, const uint8_t* frames, size
     if (count == 0) return 0;
     if (check_batch_args(s, frames, stride, count, ports, action, psn_out)) return INCCL_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
+    if (s->nonroot) return launch_nr_ingress(s, frames, stride, count, ports, action, psn_out, st);
     launch_claim(s, frames, stride, count, ports, action, psn_out, st);
     return launch_apply(apply_args(s, frames, stride, count, ports, action, psn_out), st);
 }
@@ -1646,8 +1866,12 @@ int inccl_k_switch_batch(const InccSwitchState* s, const uint8_t* frames, size_t
     int rc = ensure_tables();
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    launch_claim(s, frames, stride, count, ports, action, psn_out, st);
-    rc = launch_apply(apply_args(s, frames, stride, count, ports, action, psn_out), st);
+    if (s->nonroot) {
+        rc = launch_nr_ingress(s, frames, stride, count, ports, action, psn_out, st);
+    } else {
+        launch_claim(s, frames, stride, count, ports, action, psn_out, st);
+        rc = launch_apply(apply_args(s, frames, stride, count, ports, action, psn_out), st);
+    }
     if (rc) return rc;
     return launch_egress(s, frames, stride, count, ports, action, psn_out, tmpl, out, out_stride, out_len, st);
 }

@@ -22,8 +22,9 @@ struct inccl_switch {
     InccSwitchState st;
     void *mem;
     size_t bytes;
-    size_t first_off;   /* the first-arrival table: all-ones = "no copy seen" */
+    size_t first_off;   /* the first-arrival table (root) or the slots' list heads (non-root): all-ones */
     int device;
+    size_t link_cap;    /* non-root: frames the per-frame list links hold */
 };
 
 static int kerr2(int rc, const char *what)
@@ -80,12 +81,94 @@ struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device)
     return sw;
 }
 
+struct inccl_switch *inccl_switch_create_nonroot(int fan_in, uint32_t slots, int device, int flags)
+{
+    if (fan_in < 1 || fan_in > 31 || slots < 2 || (slots & (slots - 1)) != 0 || slots > (1u << 24) ||
+        (flags & ~(INCCL_SW_WIRE_ORDER | INCCL_SW_RECYCLE))) {
+        inccl_set_error(INCCL_ERR_ARG, "switch: fan_in must be 1..31, slots a power of two in 2..2^24, "
+                                       "flags INCCL_SW_WIRE_ORDER | INCCL_SW_RECYCLE");
+        return NULL;
+    }
+    if (device >= 0 && hipSetDevice(device) != hipSuccess) {
+        inccl_set_error(INCCL_ERR_HIP, "switch: hipSetDevice(%d) failed", device);
+        return NULL;
+    }
+    struct inccl_switch *sw = (struct inccl_switch *)calloc(1, sizeof(*sw));
+    if (!sw) return NULL;
+    /* zeroed: agg, res, bits, degree, reth, work; all-ones: head; counted and
+     * down are written by a slot's owner before anything reads them */
+    const size_t S = slots;
+    const size_t agg = S * 256 * sizeof(int32_t), words = S * sizeof(uint32_t);
+    const size_t reth = S * (size_t)fan_in * 16, work = (S + 1) * sizeof(uint32_t);
+    const size_t counted = S * (size_t)fan_in * sizeof(uint32_t);
+    const size_t zero_end = (2 * agg + 2 * words + reth + work + 15) & ~(size_t)15;
+    sw->first_off = zero_end;
+    sw->bytes = zero_end + words + counted + words;
+    hipError_t e = hipMalloc(&sw->mem, sw->bytes);
+    if (e == hipSuccess) e = hipMemset(sw->mem, 0, zero_end);
+    if (e == hipSuccess) e = hipMemset((char *)sw->mem + zero_end, 0xFF, words);
+    if (e != hipSuccess) {
+        inccl_hip_check(e, "switch: hipMalloc");
+        if (sw->mem) hipFree(sw->mem);
+        free(sw);
+        return NULL;
+    }
+    char *p = (char *)sw->mem;
+    sw->st.agg = (int32_t *)p;
+    sw->st.res = (int32_t *)(p + agg);
+    sw->st.bits = (uint32_t *)(p + 2 * agg);
+    sw->st.degree = (int32_t *)(p + 2 * agg + words);
+    sw->st.reth = (uint32_t *)(p + 2 * agg + 2 * words);
+    sw->st.work = (uint32_t *)(p + 2 * agg + 2 * words + reth);
+    sw->st.head = (uint32_t *)(p + zero_end);
+    sw->st.counted = (uint32_t *)(p + zero_end + words);
+    sw->st.down = (uint32_t *)(p + zero_end + words + counted);
+    sw->st.slots = slots;
+    sw->st.fan_in = fan_in;
+    sw->st.nonroot = 1;
+    sw->st.flags = flags;
+    hipGetDevice(&sw->device);
+    if (kerr2(inccl_k_frames_init(), "switch: CRC tables")) {
+        hipFree(sw->mem);
+        free(sw);
+        return NULL;
+    }
+    return sw;
+}
+
+const int32_t *inccl_switch_result(struct inccl_switch *sw, uint32_t psn)
+{
+    if (!sw || !sw->st.nonroot) return NULL;
+    return sw->st.res + (size_t)(psn & (sw->st.slots - 1)) * 256;
+}
+
+/* a non-root batch of `count` frames needs count list links (grown outside
+ * stream capture: a captured batch must follow an uncaptured one as large) */
+static int ensure_links(struct inccl_switch *sw, size_t count, void *stream)
+{
+    if (!sw->st.nonroot || count <= sw->link_cap) return 0;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (stream && hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        return inccl_set_error(INCCL_ERR_ARG, "non-root switch: a captured batch of %zu frames needs an earlier "
+                                              "uncaptured batch at least as large (list links)", count);
+    if (sw->st.link) {
+        hipDeviceSynchronize();
+        hipFree(sw->st.link);
+        sw->st.link = NULL;
+        sw->link_cap = 0;
+    }
+    INCCL_HIP(hipMalloc((void **)&sw->st.link, count * 2 * sizeof(uint32_t)));
+    sw->link_cap = count;
+    return 0;
+}
+
 int inccl_switch_destroy(struct inccl_switch *sw)
 {
     if (!sw) return 0;
     hipSetDevice(sw->device);
     hipDeviceSynchronize();
     hipFree(sw->mem);
+    if (sw->st.link) hipFree(sw->st.link);
     free(sw);
     return 0;
 }
@@ -94,7 +177,8 @@ int inccl_switch_reset(struct inccl_switch *sw, void *stream)
 {
     if (!sw) return inccl_set_error(INCCL_ERR_ARG, "switch is NULL");
     INCCL_HIP(hipMemsetAsync(sw->mem, 0, sw->first_off, (hipStream_t)stream));
-    INCCL_HIP(hipMemsetAsync((char *)sw->mem + sw->first_off, 0xFF, sw->bytes - sw->first_off, (hipStream_t)stream));
+    const size_t ones = sw->st.nonroot ? (size_t)sw->st.slots * sizeof(uint32_t) : sw->bytes - sw->first_off;
+    INCCL_HIP(hipMemsetAsync((char *)sw->mem + sw->first_off, 0xFF, ones, (hipStream_t)stream));
     return 0;
 }
 
@@ -114,6 +198,8 @@ int inccl_switch_ingress(struct inccl_switch *sw, const uint8_t *frames_dev, siz
      * generation is a device word the batch's commit advances, so a captured
      * batch stays correct on replay; switch state is per stream-ordered call
      * sequence, like the reference's globals) */
+    const int rc = ensure_links(sw, count, stream);
+    if (rc) return rc;
     return kerr2(inccl_k_switch_ingress(&sw->st, frames_dev, stride, count, ports_dev, action_dev, psn_dev, stream),
                  "inccl_switch_ingress");
 }
@@ -126,6 +212,8 @@ int inccl_switch_batch(struct inccl_switch *sw, const uint8_t *frames_dev, size_
     if (!sw) return inccl_set_error(INCCL_ERR_ARG, "switch is NULL");
     if (count && stride < INCCL_FRAME_MIN_STRIDE)
         return inccl_set_error(INCCL_ERR_ARG, "inccl_switch_batch: stride %zu below %d", stride, INCCL_FRAME_MIN_STRIDE);
+    const int rc = ensure_links(sw, count, stream);
+    if (rc) return rc;
     return kerr2(inccl_k_switch_batch(&sw->st, frames_dev, stride, count, ports_dev, action_dev, psn_dev,
                                       templates_dev, out_dev, out_stride, out_len_dev, stream),
                  "inccl_switch_batch");

@@ -579,7 +579,8 @@ def inccl_allreduce_sendrecv(comm: Communicator, src_data: np.ndarray, length: i
 # the reference switch's dataplane on the GPU (non_termination_switch.c:303-501,
 # util.c:331-442); frames are rows of a uint8 CUDA tensor [count, stride]
 # ---------------------------------------------------------------------------
-SW_IGNORED, SW_ABSORBED, SW_COMPLETED, SW_DROPPED, SW_REPLAY, SW_ACK, SW_INVALID = range(7)
+SW_IGNORED, SW_ABSORBED, SW_COMPLETED, SW_DROPPED, SW_REPLAY, SW_ACK, SW_INVALID, SW_FORWARD, SW_DOWN = range(9)
+SW_WIRE_ORDER, SW_RECYCLE = 1, 2   # non-root switch flags (inccl_switch_create_nonroot)
 FRAME_TEMPLATE_DTYPE = np.dtype([("src_mac", np.uint8, 6), ("dst_mac", np.uint8, 6), ("src_ip", "<u4"),
                                  ("dst_ip", "<u4"), ("src_port", "<u2"), ("dst_port", "<u2"), ("qp", "<u4")])
 assert FRAME_TEMPLATE_DTYPE.itemsize == 28
@@ -606,11 +607,20 @@ def icrc_frames(frames, stream=None):
 
 
 class GpuSwitch:
-    """A root switch (fan_in children) whose state and dataplane live on the GPU."""
+    """A switch whose state and dataplane live on the GPU: the root (fan_in
+    children), or with nonroot=True a non-root whose parent is port fan_in
+    (non_termination_switch.c:376-400, :408-423, :457-499; `flags`
+    SW_WIRE_ORDER | SW_RECYCLE, 0 = the reference).  A non-root has fan_in + 1
+    output rows and templates per input frame, the parent's last."""
 
-    def __init__(self, fan_in: int, slots: int = 1024, device: int = -1):
+    def __init__(self, fan_in: int, slots: int = 1024, device: int = -1, nonroot: bool = False, flags: int = 0):
         self.fan_in = int(fan_in)
-        self.handle = load().inccl_switch_create(self.fan_in, int(slots), int(device))
+        self.nonroot = bool(nonroot)
+        self.rows = self.fan_in + (1 if self.nonroot else 0)
+        if self.nonroot:
+            self.handle = load().inccl_switch_create_nonroot(self.fan_in, int(slots), int(device), int(flags))
+        else:
+            self.handle = load().inccl_switch_create(self.fan_in, int(slots), int(device))
         if not self.handle:
             raise IncclError(load().inccl_last_error().decode(errors="replace"))
 
@@ -629,16 +639,17 @@ class GpuSwitch:
 
     def _out_args(self, frames, count, templates, out_stride, out, out_len):
         torch = _torch()
-        if templates.dtype != torch.uint8 or templates.numel() != 28 * self.fan_in:
-            raise ValueError("templates: fan_in x 28-byte inccl_frame_template records (uint8)")
+        rows = self.rows
+        if templates.dtype != torch.uint8 or templates.numel() != 28 * rows:
+            raise ValueError(f"templates: {rows} x 28-byte inccl_frame_template records (uint8)")
         if out is None:
-            out = torch.empty((count * self.fan_in, out_stride), dtype=torch.uint8, device=frames.device)
-        elif out.dtype != torch.uint8 or out.dim() != 2 or out.shape[0] < count * self.fan_in:
-            raise ValueError("out: uint8 [count * fan_in, out_stride]")
+            out = torch.empty((count * rows, out_stride), dtype=torch.uint8, device=frames.device)
+        elif out.dtype != torch.uint8 or out.dim() != 2 or out.shape[0] < count * rows:
+            raise ValueError(f"out: uint8 [count * {rows}, out_stride]")
         if out_len is None:
-            out_len = torch.empty(count * self.fan_in, dtype=torch.int32, device=frames.device)
+            out_len = torch.empty(count * rows, dtype=torch.int32, device=frames.device)
         _dev_ptr(out, torch.uint8, "out")
-        _dev_ptr(out_len, torch.int32, "out_len", count * self.fan_in)
+        _dev_ptr(out_len, torch.int32, "out_len", count * rows)
         return out, out_len
 
     def batch(self, frames, ports, templates, out_stride: int = 1152, stream=None, out=None, out_len=None,
@@ -661,7 +672,7 @@ class GpuSwitch:
 
     def egress(self, frames, ports, action, psn, templates, out_stride: int = 1152, stream=None, out=None,
                out_len=None):
-        """Row i * fan_in + c is child c's frame for input frame i; out_len says
+        """Row i * rows + c is row c's frame for input frame i; out_len says
         which rows were written (bytes, or 0).  Unwritten rows keep whatever the
         buffer held: `out` / `out_len` may be passed in and reused."""
         torch = _torch()
@@ -674,6 +685,13 @@ class GpuSwitch:
                                          _dev_ptr(templates, torch.uint8, "templates"), out.data_ptr(), out_stride,
                                          out_len.data_ptr(), _stream_handle(stream)), "inccl_switch_egress")
         return out, out_len
+
+    def result_ptr(self, psn: int) -> int:
+        """Device address of a non-root's result slot for `psn` (inccl_switch_result)."""
+        p = load().inccl_switch_result(self.handle, int(psn))
+        if not p:
+            raise IncclError("inccl_switch_result: not a non-root switch")
+        return p
 
     def destroy(self):
         if self.handle:

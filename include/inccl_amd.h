@@ -344,6 +344,16 @@ int inccl_allreduce_f32_host(struct inccl_communicator *comm, const float *src_h
 #define INCCL_SW_REPLAY 4     /* retransmit of a completed slot: resend to its port (nts.c:354-356) */
 #define INCCL_SW_ACK 5        /* UP ACK: egress reflects a 62-B ACK to its port (nts.c:403-406) */
 #define INCCL_SW_INVALID 6    /* bad port or payload length (nts.c:350) */
+#define INCCL_SW_FORWARD 7    /* non-root: the slot's aggregate to the parent (nts.c:394-397, :476-479;
+                               * a resend after a round of retransmits, :381-384, :462-465) */
+#define INCCL_SW_DOWN 8       /* non-root: the parent's result, taken and sent to every child (nts.c:412-419) */
+
+/* Non-root switch options (inccl_switch_create_nonroot); 0 is the reference. */
+#define INCCL_SW_WIRE_ORDER 1 /* children get the parent's words as sent; the reference reverses
+                               * each word's bytes (memcpy of wire words, nts.c:413, then htonl) */
+#define INCCL_SW_RECYCLE 2    /* clear slot psn + slots/2 when the parent's result for psn is taken,
+                               * as the root does at completion; the reference never recycles a
+                               * non-root slot, so its ring serves `slots` PSNs and no more */
 
 /* One child connection (the fields of util.h connection_t that egress uses). */
 struct inccl_frame_template {
@@ -356,6 +366,22 @@ struct inccl_switch;
 
 /* fan_in children (1..31), `slots` PSN slots (power of two), on `device` (-1 = current). */
 struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device);
+/* A non-root switch (nts.c:376-400, :408-423, :457-499): children on ports 0..fan_in-1 and the
+ * parent on port fan_in; `flags` INCCL_SW_WIRE_ORDER | INCCL_SW_RECYCLE.  Ingress and egress as
+ * below with fan_in + 1 rows (and templates) per input frame, row fan_in being the parent's:
+ *   FORWARD  the parent's row: the aggregate, the frame's opcode, a zeroed RETH for WRITE_FIRST /
+ *            ONLY (send_roce_data_with_reth(FAN_IN, NULL), nts.c:464, :478)
+ *   DOWN     every child: the parent's result with the parent frame's opcode and the child's
+ *            kept RETH; a parent frame arriving before every child's, or after one was taken,
+ *            is DROPPED (nts.c:412, :420-422); an ACK from the parent is IGNORED (:424-426)
+ *   REPLAY   the retransmitting child: the parent's result (nts.c:378-380)
+ * Each slot's frames of a batch are decided in arrival order, one slot per lane, so a batch
+ * costs more the more copies one PSN has in it (a slot's first 16 in registers). */
+struct inccl_switch *inccl_switch_create_nonroot(int fan_in, uint32_t slots, int device, int flags);
+/* device pointer of a non-root's result slot for `psn`: what the reference's aggregator holds once
+ * the parent's result is taken (its wire words, or host words with INCCL_SW_WIRE_ORDER); the
+ * aggregate sent up stays in inccl_switch_slot.  NULL for a root. */
+const int32_t *inccl_switch_result(struct inccl_switch *sw, uint32_t psn);
 int inccl_switch_destroy(struct inccl_switch *sw);
 int inccl_switch_reset(struct inccl_switch *sw, void *stream);
 /* device pointer of the 256-lane aggregator slot of `psn`: the wrap-around sum of the arrivals counted

@@ -1,0 +1,236 @@
+"""The non-root switch on the GPU (inccl_switch_create_nonroot;
+non_termination_switch.c:376-400, :408-423, :457-499) against the oracle's
+serial pipeline() (gpu): every frame's action and every row it sends, byte for
+byte, in both driving modes (split ingress + egress, and one batch call), with
+the reference's byte order and no-recycle (flags 0) and with each option.
+
+Parity of the non-root role is pinned by the oracle restatement only (the
+reference needs libpcap to build and holds no non-root fixture): see
+tests/test_oracle_nonroot.py for the hand-worked sequences that check it."""
+import numpy as np
+import pytest
+
+from test_gpu_switch import ACK, MODES, STRIDE, _host_frame, _random_op, _rows, _run, _templates
+
+pytestmark = pytest.mark.gpu
+INT32_MIN, INT32_MAX = -(2 ** 31), 2 ** 31 - 1
+
+
+def _amap(orc, inccl):
+    return {orc.SW_ABSORBED: inccl.SW_ABSORBED, orc.SW_BROADCAST: inccl.SW_COMPLETED, orc.SW_REPLAY: inccl.SW_REPLAY,
+            orc.SW_DROPPED: inccl.SW_DROPPED, orc.SW_ACK: inccl.SW_ACK, orc.SW_IGNORED: inccl.SW_IGNORED,
+            orc.SW_INVALID: inccl.SW_INVALID, orc.SW_FORWARD: inccl.SW_FORWARD, orc.SW_DOWN: inccl.SW_DOWN}
+
+
+def _check(orc, inccl, ref, tmpl, frames, ports, stride, action, out, out_len, tag):
+    amap = _amap(orc, inccl)
+    rows = ref.rows
+    seen = {}
+    for i, (f, port) in enumerate(zip(frames, ports)):
+        rc, outs = ref.pipeline(tmpl, port, f, stride)
+        seen[rc] = seen.get(rc, 0) + 1
+        assert int(action[i]) == amap[rc], (tag, i, port, f[42], int(action[i]), amap[rc])
+        for c in range(rows):
+            row = i * rows + c
+            if outs[c] is None:
+                assert out_len[row] == 0, (tag, i, c, int(out_len[row]))
+            else:
+                assert out_len[row] == len(outs[c]), (tag, i, c, int(out_len[row]), len(outs[c]))
+                assert bytes(out[row, : len(outs[c])]) == outs[c], (tag, i, c)
+    return seen
+
+
+def _batch_items(rng, fan_in, psns, prev):
+    """One batch: every child's first copy of each PSN, retransmits (enough
+    for the resend rule's degree % fan_in == 0), copies of the parent's result
+    (some before the children complete), ACKs from children and the parent,
+    an opcode the switch ignores, a port past the parent; shuffled."""
+    F = fan_in
+    items = [(p, c, _random_op(rng)) for p in psns for c in range(F)]
+    items += [(int(rng.choice(psns)), int(rng.integers(0, F)), _random_op(rng)) for _ in range(len(psns) * F // 2)]
+    items += [(int(p), F, _random_op(rng)) for p in psns for _ in range(int(rng.integers(0, 3)))]
+    if prev:   # late copies of the previous batch's PSNs, from children and the parent
+        items += [(int(rng.choice(prev)), int(rng.integers(0, F + 1)), _random_op(rng)) for _ in range(4)]
+    items += [(int(rng.integers(0, 1 << 24)), int(rng.integers(0, F + 1)), ACK) for _ in range(F + 2)]
+    items += [(psns[0], 0, 0x64), (psns[0], F + 1, 0x07)]
+    return [items[i] for i in rng.permutation(len(items))]
+
+
+# flags: 0 = the reference (reversed downstream words, no recycle), 1 wire order, 2 recycle, 3 both.
+# Fan-in 2, 3, 4 and 8 take the unrolled egress; 1, 5, 20, 31 the loop (20, 31: the parent's
+# RETH past the 16 children the keeper prefetch covers).  Stride 1100: 4-byte aligned rows.
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("fan_in,stride,flags", [(2, STRIDE, 0), (2, STRIDE, 1), (2, STRIDE, 2), (3, STRIDE, 3),
+                                                 (1, STRIDE, 0), (4, 1100, 0), (8, STRIDE, 2), (5, 1100, 1),
+                                                 (20, STRIDE, 0), (31, STRIDE, 3)])
+def test_nonroot_batches(gpu, orc, fan_in, stride, flags, mode):
+    import torch
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(500 + 17 * fan_in + flags)
+    slots, per_batch, batches = 64, 8, 5
+    sw = inccl.GpuSwitch(fan_in, slots, nonroot=True, flags=flags)
+    ref = orc.Switch(fan_in, slots, nonroot=True, flags=flags)
+    tmpl = _templates(fan_in + 1)
+    tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
+    total = {}
+    prev = []
+    for b in range(batches):
+        psns = list(range(b * per_batch, (b + 1) * per_batch))
+        items = _batch_items(rng, fan_in, psns, prev)
+        prev = psns
+        frames = [_host_frame(orc, rng, p, port, op) for (p, port, op) in items]
+        ports = [port for (_, port, _) in items]
+        fr = _rows(frames, gpu, stride)
+        pt = torch.tensor(ports, dtype=torch.int32, device=gpu)
+        action, psn_out, out, out_len = _run(sw, mode, fr, pt, tmpl_dev, out_stride=stride)
+        torch.cuda.synchronize()
+        action, psn_out = action.cpu().numpy(), psn_out.cpu().numpy()
+        out, out_len = out.cpu().numpy(), out_len.cpu().numpy()
+        for i, (p, port, op) in enumerate(items):
+            if port <= fan_in:
+                assert psn_out[i] == p, (i, p)
+        for k, v in _check(orc, inccl, ref, tmpl, frames, ports, stride, action, out, out_len, b).items():
+            total[k] = total.get(k, 0) + v
+    want = [orc.SW_FORWARD, orc.SW_DOWN, orc.SW_REPLAY, orc.SW_DROPPED, orc.SW_ACK, orc.SW_IGNORED, orc.SW_INVALID]
+    if fan_in > 1:
+        want.append(orc.SW_ABSORBED)
+    for k in want:
+        assert total.get(k, 0) > 0, (k, total)
+    sw.destroy()
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("flags", [0, 2])
+def test_nonroot_reference_ring_reuse(gpu, orc, flags, mode):
+    """The reference's 16-slot ring past its first 16 PSNs: without recycling
+    (the reference) PSN p + 16 meets p's bits and result, and every copy of it
+    is answered from p's slot; with SW_RECYCLE it starts afresh.  Batches of 4
+    PSNs (span below slots / 2 with the late copies), PSNs 0..39."""
+    import torch
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(600 + flags)
+    F = 2
+    sw = inccl.GpuSwitch(F, 16, nonroot=True, flags=flags)
+    ref = orc.Switch(F, 16, nonroot=True, flags=flags)
+    tmpl = _templates(F + 1)
+    tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
+    prev = []
+    total = {}
+    for b in range(10):
+        psns = list(range(4 * b, 4 * b + 4))
+        items = _batch_items(rng, F, psns, prev)
+        items += [(p, F, 0x07) for p in psns]   # a result for every PSN after its children
+        prev = psns
+        frames = [_host_frame(orc, rng, p, port, op) for (p, port, op) in items]
+        ports = [port for (_, port, _) in items]
+        action, psn_out, out, out_len = _run(sw, mode, _rows(frames, gpu), torch.tensor(ports, dtype=torch.int32,
+                                                                                       device=gpu), tmpl_dev)
+        torch.cuda.synchronize()
+        for k, v in _check(orc, inccl, ref, tmpl, frames, ports, STRIDE, action.cpu().numpy(), out.cpu().numpy(),
+                           out_len.cpu().numpy(), b).items():
+            total[k] = total.get(k, 0) + v
+    if flags == 0:   # PSNs 16..39: stale slots, no first copy counts
+        assert total[orc.SW_REPLAY] > total.get(orc.SW_ABSORBED, 0)
+    sw.destroy()
+
+
+def test_nonroot_result_slot_and_sums(gpu, orc):
+    """A large batch (fan-in 2, 12 000 PSNs, every child's copy then the
+    parent's result): every PSN forwards the wrap-around sum once, every result
+    is taken, the parent rows carry htonl(sum), the child rows the result with
+    each word's bytes reversed (the reference), and inccl_switch_result holds
+    the parent's wire words."""
+    import torch
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(700)
+    F, P = 2, 12000
+    base = np.frombuffer(orc.build_data_frame(np.zeros(256, np.int32), psn=0, opcode=0x07, qp=0x11), np.uint8)
+    n = (F + 1) * P
+    psn = np.repeat(np.arange(P, dtype=np.uint32), F + 1)
+    port = np.tile(np.arange(F + 1, dtype=np.int32), P)   # children first, then the parent, per PSN
+    pay = rng.integers(INT32_MIN, INT32_MAX, (n, 256), dtype=np.int64, endpoint=True).astype(np.int32)
+    frames = np.zeros((n, STRIDE), np.uint8)
+    frames[:, : len(base)] = base
+    frames[:, 54:54 + 1024] = pay.astype(">i4").view(np.uint8).reshape(n, 1024)
+    frames[:, 50:54] = (psn | 0x80000000).astype(">u4").view(np.uint8).reshape(n, 4)
+    sw = inccl.GpuSwitch(F, 1 << 15, nonroot=True)
+    tmpl = _templates(F + 1)
+    tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
+    action, psn_out, out, out_len = sw.batch(torch.from_numpy(frames).to(gpu), torch.from_numpy(port).to(gpu), tmpl_dev)
+    torch.cuda.synchronize()
+    act = action.cpu().numpy().reshape(P, F + 1)
+    assert (act[:, 0] == inccl.SW_ABSORBED).all() and (act[:, 1] == inccl.SW_FORWARD).all()
+    assert (act[:, 2] == inccl.SW_DOWN).all()
+    ln = out_len.cpu().numpy().reshape(P, F + 1, F + 1)
+    assert (ln[:, 0] == 0).all()
+    assert (ln[:, 1, :F] == 0).all() and (ln[:, 1, F] == 1082).all()
+    assert (ln[:, 2, :F] == 1082).all() and (ln[:, 2, F] == 0).all()
+    o = out.view(P, F + 1, F + 1, -1)
+    agg = pay.reshape(P, F + 1, 256)[:, :F].view(np.uint32).sum(axis=1, dtype=np.uint64).astype(np.uint32)
+    up = o[:, 1, F, 54:54 + 1024].cpu().numpy().copy().view(">u4").astype(np.uint32)
+    assert np.array_equal(up, agg)
+    y = pay.reshape(P, F + 1, 256)[:, F]
+    for c in range(F):
+        dn = o[:, 2, c, 54:54 + 1024].cpu().numpy().copy().view("<u4")   # bytes reversed: little-endian reads y
+        assert np.array_equal(dn, y.view(np.uint32)), c
+    crc = inccl.icrc_frames(o[:, 2, 0].contiguous()).cpu().numpy().view(np.uint32)
+    stored = o[:, 2, 0, 1078:1082].cpu().numpy().copy().view("<u4").ravel()
+    assert np.array_equal(crc, stored)
+    for p in (0, 1, P - 1, int(rng.integers(0, P))):   # the result slot: the wire words, as nts.c:413 keeps them
+        ptr = sw.result_ptr(p)
+        import ctypes
+        from container_inc_amd._lib import runtime_libs
+        buf = torch.empty(256, dtype=torch.int32, device=gpu)
+        hip = ctypes.CDLL(runtime_libs()["libamdhip64"])
+        assert hip.hipMemcpy(ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(1024), 3) == 0
+        torch.cuda.synchronize()
+        want = np.frombuffer(y[p].astype(">i4").tobytes(), "<i4")
+        assert np.array_equal(buf.cpu().numpy(), want), p
+    sw.destroy()
+
+
+def test_nonroot_graph_replay(gpu, orc):
+    """A non-root batch captured into a hipGraph (after an uncaptured batch as
+    large, which sizes the list links) and replayed with new frames each time:
+    the same actions and rows as the oracle's serial pipeline()."""
+    import torch
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(800)
+    F, per = 3, 6
+    sw = inccl.GpuSwitch(F, 64, nonroot=True, flags=inccl.SW_RECYCLE)
+    ref = orc.Switch(F, 64, nonroot=True, flags=orc.SW_RECYCLE)
+    tmpl = _templates(F + 1)
+    tmpl_dev = torch.from_numpy(tmpl.view(np.uint8).copy()).to(gpu)
+
+    def make(b, prev):
+        psns = list(range(b * per, (b + 1) * per))
+        items = _batch_items(rng, F, psns, prev)[:48]
+        items += [(psns[0], 0, ACK)] * (48 - len(items))
+        return psns, items
+
+    psns, items = make(0, [])
+    frames = [_host_frame(orc, rng, p, port, op) for (p, port, op) in items]
+    ports = [port for (_, port, _) in items]
+    fr, pt = _rows(frames, gpu), torch.tensor(ports, dtype=torch.int32, device=gpu)
+    action, psn_out, out, out_len = sw.batch(fr, pt, tmpl_dev)
+    torch.cuda.synchronize()
+    _check(orc, inccl, ref, tmpl, frames, ports, STRIDE, action.cpu().numpy(), out.cpu().numpy(),
+           out_len.cpu().numpy(), 0)
+    st = torch.cuda.Stream(device=gpu)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        sw.batch(fr, pt, tmpl_dev, stream=st, out=out, out_len=out_len, action=action, psn=psn_out)
+    prev = psns
+    for b in range(1, 5):
+        psns, items = make(b, prev)
+        prev = psns
+        frames = [_host_frame(orc, rng, p, port, op) for (p, port, op) in items]
+        ports = [port for (_, port, _) in items]
+        fr.copy_(_rows(frames, gpu))
+        pt.copy_(torch.tensor(ports, dtype=torch.int32, device=gpu))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        _check(orc, inccl, ref, tmpl, frames, ports, STRIDE, action.cpu().numpy(), out.cpu().numpy(),
+               out_len.cpu().numpy(), b)
+    sw.destroy()
