@@ -34,12 +34,11 @@ typedef struct InccSwitchState {
                           *                     (nts.c:413: wire words; ntohl'd with INCCL_SW_WIRE_ORDER) */
     uint32_t *bits;      /* [slots]             arrival bitmap: children, bit fan_in = parent's result (nts.c:59) */
     uint32_t *head;      /* [slots]             the batch's frame list of each slot (~0: empty; reset by its owner) */
-    uint32_t *counted;   /* [slots][fan_in]     frame whose payload the batch adds for each child, ~0: none;
-                          *                     bit 31: WRITE_FIRST (payload at byte 70) */
-    uint32_t *down;      /* [slots]             the parent frame the batch takes, ~0: none; bit 31 as above */
-    uint32_t *work;      /* [1 + slots]         work[0]: slots with a sum or a result this batch; then their
-                          *                     PSNs, bit 31 = the slot held arrivals before the batch */
-    uint32_t *link;      /* [frames][2]         per frame: next frame of its slot's list, port | WF << 8 */
+    uint32_t *work;      /* [inccl_k_nr_work_words]  64 region counters, then per region the records of its
+                          *                     classify blocks' slots: PSN | the slot held arrivals before the
+                          *                     batch << 31, the parent frame taken, the frame counted for each
+                          *                     child (~0: none; bit 31: WRITE_FIRST, payload at byte 70) */
+    uint32_t *link;      /* [frames][2]         per frame (one 8-byte word): next frame of its slot's list, port | WF << 8 */
 } InccSwitchState;
 
 #define INCCL_FRAME_MIN_STRIDE 64   /* a row must hold the 62-B ACK frame (headers through the BTH) */
@@ -47,6 +46,8 @@ typedef struct InccSwitchState {
 typedef struct inccl_frame_template InccFrameTemplate;
 
 int inccl_k_frames_init(void);
+/* words of a non-root batch's work records for `count` frames */
+size_t inccl_k_nr_work_words(size_t count, int fan_in);
 int inccl_k_icrc(const uint8_t *frames, size_t stride, size_t count, uint32_t *out, void *stream);
 int inccl_k_switch_ingress(const InccSwitchState *s, const uint8_t *frames, size_t stride, size_t count,
                            const int32_t *ports, int32_t *action, uint32_t *psn_out, void *stream);

@@ -20,7 +20,10 @@
 //                     state ingress left, and the ACK reflections (:403-406),
 //                     frames per util.c:331-442
 // inccl_switch_ingress runs the first three, inccl_switch_egress the last,
-// inccl_switch_batch all four.  The ICRC is linear over GF(2), so every CRC
+// inccl_switch_batch all four.  A non-root switch (nts.c:376-400, :408-423,
+// :457-499) runs k_nr_claim / k_nr_classify / k_nr_sum for ingress (each
+// slot's frames decided in arrival order by one lane) and k_egress<F, O, true>,
+// whose row fan_in per input frame is the parent's.  The ICRC is linear over GF(2), so every CRC
 // here is a XOR of table lookups reduced over the wave with DPP -- no serial
 // byte loop.
 //
@@ -901,8 +904,8 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
 //   k_nr_classify  a lane per owner: the slot's frames in index order through
 //                  UP first copy / resend / replay and DOWN taken / ignored,
 //                  the RETH keeper (:470), bitmap and degree, the recycle
-//                  (INCCL_SW_RECYCLE); which frames' payloads count, and the
-//                  slot onto the batch's work list
+//                  (INCCL_SW_RECYCLE); the slot's work record: which frames'
+//                  payloads count
 //   k_nr_sum       a wave per work item: the counted payloads added to the
 //                  aggregate (:390-392, :472-474) and the parent's result into
 //                  res (:413, :489)
@@ -914,14 +917,23 @@ __global__ __launch_bounds__(kWave* kApplyWaves) void k_ingress_sum(ApplyArgs A,
 // so a list can never send a lane outside the batch.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr int kNrList = 16;
+constexpr int kNrList = 8;
+// work records go to kNrShards regions, classify block b into region b % kNrShards,
+// each region with its own counter (work[0 .. kNrShards-1]): one counter for
+// all serialised the waves' atomics at one L2 channel (28 us per 131 072-frame
+// batch, 2 048 atomics)
+constexpr int kNrShards = 64;
+__host__ __device__ constexpr uint32_t nr_region_cap(int64_t count)
+{
+    return (uint32_t)((((count + kClassifyBlock - 1) / kClassifyBlock) + kNrShards - 1) / kNrShards) * kClassifyBlock;
+}
 
 __global__ __launch_bounds__(kClaimBlock) void k_nr_claim(InccSwitchState s, const uint8_t* __restrict__ frames,
                                                           int64_t stride, int64_t count,
                                                           const int32_t* __restrict__ ports,
                                                           int32_t* __restrict__ action, uint32_t* __restrict__ psn_out)
 {
-    if (blockIdx.x == 0 && threadIdx.x == 0) s.work[0] = 0u;   // classify (the next launch) appends
+    if (blockIdx.x == 0 && threadIdx.x < kNrShards) s.work[threadIdx.x] = 0u;   // classify (the next launch) appends
     const int64_t f = (int64_t)blockIdx.x * kClaimBlock + threadIdx.x;
     if (f >= count) return;
     const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + f * stride);
@@ -940,8 +952,8 @@ __global__ __launch_bounds__(kClaimBlock) void k_nr_claim(InccSwitchState s, con
         if (data_len != kLanes * 4 || 54 + (wf ? 16 : 0) + kLanes * 4 > stride) act = INCCL_SW_INVALID;
         else {
             const uint32_t slot = psn & (s.slots - 1);
-            s.link[2 * f] = atomicExch(&s.head[slot], (uint32_t)f);
-            s.link[2 * f + 1] = (uint32_t)port | (wf ? 1u << 8 : 0u);
+            const uint32_t next = atomicExch(&s.head[slot], (uint32_t)f);
+            reinterpret_cast<u2*>(s.link)[f] = u2{next, (uint32_t)port | (wf ? 1u << 8 : 0u)};
             act = kActPending;
         }
     }
@@ -955,43 +967,67 @@ __global__ __launch_bounds__(kClassifyBlock) void k_nr_classify(InccSwitchState 
                                                                 const uint32_t* __restrict__ psns)
 {
     const int64_t f = (int64_t)blockIdx.x * kClassifyBlock + threadIdx.x;
-    if (f >= count || action[f] != kActPending || s.link[2 * f] != kNone) return;   // owners only
-    const uint32_t psn = psns[f], slot = psn & (s.slots - 1);
-    const int fan = s.fan_in;
+    if (f >= count) return;
+    const u2* link = reinterpret_cast<const u2*>(s.link);
+    // one round trip: the claim result, the frame's own link, its PSN
+    const int a = (int)opaque_u32((uint32_t)action[f]);
+    const u2 own = link[f];
+    const uint32_t psn = opaque_u32(psns[f]);
+    if (a != kActPending || own.x != kNone) return;   // owners only (next = none)
+    const uint32_t slot = psn & (s.slots - 1);
     const uint32_t h0 = s.head[slot];
+    uint32_t B = s.bits[slot], D = (uint32_t)s.degree[slot], downf = kNone;   // (loaded while the list is walked)
     s.head[slot] = kNone;   // empty for the next batch
-    __shared__ uint32_t lds_list[kClassifyBlock][kNrList + 1];   // (+1: no two lanes' rows on one bank)
-    uint32_t* L = lds_list[threadIdx.x];
+    // the slot's work record for the sum: {psn | partial << 31, parent frame,
+    // counted frame per child}, in this block's region (the compiler makes the
+    // wave's owners one atomic)
+    const int fan = s.fan_in;
+    const uint32_t k = blockIdx.x % kNrShards;
+    const uint32_t idx = atomicAdd(&s.work[k], 1u);
+    uint32_t* rec = s.work + kNrShards + ((size_t)k * nr_region_cap(count) + idx) * (fan + 2);
+    // the list: (frame, port | WF << 8) pairs, each hop one 8-byte load; the
+    // owner's own entry (the list's end) is already in registers
+    __shared__ u2 lds_list[kClassifyBlock][kNrList + 1];   // (+1: lanes' rows spread over the banks)
+    u2* L = lds_list[threadIdx.x];
     const uint32_t nfr = (uint32_t)count;
     int n = 0;
-    for (uint32_t g = h0; g < nfr; g = s.link[2 * (size_t)g]) {
-        if (n < kNrList) L[n] = g;
+    for (uint32_t g = h0; g < nfr;) {
+        const u2 e = g == (uint32_t)f ? own : link[g];
+        if (n < kNrList) L[n] = u2{g, e.y};
         ++n;
+        g = e.x;
     }
     const bool kept = n <= kNrList;
     if (kept)
         for (int i = 1; i < n; ++i)   // insertion sort: arrival order
-            for (int j = i; j > 0 && L[j - 1] > L[j]; --j) {
-                const uint32_t t = L[j];
+            for (int j = i; j > 0 && L[j - 1].x > L[j].x; --j) {
+                const u2 t = L[j];
                 L[j] = L[j - 1];
                 L[j - 1] = t;
             }
     const uint32_t cmask = 0xFFFFFFFFu >> (32 - fan), rbit = 1u << fan;   // nts.c:29, :366
-    uint32_t B = s.bits[slot], D = (uint32_t)s.degree[slot], downf = kNone;
     const bool partial = (B & cmask) != 0u;
-    bool summed = false;
-    uint32_t* cnt = s.counted + (size_t)slot * fan;
+    uint32_t* cnt = rec + 2;
     for (int q = 0; q < fan; ++q) cnt[q] = kNone;
     int64_t prev = -1;
     for (int i = 0; i < n; ++i) {
-        uint32_t g = kNone;
-        if (kept) g = L[i];
-        else   // the earliest frame after the previous one
-            for (uint32_t h = h0; h < nfr; h = s.link[2 * (size_t)h])
-                if ((int64_t)h > prev && h < g) g = h;
+        uint32_t g = kNone, info = 0u;
+        if (kept) {
+            g = L[i].x;
+            info = L[i].y;
+        } else {   // the earliest frame after the previous one
+            for (uint32_t h = h0; h < nfr;) {
+                const u2 e = link[h];
+                if ((int64_t)h > prev && h < g) {
+                    g = h;
+                    info = e.y;
+                }
+                h = e.x;
+            }
+        }
         if (g >= nfr) break;
         prev = g;
-        const uint32_t info = s.link[2 * (size_t)g + 1], port = info & 0xFFu, wf = (info >> 8) & 1u;
+        const uint32_t port = info & 0xFFu, wf = (info >> 8) & 1u;
         int act;
         if ((int)port < fan) {
             D += 1u;   // nts.c:351, :431
@@ -1003,7 +1039,6 @@ __global__ __launch_bounds__(kClassifyBlock) void k_nr_classify(InccSwitchState 
             else {   // first transmission (:387-398, :468-480)
                 B |= pb;
                 cnt[port] = g | (wf << 31);
-                summed = true;
                 if (wf) {   // the RETH into the keeper (:470): frame bytes 54-69
                     const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + (int64_t)g * stride);
                     uint32_t rw[5];
@@ -1032,45 +1067,120 @@ __global__ __launch_bounds__(kClassifyBlock) void k_nr_classify(InccSwitchState 
     }
     s.bits[slot] = B;
     s.degree[slot] = (int32_t)D;
-    s.down[slot] = downf;
-    if (summed || downf != kNone) s.work[1 + atomicAdd(&s.work[0], 1u)] = (psn & 0x00FFFFFFu) | (partial ? 1u << 31 : 0u);
+    rec[0] = (psn & 0x00FFFFFFu) | (partial ? 1u << 31 : 0u);
+    rec[1] = downf;
 }
 
 constexpr int kNrSumWaves = 4;
+constexpr int kNrSumRows = 2;   // rows whose payload chunks a wave has in flight at once
 
+// Payload words 4 lane .. 4 lane + 3 of a row (host order) from its 16-byte
+// chunks: xx = chunk 3 + lane, ee = the tail chunks lane 63 needs
+// (tail_chunks); the payload starts 6 bytes into chunk 3 + wf (as k_ingress_sum)
+__device__ __forceinline__ void chunks_payload(const u4& xx, const u2& ee, uint32_t wf, int lane, int next4,
+                                               uint32_t (&P)[4])
+{
+    const bool last = lane == kWave - 1;
+    uint32_t y0 = from_next(xx.x, next4), y1 = from_next(xx.y, next4);
+    y0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.x, 0) : y0;
+    y1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.y, 0) : y1;
+    if (wf) {
+        uint32_t y2 = from_next(xx.z, next4), y3 = from_next(xx.w, next4);
+        uint32_t z0 = from_next(y0, next4), z1 = from_next(y1, next4);
+        y2 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.x, 1) : y2;
+        y3 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.y, 1) : y3;
+        z0 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.x, 2) : z0;
+        z1 = last ? (uint32_t)__builtin_amdgcn_readlane((int)ee.y, 2) : z1;
+        payload_from_chunks(u4{y0, y1, y2, y3}, z0, z1, P);
+    } else {
+        payload_from_chunks(xx, y0, y1, P);
+    }
+}
+
+// A wave per work record (lane j: word j), the next record in flight while
+// one is summed: its rows' payload chunks kNrSumRows at a time (the children's
+// counted copies, then the parent's result) with the slot's partial.
 __global__ __launch_bounds__(kWave* kNrSumWaves) void k_nr_sum(InccSwitchState s, const uint8_t* __restrict__ frames,
                                                               int64_t stride, int64_t count, int wide)
 {
-    const uint32_t n = s.work[0];
     const int lane = threadIdx.x % kWave, fan = s.fan_in;
-    const uint32_t nw = gridDim.x * kNrSumWaves;
-    for (uint32_t i = blockIdx.x * kNrSumWaves + threadIdx.x / kWave; i < n; i += nw) {
-        const uint32_t w = s.work[1 + i], slot = w & (s.slots - 1);
+    const int next4 = ((lane + 1) & (kWave - 1)) * 4;
+    // wave w takes region w % kNrShards, its records w / kNrShards, + nw / kNrShards, ...
+    const uint32_t wid = blockIdx.x * kNrSumWaves + threadIdx.x / kWave;
+    const uint32_t k = wid % kNrShards, nw = gridDim.x * kNrSumWaves / kNrShards, nfr = (uint32_t)count;
+    const uint32_t n = s.work[k];
+    const bool wire = (s.flags & INCCL_SW_WIRE_ORDER) != 0;
+    const int rw = fan + 2;   // record words
+    const uint32_t* recs = s.work + kNrShards + (size_t)k * nr_region_cap(count) * rw;
+    uint32_t i = wid / kNrShards;
+    uint32_t r = i < n && lane < rw ? recs[(size_t)i * rw + lane] : kNone;
+    for (; i < n; i += nw) {
+        const uint32_t cq = r;
+        r = i + nw < n && lane < rw ? recs[(size_t)(i + nw) * rw + lane] : kNone;
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cq, 0), slot = w & (s.slots - 1);
+        const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)cq, 1);
         u4 acc = {0u, 0u, 0u, 0u};
         if (w >> 31) acc = reinterpret_cast<const u4*>(s.agg + (size_t)slot * kLanes)[lane];
-        bool any = false;
-        uint32_t P[4];
-        for (int q = 0; q < fan; ++q) {
-            const uint32_t c = s.counted[(size_t)slot * fan + q];
-            if ((c & 0x7FFFFFFFu) >= (uint64_t)count) continue;   // none (~0)
-            any = true;
-            payload16(frames + (int64_t)(c & 0x7FFFFFFFu) * stride, c >> 31, lane, wide != 0, P);
-            acc.x += P[0];
-            acc.y += P[1];
-            acc.z += P[2];
-            acc.w += P[3];
+        uint64_t m = __ballot(lane >= 2 && lane < rw && (cq & 0x7FFFFFFFu) < nfr);   // (~0: none)
+        const bool any = m != 0;
+        bool down = (d & 0x7FFFFFFFu) < nfr;
+        while (m || down) {
+            uint32_t row[kNrSumRows];
+            int kind[kNrSumRows];   // 0 none, 1 a child's counted copy, 2 the parent's result
+#pragma unroll
+            for (int r = 0; r < kNrSumRows; ++r) {
+                if (m) {
+                    row[r] = (uint32_t)__builtin_amdgcn_readlane((int)cq, __builtin_ctzll(m));
+                    m &= m - 1;
+                    kind[r] = 1;
+                } else if (down) {
+                    row[r] = d;
+                    down = false;
+                    kind[r] = 2;
+                } else {
+                    row[r] = 0u;
+                    kind[r] = 0;
+                }
+            }
+            uint32_t P[kNrSumRows][4];
+            if (wide) {
+                u4 x[kNrSumRows];
+                u2 e[kNrSumRows];
+#pragma unroll
+                for (int r = 0; r < kNrSumRows; ++r) {
+                    const __amdgpu_buffer_rsrc_t rs =
+                        uniform_rsrc(frames + (int64_t)(row[r] & 0x7FFFFFFFu) * stride, kind[r] ? stride : 0);
+                    x[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, 48 + 16 * lane, 0, 0);
+                    e[r] = tail_chunks(rs, 0, lane);
+                }
+#pragma unroll
+                for (int r = 0; r < kNrSumRows; ++r) chunks_payload(x[r], e[r], row[r] >> 31, lane, next4, P[r]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < kNrSumRows; ++r)
+                    if (kind[r]) payload16(frames + (int64_t)(row[r] & 0x7FFFFFFFu) * stride, row[r] >> 31, lane, false, P[r]);
+            }
+#pragma unroll
+            for (int r = 0; r < kNrSumRows; ++r) {
+                if (kind[r] == 1) {
+                    acc.x += P[r][0];
+                    acc.y += P[r][1];
+                    acc.z += P[r][2];
+                    acc.w += P[r][3];
+                } else if (kind[r] == 2) {
+                    // the reference keeps the wire bytes (memcpy, :413): the host words back to wire order
+                    const u4 v = wire ? u4{P[r][0], P[r][1], P[r][2], P[r][3]}
+                                      : u4{__builtin_bswap32(P[r][0]), __builtin_bswap32(P[r][1]),
+                                           __builtin_bswap32(P[r][2]), __builtin_bswap32(P[r][3])};
+                    __builtin_amdgcn_raw_buffer_store_b128(v, uniform_rsrc(s.res + (size_t)slot * kLanes, kLanes * 4),
+                                                           16 * lane, 0, kAuxSc1);
+                }
+            }
         }
-        if (any) reinterpret_cast<u4*>(s.agg + (size_t)slot * kLanes)[lane] = acc;
-        const uint32_t d = s.down[slot];
-        if ((d & 0x7FFFFFFFu) < (uint64_t)count) {   // (~0: none)
-            payload16(frames + (int64_t)(d & 0x7FFFFFFFu) * stride, d >> 31, lane, wide != 0, P);   // ntohl'd
-            const bool wire = (s.flags & INCCL_SW_WIRE_ORDER) != 0;
-            // the reference keeps the wire bytes (memcpy, :413): the host words back to wire order
-            const u4 r = wire ? u4{P[0], P[1], P[2], P[3]}
-                              : u4{__builtin_bswap32(P[0]), __builtin_bswap32(P[1]), __builtin_bswap32(P[2]),
-                                   __builtin_bswap32(P[3])};
-            reinterpret_cast<u4*>(s.res + (size_t)slot * kLanes)[lane] = r;
-        }
+        // write-through, as the root's sum: egress reads the aggregate next
+        if (any)
+            __builtin_amdgcn_raw_buffer_store_b128(acc, uniform_rsrc(s.agg + (size_t)slot * kLanes, kLanes * 4),
+                                                   16 * lane, 0, kAuxSc1);
     }
 }
 
@@ -1802,9 +1912,12 @@ int launch_nr_ingress(const InccSwitchState* s, const uint8_t* frames, size_t st
     hipLaunchKernelGGL(k_nr_classify, dim3((unsigned)((n + kClassifyBlock - 1) / kClassifyBlock)), dim3(kClassifyBlock),
                        0, st, *s, frames, (int64_t)stride, n, action, (const uint32_t*)psn_out);
     const int wide = ((uintptr_t)frames & 15) == 0 && (stride & 15) == 0;
+    // whole groups of kNrShards waves (every region gets the same number of waves)
+    constexpr int64_t group = kNrShards / kNrSumWaves;
     const int64_t need = (n + kNrSumWaves - 1) / kNrSumWaves, cap = (int64_t)num_cus() * 8;
-    hipLaunchKernelGGL(k_nr_sum, dim3((unsigned)(need < cap ? need : cap)), dim3(kWave * kNrSumWaves), 0, st, *s,
-                       frames, (int64_t)stride, n, wide);
+    const int64_t blocks = ((need < cap ? need : cap) + group - 1) / group * group;
+    hipLaunchKernelGGL(k_nr_sum, dim3((unsigned)blocks), dim3(kWave * kNrSumWaves), 0, st, *s, frames, (int64_t)stride,
+                       n, wide);
     return (int)hipGetLastError();
 }
 
@@ -1821,6 +1934,11 @@ int egress_args_ok(const InccSwitchState* s, const uint8_t* frames, const int32_
 extern "C" {
 
 int inccl_k_frames_init(void) { return ensure_tables(); }
+
+size_t inccl_k_nr_work_words(size_t count, int fan_in)
+{
+    return kNrShards + (size_t)kNrShards * nr_region_cap((int64_t)count) * (size_t)(fan_in + 2);
+}
 
 int inccl_k_icrc(const uint8_t* frames, size_t stride, size_t count, uint32_t* out, void* stream)
 {

@@ -1,4 +1,7 @@
-/* switch.c -- host side of the GPU switch dataplane (inccl_frames.hip).
+/* switch.c -- host side of the GPU switch dataplane (inccl_frames.hip), the
+ * root switch (inccl_switch_create) and the non-root one
+ * (inccl_switch_create_nonroot: children below port fan_in, the parent on it,
+ * nts.c:376-400, :408-423, :457-499).
  *
  * The reference's root switch keeps its aggregation state in globals
  * (non_termination_switch.c:55-60) and processes one frame at a time on one
@@ -95,15 +98,14 @@ struct inccl_switch *inccl_switch_create_nonroot(int fan_in, uint32_t slots, int
     }
     struct inccl_switch *sw = (struct inccl_switch *)calloc(1, sizeof(*sw));
     if (!sw) return NULL;
-    /* zeroed: agg, res, bits, degree, reth, work; all-ones: head; counted and
-     * down are written by a slot's owner before anything reads them */
+    /* zeroed: agg, res, bits, degree, reth; all-ones: head (the per-batch
+     * list links and work records grow with the batch, ensure_batch_mem) */
     const size_t S = slots;
     const size_t agg = S * 256 * sizeof(int32_t), words = S * sizeof(uint32_t);
-    const size_t reth = S * (size_t)fan_in * 16, work = (S + 1) * sizeof(uint32_t);
-    const size_t counted = S * (size_t)fan_in * sizeof(uint32_t);
-    const size_t zero_end = (2 * agg + 2 * words + reth + work + 15) & ~(size_t)15;
+    const size_t reth = S * (size_t)fan_in * 16;
+    const size_t zero_end = (2 * agg + 2 * words + reth + 15) & ~(size_t)15;
     sw->first_off = zero_end;
-    sw->bytes = zero_end + words + counted + words;
+    sw->bytes = zero_end + words;
     hipError_t e = hipMalloc(&sw->mem, sw->bytes);
     if (e == hipSuccess) e = hipMemset(sw->mem, 0, zero_end);
     if (e == hipSuccess) e = hipMemset((char *)sw->mem + zero_end, 0xFF, words);
@@ -119,10 +121,7 @@ struct inccl_switch *inccl_switch_create_nonroot(int fan_in, uint32_t slots, int
     sw->st.bits = (uint32_t *)(p + 2 * agg);
     sw->st.degree = (int32_t *)(p + 2 * agg + words);
     sw->st.reth = (uint32_t *)(p + 2 * agg + 2 * words);
-    sw->st.work = (uint32_t *)(p + 2 * agg + 2 * words + reth);
     sw->st.head = (uint32_t *)(p + zero_end);
-    sw->st.counted = (uint32_t *)(p + zero_end + words);
-    sw->st.down = (uint32_t *)(p + zero_end + words + counted);
     sw->st.slots = slots;
     sw->st.fan_in = fan_in;
     sw->st.nonroot = 1;
@@ -142,8 +141,9 @@ const int32_t *inccl_switch_result(struct inccl_switch *sw, uint32_t psn)
     return sw->st.res + (size_t)(psn & (sw->st.slots - 1)) * 256;
 }
 
-/* a non-root batch of `count` frames needs count list links (grown outside
- * stream capture: a captured batch must follow an uncaptured one as large) */
+/* a non-root batch of `count` frames needs count list links and its work
+ * records (inccl_k_nr_work_words; grown outside stream capture: a captured
+ * batch must follow an uncaptured one as large) */
 static int ensure_links(struct inccl_switch *sw, size_t count, void *stream)
 {
     if (!sw->st.nonroot || count <= sw->link_cap) return 0;
@@ -155,9 +155,12 @@ static int ensure_links(struct inccl_switch *sw, size_t count, void *stream)
         hipDeviceSynchronize();
         hipFree(sw->st.link);
         sw->st.link = NULL;
+        sw->st.work = NULL;
         sw->link_cap = 0;
     }
-    INCCL_HIP(hipMalloc((void **)&sw->st.link, count * 2 * sizeof(uint32_t)));
+    const size_t link = count * 2 * sizeof(uint32_t);
+    INCCL_HIP(hipMalloc((void **)&sw->st.link, link + inccl_k_nr_work_words(count, sw->st.fan_in) * sizeof(uint32_t)));
+    sw->st.work = sw->st.link + count * 2;
     sw->link_cap = count;
     return 0;
 }
