@@ -234,3 +234,77 @@ def test_nonroot_graph_replay(gpu, orc):
         _check(orc, inccl, ref, tmpl, frames, ports, STRIDE, action.cpu().numpy(), out.cpu().numpy(),
                out_len.cpu().numpy(), b)
     sw.destroy()
+
+
+@pytest.mark.parametrize("flags", [1, 3])
+def test_two_tier_tree_on_gpu(gpu, orc, flags):
+    """Eight hosts, four fan-in-2 non-root switches and a fan-in-4 root, all on
+    the GPU, 4 096 PSNs per round: the hosts' frames -> each leaf (up batch) ->
+    the leaves' FORWARD rows -> the root (one batch, port = leaf) -> the root's
+    COMPLETED rows -> each leaf (port 2, down batch) -> the DOWN rows -> the
+    hosts.  Every host row carries the eight-way wrap-around sum in wire order
+    (SW_WIRE_ORDER; with SW_RECYCLE too for flags 3) with a valid ICRC; two
+    rounds on consecutive PSN ranges, WRITE_FIRST and WRITE_MIDDLE opcodes."""
+    import torch
+    from container_inc_amd import inccl
+    rng = np.random.default_rng(900 + flags)
+    H, F, L, P = 8, 2, 4, 4096
+    leaves = [inccl.GpuSwitch(F, 4 * P, nonroot=True, flags=flags) for _ in range(L)]
+    root = inccl.GpuSwitch(L, 4 * P)
+    t_leaf = torch.from_numpy(_templates(F + 1).view(np.uint8).copy()).to(gpu)
+    t_root = torch.from_numpy(_templates(L).view(np.uint8).copy()).to(gpu)
+    base = {op: np.frombuffer(orc.build_data_frame(np.zeros(256, np.int32), psn=0, opcode=op, with_reth=op == 0x06,
+                                                   reth=bytes(16) if op == 0x06 else None), np.uint8)
+            for op in (0x06, 0x07)}
+    for rnd in range(2):
+        psn0 = rnd * P
+        pay = rng.integers(INT32_MIN, INT32_MAX, (H, P, 256), dtype=np.int64, endpoint=True).astype(np.int32)
+        total = pay.view(np.uint32).sum(axis=0, dtype=np.uint64).astype(np.uint32)   # [P, 256]
+        ops = np.where(np.arange(P) % 2 == 0, 0x06, 0x07).astype(np.uint8)
+        fwd_rows = []
+        for l in range(L):   # up: each leaf's two hosts, PSN-major
+            n = F * P
+            fr = np.zeros((n, STRIDE), np.uint8)
+            psn = np.repeat(np.arange(P, dtype=np.uint32) + psn0, F)
+            host = np.tile(np.arange(F), P) + F * l
+            for op in (0x06, 0x07):
+                sel = np.repeat(ops == op, F)
+                fr[sel, : len(base[op])] = base[op]
+                off = 70 if op == 0x06 else 54
+                fr[sel, off:off + 1024] = pay[host[sel], psn[sel] - psn0].astype(">i4").view(np.uint8).reshape(-1, 1024)
+            fr[:, 50:54] = (psn | 0x80000000).astype(">u4").view(np.uint8).reshape(n, 4)
+            ports = torch.from_numpy(np.tile(np.arange(F, dtype=np.int32), P)).to(gpu)
+            a, _, out, ln = leaves[l].batch(torch.from_numpy(fr).to(gpu), ports, t_leaf)
+            torch.cuda.synchronize()
+            fw = np.nonzero(a.cpu().numpy() == inccl.SW_FORWARD)[0]
+            assert len(fw) == P
+            fwd_rows.append(out[torch.from_numpy(fw * (F + 1) + F).to(gpu)])
+        # the root: the leaves' forwards interleaved PSN by PSN, port = leaf
+        rf = torch.stack(fwd_rows, dim=1).reshape(L * P, STRIDE)
+        rp = torch.from_numpy(np.tile(np.arange(L, dtype=np.int32), P)).to(gpu)
+        a, _, out, ln = root.batch(rf, rp, t_root)
+        torch.cuda.synchronize()
+        done = np.nonzero(a.cpu().numpy() == inccl.SW_COMPLETED)[0]
+        assert len(done) == P
+        for l in range(L):   # down: the root's frames for leaf l into its parent port
+            dn = out[torch.from_numpy(done * L + l).to(gpu)]
+            a2, _, out2, ln2 = leaves[l].batch(dn.contiguous(), torch.full((P,), F, dtype=torch.int32, device=gpu),
+                                               t_leaf)
+            torch.cuda.synchronize()
+            assert (a2.cpu().numpy() == inccl.SW_DOWN).all()
+            hosts = out2.view(P, F + 1, STRIDE)[:, :F].cpu().numpy()
+            lens = ln2.cpu().numpy().reshape(P, F + 1)
+            wf = ops == 0x06
+            assert (lens[:, :F] == np.where(wf, 1098, 1082)[:, None]).all() and (lens[:, F] == 0).all()
+            for d in (54, 70):
+                sel = np.where(wf, 70, 54) == d
+                got = hosts[sel, :, d:d + 1024].copy().view(">u4").astype(np.uint32)   # [p, child, 256]
+                assert np.array_equal(got, np.repeat(total[sel][:, None, :], F, axis=1)), (rnd, l, d)
+            rows = torch.from_numpy(hosts.reshape(P * F, STRIDE)).to(gpu)
+            crc = inccl.icrc_frames(rows).cpu().numpy().view(np.uint32)
+            ln_flat = lens[:, :F].reshape(-1)
+            stored = np.array([int.from_bytes(hosts.reshape(P * F, STRIDE)[i, ln_flat[i] - 4:ln_flat[i]].tobytes(),
+                                              "little") for i in range(P * F)], np.uint32)
+            assert np.array_equal(crc, stored)
+    for sw in leaves + [root]:
+        sw.destroy()

@@ -164,3 +164,41 @@ def test_nonroot_bad_ports_and_lengths(orc):
     assert sw.pipeline(t, 2, bytes(odd))[0] == orc.SW_IGNORED
     with pytest.raises(ValueError):
         orc.Switch(F, 16, nonroot=True, flags=4)
+
+
+@pytest.mark.parametrize("flags", [0, 1])
+def test_two_tier_tree_allreduce(orc, flags):
+    """Four hosts under two non-root switches under one root (the reference's
+    multi-switch topology, fan-in 2 at each tier): every host's packet goes up,
+    each non-root forwards its children's aggregate to the root, the root
+    broadcasts the total, each non-root takes it and sends it down.  With
+    SW_WIRE_ORDER every host receives the four-way wrap-around sum; in the
+    reference's byte order, every word byte-reversed."""
+    rng = np.random.default_rng(17 + flags)
+    P = 6
+    x = [[_pay(rng) for _ in range(P)] for _ in range(4)]
+    leaves = [orc.Switch(2, 16, nonroot=True, flags=flags) for _ in range(2)]
+    root = orc.Switch(2, 16)
+    tl, tr = _conns(3), _conns(2)
+    for p in range(P):
+        op = (0x07, 0x06, 0x08)[p % 3]
+        up = []
+        for s in range(2):
+            for c in range(2):
+                rc, outs = leaves[s].pipeline(tl, c, _in(orc, x[2 * s + c][p], p, op))
+                if rc == orc.SW_FORWARD:
+                    up.append((s, outs[2]))
+        assert [s for s, _ in up] == [0, 1]
+        for s, fr in up:
+            rc, down = root.pipeline(tr, s, fr)
+        assert rc == orc.SW_BROADCAST
+        total = _wrap_sum(*[x[h][p] for h in range(4)])
+        want = total if flags & orc.SW_WIRE_ORDER else _reversed_words(total)
+        off = 70 if op == 0x06 else 54
+        for s in range(2):
+            rc, outs = leaves[s].pipeline(tl, 2, down[s])
+            assert rc == orc.SW_DOWN
+            for c in range(2):
+                got = np.frombuffer(outs[c][off:off + 1024], ">i4").astype(np.int32)
+                assert np.array_equal(got, want), (p, s, c)
+                assert orc.icrc(outs[c]) == int.from_bytes(outs[c][-4:], "little")
