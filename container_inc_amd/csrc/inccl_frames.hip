@@ -928,6 +928,11 @@ __host__ __device__ constexpr uint32_t nr_region_cap(int64_t count)
     return (uint32_t)((((count + kClassifyBlock - 1) / kClassifyBlock) + kNrShards - 1) / kNrShards) * kClassifyBlock;
 }
 
+// A run of consecutive frames of one slot in a wave (a PSN's copies arriving
+// together, the common case) is pushed with ONE atomicExch by its last frame:
+// each frame links to the frame before it and the run's first frame to what
+// the exchange returned (an atomic per frame, two to one address for a fan-in-2
+// PSN: 12.6 us per 131 072-frame batch).
 __global__ __launch_bounds__(kClaimBlock) void k_nr_claim(InccSwitchState s, const uint8_t* __restrict__ frames,
                                                           int64_t stride, int64_t count,
                                                           const int32_t* __restrict__ ports,
@@ -935,30 +940,41 @@ __global__ __launch_bounds__(kClaimBlock) void k_nr_claim(InccSwitchState s, con
 {
     if (blockIdx.x == 0 && threadIdx.x < kNrShards) s.work[threadIdx.x] = 0u;   // classify (the next launch) appends
     const int64_t f = (int64_t)blockIdx.x * kClaimBlock + threadIdx.x;
-    if (f >= count) return;
-    const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + f * stride);
+    const bool in = f < count;
+    const int64_t fr = in ? f : 0;   // (every lane stays for the wave-wide steps below)
+    const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + fr * stride);
     const uint32_t w9 = opaque_u32(fw[9]), w10 = opaque_u32(fw[10]), w12 = opaque_u32(fw[12]);
     const uint32_t w13 = opaque_u32(fw[13]);
-    const int port = (int)opaque_u32((uint32_t)ports[f]);
+    const int port = (int)opaque_u32((uint32_t)ports[fr]);
     const uint8_t op = (uint8_t)(w10 >> 16);                                    // byte 42
     const uint32_t psn = ((w12 >> 24) << 16) | ((w13 & 0xFFu) << 8) | ((w13 >> 8) & 0xFFu);   // nts.c:311
     const int udp_len = (int)(((w9 >> 16) & 0xFFu) << 8 | (w9 >> 24));
+    const bool wf = is_write_first(op);
     int act = INCCL_SW_IGNORED;
     if (port < 0 || port > s.fan_in) act = INCCL_SW_INVALID;
     else if (op == 0x11) act = port < s.fan_in ? INCCL_SW_ACK : INCCL_SW_IGNORED;   // UP_ACK / DOWN_ACK (:424-426)
-    else if (is_data_opcode(op) || is_write_first(op)) {
-        const bool wf = is_write_first(op);
+    else if (is_data_opcode(op) || wf) {
         const int data_len = udp_len - 12 - 8 - 4 - (wf ? 16 : 0);   // nts.c:349, :410, :429, :486
-        if (data_len != kLanes * 4 || 54 + (wf ? 16 : 0) + kLanes * 4 > stride) act = INCCL_SW_INVALID;
-        else {
-            const uint32_t slot = psn & (s.slots - 1);
-            const uint32_t next = atomicExch(&s.head[slot], (uint32_t)f);
-            reinterpret_cast<u2*>(s.link)[f] = u2{next, (uint32_t)port | (wf ? 1u << 8 : 0u)};
-            act = kActPending;
-        }
+        act = (data_len != kLanes * 4 || 54 + (wf ? 16 : 0) + kLanes * 4 > stride) ? INCCL_SW_INVALID : kActPending;
     }
-    action[f] = act;
-    psn_out[f] = psn;
+    const bool linked = in && act == kActPending;
+    const uint32_t slot = psn & (s.slots - 1);
+    const int lane = threadIdx.x % kWave;
+    const uint32_t pslot = (uint32_t)__shfl_up((int)slot, 1, kWave), nslot = (uint32_t)__shfl_down((int)slot, 1, kWave);
+    const uint64_t lk = __ballot(linked);
+    const bool same_prev = linked && lane > 0 && ((lk >> (lane - 1)) & 1u) && pslot == slot;
+    const bool same_next = linked && lane < kWave - 1 && ((lk >> (lane + 1)) & 1u) && nslot == slot;
+    const uint64_t ends = __ballot(linked && !same_next) >> lane;
+    const int end_lane = ends ? lane + __builtin_ctzll(ends) : lane;   // this frame's run's last frame
+    uint32_t old = kNone;
+    if (linked && !same_next) old = atomicExch(&s.head[slot], (uint32_t)f);
+    const uint32_t run_next = (uint32_t)__shfl((int)old, end_lane, kWave);
+    if (linked)
+        reinterpret_cast<u2*>(s.link)[f] = u2{same_prev ? (uint32_t)f - 1u : run_next, (uint32_t)port | (wf ? 1u << 8 : 0u)};
+    if (in) {
+        action[f] = act;
+        psn_out[f] = psn;
+    }
 }
 
 __global__ __launch_bounds__(kClassifyBlock) void k_nr_classify(InccSwitchState s, const uint8_t* __restrict__ frames,
