@@ -376,7 +376,7 @@ struct inccl_switch *inccl_switch_create(int fan_in, uint32_t slots, int device)
  *            is DROPPED (nts.c:412, :420-422); an ACK from the parent is IGNORED (:424-426)
  *   REPLAY   the retransmitting child: the parent's result (nts.c:378-380)
  * Each slot's frames of a batch are decided in arrival order, one slot per lane, so a batch
- * costs more the more copies one PSN has in it (a slot's first 16 in registers). */
+ * costs more the more copies one PSN has in it (up to 8 per slot are kept in LDS, more are walked). */
 struct inccl_switch *inccl_switch_create_nonroot(int fan_in, uint32_t slots, int device, int flags);
 /* device pointer of a non-root's result slot for `psn`: what the reference's aggregator holds once
  * the parent's result is taken (its wire words, or host words with INCCL_SW_WIRE_ORDER); the
