@@ -136,12 +136,29 @@ def quant_kat() -> None:
               open(os.path.join(HERE, "quant_kat.json"), "w"))
 
 
+def nonroot_down_survey() -> None:
+    """The one recorded output of the reference's non-root branches (SURVEY.md
+    section 0, line 28, from driving its pipeline() as a non-root): a child
+    decoded 234881024 where the parent sent 14 -- 0x0000000E with its bytes
+    reversed (nts.c:413 keeps the wire bytes, util.c:403-405 htonls them again)."""
+    parent = 14
+    child = int.from_bytes(parent.to_bytes(4, "big"), "little")
+    assert child == 234881024
+    json.dump({"source": "SURVEY.md section 0 (line 28): the reference's own pipeline() driven as a non-root "
+                         "switch (nts.c:408-419) -- a child received 234881024 for a parent value of 14",
+               "parent_value": parent, "child_value": child,
+               "note": "the child's value is what a host decodes with ntohl (api.c:428-430) from the word the "
+                       "non-root sent down"},
+              open(os.path.join(HERE, "nonroot_down_survey.json"), "w"), indent=1)
+
+
 def main() -> None:
     ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     host_known_answer(ref)
     icrc_test_c(ref)
     sum_edge()
     quant_kat()
+    nonroot_down_survey()
     print("fixtures written to", HERE)
 
 

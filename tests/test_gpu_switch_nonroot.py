@@ -4,9 +4,10 @@ serial pipeline() (gpu): every frame's action and every row it sends, byte for
 byte, in both driving modes (split ingress + egress, and one batch call), with
 the reference's byte order and no-recycle (flags 0) and with each option.
 
-Parity of the non-root role is pinned by the oracle restatement only (the
-reference needs libpcap to build and holds no non-root fixture): see
-tests/test_oracle_nonroot.py for the hand-worked sequences that check it."""
+Parity of the non-root role rests on the oracle restatement (the reference
+needs libpcap to build): tests/test_oracle_nonroot.py checks it on hand-worked
+sequences and against the one reference-produced output SURVEY §0 recorded
+(tests/golden/nonroot_down_survey.json), which the GPU reproduces too."""
 import numpy as np
 import pytest
 
@@ -307,4 +308,31 @@ def test_two_tier_tree_on_gpu(gpu, orc, flags):
                                               "little") for i in range(P * F)], np.uint32)
             assert np.array_equal(crc, stored)
     for sw in leaves + [root]:
+        sw.destroy()
+
+
+def test_nonroot_down_matches_surveyed_reference_output(gpu, orc):
+    """SURVEY §0's reference-produced output for a non-root (a child decodes
+    234881024 where the parent sent 14, tests/golden/nonroot_down_survey.json)
+    on the GPU switch with the reference's byte order (flags 0), and the
+    parent's 14 with SW_WIRE_ORDER."""
+    import json
+    import os
+
+    import torch
+    from conftest import GOLDEN
+    from container_inc_amd import inccl
+    g = json.load(open(os.path.join(GOLDEN, "nonroot_down_survey.json")))
+    for flags, want in ((0, g["child_value"]), (inccl.SW_WIRE_ORDER, g["parent_value"])):
+        sw = inccl.GpuSwitch(2, 16, nonroot=True, flags=flags)
+        tmpl = torch.from_numpy(_templates(3).view(np.uint8).copy()).to(gpu)
+        frames = [orc.build_data_frame(np.arange(256, dtype=np.int32), psn=3, opcode=0x07) for _ in range(2)]
+        frames.append(orc.build_data_frame(np.full(256, g["parent_value"], np.int32), psn=3, opcode=0x07))
+        a, _, out, ln = sw.batch(_rows(frames, gpu), torch.tensor([0, 1, 2], dtype=torch.int32, device=gpu), tmpl)
+        torch.cuda.synchronize()
+        assert a.cpu().tolist() == [inccl.SW_ABSORBED, inccl.SW_FORWARD, inccl.SW_DOWN]
+        o = out.cpu().numpy()
+        for c in range(2):
+            got = o[2 * 3 + c, 54:54 + 1024].copy().view(">i4")
+            assert (got == want).all(), (flags, c)
         sw.destroy()

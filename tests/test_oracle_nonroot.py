@@ -4,10 +4,10 @@ reference's branches send -- send_roce_data / _with_reth with the aggregator
 re-encoded by htonl (util.c:403-405) -- with the sums and byte orders computed
 in this file, not by the restatement under test.
 
-Parity of the non-root role is unpinned by reference output: the reference
-needs libpcap to build, and it holds no non-root fixture.  SURVEY §0 drove the
-reference's pipeline() as a non-root and recorded what these tests encode: the
-parent's result goes down with every word's bytes reversed."""
+The reference needs libpcap to build, so its non-root branches cannot be run
+here.  SURVEY §0 drove them once and recorded one output -- a child decodes
+234881024 where the parent sent 14, every word's bytes reversed -- kept as
+tests/golden/nonroot_down_survey.json and checked below."""
 import numpy as np
 import pytest
 
@@ -202,3 +202,26 @@ def test_two_tier_tree_allreduce(orc, flags):
                 got = np.frombuffer(outs[c][off:off + 1024], ">i4").astype(np.int32)
                 assert np.array_equal(got, want), (p, s, c)
                 assert orc.icrc(outs[c]) == int.from_bytes(outs[c][-4:], "little")
+
+
+def test_nonroot_down_matches_surveyed_reference_output(orc):
+    """The one reference-produced output for the non-root role: SURVEY §0
+    drove the reference's pipeline() as a non-root and recorded that a child
+    decodes 234881024 where the parent sent 14 (tests/golden/
+    nonroot_down_survey.json).  The restatement (flags 0) gives exactly that in
+    every lane; SW_WIRE_ORDER gives the parent's 14 back."""
+    import json
+    import os
+
+    from conftest import GOLDEN
+    g = json.load(open(os.path.join(GOLDEN, "nonroot_down_survey.json")))
+    for flags, want in ((0, g["child_value"]), (orc.SW_WIRE_ORDER, g["parent_value"])):
+        t = _conns(3)
+        sw = orc.Switch(2, 16, nonroot=True, flags=flags)
+        for c in range(2):
+            sw.pipeline(t, c, _in(orc, np.arange(256, dtype=np.int32), 3, 0x07))
+        rc, outs = sw.pipeline(t, 2, _in(orc, np.full(256, g["parent_value"], np.int32), 3, 0x07))
+        assert rc == orc.SW_DOWN
+        for c in range(2):
+            got = np.frombuffer(outs[c][54:54 + 1024], ">i4")   # what the host's ntohl decodes
+            assert (got == want).all(), (flags, c)
