@@ -737,11 +737,11 @@ def rs_oracle_check(srcs, out_shard, lanes, k: int, rank: int, world: int) -> di
 
 
 def reduce_scatter_engines(comm, dev, R: int, rank: int, world: int, mib: float = 256,
-                           engines=("rccl", "p2p", "mesh")) -> list:
+                           engines=("rccl", "p2p")) -> list:
     """N > 1: inccl_reduce_scatter_f32 of R resident `mib` MiB fp32 buckets per
     rank (each rank keeps its 1/W shard of the reduced bucket: the sharded-
-    gradient callers' half of the allreduce) on rccl (ncclReduceScatter), p2p
-    (pull-reduce into the shard) and mesh (the persistent kernel), each verified bit-identical to the first engine
+    gradient callers' half of the allreduce) on rccl (ncclReduceScatter) and p2p
+    (pull-reduce into the shard), each verified bit-identical to the first engine
     that passes, over two alternating input sets, and against the oracle on
     every rank's shard; wall time per call (max over ranks) and the xGMI link
     fraction of its (W-1)/W * n * 4 bytes."""
@@ -1832,10 +1832,12 @@ def main():
         with Phase("reduce_scatter"):
             if agree([time.monotonic() - T_START], world)[0] <= sweep_soft:
                 try:
+                    # (the mesh engines reduce-scatter through the p2p pull-reduce unless
+                    # INCCL_MESH_RS opts into their own route, so they have no row of their own)
                     res["reduce_scatter"] = reduce_scatter_engines(comm, dev, R, rank, world)
                     for small in (1 / 16, 1.0):   # 64 KiB and 1 MiB buckets: the ll engine's one kernel too
                         res["reduce_scatter"] += reduce_scatter_engines(comm, dev, R, rank, world, small,
-                                                                        ("rccl", "p2p", "ll", "mesh"))
+                                                                        ("rccl", "p2p", "ll"))
                 except Exception as e:  # noqa: BLE001
                     print(f"rank {rank}: reduce_scatter key failed: {e!r}", file=sys.stderr, flush=True)
                     res["reduce_scatter"] = {"error": repr(e)}

@@ -508,6 +508,8 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     const char *llb = getenv("INCCL_LL_MAX_BYTES");   /* small-bucket one-kernel path; 0 disables */
     c->ll_max_bytes = llb ? (size_t)strtoull(llb, NULL, 0) : ((size_t)1 << 20);
     if (c->ll_max_bytes > ((size_t)1 << 30)) c->ll_max_bytes = (size_t)1 << 30;   /* 32-bit buffer offsets */
+    const char *mrs = getenv("INCCL_MESH_RS");        /* the mesh engines' own reduce-scatter route (opt-in) */
+    c->mesh_rs = mrs && atoi(mrs) != 0;
     const char *arb = getenv("INCCL_RCCL_AR_BYTES");  /* rccl engine: one all-reduce up to this; 0 disables */
     c->rccl_ar_bytes = arb ? (size_t)strtoull(arb, NULL, 0) : ((size_t)1 << 20);
     const char *eng = getenv("INCCL_ENGINE");
@@ -1158,9 +1160,13 @@ static int reduce_scatter_body(struct inccl_communicator *c, int kind, const voi
     }
     const int ipc = c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH;
     const uintptr_t dst_align = kind == INCCL_KIND_F32 ? 15u : 7u;
-    /* the mesh engines: their one persistent kernel, each reduce writing its
-     * chunk of this rank's shard into dst (shards of whole 64-element groups) */
-    if (c->engine == INCCL_ENGINE_MESH && c->group->transport == INCCL_TRANSPORT_RCCL && !(shard % 64) &&
+    /* the mesh engines' own route, opt-in (INCCL_MESH_RS=1): their one
+     * persistent kernel, each reduce writing its chunk of this rank's shard
+     * into dst (shards of whole 64-element groups).  Off by default: with four
+     * and eight processes on one GPU it returned wrong shards and faulted
+     * ("Mesh reduce-scatter route"); the mesh engines take the p2p
+     * pull-reduce below instead */
+    if (c->mesh_rs && c->engine == INCCL_ENGINE_MESH && c->group->transport == INCCL_TRANSPORT_RCCL && !(shard % 64) &&
         ((uintptr_t)dst & dst_align) == 0)
         return inccl_mesh_reduce_scatter(c, kind, srcs, R, dst, n, k, amax, scale_R, st);
     /* the ll engine's one kernel for a small fp32 bucket: every rank's quads

@@ -99,6 +99,7 @@ struct inccl_communicator {
     uint64_t ll_timeout_ticks;
     hipStream_t ll_last_stream;  /* ordering across caller streams (ev[7]) */
     size_t ll_max_bytes;         /* buckets up to this size take the ll kernel */
+    int mesh_rs;                 /* INCCL_MESH_RS: reduce-scatter through the mesh kernel (opt-in) */
     size_t rccl_ar_bytes;        /* rccl engine: int32 partials up to this size take one
                                     ncclAllReduce instead of reduce-scatter + all-gather */
     /* mesh engine (large buckets, one persistent kernel per call): one IPC buffer

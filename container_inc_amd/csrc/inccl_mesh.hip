@@ -281,7 +281,12 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
                     for (int j = 0; j < kMaxR; ++j)
                         if (j < a.W) __builtin_amdgcn_raw_buffer_store_b64(o, outs[j], (int)(q * 8), 0, kAuxSys);
                 } else {
-                    __builtin_amdgcn_raw_buffer_store_b64(o, res, (int)(q * 8), 0, kAuxSys);
+                    // (reduce-scatter: dst is the caller's, read by ordinary loads -- sc1
+                    // write-through as the gathers' dst stores, not system scope)
+                    if (a.rs)
+                        __builtin_amdgcn_raw_buffer_store_b64(o, res, (int)(q * 8), 0, 16);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b64(o, res, (int)(q * 8), 0, kAuxSys);
                 }
             } else {
                 u32x4 o;
@@ -293,6 +298,8 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
 #pragma unroll
                     for (int j = 0; j < kMaxR; ++j)
                         if (j < a.W) st_sys16(outs[j], (uint32_t)(q * 16), o);
+                } else if (a.rs) {
+                    __builtin_amdgcn_raw_buffer_store_b128(o, res, (int)(q * 16), 0, 16);   // sc1, as above
                 } else {
                     st_sys16(res, (uint32_t)(q * 16), o);
                 }
