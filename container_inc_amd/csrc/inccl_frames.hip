@@ -1467,12 +1467,16 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
         pr.w = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)p3);
     }
     const bool tail = lane == hchunks - 1;   // the frame's last chunk, in the second store
-    const uint32_t emit_mask = all ? (1u << fan) - 1u : (one ? 1u << port : 0u);   // children that get a frame
-    uint8_t* row = A.out + (size_t)e.f * dests * A.out_stride;
-    constexpr int kUnroll = kFan ? kFan + (kNR ? 1 : 0) : 1;
+    // fan row slots per frame: "all" fills them with rows 0 .. fan-1, "one" puts
+    // its single row (port; a non-root's parent row fan_in included) in the
+    // first and drops the rest.  So a non-root issues fan rows' stores, not
+    // fan + 1, and the count stays fixed (k_egress's waits are counts)
+    uint8_t* const row0 = A.out + (size_t)e.f * dests * A.out_stride;
+    constexpr int kUnroll = kFan ? kFan : 1;
 #pragma unroll kUnroll
-    for (int c = 0; c < dests; ++c) {
-        const bool em = (emit_mask >> c) & 1u;
+    for (int i = 0; i < fan; ++i) {
+        const int c = one ? (int)port : i;
+        const bool em = all || (one && i == 0);
         u4 h = unset4(), v = unset4();
         if (em) {
             h = reinterpret_cast<const u4*>(t.img[2 * c + wf])[lane < 5 ? lane : 0];
@@ -1519,8 +1523,7 @@ __device__ __forceinline__ void egress_emit(const EgressLds& t, const EgressArgs
             }
         }
         const __amdgpu_buffer_rsrc_t orow =
-            __builtin_amdgcn_make_buffer_rsrc(row, 0, em ? (int)A.out_stride : 0, 0x00020000);
-        row += A.out_stride;
+            __builtin_amdgcn_make_buffer_rsrc(row0 + (size_t)c * A.out_stride, 0, em ? (int)A.out_stride : 0, 0x00020000);
         if (kOut16) {
             __builtin_amdgcn_raw_buffer_store_b128(h, orow, 16 * lane, 0, kAuxNt);
             __builtin_amdgcn_raw_buffer_store_b128(v, orow, lane < hchunks ? 16 * (kWave + lane) : kOobOffset, 0,
@@ -1698,7 +1701,7 @@ __global__ __launch_bounds__(kWave* kEgressWaves) __attribute__((amdgpu_waves_pe
             // entered with its back edge's memory history, so its waits are counts
             const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(A.out_len, 0, 0, 0x00020000);
 #pragma unroll
-            for (int k = 0; k < kEgressAhead * (kFan + (kNR ? 1 : 0)) * (kOut16 ? 2 : 8); ++k)
+            for (int k = 0; k < kEgressAhead * kFan * (kOut16 ? 2 : 8); ++k)
                 __builtin_amdgcn_raw_buffer_store_b32(0u, none, 16 * k, 0, 0);
         }
         for (;;) {
