@@ -996,7 +996,8 @@ __global__ __launch_bounds__(kClassifyBlock) void k_nr_classify(InccSwitchState 
     s.head[slot] = kNone;   // empty for the next batch
     // the slot's work record for the sum: {psn | partial << 31, parent frame,
     // counted frame per child}, in this block's region (the compiler makes the
-    // wave's owners one atomic)
+    // wave's owners one atomic).  Every word is stored inverted, so that the
+    // sum's range-checked loads (0 past a record) read kNone
     const int fan = s.fan_in;
     const uint32_t k = blockIdx.x % kNrShards;
     const uint32_t idx = atomicAdd(&s.work[k], 1u);
@@ -1024,7 +1025,7 @@ __global__ __launch_bounds__(kClassifyBlock) void k_nr_classify(InccSwitchState 
     const uint32_t cmask = 0xFFFFFFFFu >> (32 - fan), rbit = 1u << fan;   // nts.c:29, :366
     const bool partial = (B & cmask) != 0u;
     uint32_t* cnt = rec + 2;
-    for (int q = 0; q < fan; ++q) cnt[q] = kNone;
+    for (int q = 0; q < fan; ++q) cnt[q] = ~kNone;
     int64_t prev = -1;
     for (int i = 0; i < n; ++i) {
         uint32_t g = kNone, info = 0u;
@@ -1054,7 +1055,7 @@ __global__ __launch_bounds__(kClassifyBlock) void k_nr_classify(InccSwitchState 
                                                                                          : INCCL_SW_DROPPED);
             else {   // first transmission (:387-398, :468-480)
                 B |= pb;
-                cnt[port] = g | (wf << 31);
+                cnt[port] = ~(g | (wf << 31));
                 if (wf) {   // the RETH into the keeper (:470): frame bytes 54-69
                     const uint32_t* fw = reinterpret_cast<const uint32_t*>(frames + (int64_t)g * stride);
                     uint32_t rw[5];
@@ -1083,8 +1084,8 @@ __global__ __launch_bounds__(kClassifyBlock) void k_nr_classify(InccSwitchState 
     }
     s.bits[slot] = B;
     s.degree[slot] = (int32_t)D;
-    rec[0] = (psn & 0x00FFFFFFu) | (partial ? 1u << 31 : 0u);
-    rec[1] = downf;
+    rec[0] = ~((psn & 0x00FFFFFFu) | (partial ? 1u << 31 : 0u));
+    rec[1] = ~downf;
 }
 
 constexpr int kNrSumWaves = 4;
@@ -1113,11 +1114,24 @@ __device__ __forceinline__ void chunks_payload(const u4& xx, const u2& ee, uint3
     }
 }
 
-// A wave per work record (lane j: word j), the next record in flight while
-// one is summed: its rows' payload chunks kNrSumRows at a time (the children's
-// counted copies, then the parent's result) with the slot's partial.
+// A wave per two work records at a time (lane j: word j of each), the next two
+// in flight while they are summed: each record's rows' payload chunks
+// kNrSumRows at a time (the children's counted copies, then the parent's
+// result) with the slot's partial, the second record's rows loading while the
+// first's are added.  A wave waits on one payload round trip per pair, not per
+// record.
+//
+// The waits are counts (vmcnt), so every memory instruction of the common
+// path is issued unconditionally: range-checked buffer accesses at an
+// out-of-range offset where there is nothing to load or store (a conditional
+// one makes the compiler wait for everything, vmcnt(0)).  The loop is entered
+// with as many (dropped) stores after the first records' loads as a pass
+// issues after its prefetch, its four stores.
+constexpr int kNrSumTail = 4;
+
+template <bool kWide>
 __global__ __launch_bounds__(kWave* kNrSumWaves) void k_nr_sum(InccSwitchState s, const uint8_t* __restrict__ frames,
-                                                              int64_t stride, int64_t count, int wide)
+                                                              int64_t stride, int64_t count)
 {
     const int lane = threadIdx.x % kWave, fan = s.fan_in;
     const int next4 = ((lane + 1) & (kWave - 1)) * 4;
@@ -1127,76 +1141,121 @@ __global__ __launch_bounds__(kWave* kNrSumWaves) void k_nr_sum(InccSwitchState s
     const uint32_t n = s.work[k];
     const bool wire = (s.flags & INCCL_SW_WIRE_ORDER) != 0;
     const int rw = fan + 2;   // record words
-    const uint32_t* recs = s.work + kNrShards + (size_t)k * nr_region_cap(count) * rw;
-    uint32_t i = wid / kNrShards;
-    uint32_t r = i < n && lane < rw ? recs[(size_t)i * rw + lane] : kNone;
-    for (; i < n; i += nw) {
-        const uint32_t cq = r;
-        r = i + nw < n && lane < rw ? recs[(size_t)(i + nw) * rw + lane] : kNone;
-        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cq, 0), slot = w & (s.slots - 1);
-        const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)cq, 1);
-        u4 acc = {0u, 0u, 0u, 0u};
-        if (w >> 31) acc = reinterpret_cast<const u4*>(s.agg + (size_t)slot * kLanes)[lane];
-        uint64_t m = __ballot(lane >= 2 && lane < rw && (cq & 0x7FFFFFFFu) < nfr);   // (~0: none)
-        const bool any = m != 0;
-        bool down = (d & 0x7FFFFFFFu) < nfr;
-        while (m || down) {
-            uint32_t row[kNrSumRows];
-            int kind[kNrSumRows];   // 0 none, 1 a child's counted copy, 2 the parent's result
+    const __amdgpu_buffer_rsrc_t rrec =
+        uniform_rsrc(s.work + kNrShards + (size_t)k * nr_region_cap(count) * rw, (int64_t)n * rw * 4);
+    // record i's word `lane`, inverted as classify stored it (past the region's
+    // n records or the record's rw words: 0, i.e. kNone once inverted back)
+    auto rec = [&](uint32_t i) {
+        return __builtin_amdgcn_raw_buffer_load_b32(rrec, lane < rw ? (int)((i * (uint32_t)rw + (uint32_t)lane) * 4u)
+                                                                    : kOobOffset,
+                                                    0, 0);
+    };
+    struct Rec {
+        uint32_t cq, d;
+        uint64_t m;   // counted rows left (record lanes)
+        bool down;    // the parent's row left
+        bool any, has_down;
+        __amdgpu_buffer_rsrc_t ragg, rres;
+        u4 acc, vres;
+    };
+    struct Rows {
+        uint32_t row[kNrSumRows];
+        int kind[kNrSumRows];   // 0 none, 1 a child's counted copy, 2 the parent's result
+        u4 x[kNrSumRows];
+        u2 e[kNrSumRows];
+    };
+    // a record (a past-the-end one is all kNone: no rows, both stores dropped)
+    auto open = [&](uint32_t rn) {
+        Rec R;
+        R.cq = ~rn;
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)R.cq, 0), slot = w & (s.slots - 1);
+        R.d = (uint32_t)__builtin_amdgcn_readlane((int)R.cq, 1);
+        R.ragg = uniform_rsrc(s.agg + (size_t)slot * kLanes, kLanes * 4);
+        R.rres = uniform_rsrc(s.res + (size_t)slot * kLanes, kLanes * 4);
+        R.acc = __builtin_amdgcn_raw_buffer_load_b128(R.ragg, (w >> 31) ? 16 * lane : kOobOffset, 0, 0);   // partial or 0
+        R.vres = u4{0u, 0u, 0u, 0u};
+        R.m = __ballot(lane >= 2 && lane < rw && (R.cq & 0x7FFFFFFFu) < nfr);
+        R.any = R.m != 0;
+        R.has_down = (R.d & 0x7FFFFFFFu) < nfr;
+        R.down = R.has_down;
+        return R;
+    };
+    // the record's next kNrSumRows rows, their loads issued (16-byte rows)
+    auto take = [&](Rec& R) {
+        Rows L;
 #pragma unroll
-            for (int r = 0; r < kNrSumRows; ++r) {
-                if (m) {
-                    row[r] = (uint32_t)__builtin_amdgcn_readlane((int)cq, __builtin_ctzll(m));
-                    m &= m - 1;
-                    kind[r] = 1;
-                } else if (down) {
-                    row[r] = d;
-                    down = false;
-                    kind[r] = 2;
-                } else {
-                    row[r] = 0u;
-                    kind[r] = 0;
-                }
-            }
-            uint32_t P[kNrSumRows][4];
-            if (wide) {
-                u4 x[kNrSumRows];
-                u2 e[kNrSumRows];
-#pragma unroll
-                for (int r = 0; r < kNrSumRows; ++r) {
-                    const __amdgpu_buffer_rsrc_t rs =
-                        uniform_rsrc(frames + (int64_t)(row[r] & 0x7FFFFFFFu) * stride, kind[r] ? stride : 0);
-                    x[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, 48 + 16 * lane, 0, 0);
-                    e[r] = tail_chunks(rs, 0, lane);
-                }
-#pragma unroll
-                for (int r = 0; r < kNrSumRows; ++r) chunks_payload(x[r], e[r], row[r] >> 31, lane, next4, P[r]);
+        for (int r = 0; r < kNrSumRows; ++r) {
+            if (R.m) {
+                L.row[r] = (uint32_t)__builtin_amdgcn_readlane((int)R.cq, __builtin_ctzll(R.m));
+                R.m &= R.m - 1;
+                L.kind[r] = 1;
+            } else if (R.down) {
+                L.row[r] = R.d;
+                R.down = false;
+                L.kind[r] = 2;
             } else {
-#pragma unroll
-                for (int r = 0; r < kNrSumRows; ++r)
-                    if (kind[r]) payload16(frames + (int64_t)(row[r] & 0x7FFFFFFFu) * stride, row[r] >> 31, lane, false, P[r]);
+                L.row[r] = 0u;
+                L.kind[r] = 0;
             }
-#pragma unroll
-            for (int r = 0; r < kNrSumRows; ++r) {
-                if (kind[r] == 1) {
-                    acc.x += P[r][0];
-                    acc.y += P[r][1];
-                    acc.z += P[r][2];
-                    acc.w += P[r][3];
-                } else if (kind[r] == 2) {
-                    // the reference keeps the wire bytes (memcpy, :413): the host words back to wire order
-                    const u4 v = wire ? u4{P[r][0], P[r][1], P[r][2], P[r][3]}
-                                      : u4{__builtin_bswap32(P[r][0]), __builtin_bswap32(P[r][1]),
-                                           __builtin_bswap32(P[r][2]), __builtin_bswap32(P[r][3])};
-                    __builtin_amdgcn_raw_buffer_store_b128(v, uniform_rsrc(s.res + (size_t)slot * kLanes, kLanes * 4),
-                                                           16 * lane, 0, kAuxSc1);
-                }
+            if (kWide) {
+                const __amdgpu_buffer_rsrc_t rs =
+                    uniform_rsrc(frames + (int64_t)(L.row[r] & 0x7FFFFFFFu) * stride, L.kind[r] ? stride : 0);
+                L.x[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, 48 + 16 * lane, 0, 0);
+                L.e[r] = tail_chunks(rs, 0, lane);
             }
         }
-        // write-through, as the root's sum: egress reads the aggregate next
-        if (any)
-            __builtin_amdgcn_raw_buffer_store_b128(acc, uniform_rsrc(s.agg + (size_t)slot * kLanes, kLanes * 4),
-                                                   16 * lane, 0, kAuxSc1);
+        return L;
+    };
+    auto add = [&](Rec& R, const Rows& L) {
+        uint32_t P[kNrSumRows][4];
+#pragma unroll
+        for (int r = 0; r < kNrSumRows; ++r) {
+            if (kWide)
+                chunks_payload(L.x[r], L.e[r], L.row[r] >> 31, lane, next4, P[r]);
+            else if (L.kind[r])
+                payload16(frames + (int64_t)(L.row[r] & 0x7FFFFFFFu) * stride, L.row[r] >> 31, lane, false, P[r]);
+            else
+                P[r][0] = P[r][1] = P[r][2] = P[r][3] = 0u;
+            if (L.kind[r] == 1) {
+                R.acc.x += P[r][0];
+                R.acc.y += P[r][1];
+                R.acc.z += P[r][2];
+                R.acc.w += P[r][3];
+            } else if (L.kind[r] == 2) {
+                // the reference keeps the wire bytes (memcpy, :413): the host words back to wire order
+                R.vres = wire ? u4{P[r][0], P[r][1], P[r][2], P[r][3]}
+                              : u4{__builtin_bswap32(P[r][0]), __builtin_bswap32(P[r][1]),
+                                   __builtin_bswap32(P[r][2]), __builtin_bswap32(P[r][3])};
+            }
+        }
+    };
+    // the rest of its rows (fan_in > kNrSumRows, resends), then the aggregate and
+    // the parent's result, write-through as the root's sum: egress reads them next
+    auto close = [&](Rec& R) {
+        while (R.m || R.down) {
+            const Rows L = take(R);
+            add(R, L);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(R.acc, R.ragg, R.any ? 16 * lane : kOobOffset, 0, kAuxSc1);
+        __builtin_amdgcn_raw_buffer_store_b128(R.vres, R.rres, R.has_down ? 16 * lane : kOobOffset, 0, kAuxSc1);
+    };
+    uint32_t i = wid / kNrShards;
+    uint32_t rn0 = rec(i), rn1 = rec(i + nw);
+    {
+        const __amdgpu_buffer_rsrc_t none = uniform_rsrc(s.agg, 0);
+#pragma unroll
+        for (int j = 0; j < kNrSumTail; ++j)   // (1 KiB apart: separate instructions, not one merged store)
+            __builtin_amdgcn_raw_buffer_store_b32(0u, none, 1024 * j, 0, 0);
+    }
+    for (; i < n; i += 2 * nw) {
+        Rec A = open(rn0), B = open(rn1);
+        rn0 = rec(i + 2 * nw);
+        rn1 = rec(i + 3 * nw);
+        const Rows LA = take(A), LB = take(B);
+        add(A, LA);
+        close(A);
+        add(B, LB);
+        close(B);
     }
 }
 
@@ -1930,13 +1989,17 @@ int launch_nr_ingress(const InccSwitchState* s, const uint8_t* frames, size_t st
                        frames, (int64_t)stride, n, ports, action, psn_out);
     hipLaunchKernelGGL(k_nr_classify, dim3((unsigned)((n + kClassifyBlock - 1) / kClassifyBlock)), dim3(kClassifyBlock),
                        0, st, *s, frames, (int64_t)stride, n, action, (const uint32_t*)psn_out);
-    const int wide = ((uintptr_t)frames & 15) == 0 && (stride & 15) == 0;
+    const bool wide = ((uintptr_t)frames & 15) == 0 && (stride & 15) == 0;
     // whole groups of kNrShards waves (every region gets the same number of waves)
     constexpr int64_t group = kNrShards / kNrSumWaves;
     const int64_t need = (n + kNrSumWaves - 1) / kNrSumWaves, cap = (int64_t)num_cus() * 8;
     const int64_t blocks = ((need < cap ? need : cap) + group - 1) / group * group;
-    hipLaunchKernelGGL(k_nr_sum, dim3((unsigned)blocks), dim3(kWave * kNrSumWaves), 0, st, *s, frames, (int64_t)stride,
-                       n, wide);
+    if (wide)
+        hipLaunchKernelGGL(k_nr_sum<true>, dim3((unsigned)blocks), dim3(kWave * kNrSumWaves), 0, st, *s, frames,
+                           (int64_t)stride, n);
+    else
+        hipLaunchKernelGGL(k_nr_sum<false>, dim3((unsigned)blocks), dim3(kWave * kNrSumWaves), 0, st, *s, frames,
+                           (int64_t)stride, n);
     return (int)hipGetLastError();
 }
 
