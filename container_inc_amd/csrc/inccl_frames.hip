@@ -1172,10 +1172,12 @@ __global__ __launch_bounds__(kWave* kNrSumWaves) void k_nr_sum(InccSwitchState s
         R.d = (uint32_t)__builtin_amdgcn_readlane((int)R.cq, 1);
         R.ragg = uniform_rsrc(s.agg + (size_t)slot * kLanes, kLanes * 4);
         R.rres = uniform_rsrc(s.res + (size_t)slot * kLanes, kLanes * 4);
-        R.acc = __builtin_amdgcn_raw_buffer_load_b128(R.ragg, (w >> 31) ? 16 * lane : kOobOffset, 0, 0);   // partial or 0
-        R.vres = u4{0u, 0u, 0u, 0u};
         R.m = __ballot(lane >= 2 && lane < rw && (R.cq & 0x7FFFFFFFu) < nfr);
         R.any = R.m != 0;
+        // the partial, or 0 -- and not read at all without a counted row (a
+        // down batch's records: the aggregate is neither summed nor stored)
+        R.acc = __builtin_amdgcn_raw_buffer_load_b128(R.ragg, ((w >> 31) && R.any) ? 16 * lane : kOobOffset, 0, 0);
+        R.vres = u4{0u, 0u, 0u, 0u};
         R.has_down = (R.d & 0x7FFFFFFFu) < nfr;
         R.down = R.has_down;
         return R;
