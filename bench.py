@@ -1832,9 +1832,9 @@ def main():
         with Phase("reduce_scatter"):
             if agree([time.monotonic() - T_START], world)[0] <= sweep_soft:
                 try:
-                    # (the mesh engines reduce-scatter through the p2p pull-reduce unless
-                    # INCCL_MESH_RS opts into their own route, so they have no row of their own)
-                    res["reduce_scatter"] = reduce_scatter_engines(comm, dev, R, rank, world)
+                    # the mesh engine's row is its persistent kernel's own route (default on)
+                    res["reduce_scatter"] = reduce_scatter_engines(comm, dev, R, rank, world,
+                                                                   engines=("rccl", "p2p", "mesh"))
                     for small in (1 / 16, 1.0):   # 64 KiB and 1 MiB buckets: the ll engine's one kernel too
                         res["reduce_scatter"] += reduce_scatter_engines(comm, dev, R, rank, world, small,
                                                                         ("rccl", "p2p", "ll"))

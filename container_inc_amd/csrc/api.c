@@ -127,10 +127,14 @@ int inccl_ws_claim(struct inccl_communicator *c, hipStream_t st)
 
 static int ws_leave(struct inccl_communicator *c, int rc)
 {
-    if (rc == 0 && c->ws_claimed && !c->ws_capturing) {
+    /* recorded on failure too: work the failed call already queued on its
+     * stream (absmax into d_words, quantise into d_q32, ...) may still run, and
+     * the next call on another stream must not write those workspaces under it.
+     * A failure keeps its own rc. */
+    if (c->ws_claimed && !c->ws_capturing) {
         const hipError_t e = hipEventRecord(c->ev[9], c->ws_stream);
         if (e == hipSuccess) c->ws_last_stream = c->ws_stream;
-        else rc = inccl_hip_check(e, "hipEventRecord(workspace order)");
+        else if (rc == 0) rc = inccl_hip_check(e, "hipEventRecord(workspace order)");
     }
     c->ws_claimed = 0;
     return rc;
@@ -470,6 +474,55 @@ const char *inccl_group_transport(const struct inccl_group *g)
 /* ------------------------------------------------------------------ */
 /* communicators                                                        */
 /* ------------------------------------------------------------------ */
+
+/* The knobs that pick a call's route or schedule come from each process's
+ * environment.  Ranks that read different values would take different routes
+ * for the same call (one rank the mesh kernel, another the p2p pull-reduce; one
+ * ncclAllReduce, another ncclReduceScatter + ncclAllGather): mismatched
+ * barriers or collectives, a hang or wrong shards.  So the group agrees on them
+ * once, here, as inccl_group_create_ex does for the IPC bound: thresholds and
+ * switches take the group minimum (a route is used only where every rank
+ * allows it), and INCCL_ENGINE must name the same engine on every rank. */
+typedef struct {
+    uint64_t ll_max_bytes, rccl_ar_bytes, mesh_chunk;
+    int32_t mesh_rs, force_sharded, mesh_lag, host_chunk_mib;
+    char engine[16];
+} comm_knobs;
+
+static int agree_knobs(struct inccl_communicator *c, const char *eng)
+{
+    struct inccl_group *g = c->group;
+    comm_knobs mine, *all = (comm_knobs *)calloc((size_t)g->world_size, sizeof(comm_knobs));
+    if (!all) return inccl_set_error(INCCL_ERR_NOMEM, "communicator: out of memory");
+    memset(&mine, 0, sizeof(mine));
+    mine.ll_max_bytes = c->ll_max_bytes;
+    mine.rccl_ar_bytes = c->rccl_ar_bytes;
+    mine.mesh_chunk = c->mesh_chunk_env;
+    mine.mesh_rs = c->mesh_rs;
+    mine.force_sharded = c->force_sharded;
+    mine.mesh_lag = c->mesh_lag_env;
+    mine.host_chunk_mib = c->host_chunk_mib;
+    snprintf(mine.engine, sizeof(mine.engine), "%s", eng ? eng : "");
+    int rc = inccl_boot_allgather(g, &mine, all, sizeof(comm_knobs));
+    for (int j = 0; !rc && j < g->world_size; ++j) {
+        const comm_knobs *k = &all[j];
+        if (strncmp(k->engine, mine.engine, sizeof(mine.engine)) != 0) {
+            rc = inccl_set_error(INCCL_ERR_ARG, "INCCL_ENGINE differs across ranks (rank %d: \"%.15s\", rank %d: \"%.15s\")",
+                                 g->rank, mine.engine, j, k->engine);
+            break;
+        }
+        if (k->ll_max_bytes < c->ll_max_bytes) c->ll_max_bytes = (size_t)k->ll_max_bytes;
+        if (k->rccl_ar_bytes < c->rccl_ar_bytes) c->rccl_ar_bytes = (size_t)k->rccl_ar_bytes;
+        if (k->mesh_chunk < c->mesh_chunk_env) c->mesh_chunk_env = (size_t)k->mesh_chunk;
+        if (k->mesh_rs < c->mesh_rs) c->mesh_rs = k->mesh_rs;
+        if (k->force_sharded < c->force_sharded) c->force_sharded = k->force_sharded;
+        if (k->mesh_lag < c->mesh_lag_env) c->mesh_lag_env = k->mesh_lag;
+        if (k->host_chunk_mib < c->host_chunk_mib) c->host_chunk_mib = k->host_chunk_mib;
+    }
+    free(all);
+    return rc;
+}
+
 static int comm_init(struct inccl_communicator *c, uint32_t size)
 {
     struct inccl_group *g = c->group;
@@ -508,11 +561,25 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     const char *llb = getenv("INCCL_LL_MAX_BYTES");   /* small-bucket one-kernel path; 0 disables */
     c->ll_max_bytes = llb ? (size_t)strtoull(llb, NULL, 0) : ((size_t)1 << 20);
     if (c->ll_max_bytes > ((size_t)1 << 30)) c->ll_max_bytes = (size_t)1 << 30;   /* 32-bit buffer offsets */
-    const char *mrs = getenv("INCCL_MESH_RS");        /* the mesh engines' own reduce-scatter route (opt-in) */
-    c->mesh_rs = mrs && atoi(mrs) != 0;
+    const char *mrs = getenv("INCCL_MESH_RS");        /* the mesh engines' own reduce-scatter route (0: off) */
+    c->mesh_rs = mrs ? atoi(mrs) != 0 : 1;
     const char *arb = getenv("INCCL_RCCL_AR_BYTES");  /* rccl engine: one all-reduce up to this; 0 disables */
     c->rccl_ar_bytes = arb ? (size_t)strtoull(arb, NULL, 0) : ((size_t)1 << 20);
+    const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: the sharded paths even at world 1 */
+    c->force_sharded = fs && atoi(fs) != 0;
+    const char *mce = getenv("INCCL_MESH_CHUNK");
+    c->mesh_chunk_env = mce ? (size_t)strtoull(mce, NULL, 0) : 0;
+    const char *mle = getenv("INCCL_MESH_LAG");
+    c->mesh_lag_env = mle ? atoi(mle) : 0;
+    if (c->mesh_lag_env < 0) c->mesh_lag_env = 0;
+    const char *hce = getenv("INCCL_HOST_CHUNK_MIB");
+    c->host_chunk_mib = hce ? atoi(hce) : 0;
+    if (c->host_chunk_mib < 1 || c->host_chunk_mib > 1024) c->host_chunk_mib = 16;
     const char *eng = getenv("INCCL_ENGINE");
+    if (g->transport == INCCL_TRANSPORT_RCCL && g->world_size > 1) {
+        int rc = agree_knobs(c, eng);
+        if (rc) return rc;
+    }
     if (eng && *eng && g->transport == INCCL_TRANSPORT_RCCL) {
         int rc = inccl_comm_set_engine(c, eng);
         if (rc) return rc;
@@ -890,8 +957,7 @@ static int allreduce_f32_body(struct inccl_communicator *c, const float *const *
     if (rc) return rc;
     const int scale_R = R * W;
 
-    const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: RS/AG path even at world 1 */
-    if (W == 1 && !(fs && atoi(fs) != 0))   /* one fused HBM pass: quant + sum + dequant */
+    if (W == 1 && !c->force_sharded)   /* one fused HBM pass: quant + sum + dequant */
         return kerr(inccl_k_stream_s(INCCL_KIND_F32, INCCL_KIND_F32, (const void *const *)srcs_dev, R, dst_dev, n, k,
                                      amax, scale_R, c->out_shift, st));
 
@@ -1035,8 +1101,7 @@ static int allreduce_16_body(struct inccl_communicator *c, int kind, const uint1
         if (rc) return rc;
     }
     const int scale_R = R * W;
-    const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: RS/AG path even at world 1 */
-    if (W == 1 && !(fs && atoi(fs) != 0))   /* one fused HBM pass */
+    if (W == 1 && !c->force_sharded)   /* one fused HBM pass */
         return kerr(inccl_k_stream_s(kind, kind, srcs, R, dst_dev, n, k, amax, scale_R,
                                      c->out_shift, st));
 
@@ -1076,12 +1141,23 @@ static int allreduce_16_body(struct inccl_communicator *c, int kind, const uint1
     /* the mesh engines: the persistent kernel with 2-byte sources and results (mesh.c) */
     if (c->engine == INCCL_ENGINE_MESH && c->group->transport == INCCL_TRANSPORT_RCCL)
         return inccl_mesh_piece16(c, kind, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
-    /* the p2p engine: 2-byte result shards gathered over xGMI (p2p.c) */
-    if (c->engine == INCCL_ENGINE_P2P && c->group->transport == INCCL_TRANSPORT_RCCL && ((uintptr_t)dst_dev & 3u) == 0)
-        return inccl_p2p_piece16(c, kind, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
-    /* every other engine (and a p2p dst that is not 4-B aligned): its int32
-     * allreduce of the quantised partials (RCCL all-reduce for "ar" / "a2a",
-     * the p2p exchange for the IPC engines) */
+    /* the p2p engine: 2-byte result shards gathered over xGMI (p2p.c).  The
+     * route never depends on this rank's dst alignment (every rank must take
+     * it): a dst that is not 4-B aligned gets it into the aligned workspace and
+     * one copy out */
+    if (c->engine == INCCL_ENGINE_P2P && c->group->transport == INCCL_TRANSPORT_RCCL) {
+        if (((uintptr_t)dst_dev & 3u) == 0) return inccl_p2p_piece16(c, kind, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+        int rc = inccl_ws_claim(c, st);
+        if (rc) return rc;
+        rc = inccl_ensure_dev(&c->d_f32, &c->d_f32_bytes, n * sizeof(uint16_t));
+        if (rc) return rc;
+        rc = inccl_p2p_piece16(c, kind, srcs_dev, R, (uint16_t *)c->d_f32, n, k, amax, scale_R, st);
+        if (rc) return rc;
+        INCCL_HIP(hipMemcpyAsync(dst_dev, c->d_f32, n * sizeof(uint16_t), hipMemcpyDeviceToDevice, st));
+        return 0;
+    }
+    /* every other engine: its int32 allreduce of the quantised partials (RCCL
+     * all-reduce for "ar" / "a2a", the p2p exchange for the IPC engines) */
     int rc = inccl_ws_claim(c, st);
     if (rc) return rc;
     rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
@@ -1141,8 +1217,7 @@ static int reduce_scatter_body(struct inccl_communicator *c, int kind, const voi
     int rc = resolve_scale(c, kind, srcs, R, n, scale_exp, st, &amax, &k);
     if (rc) return rc;
     const int scale_R = R * W;
-    const char *fs = getenv("INCCL_FORCE_SHARDED");   /* test hook: the reduce-scatter path even at world 1 */
-    if (W == 1 && !(fs && atoi(fs) != 0))   /* one fused HBM pass */
+    if (W == 1 && !c->force_sharded)   /* one fused HBM pass */
         return kerr(inccl_k_stream_s(kind, kind, srcs, R, dst, n, k, amax, scale_R, c->out_shift, st));
     if (c->engine == INCCL_ENGINE_RCCL || c->group->transport == INCCL_TRANSPORT_LOCAL) {
         /* quant + local sum -> int32 reduce-scatter -> dequantise the shard */
@@ -1159,25 +1234,39 @@ static int reduce_scatter_body(struct inccl_communicator *c, int kind, const voi
         return kerr(inccl_k_stream_s(INCCL_KIND_Q32, kind, s1, 1, dst, shard, k, amax, scale_R, c->out_shift, st));
     }
     const int ipc = c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH;
-    const uintptr_t dst_align = kind == INCCL_KIND_F32 ? 15u : 7u;
-    /* the mesh engines' own route, opt-in (INCCL_MESH_RS=1): their one
-     * persistent kernel, each reduce writing its chunk of this rank's shard
-     * into dst (shards of whole 64-element groups).  Off by default: with four
-     * and eight processes on one GPU it returned wrong shards and faulted
-     * ("Mesh reduce-scatter route"); the mesh engines take the p2p
-     * pull-reduce below instead */
-    if (c->mesh_rs && c->engine == INCCL_ENGINE_MESH && c->group->transport == INCCL_TRANSPORT_RCCL && !(shard % 64) &&
-        ((uintptr_t)dst & dst_align) == 0)
-        return inccl_mesh_reduce_scatter(c, kind, srcs, R, dst, n, k, amax, scale_R, st);
-    /* the ll engine's one kernel for a small fp32 bucket: every rank's quads
-     * published with a flag, this rank's shard summed and dequantised */
-    if (kind == INCCL_KIND_F32 && c->engine == INCCL_ENGINE_LL && c->group->transport == INCCL_TRANSPORT_RCCL &&
-        n <= c->ll_max_bytes / sizeof(float) && !(shard & 3))
-        return inccl_ll_piece(c, (const float *const *)srcs, R, (float *)dst, n, k, amax, scale_R, (size_t)me * shard,
-                              shard, st);
-    if (ipc && c->group->transport == INCCL_TRANSPORT_RCCL && !(shard & 3) &&
-        ((uintptr_t)dst & (kind == INCCL_KIND_F32 ? 15u : 7u)) == 0)
-        return inccl_p2p_reduce_scatter(c, kind, srcs, R, dst, n, k, amax, scale_R, st);
+    /* Every route below is chosen from what all ranks share (engine, n, W and
+     * the knobs agreed in agree_knobs), never from this rank's dst alignment:
+     * a dst the vector kernels cannot store to (fp32 not 16-B, 16-bit not 8-B
+     * aligned) gets the same route into an aligned workspace and one copy out. */
+    const int rcclt = c->group->transport == INCCL_TRANSPORT_RCCL;
+    const int mesh_route = c->mesh_rs && c->engine == INCCL_ENGINE_MESH && rcclt && !(shard % 64);
+    const int p2p_route = ipc && rcclt && !(shard & 3);
+    if (mesh_route || p2p_route) {
+        void *out = dst;
+        if (((uintptr_t)dst & (kind == INCCL_KIND_F32 ? 15u : 7u)) != 0) {
+            rc = inccl_ws_claim(c, st);
+            if (rc) return rc;
+            rc = inccl_ensure_dev(&c->d_f32, &c->d_f32_bytes, shard * es);
+            if (rc) return rc;
+            out = c->d_f32;
+        }
+        /* the mesh engines' own route (INCCL_MESH_RS, default on): their one
+         * persistent kernel, the allreduce's instructions with the other ranks'
+         * gathers reduced to their waits (mesh.c; DESIGN.md, "Mesh
+         * reduce-scatter route").  The ll engine's one kernel for a small fp32
+         * bucket: every rank's quads published with a flag, this rank's shard
+         * summed and dequantised.  Otherwise the p2p pull-reduce. */
+        if (mesh_route)
+            rc = inccl_mesh_reduce_scatter(c, kind, srcs, R, out, n, k, amax, scale_R, st);
+        else if (kind == INCCL_KIND_F32 && c->engine == INCCL_ENGINE_LL && n <= c->ll_max_bytes / sizeof(float))
+            rc = inccl_ll_piece(c, (const float *const *)srcs, R, (float *)out, n, k, amax, scale_R,
+                                (size_t)me * shard, shard, st);
+        else
+            rc = inccl_p2p_reduce_scatter(c, kind, srcs, R, out, n, k, amax, scale_R, st);
+        if (rc || out == dst) return rc;
+        INCCL_HIP(hipMemcpyAsync(dst, out, shard * es, hipMemcpyDeviceToDevice, st));
+        return 0;
+    }
     /* every other engine, or a shard the pull-reduce cannot take: the engine's
      * int32 allreduce, then the shard dequantised */
     rc = inccl_ws_claim(c, st);
@@ -1312,18 +1401,16 @@ static int host_registered(const struct inccl_communicator *c, const void *p, si
         }                                              \
     }
 
-static size_t host_chunk_elems(void)
+/* INCCL_HOST_CHUNK_MIB, agreed over the group (agree_knobs): chunks are collective */
+static size_t host_chunk_elems(const struct inccl_communicator *c)
 {
-    const char *e = getenv("INCCL_HOST_CHUNK_MIB");
-    long v = e ? atol(e) : 0;
-    if (v < 1 || v > 1024) v = 16;
-    return ((size_t)v << 20) / sizeof(int32_t);
+    return ((size_t)c->host_chunk_mib << 20) / sizeof(int32_t);
 }
 
 static int allreduce_host_q32_direct(struct inccl_communicator *c, const int32_t *src, size_t n, int32_t *dst,
                                      int pageable)
 {
-    const size_t CH = host_chunk_elems();
+    const size_t CH = host_chunk_elems(c);
     int rc = inccl_ensure_dev(&c->d_stage, &c->d_stage_bytes, 2 * CH * sizeof(int32_t));
     if (rc) return rc;
     if (pageable && !c->d2h) c->d2h = inccl_d2h_worker_create(c->group->device);

@@ -99,7 +99,14 @@ struct inccl_communicator {
     uint64_t ll_timeout_ticks;
     hipStream_t ll_last_stream;  /* ordering across caller streams (ev[7]) */
     size_t ll_max_bytes;         /* buckets up to this size take the ll kernel */
-    int mesh_rs;                 /* INCCL_MESH_RS: reduce-scatter through the mesh kernel (opt-in) */
+    int mesh_rs;                 /* INCCL_MESH_RS (default 1): reduce-scatter through the mesh kernel */
+    int force_sharded;           /* INCCL_FORCE_SHARDED: test hook, the sharded paths even at world 1 */
+    size_t mesh_chunk_env;       /* INCCL_MESH_CHUNK elements (0: mesh.c's default) */
+    int mesh_lag_env;            /* INCCL_MESH_LAG slots (0: the whole shard) */
+    int host_chunk_mib;          /* INCCL_HOST_CHUNK_MIB: host pipeline chunk (default 16) */
+    /* every knob above that picks a route or a schedule is agreed over the
+     * group when the communicator is created (api.c agree_knobs): ranks whose
+     * environments differ still take the same route on every call */
     size_t rccl_ar_bytes;        /* rccl engine: int32 partials up to this size take one
                                     ncclAllReduce instead of reduce-scatter + all-gather */
     /* mesh engine (large buckets, one persistent kernel per call): one IPC buffer

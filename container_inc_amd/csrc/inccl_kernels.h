@@ -100,7 +100,14 @@ struct inccl_mesh_launch {
     const uint32_t *amax_bits;
     int scale_R;
     int out_shift;                                     /* dequantise with 2^-(k + out_shift) */
+    /* region sizes for the kernel's per-item bounds check (every rank's regions
+     * have the same sizes): a work item whose buffer range falls outside its
+     * region stores INCCL_MESH_ERR_BOUNDS | item << 8 | peer << 4 into *err
+     * and aborts the call instead of touching memory */
+    size_t src_bytes, dst_bytes, inbox_bytes, res_bytes, resin_bytes;
 };
+#define INCCL_MESH_ERR_TIMEOUT 1u
+#define INCCL_MESH_ERR_BOUNDS 2u
 int inccl_k_mesh(const struct inccl_mesh_launch *l, void *stream);
 
 #ifdef __cplusplus

@@ -88,8 +88,10 @@ struct MeshArgs {
     uint32_t* err;                       // host-mapped error word
     uint64_t timeout_ticks;
     int nchunks, W, me, lag, vec_src, vec_dst, push_res;
-    int rs;                              // reduce-scatter: reduce(c) writes dst (the shard), gathers only wait
+    int rs;                              // reduce-scatter: gather(c, me) copies my result chunk into dst (the
+                                         // shard), the other gathers only wait
     Scale sc;
+    uint64_t src_bytes, dst_bytes, inbox_bytes, res_bytes, resin_bytes;   // region sizes (bounds check)
 };
 
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
@@ -124,13 +126,34 @@ __device__ bool wait_flag(const MeshArgs& a, const uint32_t* f, uint32_t epoch)
     while ((int32_t)(ld_sys(f) - epoch) < 0) {
         if (__hip_atomic_load(a.ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
         if (now_ticks() - t0 > a.timeout_ticks) {
-            __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.err, INCCL_MESH_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(a.ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
         }
         __builtin_amdgcn_s_sleep(2);
     }
     return true;
+}
+
+// Per-item bounds check (wave-uniform, a few scalar instructions per item): the
+// byte range [p, p + bytes) an item is about to build a buffer resource over, or
+// read through plain loads, must lie inside its region [base, base + size).
+// Otherwise the item reports where (*err = INCCL_MESH_ERR_BOUNDS | item << 8 |
+// peer << 4, the first report wins) and the call aborts without the access --
+// the evidence a fault would have destroyed (DESIGN.md "Mesh reduce-scatter
+// route"; a later report may overwrite an earlier one).  item: 1 push src, 2 push inbox, 3 reduce inbox, 4 reduce res,
+// 5 reduce resin, 6 gather src, 7 gather dst.
+__device__ bool inside(const MeshArgs& a, const void* base, uint64_t size, const void* p, uint64_t bytes,
+                       uint32_t item, int peer)
+{
+    const uint64_t b = reinterpret_cast<uint64_t>(base), q = reinterpret_cast<uint64_t>(p);
+    if (base != nullptr && q >= b && bytes <= size && q - b <= size - bytes) return true;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(a.err, INCCL_MESH_ERR_BOUNDS | item << 8 | (uint32_t)peer << 4, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return false;
 }
 
 __device__ __forceinline__ int64_t chunk_len(const MeshArgs& a, int c)
@@ -145,12 +168,22 @@ __device__ __forceinline__ int64_t chunk_len(const MeshArgs& a, int c)
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 template <int R, int E>
-__device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float scale)
+__device__ bool do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float scale)
 {
     const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;   // global element index
     const int64_t nq = chunk_len(a, c) >> 2;
-    const __amdgpu_buffer_rsrc_t out =
-        rsrc(a.peer_inbox[j] + (int64_t)a.me * a.inbox_stride + (int64_t)c * a.chunk, (uint32_t)(nq * 16));
+    constexpr int SE = is16(E) ? 2 : 4;   // source element bytes
+    if (lo < a.n) {
+        const int64_t cnt = a.n - lo < 4 * nq ? a.n - lo : 4 * nq;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (!inside(a, a.src.p[r], a.src_bytes, reinterpret_cast<const char*>(a.src.p[r]) + lo * SE,
+                        (uint64_t)cnt * SE, 1, r))
+                return false;
+    }
+    uint32_t* obase = a.peer_inbox[j] + (int64_t)a.me * a.inbox_stride + (int64_t)c * a.chunk;
+    if (!inside(a, a.peer_inbox[j], a.inbox_bytes, obase, (uint64_t)nq * 16, 2, j)) return false;
+    const __amdgpu_buffer_rsrc_t out = rsrc(obase, (uint32_t)(nq * 16));
     const bool full = a.vec_src && lo + 4 * nq <= a.n;
     for (int64_t q0 = threadIdx.x; q0 < nq; q0 += (int64_t)kMeshBlock * kMeshU) {
         u32x4 acc[kMeshU];
@@ -223,6 +256,7 @@ __device__ void do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float s
     __builtin_amdgcn_s_waitcnt(0);   // this lane's stores acknowledged at system scope
     __syncthreads();                 // ... and every lane's
     if (threadIdx.x == 0) st_sys(a.peer_sig[j] + arrive_idx(a.me, c), epoch);
+    return true;
 }
 
 // reduce(c): my shard's chunk c = dequant(sum over the W inbox slots); E = BF16 /
@@ -236,18 +270,30 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
     if (!__syncthreads_and(ok)) return false;
     const int64_t nq = chunk_len(a, c) >> 2;
     const uint32_t bytes = (uint32_t)(nq * 16);
+    for (int j = 0; j < a.W; ++j)
+        if (!inside(a, a.own_inbox, a.inbox_bytes, a.own_inbox + (int64_t)j * a.inbox_stride + (int64_t)c * a.chunk,
+                    bytes, 3, j))
+            return false;
     __amdgpu_buffer_rsrc_t in[kMaxR];
 #pragma unroll
     for (int j = 0; j < kMaxR; ++j)
         in[j] = rsrc(a.own_inbox + (int64_t)(j < a.W ? j : 0) * a.inbox_stride + (int64_t)c * a.chunk, bytes);
     constexpr int ES = is16(E) ? 2 : 4;   // result element bytes
     const uint32_t obytes = (uint32_t)(nq * 4 * ES);
-    // reduce-scatter: the chunk goes straight into dst, this rank's shard
-    const char* rbase = a.rs ? reinterpret_cast<const char*>(a.dst) : reinterpret_cast<const char*>(a.own_res);
-    const __amdgpu_buffer_rsrc_t res = rsrc(rbase + (int64_t)c * a.chunk * ES, obytes);
     const bool push = a.push_res && !a.rs;
+    // my result chunk, in every mode but meshw's allreduce the same store into
+    // own_res (IPC memory); reduce-scatter copies it into dst in gather(c, me)
+    const char* rbase = reinterpret_cast<const char*>(a.own_res) + (int64_t)c * a.chunk * ES;
+    if (!push && !inside(a, a.own_res, a.res_bytes, rbase, obytes, 4, a.me)) return false;
+    const __amdgpu_buffer_rsrc_t res = rsrc(rbase, obytes);
     __amdgpu_buffer_rsrc_t outs[kMaxR];   // push_res: my slot of every rank's result inbox
     if (push) {
+        for (int j = 0; j < a.W; ++j)
+            if (!inside(a, a.peer_resin[j], a.resin_bytes,
+                        reinterpret_cast<const char*>(a.peer_resin[j]) +
+                            ((int64_t)a.me * a.inbox_stride + (int64_t)c * a.chunk) * ES,
+                        obytes, 5, j))
+                return false;
 #pragma unroll
         for (int j = 0; j < kMaxR; ++j)
             outs[j] = rsrc(reinterpret_cast<const char*>(a.peer_resin[j < a.W ? j : 0]) +
@@ -281,12 +327,7 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
                     for (int j = 0; j < kMaxR; ++j)
                         if (j < a.W) __builtin_amdgcn_raw_buffer_store_b64(o, outs[j], (int)(q * 8), 0, kAuxSys);
                 } else {
-                    // (reduce-scatter: dst is the caller's, read by ordinary loads -- sc1
-                    // write-through as the gathers' dst stores, not system scope)
-                    if (a.rs)
-                        __builtin_amdgcn_raw_buffer_store_b64(o, res, (int)(q * 8), 0, 16);
-                    else
-                        __builtin_amdgcn_raw_buffer_store_b64(o, res, (int)(q * 8), 0, kAuxSys);
+                    __builtin_amdgcn_raw_buffer_store_b64(o, res, (int)(q * 8), 0, kAuxSys);
                 }
             } else {
                 u32x4 o;
@@ -298,8 +339,6 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
 #pragma unroll
                     for (int j = 0; j < kMaxR; ++j)
                         if (j < a.W) st_sys16(outs[j], (uint32_t)(q * 16), o);
-                } else if (a.rs) {
-                    __builtin_amdgcn_raw_buffer_store_b128(o, res, (int)(q * 16), 0, 16);   // sc1, as above
                 } else {
                     st_sys16(res, (uint32_t)(q * 16), o);
                 }
@@ -312,26 +351,35 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
     return true;
 }
 
-// gather(c, j): rank j's result chunk c -> dst (clipped to n).  Reduce-scatter:
-// the wait alone -- the call then ends only after every rank has reduced every
-// chunk, i.e. read its inbox, which is what lets the next call push into it
+// gather(c, j): rank j's result chunk c -> dst (clipped to n).
+// Reduce-scatter: gather(c, me) copies my own result chunk into my shard (the
+// pull path with j = me, as in the allreduce); gather(c, j != me) is the wait
+// alone -- the call then ends only after every rank has reduced every chunk,
+// i.e. read its inbox, which is what lets the next call push into it.  So a
+// reduce-scatter issues no instruction the allreduce does not (DESIGN.md,
+// "Mesh reduce-scatter route").
 __device__ bool do_gather(const MeshArgs& a, int c, int j, uint32_t epoch)
 {
     bool ok = true;
     if (threadIdx.x == 0) ok = wait_flag(a, a.own_sig + ready_idx(j, c), epoch);
     if (!__syncthreads_and(ok)) return false;
-    if (a.rs) return true;
+    if (a.rs && j != a.me) return true;
     const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;
     if (lo >= a.n) return true;
     int64_t cnt = chunk_len(a, c);
     if (lo + cnt > a.n) cnt = a.n - lo;
     const int64_t nq = cnt >> 2;
     // pull rank j's result chunk over xGMI, or (push_res) copy what rank j pushed
-    // into my result inbox
-    const uint32_t* sbase = a.push_res ? a.own_resin + (int64_t)j * a.inbox_stride + (int64_t)c * a.chunk
-                                       : a.peer_res[j] + (int64_t)c * a.chunk;
+    // into my result inbox; reduce-scatter: my own result chunk
+    const bool inbox = a.push_res && !a.rs;
+    const uint32_t* sbase = inbox ? a.own_resin + (int64_t)j * a.inbox_stride + (int64_t)c * a.chunk
+                                  : a.peer_res[j] + (int64_t)c * a.chunk;
+    if (!inside(a, inbox ? a.own_resin : a.peer_res[j], inbox ? a.resin_bytes : a.res_bytes, sbase,
+                (uint64_t)chunk_len(a, c) * 4, 6, j))
+        return false;
     const __amdgpu_buffer_rsrc_t src = rsrc(sbase, (uint32_t)(chunk_len(a, c) * 4));
-    uint32_t* d = reinterpret_cast<uint32_t*>(a.dst) + lo;
+    uint32_t* d = reinterpret_cast<uint32_t*>(a.dst) + (a.rs ? (int64_t)c * a.chunk : lo);
+    if (!inside(a, a.dst, a.dst_bytes, d, (uint64_t)cnt * 4, 7, j)) return false;
     const __amdgpu_buffer_rsrc_t drs = rsrc(d, (uint32_t)(nq * 16));   // write-through dst stores (vec_dst)
     for (int64_t q0 = threadIdx.x; q0 < nq; q0 += (int64_t)kMeshBlock * kMeshU) {
         u32x4 v[kMeshU];
@@ -365,17 +413,22 @@ __device__ bool do_gather16(const MeshArgs& a, int c, int j, uint32_t epoch)
     bool ok = true;
     if (threadIdx.x == 0) ok = wait_flag(a, a.own_sig + ready_idx(j, c), epoch);
     if (!__syncthreads_and(ok)) return false;
-    if (a.rs) return true;
+    if (a.rs && j != a.me) return true;   // reduce-scatter: as do_gather
     const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;
     if (lo >= a.n) return true;
     int64_t cnt = chunk_len(a, c);
     if (lo + cnt > a.n) cnt = a.n - lo;
     const int64_t n8 = cnt >> 3;
-    const uint16_t* sbase = a.push_res
+    const bool inbox = a.push_res && !a.rs;
+    const uint16_t* sbase = inbox
                                 ? reinterpret_cast<const uint16_t*>(a.own_resin) + (int64_t)j * a.inbox_stride + (int64_t)c * a.chunk
                                 : reinterpret_cast<const uint16_t*>(a.peer_res[j]) + (int64_t)c * a.chunk;
+    if (!inside(a, inbox ? a.own_resin : a.peer_res[j], inbox ? a.resin_bytes : a.res_bytes, sbase,
+                (uint64_t)chunk_len(a, c) * 2, 6, j))
+        return false;
     const __amdgpu_buffer_rsrc_t src = rsrc(sbase, (uint32_t)(chunk_len(a, c) * 2));
-    uint16_t* d = reinterpret_cast<uint16_t*>(a.dst) + lo;
+    uint16_t* d = reinterpret_cast<uint16_t*>(a.dst) + (a.rs ? (int64_t)c * a.chunk : lo);
+    if (!inside(a, a.dst, a.dst_bytes, d, (uint64_t)cnt * 2, 7, j)) return false;
     const __amdgpu_buffer_rsrc_t drs = rsrc(d, (uint32_t)(n8 * 16));
     for (int64_t q0 = threadIdx.x; q0 < n8; q0 += (int64_t)kMeshBlock * kMeshU) {
         u32x4 v[kMeshU];
@@ -425,7 +478,7 @@ __global__ __launch_bounds__(kMeshBlock) void k_mesh(MeshArgs a)
         if (t >= total) break;
         const int s = t / per_slot, pos = t - s * per_slot;
         if (pos < W) {
-            if (s < a.nchunks) do_push<R, E>(a, s, (a.me + 1 + pos) % W, epoch, scale);
+            if (s < a.nchunks && !do_push<R, E>(a, s, (a.me + 1 + pos) % W, epoch, scale)) break;
         } else if (pos == W) {
             const int c = s - a.lag;
             if (c >= 0 && c < a.nchunks && !do_reduce<E>(a, c, epoch, inv)) break;
@@ -492,6 +545,11 @@ extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
     a.sc.amax_bits = l->amax_bits;
     a.sc.scale_R = l->scale_R;
     a.sc.out_shift = l->out_shift;
+    a.src_bytes = l->src_bytes;
+    a.dst_bytes = l->dst_bytes;
+    a.inbox_bytes = l->inbox_bytes;
+    a.res_bytes = l->res_bytes;
+    a.resin_bytes = l->resin_bytes;
     hipStream_t st = (hipStream_t)stream;
     const dim3 g((unsigned)l->grid), b(kMeshBlock);
 #define INCCL_MESH_CASE(RR)                                                  \

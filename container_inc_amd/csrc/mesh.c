@@ -203,11 +203,10 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
 }
 
 /* Chunk size: about 256 chunks per shard for overlap, 16-256 KiB each
- * ($INCCL_MESH_CHUNK elements overrides; same on every rank). */
-static size_t mesh_chunk(size_t shard)
+ * ($INCCL_MESH_CHUNK elements overrides; agreed over the group, api.c). */
+static size_t mesh_chunk(const struct inccl_communicator *c, size_t shard)
 {
-    const char *ce = getenv("INCCL_MESH_CHUNK");
-    size_t ch = ce ? (size_t)strtoull(ce, NULL, 0) : 0;
+    size_t ch = c->mesh_chunk_env;
     if (ch == 0) {
         ch = (shard + 255) / 256;
         ch = (ch + 4095) & ~(size_t)4095;
@@ -234,9 +233,13 @@ static int mesh_piece(struct inccl_communicator *c, int kind16, const void *cons
         return inccl_set_error(INCCL_ERR_STATE, "mesh: make one call of this size outside graph capture first");
     int rc = mesh_ensure(c, shard);
     if (rc) return rc;
-    if (*(volatile uint32_t *)c->mesh_err_host)
+    const uint32_t err = *(volatile uint32_t *)c->mesh_err_host;
+    if (err & INCCL_MESH_ERR_BOUNDS)   /* the kernel's per-item bounds check (inccl_mesh.hip inside()) */
+        return inccl_set_error(INCCL_ERR_STATE, "mesh: an earlier call stopped at its bounds check (item %u, peer %u; "
+                               "results invalid)", (err >> 8) & 0xffu, (err >> 4) & 0xfu);
+    if (err)
         return inccl_set_error(INCCL_ERR_STATE, "mesh: an earlier call timed out waiting for a peer (results invalid)");
-    const size_t chunk = mesh_chunk(shard);
+    const size_t chunk = mesh_chunk(c, shard);
     const int nchunks = (int)((shard + chunk - 1) / chunk);
     /* a reduce / gather starts `lag` slots after what it waits for.  Default: the
      * whole shard, i.e. every push is taken before the first reduce and every
@@ -244,9 +247,8 @@ static int mesh_piece(struct inccl_communicator *c, int kind16, const void *cons
      * CU slot idle, and on one GPU (256 MiB, R = 2) lag = 1 / 171 / 400 / all
      * chunks ran 823 / 668 / 474 / 402 us.  Phases still overlap at their
      * seams, and both xGMI directions are busy in the push and gather phases.
-     * ($INCCL_MESH_LAG slots overrides; same on every rank.) */
-    const char *le = getenv("INCCL_MESH_LAG");
-    int lag = le ? atoi(le) : nchunks;
+     * ($INCCL_MESH_LAG slots overrides; agreed over the group, api.c.) */
+    int lag = c->mesh_lag_env ? c->mesh_lag_env : nchunks;
     if (lag < 1) lag = 1;
     if (lag > nchunks) lag = nchunks;
     struct inccl_mesh_launch l;
@@ -283,6 +285,12 @@ static int mesh_piece(struct inccl_communicator *c, int kind16, const void *cons
     l.amax_bits = amax;
     l.scale_R = scale_R;
     l.out_shift = c->out_shift;
+    const size_t es = kind16 ? sizeof(uint16_t) : sizeof(float);   /* source and result element bytes */
+    l.src_bytes = n * es;
+    l.dst_bytes = (rs ? shard : n) * es;
+    l.inbox_bytes = mesh_region_bytes(1, W, c->mesh_cap);
+    l.res_bytes = mesh_region_bytes(2, W, c->mesh_cap);
+    l.resin_bytes = mesh_region_bytes(3, W, c->mesh_cap);
     /* the buffer-reuse argument needs this rank's calls in order: chain across
      * streams (inside a capture the caller's capture stream orders them) */
     if (!capturing && c->mesh_last_stream && c->mesh_last_stream != st) INCCL_HIP(hipStreamWaitEvent(st, c->ev[6], 0));
@@ -302,9 +310,11 @@ int inccl_mesh_piece(struct inccl_communicator *c, const float *const *srcs, int
     return mesh_piece(c, 0, (const void *const *)srcs, R, dst, n, k, amax, scale_R, 0, st);
 }
 
-/* reduce-scatter (inccl_reduce_scatter_*): the same kernel, each reduce writing
- * its chunk into dst (this rank's n / W elements, n % (64 W) == 0) and the
- * gathers reduced to their waits; kind INCCL_KIND_F32, BF16 or F16 */
+/* reduce-scatter (inccl_reduce_scatter_*): the same kernel and the same
+ * instructions as the allreduce, with the gathers of other ranks' chunks reduced
+ * to their flag waits and gather(c, me) copying this rank's own result chunk
+ * into dst (its n / W elements, n % (64 W) == 0); kind INCCL_KIND_F32, BF16 or
+ * F16 */
 int inccl_mesh_reduce_scatter(struct inccl_communicator *c, int kind, const void *const *srcs, int R, void *dst,
                               size_t n, int k, const uint32_t *amax, int scale_R, hipStream_t st)
 {

@@ -396,20 +396,26 @@ const int32_t *inccl_switch_slot(struct inccl_switch *sw, uint32_t psn);
  * nts.c:367, which the reference runs at completion, in its ingress pipeline). */
 int inccl_switch_ingress(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
                          const int32_t *ports_dev, int32_t *action_dev, uint32_t *psn_dev, void *stream);
-/* For every COMPLETED frame i: fan_in egress frames to children c at
- * out_dev[(i*fan_in + c) * out_stride] with frame i's opcode (and, for a
- * WRITE_FIRST / WRITE_ONLY opcode, child c's kept RETH); for every REPLAY frame:
- * one such frame to its port; for every ACK frame: the 62-B ACK of
- * send_roce_ack (opcode 0x11, its PSN, AETH MSN = PSN + 1) to its port.  out_len_dev[i*fan_in + c] = frame bytes or 0 (bytes past a frame, up to its 16-byte
- * rounded length, are written as zero or left as they were).  templates_dev holds
- * fan_in inccl_frame_template records (device memory). */
+/* Rows per input frame: rows = fan_in for a root switch, fan_in + 1 for a
+ * non-root switch (the parent's row last, index fan_in).  For every COMPLETED
+ * frame i: fan_in egress frames to children c at out_dev[(i*rows + c) *
+ * out_stride] with frame i's opcode (and, for a WRITE_FIRST / WRITE_ONLY opcode,
+ * child c's kept RETH); for every REPLAY frame: one such frame to its port; for
+ * every ACK frame: the 62-B ACK of send_roce_ack (opcode 0x11, its PSN, AETH
+ * MSN = PSN + 1) to its port; a non-root switch also uses row fan_in for the
+ * frame it sends up.  out_len_dev[i*rows + c] = frame bytes or 0 (bytes past a
+ * frame, up to its 16-byte rounded length, are written as zero or left as they
+ * were).  templates_dev holds `rows` inccl_frame_template records (device
+ * memory): children 0..fan_in-1, then the parent's for a non-root switch.
+ * Size out_dev, out_len_dev and templates_dev for `rows`, not fan_in. */
 int inccl_switch_egress(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
                         const int32_t *ports_dev, const int32_t *action_dev, const uint32_t *psn_dev,
                         const struct inccl_frame_template *templates_dev, uint8_t *out_dev, size_t out_stride,
                         int32_t *out_len_dev, void *stream);
 /* inccl_switch_ingress followed by inccl_switch_egress of the same batch, in
  * one call (the reference's pipeline() runs both per frame): the same actions,
- * state, out rows and lengths, from the same kernels on `stream`. */
+ * state, out rows and lengths (`rows` per frame, as for inccl_switch_egress:
+ * fan_in + 1 on a non-root switch), from the same kernels on `stream`. */
 int inccl_switch_batch(struct inccl_switch *sw, const uint8_t *frames_dev, size_t stride, size_t count,
                        const int32_t *ports_dev, int32_t *action_dev, uint32_t *psn_dev,
                        const struct inccl_frame_template *templates_dev, uint8_t *out_dev, size_t out_stride,

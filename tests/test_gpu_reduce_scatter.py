@@ -150,11 +150,16 @@ def _free_port():
     return p
 
 
-def _ipc_rank(rank, world, port, q, engine, mesh_rs=False):
+def _ipc_rank(rank, world, port, q, engine, mesh_rs=None, misalign=False):
+    """One process of the multi-process tests.  mesh_rs: None = the default
+    (the mesh engines' own route), "0" = INCCL_MESH_RS=0 (the p2p pull-reduce).
+    misalign: odd ranks pass a dst one element into a buffer, so that it is not
+    16-B (fp32) or 8-B (16-bit) aligned while the even ranks' is: every rank
+    must still take the same route (api.c reduce_scatter_body)."""
     try:
         os.environ["INCCL_ENGINE"] = engine
-        if mesh_rs:
-            os.environ["INCCL_MESH_RS"] = "1"
+        if mesh_rs is not None:
+            os.environ["INCCL_MESH_RS"] = mesh_rs
         os.environ["INCCL_DEVICE"] = "0"
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
         import sys
@@ -166,6 +171,7 @@ def _ipc_rank(rank, world, port, q, engine, mesh_rs=False):
         grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=0)
         comm = inccl.inccl_communicator_create(grp, 0)
         ok = []
+        mesh_route = engine in ("mesh", "meshw") and mesh_rs != "0"
         for kind in KINDS:
             for shard, R, seed in ((1 << 18, 2, 1), (1001, 1, 2), (4096, 2, 3)):   # 1001: the int32-allreduce route
                 n = world * shard
@@ -175,16 +181,35 @@ def _ipc_rank(rank, world, port, q, engine, mesh_rs=False):
                 want = _reduce(O, every, kind, _auto_k(O, every, kind, world * R))[rank * shard:(rank + 1) * shard]
                 srcs = [_dev(h, dev, kind) for h in hs[rank]]
                 for _ in range(2):
-                    out = comm.reduce_scatter(srcs, stream=comm.stream)
+                    out = None
+                    if misalign and rank % 2:
+                        out = torch.empty(shard + 1, dtype=srcs[0].dtype, device=dev)[1:]
+                    out = comm.reduce_scatter(srcs, out=out, stream=comm.stream)
                     torch.cuda.synchronize()
                     ok.append(bool(np.array_equal(_host(out, kind), want)))
                 if engine == "ll" and kind == "f32" and shard == 4096:
                     comm.ipc_mem_kind("ll")   # raises unless the ll kernel's buffers exist: the ll route ran
                 if engine in ("mesh", "meshw") and shard == 1 << 18:
-                    if mesh_rs:
+                    if mesh_route:
                         comm.ipc_mem_kind("mesh")   # the persistent kernel's reduce-scatter route ran
+                        if kind == "f32":   # ... and the p2p pull-reduce did not (shard 1001 comes later)
+                            with pytest.raises(Exception):
+                                comm.ipc_mem_kind("p2p")
                     else:
-                        comm.ipc_mem_kind("p2p")    # by default the mesh engines take the p2p pull-reduce
+                        comm.ipc_mem_kind("p2p")    # INCCL_MESH_RS=0: the p2p pull-reduce
+        if misalign:   # the 16-bit allreduce: a dst that is not 4-B aligned on odd ranks (api.c allreduce_16_body)
+            for kind in ("bf16", "f16"):
+                n = world * 4096 + 2
+                hs = [_bucket(np.random.default_rng(77 + r), n, kind) for r in range(world)]
+                want = _reduce(O, hs, kind, 20)
+                src = _dev(hs[rank], dev, kind)
+                out = torch.empty(n + 1, dtype=src.dtype, device=dev)
+                out = out[1:] if rank % 2 else out[:n]
+                fn = comm.allreduce_bf16 if kind == "bf16" else comm.allreduce_f16
+                fn([src], out=out, scale_exp=20, stream=comm.stream)
+                torch.cuda.synchronize()
+                ok.append(bool(np.array_equal(_host(out, kind), want)))
+        comm.barrier()
         comm.destroy()
         grp.destroy()
         q.put((rank, ok, None))
@@ -192,17 +217,17 @@ def _ipc_rank(rank, world, port, q, engine, mesh_rs=False):
         q.put((rank, None, repr(e)))
 
 
-def _run_ipc(world, engine, mesh_rs=False):
+def _run_mp(world, target, *args, timeout=240):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_ipc_rank, args=(r, world, port, q, engine, mesh_rs)) for r in range(world)]
+    ps = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
     for p in ps:
         p.start()
     res = {}
     try:
         for _ in range(world):
-            r, ok, err = q.get(timeout=240)
+            r, ok, err = q.get(timeout=timeout)
             res[r] = (ok, err)
     finally:
         for p in ps:
@@ -215,25 +240,99 @@ def _run_ipc(world, engine, mesh_rs=False):
         assert all(ok), f"rank {r}: {ok}"
 
 
+def _run_ipc(world, engine, mesh_rs=None, misalign=False):
+    _run_mp(world, _ipc_rank, engine, mesh_rs, misalign)
+
+
 @pytest.mark.parametrize("world,engine", [(2, "p2p"), (3, "p2p"), (2, "mesh"), (3, "mesh"), (4, "meshw"), (2, "ll"),
                                          (4, "ll")])
 def test_reduce_scatter_ipc_multiprocess(gpu, world, engine):
     """ll: a small fp32 bucket (shard 4096) through the one-kernel ll reduce-
-    scatter; mesh / meshw: the p2p pull-reduce (their own route is opt-in);
+    scatter; mesh / meshw: their persistent kernel's own route (shards of whole
+    64-element groups; the allreduce's instructions with the other ranks'
+    gathers reduced to their waits, DESIGN.md "Mesh reduce-scatter route");
     the others through the p2p pull-reduce or the int32 allreduce (shard
     1001)."""
     _run_ipc(world, engine)
 
 
-@pytest.mark.skipif(not os.environ.get("INCCL_TEST_MESH_RS"),
-                    reason="the mesh engines' own reduce-scatter route is opt-in (INCCL_MESH_RS): with four and "
-                           "eight processes on one GPU it returned wrong shards and faulted (DESIGN.md); "
-                           "set INCCL_TEST_MESH_RS=1 to run it")
-@pytest.mark.parametrize("world,engine", [(2, "mesh"), (3, "mesh")])
-def test_reduce_scatter_mesh_route_opt_in(gpu, world, engine):
-    """The mesh kernel's reduce-scatter route (INCCL_MESH_RS=1): each reduce
-    writing its chunk into dst, the gathers reduced to their waits."""
-    _run_ipc(world, engine, mesh_rs=True)
+@pytest.mark.parametrize("world,engine", [(2, "mesh"), (3, "meshw")])
+def test_reduce_scatter_mesh_route_off(gpu, world, engine):
+    """INCCL_MESH_RS=0: the mesh engines reduce-scatter through the p2p
+    pull-reduce instead."""
+    _run_ipc(world, engine, mesh_rs="0")
+
+
+@pytest.mark.parametrize("world,engine", [(2, "p2p"), (2, "mesh"), (3, "ll")])
+def test_reduce_scatter_misaligned_dst_on_some_ranks(gpu, world, engine):
+    """Odd ranks pass a dst that is not 16-B / 8-B aligned, even ranks an
+    aligned one.  The route must not depend on it: before, the
+    misaligned ranks fell back to the int32 allreduce while the others ran the
+    pull-reduce or the mesh kernel -- mismatched barriers."""
+    _run_ipc(world, engine, misalign=True)
+
+
+def _mode_switch_rank(rank, world, port, q, shard_log2):
+    """The mesh engines' kernel across mode switches on one communicator:
+    allreduce <-> reduce-scatter, fp32 <-> bf16, mesh <-> meshw, and a regrow,
+    with exact fixed-point data (rank r's bucket is (r + 1) * b, b a multiple of
+    2^-12 with |b| < 1/2: every partial is exact at k = 20), so every call is
+    checked exactly without the oracle."""
+    try:
+        os.environ["INCCL_ENGINE"] = "mesh"
+        os.environ["INCCL_DEVICE"] = "0"
+        os.environ["INCCL_BOOT_TIMEOUT"] = "120"
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        from container_inc_amd import inccl
+        dev = torch.device("cuda", 0)
+        grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=0)
+        comm = inccl.inccl_communicator_create(grp, 0)
+        ok = []
+        for lg in (shard_log2 - 2, shard_log2):   # the second size regrows the buffers
+            shard = 1 << lg
+            n = world * shard
+            i = torch.arange(n, device=dev, dtype=torch.int64)
+            b = ((i % 4093) - 2046).to(torch.float32) * 2.0 ** -12
+            x = b * float(rank + 1)
+
+            def want_of(dt):   # the exact sum of every rank's bucket as `dt`, rounded once to `dt`
+                acc = torch.zeros(n, device=dev, dtype=torch.float32)
+                for r in range(world):
+                    acc += (b * float(r + 1)).to(dt).float()
+                return acc.to(dt)
+
+            f32, b16 = torch.float32, torch.bfloat16
+            for eng, op, dt in [("mesh", "ar", f32), ("mesh", "rs", f32), ("mesh", "ar", b16), ("mesh", "rs", b16),
+                                ("meshw", "rs", f32), ("meshw", "ar", f32), ("mesh", "rs", f32),
+                                ("meshw", "ar", b16), ("meshw", "rs", b16), ("mesh", "ar", f32)]:
+                comm.set_engine(eng)
+                src = x.to(dt)
+                if op == "ar":
+                    out = (comm.allreduce_f32([src], scale_exp=20, stream=comm.stream) if dt == torch.float32 else
+                           comm.allreduce_bf16([src], out=torch.empty_like(src), scale_exp=20, stream=comm.stream))
+                    want = want_of(dt)
+                else:
+                    out = comm.reduce_scatter([src], scale_exp=20, stream=comm.stream)
+                    want = want_of(dt)[rank * shard:(rank + 1) * shard]
+                torch.cuda.synchronize()
+                ok.append(bool(torch.equal(out, want)))
+            comm.ipc_mem_kind("mesh")
+        comm.barrier()
+        comm.destroy()
+        grp.destroy()
+        q.put((rank, ok, None))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("world,shard_log2", [(2, 16), (3, 14), (4, 22)])
+def test_mesh_mode_switches(gpu, world, shard_log2):
+    """One communicator, the mesh kernel in every mode in turn (CPU model:
+    tests/test_mesh_schedule_model.py); (4, 2^22) is the configuration in
+    which round 5's reduce-scatter route faulted."""
+    _run_mp(world, _mode_switch_rank, shard_log2)
 
 
 def test_calls_on_alternating_streams(gpu, orc):

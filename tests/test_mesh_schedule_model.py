@@ -8,15 +8,16 @@ pos) % W), pos == W reduce(s - lag), else gather(s - 2 lag, (me + pos - W) % W)
 -- the kernel's decomposition.  A push writes the rank's partial of chunk c
 into rank j's inbox slot and then raises j's arrival flag; a reduce waits for
 every rank's arrival flag of its chunk, reads the W inbox slots, writes its
-result (own_res, or dst in reduce-scatter mode) and raises its ready flag at
-every rank; a gather waits for rank j's ready flag and (allreduce) reads rank
-j's result chunk.  Flags hold the call's epoch; a wait is `flag >= epoch`.  The
+result (own_res) and raises its ready flag at every rank; a gather waits for
+rank j's ready flag and reads rank j's result chunk (reduce-scatter: only its
+own, j == me; the other gathers only wait).  Flags hold the call's epoch; a wait is `flag >= epoch`.  The
 last workgroup to retire resets the ticket counter and publishes the epoch;
 a rank's next call starts only after every workgroup of its previous call
 retired (stream order).
 
 The model interleaves the workgroups of every rank at random (sequentially
-consistent memory: it checks the schedule's logic, not the memory model) and
+consistent memory: it checks the schedule's logic; the memory model is
+tests/test_mesh_weak_memory_model.py's) and
 asserts, over many seeds, shapes and both modes:
   * no deadlock, with every rank's workgroups co-resident (the kernel's launch
     assumption, mesh.c grid sizing);
@@ -101,8 +102,7 @@ def _run(W, G, nchunks, lag, calls, rs, seed):
             for j in range(W):
                 got = rk.inbox.get((j, c))
                 assert got == e, f"rank {rk.me} call {e} reduce chunk {c}: inbox slot {j} holds call {got}"
-            if not rs:
-                rk.res[c] = e
+            rk.res[c] = e   # own_res in every mode (round 6; round 5's reduce-scatter wrote dst)
             rk.reduced[(e, c)] = rk.reduced.get((e, c), 0) + 1
             for j in range(W):
                 ranks[j].ready[(rk.me, c)] = e
@@ -112,7 +112,7 @@ def _run(W, G, nchunks, lag, calls, rs, seed):
             _, c, j = task
             if rk.ready.get((j, c), 0) < e:
                 return False
-            if not rs:
+            if not rs or j == rk.me:   # reduce-scatter: gather(c, me) copies my own result chunk into dst
                 got = ranks[j].res.get(c)
                 assert got == e, f"rank {rk.me} call {e} gather chunk {c} of rank {j}: result of call {got}"
             rk.wgs[w] = "fetch"

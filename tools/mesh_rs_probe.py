@@ -7,6 +7,12 @@ shard's elements differ, and the first differing chunks (the mesh engines'
 chunk size), for the first call and for a later one.
 
     python tools/mesh_rs_probe.py W engine [--pre16] shard_log2 [shard_log2 ...]
+    python tools/mesh_rs_probe.py --rank R PORT W engine [--pre16] shard_log2 ...
+
+The --rank form runs ONE rank in this process and prints its JSON line, so
+that each rank can be started under its own rocprofv3 from a shell
+(tools/gpu_mesh_rs.sh): no launcher that forks after the profiler initialised
+the GPU.
 
 --pre16: a bf16 allreduce of the same bucket size on the same communicator
 before the reduce-scatter calls (the bench's order: its bf16 / f16 phases run
@@ -26,7 +32,7 @@ def _rank(rank, world, port, engine, logs, pre16, q):
         os.environ["INCCL_ENGINE"] = engine
         os.environ["INCCL_DEVICE"] = "0"
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
-        os.environ["INCCL_MESH_RS"] = "1"   # the mesh engines' own route is opt-in
+        os.environ["INCCL_MESH_RS"] = "1"   # the mesh engines' own route (the default since round 6)
         sys.path.insert(0, ROOT)
         import torch
         from container_inc_amd import inccl
@@ -68,7 +74,20 @@ def _rank(rank, world, port, engine, logs, pre16, q):
         q.put((rank, None, repr(e)))
 
 
+class _Print:
+    def put(self, item):
+        rank, res, err = item
+        print(json.dumps({"rank": rank, "rows": res, "error": err}), flush=True)
+
+
 def main():
+    if sys.argv[1] == "--rank":
+        rank, port, world, engine = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+        rest = sys.argv[6:]
+        pre16 = "--pre16" in rest
+        logs = [int(v) for v in rest if v != "--pre16"] or [18, 23]
+        _rank(rank, world, port, engine, logs, pre16, _Print())
+        return
     world, engine = int(sys.argv[1]), sys.argv[2]
     pre16 = "--pre16" in sys.argv[3:]
     logs = [int(v) for v in sys.argv[3:] if v != "--pre16"] or [18, 23]
