@@ -1014,6 +1014,9 @@ def n1_sizes(dev, R: int, k: int, sizes=SIZES_BYTES) -> list:
       prepared_us  the same bucket through a prepared op (inccl_op_run: the
                    arguments bound once, one ctypes argument per call)
       graph1_us    a hipGraph holding one call, replayed per call
+      graph20_us   a hipGraph holding 20 calls, host time per call over its
+                   back-to-back replays (as the N > 1 sweep's graph_us,
+                   graph_replay_us): the launch cost a captured step pays
       kernel_us    a hipGraph holding `per` calls, per call: the device rate of
                    back-to-back kernels (HIP events on the replay stream)
       GBps_buckets R * bucket bytes / eager_us (the call); GBps_buckets_prepared
@@ -1039,7 +1042,7 @@ def n1_sizes(dev, R: int, k: int, sizes=SIZES_BYTES) -> list:
         op.destroy()
         per = max(10, min(100, iters // 4))
         res = {}
-        for cnt in (1, per):
+        for tag, cnt in (("g1", 1), ("g20", 20), ("dev", per)):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=st):
                 for _ in range(cnt):
@@ -1047,8 +1050,8 @@ def n1_sizes(dev, R: int, k: int, sizes=SIZES_BYTES) -> list:
             reps = max(4, iters // cnt)
             with torch.cuda.stream(st):   # replay() launches on the current stream
                 g.replay()
-                if cnt == 1:
-                    res[cnt] = host_us_per_call(g.replay, reps)
+                if tag != "dev":
+                    res[tag] = host_us_per_call(g.replay, reps) / cnt
                 else:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(st)
@@ -1056,13 +1059,14 @@ def n1_sizes(dev, R: int, k: int, sizes=SIZES_BYTES) -> list:
                         g.replay()
                     e1.record(st)
                     torch.cuda.synchronize()
-                    res[cnt] = e0.elapsed_time(e1) * 1e3 / (reps * cnt)
+                    res[tag] = e0.elapsed_time(e1) * 1e3 / (reps * cnt)
             del g
-        kernel_us = res[per]
+        kernel_us = res["dev"]
         alg = (R + 1) * 4 * n
         rows.append({"bucket_bytes": b, "bucket_mib": round(b / (1 << 20), 6),
                      "eager_us": round(eager, 2), "prepared_us": round(prepared, 2),
-                     "graph1_us": round(res[1], 2), "kernel_us": round(kernel_us, 2),
+                     "graph1_us": round(res["g1"], 2), "graph20_us": round(res["g20"], 2),
+                     "kernel_us": round(kernel_us, 2),
                      "GBps_buckets": round(R * b / (eager * 1e-6) / 1e9, 1),
                      "GBps_buckets_prepared": round(R * b / (prepared * 1e-6) / 1e9, 1),
                      "GBps_buckets_kernel": round(R * b / (kernel_us * 1e-6) / 1e9, 1),

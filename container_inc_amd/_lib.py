@@ -69,6 +69,8 @@ SIGNATURES = {
     "inccl_comm_clear_error": (_I, [_P]),
     "inccl_comm_set_average": (_I, [_P, _I]),
     "inccl_comm_set_nonfinite": (_I, [_P, _I]),
+    "inccl_comm_set_stage_timing": (_I, [_P, _I]),
+    "inccl_comm_stage_times": (_I, [_P, _P, _I, _P]),
     "inccl_reduce_scatter_f32": (_I, [_P, _P, _I, _P, _SZ, _I, _P]),
     "inccl_reduce_scatter_bf16": (_I, [_P, _P, _I, _P, _SZ, _I, _P]),
     "inccl_reduce_scatter_f16": (_I, [_P, _P, _I, _P, _SZ, _I, _P]),

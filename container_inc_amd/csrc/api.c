@@ -144,8 +144,66 @@ static int ws_leave(struct inccl_communicator *c, int rc)
     do {                                                            \
         if (!(c)) return (call);                                    \
         (c)->ws_claimed = 0;                                        \
+        (c)->stage_cnt = 0;                                         \
         return ws_leave((c), (call));                               \
     } while (0)
+
+/* ---- per-stage timing (inccl_comm_set_stage_timing) ----
+ * stage_open records a begin event on the stage's stream and returns its slot
+ * (-1: timing off, the stream is being captured, or the slots are full);
+ * stage_close records the matching end event.  Failures to record only drop
+ * the sample: timing never changes a call's outcome. */
+static int stage_open(struct inccl_communicator *c, hipStream_t st)
+{
+    if (!c->stage_on || c->stage_cnt >= INCCL_STAGE_SLOTS) return -1;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return -1;
+    const int i = c->stage_cnt;
+    for (int e = 2 * i; e < 2 * i + 2; ++e)
+        if (!c->stage_ev[e] && hipEventCreate(&c->stage_ev[e]) != hipSuccess) return -1;
+    if (hipEventRecord(c->stage_ev[2 * i], st) != hipSuccess) return -1;
+    c->stage_kind[i] = -1;   /* closed by stage_close */
+    c->stage_cnt = i + 1;
+    return i;
+}
+
+static void stage_close(struct inccl_communicator *c, int i, hipStream_t st, int kind)
+{
+    if (i < 0) return;
+    if (hipEventRecord(c->stage_ev[2 * i + 1], st) == hipSuccess) c->stage_kind[i] = kind;
+}
+
+int inccl_comm_set_stage_timing(struct inccl_communicator *comm, int on)
+{
+    if (!comm) return inccl_set_error(INCCL_ERR_ARG, "communicator is NULL");
+    comm->stage_on = on != 0;
+    comm->stage_cnt = 0;
+    return 0;
+}
+
+int inccl_comm_stage_times(struct inccl_communicator *comm, double *us, int kinds, double *wall_us)
+{
+    if (!comm || (!us && kinds > 0) || kinds < 0) return inccl_set_error(INCCL_ERR_ARG, "bad stage_times args");
+    for (int k = 0; k < kinds; ++k) us[k] = 0.0;
+    if (wall_us) *wall_us = 0.0;
+    int n = 0;
+    double t0 = 0.0, t1 = 0.0;
+    /* every event against the first begin event: stage 0 opens on the call's
+     * stream before any other stage starts (the side stream waits for it) */
+    for (int i = 0; i < comm->stage_cnt; ++i) {
+        if (comm->stage_kind[i] < 0) continue;
+        INCCL_HIP(hipEventSynchronize(comm->stage_ev[2 * i + 1]));
+        float b = 0.f, e = 0.f;
+        INCCL_HIP(hipEventElapsedTime(&b, comm->stage_ev[0], comm->stage_ev[2 * i]));
+        INCCL_HIP(hipEventElapsedTime(&e, comm->stage_ev[0], comm->stage_ev[2 * i + 1]));
+        if (comm->stage_kind[i] < kinds) us[comm->stage_kind[i]] += ((double)e - (double)b) * 1e3;
+        if (n == 0 || b < t0) t0 = b;
+        if (n == 0 || e > t1) t1 = e;
+        ++n;
+    }
+    if (wall_us) *wall_us = (t1 - t0) * 1e3;
+    return n;
+}
 
 /* ---- prepared stream ops ---- */
 struct inccl_op {
@@ -650,6 +708,8 @@ int inccl_communicator_destroy(struct inccl_communicator *comm)
     if (comm->receive_payload) hipHostFree(comm->receive_payload);
     for (int i = 0; i < 10; ++i)
         if (comm->ev[i]) hipEventDestroy(comm->ev[i]);
+    for (int i = 0; i < 2 * INCCL_STAGE_SLOTS; ++i)
+        if (comm->stage_ev[i]) hipEventDestroy(comm->stage_ev[i]);
     if (comm->copy_streams[0]) hipStreamDestroy(comm->copy_streams[0]);
     if (comm->copy_streams[1]) hipStreamDestroy(comm->copy_streams[1]);
     if (comm->side_stream) hipStreamDestroy(comm->side_stream);
@@ -854,22 +914,34 @@ static int allreduce_piece(struct inccl_communicator *c, const float *const *src
     const int W = c->group->world_size, me = c->group->rank;
     const size_t shard = inccl_shard_elems(n, W), total = shard * (size_t)W;
     int32_t *qsend = ws, *qrecv = ws + total;
+    int si = stage_open(c, st);
     int rc = kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_Q32, (const void *const *)srcs, R, qsend, n, k, amax,
                                  scale_R, st));
     if (rc) return rc;
     if (total > n) INCCL_HIP(hipMemsetAsync(qsend + n, 0, (total - n) * sizeof(int32_t), st));
+    stage_close(c, si, st, INCCL_STAGE_QUANT);
+    si = stage_open(c, st);
     rc = inccl_tp_reduce_scatter_q32(c, qsend, qrecv, shard, st);
     if (rc) return rc;
+    stage_close(c, si, st, INCCL_STAGE_RS);
     const size_t lo = (size_t)me * shard;
     const int in_place = (total == n);
     float *gather = in_place ? dst : fws;
     const void *s1[1] = {qrecv};
+    si = stage_open(c, st);
     rc = kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, gather + lo, shard, k, amax, scale_R,
                                c->out_shift, st));
     if (rc) return rc;
+    stage_close(c, si, st, INCCL_STAGE_DEQUANT);
+    si = stage_open(c, st);
     rc = inccl_tp_all_gather_f32(c, gather + lo, gather, shard, st);
     if (rc) return rc;
-    if (!in_place) INCCL_HIP(hipMemcpyAsync(dst, fws, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    stage_close(c, si, st, INCCL_STAGE_AG);
+    if (!in_place) {
+        si = stage_open(c, st);
+        INCCL_HIP(hipMemcpyAsync(dst, fws, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+        stage_close(c, si, st, INCCL_STAGE_COPY);
+    }
     return 0;
 }
 
@@ -967,10 +1039,15 @@ static int allreduce_f32_body(struct inccl_communicator *c, const float *const *
      * fallback to it when RCCL is unavailable) never routes to ll by itself. */
     if ((c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH) &&
         c->group->transport == INCCL_TRANSPORT_RCCL) {
+        const int si = stage_open(c, st);
         if (c->engine == INCCL_ENGINE_LL && n <= c->ll_max_bytes / sizeof(float) && W > 1)
-            return inccl_ll_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, 0, 0, st);
-        if (c->engine == INCCL_ENGINE_MESH) return inccl_mesh_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
-        return inccl_p2p_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+            rc = inccl_ll_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, 0, 0, st);
+        else if (c->engine == INCCL_ENGINE_MESH)
+            rc = inccl_mesh_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+        else
+            rc = inccl_p2p_piece(c, srcs_dev, R, dst_dev, n, k, amax, scale_R, st);
+        if (!rc) stage_close(c, si, st, INCCL_STAGE_IPC);
+        return rc;
     }
     /* RCCL's own allreduce on the int32 partials: quant + local sum -> in-place
      * ncclAllReduce(int32, sum) -> dequantise (the switch aggregate inside RCCL).
@@ -982,14 +1059,21 @@ static int allreduce_f32_body(struct inccl_communicator *c, const float *const *
         rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, n * sizeof(int32_t));
         if (rc) return rc;
         int32_t *q = (int32_t *)c->d_q32;
+        int si = stage_open(c, st);
         rc = kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_Q32, (const void *const *)srcs_dev, R, q, n, k, amax,
                                  scale_R, st));
         if (rc) return rc;
+        stage_close(c, si, st, INCCL_STAGE_QUANT);
+        si = stage_open(c, st);
         rc = inccl_tp_allreduce_q32(c, q, q, n, st);
         if (rc) return rc;
+        stage_close(c, si, st, INCCL_STAGE_AR);
+        si = stage_open(c, st);
         const void *s1[1] = {q};
-        return kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, dst_dev, n, k, amax, scale_R,
-                                     c->out_shift, st));
+        rc = kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, dst_dev, n, k, amax, scale_R,
+                                   c->out_shift, st));
+        stage_close(c, si, st, INCCL_STAGE_DEQUANT);
+        return rc;
     }
     if (c->engine == INCCL_ENGINE_A2A && c->group->transport == INCCL_TRANSPORT_RCCL) {
         if (W > INCCL_MAX_LOCAL_INPUTS)
@@ -1038,6 +1122,9 @@ static int allreduce_f32_body(struct inccl_communicator *c, const float *const *
     /* pipelined: quantise chunk i+1 on the side stream while chunk i's
      * collectives run on `st` (RCCL kernels and the HBM-bound quantiser share
      * the chip).  ev[0]: side stream caught up with st's prior work. */
+    /* (stage timing: a first, empty stage on st anchors the clock before the
+     * side stream starts) */
+    stage_close(c, stage_open(c, st), st, INCCL_STAGE_KINDS);
     INCCL_HIP(hipEventRecord(c->ev[0], st));
     INCCL_HIP(hipStreamWaitEvent(c->side_stream, c->ev[0], 0));
     for (size_t off = 0; off < n; off += per) {
@@ -1045,25 +1132,36 @@ static int allreduce_f32_body(struct inccl_communicator *c, const float *const *
         const size_t shard = inccl_shard_elems(cnt, W), total = shard * (size_t)W;
         for (int r = 0; r < R; ++r) sub[r] = srcs_dev[r] + off;
         int32_t *qsend = ws, *qrecv = ws + total;
+        int si = stage_open(c, c->side_stream);
         rc = kerr(inccl_k_stream(INCCL_KIND_F32, INCCL_KIND_Q32, (const void *const *)sub, R, qsend, cnt, k, amax,
                                  scale_R, c->side_stream));
         if (rc) return rc;
         if (total > cnt) INCCL_HIP(hipMemsetAsync(qsend + cnt, 0, (total - cnt) * sizeof(int32_t), c->side_stream));
+        stage_close(c, si, c->side_stream, INCCL_STAGE_QUANT);
         INCCL_HIP(hipEventRecord(c->ev[1], c->side_stream));
         INCCL_HIP(hipStreamWaitEvent(st, c->ev[1], 0));
+        si = stage_open(c, st);
         rc = inccl_tp_reduce_scatter_q32(c, qsend, qrecv, shard, st);
         if (rc) return rc;
+        stage_close(c, si, st, INCCL_STAGE_RS);
         const int in_place = (total == cnt);
         float *gather = in_place ? dst_dev + off : (float *)c->d_f32;
         const size_t lo = (size_t)c->group->rank * shard;
         const void *s1[1] = {qrecv};
+        si = stage_open(c, st);
         rc = kerr(inccl_k_stream_s(INCCL_KIND_Q32, INCCL_KIND_F32, s1, 1, gather + lo, shard, k, amax, scale_R,
                                    c->out_shift, st));
         if (rc) return rc;
+        stage_close(c, si, st, INCCL_STAGE_DEQUANT);
+        si = stage_open(c, st);
         rc = inccl_tp_all_gather_f32(c, gather + lo, gather, shard, st);
         if (rc) return rc;
-        if (!in_place)
+        stage_close(c, si, st, INCCL_STAGE_AG);
+        if (!in_place) {
+            si = stage_open(c, st);
             INCCL_HIP(hipMemcpyAsync(dst_dev + off, c->d_f32, cnt * sizeof(float), hipMemcpyDeviceToDevice, st));
+            stage_close(c, si, st, INCCL_STAGE_COPY);
+        }
         ws += total + shard;
     }
     /* `st` already waited on every side-stream chunk */
@@ -1226,12 +1324,19 @@ static int reduce_scatter_body(struct inccl_communicator *c, int kind, const voi
         rc = inccl_ensure_dev(&c->d_q32, &c->d_q32_bytes, (n + shard) * sizeof(int32_t));
         if (rc) return rc;
         int32_t *qsend = (int32_t *)c->d_q32, *qrecv = qsend + n;
+        int si = stage_open(c, st);
         rc = kerr(inccl_k_stream(kind, INCCL_KIND_Q32, srcs, R, qsend, n, k, amax, scale_R, st));
         if (rc) return rc;
+        stage_close(c, si, st, INCCL_STAGE_QUANT);
+        si = stage_open(c, st);
         rc = inccl_tp_reduce_scatter_q32(c, qsend, qrecv, shard, st);
         if (rc) return rc;
+        stage_close(c, si, st, INCCL_STAGE_RS);
+        si = stage_open(c, st);
         const void *s1[1] = {qrecv};
-        return kerr(inccl_k_stream_s(INCCL_KIND_Q32, kind, s1, 1, dst, shard, k, amax, scale_R, c->out_shift, st));
+        rc = kerr(inccl_k_stream_s(INCCL_KIND_Q32, kind, s1, 1, dst, shard, k, amax, scale_R, c->out_shift, st));
+        stage_close(c, si, st, INCCL_STAGE_DEQUANT);
+        return rc;
     }
     const int ipc = c->engine == INCCL_ENGINE_P2P || c->engine == INCCL_ENGINE_LL || c->engine == INCCL_ENGINE_MESH;
     /* Every route below is chosen from what all ranks share (engine, n, W and
@@ -1256,6 +1361,7 @@ static int reduce_scatter_body(struct inccl_communicator *c, int kind, const voi
          * reduce-scatter route").  The ll engine's one kernel for a small fp32
          * bucket: every rank's quads published with a flag, this rank's shard
          * summed and dequantised.  Otherwise the p2p pull-reduce. */
+        const int si = stage_open(c, st);
         if (mesh_route)
             rc = inccl_mesh_reduce_scatter(c, kind, srcs, R, out, n, k, amax, scale_R, st);
         else if (kind == INCCL_KIND_F32 && c->engine == INCCL_ENGINE_LL && n <= c->ll_max_bytes / sizeof(float))
@@ -1263,7 +1369,9 @@ static int reduce_scatter_body(struct inccl_communicator *c, int kind, const voi
                                 (size_t)me * shard, shard, st);
         else
             rc = inccl_p2p_reduce_scatter(c, kind, srcs, R, out, n, k, amax, scale_R, st);
-        if (rc || out == dst) return rc;
+        if (rc) return rc;
+        stage_close(c, si, st, INCCL_STAGE_IPC);
+        if (out == dst) return 0;
         INCCL_HIP(hipMemcpyAsync(dst, out, shard * es, hipMemcpyDeviceToDevice, st));
         return 0;
     }

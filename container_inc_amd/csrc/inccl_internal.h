@@ -6,6 +6,7 @@
  * pinned host staging buffers (the registered MRs) and device workspaces. */
 #ifndef INCCL_INTERNAL_H
 #define INCCL_INTERNAL_H
+#define INCCL_STAGE_SLOTS 64   /* stages recorded per call (16 chunks x 4 stages) */
 
 #include <pthread.h>
 #include <stddef.h>
@@ -129,6 +130,10 @@ struct inccl_communicator {
     struct inccl_d2h_worker *d2h;  /* issues pageable D2H copies beside the H2Ds (hostdma.c) */
     hipEvent_t ev[10];           /* [8]: p2p ordering across caller streams; [9]: workspace ordering
                                   * across caller streams (ws_last_stream) */
+    /* per-stage timing (inccl_comm_set_stage_timing): begin/end timing events
+     * per recorded stage of the last call, ev[2*i] / ev[2*i+1] */
+    int stage_on, stage_cnt, stage_kind[INCCL_STAGE_SLOTS];
+    hipEvent_t stage_ev[2 * INCCL_STAGE_SLOTS];
     hipStream_t ws_last_stream;  /* the stream of the last call that used the shared workspaces */
     hipStream_t ws_stream;       /* this call's stream, once it claimed them (inccl_ws_claim) */
     int ws_claimed, ws_capturing;

@@ -363,6 +363,32 @@ class Communicator:
             check(rc, "inccl_comm_clear_error")
         return rc == 1
 
+    STAGE_NAMES = ("quant", "reduce_scatter", "dequant", "all_gather", "copy", "allreduce", "ipc")
+
+    def set_stage_timing(self, on: bool = True) -> None:
+        """Per-stage HIP-event timing of this rank's later non-captured calls
+        (include/inccl_amd.h inccl_comm_set_stage_timing; diagnostics, never in
+        a timed loop)."""
+        check(load().inccl_comm_set_stage_timing(self.handle, 1 if on else 0), "inccl_comm_set_stage_timing")
+
+    def stage_times(self) -> dict:
+        """The last call's stages: {stage: us summed over its chunks, ...,
+        "wall_us": first start to last end, "overlap_us": sum - wall,
+        "stages": how many were recorded}; synchronises their events."""
+        import ctypes
+        kinds = len(self.STAGE_NAMES)
+        us = (ctypes.c_double * kinds)()
+        wall = ctypes.c_double(0.0)
+        n = load().inccl_comm_stage_times(self.handle, ctypes.cast(us, ctypes.c_void_p), kinds,
+                                          ctypes.cast(ctypes.pointer(wall), ctypes.c_void_p))
+        if n < 0:
+            check(n, "inccl_comm_stage_times")
+        out = {name: round(us[i], 2) for i, name in enumerate(self.STAGE_NAMES) if us[i] > 0.0}
+        out["wall_us"] = round(wall.value, 2)
+        out["overlap_us"] = round(sum(us[i] for i in range(kinds)) - wall.value, 2)
+        out["stages"] = n
+        return out
+
     def set_average(self, on: bool = True) -> None:
         """Results of allreduce_f32 / _bf16 become the mean over ranks (power-of-two
         worlds; raises IncclError otherwise).  Bit-identical to sum / W."""

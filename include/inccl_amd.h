@@ -221,6 +221,28 @@ int inccl_comm_set_average(struct inccl_communicator *comm, int on);
 #define INCCL_NONFINITE_NAN 1
 int inccl_comm_set_nonfinite(struct inccl_communicator *comm, int mode);
 
+/* Per-stage timing of this rank's calls (diagnostics; off by default).  on != 0:
+ * every later non-captured allreduce / reduce-scatter records a pair of HIP
+ * timing events around each of its stages, on the stream the stage runs on
+ * (about 2 x 3 us of GPU time per stage: never in a timed loop).  After a call,
+ * inccl_comm_stage_times synchronises those events and fills us[kind] with the
+ * summed microseconds of each stage kind (us[] of INCCL_STAGE_KINDS entries,
+ * chunks of a pipelined call added up) and *wall_us with the first stage's start
+ * to the last one's end; sum(us) - wall is the time the stages overlapped (the
+ * pipelined rccl path quantises chunk i+1 beside chunk i's collectives).
+ * Returns the number of stages recorded (0: none, e.g. timing off or a captured
+ * call), negative on error. */
+#define INCCL_STAGE_QUANT 0    /* quantise + local sum (+ the tail memset) */
+#define INCCL_STAGE_RS 1       /* int32 reduce-scatter (ncclReduceScatter, or the in-process one) */
+#define INCCL_STAGE_DEQUANT 2  /* dequantise the own shard */
+#define INCCL_STAGE_AG 3       /* all-gather of the result shards (ncclAllGather) */
+#define INCCL_STAGE_COPY 4     /* copy out of a workspace (ragged or misaligned buckets) */
+#define INCCL_STAGE_AR 5       /* int32 allreduce (ncclAllReduce: "ar" engine, small buckets) */
+#define INCCL_STAGE_IPC 6      /* an IPC engine's whole exchange (p2p / ll / mesh kernels) */
+#define INCCL_STAGE_KINDS 7
+int inccl_comm_set_stage_timing(struct inccl_communicator *comm, int on);
+int inccl_comm_stage_times(struct inccl_communicator *comm, double *us, int kinds, double *wall_us);
+
 /* Device-resident fp32 allreduce of R local buckets per rank:
  *   dst = dequant( sum over ranks, sum over r<R  quant(srcs[r]) )
  * world == 1: one fused kernel.  world > 1: quant+local sum -> reduce-scatter

@@ -17,6 +17,11 @@ timeout -k 10 600 python -u bench.py --steps 50 --warmup 10 --json-out gpurun_ou
 echo "bench ok"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-extras --json-out gpurun_out/bench_profiled.json > gpurun_out/prof.log 2>&1 || { echo prof failed; tail -20 gpurun_out/prof.log; exit 6; }
 grep -h k_stream gpurun_out/prof/run_kernel_stats.csv | cut -c1-200
+# the bench's frac_cold (cold_run: four rotated input/output sets, 3 GiB, beyond
+# the Infinity Cache) reproduced from a kernel trace: the same rotation, so
+# 805,306,368 B / k_stream_vec's average duration / 8 TB/s is frac_cold
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cold -o run --output-format csv -- python3 tools/kernel_probe.py --kernel fused --R 2 --mib 256 --sets 4 --iters 40 > gpurun_out/prof_cold.log 2>&1 || { echo prof cold failed; tail -20 gpurun_out/prof_cold.log; exit 6; }
+grep -h k_stream gpurun_out/prof_cold/run_kernel_stats.csv | cut -c1-200
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bf16 -o run --output-format csv -- python3 tools/kernel_probe.py --kernel bf16 --R 2 --mib 256 --iters 50 > gpurun_out/prof_bf16.log 2>&1 || { echo prof bf16 failed; tail -20 gpurun_out/prof_bf16.log; exit 6; }
 for k in fused quant_sum bf16 f16; do
   for c in FETCH_SIZE WRITE_SIZE; do
