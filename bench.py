@@ -475,6 +475,32 @@ def agree(values, world: int):
     return v.tolist()
 
 
+def stage_probe(comm, xs, out, k: int, chunks: int, st, world: int, calls: int = 3) -> dict:
+    """Where one allreduce's time goes (N > 1): `calls` untimed calls with
+    per-stage HIP events (inccl_comm_set_stage_timing), after the timed ones;
+    per stage the mean microseconds over the calls, max over ranks, plus the
+    call's wall span and the overlap between stages (sum - wall: the pipelined
+    rccl path quantises chunk i+1 beside chunk i's collectives).  Stages:
+    quant (+ local sum), reduce_scatter (int32), dequant, all_gather, copy,
+    allreduce (the "ar" engine's ncclAllReduce), ipc (an IPC engine's whole
+    exchange: its kernels do every stage)."""
+    import torch
+    names = list(comm.STAGE_NAMES) + ["wall_us", "overlap_us"]
+    acc = {key: 0.0 for key in names}
+    try:
+        comm.set_stage_timing(True)
+        for _ in range(calls):
+            comm.allreduce_f32(xs, out=out, scale_exp=k, chunks=chunks, stream=st.cuda_stream)
+            torch.cuda.synchronize()
+            t = comm.stage_times()
+            for key in names:
+                acc[key] += t.get(key, 0.0) / calls
+    finally:
+        comm.set_stage_timing(False)
+    v = agree([acc[key] for key in names], world)
+    return {key: round(x, 2) for key, x in zip(names, v) if x != 0.0 or key == "overlap_us"}
+
+
 def graph_replay_us(comm, xs, out, k: int, st, world: int, want, per: int = 20, reps: int = 10):
     """Latency floor of a small bucket: `per` calls captured in one hipGraph
     (torch.cuda.CUDAGraph around the C-ABI call), replayed `reps` times; µs per
@@ -566,6 +592,10 @@ def size_sweep(comm, dev, R: int, k: int, rank: int, world: int, soft_budget_s: 
                 refs = (got[0], got[1])
             del got
         for eng in engines:
+            if agree([time.monotonic() - T_START], world)[0] > soft_budget_s:   # the budget holds per engine too
+                rows.append({"bucket_bytes": b, "engine": eng,
+                             "skipped": f"run past {soft_budget_s:.0f} s from process start"})
+                continue
             set_stage(f"sweep {b} B engine {eng}")
             ok, dt, dtp, same, got = 1, float("inf"), float("inf"), False, None
             try:
@@ -1467,6 +1497,12 @@ def main():
             except Exception as e:  # noqa: BLE001
                 print(f"rank {rank}: engine {eng} chunks {ch} {env} failed: {e}", file=sys.stderr, flush=True)
                 ok, err = 0, str(e)[:400]
+            stages = None
+            if agree([0.0 if ok else 1.0], world)[0] == 0.0:   # every rank probes, or none does
+                try:
+                    stages = stage_probe(comm, srcs, out, k, ch, stream, world)
+                except Exception as e:  # noqa: BLE001
+                    stages = {"error": str(e)[:200]}
             for key in env:
                 os.environ.pop(key, None)
             v = agree([dt if ok else float("inf"), 0.0 if ok else 1.0, 0.0 if same else 1.0], world)
@@ -1487,6 +1523,7 @@ def main():
                            "bit_identical": v[1] == 0.0 and v[2] == 0.0, "verified": good,
                            "oracle_mismatches": par["mismatches"] if par else None,
                            "ms": round(v[0] * 1e3, 3) if v[1] == 0.0 else None,
+                           "stages_us": stages,
                            # rank 0's error text (RCCL's own reason, ncclGetLastError, included)
                            **({"error": err} if err else {})})
             if good and (best is None or v[0] < best[0]):
@@ -1555,10 +1592,15 @@ def main():
         step()
         torch.cuda.synchronize()
         parity = oracle_check(srcs, out, oracle_lanes(n, world, ch, 1 << 20), k, rank, world)
+        stages = None
+        if world > 1:   # after the timed steps: where a step's time goes, per stage
+            set_stage(f"stage timing of the timed engine {eng}")
+            stages = stage_probe(comm, srcs, out, k, ch, stream, world)
         for key in env:
             os.environ.pop(key, None)
         return {"engine": eng if world > 1 else "fused", "chunks": ch, "env": env, "ms_per_step": wall * 1e3 / a.steps,
-                "settle_steps": settle_steps, "dev_ms": dev_ms, "verified": verified, "parity": parity}
+                "settle_steps": settle_steps, "dev_ms": dev_ms, "verified": verified, "parity": parity,
+                "stages": stages}
 
     # dominant kernel alone: fused (N=1) or quant + local sum (N>1), HIP events
     # on its stream; timed once, right after the first headline measurement
@@ -1670,6 +1712,9 @@ def main():
             res["roofline_cold"] = kinfo["cold"]
         if world > 1:
             res["roofline_hbm_kernel"] = kinfo["hbm"]
+            # per-stage microseconds of one step of the headline engine (HIP events
+            # around each stage, untimed calls after the timed ones; stage_probe)
+            res["stages_us"] = m["stages"]
             res["verified_vs_reference_engine"] = m["verified"]
             # nccl-tests convention (BASELINE config 4): algbw = one rank's bucket
             # bytes / step time; busbw = algbw * 2(W-1)/W, the per-GPU link traffic
@@ -1717,7 +1762,13 @@ def main():
 
     measured = []   # (measurement, line) per headline measurement, in order
     PHASES["startup"] = round(time.monotonic() - T_START, 1)
-    sweep_soft = float(os.environ.get("INCCL_BENCH_SWEEP_SOFT", "300"))
+    # time budgets from process start (agreed over ranks): the size sweeps start
+    # no size -- and no engine of a size -- past sweep_soft, so that the bf16,
+    # f16, reduce_scatter and host_e2e keys, which start until extra_soft, are
+    # reached inside the watchdog's budget (INCCL_BENCH_BUDGET, 480 s) even when
+    # every call is slow (the one-GPU N-rank rehearsal)
+    sweep_soft = float(os.environ.get("INCCL_BENCH_SWEEP_SOFT", "180"))
+    extra_soft = float(os.environ.get("INCCL_BENCH_EXTRA_SOFT", "400"))
     sweep_refs = {}   # bucket bytes -> the sweep's reference engine (pass 1), for pass 2
 
     def sweep_pass(name, want):
@@ -1816,25 +1867,25 @@ def main():
             time.sleep(1e9)
         sweep_pass("sweep_other", lambda eng: eng != "rccl")
         with Phase("bf16"):
-            if agree([time.monotonic() - T_START], world)[0] <= sweep_soft:
+            if agree([time.monotonic() - T_START], world)[0] <= extra_soft:
                 try:
                     res["bf16"] = bf16_engines(comm, dev, R, rank, world)
                 except Exception as e:  # noqa: BLE001
                     print(f"rank {rank}: bf16 key failed: {e!r}", file=sys.stderr, flush=True)
                     res["bf16"] = {"error": repr(e)}
             else:
-                res["bf16"] = {"skipped": f"run past {sweep_soft:.0f} s from process start"}
+                res["bf16"] = {"skipped": f"run past {extra_soft:.0f} s from process start"}
         with Phase("f16"):
-            if agree([time.monotonic() - T_START], world)[0] <= sweep_soft:
+            if agree([time.monotonic() - T_START], world)[0] <= extra_soft:
                 try:
                     res["f16"] = bf16_engines(comm, dev, R, rank, world, fmt="f16")
                 except Exception as e:  # noqa: BLE001
                     print(f"rank {rank}: f16 key failed: {e!r}", file=sys.stderr, flush=True)
                     res["f16"] = {"error": repr(e)}
             else:
-                res["f16"] = {"skipped": f"run past {sweep_soft:.0f} s from process start"}
+                res["f16"] = {"skipped": f"run past {extra_soft:.0f} s from process start"}
         with Phase("reduce_scatter"):
-            if agree([time.monotonic() - T_START], world)[0] <= sweep_soft:
+            if agree([time.monotonic() - T_START], world)[0] <= extra_soft:
                 try:
                     # the mesh engine's row is its persistent kernel's own route (default on)
                     res["reduce_scatter"] = reduce_scatter_engines(comm, dev, R, rank, world,
@@ -1846,12 +1897,12 @@ def main():
                     print(f"rank {rank}: reduce_scatter key failed: {e!r}", file=sys.stderr, flush=True)
                     res["reduce_scatter"] = {"error": repr(e)}
             else:
-                res["reduce_scatter"] = {"skipped": f"run past {sweep_soft:.0f} s from process start"}
+                res["reduce_scatter"] = {"skipped": f"run past {extra_soft:.0f} s from process start"}
         comm.set_engine(chosen[0])
         # north_star: the path starts and ends in host memory -- the end-to-end
         # rate with pinned H2D / D2H, at this N too
         with Phase("host_e2e"):
-            if agree([time.monotonic() - T_START], world)[0] <= sweep_soft:
+            if agree([time.monotonic() - T_START], world)[0] <= extra_soft:
                 set_stage("host_e2e at N > 1")
                 try:
                     res["host_e2e"] = host_e2e(comm, k, world=world)
@@ -1859,7 +1910,7 @@ def main():
                     print(f"rank {rank}: host_e2e failed: {e!r}", file=sys.stderr, flush=True)
                     res["host_e2e"] = {"error": repr(e)}
             else:
-                res["host_e2e"] = {"skipped": f"run past {sweep_soft:.0f} s from process start"}
+                res["host_e2e"] = {"skipped": f"run past {extra_soft:.0f} s from process start"}
     def extra(key, fn):
         """An N = 1 extra key (one process, no collectives): a failure is recorded
         in the key instead of costing the headline line."""

@@ -309,6 +309,7 @@ def _mode_switch_rank(rank, world, port, q, shard_log2):
                                 ("meshw", "ar", b16), ("meshw", "rs", b16), ("mesh", "ar", f32)]:
                 comm.set_engine(eng)
                 src = x.to(dt)
+                torch.cuda.synchronize()   # src is made on torch's stream; the library runs on comm.stream
                 if op == "ar":
                     out = (comm.allreduce_f32([src], scale_exp=20, stream=comm.stream) if dt == torch.float32 else
                            comm.allreduce_bf16([src], out=torch.empty_like(src), scale_exp=20, stream=comm.stream))

@@ -47,6 +47,7 @@ def _rank(rank, world, port, engine, logs, pre16, q):
             b = ((i % 4093) - 2046).to(torch.float32) * 2.0 ** -12
             x = b * float(rank + 1)
             want = (b * float(world * (world + 1) // 2))[rank * shard:(rank + 1) * shard]
+            torch.cuda.synchronize()   # x is made on torch's stream; the calls run on comm.stream
             chunk = None
             if pre16:
                 h = torch.randn(n, device=dev).to(torch.bfloat16)
