@@ -120,13 +120,20 @@ __device__ __forceinline__ int arrive_idx(int j, int c) { return j * INCCL_MESH_
 __device__ __forceinline__ int ready_idx(int j, int c) { return (kMaxR + j) * INCCL_MESH_MAX_CHUNKS + c; }
 
 // Bounded wait for *f >= epoch (serial-number order).  false: timed out or aborted.
-__device__ bool wait_flag(const MeshArgs& a, const uint32_t* f, uint32_t epoch)
+// A timeout reports which wait expired: err[0] = INCCL_MESH_ERR_TIMEOUT | item << 8
+// | peer << 4 | chunk << 16 (item 3: a reduce's arrival flag, 6: a gather's ready
+// flag), err[1] = the flag's last value, err[2] = the epoch waited for.
+__device__ bool wait_flag(const MeshArgs& a, const uint32_t* f, uint32_t epoch, uint32_t item, int peer, int c)
 {
     const uint64_t t0 = now_ticks();
-    while ((int32_t)(ld_sys(f) - epoch) < 0) {
+    uint32_t v;
+    while ((int32_t)((v = ld_sys(f)) - epoch) < 0) {
         if (__hip_atomic_load(a.ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
         if (now_ticks() - t0 > a.timeout_ticks) {
-            __hip_atomic_store(a.err, INCCL_MESH_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.err + 1, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.err + 2, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.err, INCCL_MESH_ERR_TIMEOUT | item << 8 | (uint32_t)peer << 4 | (uint32_t)c << 16,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(a.ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
         }
@@ -266,7 +273,7 @@ template <int E>
 __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
 {
     bool ok = true;
-    if (threadIdx.x < a.W) ok = wait_flag(a, a.own_sig + arrive_idx(threadIdx.x, c), epoch);
+    if (threadIdx.x < a.W) ok = wait_flag(a, a.own_sig + arrive_idx(threadIdx.x, c), epoch, 3, threadIdx.x, c);
     if (!__syncthreads_and(ok)) return false;
     const int64_t nq = chunk_len(a, c) >> 2;
     const uint32_t bytes = (uint32_t)(nq * 16);
@@ -361,7 +368,7 @@ __device__ bool do_reduce(const MeshArgs& a, int c, uint32_t epoch, float inv)
 __device__ bool do_gather(const MeshArgs& a, int c, int j, uint32_t epoch)
 {
     bool ok = true;
-    if (threadIdx.x == 0) ok = wait_flag(a, a.own_sig + ready_idx(j, c), epoch);
+    if (threadIdx.x == 0) ok = wait_flag(a, a.own_sig + ready_idx(j, c), epoch, 6, j, c);
     if (!__syncthreads_and(ok)) return false;
     if (a.rs && j != a.me) return true;
     const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;
@@ -411,7 +418,7 @@ __device__ bool do_gather(const MeshArgs& a, int c, int j, uint32_t epoch)
 __device__ bool do_gather16(const MeshArgs& a, int c, int j, uint32_t epoch)
 {
     bool ok = true;
-    if (threadIdx.x == 0) ok = wait_flag(a, a.own_sig + ready_idx(j, c), epoch);
+    if (threadIdx.x == 0) ok = wait_flag(a, a.own_sig + ready_idx(j, c), epoch, 6, j, c);
     if (!__syncthreads_and(ok)) return false;
     if (a.rs && j != a.me) return true;   // reduce-scatter: as do_gather
     const int64_t lo = (int64_t)j * a.shard + (int64_t)c * a.chunk;

@@ -129,9 +129,9 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     c->mesh_buf = c->mesh_reg[0];
     if (e == hipSuccess) e = hipMemset(c->mesh_buf, 0, MESH_DATA_OFFSET);   /* flags + counters */
     if (e == hipSuccess) e = hipDeviceSynchronize();   /* zeroed before any peer maps it */
-    if (e == hipSuccess) e = hipHostMalloc((void **)&c->mesh_err_host, sizeof(uint32_t), hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&c->mesh_err_host, 4 * sizeof(uint32_t), hipHostMallocMapped);
     if (e == hipSuccess) {
-        *(volatile uint32_t *)c->mesh_err_host = 0;
+        for (int i = 0; i < 4; ++i) ((volatile uint32_t *)c->mesh_err_host)[i] = 0;
         e = hipHostGetDevicePointer((void **)&c->mesh_err_dev, c->mesh_err_host, 0);
     }
     if (e == hipSuccess) e = hipDeviceGetAttribute(&mine.pci_domain, hipDeviceAttributePciDomainID, dev);
@@ -237,8 +237,13 @@ static int mesh_piece(struct inccl_communicator *c, int kind16, const void *cons
     if (err & INCCL_MESH_ERR_BOUNDS)   /* the kernel's per-item bounds check (inccl_mesh.hip inside()) */
         return inccl_set_error(INCCL_ERR_STATE, "mesh: an earlier call stopped at its bounds check (item %u, peer %u; "
                                "results invalid)", (err >> 8) & 0xffu, (err >> 4) & 0xfu);
-    if (err)
-        return inccl_set_error(INCCL_ERR_STATE, "mesh: an earlier call timed out waiting for a peer (results invalid)");
+    if (err) {   /* which wait expired (inccl_mesh.hip wait_flag) */
+        const volatile uint32_t *e4 = (const volatile uint32_t *)c->mesh_err_host;
+        return inccl_set_error(INCCL_ERR_STATE, "mesh: an earlier call timed out waiting for a peer (results invalid; "
+                               "rank %d, %s of chunk %u, peer %u: flag %u, waited for epoch %u)", me,
+                               ((err >> 8) & 0xffu) == 3 ? "reduce's arrival flag" : "gather's ready flag",
+                               err >> 16, (err >> 4) & 0xfu, e4[1], e4[2]);
+    }
     const size_t chunk = mesh_chunk(c, shard);
     const int nchunks = (int)((shard + chunk - 1) / chunk);
     /* a reduce / gather starts `lag` slots after what it waits for.  Default: the

@@ -234,10 +234,10 @@ def _run_mp(world, target, *args, timeout=240):
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
-    for r in range(world):
-        ok, err = res[r]
-        assert err is None, f"rank {r}: {err}"
-        assert all(ok), f"rank {r}: {ok}"
+    errs = {r: res[r][1] for r in range(world) if res[r][1] is not None}
+    assert not errs, f"errors by rank: {errs}"   # every rank's, not only the first
+    bad = {r: res[r][0] for r in range(world) if not all(res[r][0])}
+    assert not bad, f"mismatches by rank: {bad}"
 
 
 def _run_ipc(world, engine, mesh_rs=None, misalign=False):
@@ -278,6 +278,7 @@ def _mode_switch_rank(rank, world, port, q, shard_log2):
     with exact fixed-point data (rank r's bucket is (r + 1) * b, b a multiple of
     2^-12 with |b| < 1/2: every partial is exact at k = 20), so every call is
     checked exactly without the oracle."""
+    where = ["setup"]
     try:
         os.environ["INCCL_ENGINE"] = "mesh"
         os.environ["INCCL_DEVICE"] = "0"
@@ -290,7 +291,7 @@ def _mode_switch_rank(rank, world, port, q, shard_log2):
         grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=0)
         comm = inccl.inccl_communicator_create(grp, 0)
         ok = []
-        for lg in (shard_log2 - 2, shard_log2):   # the second size regrows the buffers
+        for lg in (shard_log2 - 2, shard_log2):   # the second size regrows the buffers (beyond 2^19 elements)
             shard = 1 << lg
             n = world * shard
             i = torch.arange(n, device=dev, dtype=torch.int64)
@@ -304,9 +305,11 @@ def _mode_switch_rank(rank, world, port, q, shard_log2):
                 return acc.to(dt)
 
             f32, b16 = torch.float32, torch.bfloat16
-            for eng, op, dt in [("mesh", "ar", f32), ("mesh", "rs", f32), ("mesh", "ar", b16), ("mesh", "rs", b16),
-                                ("meshw", "rs", f32), ("meshw", "ar", f32), ("mesh", "rs", f32),
-                                ("meshw", "ar", b16), ("meshw", "rs", b16), ("mesh", "ar", f32)]:
+            for step, (eng, op, dt) in enumerate([("mesh", "ar", f32), ("mesh", "rs", f32), ("mesh", "ar", b16),
+                                                  ("mesh", "rs", b16), ("meshw", "rs", f32), ("meshw", "ar", f32),
+                                                  ("mesh", "rs", f32), ("meshw", "ar", b16), ("meshw", "rs", b16),
+                                                  ("mesh", "ar", f32)]):
+                where[0] = f"shard 2^{lg} step {step} ({eng} {op} {dt})"
                 comm.set_engine(eng)
                 src = x.to(dt)
                 torch.cuda.synchronize()   # src is made on torch's stream; the library runs on comm.stream
@@ -325,7 +328,7 @@ def _mode_switch_rank(rank, world, port, q, shard_log2):
         grp.destroy()
         q.put((rank, ok, None))
     except BaseException as e:  # noqa: BLE001
-        q.put((rank, None, repr(e)))
+        q.put((rank, None, f"{where[0]}: {e!r}"))
 
 
 @pytest.mark.parametrize("world,shard_log2", [(2, 16), (3, 14), (4, 22)])

@@ -54,3 +54,34 @@ def test_stage_times_allreduce_local(gpu, orc, chunks):
         assert sum(v for key, v in st.items() if key in inccl.Communicator.STAGE_NAMES) >= 0.5 * st["wall_us"]
         for name in ("quant", "reduce_scatter", "dequant"):
             assert st_rs.get(name, 0.0) > 0.0, (name, st_rs)
+
+
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_stage_times_rccl_world1(gpu, orc, monkeypatch, chunks):
+    """The rccl engine's own stages around real RCCL collectives (world 1, the
+    sharded route forced: ncclReduceScatter and ncclAllGather are launched)."""
+    import torch
+    from container_inc_amd import inccl
+    monkeypatch.setenv("INCCL_FORCE_RCCL", "1")
+    monkeypatch.setenv("INCCL_FORCE_SHARDED", "1")
+    monkeypatch.setenv("INCCL_MASTER_PORT", "0")
+    grp = inccl.inccl_group_create(1, 0, "127.0.0.1")
+    comm = inccl.inccl_communicator_create(grp, 0)
+    comm.set_engine("rccl")
+    n, k = 1 << 22, 25
+    rng = np.random.default_rng(5 + chunks)
+    hs = [rng.standard_normal(n).astype(np.float32) for _ in range(2)]
+    xs = [torch.from_numpy(h).to(gpu) for h in hs]
+    comm.allreduce_f32(xs, scale_exp=k, chunks=chunks, stream=comm.stream)
+    torch.cuda.synchronize()
+    comm.set_stage_timing(True)
+    out = comm.allreduce_f32(xs, scale_exp=k, chunks=chunks, stream=comm.stream)
+    torch.cuda.synchronize()
+    st = comm.stage_times()
+    comm.set_stage_timing(False)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), orc.reduce_f32(hs, k).view(np.uint32))
+    for name in ("quant", "reduce_scatter", "dequant", "all_gather"):
+        assert st.get(name, 0.0) > 0.0, (name, st)
+    assert st["stages"] >= 4 * chunks, st
+    comm.destroy()
+    grp.destroy()
