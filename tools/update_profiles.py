@@ -42,6 +42,9 @@ def main():
     for name, out in (("bench.json", "bench.json"), (os.path.join("prof", "run_kernel_stats.csv"), "bench_kernel_stats.csv"),
                       ("bench_profiled.json", "bench_profiled.json"),
                       (os.path.join("prof_bf16", "run_kernel_stats.csv"), "bf16_kernel_stats.csv"),
+                      # the rotated-set (cold) run: k_stream_vec's average here reproduces frac_cold
+                      (os.path.join("prof_cold", "run_kernel_stats.csv"), "cold_kernel_stats.csv"),
+                      ("prof_cold.log", "cold_probe.log"),
                       ("pytest_gpu.log", "pytest_gpu.log"), ("rehearse_n2.json", "rehearse_n2.json"), ("smoke.log", "smoke.log")):
         if os.path.exists(os.path.join(src, name)):
             shutil.copy(os.path.join(src, name), os.path.join(dest, out))
