@@ -1,0 +1,91 @@
+"""The N > 1 bench's engine sequence (tuning -> 16-bit legs -> reduce-scatter
+leg: bench.py main, bf16_engines, reduce_scatter_engines) with exact
+fixed-point data, so that every call of every engine is checked exactly on
+every rank without the oracle.  One rank per process, started from a shell
+(tools/gpu_rs_sequence.sh), every rank on device 0.
+
+    python tools/rs_sequence_probe.py RANK PORT WORLD [MIB]
+
+Rank r's buckets are (r + 1) * b and (r + 1) * b / 2 with b[i] = ((i % 4093) -
+2046) * 2^-12: every quantised partial and sum is exact at k = 20, so the
+reduced bucket is the exact sum (16-bit buckets: the sum of the rounded
+inputs, rounded once).  Prints one JSON line per step: engine, op, format,
+bytes, and per call the number of wrong elements."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    rank, port, world = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    mib = float(sys.argv[4]) if len(sys.argv) > 4 else 256.0
+    os.environ.setdefault("INCCL_ENGINE", "p2p")
+    os.environ["INCCL_DEVICE"] = "0"
+    os.environ.setdefault("INCCL_BOOT_TIMEOUT", "120")
+    import torch
+    from container_inc_amd import inccl
+    dev = torch.device("cuda", 0)
+    grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=0)
+    comm = inccl.inccl_communicator_create(grp, 0)
+    k = 20
+    bad_total = 0
+
+    def inputs(n, dt):
+        i = torch.arange(n, device=dev, dtype=torch.int64)
+        b = ((i % 4093) - 2046).to(torch.float32) * 2.0 ** -12
+        mine = [(b * float(rank + 1)).to(dt), (b * float(rank + 1) * 0.5).to(dt)]
+        acc = torch.zeros(n, device=dev, dtype=torch.float32)
+        for r in range(world):
+            acc += (b * float(r + 1)).to(dt).float() + (b * float(r + 1) * 0.5).to(dt).float()
+        torch.cuda.synchronize()   # made on torch's stream; the calls run on comm.stream
+        return mine, acc.to(dt)
+
+    def step(eng, op, dt, nbytes):
+        nonlocal bad_total
+        es = 4 if dt == torch.float32 else 2
+        n = int(nbytes) // es
+        n -= n % (world * 64)
+        xs, full = inputs(n, dt)
+        shard = n // world
+        want = full if op == "ar" else full[rank * shard:(rank + 1) * shard]
+        row = {"rank": rank, "engine": eng, "op": op, "dtype": str(dt).split(".")[-1], "n": n, "bad": []}
+        try:
+            comm.set_engine(eng)
+            for _ in range(3):
+                if op == "rs":
+                    out = comm.reduce_scatter(xs, scale_exp=k, stream=comm.stream)
+                elif dt == torch.float32:
+                    out = comm.allreduce_f32(xs, scale_exp=k, stream=comm.stream)
+                else:
+                    fn = comm.allreduce_bf16 if dt == torch.bfloat16 else comm.allreduce_f16
+                    out = fn(xs, out=torch.empty_like(xs[0]), scale_exp=k, stream=comm.stream)
+                torch.cuda.synchronize()
+                row["bad"].append(int((out != want).sum().item()))
+        except Exception as e:  # noqa: BLE001
+            row["error"] = repr(e)[:300]
+        bad_total += sum(row["bad"])
+        print(json.dumps(row), flush=True)
+
+    big = mib * (1 << 20)
+    f32, b16, h16 = torch.float32, torch.bfloat16, torch.float16
+    for eng in ("p2p", "mesh", "meshw"):            # tuning
+        step(eng, "ar", f32, big)
+    for dt in (b16, h16):                           # the bf16 / f16 keys
+        for eng in ("p2p", "mesh", "meshw"):
+            step(eng, "ar", dt, big)
+    for eng in ("p2p", "mesh"):                     # the reduce_scatter key
+        step(eng, "rs", f32, big)
+    for small in (64 << 10, 1 << 20):
+        for eng in ("p2p", "ll"):
+            step(eng, "rs", f32, small)
+    comm.barrier()
+    comm.destroy()
+    grp.destroy()
+    print(json.dumps({"rank": rank, "bad_total": bad_total}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
