@@ -4,7 +4,13 @@ fixed-point data, so that every call of every engine is checked exactly on
 every rank without the oracle.  One rank per process, started from a shell
 (tools/gpu_rs_sequence.sh), every rank on device 0.
 
-    python tools/rs_sequence_probe.py RANK PORT WORLD [MIB]
+    python tools/rs_sequence_probe.py RANK PORT WORLD [MIB] [--rccl] [--random]
+
+--rccl: before each step's engine list, a call on the rccl engine as the bench
+makes one (it fails on one GPU: RCCL refuses two ranks on one device; the
+error is expected and recorded).  --random: N(0,1) buckets at k = 25, as the
+bench, checked against the float64 sum wrapped like the int32 partials
+(exact: the partials are integers).
 
 Rank r's buckets are (r + 1) * b and (r + 1) * b / 2 with b[i] = ((i % 4093) -
 2046) * 2^-12: every quantised partial and sum is exact at k = 20, so the
@@ -20,8 +26,11 @@ sys.path.insert(0, ROOT)
 
 
 def main():
-    rank, port, world = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
-    mib = float(sys.argv[4]) if len(sys.argv) > 4 else 256.0
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    rank, port, world = int(args[0]), int(args[1]), int(args[2])
+    mib = float(args[3]) if len(args) > 3 else 256.0
+    with_rccl = "--rccl" in sys.argv
+    rand = "--random" in sys.argv
     os.environ.setdefault("INCCL_ENGINE", "p2p")
     os.environ["INCCL_DEVICE"] = "0"
     os.environ.setdefault("INCCL_BOOT_TIMEOUT", "120")
@@ -30,10 +39,28 @@ def main():
     dev = torch.device("cuda", 0)
     grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=0)
     comm = inccl.inccl_communicator_create(grp, 0)
-    k = 20
+    k = 25 if rand else 20
     bad_total = 0
 
     def inputs(n, dt):
+        if rand:   # every rank regenerates every rank's buckets from its seed
+            qs = torch.zeros(n, device=dev, dtype=torch.int64)
+            mine = None
+            for r in range(world):
+                g = torch.Generator(device=dev)
+                g.manual_seed(9100 + r)
+                xr = [torch.randn(n, generator=g, device=dev).to(dt) for _ in range(2)]
+                for x in xr:   # the quantiser: round half to even at 2^-k, saturate to int32
+                    q = torch.round(x.double() * 2.0 ** k).clamp(-2 ** 31, 2 ** 31 - 1).to(torch.int64)
+                    qs += q
+                if r == rank:
+                    mine = xr
+            qs = ((qs + 2 ** 31) % 2 ** 32 - 2 ** 31)   # int32 wrap-around sum
+            want = (qs.double() * 2.0 ** -k).float().to(dt) if dt == torch.float32 else None
+            if want is None:   # 16-bit: dequantise in fp32, then round once
+                want = (qs.to(torch.float32) * 2.0 ** -k).to(dt)
+            torch.cuda.synchronize()
+            return mine, want
         i = torch.arange(n, device=dev, dtype=torch.int64)
         b = ((i % 4093) - 2046).to(torch.float32) * 2.0 ** -12
         mine = [(b * float(rank + 1)).to(dt), (b * float(rank + 1) * 0.5).to(dt)]
@@ -71,15 +98,16 @@ def main():
 
     big = mib * (1 << 20)
     f32, b16, h16 = torch.float32, torch.bfloat16, torch.float16
-    for eng in ("p2p", "mesh", "meshw"):            # tuning
+    rc = ("rccl",) if with_rccl else ()
+    for eng in rc + ("p2p", "mesh", "meshw"):            # tuning
         step(eng, "ar", f32, big)
-    for dt in (b16, h16):                           # the bf16 / f16 keys
-        for eng in ("p2p", "mesh", "meshw"):
+    for dt in (b16, h16):                                # the bf16 / f16 keys
+        for eng in rc + ("p2p", "mesh", "meshw"):
             step(eng, "ar", dt, big)
-    for eng in ("p2p", "mesh"):                     # the reduce_scatter key
+    for eng in rc + ("p2p", "mesh"):                     # the reduce_scatter key
         step(eng, "rs", f32, big)
     for small in (64 << 10, 1 << 20):
-        for eng in ("p2p", "ll"):
+        for eng in rc + ("p2p", "ll"):
             step(eng, "rs", f32, small)
     comm.barrier()
     comm.destroy()
