@@ -758,11 +758,17 @@ def rs_oracle_check(srcs, out_shard, lanes, k: int, rank: int, world: int) -> di
         arr = [b.numpy() for b in bucket]
         want = O.reduce_f32([a[j].view(np.float32) for a in arr for j in range(R)], k).view(np.uint32)
         lane = np.asarray(lanes)
-        bad = 0
+        bad, by_rank = 0, {}
         for r, a in enumerate(arr):
             sel = (lane >= r * shard) & (lane < (r + 1) * shard)
-            bad += int(np.count_nonzero(a[R].view(np.uint32)[sel] != want[sel]))
+            nb = int(np.count_nonzero(a[R].view(np.uint32)[sel] != want[sel]))
+            bad += nb
+            if nb:
+                by_rank[r] = nb
         res["mismatches"] = bad
+        if by_rank:   # which ranks' shards, out of how many lanes each
+            res["mismatches_by_rank"] = by_rank
+            res["lanes_per_rank"] = int(np.count_nonzero((lane >= 0) & (lane < shard)))
     return res
 
 
@@ -822,6 +828,8 @@ def reduce_scatter_engines(comm, dev, R: int, rank: int, world: int, mib: float 
                "ms": round(v[0] * 1e3, 4) if good else None}
         if good:
             row["parity_vs_oracle"] = rs_oracle_check(inputs[0], got[0], lanes, 25, rank, world)
+            if not (good and ident):   # the third verification call (inputs[0] again) checked as well
+                row["parity_vs_oracle_call3"] = rs_oracle_check(inputs[0], got[2], lanes, 25, rank, world)
             link = (world - 1) * n * 4 // world
             row["GBps_buckets"] = round(world * R * 4 * n / v[0] / 1e9, 1)
             # both directions counted: (W-1)/W * n * 4 bytes out and as many in
