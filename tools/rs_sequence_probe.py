@@ -6,6 +6,8 @@ every rank without the oracle.  One rank per process, started from a shell
 
     python tools/rs_sequence_probe.py RANK PORT WORLD [MIB] [--rccl] [--random]
 
+--bench-like: each step on a new torch side stream with a preallocated out
+(bench.py reduce_scatter_engines / bf16_engines), not comm.stream.
 --rccl: before each step's engine list, a call on the rccl engine as the bench
 makes one (it fails on one GPU: RCCL refuses two ranks on one device; the
 error is expected and recorded).  --random: N(0,1) buckets at k = 25, as the
@@ -31,6 +33,7 @@ def main():
     mib = float(args[3]) if len(args) > 3 else 256.0
     with_rccl = "--rccl" in sys.argv
     rand = "--random" in sys.argv
+    benchlike = "--bench-like" in sys.argv   # the bench's form: a torch side stream per leg, a preallocated out
     os.environ.setdefault("INCCL_ENGINE", "p2p")
     os.environ["INCCL_DEVICE"] = "0"
     os.environ.setdefault("INCCL_BOOT_TIMEOUT", "120")
@@ -41,6 +44,7 @@ def main():
     comm = inccl.inccl_communicator_create(grp, 0)
     k = 25 if rand else 20
     bad_total = 0
+    legs = {}
 
     def inputs(n, dt):
         if rand:   # every rank regenerates every rank's buckets from its seed
@@ -79,16 +83,26 @@ def main():
         shard = n // world
         want = full if op == "ar" else full[rank * shard:(rank + 1) * shard]
         row = {"rank": rank, "engine": eng, "op": op, "dtype": str(dt).split(".")[-1], "n": n, "bad": []}
+        sh = comm.stream
+        pre = None
+        if benchlike:   # one stream and one out per leg (op, format, size), shared by its engines
+            key = (op, str(dt), n)
+            if key not in legs:
+                legs.clear()   # the previous leg's stream and out are dropped, as the bench's are
+                legs[key] = (torch.cuda.Stream(device=dev), torch.empty(shard if op == "rs" else n, device=dev, dtype=dt))
+                torch.cuda.synchronize()
+            sh = legs[key][0].cuda_stream
+            pre = legs[key][1]
         try:
             comm.set_engine(eng)
             for _ in range(3):
                 if op == "rs":
-                    out = comm.reduce_scatter(xs, scale_exp=k, stream=comm.stream)
+                    out = comm.reduce_scatter(xs, out=pre, scale_exp=k, stream=sh)
                 elif dt == torch.float32:
-                    out = comm.allreduce_f32(xs, scale_exp=k, stream=comm.stream)
+                    out = comm.allreduce_f32(xs, out=pre, scale_exp=k, stream=sh)
                 else:
                     fn = comm.allreduce_bf16 if dt == torch.bfloat16 else comm.allreduce_f16
-                    out = fn(xs, out=torch.empty_like(xs[0]), scale_exp=k, stream=comm.stream)
+                    out = fn(xs, out=pre if pre is not None else torch.empty_like(xs[0]), scale_exp=k, stream=sh)
                 torch.cuda.synchronize()
                 row["bad"].append(int((out != want).sum().item()))
         except Exception as e:  # noqa: BLE001
