@@ -6,6 +6,8 @@ every rank without the oracle.  One rank per process, started from a shell
 
     python tools/rs_sequence_probe.py RANK PORT WORLD [MIB] [--rccl] [--random]
 
+--skew: rank 0 starts every step 0.2 s after the others (in the bench, rank 0
+runs the oracle check of the previous engine while the others go on).
 --bench-like: each step on a new torch side stream with a preallocated out
 (bench.py reduce_scatter_engines / bf16_engines), not comm.stream.
 --rccl: before each step's engine list, a call on the rccl engine as the bench
@@ -34,6 +36,7 @@ def main():
     with_rccl = "--rccl" in sys.argv
     rand = "--random" in sys.argv
     benchlike = "--bench-like" in sys.argv   # the bench's form: a torch side stream per leg, a preallocated out
+    skew = "--skew" in sys.argv   # rank 0 enters each step 0.2 s late (the bench's rank-0 oracle check)
     os.environ.setdefault("INCCL_ENGINE", "p2p")
     os.environ["INCCL_DEVICE"] = "0"
     os.environ.setdefault("INCCL_BOOT_TIMEOUT", "120")
@@ -93,6 +96,9 @@ def main():
                 torch.cuda.synchronize()
             sh = legs[key][0].cuda_stream
             pre = legs[key][1]
+        if skew and rank == 0:
+            import time
+            time.sleep(0.2)
         try:
             comm.set_engine(eng)
             for _ in range(3):
