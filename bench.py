@@ -697,6 +697,8 @@ def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256, fmt: 
                 torch.cuda.synchronize()
             same = (torch.equal(got[0], got[2]) if refs is None
                     else all(torch.equal(g, refs[i % 2]) for i, g in enumerate(got)))
+            if first_out is not None:
+                first_out[eng] = got[0].clone()
             for _ in range(5):
                 allreduce(inputs[0], out=out, scale_exp=25, stream=st.cuda_stream)
             torch.cuda.synchronize()
@@ -773,7 +775,7 @@ def rs_oracle_check(srcs, out_shard, lanes, k: int, rank: int, world: int) -> di
 
 
 def reduce_scatter_engines(comm, dev, R: int, rank: int, world: int, mib: float = 256,
-                           engines=("rccl", "p2p")) -> list:
+                           engines=("rccl", "p2p"), inputs=None, first_out=None) -> list:
     """N > 1: inccl_reduce_scatter_f32 of R resident `mib` MiB fp32 buckets per
     rank (each rank keeps its 1/W shard of the reduced bucket: the sharded-
     gradient callers' half of the allreduce) on rccl (ncclReduceScatter) and p2p
@@ -783,11 +785,13 @@ def reduce_scatter_engines(comm, dev, R: int, rank: int, world: int, mib: float 
     fraction of its (W-1)/W * n * 4 bytes."""
     import torch
     import torch.distributed as dist
-    n = int(mib * (1 << 20)) // 4
+    n = int(mib * (1 << 20)) // 4 if inputs is None else inputs[0][0].numel()
     if n % world:
         return [{"skipped": f"{n} elements do not split into {world} shards"}]
-    inputs = []
-    for seed in (9100, 9600):
+    # (inputs / first_out: diagnostics, tools/rs_leg_probe.py -- given input sets,
+    # and each engine's first output kept)
+    given, inputs = inputs, [] if inputs is None else list(inputs)
+    for seed in (9100, 9600) if given is None else ():
         gen = torch.Generator(device=dev)
         gen.manual_seed(seed + rank)
         inputs.append([torch.randn(n, generator=gen, device=dev) for _ in range(R)])
@@ -808,6 +812,8 @@ def reduce_scatter_engines(comm, dev, R: int, rank: int, world: int, mib: float 
                 got.append(out.clone())
             same = (torch.equal(got[0], got[2]) if refs is None
                     else all(torch.equal(g, refs[i % 2]) for i, g in enumerate(got)))
+            if first_out is not None:
+                first_out[eng] = got[0].clone()
             for _ in range(5):
                 comm.reduce_scatter(inputs[0], out=out, scale_exp=25, stream=st.cuda_stream)
             torch.cuda.synchronize()

@@ -99,6 +99,56 @@ def main():
         grp.destroy()
         dist.destroy_process_group()
         return
+    if "--bench-digits" in sys.argv:   # bench.reduce_scatter_engines itself on digit-coded data (k = 25)
+        def sets(mib):
+            n = int(mib * (1 << 20)) // 4
+            i = torch.arange(n, device=dev, dtype=torch.int64)
+            out = []
+            for base in (1, 4):
+                d = ((i % 3) + base).to(torch.float32)
+                out.append([d * float(8 ** rank) * 2.0 ** -25, torch.zeros(n, device=dev)])
+            torch.cuda.synchronize()
+            return out
+
+        def decode(t, mib, eng):
+            n = int(mib * (1 << 20)) // 4
+            shard = n // world
+            i = torch.arange(rank * shard, (rank + 1) * shard, device=dev, dtype=torch.int64)
+            want = torch.zeros(shard, device=dev, dtype=torch.float64)
+            for r in range(world):
+                want += ((i % 3) + 1).double() * float(8 ** r)
+            got = torch.round(t.double() * 2.0 ** 25)
+            bad = (got != want).nonzero().flatten()
+            rec = {"engine": eng, "mib": mib, "rank": rank, "bad": int(bad.numel())}
+            if bad.numel():
+                e = int(bad[0])
+                g, w = int(got[e]), int(want[e])
+                rec.update(first=e, got_digits=[(g >> (3 * r)) & 7 for r in range(world)],
+                           want_digits=[(w >> (3 * r)) & 7 for r in range(world)])
+                # how many bad elements, per rank-digit position that is wrong
+                gi = got[bad].to(torch.int64)
+                wi = want[bad].to(torch.int64)
+                rec["wrong_digit_counts"] = [int(((gi >> (3 * r)) & 7).ne((wi >> (3 * r)) & 7).sum()) for r in range(world)]
+            return rec
+
+        for rep in range(repeats):
+            for mib, engs in ((256, big), (1 / 16, small), (1.0, small)):
+                firsts = {}
+                rows = bench.reduce_scatter_engines(comm, dev, 2, rank, world, mib, engs, inputs=sets(mib),
+                                                    first_out=firsts)
+                recs = [decode(t, mib, eng) for eng, t in firsts.items()]
+                everyone = [None] * world
+                dist.all_gather_object(everyone, recs)
+                if rank == 0:
+                    for rr in everyone:
+                        for r in rr:
+                            if r["bad"]:
+                                print(json.dumps({"rep": rep, **r}), flush=True)
+                    print(json.dumps({"rep": rep, "mib": mib, "rows": [(x["engine"], x["ok"], x["bit_identical"]) for x in rows]}), flush=True)
+        comm.destroy()
+        grp.destroy()
+        dist.destroy_process_group()
+        return
     for rep in range(repeats):
         rows = bench.reduce_scatter_engines(comm, dev, 2, rank, world, engines=big)
         for mib in (1 / 16, 1.0):
