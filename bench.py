@@ -697,8 +697,6 @@ def bf16_engines(comm, dev, R: int, rank: int, world: int, mib: int = 256, fmt: 
                 torch.cuda.synchronize()
             same = (torch.equal(got[0], got[2]) if refs is None
                     else all(torch.equal(g, refs[i % 2]) for i, g in enumerate(got)))
-            if first_out is not None:
-                first_out[eng] = got[0].clone()
             for _ in range(5):
                 allreduce(inputs[0], out=out, scale_exp=25, stream=st.cuda_stream)
             torch.cuda.synchronize()
@@ -810,6 +808,11 @@ def reduce_scatter_engines(comm, dev, R: int, rank: int, world: int, mib: float 
                 comm.reduce_scatter(xs, out=out, scale_exp=25, stream=st.cuda_stream)
                 torch.cuda.synchronize()
                 got.append(out.clone())
+                # the clone runs on torch's stream and the next call on `st`:
+                # without this wait the next call overwrote `out` under the clone
+                # (round 6: the first call's copy held the second call's result
+                # on one or two of eight ranks sharing a GPU, every engine alike)
+                torch.cuda.synchronize()
             same = (torch.equal(got[0], got[2]) if refs is None
                     else all(torch.equal(g, refs[i % 2]) for i, g in enumerate(got)))
             if first_out is not None:
