@@ -487,6 +487,11 @@ def stage_probe(comm, xs, out, k: int, chunks: int, st, world: int, calls: int =
     import torch
     names = list(comm.STAGE_NAMES) + ["wall_us", "overlap_us"]
     acc = {key: 0.0 for key in names}
+    # ranks arrive skewed (rank 0 has just run the oracle check): one untimed call
+    # after a barrier absorbs that, so no stage counts a wait for a late peer
+    agree([0.0], world)
+    comm.allreduce_f32(xs, out=out, scale_exp=k, chunks=chunks, stream=st.cuda_stream)
+    torch.cuda.synchronize()
     try:
         comm.set_stage_timing(True)
         for _ in range(calls):
