@@ -423,3 +423,49 @@ def test_reduce_scatter_graph_capture_world1(gpu, orc, monkeypatch, engine):
     del graph
     comm.destroy()
     grp.destroy()
+
+
+def _knobs_rank(rank, world, port, q, case):
+    """knobs read from each process's environment are agreed when
+    the communicator is created (api.c agree_knobs)."""
+    try:
+        os.environ["INCCL_DEVICE"] = "0"
+        os.environ["INCCL_BOOT_TIMEOUT"] = "60"
+        if case == "mesh_rs":   # only rank 1 opts out of the mesh route: every rank must take the p2p route
+            os.environ["INCCL_ENGINE"] = "mesh"
+            if rank == 1:
+                os.environ["INCCL_MESH_RS"] = "0"
+        else:                   # different engines: creation fails on every rank, naming both
+            os.environ["INCCL_ENGINE"] = "mesh" if rank == 0 else "p2p"
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        from container_inc_amd import inccl
+        from oracle import oracle as O
+        dev = torch.device("cuda", 0)
+        grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=0)
+        comm = inccl.inccl_communicator_create(grp, 0)
+        if case != "mesh_rs":
+            from container_inc_amd import load
+            ok = [comm is None and "INCCL_ENGINE differs" in load().inccl_last_error().decode()]
+            grp.destroy()
+            q.put((rank, ok, None))
+            return
+        shard = 1 << 16
+        hs = [_bucket(np.random.default_rng(40 + r), world * shard, "f32") for r in range(world)]
+        want = O.reduce_f32(hs, 25)[rank * shard:(rank + 1) * shard]
+        out = comm.reduce_scatter([_dev(hs[rank], dev, "f32")], scale_exp=25, stream=comm.stream)
+        torch.cuda.synchronize()
+        ok = [bool(np.array_equal(_host(out, "f32"), want))]
+        comm.ipc_mem_kind("p2p")   # the agreed route: the p2p pull-reduce on both ranks
+        comm.barrier()
+        comm.destroy()
+        grp.destroy()
+        q.put((rank, ok, None))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("case", ["mesh_rs", "engine"])
+def test_environment_knobs_agreed_across_ranks(gpu, case):
+    _run_mp(2, _knobs_rank, case, timeout=120)
