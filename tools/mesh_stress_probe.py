@@ -1,0 +1,67 @@
+"""One rank of a mesh-engine stress run: W processes on one GPU, many calls of
+one mode sequence, every call checked exactly, a timed-out wait reported with
+the wait it was (inccl_mesh.hip wait_flag).  Started per rank from a shell
+(tools/gpu_mesh_stress.sh), so no launcher forks after GPU init.
+
+    python tools/mesh_stress_probe.py RANK PORT W MODE CALLS LOG2 [LOG2 ...]
+
+MODE: ar (mesh allreduce fp32), rs (mesh reduce-scatter fp32), mix (the two
+alternating), w (meshw allreduce).  Rank r's bucket is (r + 1) * b with b a
+multiple of 2^-12 below 1/2: exact at k = 20.  One JSON line per rank: calls
+made, wrong calls, and the first error (a timeout names its wait)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    rank, port, world, mode, calls = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4],
+                                      int(sys.argv[5]))
+    logs = [int(v) for v in sys.argv[6:]] or [20]
+    os.environ["INCCL_ENGINE"] = "meshw" if mode == "w" else "mesh"
+    os.environ["INCCL_DEVICE"] = "0"
+    os.environ.setdefault("INCCL_BOOT_TIMEOUT", "120")
+    os.environ.setdefault("INCCL_LL_TIMEOUT_MS", "10000")
+    import torch
+    from container_inc_amd import inccl
+    dev = torch.device("cuda", 0)
+    grp = inccl.inccl_group_create(world, rank, "127.0.0.1", port=port, device=0)
+    comm = inccl.inccl_communicator_create(grp, 0)
+    made, wrong, err = 0, 0, None
+    try:
+        for lg in logs:
+            shard = 1 << lg
+            n = world * shard
+            i = torch.arange(n, device=dev, dtype=torch.int64)
+            b = ((i % 4093) - 2046).to(torch.float32) * 2.0 ** -12
+            x = b * float(rank + 1)
+            full = b * float(world * (world + 1) // 2)
+            mine = full[rank * shard:(rank + 1) * shard]
+            torch.cuda.synchronize()
+            for call in range(calls):
+                rs = mode == "rs" or (mode == "mix" and call % 2 == 1)
+                if rs:
+                    out = comm.reduce_scatter([x], scale_exp=20, stream=comm.stream)
+                else:
+                    out = comm.allreduce_f32([x], scale_exp=20, stream=comm.stream)
+                torch.cuda.synchronize()
+                made += 1
+                wrong += 0 if torch.equal(out, mine if rs else full) else 1
+            del i, b, x, full, mine
+        if comm.clear_error():   # a timeout of the last call is reported here
+            err = "the last call timed out"
+    except Exception as e:  # noqa: BLE001
+        err = repr(e)[:400]
+    print(json.dumps({"rank": rank, "mode": mode, "calls": made, "wrong": wrong, "error": err}), flush=True)
+    try:
+        comm.destroy()
+        grp.destroy()
+    except Exception:  # noqa: BLE001
+        pass
+
+
+if __name__ == "__main__":
+    main()
