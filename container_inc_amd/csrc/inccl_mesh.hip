@@ -122,7 +122,8 @@ __device__ __forceinline__ int ready_idx(int j, int c) { return (kMaxR + j) * IN
 // Bounded wait for *f >= epoch (serial-number order).  false: timed out or aborted.
 // A timeout reports which wait expired: err[0] = INCCL_MESH_ERR_TIMEOUT | item << 8
 // | peer << 4 | chunk << 16 (item 3: a reduce's arrival flag, 6: a gather's ready
-// flag), err[1] = the flag's last value, err[2] = the epoch waited for.
+// flag), err[1] = the flag's last value, err[2] = the epoch waited for, err[3] =
+// the tickets this rank's workgroups had taken.
 __device__ bool wait_flag(const MeshArgs& a, const uint32_t* f, uint32_t epoch, uint32_t item, int peer, int c)
 {
     const uint64_t t0 = now_ticks();
@@ -132,6 +133,8 @@ __device__ bool wait_flag(const MeshArgs& a, const uint32_t* f, uint32_t epoch, 
         if (now_ticks() - t0 > a.timeout_ticks) {
             __hip_atomic_store(a.err + 1, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(a.err + 2, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.err + 3, __hip_atomic_load(a.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);   // tickets taken so far
             __hip_atomic_store(a.err, INCCL_MESH_ERR_TIMEOUT | item << 8 | (uint32_t)peer << 4 | (uint32_t)c << 16,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(a.ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

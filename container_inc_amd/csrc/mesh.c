@@ -240,9 +240,9 @@ static int mesh_piece(struct inccl_communicator *c, int kind16, const void *cons
     if (err) {   /* which wait expired (inccl_mesh.hip wait_flag) */
         const volatile uint32_t *e4 = (const volatile uint32_t *)c->mesh_err_host;
         return inccl_set_error(INCCL_ERR_STATE, "mesh: an earlier call timed out waiting for a peer (results invalid; "
-                               "rank %d, %s of chunk %u, peer %u: flag %u, waited for epoch %u)", me,
-                               ((err >> 8) & 0xffu) == 3 ? "reduce's arrival flag" : "gather's ready flag",
-                               err >> 16, (err >> 4) & 0xfu, e4[1], e4[2]);
+                               "rank %d, %s of chunk %u, peer %u: flag %u, waited for epoch %u; %u tickets taken)",
+                               me, ((err >> 8) & 0xffu) == 3 ? "reduce's arrival flag" : "gather's ready flag",
+                               err >> 16, (err >> 4) & 0xfu, e4[1], e4[2], e4[3]);
     }
     const size_t chunk = mesh_chunk(c, shard);
     const int nchunks = (int)((shard + chunk - 1) / chunk);
