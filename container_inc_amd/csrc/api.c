@@ -17,7 +17,7 @@
 /* ------------------------------------------------------------------ */
 /* errors                                                               */
 /* ------------------------------------------------------------------ */
-static __thread char g_err[512];
+static __thread char g_err[1536];
 
 int inccl_set_error(int code, const char *fmt, ...)
 {
@@ -630,6 +630,10 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     const char *mle = getenv("INCCL_MESH_LAG");
     c->mesh_lag_env = mle ? atoi(mle) : 0;
     if (c->mesh_lag_env < 0) c->mesh_lag_env = 0;
+    const char *mre = getenv("INCCL_MESH_RESCUE");   /* 0: flag polls are loads only (diagnostics) */
+    c->mesh_rescue = mre ? atoi(mre) : 16;
+    if (c->mesh_rescue < 0) c->mesh_rescue = 16;
+    while (c->mesh_rescue & (c->mesh_rescue - 1)) c->mesh_rescue &= c->mesh_rescue - 1;   /* a power of two */
     const char *hce = getenv("INCCL_HOST_CHUNK_MIB");
     c->host_chunk_mib = hce ? atoi(hce) : 0;
     if (c->host_chunk_mib < 1 || c->host_chunk_mib > 1024) c->host_chunk_mib = 16;

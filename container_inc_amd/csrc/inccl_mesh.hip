@@ -84,14 +84,21 @@ struct MeshArgs {
     const uint32_t* own_resin;
     uint32_t* peer_sig[kMaxR];           // rank j's signal array ([me] = own)
     const uint32_t* own_sig;
-    uint32_t* ctr;                       // [0] calls done, [1] retired, [2] ticket, [3] abort
-    uint32_t* err;                       // host-mapped error word
+    uint32_t* ctr;                       // [0] calls done, [1] retired, [2] ticket, [3] abort, [4] started,
+                                         // [6] polls rescued, [7] ended by the control load (all calls),
+                                         // [8 + j] pushes to rank j finished; 64-bit at [32]: call start,
+                                         // [34 + 2 j]: last push flag store to rank j (s_memrealtime)
+                                         // (this call)
+    uint32_t* err;                       // host-mapped error words (16)
     uint64_t timeout_ticks;
     int nchunks, W, me, lag, vec_src, vec_dst, push_res;
     int rs;                              // reduce-scatter: gather(c, me) copies my result chunk into dst (the
                                          // shard), the other gathers only wait
     Scale sc;
     uint64_t src_bytes, dst_bytes, inbox_bytes, res_bytes, resin_bytes;   // region sizes (bounds check)
+    uint32_t zero;                       // 0 (wait_flag's read-modify-write operand)
+    uint32_t rescue_every;               // wait_flag: a read-modify-write every this many polls (a power of
+                                         // two; 0: never)
 };
 
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
@@ -123,18 +130,76 @@ __device__ __forceinline__ int ready_idx(int j, int c) { return (kMaxR + j) * IN
 // A timeout reports which wait expired: err[0] = INCCL_MESH_ERR_TIMEOUT | item << 8
 // | peer << 4 | chunk << 16 (item 3: a reduce's arrival flag, 6: a gather's ready
 // flag), err[1] = the flag's last value, err[2] = the epoch waited for, err[3] =
-// the tickets this rank's workgroups had taken.
+// the tickets this rank's workgroups had taken, err[4] / err[5] = its workgroups
+// started / retired, err[6 + j] = its pushes to rank j finished, err[12] = the
+// polls rescued so far, err[13] = the call's chunks, err[14] = the flag re-read
+// by a read-modify-write, err[15] / err[16] / err[17 + j] = the clock (/16) at
+// the timeout, at the call's start, at the last push flag store to rank j.
+//
+// The poll is a system-scope load, and every 16th poll (a.rescue_every,
+// $INCCL_MESH_RESCUE) a read-modify-write
+// (add a.zero: 0, but opaque to the compiler, which would turn an idempotent
+// RMW into a load).  A load alone can keep returning an old value after the
+// peer's store has reached memory: four ranks on one GPU deadlocked that way
+// (DESIGN.md "Mesh reduce-scatter route": the timed-out poll read 6 for 30 s,
+// the host then read 7 in every flag).  The RMW is performed at the memory
+// side; a wait it ends adds one to ctr[6] (kept across calls), and to ctr[7]
+// when one more load after it still returns the old value.
 __device__ bool wait_flag(const MeshArgs& a, const uint32_t* f, uint32_t epoch, uint32_t item, int peer, int c)
 {
     const uint64_t t0 = now_ticks();
     uint32_t v;
-    while ((int32_t)((v = ld_sys(f)) - epoch) < 0) {
+    for (uint32_t spin = 1;; ++spin) {
+        if ((int32_t)((v = ld_sys(f)) - epoch) >= 0) break;
+        if (a.rescue_every && (spin & (a.rescue_every - 1u)) == 0u) {
+            // control: a second load straight away (a flag landing between two
+            // polls ends the wait here as often as at the RMW below)
+            if ((int32_t)((v = ld_sys(f)) - epoch) >= 0) {
+                __hip_atomic_fetch_add(a.ctr + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            if ((int32_t)((v = __hip_atomic_fetch_add(const_cast<uint32_t*>(f), a.zero, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM)) - epoch) >= 0) {
+                __hip_atomic_fetch_add(a.ctr + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
         if (__hip_atomic_load(a.ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
         if (now_ticks() - t0 > a.timeout_ticks) {
             __hip_atomic_store(a.err + 1, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(a.err + 2, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(a.err + 3, __hip_atomic_load(a.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);   // tickets taken so far
+            // the rank's own progress: workgroups started and retired, pushes
+            // finished per destination; and the flag re-read by a system-scope
+            // read-modify-write (performed at the coherence point, never a
+            // cached copy)
+            __hip_atomic_store(a.err + 4, __hip_atomic_load(a.ctr + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.err + 5, __hip_atomic_load(a.ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            for (int j = 0; j < a.W; ++j)
+                __hip_atomic_store(a.err + 6 + j, __hip_atomic_load(a.ctr + 8 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.err + 13, (uint32_t)a.nchunks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // clock readings (s_memrealtime / 16, one GPU-wide 100 MHz clock):
+            // this timeout, this call's first workgroup start, and the last
+            // flag store of this rank's pushes to each rank
+            const uint64_t* t64 = reinterpret_cast<const uint64_t*>(a.ctr + 32);
+            __hip_atomic_store(a.err + 15, (uint32_t)(now_ticks() >> 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.err + 16,
+                               (uint32_t)(__hip_atomic_load(t64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 4),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            for (int j = 0; j < a.W; ++j)
+                __hip_atomic_store(a.err + 17 + j,
+                                   (uint32_t)(__hip_atomic_load(t64 + 1 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 4),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.err + 12, __hip_atomic_load(a.ctr + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.err + 14,
+                               __hip_atomic_fetch_add(const_cast<uint32_t*>(f), a.zero, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(a.err, INCCL_MESH_ERR_TIMEOUT | item << 8 | (uint32_t)peer << 4 | (uint32_t)c << 16,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(a.ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -265,7 +330,12 @@ __device__ bool do_push(const MeshArgs& a, int c, int j, uint32_t epoch, float s
     }
     __builtin_amdgcn_s_waitcnt(0);   // this lane's stores acknowledged at system scope
     __syncthreads();                 // ... and every lane's
-    if (threadIdx.x == 0) st_sys(a.peer_sig[j] + arrive_idx(a.me, c), epoch);
+    if (threadIdx.x == 0) {
+        st_sys(a.peer_sig[j] + arrive_idx(a.me, c), epoch);
+        __hip_atomic_fetch_add(a.ctr + 8 + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // progress record
+        __hip_atomic_fetch_max(reinterpret_cast<uint64_t*>(a.ctr + 32) + 1 + j, now_ticks(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
     return true;
 }
 
@@ -479,6 +549,9 @@ __global__ __launch_bounds__(kMeshBlock) void k_mesh(MeshArgs a)
     const int W = a.W;
     const int per_slot = 2 * W + 1;
     const int total = (a.nchunks + 2 * a.lag) * per_slot;
+    if (threadIdx.x == 0 && __hip_atomic_fetch_add(a.ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(a.ctr + 32), now_ticks(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);   // this call's start (the first workgroup's)
     for (;;) {
         if (threadIdx.x == 0)
             s_ticket = (int)__hip_atomic_fetch_add(a.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -504,6 +577,8 @@ __global__ __launch_bounds__(kMeshBlock) void k_mesh(MeshArgs a)
         if (done == gridDim.x - 1) {
             __hip_atomic_store(a.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.ctr + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.ctr + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int j = 0; j < W; ++j) __hip_atomic_store(a.ctr + 8 + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -560,6 +635,9 @@ extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
     a.inbox_bytes = l->inbox_bytes;
     a.res_bytes = l->res_bytes;
     a.resin_bytes = l->resin_bytes;
+    a.zero = 0;
+    a.rescue_every = l->rescue_every > 0 ? (uint32_t)l->rescue_every : 0u;
+    if (a.rescue_every & (a.rescue_every - 1u)) return INCCL_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     const dim3 g((unsigned)l->grid), b(kMeshBlock);
 #define INCCL_MESH_CASE(RR)                                                  \

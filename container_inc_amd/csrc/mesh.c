@@ -12,7 +12,9 @@
  * Per rank, four device allocations shared over HIP IPC (separate, so that no
  * single export needs to exceed the group's IPC bound; see runtime.c):
  *   sig    [0, 64 KiB) signal array: arrive[8][1024] and ready[8][1024] words;
- *          [64 KiB, +16) call counter, retired workgroups, ticket, abort word
+ *          [64 KiB, +256) call counter, retired workgroups, ticket, abort word,
+ *          started workgroups, polls rescued, pushes finished per destination,
+ *          clock readings (inccl_mesh.hip MeshArgs::ctr)
  *   inbox  W * cap int32: slot j holds rank j's partial of my shard
  *   res    cap fp32: my dequantised result shard
  *   resin  W * cap fp32 ("meshw"): slot j holds rank j's result shard
@@ -54,6 +56,13 @@ void inccl_mesh_release(struct inccl_communicator *c)
     const int W = c->group->world_size, me = c->group->rank;
     if (!c->mesh_buf && !c->mesh_reg[1] && !c->mesh_reg[2] && !c->mesh_reg[3]) return;
     hipDeviceSynchronize();
+    if (c->mesh_buf && getenv("INCCL_MESH_STATS")) {   /* flag polls a read-modify-write ended (inccl_mesh.hip) */
+        uint32_t r[2] = {0, 0};
+        if (hipMemcpy(r, c->mesh_buf + MESH_CTR_OFFSET + 6 * sizeof(uint32_t), sizeof(r), hipMemcpyDeviceToHost) ==
+            hipSuccess)
+            fprintf(stderr, "inccl mesh rank %d: %u flag polls rescued by a read-modify-write, %u ended by the "
+                    "control load before it\n", me, r[0], r[1]);
+    }
     for (int r = 0; r < INCCL_MESH_REGIONS; ++r) {
         for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS; ++j) {
             if (j != me && c->mesh_peer[r][j]) hipIpcCloseMemHandle(c->mesh_peer[r][j]);
@@ -129,9 +138,9 @@ static int mesh_ensure(struct inccl_communicator *c, size_t shard)
     c->mesh_buf = c->mesh_reg[0];
     if (e == hipSuccess) e = hipMemset(c->mesh_buf, 0, MESH_DATA_OFFSET);   /* flags + counters */
     if (e == hipSuccess) e = hipDeviceSynchronize();   /* zeroed before any peer maps it */
-    if (e == hipSuccess) e = hipHostMalloc((void **)&c->mesh_err_host, 4 * sizeof(uint32_t), hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&c->mesh_err_host, 32 * sizeof(uint32_t), hipHostMallocMapped);
     if (e == hipSuccess) {
-        for (int i = 0; i < 4; ++i) ((volatile uint32_t *)c->mesh_err_host)[i] = 0;
+        for (int i = 0; i < 32; ++i) ((volatile uint32_t *)c->mesh_err_host)[i] = 0;
         e = hipHostGetDevicePointer((void **)&c->mesh_err_dev, c->mesh_err_host, 0);
     }
     if (e == hipSuccess) e = hipDeviceGetAttribute(&mine.pci_domain, hipDeviceAttributePciDomainID, dev);
@@ -219,6 +228,47 @@ static size_t mesh_chunk(const struct inccl_communicator *c, size_t shard)
     return ch;
 }
 
+/* After a timed-out call (epoch e, nchunks chunks): how many of its flags are
+ * raised, counted by the host through both mappings of each signal array --
+ * this rank's own allocation, and its IPC mapping of every peer's.  "arrived
+ * from" j = my arrive[j][*] >= e; "mine at" j = arrive[me][*] in rank j's array
+ * as read through my mapping of it (what my pushes wrote there); "ready" the
+ * same for ready flags.  A push counted as finished whose flag is missing from
+ * the receiver's own view but present through the sender's mapping would mean
+ * the two mappings do not reach the same memory. */
+static void mesh_flag_census(struct inccl_communicator *c, uint32_t e, uint32_t nchunks, char *out, size_t len)
+{
+    const int W = c->group->world_size, me = c->group->rank;
+    if (nchunks == 0 || nchunks > INCCL_MESH_MAX_CHUNKS) {
+        snprintf(out, len, "no flag census");
+        return;
+    }
+    static uint32_t buf[INCCL_MESH_MAX_CHUNKS];
+    int cnt[4][INCCL_MAX_LOCAL_INPUTS];
+    memset(cnt, 0xff, sizeof(cnt));   /* -1: not read */
+    for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS; ++j) {
+        const uint32_t *own = (const uint32_t *)c->mesh_buf, *peer = (const uint32_t *)c->mesh_peer[0][j];
+        const uint32_t *src[4] = {own + (size_t)j * INCCL_MESH_MAX_CHUNKS,
+                                  own + (size_t)(INCCL_MAX_LOCAL_INPUTS + j) * INCCL_MESH_MAX_CHUNKS,
+                                  peer ? peer + (size_t)me * INCCL_MESH_MAX_CHUNKS : NULL,
+                                  peer ? peer + (size_t)(INCCL_MAX_LOCAL_INPUTS + me) * INCCL_MESH_MAX_CHUNKS : NULL};
+        for (int k = 0; k < 4; ++k) {
+            if (!src[k] || hipMemcpy(buf, src[k], nchunks * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+                continue;
+            cnt[k][j] = 0;
+            for (uint32_t i = 0; i < nchunks; ++i) cnt[k][j] += (int32_t)(buf[i] - e) >= 0;
+        }
+    }
+    static const char *const names[4] = {"arrived from", "ready from", "mine at", "my ready at"};
+    size_t o = 0;
+    for (int k = 0; k < 4 && o < len; ++k) {
+        o += (size_t)snprintf(out + o, len - o, "%s%s [", k ? "; " : "", names[k]);
+        for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS && o < len; ++j)
+            o += (size_t)snprintf(out + o, len - o, "%s%d", j ? "," : "", cnt[k][j]);
+        if (o < len) o += (size_t)snprintf(out + o, len - o, "] of %u", nchunks);
+    }
+}
+
 static int mesh_piece(struct inccl_communicator *c, int kind16, const void *const *srcs, int R, void *dst, size_t n,
                       int k, const uint32_t *amax, int scale_R, int rs, hipStream_t st)
 {
@@ -231,19 +281,34 @@ static int mesh_piece(struct inccl_communicator *c, int kind16, const void *cons
     const int capturing = cap != hipStreamCaptureStatusNone;
     if (capturing && (!c->mesh_buf || c->mesh_cap < shard))   /* collective setup cannot run in a capture */
         return inccl_set_error(INCCL_ERR_STATE, "mesh: make one call of this size outside graph capture first");
-    int rc = mesh_ensure(c, shard);
-    if (rc) return rc;
-    const uint32_t err = *(volatile uint32_t *)c->mesh_err_host;
+    /* an earlier call's failure is reported before anything else, a regrow
+     * included (it would replace the error words) */
+    const uint32_t err = c->mesh_err_host ? *(volatile uint32_t *)c->mesh_err_host : 0;
     if (err & INCCL_MESH_ERR_BOUNDS)   /* the kernel's per-item bounds check (inccl_mesh.hip inside()) */
         return inccl_set_error(INCCL_ERR_STATE, "mesh: an earlier call stopped at its bounds check (item %u, peer %u; "
                                "results invalid)", (err >> 8) & 0xffu, (err >> 4) & 0xfu);
-    if (err) {   /* which wait expired (inccl_mesh.hip wait_flag) */
+    if (err) {   /* which wait expired, and this rank's progress (inccl_mesh.hip wait_flag) */
         const volatile uint32_t *e4 = (const volatile uint32_t *)c->mesh_err_host;
+        char pushes[96], flags[320], clock[160];
+        int o = 0;
+        for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS; ++j)
+            o += snprintf(pushes + o, sizeof(pushes) - (size_t)o, "%s%u", j ? "," : "", e4[6 + j]);
+        /* GPU clock (100 MHz / 16) in ms: timeout, call start, last push per destination */
+        o = snprintf(clock, sizeof(clock), "clock ms: timeout %.3f, start %.3f, last push to", e4[15] * 1.6e-4,
+                     e4[16] * 1.6e-4);
+        for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS && o < (int)sizeof(clock); ++j)
+            o += snprintf(clock + o, sizeof(clock) - (size_t)o, "%s%.3f", j ? "," : " ", e4[17 + j] * 1.6e-4);
+        mesh_flag_census(c, e4[2], e4[13], flags, sizeof(flags));
         return inccl_set_error(INCCL_ERR_STATE, "mesh: an earlier call timed out waiting for a peer (results invalid; "
-                               "rank %d, %s of chunk %u, peer %u: flag %u, waited for epoch %u; %u tickets taken)",
+                               "rank %d, %s of chunk %u, peer %u: flag %u, waited for epoch %u, re-read %u; "
+                               "%u tickets taken, %u workgroups started, %u retired of %d; pushes finished per "
+                               "destination [%s]; %u polls rescued; %s; %s)",
                                me, ((err >> 8) & 0xffu) == 3 ? "reduce's arrival flag" : "gather's ready flag",
-                               err >> 16, (err >> 4) & 0xfu, e4[1], e4[2], e4[3]);
+                               err >> 16, (err >> 4) & 0xfu, e4[1], e4[2], e4[14], e4[3], e4[4], e4[5], c->mesh_grid,
+                               pushes, e4[12], flags, clock);
     }
+    int rc = mesh_ensure(c, shard);
+    if (rc) return rc;
     const size_t chunk = mesh_chunk(c, shard);
     const int nchunks = (int)((shard + chunk - 1) / chunk);
     /* a reduce / gather starts `lag` slots after what it waits for.  Default: the
@@ -278,6 +343,7 @@ static int mesh_piece(struct inccl_communicator *c, int kind16, const void *cons
     l.own_resin = l.peer_resin[me];
     l.push_res = c->mesh_push;
     l.rs = rs;
+    l.rescue_every = c->mesh_rescue;
     l.own_inbox = l.peer_inbox[me];
     l.own_res = (uint32_t *)l.peer_res[me];
     l.own_sig = (const uint32_t *)c->mesh_buf;

@@ -275,9 +275,10 @@ def test_reduce_scatter_misaligned_dst_on_some_ranks(gpu, world, engine):
 def _mode_switch_rank(rank, world, port, q, shard_log2):
     """The mesh engines' kernel across mode switches on one communicator:
     allreduce <-> reduce-scatter, fp32 <-> bf16, mesh <-> meshw, and a regrow,
-    with exact fixed-point data (rank r's bucket is (r + 1) * b, b a multiple of
-    2^-12 with |b| < 1/2: every partial is exact at k = 20), so every call is
-    checked exactly without the oracle."""
+    with exact fixed-point data (rank r's bucket in step i is (r + 1) * m * b,
+    m = 1 + i % 3 and b a multiple of 2^-12 with |b| < 1/2: every partial is
+    exact at k = 20, and no step's partials equal the previous step's), so every
+    call is checked exactly without the oracle."""
     where = ["setup"]
     try:
         os.environ["INCCL_ENGINE"] = "mesh"
@@ -303,10 +304,10 @@ def _mode_switch_rank(rank, world, port, q, shard_log2):
             b = ((i % 4093) - 2046).to(torch.float32) * 2.0 ** -12
             x = b * float(rank + 1)
 
-            def want_of(dt):   # the exact sum of every rank's bucket as `dt`, rounded once to `dt`
+            def want_of(dt, m):   # the exact sum of every rank's bucket as `dt`, rounded once to `dt`
                 acc = torch.zeros(n, device=dev, dtype=torch.float32)
                 for r in range(world):
-                    acc += (b * float(r + 1)).to(dt).float()
+                    acc += (b * float((r + 1) * m)).to(dt).float()
                 return acc.to(dt)
 
             f32, b16 = torch.float32, torch.bfloat16
@@ -316,15 +317,16 @@ def _mode_switch_rank(rank, world, port, q, shard_log2):
                                                   ("mesh", "ar", f32)]):
                 where[0] = f"shard 2^{lg} step {step} ({eng} {op} {dt})"
                 comm.set_engine(eng)
-                src = x.to(dt)
+                m = 1 + step % 3   # a bucket unlike the previous step's: a partial read stale would show
+                src = (x * float(m)).to(dt)
                 torch.cuda.synchronize()   # src is made on torch's stream; the library runs on comm.stream
                 if op == "ar":
                     out = (comm.allreduce_f32([src], scale_exp=20, stream=comm.stream) if dt == torch.float32 else
                            comm.allreduce_bf16([src], out=torch.empty_like(src), scale_exp=20, stream=comm.stream))
-                    want = want_of(dt)
+                    want = want_of(dt, m)
                 else:
                     out = comm.reduce_scatter([src], scale_exp=20, stream=comm.stream)
-                    want = want_of(dt)[rank * shard:(rank + 1) * shard]
+                    want = want_of(dt, m)[rank * shard:(rank + 1) * shard]
                 torch.cuda.synchronize()
                 ok.append(bool(torch.equal(out, want)))
             comm.ipc_mem_kind("mesh")

@@ -6,8 +6,9 @@ the wait it was (inccl_mesh.hip wait_flag).  Started per rank from a shell
     python tools/mesh_stress_probe.py RANK PORT W MODE CALLS LOG2 [LOG2 ...]
 
 MODE: ar (mesh allreduce fp32), rs (mesh reduce-scatter fp32), mix (the two
-alternating), w (meshw allreduce).  Rank r's bucket is (r + 1) * b with b a
-multiple of 2^-12 below 1/2: exact at k = 20.  One JSON line per rank: calls
+alternating), w (meshw allreduce).  Rank r's bucket in call i is (r + 1) * m * b
+with m = 1 + i % 3 and b a multiple of 2^-12 below 1/2: exact at k = 20, and
+different from the previous call's.  One JSON line per rank: calls
 made, wrong calls, and the first error (a timeout names its wait)."""
 import json
 import os
@@ -37,20 +38,22 @@ def main():
             n = world * shard
             i = torch.arange(n, device=dev, dtype=torch.int64)
             b = ((i % 4093) - 2046).to(torch.float32) * 2.0 ** -12
-            x = b * float(rank + 1)
-            full = b * float(world * (world + 1) // 2)
-            mine = full[rank * shard:(rank + 1) * shard]
+            # three buckets that differ call to call (m = 1, 2, 3), so a partial
+            # read stale from the previous call cannot pass as the right one
+            xs = [b * float((rank + 1) * m) for m in (1, 2, 3)]
+            fulls = [b * float(world * (world + 1) // 2 * m) for m in (1, 2, 3)]
             torch.cuda.synchronize()
             for call in range(calls):
                 rs = mode == "rs" or (mode == "mix" and call % 2 == 1)
+                x, full = xs[call % 3], fulls[call % 3]
                 if rs:
                     out = comm.reduce_scatter([x], scale_exp=20, stream=comm.stream)
                 else:
                     out = comm.allreduce_f32([x], scale_exp=20, stream=comm.stream)
                 torch.cuda.synchronize()
                 made += 1
-                wrong += 0 if torch.equal(out, mine if rs else full) else 1
-            del i, b, x, full, mine
+                wrong += 0 if torch.equal(out, full[rank * shard:(rank + 1) * shard] if rs else full) else 1
+            del i, b, xs, fulls
         if comm.clear_error():   # a timeout of the last call is reported here
             err = "the last call timed out"
     except Exception as e:  # noqa: BLE001
