@@ -149,18 +149,30 @@ __device__ bool wait_flag(const MeshArgs& a, const uint32_t* f, uint32_t epoch, 
 {
     const uint64_t t0 = now_ticks();
     uint32_t v;
+    // tallies (all calls): waits ended by the RMW (ctr[6]), by the control load
+    // (ctr[7]); of those that had lasted over 1 ms: by a poll (ctr[25]), by the
+    // control load (ctr[24]), by the RMW (ctr[5])
+    constexpr uint64_t kLong = 100000;   // 1 ms of s_memrealtime
     for (uint32_t spin = 1;; ++spin) {
-        if ((int32_t)((v = ld_sys(f)) - epoch) >= 0) break;
+        if ((int32_t)((v = ld_sys(f)) - epoch) >= 0) {
+            if (spin > 1 && now_ticks() - t0 > kLong)
+                __hip_atomic_fetch_add(a.ctr + 25, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
         if (a.rescue_every && (spin & (a.rescue_every - 1u)) == 0u) {
             // control: a second load straight away (a flag landing between two
             // polls ends the wait here as often as at the RMW below)
             if ((int32_t)((v = ld_sys(f)) - epoch) >= 0) {
                 __hip_atomic_fetch_add(a.ctr + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (now_ticks() - t0 > kLong)
+                    __hip_atomic_fetch_add(a.ctr + 24, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
             if ((int32_t)((v = __hip_atomic_fetch_add(const_cast<uint32_t*>(f), a.zero, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_SYSTEM)) - epoch) >= 0) {
                 __hip_atomic_fetch_add(a.ctr + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (now_ticks() - t0 > kLong)
+                    __hip_atomic_fetch_add(a.ctr + 5, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
         }

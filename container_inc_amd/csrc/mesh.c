@@ -57,11 +57,11 @@ void inccl_mesh_release(struct inccl_communicator *c)
     if (!c->mesh_buf && !c->mesh_reg[1] && !c->mesh_reg[2] && !c->mesh_reg[3]) return;
     hipDeviceSynchronize();
     if (c->mesh_buf && getenv("INCCL_MESH_STATS")) {   /* flag polls a read-modify-write ended (inccl_mesh.hip) */
-        uint32_t r[2] = {0, 0};
-        if (hipMemcpy(r, c->mesh_buf + MESH_CTR_OFFSET + 6 * sizeof(uint32_t), sizeof(r), hipMemcpyDeviceToHost) ==
-            hipSuccess)
-            fprintf(stderr, "inccl mesh rank %d: %u flag polls rescued by a read-modify-write, %u ended by the "
-                    "control load before it\n", me, r[0], r[1]);
+        uint32_t r[32];
+        if (hipMemcpy(r, c->mesh_buf + MESH_CTR_OFFSET, sizeof(r), hipMemcpyDeviceToHost) == hipSuccess)
+            fprintf(stderr, "inccl mesh rank %d: waits ended by a read-modify-write %u, by the control load before it "
+                    "%u; waits over 1 ms ended by a poll %u, by the control load %u, by a read-modify-write %u\n", me,
+                    r[6], r[7], r[25], r[24], r[5]);
     }
     for (int r = 0; r < INCCL_MESH_REGIONS; ++r) {
         for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS; ++j) {

@@ -3,7 +3,10 @@ one mode sequence, every call checked exactly, a timed-out wait reported with
 the wait it was (inccl_mesh.hip wait_flag).  Started per rank from a shell
 (tools/gpu_mesh_stress.sh), so no launcher forks after GPU init.
 
-    python tools/mesh_stress_probe.py RANK PORT W MODE CALLS LOG2 [LOG2 ...]
+    python tools/mesh_stress_probe.py RANK PORT W MODE CALLS LOG2 [LOG2 ...] [--concurrent]
+
+--concurrent: while each call's kernel runs, W + 1 elementwise torch kernels
+over the bucket on torch's stream (what the tests' expected-value code does).
 
 MODE: ar (mesh allreduce fp32), rs (mesh reduce-scatter fp32), mix (the two
 alternating), w (meshw allreduce).  Rank r's bucket in call i is (r + 1) * m * b
@@ -21,7 +24,8 @@ sys.path.insert(0, ROOT)
 def main():
     rank, port, world, mode, calls = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4],
                                       int(sys.argv[5]))
-    logs = [int(v) for v in sys.argv[6:]] or [20]
+    concurrent = "--concurrent" in sys.argv
+    logs = [int(v) for v in sys.argv[6:] if not v.startswith("--")] or [20]
     os.environ["INCCL_ENGINE"] = "meshw" if mode == "w" else "mesh"
     os.environ["INCCL_DEVICE"] = "0"
     os.environ.setdefault("INCCL_BOOT_TIMEOUT", "120")
@@ -50,6 +54,11 @@ def main():
                     out = comm.reduce_scatter([x], scale_exp=20, stream=comm.stream)
                 else:
                     out = comm.allreduce_f32([x], scale_exp=20, stream=comm.stream)
+                if concurrent:   # torch work on its own stream while the mesh kernel runs (as the tests' checks)
+                    acc = torch.zeros_like(x)
+                    for r in range(world):
+                        acc += b * float(r + 1)
+                    del acc
                 torch.cuda.synchronize()
                 made += 1
                 wrong += 0 if torch.equal(out, full[rank * shard:(rank + 1) * shard] if rs else full) else 1
