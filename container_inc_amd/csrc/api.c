@@ -597,21 +597,7 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     c->window_size = WINDOW_SIZE;                /* api.c:226 */
     INCCL_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     INCCL_HIP(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
-    /* The host paths' H2D and D2H streams are high-priority streams: those come
-     * from their own hardware-queue pool.  Created as normal streams after the
-     * process had already launched work (e.g. torch tensors made first), the
-     * H2D and D2H copies of config 3 ran one after the other (28 GB/s instead
-     * of 44-46 GB/s both ways at once; tools/host_pipe_probe.py).
-     * $INCCL_COPY_STREAMS=default keeps normal priority. */
-    const char *cse = getenv("INCCL_COPY_STREAMS");
-    int prio_lo = 0, prio_hi = 0;
-    INCCL_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    for (int i = 0; i < 2; ++i) {
-        if (cse && strcmp(cse, "default") == 0)
-            INCCL_HIP(hipStreamCreateWithFlags(&c->copy_streams[i], hipStreamNonBlocking));
-        else
-            INCCL_HIP(hipStreamCreateWithPriority(&c->copy_streams[i], hipStreamNonBlocking, prio_hi));
-    }
+    /* the host paths' copy streams are made on their first use (copy_streams_ensure) */
     for (int i = 0; i < 10; ++i) INCCL_HIP(hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming));
     INCCL_HIP(hipMalloc((void **)&c->d_words, 256));
     INCCL_HIP(hipMemset(c->d_words, 0, 256));
@@ -630,10 +616,6 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     const char *mle = getenv("INCCL_MESH_LAG");
     c->mesh_lag_env = mle ? atoi(mle) : 0;
     if (c->mesh_lag_env < 0) c->mesh_lag_env = 0;
-    const char *mre = getenv("INCCL_MESH_RESCUE");   /* 0: flag polls are loads only (diagnostics) */
-    c->mesh_rescue = mre ? atoi(mre) : 16;
-    if (c->mesh_rescue < 0) c->mesh_rescue = 16;
-    while (c->mesh_rescue & (c->mesh_rescue - 1)) c->mesh_rescue &= c->mesh_rescue - 1;   /* a power of two */
     const char *hce = getenv("INCCL_HOST_CHUNK_MIB");
     c->host_chunk_mib = hce ? atoi(hce) : 0;
     if (c->host_chunk_mib < 1 || c->host_chunk_mib > 1024) c->host_chunk_mib = 16;
@@ -1427,13 +1409,40 @@ int inccl_reduce_scatter_f16(struct inccl_communicator *c, const uint16_t *const
  * become large chunks staged through the pinned send/receive buffers, the
  * sum runs on the GPU (RCCL or the local hub's sum kernel), and the same
  * "whole messages only" rule applies. */
+/* The host paths' H2D and D2H streams, made on a communicator's first host-
+ * path call.  They are high-priority streams: those come from their own
+ * hardware-queue pool.  Created as normal streams after the process had
+ * already launched work (e.g. torch tensors made first), the H2D and D2H copies
+ * of config 3 ran one after the other (28 GB/s instead of 44-46 GB/s both ways
+ * at once; tools/host_pipe_probe.py).  Not at creation: a high-
+ * priority hardware queue held by any process on a GPU stalled the mesh
+ * engines' persistent kernels of four other processes on that GPU for seconds
+ * at a time (DESIGN.md "Mesh reduce-scatter route", liveness), so a
+ * communicator that never uses the host paths holds none.
+ * $INCCL_COPY_STREAMS=default keeps normal priority. */
+static int copy_streams_ensure(struct inccl_communicator *c)
+{
+    if (c->copy_streams[0] && c->copy_streams[1]) return 0;
+    const char *cse = getenv("INCCL_COPY_STREAMS");
+    int prio_lo = 0, prio_hi = 0;
+    INCCL_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    for (int i = 0; i < 2; ++i) {
+        if (c->copy_streams[i]) continue;
+        if (cse && strcmp(cse, "default") == 0)
+            INCCL_HIP(hipStreamCreateWithFlags(&c->copy_streams[i], hipStreamNonBlocking));
+        else
+            INCCL_HIP(hipStreamCreateWithPriority(&c->copy_streams[i], hipStreamNonBlocking, prio_hi));
+    }
+    return 0;
+}
+
 /* Grow the pinned staging (the reference's 2*size registered buffers) so each
  * ping-pong half holds `half_bytes`. */
 static int ensure_staging(struct inccl_communicator *c, size_t half_bytes)
 {
     if ((size_t)c->payload_buf_size >= 2 * half_bytes && c->send_payload) return 0;
-    INCCL_HIP(hipStreamSynchronize(c->copy_streams[0]));
-    INCCL_HIP(hipStreamSynchronize(c->copy_streams[1]));
+    if (c->copy_streams[0]) INCCL_HIP(hipStreamSynchronize(c->copy_streams[0]));
+    if (c->copy_streams[1]) INCCL_HIP(hipStreamSynchronize(c->copy_streams[1]));
     if (c->send_payload) hipHostFree(c->send_payload);
     if (c->receive_payload) hipHostFree(c->receive_payload);
     c->send_payload = c->receive_payload = NULL;
@@ -1465,8 +1474,8 @@ int inccl_host_deregister(struct inccl_communicator *c, void *ptr)
     if (!c || !ptr) return inccl_set_error(INCCL_ERR_ARG, "bad host_deregister args");
     for (int i = 0; i < c->nreg; ++i)
         if (c->reg[i].p == (char *)ptr) {
-            INCCL_HIP(hipStreamSynchronize(c->copy_streams[0]));
-            INCCL_HIP(hipStreamSynchronize(c->copy_streams[1]));
+            if (c->copy_streams[0]) INCCL_HIP(hipStreamSynchronize(c->copy_streams[0]));
+            if (c->copy_streams[1]) INCCL_HIP(hipStreamSynchronize(c->copy_streams[1]));
             INCCL_HIP(hipHostUnregister(ptr));
             c->reg[i] = c->reg[--c->nreg];
             return 0;
@@ -1528,6 +1537,8 @@ static int allreduce_host_q32_direct(struct inccl_communicator *c, const int32_t
     if (pageable && !c->d2h) c->d2h = inccl_d2h_worker_create(c->group->device);
     struct inccl_d2h_worker *w = pageable ? c->d2h : NULL;   /* NULL: D2Hs issued here */
     int32_t *d[2] = {(int32_t *)c->d_stage, (int32_t *)c->d_stage + CH};
+    rc = copy_streams_ensure(c);
+    if (rc) return rc;
     hipStream_t h2d = c->copy_streams[0], d2h = c->copy_streams[1], ks = c->stream;
     hipEvent_t e_h2d[2] = {c->ev[0], c->ev[1]}, e_ar[2] = {c->ev[2], c->ev[3]}, e_d2h[2] = {c->ev[4], c->ev[5]};
     INCCL_HIP(hipStreamSynchronize(ks));
@@ -1607,6 +1618,8 @@ static int allreduce_host_q32(struct inccl_communicator *c, const int32_t *src, 
     int32_t *d[2] = {(int32_t *)c->d_stage, (int32_t *)c->d_stage + CH};
     char *in[2] = {c->send_payload, c->send_payload + chunk_bytes};
     char *out[2] = {c->receive_payload, c->receive_payload + chunk_bytes};
+    rc = copy_streams_ensure(c);
+    if (rc) return rc;
     hipStream_t h2d = c->copy_streams[0], d2h = c->copy_streams[1], ks = c->stream;
     hipEvent_t e_h2d[2] = {c->ev[0], c->ev[1]}, e_ar[2] = {c->ev[2], c->ev[3]}, e_d2h[2] = {c->ev[4], c->ev[5]};
     INCCL_HIP(hipStreamSynchronize(ks));
@@ -1675,6 +1688,8 @@ int inccl_allreduce_f32_host(struct inccl_communicator *c, const float *src_host
     if (rc) return rc;
     float *in[2] = {(float *)c->d_stage, (float *)c->d_stage + B};
     float *out[2] = {(float *)c->d_stage + 2 * B, (float *)c->d_stage + 3 * B};
+    rc = copy_streams_ensure(c);
+    if (rc) return rc;
     hipStream_t h2d = c->copy_streams[0], d2h = c->copy_streams[1], ks = c->stream;
     hipEvent_t ev_h2d[2] = {c->ev[0], c->ev[1]}, ev_k[2] = {c->ev[2], c->ev[3]}, ev_d2h[2] = {c->ev[4], c->ev[5]};
     /* pageable dst: its D2Hs come from the helper thread (hostdma.c), or each one

@@ -104,7 +104,6 @@ struct inccl_communicator {
     int force_sharded;           /* INCCL_FORCE_SHARDED: test hook, the sharded paths even at world 1 */
     size_t mesh_chunk_env;       /* INCCL_MESH_CHUNK elements (0: mesh.c's default) */
     int mesh_lag_env;            /* INCCL_MESH_LAG slots (0: the whole shard) */
-    int mesh_rescue;             /* INCCL_MESH_RESCUE: a poll's read-modify-write every this many (0: never) */
     int host_chunk_mib;          /* INCCL_HOST_CHUNK_MIB: host pipeline chunk (default 16) */
     /* every knob above that picks a route or a schedule is agreed over the
      * group when the communicator is created (api.c agree_knobs): ranks whose

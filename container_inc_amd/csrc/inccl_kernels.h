@@ -90,8 +90,6 @@ struct inccl_mesh_launch {
     int push_res;                                      /* 1: reduce pushes results, gather copies locally */
     int rs;                                            /* 1: reduce-scatter -- dst is this rank's shard */
     int kind16;                                        /* 0: fp32 src / dst; INCCL_KIND_BF16 / _F16: 2-byte ones */
-    int rescue_every;                                  /* a flag poll's read-modify-write every this many polls
-                                                          (a power of two; 0: loads only) */
     uint32_t *peer_sig[INCCL_MAX_LOCAL_INPUTS];        /* every rank's signal array */
     const uint32_t *own_sig;
     uint32_t *ctr;                                     /* own words: calls, retired, ticket, abort */

@@ -85,7 +85,6 @@ struct MeshArgs {
     uint32_t* peer_sig[kMaxR];           // rank j's signal array ([me] = own)
     const uint32_t* own_sig;
     uint32_t* ctr;                       // [0] calls done, [1] retired, [2] ticket, [3] abort, [4] started,
-                                         // [6] polls rescued, [7] ended by the control load (all calls),
                                          // [8 + j] pushes to rank j finished; 64-bit at [32]: call start,
                                          // [34 + 2 j]: last push flag store to rank j (s_memrealtime)
                                          // (this call)
@@ -96,9 +95,7 @@ struct MeshArgs {
                                          // shard), the other gathers only wait
     Scale sc;
     uint64_t src_bytes, dst_bytes, inbox_bytes, res_bytes, resin_bytes;   // region sizes (bounds check)
-    uint32_t zero;                       // 0 (wait_flag's read-modify-write operand)
-    uint32_t rescue_every;               // wait_flag: a read-modify-write every this many polls (a power of
-                                         // two; 0: never)
+    uint32_t zero;                       // 0, opaque to the compiler (which turns an idempotent RMW into a load)
 };
 
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
@@ -131,51 +128,16 @@ __device__ __forceinline__ int ready_idx(int j, int c) { return (kMaxR + j) * IN
 // | peer << 4 | chunk << 16 (item 3: a reduce's arrival flag, 6: a gather's ready
 // flag), err[1] = the flag's last value, err[2] = the epoch waited for, err[3] =
 // the tickets this rank's workgroups had taken, err[4] / err[5] = its workgroups
-// started / retired, err[6 + j] = its pushes to rank j finished, err[12] = the
-// polls rescued so far, err[13] = the call's chunks, err[14] = the flag re-read
-// by a read-modify-write, err[15] / err[16] / err[17 + j] = the clock (/16) at
-// the timeout, at the call's start, at the last push flag store to rank j.
-//
-// The poll is a system-scope load, and every 16th poll (a.rescue_every,
-// $INCCL_MESH_RESCUE) a read-modify-write
-// (add a.zero: 0, but opaque to the compiler, which would turn an idempotent
-// RMW into a load).  A load alone can keep returning an old value after the
-// peer's store has reached memory: four ranks on one GPU deadlocked that way
-// (DESIGN.md "Mesh reduce-scatter route": the timed-out poll read 6 for 30 s,
-// the host then read 7 in every flag).  The RMW is performed at the memory
-// side; a wait it ends adds one to ctr[6] (kept across calls), and to ctr[7]
-// when one more load after it still returns the old value.
+// started / retired, err[6 + j] = its pushes to rank j finished, err[13] = the
+// call's chunks, err[14] = the flag re-read by a read-modify-write, err[15] /
+// err[16] / err[17 + j] = the clock (/16) at the timeout, at the call's start,
+// at the last push flag store to rank j.  (DESIGN.md "Mesh reduce-scatter
+// route", liveness: what these told apart.)
 __device__ bool wait_flag(const MeshArgs& a, const uint32_t* f, uint32_t epoch, uint32_t item, int peer, int c)
 {
     const uint64_t t0 = now_ticks();
     uint32_t v;
-    // tallies (all calls): waits ended by the RMW (ctr[6]), by the control load
-    // (ctr[7]); of those that had lasted over 1 ms: by a poll (ctr[25]), by the
-    // control load (ctr[24]), by the RMW (ctr[5])
-    constexpr uint64_t kLong = 100000;   // 1 ms of s_memrealtime
-    for (uint32_t spin = 1;; ++spin) {
-        if ((int32_t)((v = ld_sys(f)) - epoch) >= 0) {
-            if (spin > 1 && now_ticks() - t0 > kLong)
-                __hip_atomic_fetch_add(a.ctr + 25, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-        }
-        if (a.rescue_every && (spin & (a.rescue_every - 1u)) == 0u) {
-            // control: a second load straight away (a flag landing between two
-            // polls ends the wait here as often as at the RMW below)
-            if ((int32_t)((v = ld_sys(f)) - epoch) >= 0) {
-                __hip_atomic_fetch_add(a.ctr + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (now_ticks() - t0 > kLong)
-                    __hip_atomic_fetch_add(a.ctr + 24, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            if ((int32_t)((v = __hip_atomic_fetch_add(const_cast<uint32_t*>(f), a.zero, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_SYSTEM)) - epoch) >= 0) {
-                __hip_atomic_fetch_add(a.ctr + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (now_ticks() - t0 > kLong)
-                    __hip_atomic_fetch_add(a.ctr + 5, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
+    while ((int32_t)((v = ld_sys(f)) - epoch) < 0) {
         if (__hip_atomic_load(a.ctr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
         if (now_ticks() - t0 > a.timeout_ticks) {
             __hip_atomic_store(a.err + 1, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -206,8 +168,6 @@ __device__ bool wait_flag(const MeshArgs& a, const uint32_t* f, uint32_t epoch, 
                 __hip_atomic_store(a.err + 17 + j,
                                    (uint32_t)(__hip_atomic_load(t64 + 1 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 4),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(a.err + 12, __hip_atomic_load(a.ctr + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(a.err + 14,
                                __hip_atomic_fetch_add(const_cast<uint32_t*>(f), a.zero, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_SYSTEM),
@@ -648,8 +608,6 @@ extern "C" int inccl_k_mesh(const struct inccl_mesh_launch* l, void* stream)
     a.res_bytes = l->res_bytes;
     a.resin_bytes = l->resin_bytes;
     a.zero = 0;
-    a.rescue_every = l->rescue_every > 0 ? (uint32_t)l->rescue_every : 0u;
-    if (a.rescue_every & (a.rescue_every - 1u)) return INCCL_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     const dim3 g((unsigned)l->grid), b(kMeshBlock);
 #define INCCL_MESH_CASE(RR)                                                  \

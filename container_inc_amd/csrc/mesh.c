@@ -13,8 +13,8 @@
  * single export needs to exceed the group's IPC bound; see runtime.c):
  *   sig    [0, 64 KiB) signal array: arrive[8][1024] and ready[8][1024] words;
  *          [64 KiB, +256) call counter, retired workgroups, ticket, abort word,
- *          started workgroups, polls rescued, pushes finished per destination,
- *          clock readings (inccl_mesh.hip MeshArgs::ctr)
+ *          started workgroups, pushes finished per destination, clock
+ *          readings (inccl_mesh.hip MeshArgs::ctr)
  *   inbox  W * cap int32: slot j holds rank j's partial of my shard
  *   res    cap fp32: my dequantised result shard
  *   resin  W * cap fp32 ("meshw"): slot j holds rank j's result shard
@@ -56,13 +56,6 @@ void inccl_mesh_release(struct inccl_communicator *c)
     const int W = c->group->world_size, me = c->group->rank;
     if (!c->mesh_buf && !c->mesh_reg[1] && !c->mesh_reg[2] && !c->mesh_reg[3]) return;
     hipDeviceSynchronize();
-    if (c->mesh_buf && getenv("INCCL_MESH_STATS")) {   /* flag polls a read-modify-write ended (inccl_mesh.hip) */
-        uint32_t r[32];
-        if (hipMemcpy(r, c->mesh_buf + MESH_CTR_OFFSET, sizeof(r), hipMemcpyDeviceToHost) == hipSuccess)
-            fprintf(stderr, "inccl mesh rank %d: waits ended by a read-modify-write %u, by the control load before it "
-                    "%u; waits over 1 ms ended by a poll %u, by the control load %u, by a read-modify-write %u\n", me,
-                    r[6], r[7], r[25], r[24], r[5]);
-    }
     for (int r = 0; r < INCCL_MESH_REGIONS; ++r) {
         for (int j = 0; j < W && j < INCCL_MAX_LOCAL_INPUTS; ++j) {
             if (j != me && c->mesh_peer[r][j]) hipIpcCloseMemHandle(c->mesh_peer[r][j]);
@@ -302,10 +295,10 @@ static int mesh_piece(struct inccl_communicator *c, int kind16, const void *cons
         return inccl_set_error(INCCL_ERR_STATE, "mesh: an earlier call timed out waiting for a peer (results invalid; "
                                "rank %d, %s of chunk %u, peer %u: flag %u, waited for epoch %u, re-read %u; "
                                "%u tickets taken, %u workgroups started, %u retired of %d; pushes finished per "
-                               "destination [%s]; %u polls rescued; %s; %s)",
+                               "destination [%s]; %s; %s)",
                                me, ((err >> 8) & 0xffu) == 3 ? "reduce's arrival flag" : "gather's ready flag",
                                err >> 16, (err >> 4) & 0xfu, e4[1], e4[2], e4[14], e4[3], e4[4], e4[5], c->mesh_grid,
-                               pushes, e4[12], flags, clock);
+                               pushes, flags, clock);
     }
     int rc = mesh_ensure(c, shard);
     if (rc) return rc;
@@ -343,7 +336,6 @@ static int mesh_piece(struct inccl_communicator *c, int kind16, const void *cons
     l.own_resin = l.peer_resin[me];
     l.push_res = c->mesh_push;
     l.rs = rs;
-    l.rescue_every = c->mesh_rescue;
     l.own_inbox = l.peer_inbox[me];
     l.own_res = (uint32_t *)l.peer_res[me];
     l.own_sig = (const uint32_t *)c->mesh_buf;
