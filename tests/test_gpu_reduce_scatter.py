@@ -282,10 +282,11 @@ def _mode_switch_rank(rank, world, port, q, shard_log2):
     where = ["setup"]
     try:
         os.environ["INCCL_ENGINE"] = "mesh"
-        # a bounded wait here is a liveness check, not a latency one: four ranks
-        # time-slice one GPU, and a first run of this test saw one 5 s wait
-        # expire (DESIGN.md "Mesh reduce-scatter route"); a deadlock still fails,
-        # with the expired wait named in the error
+        # the bounded wait is a liveness check, not a latency one: four ranks
+        # share one GPU, and while another process held high-priority queues on
+        # it they were time-sliced and a wait expired (DESIGN.md "Mesh
+        # reduce-scatter route", liveness); a stall still fails, with the
+        # expired wait, the ranks' progress and the raised flags in the error
         os.environ["INCCL_LL_TIMEOUT_MS"] = "30000"
         os.environ["INCCL_DEVICE"] = "0"
         os.environ["INCCL_BOOT_TIMEOUT"] = "120"
