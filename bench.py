@@ -1289,7 +1289,7 @@ def host_e2e(comm, k: int, gib: int = 1, bucket_mib: int = 64, world: int = 1) -
     # this box's PCIe ceiling on the same pinned buffers: H2D alone, D2H alone,
     # and both at once on two streams (what the pipeline overlaps).  The streams
     # have the greatest priority, as the pipeline's copy streams do (api.c
-    # comm_init): normal-priority ones can serialise the two directions, which
+    # copy_streams_ensure): normal-priority ones can serialise the two directions, which
     # would make this "ceiling" lower than the pipeline itself.
     dev = torch.device("cuda", torch.cuda.current_device())
     m = (bucket_mib << 20) // 4

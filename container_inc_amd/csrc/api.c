@@ -581,6 +581,8 @@ static int agree_knobs(struct inccl_communicator *c, const char *eng)
     return rc;
 }
 
+static int copy_streams_ensure(struct inccl_communicator *c);
+
 static int comm_init(struct inccl_communicator *c, uint32_t size)
 {
     struct inccl_group *g = c->group;
@@ -597,7 +599,12 @@ static int comm_init(struct inccl_communicator *c, uint32_t size)
     c->window_size = WINDOW_SIZE;                /* api.c:226 */
     INCCL_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     INCCL_HIP(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
-    /* the host paths' copy streams are made on their first use (copy_streams_ensure) */
+    /* the host paths' copy streams (copy_streams_ensure): made here for a
+     * one-rank communicator, on first use otherwise */
+    if (g->world_size == 1) {
+        int rc_cs = copy_streams_ensure(c);
+        if (rc_cs) return rc_cs;
+    }
     for (int i = 0; i < 10; ++i) INCCL_HIP(hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming));
     INCCL_HIP(hipMalloc((void **)&c->d_words, 256));
     INCCL_HIP(hipMemset(c->d_words, 0, 256));
@@ -1409,17 +1416,17 @@ int inccl_reduce_scatter_f16(struct inccl_communicator *c, const uint16_t *const
  * become large chunks staged through the pinned send/receive buffers, the
  * sum runs on the GPU (RCCL or the local hub's sum kernel), and the same
  * "whole messages only" rule applies. */
-/* The host paths' H2D and D2H streams, made on a communicator's first host-
- * path call.  They are high-priority streams: those come from their own
- * hardware-queue pool.  Created as normal streams after the process had
- * already launched work (e.g. torch tensors made first), the H2D and D2H copies
- * of config 3 ran one after the other (28 GB/s instead of 44-46 GB/s both ways
- * at once; tools/host_pipe_probe.py).  Not at creation: a high-
- * priority hardware queue held by any process on a GPU stalled the mesh
- * engines' persistent kernels of four other processes on that GPU for seconds
- * at a time (DESIGN.md "Mesh reduce-scatter route", liveness), so a
- * communicator that never uses the host paths holds none.
- * $INCCL_COPY_STREAMS=default keeps normal priority. */
+/* The host paths' H2D and D2H streams.  They are high-priority streams: those
+ * come from their own hardware-queue pool.  Created as normal streams after the
+ * process had already launched work (e.g. torch tensors made first), the H2D
+ * and D2H copies of config 3 ran one after the other (28 GB/s instead of
+ * 44-46 GB/s both ways at once; tools/host_pipe_probe.py).
+ * When: a one-rank communicator makes them at creation (made after the
+ * process's big allocations they ran the pipeline at 44 instead of 45.7 GB/s);
+ * a multi-rank one on its first host-path call, because high-priority queues
+ * held by the processes sharing a GPU stalled their mesh engines' persistent
+ * kernels for seconds at a time (DESIGN.md "Mesh reduce-scatter route",
+ * liveness).  $INCCL_COPY_STREAMS=default keeps normal priority. */
 static int copy_streams_ensure(struct inccl_communicator *c)
 {
     if (c->copy_streams[0] && c->copy_streams[1]) return 0;

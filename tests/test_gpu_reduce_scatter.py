@@ -347,6 +347,29 @@ def test_mesh_mode_switches(gpu, world, shard_log2):
     _run_mp(world, _mode_switch_rank, shard_log2)
 
 
+def test_mesh_w4_beside_a_live_communicator(gpu):
+    """Liveness regression (DESIGN.md "Mesh reduce-scatter route", liveness):
+    this process keeps a one-rank communicator (which holds the host paths'
+    high-priority copy streams) alive while four rank processes run the
+    mode-switch sequence on the same GPU.  While every communicator created
+    those streams at creation, the ranks included, this took 54-93 s or timed
+    out (the ranks' persistent kernels time-sliced); now a multi-rank
+    communicator makes them on its first host-path call, and it takes about
+    3 s."""
+    import time
+    from container_inc_amd import inccl
+    grp = inccl.inccl_group_create_local(1, 0, "liveness")
+    comm = inccl.inccl_communicator_create(grp, 0)
+    try:
+        t0 = time.monotonic()
+        _run_mp(4, _mode_switch_rank, 22)
+        took = time.monotonic() - t0
+        assert took < 30, f"four ranks took {took:.1f} s beside a live communicator"
+    finally:
+        comm.destroy()
+        grp.destroy()
+
+
 def test_calls_on_alternating_streams(gpu, orc):
     """A communicator's calls share its workspaces (int32 partials, the auto
     scale's word): back-to-back calls on two streams, no host sync between them,
