@@ -1420,9 +1420,17 @@ def main():
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["INCCL_BENCH_WATCHDOG"]), repeat=True)
     # rehearsal hook: every rank on device 0 (a one-GPU box running N>1 over the
-    # p2p engine; RCCL refuses two ranks on one GPU)
+    # p2p engine; RCCL refuses two ranks on one GPU).  Each rank then opens two
+    # hardware queues, not HIP's default four (set before this process's first
+    # HIP call): eight processes x four queues oversubscribe the GPU's queue
+    # slots, and the scheduler time-slices the ranks -- the 8-rank rehearsal
+    # step took 23.2 ms with four and 2.26 ms with two (DESIGN.md "Mesh
+    # reduce-scatter route", liveness).  Never on the driver's one-process-per-
+    # GPU runs.  ($INCCL_BENCH_REHEARSAL_HW_QUEUES: another count.)
     if os.environ.get("INCCL_BENCH_SAME_DEVICE") == "1":
         local_rank = 0
+        if world > 1:
+            os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("INCCL_BENCH_REHEARSAL_HW_QUEUES", "2")
     os.environ.setdefault("INCCL_BOOT_TIMEOUT", "120")
     # an ll / mesh candidate whose peer never arrives costs 2 s, not 5
     os.environ.setdefault("INCCL_LL_TIMEOUT_MS", "2000")
@@ -1718,6 +1726,8 @@ def main():
                 "chunks": chunks,
                 "engine": m["engine"],
                 "engine_env": (m["env"] or None) if world > 1 else None,
+                "same_device_rehearsal": ({"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")}
+                                          if os.environ.get("INCCL_BENCH_SAME_DEVICE") == "1" and world > 1 else None),
                 "engine_tuning": tuning or None,
                 "shard_elems": chunk_plan(n, world, chunks)[0][2] if world > 1 else n,
             },
