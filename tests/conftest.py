@@ -65,4 +65,10 @@ def gpu():
     if not os.path.exists(cia.LIB_PATH):
         cia.build()
     cia.load()
+    # The multi-process tests put every rank on this one GPU.  Processes started
+    # from here on (this process's HIP runtime is already up, so it keeps its
+    # own count) open two hardware queues each instead of four: eight ranks x
+    # four queues oversubscribe the GPU's queue slots and the scheduler time-
+    # slices the ranks (DESIGN.md "Mesh reduce-scatter route", liveness).
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("INCCL_TEST_RANK_HW_QUEUES", "2")
     return torch.device("cuda:0")

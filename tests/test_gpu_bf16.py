@@ -202,6 +202,7 @@ def _p2p_rank(rank, world, port, q, engine="p2p"):
             if k != "auto":   # prepared (inccl_op_create_allreduce16), run twice on fresh inputs
                 srcs = [_dev(h, dev) for h in hs[rank]]
                 out.fill_(float("nan"))
+                torch.cuda.synchronize()   # inputs and out made on torch's stream; op() runs on comm.stream
                 op = comm.prepare_allreduce_bf16(srcs, out=out, scale_exp=k, stream=comm.stream)
                 for _ in range(2):
                     op()

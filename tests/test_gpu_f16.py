@@ -194,6 +194,7 @@ def _ipc_rank(rank, world, port, q, engine):
             if k != "auto":   # prepared (inccl_op_create_allreduce16), run twice on fresh inputs
                 srcs = [_dev(h, dev) for h in hs[rank]]
                 out.fill_(float("nan"))
+                torch.cuda.synchronize()   # inputs and out made on torch's stream; op() runs on comm.stream
                 op = comm.prepare_allreduce_f16(srcs, out=out, scale_exp=k, stream=comm.stream)
                 for _ in range(2):
                     op()
