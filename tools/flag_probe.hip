@@ -1,7 +1,7 @@
 // flag_probe.hip -- does a polling load see a flag another workgroup stored?
 //
-// The question behind the mesh engine's rescue poll (inccl_mesh.hip
-// wait_flag, DESIGN.md "Mesh reduce-scatter route"): a reader workgroup loads a
+// Asked while the mesh engine's W = 4 one-GPU stalls were open (DESIGN.md "Mesh
+// reduce-scatter route", liveness: they were not stale loads): a reader workgroup loads a
 // flag word (system-scope load, as the mesh kernel polls), so that the word's
 // line is warm; then it tells a writer workgroup to go; the writer waits a
 // little and stores the next value (system-scope store, as the mesh kernel's
