@@ -416,6 +416,18 @@ def test_engine_peer_timeout(gpu, engine):
     assert all(res[0][0].values()) and all(res[1][0].values()), res
     assert res[1][1] is None, res
     assert res[0][1] is not None and "timed out" in res[0][1], res
+    if engine in ("mesh", "meshw"):
+        # the report (DESIGN.md "Mesh reduce-scatter route", liveness): the
+        # expired wait, the rank's progress, and the flag census -- one chunk
+        # per shard here: rank 0's own partial arrived, rank 1's never did;
+        # rank 0's pushes reached both signal arrays
+        e = res[0][1]
+        # every wait of the call expires at about the same time (rank 0's own
+        # reduce and ready never happen either); the last report stays
+        assert "reduce's arrival flag of chunk 0" in e or "gather's ready flag of chunk 0" in e, e
+        assert "pushes finished per destination [1,1]" in e, e
+        assert "arrived from [1,0] of 1" in e and "mine at [1,1] of 1" in e, e
+        assert "clock ms: timeout" in e, e
 
 
 def _refapi_main(rank, world, port, q, engine):
