@@ -98,12 +98,19 @@ int inccl_boot_master(struct inccl_group *g)
     addr.sin_family = AF_INET;
     addr.sin_addr.s_addr = htonl(INADDR_ANY);
     addr.sin_port = htons((uint16_t)g->port);
-    if (bind(ls, (struct sockaddr *)&addr, sizeof(addr)) < 0 || listen(ls, peers + 4) < 0) {
+    /* EADDRINUSE is retried until the boot deadline: a peer's connect attempt
+     * made before this bind can take the port itself as its local ephemeral
+     * port and connect to itself (TCP simultaneous open), holding the port
+     * until it notices and closes (inccl_boot_worker) */
+    const double deadline = now_s() + boot_timeout_s();
+    int brc;
+    while ((brc = bind(ls, (struct sockaddr *)&addr, sizeof(addr))) < 0 && errno == EADDRINUSE && now_s() < deadline)
+        usleep(20000);
+    if (brc < 0 || listen(ls, peers + 4) < 0) {
         int rc = inccl_set_error(INCCL_ERR_SYS, "bootstrap: bind/listen port %d: %s", g->port, strerror(errno));
         close(ls);
         return rc;
     }
-    const double deadline = now_s() + boot_timeout_s();
     int joined = 0;
     while (joined < peers) {
         struct pollfd pf = {ls, POLLIN, 0};
@@ -150,7 +157,16 @@ int inccl_boot_worker(struct inccl_group *g)
     while (now_s() < deadline) {
         fd = socket(AF_INET, SOCK_STREAM, 0);
         if (fd < 0) break;
-        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0) break;
+        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
+            /* a connect to a port in the ephemeral range can land on itself
+             * (local port == rank 0's port, before rank 0 has bound it): that
+             * is no rank 0, and it holds rank 0's port -- drop it and retry */
+            struct sockaddr_in la, pa;
+            socklen_t ll = sizeof(la), pl = sizeof(pa);
+            if (getsockname(fd, (struct sockaddr *)&la, &ll) != 0 || getpeername(fd, (struct sockaddr *)&pa, &pl) != 0 ||
+                la.sin_port != pa.sin_port || la.sin_addr.s_addr != pa.sin_addr.s_addr)
+                break;
+        }
         close(fd);
         fd = -1;
         usleep(20000);   /* rank 0 may not be listening yet */
