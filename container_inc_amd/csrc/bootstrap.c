@@ -98,10 +98,11 @@ int inccl_boot_master(struct inccl_group *g)
     addr.sin_family = AF_INET;
     addr.sin_addr.s_addr = htonl(INADDR_ANY);
     addr.sin_port = htons((uint16_t)g->port);
-    /* EADDRINUSE is retried until the boot deadline: a peer's connect attempt
-     * made before this bind can take the port itself as its local ephemeral
-     * port and connect to itself (TCP simultaneous open), holding the port
-     * until it notices and closes (inccl_boot_worker) */
+    /* EADDRINUSE is retried until the boot deadline: a port from the
+     * ephemeral range (what a caller's "free port" usually is) can be held for
+     * a while as the local end of another connection on this host -- one GPU
+     * test run lost a group that way -- or by a peer's own connect attempt
+     * that landed on itself (dropped in inccl_boot_worker) */
     const double deadline = now_s() + boot_timeout_s();
     int brc;
     while ((brc = bind(ls, (struct sockaddr *)&addr, sizeof(addr))) < 0 && errno == EADDRINUSE && now_s() < deadline)
