@@ -48,6 +48,29 @@ def test_tcp_rendezvous(lib, world):
         assert res[r] == (r, world, "rccl"), res
 
 
+def test_tcp_rendezvous_port_briefly_in_use(lib):
+    """Rank 0's port is held by another socket for the first 1.5 s (as a port
+    from the ephemeral range can be, as the local end of some connection): the
+    bind is retried until the boot deadline and the group still forms."""
+    import time
+    port = _free_port()
+    holder = socket.socket()
+    holder.bind(("0.0.0.0", port))
+    holder.listen(1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_boot_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    time.sleep(1.5)
+    holder.close()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(2):
+        assert res[r] == (r, 2, "rccl"), res
+
+
 def test_rendezvous_timeout_returns_null(lib):
     env = dict(os.environ, INCCL_BOOTSTRAP_ONLY="1", INCCL_BOOT_TIMEOUT="1")
     import subprocess
